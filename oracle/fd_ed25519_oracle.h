@@ -1,0 +1,52 @@
+/* fd_ed25519_oracle.h -- TEST INFRASTRUCTURE ONLY (see fd_ed25519_oracle.c).
+   CPU restatement of the reference Ed25519 verify path; the parity
+   checker for firedancer_amd.  Never linked into the product. */
+#ifndef FD_ED25519_ORACLE_H
+#define FD_ED25519_ORACLE_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Codes as fd_ed25519.h:11-14 */
+#define ORACLE_SUCCESS     ( 0)
+#define ORACLE_ERR_SIG     (-1)
+#define ORACLE_ERR_PUBKEY  (-2)
+#define ORACLE_ERR_MSG     (-3)
+
+/* Error-code mapping: the AVX-512 backend (the reference's production
+   build) or the portable backend. */
+#define ORACLE_MAP_AVX512  0
+#define ORACLE_MAP_REF     1
+
+typedef struct {
+  uint32_t msg_off;   /* byte offsets into the arena */
+  uint32_t msg_sz;
+  uint32_t sig_off;   /* sig_cnt contiguous 64-B signatures */
+  uint32_t pub_off;   /* sig_cnt contiguous 32-B public keys */
+  uint32_t sig_cnt;
+} oracle_txn_t;
+
+void oracle_init( void );
+void oracle_sha512( uint8_t const * data, uint64_t sz, uint8_t out[64] );
+void oracle_scalar_reduce( uint8_t out[32], uint8_t const in[64] );
+int  oracle_scalar_validate( uint8_t const s[32] );
+int  oracle_point_decode( uint8_t const enc[32], int mapping, int * small_order, uint8_t xy_out[64] );
+
+int  oracle_verify( uint8_t const * msg, uint64_t msg_sz, uint8_t const sig[64], uint8_t const pub[32], int mapping );
+int  oracle_verify_batch_single_msg( uint8_t const * msg, uint64_t msg_sz, uint8_t const * sigs,
+                                     uint8_t const * pubs, uint32_t batch_sz, int mapping );
+void oracle_verify_detail( uint8_t const * msg, uint64_t msg_sz, uint8_t const sig[64], uint8_t const pub[32],
+                           int mapping, int * pass1_code, int * eq, uint8_t k_out[32] );
+void oracle_verify_txns( uint8_t const * arena, oracle_txn_t const * txns, uint64_t n,
+                         int8_t * codes, int mapping, int nthreads );
+
+void oracle_public_from_private( uint8_t pub[32], uint8_t const prv[32] );
+void oracle_sign( uint8_t sig[64], uint8_t const * msg, uint64_t sz, uint8_t const pub[32], uint8_t const prv[32] );
+
+#ifdef __cplusplus
+}
+#endif
+#endif
