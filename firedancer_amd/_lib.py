@@ -1,0 +1,85 @@
+"""Loader for the C-ABI engine library (libfd_ed25519_gpu.so).
+
+The library is built in-tree (``make -C firedancer_amd/csrc`` or
+``__graft_entry__.build()``).  There is deliberately no fallback: if the
+library is missing or cannot be loaded, every entry point raises.
+"""
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libfd_ed25519_gpu.so")
+HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "fd_ed25519_gpu.h")
+
+_LIB = None
+
+
+class FdgpuTxn(ctypes.Structure):
+    """fdgpu_txn_t (include/fd_ed25519_gpu.h)."""
+    _fields_ = [("msg_off", ctypes.c_uint32), ("msg_sz", ctypes.c_uint32),
+                ("sig_off", ctypes.c_uint32), ("pub_off", ctypes.c_uint32),
+                ("sig_cnt", ctypes.c_uint32)]
+
+
+class FdgpuCfg(ctypes.Structure):
+    """fdgpu_cfg_t (include/fd_ed25519_gpu.h)."""
+    _fields_ = [("max_txn", ctypes.c_uint64), ("max_sig", ctypes.c_uint64),
+                ("max_arena", ctypes.c_uint64), ("ring_depth", ctypes.c_uint32),
+                ("flags", ctypes.c_uint32)]
+
+
+def lib():
+    """Load libfd_ed25519_gpu.so and declare prototypes.  Raises if absent."""
+    global _LIB
+    if _LIB is not None:
+        return _LIB
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError(f"firedancer_amd: engine library not built: {LIB_PATH} "
+                           "(run `make -C firedancer_amd/csrc`)")
+    L = ctypes.CDLL(LIB_PATH)
+    c = ctypes
+    vp, u8p = c.c_void_p, c.c_char_p
+    L.fd_ed25519_verify.argtypes = [u8p, c.c_uint64, u8p, u8p, vp]
+    L.fd_ed25519_verify.restype = c.c_int
+    L.fd_ed25519_verify_batch_single_msg.argtypes = [u8p, c.c_uint64, u8p, u8p, vp, c.c_uint8]
+    L.fd_ed25519_verify_batch_single_msg.restype = c.c_int
+    L.fd_ed25519_strerror.argtypes = [c.c_int]
+    L.fd_ed25519_strerror.restype = c.c_char_p
+    L.fdgpu_engine_open.argtypes = [c.c_int, c.POINTER(FdgpuCfg)]
+    L.fdgpu_engine_open.restype = vp
+    L.fdgpu_engine_close.argtypes = [vp]
+    L.fdgpu_engine_close.restype = None
+    L.fdgpu_last_error.argtypes = []
+    L.fdgpu_last_error.restype = c.c_char_p
+    L.fdgpu_submit.argtypes = [vp, vp, c.c_uint64, vp, c.c_uint64]
+    L.fdgpu_submit.restype = c.c_int64
+    L.fdgpu_poll.argtypes = [vp, c.c_int64, vp, c.c_int]
+    L.fdgpu_poll.restype = c.c_int
+    L.fdgpu_verify_device.argtypes = [vp, vp, vp, c.c_uint64, vp, c.c_uint64, vp, vp, vp]
+    L.fdgpu_verify_device.restype = c.c_int
+    L.fdgpu_engine_info.argtypes = [vp, c.POINTER(c.c_uint32), c.POINTER(c.c_uint32), c.POINTER(c.c_uint64)]
+    L.fdgpu_engine_info.restype = c.c_int
+    L.fdgpu_debug_fe_ops.argtypes = [vp, vp, c.c_uint64, vp]
+    L.fdgpu_debug_decode.argtypes = [vp, vp, c.c_uint64, c.c_int, vp]
+    L.fdgpu_debug_sha512.argtypes = [vp, vp, c.c_uint64, vp, c.c_uint64, vp]
+    L.fdgpu_debug_hram.argtypes = [vp, vp, c.c_uint64, vp, c.c_uint64, vp]
+    L.fdgpu_debug_sc_reduce.argtypes = [vp, vp, c.c_uint64, vp]
+    L.fdgpu_debug_sig_codes.argtypes = [vp, vp, c.c_uint64, vp, c.c_uint64, vp]
+    for fn in ("fdgpu_debug_fe_ops", "fdgpu_debug_decode", "fdgpu_debug_sha512", "fdgpu_debug_hram",
+               "fdgpu_debug_sc_reduce", "fdgpu_debug_sig_codes"):
+        getattr(L, fn).restype = c.c_int
+    _LIB = L
+    return L
+
+
+def header_functions():
+    """Names of the functions declared by include/fd_ed25519_gpu.h."""
+    import re
+    text = open(HEADER_PATH).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    names = re.findall(r"^[A-Za-z_][\w \t\*]*?\b(fd\w+)\s*\(", text, flags=re.M)
+    return sorted(set(n for n in names if not n.startswith("FD_")))
+
+
+def last_error():
+    return lib().fdgpu_last_error().decode()

@@ -1,0 +1,469 @@
+/* fdgpu_engine.cpp -- host side of the MI355X Ed25519 verify engine and the
+   exported C ABI (include/fd_ed25519_gpu.h).
+
+   Per engine (one per GPU):
+     - one compute stream running the verify + combine kernels in order
+       (they share the per-lane A-table workspace);
+     - `ring_depth` staging slots, each with pinned host buffers, device
+       buffers, a copy stream and events, so the PCIe copies of batch i+1
+       and the D2H of batch i-1 overlap the kernels of batch i;
+     - the B table (built on the device at open) and the workspace sized for
+       the persistent grid (resident workgroups x 256 lanes).
+   Untrusted descriptors are bounds-checked on the host before anything is
+   handed to the GPU (offsets + sizes must lie inside the arena). */
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdarg>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/fd_ed25519_gpu.h"
+#include "fdgpu_internal.h"
+
+namespace {
+
+thread_local std::string g_err;
+
+void set_err(const char *fmt, ...) {
+  char buf[512];
+  va_list ap; va_start(ap, fmt); vsnprintf(buf, sizeof buf, fmt, ap); va_end(ap);
+  g_err = buf;
+}
+
+#define HIPCHK(x, ret) do { hipError_t e_ = (x); if (e_ != hipSuccess) { \
+  set_err("%s failed: %s (%s:%d)", #x, hipGetErrorString(e_), __FILE__, __LINE__); return ret; } } while (0)
+
+struct Slot {
+  hipStream_t stream = nullptr;
+  hipEvent_t h2d_done = nullptr, comp_done = nullptr, done = nullptr;
+  uint8_t *h_arena = nullptr, *d_arena = nullptr;
+  fdgpu_sig_desc_t *h_sigs = nullptr, *d_sigs = nullptr;
+  fdgpu_txn_desc_t *h_txns = nullptr, *d_txns = nullptr;
+  int8_t *h_codes = nullptr, *d_txn_codes = nullptr, *d_sig_codes = nullptr;
+  int64_t ticket = -1;      /* -1: free */
+  uint64_t txn_cnt = 0;
+};
+
+}  // namespace
+
+struct fdgpu_engine {
+  int device = 0;
+  fdgpu_cfg_t cfg{};
+  hipStream_t compute = nullptr;
+  uint32_t *d_btab = nullptr;
+  uint32_t *d_ws = nullptr;          /* per-lane A-table workspace, fdgpu_ws_bytes(ws_sig) */
+  size_t ws_bytes = 0;
+  uint64_t ws_sig = 0;
+  uint32_t resident_blocks = 0;     /* occupancy x CUs, for reporting */
+  std::vector<Slot> slots;
+  int64_t next_ticket = 0;
+  int8_t *d_scratch_codes = nullptr;   /* for fdgpu_verify_device with d_sig_codes == NULL */
+  uint64_t scratch_cap = 0;
+};
+
+namespace {
+
+void slot_free(Slot &s) {
+  if (s.stream) (void)hipStreamDestroy(s.stream);
+  if (s.h2d_done) (void)hipEventDestroy(s.h2d_done);
+  if (s.comp_done) (void)hipEventDestroy(s.comp_done);
+  if (s.done) (void)hipEventDestroy(s.done);
+  if (s.h_arena) (void)hipHostFree(s.h_arena);
+  if (s.h_sigs) (void)hipHostFree(s.h_sigs);
+  if (s.h_txns) (void)hipHostFree(s.h_txns);
+  if (s.h_codes) (void)hipHostFree(s.h_codes);
+  if (s.d_arena) (void)hipFree(s.d_arena);
+  if (s.d_sigs) (void)hipFree(s.d_sigs);
+  if (s.d_txns) (void)hipFree(s.d_txns);
+  if (s.d_txn_codes) (void)hipFree(s.d_txn_codes);
+  if (s.d_sig_codes) (void)hipFree(s.d_sig_codes);
+  s = Slot{};
+}
+
+bool slot_alloc(Slot &s, const fdgpu_cfg_t &c) {
+  const size_t arena = c.max_arena + FDGPU_ARENA_SLACK;
+  HIPCHK(hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking), false);
+  HIPCHK(hipEventCreateWithFlags(&s.h2d_done, hipEventDisableTiming), false);
+  HIPCHK(hipEventCreateWithFlags(&s.comp_done, hipEventDisableTiming), false);
+  HIPCHK(hipEventCreateWithFlags(&s.done, hipEventDisableTiming), false);
+  HIPCHK(hipHostMalloc((void **)&s.h_arena, arena, hipHostMallocDefault), false);
+  HIPCHK(hipHostMalloc((void **)&s.h_sigs, c.max_sig * sizeof(fdgpu_sig_desc_t) + 16, hipHostMallocDefault), false);
+  HIPCHK(hipHostMalloc((void **)&s.h_txns, c.max_txn * sizeof(fdgpu_txn_desc_t) + 16, hipHostMallocDefault), false);
+  HIPCHK(hipHostMalloc((void **)&s.h_codes, c.max_txn + 16, hipHostMallocDefault), false);
+  HIPCHK(hipMalloc((void **)&s.d_arena, arena), false);
+  HIPCHK(hipMalloc((void **)&s.d_sigs, c.max_sig * sizeof(fdgpu_sig_desc_t) + 16), false);
+  HIPCHK(hipMalloc((void **)&s.d_txns, c.max_txn * sizeof(fdgpu_txn_desc_t) + 16), false);
+  HIPCHK(hipMalloc((void **)&s.d_txn_codes, c.max_txn + 16), false);
+  HIPCHK(hipMalloc((void **)&s.d_sig_codes, c.max_sig + 16), false);
+  return true;
+}
+
+/* Validate and expand transactions into per-signature work items.
+   Returns the number of signatures or -1 on invalid input. */
+int64_t expand(const uint8_t *arena_unused, uint64_t arena_sz, const fdgpu_txn_t *txns, uint64_t txn_cnt,
+               uint64_t max_sig, fdgpu_sig_desc_t *sigs, fdgpu_txn_desc_t *tds) {
+  (void)arena_unused;
+  uint64_t ns = 0;
+  for (uint64_t t = 0; t < txn_cnt; t++) {
+    const fdgpu_txn_t &x = txns[t];
+    const uint32_t cnt = x.sig_cnt;
+    tds[t].sig0 = (uint32_t)ns;
+    tds[t].sig_cnt = cnt;
+    if (cnt == 0 || cnt > 16) { tds[t].sig_cnt = 0; continue; }   /* -> ERR_SIG without verifying */
+    if ((uint64_t)x.msg_off + x.msg_sz > arena_sz || (uint64_t)x.sig_off + 64ull * cnt > arena_sz ||
+        (uint64_t)x.pub_off + 32ull * cnt > arena_sz) {
+      set_err("txn %llu: descriptor out of arena bounds", (unsigned long long)t);
+      return -1;
+    }
+    if (ns + cnt > max_sig) { set_err("batch exceeds max_sig"); return -1; }
+    for (uint32_t j = 0; j < cnt; j++) {
+      sigs[ns + j].msg_off = x.msg_off;
+      sigs[ns + j].msg_sz = x.msg_sz;
+      sigs[ns + j].sig_off = x.sig_off + 64u * j;
+      sigs[ns + j].pub_off = x.pub_off + 32u * j;
+    }
+    ns += cnt;
+  }
+  return (int64_t)ns;
+}
+
+template <typename T>
+T *dalloc(size_t n) { T *p = nullptr; if (hipMalloc((void **)&p, n * sizeof(T) + 64) != hipSuccess) return nullptr; return p; }
+
+/* (Re)size the per-lane workspace to cover n_sig signatures. */
+int ensure_ws(fdgpu_engine *e, uint64_t n_sig) {
+  if (n_sig <= e->ws_sig && e->d_ws) return FDGPU_OK;
+  if (e->d_ws) { (void)hipFree(e->d_ws); e->d_ws = nullptr; }
+  e->ws_bytes = fdgpu_ws_bytes(n_sig ? n_sig : 1);
+  if (hipMalloc((void **)&e->d_ws, e->ws_bytes) != hipSuccess) {
+    set_err("workspace alloc (%zu bytes)", e->ws_bytes); e->ws_sig = 0; return FDGPU_ERR_DEVICE;
+  }
+  e->ws_sig = n_sig ? n_sig : 1;
+  return FDGPU_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+char const *fdgpu_last_error(void) { return g_err.c_str(); }
+
+fdgpu_engine_t *fdgpu_engine_open(int device, fdgpu_cfg_t const *cfg_in) {
+  fdgpu_cfg_t cfg{};
+  if (cfg_in) cfg = *cfg_in;
+  if (!cfg.max_txn) cfg.max_txn = 1u << 16;
+  if (!cfg.max_sig) cfg.max_sig = cfg.max_txn * 2;
+  if (!cfg.max_arena) cfg.max_arena = cfg.max_txn * 1232ull;
+  if (!cfg.ring_depth) cfg.ring_depth = 2;
+  if (cfg.max_arena > 0xFFFFFFF0ull || cfg.max_sig > 0xFFFFFFF0ull || cfg.max_txn > 0xFFFFFFF0ull) {
+    set_err("batch limits exceed 32-bit offsets");
+    return nullptr;
+  }
+  int ndev = 0;
+  HIPCHK(hipGetDeviceCount(&ndev), nullptr);
+  if (device < 0 || device >= ndev) { set_err("device %d not present (%d devices)", device, ndev); return nullptr; }
+  HIPCHK(hipSetDevice(device), nullptr);
+  fdgpu_engine *e = new fdgpu_engine();
+  e->device = device;
+  e->cfg = cfg;
+  auto fail = [&]() -> fdgpu_engine_t * { fdgpu_engine_close(e); return nullptr; };
+  if (hipStreamCreateWithFlags(&e->compute, hipStreamNonBlocking) != hipSuccess) { set_err("stream"); return fail(); }
+  if (hipMalloc((void **)&e->d_btab, FDGPU_BTAB_ENTRIES * FDGPU_BTAB_STRIDE * sizeof(uint32_t)) != hipSuccess) {
+    set_err("btab alloc"); return fail();
+  }
+  if (fdgpu_launch_btab_init(e->d_btab, e->compute) != hipSuccess) { set_err("btab init launch"); return fail(); }
+  int bpcu = 0;
+  hipDeviceProp_t prop;
+  if (fdgpu_verify_occupancy(&bpcu) != hipSuccess || bpcu < 1) bpcu = 1;
+  if (hipGetDeviceProperties(&prop, device) != hipSuccess) { set_err("props"); return fail(); }
+  e->resident_blocks = (uint32_t)(bpcu * prop.multiProcessorCount);
+  if (ensure_ws(e, cfg.max_sig) != FDGPU_OK) return fail();
+  e->slots.resize(cfg.ring_depth);
+  for (auto &s : e->slots) if (!slot_alloc(s, cfg)) return fail();
+  if (hipStreamSynchronize(e->compute) != hipSuccess) { set_err("btab init failed"); return fail(); }
+  return e;
+}
+
+void fdgpu_engine_close(fdgpu_engine_t *e) {
+  if (!e) return;
+  (void)hipSetDevice(e->device);
+  if (e->compute) (void)hipStreamSynchronize(e->compute);
+  for (auto &s : e->slots) { if (s.stream) (void)hipStreamSynchronize(s.stream); slot_free(s); }
+  if (e->d_btab) (void)hipFree(e->d_btab);
+  if (e->d_ws) (void)hipFree(e->d_ws);
+  if (e->d_scratch_codes) (void)hipFree(e->d_scratch_codes);
+  if (e->compute) (void)hipStreamDestroy(e->compute);
+  delete e;
+}
+
+int fdgpu_engine_info(fdgpu_engine_t *e, uint32_t *grid_blocks, uint32_t *block_threads, uint64_t *ws_bytes) {
+  if (!e) return FDGPU_ERR_INVAL;
+  if (grid_blocks) *grid_blocks = e->resident_blocks;
+  if (block_threads) *block_threads = FDGPU_BLOCK;
+  if (ws_bytes) *ws_bytes = e->ws_bytes;
+  return FDGPU_OK;
+}
+
+static int enqueue_verify(fdgpu_engine_t *e, const uint8_t *d_arena, const fdgpu_sig_desc_t *d_sigs, uint64_t n_sig,
+                          const fdgpu_txn_desc_t *d_txns, uint64_t n_txn, int8_t *d_sig_codes, int8_t *d_txn_codes,
+                          hipStream_t st) {
+  const uint32_t flags = (e->cfg.flags & FDGPU_FLAG_REF_MAPPING) ? FDGPU_FLAG_REF_MAP : 0u;
+  if (n_sig > e->ws_sig) {
+    HIPCHK(hipStreamSynchronize(st), FDGPU_ERR_DEVICE);
+    HIPCHK(hipStreamSynchronize(e->compute), FDGPU_ERR_DEVICE);
+    int rc = ensure_ws(e, n_sig);
+    if (rc) return rc;
+  }
+  HIPCHK(fdgpu_launch_verify_sigs(d_arena, d_sigs, (uint32_t)n_sig, e->d_btab, e->d_ws, d_sig_codes, flags, st),
+         FDGPU_ERR_DEVICE);
+  HIPCHK(fdgpu_launch_combine(d_txns, (uint32_t)n_txn, d_sig_codes, d_txn_codes, st), FDGPU_ERR_DEVICE);
+  return FDGPU_OK;
+}
+
+int64_t fdgpu_submit(fdgpu_engine_t *e, uint8_t const *arena, uint64_t arena_sz, fdgpu_txn_t const *txns,
+                     uint64_t txn_cnt) {
+  if (!e || (!arena && arena_sz) || (!txns && txn_cnt)) { set_err("null argument"); return FDGPU_ERR_INVAL; }
+  if (arena_sz > e->cfg.max_arena || txn_cnt > e->cfg.max_txn) { set_err("batch exceeds engine limits"); return FDGPU_ERR_INVAL; }
+  HIPCHK(hipSetDevice(e->device), FDGPU_ERR_DEVICE);
+  Slot *s = nullptr;
+  for (auto &c : e->slots) if (c.ticket < 0) { s = &c; break; }
+  if (!s) { set_err("all ring slots hold unpolled batches"); return FDGPU_ERR_FULL; }
+  /* the slot's previous batch was polled, so its copies are complete */
+  const int64_t ns = expand(arena, arena_sz, txns, txn_cnt, e->cfg.max_sig, s->h_sigs, s->h_txns);
+  if (ns < 0) return FDGPU_ERR_INVAL;
+  if (arena_sz) memcpy(s->h_arena, arena, arena_sz);
+  memset(s->h_arena + arena_sz, 0, FDGPU_ARENA_SLACK);
+  const size_t asz = arena_sz + FDGPU_ARENA_SLACK;
+  HIPCHK(hipMemcpyAsync(s->d_arena, s->h_arena, asz, hipMemcpyHostToDevice, s->stream), FDGPU_ERR_DEVICE);
+  if (ns) HIPCHK(hipMemcpyAsync(s->d_sigs, s->h_sigs, (size_t)ns * sizeof(fdgpu_sig_desc_t), hipMemcpyHostToDevice, s->stream), FDGPU_ERR_DEVICE);
+  if (txn_cnt) HIPCHK(hipMemcpyAsync(s->d_txns, s->h_txns, txn_cnt * sizeof(fdgpu_txn_desc_t), hipMemcpyHostToDevice, s->stream), FDGPU_ERR_DEVICE);
+  HIPCHK(hipEventRecord(s->h2d_done, s->stream), FDGPU_ERR_DEVICE);
+  HIPCHK(hipStreamWaitEvent(e->compute, s->h2d_done, 0), FDGPU_ERR_DEVICE);
+  int rc = enqueue_verify(e, s->d_arena, s->d_sigs, (uint64_t)ns, s->d_txns, txn_cnt, s->d_sig_codes, s->d_txn_codes,
+                          e->compute);
+  if (rc) return rc;
+  HIPCHK(hipEventRecord(s->comp_done, e->compute), FDGPU_ERR_DEVICE);
+  HIPCHK(hipStreamWaitEvent(s->stream, s->comp_done, 0), FDGPU_ERR_DEVICE);
+  if (txn_cnt) HIPCHK(hipMemcpyAsync(s->h_codes, s->d_txn_codes, txn_cnt, hipMemcpyDeviceToHost, s->stream), FDGPU_ERR_DEVICE);
+  HIPCHK(hipEventRecord(s->done, s->stream), FDGPU_ERR_DEVICE);
+  s->ticket = e->next_ticket++;
+  s->txn_cnt = txn_cnt;
+  return s->ticket;
+}
+
+int fdgpu_poll(fdgpu_engine_t *e, int64_t ticket, int8_t *txn_codes, int blocking) {
+  if (!e) return FDGPU_ERR_INVAL;
+  Slot *s = nullptr;
+  for (auto &c : e->slots) if (c.ticket == ticket && ticket >= 0) { s = &c; break; }
+  if (!s) { set_err("unknown ticket %lld", (long long)ticket); return FDGPU_ERR_TICKET; }
+  HIPCHK(hipSetDevice(e->device), FDGPU_ERR_DEVICE);
+  if (blocking) {
+    HIPCHK(hipEventSynchronize(s->done), FDGPU_ERR_DEVICE);
+  } else {
+    hipError_t q = hipEventQuery(s->done);
+    if (q == hipErrorNotReady) return FDGPU_PENDING;
+    HIPCHK(q, FDGPU_ERR_DEVICE);
+  }
+  if (txn_codes && s->txn_cnt) memcpy(txn_codes, s->h_codes, s->txn_cnt);
+  s->ticket = -1;
+  return FDGPU_OK;
+}
+
+int fdgpu_verify_device(fdgpu_engine_t *e, void const *d_arena, void const *d_sig_desc, uint64_t sig_cnt,
+                        void const *d_txn_desc, uint64_t txn_cnt, int8_t *d_sig_codes, int8_t *d_txn_codes,
+                        void *hip_stream) {
+  if (!e || sig_cnt > 0xFFFFFFF0ull || txn_cnt > 0xFFFFFFF0ull) return FDGPU_ERR_INVAL;
+  HIPCHK(hipSetDevice(e->device), FDGPU_ERR_DEVICE);
+  hipStream_t st = hip_stream ? (hipStream_t)hip_stream : e->compute;
+  if (!d_sig_codes) {
+    if (e->scratch_cap < sig_cnt + 16) {
+      if (e->d_scratch_codes) { HIPCHK(hipStreamSynchronize(st), FDGPU_ERR_DEVICE); (void)hipFree(e->d_scratch_codes); }
+      e->d_scratch_codes = nullptr;
+      HIPCHK(hipMalloc((void **)&e->d_scratch_codes, sig_cnt + 16), FDGPU_ERR_DEVICE);
+      e->scratch_cap = sig_cnt + 16;
+    }
+    d_sig_codes = e->d_scratch_codes;
+  }
+  return enqueue_verify(e, (const uint8_t *)d_arena, (const fdgpu_sig_desc_t *)d_sig_desc, sig_cnt,
+                        (const fdgpu_txn_desc_t *)d_txn_desc, txn_cnt, d_sig_codes, d_txn_codes, st);
+}
+
+/* ------------------------------------------------------------ sync API */
+
+static std::mutex g_sync_mu;
+static fdgpu_engine_t *g_sync_engine = nullptr;
+
+static fdgpu_engine_t *sync_engine() {
+  if (!g_sync_engine) {
+    fdgpu_cfg_t cfg{};
+    cfg.max_txn = 1; cfg.max_sig = 16; cfg.max_arena = 64 * 16 + 32 * 16 + 65536; cfg.ring_depth = 1;
+    g_sync_engine = fdgpu_engine_open(0, &cfg);
+    if (!g_sync_engine) {
+      fprintf(stderr, "fd_ed25519_gpu: cannot open the GPU engine: %s\n", fdgpu_last_error());
+      abort();   /* no silent CPU fallback */
+    }
+  }
+  return g_sync_engine;
+}
+
+static int sync_verify(const uint8_t *msg, uint64_t msg_sz, const uint8_t *sigs, const uint8_t *pubs, uint32_t n) {
+  if (n == 0 || n > 16) return FD_ED25519_ERR_SIG;
+  std::lock_guard<std::mutex> lk(g_sync_mu);
+  fdgpu_engine_t *e = sync_engine();
+  const uint64_t need = 64ull * n + 32ull * n + msg_sz;
+  std::vector<uint8_t> arena(need);
+  memcpy(arena.data(), sigs, 64ull * n);
+  memcpy(arena.data() + 64ull * n, pubs, 32ull * n);
+  if (msg_sz) memcpy(arena.data() + 96ull * n, msg, msg_sz);
+  if (need > e->cfg.max_arena) {
+    /* grow the sync engine for long messages */
+    fdgpu_engine_close(e);
+    fdgpu_cfg_t cfg{}; cfg.max_txn = 1; cfg.max_sig = 16; cfg.max_arena = need * 2; cfg.ring_depth = 1;
+    g_sync_engine = e = fdgpu_engine_open(0, &cfg);
+    if (!e) { fprintf(stderr, "fd_ed25519_gpu: %s\n", fdgpu_last_error()); abort(); }
+  }
+  fdgpu_txn_t t;
+  t.sig_off = 0; t.pub_off = 64u * n; t.msg_off = 96u * n; t.msg_sz = (uint32_t)msg_sz; t.sig_cnt = n;
+  const int64_t tk = fdgpu_submit(e, arena.data(), need, &t, 1);
+  if (tk < 0) { fprintf(stderr, "fd_ed25519_gpu: submit failed: %s\n", fdgpu_last_error()); abort(); }
+  int8_t code = 0;
+  if (fdgpu_poll(e, tk, &code, 1) != FDGPU_OK) { fprintf(stderr, "fd_ed25519_gpu: %s\n", fdgpu_last_error()); abort(); }
+  return code;
+}
+
+int fd_ed25519_verify(uint8_t const msg[], uint64_t msg_sz, uint8_t const sig[64], uint8_t const public_key[32],
+                      fd_sha512_t *sha) {
+  (void)sha;
+  return sync_verify(msg, msg_sz, sig, public_key, 1);
+}
+
+int fd_ed25519_verify_batch_single_msg(uint8_t const msg[], uint64_t const msg_sz, uint8_t const signatures[64],
+                                       uint8_t const pubkeys[32], fd_sha512_t *shas[1], uint8_t const batch_sz) {
+  (void)shas;
+  return sync_verify(msg, msg_sz, signatures, pubkeys, batch_sz);
+}
+
+char const *fd_ed25519_strerror(int err) {
+  switch (err) {
+    case FD_ED25519_SUCCESS: return "success";
+    case FD_ED25519_ERR_SIG: return "bad signature";
+    case FD_ED25519_ERR_PUBKEY: return "bad public key";
+    case FD_ED25519_ERR_MSG: return "bad message";
+    default: break;
+  }
+  return "unknown";
+}
+
+/* --------------------------------------------------------- diagnostics */
+
+int fdgpu_debug_fe_ops(fdgpu_engine_t *e, uint8_t const *ab, uint64_t n, uint8_t *out) {
+  if (!e || !n) return FDGPU_ERR_INVAL;
+  HIPCHK(hipSetDevice(e->device), FDGPU_ERR_DEVICE);
+  uint32_t *din = dalloc<uint32_t>(n * 16), *dout = dalloc<uint32_t>(n * 64);
+  if (!din || !dout) { set_err("alloc"); return FDGPU_ERR_DEVICE; }
+  HIPCHK(hipMemcpy(din, ab, n * 64, hipMemcpyHostToDevice), FDGPU_ERR_DEVICE);
+  HIPCHK(fdgpu_launch_test_fe(din, dout, (uint32_t)n, e->compute), FDGPU_ERR_DEVICE);
+  HIPCHK(hipStreamSynchronize(e->compute), FDGPU_ERR_DEVICE);
+  HIPCHK(hipMemcpy(out, dout, n * 256, hipMemcpyDeviceToHost), FDGPU_ERR_DEVICE);
+  (void)hipFree(din); (void)hipFree(dout);
+  return FDGPU_OK;
+}
+
+int fdgpu_debug_decode(fdgpu_engine_t *e, uint8_t const *enc, uint64_t n, int ref_mapping, uint8_t *out) {
+  if (!e || !n) return FDGPU_ERR_INVAL;
+  HIPCHK(hipSetDevice(e->device), FDGPU_ERR_DEVICE);
+  uint32_t *din = dalloc<uint32_t>(n * 8), *dout = dalloc<uint32_t>(n * 18);
+  if (!din || !dout) { set_err("alloc"); return FDGPU_ERR_DEVICE; }
+  HIPCHK(hipMemcpy(din, enc, n * 32, hipMemcpyHostToDevice), FDGPU_ERR_DEVICE);
+  HIPCHK(fdgpu_launch_test_decode(din, dout, (uint32_t)n, ref_mapping ? FDGPU_FLAG_REF_MAP : 0u, e->compute), FDGPU_ERR_DEVICE);
+  HIPCHK(hipStreamSynchronize(e->compute), FDGPU_ERR_DEVICE);
+  HIPCHK(hipMemcpy(out, dout, n * 72, hipMemcpyDeviceToHost), FDGPU_ERR_DEVICE);
+  (void)hipFree(din); (void)hipFree(dout);
+  return FDGPU_OK;
+}
+
+static int debug_msgs(fdgpu_engine_t *e, uint8_t const *arena, uint64_t arena_sz, fdgpu_txn_t const *txns, uint64_t n,
+                      uint8_t *out, int hram) {
+  if (!e || !n) return FDGPU_ERR_INVAL;
+  HIPCHK(hipSetDevice(e->device), FDGPU_ERR_DEVICE);
+  std::vector<fdgpu_sig_desc_t> d(n);
+  for (uint64_t i = 0; i < n; i++) {
+    if ((uint64_t)txns[i].msg_off + txns[i].msg_sz > arena_sz ||
+        (hram && ((uint64_t)txns[i].sig_off + 64 > arena_sz || (uint64_t)txns[i].pub_off + 32 > arena_sz))) {
+      set_err("descriptor out of bounds"); return FDGPU_ERR_INVAL;
+    }
+    d[i].msg_off = txns[i].msg_off; d[i].msg_sz = txns[i].msg_sz;
+    d[i].sig_off = txns[i].sig_off; d[i].pub_off = txns[i].pub_off;
+  }
+  uint8_t *da = dalloc<uint8_t>(arena_sz + FDGPU_ARENA_SLACK);
+  fdgpu_sig_desc_t *dd = dalloc<fdgpu_sig_desc_t>(n);
+  uint32_t *dout = dalloc<uint32_t>(n * 16);
+  if (!da || !dd || !dout) { set_err("alloc"); return FDGPU_ERR_DEVICE; }
+  HIPCHK(hipMemset(da, 0, arena_sz + FDGPU_ARENA_SLACK), FDGPU_ERR_DEVICE);
+  if (arena_sz) HIPCHK(hipMemcpy(da, arena, arena_sz, hipMemcpyHostToDevice), FDGPU_ERR_DEVICE);
+  HIPCHK(hipMemcpy(dd, d.data(), n * sizeof(fdgpu_sig_desc_t), hipMemcpyHostToDevice), FDGPU_ERR_DEVICE);
+  if (hram) HIPCHK(fdgpu_launch_test_hram(da, dd, (uint32_t)n, dout, e->compute), FDGPU_ERR_DEVICE);
+  else HIPCHK(fdgpu_launch_test_sha512(da, dd, (uint32_t)n, dout, e->compute), FDGPU_ERR_DEVICE);
+  HIPCHK(hipStreamSynchronize(e->compute), FDGPU_ERR_DEVICE);
+  HIPCHK(hipMemcpy(out, dout, n * (hram ? 32 : 64), hipMemcpyDeviceToHost), FDGPU_ERR_DEVICE);
+  (void)hipFree(da); (void)hipFree(dd); (void)hipFree(dout);
+  return FDGPU_OK;
+}
+
+int fdgpu_debug_sha512(fdgpu_engine_t *e, uint8_t const *arena, uint64_t arena_sz, fdgpu_txn_t const *msgs,
+                       uint64_t n, uint8_t *out) {
+  return debug_msgs(e, arena, arena_sz, msgs, n, out, 0);
+}
+
+int fdgpu_debug_hram(fdgpu_engine_t *e, uint8_t const *arena, uint64_t arena_sz, fdgpu_txn_t const *txns,
+                     uint64_t n, uint8_t *out) {
+  return debug_msgs(e, arena, arena_sz, txns, n, out, 1);
+}
+
+int fdgpu_debug_sc_reduce(fdgpu_engine_t *e, uint8_t const *in, uint64_t n, uint8_t *out) {
+  if (!e || !n) return FDGPU_ERR_INVAL;
+  HIPCHK(hipSetDevice(e->device), FDGPU_ERR_DEVICE);
+  uint32_t *din = dalloc<uint32_t>(n * 16), *dout = dalloc<uint32_t>(n * 8);
+  if (!din || !dout) { set_err("alloc"); return FDGPU_ERR_DEVICE; }
+  HIPCHK(hipMemcpy(din, in, n * 64, hipMemcpyHostToDevice), FDGPU_ERR_DEVICE);
+  HIPCHK(fdgpu_launch_test_sc_reduce(din, dout, (uint32_t)n, e->compute), FDGPU_ERR_DEVICE);
+  HIPCHK(hipStreamSynchronize(e->compute), FDGPU_ERR_DEVICE);
+  HIPCHK(hipMemcpy(out, dout, n * 32, hipMemcpyDeviceToHost), FDGPU_ERR_DEVICE);
+  (void)hipFree(din); (void)hipFree(dout);
+  return FDGPU_OK;
+}
+
+int fdgpu_debug_sig_codes(fdgpu_engine_t *e, uint8_t const *arena, uint64_t arena_sz, fdgpu_txn_t const *txns,
+                          uint64_t txn_cnt, int8_t *sig_codes) {
+  if (!e) return FDGPU_ERR_INVAL;
+  HIPCHK(hipSetDevice(e->device), FDGPU_ERR_DEVICE);
+  std::vector<fdgpu_sig_desc_t> sd;
+  std::vector<fdgpu_txn_desc_t> td(txn_cnt);
+  uint64_t total = 0;
+  for (uint64_t t = 0; t < txn_cnt; t++) total += (txns[t].sig_cnt >= 1 && txns[t].sig_cnt <= 16) ? txns[t].sig_cnt : 0;
+  sd.resize(total + 1);
+  const int64_t ns = expand(arena, arena_sz, txns, txn_cnt, total, sd.data(), td.data());
+  if (ns < 0) return FDGPU_ERR_INVAL;
+  if (!ns) return FDGPU_OK;
+  uint8_t *da = dalloc<uint8_t>(arena_sz + FDGPU_ARENA_SLACK);
+  fdgpu_sig_desc_t *dd = dalloc<fdgpu_sig_desc_t>(ns);
+  int8_t *dc = dalloc<int8_t>(ns);
+  if (!da || !dd || !dc) { set_err("alloc"); return FDGPU_ERR_DEVICE; }
+  HIPCHK(hipMemset(da, 0, arena_sz + FDGPU_ARENA_SLACK), FDGPU_ERR_DEVICE);
+  HIPCHK(hipMemcpy(da, arena, arena_sz, hipMemcpyHostToDevice), FDGPU_ERR_DEVICE);
+  HIPCHK(hipMemcpy(dd, sd.data(), ns * sizeof(fdgpu_sig_desc_t), hipMemcpyHostToDevice), FDGPU_ERR_DEVICE);
+  const uint32_t flags = (e->cfg.flags & FDGPU_FLAG_REF_MAPPING) ? FDGPU_FLAG_REF_MAP : 0u;
+  if ((uint64_t)ns > e->ws_sig) { int rc = ensure_ws(e, (uint64_t)ns); if (rc) return rc; }
+  HIPCHK(fdgpu_launch_verify_sigs(da, dd, (uint32_t)ns, e->d_btab, e->d_ws, dc, flags, e->compute), FDGPU_ERR_DEVICE);
+  HIPCHK(hipStreamSynchronize(e->compute), FDGPU_ERR_DEVICE);
+  HIPCHK(hipMemcpy(sig_codes, dc, ns, hipMemcpyDeviceToHost), FDGPU_ERR_DEVICE);
+  (void)hipFree(da); (void)hipFree(dd); (void)hipFree(dc);
+  return FDGPU_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,62 @@
+/* fdgpu_internal.h -- declarations shared by the kernels (fdgpu_kernels.hip)
+   and the host engine (fdgpu_engine.cpp).  Not part of the public C ABI. */
+#pragma once
+
+#include <hip/hip_runtime_api.h>
+#include <stddef.h>
+#include <stdint.h>
+
+/* Per-signature work item (16 B, one dwordx4 per lane).  Offsets index the
+   batch arena; the arena carries FDGPU_ARENA_SLACK readable bytes after
+   the last payload byte. */
+typedef struct {
+  uint32_t msg_off;
+  uint32_t msg_sz;
+  uint32_t sig_off;   /* 64-B signature R || S */
+  uint32_t pub_off;   /* 32-B public key */
+} fdgpu_sig_desc_t;
+
+/* Per-transaction combine item: signatures sig0 .. sig0+sig_cnt-1 of the
+   signature array (batch_single_msg order).  sig_cnt outside [1,16] means
+   the batch is rejected without verification (fd_ed25519_user.c:238-241). */
+typedef struct {
+  uint32_t sig0;
+  uint32_t sig_cnt;
+} fdgpu_txn_desc_t;
+
+#define FDGPU_ARENA_SLACK   160u          /* readable bytes past the arena (SHA block loads) */
+#define FDGPU_BTAB_ENTRIES  129u          /* 0 (identity), 1B .. 128B */
+#define FDGPU_BTAB_STRIDE   32u           /* u32 per niels entry (30 used) */
+#define FDGPU_ATAB_ENTRIES  9u            /* 0 (identity), 1A .. 8A (A negated) */
+#define FDGPU_ATAB_WORDS    40u           /* u32 per cached entry */
+#define FDGPU_WS_ENTRIES    10u           /* per-lane workspace entries: table + parked (x_R, y_R) */
+#define FDGPU_BLOCK         256u
+#define FDGPU_FLAG_REF_MAP  1u            /* portable-backend error mapping */
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* launchers (fdgpu_kernels.hip); all asynchronous on `stream` */
+hipError_t fdgpu_launch_btab_init(uint32_t *d_btab, hipStream_t stream);
+/* one signature per lane; d_ws must hold fdgpu_ws_bytes(n_sig) bytes */
+hipError_t fdgpu_launch_verify_sigs(const uint8_t *d_arena, const fdgpu_sig_desc_t *d_sigs, uint32_t n_sig,
+                                    const uint32_t *d_btab, uint32_t *d_ws, int8_t *d_sig_codes, uint32_t flags,
+                                    hipStream_t stream);
+hipError_t fdgpu_launch_combine(const fdgpu_txn_desc_t *d_txns, uint32_t n_txn, const int8_t *d_sig_codes,
+                                int8_t *d_txn_codes, hipStream_t stream);
+hipError_t fdgpu_verify_occupancy(int *blocks_per_cu);
+size_t     fdgpu_ws_bytes(uint64_t n_sig);
+
+/* test/diagnostic kernels */
+hipError_t fdgpu_launch_test_fe(const uint32_t *d_in, uint32_t *d_out, uint32_t n, hipStream_t stream);
+hipError_t fdgpu_launch_test_decode(const uint32_t *d_enc, uint32_t *d_out, uint32_t n, uint32_t flags, hipStream_t stream);
+hipError_t fdgpu_launch_test_sha512(const uint8_t *d_arena, const fdgpu_sig_desc_t *d_msgs, uint32_t n,
+                                    uint32_t *d_out, hipStream_t stream);
+hipError_t fdgpu_launch_test_hram(const uint8_t *d_arena, const fdgpu_sig_desc_t *d_sigs, uint32_t n,
+                                  uint32_t *d_out, hipStream_t stream);
+hipError_t fdgpu_launch_test_sc_reduce(const uint32_t *d_in, uint32_t *d_out, uint32_t n, hipStream_t stream);
+
+#ifdef __cplusplus
+}
+#endif

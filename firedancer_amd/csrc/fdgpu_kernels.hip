@@ -1,0 +1,428 @@
+/* fdgpu_kernels.hip -- MI355X (gfx950) kernels of the batched Ed25519
+   verify engine.
+
+   fdgpu_verify_sigs: one signature per lane, whole verify in one pass
+     (fd_ed25519_user.c:135-230):
+       S < L  ->  SHA-512(R||A||M) mod L  ->  decode A, R  ->  small-order
+       tests  ->  [S]B + [k](-A) == R  ->  per-signature code.
+     Every lane executes the same instruction stream (failures are masked,
+     not branched on; a wave whose lanes all failed pass 1 skips the scalar
+     multiplication).  The double-scalar multiplication uses fixed signed
+     windows: radix 16 for k over a per-lane table {O, -A, ..., -8A} kept
+     in a global workspace laid out lane-interleaved, and radix 256 for S
+     over the fixed table {O, B, ..., 128B} staged into LDS once per
+     workgroup (the reference's wNAF-4 / wNAF-8 split,
+     fd_curve25519.c:109-153, made divergence-free).
+     Persistent grid: grid = resident workgroups, grid-stride over the batch.
+   fdgpu_combine: per transaction, batch_single_msg first-error semantics
+     (fd_ed25519_user.c:232-310).
+   fdgpu_btab_init: builds the B table on the device at engine open. */
+#include <hip/hip_runtime.h>
+
+#include "fdgpu_ge.h"
+#include "fdgpu_internal.h"
+#include "fdgpu_sc.h"
+#include "fdgpu_sha512.h"
+
+using namespace fdgpu;
+
+namespace {
+
+FDG_DEV void load32(uint32_t (&w)[8], const uint8_t *p) {
+  /* 32-byte field (any 4-byte alignment in practice; use dword loads) */
+  const uint32_t *q = (const uint32_t *)p;
+  if (((uintptr_t)p & 3u) == 0) {
+#pragma unroll
+    for (int i = 0; i < 8; i++) w[i] = q[i];
+  } else {
+#pragma unroll
+    for (int i = 0; i < 8; i++) w[i] = load_u32_unaligned(p + 4 * i);
+  }
+}
+
+/* ---- B table: entry j = j*B in affine niels form, canonical limbs ---- */
+
+FDG_DEV void niels_store(uint32_t *dst, const fe &ypx, const fe &ymx, const fe &xy2d) {
+#pragma unroll
+  for (int i = 0; i < 10; i++) { dst[i] = ypx.v[i]; dst[10 + i] = ymx.v[i]; dst[20 + i] = xy2d.v[i]; }
+  dst[30] = 0; dst[31] = 0;
+}
+
+__global__ void fdgpu_btab_init_kernel(uint32_t *btab) {
+  const uint32_t j = threadIdx.x;                       /* 0 .. 128 */
+  if (j >= FDGPU_BTAB_ENTRIES) return;
+  fe one; fe_1(one);
+  if (j == 0) { fe z; fe_0(z); niels_store(btab, one, one, z); return; }
+  constexpr uint32_t BX[10] = FDGPU_FE_BX, BY[10] = FDGPU_FE_BY, BT[10] = FDGPU_FE_BT, D2[10] = FDGPU_FE_D2;
+  ge_p3 B; fe_set(B.X, BX); fe_set(B.Y, BY); fe_1(B.Z); fe_set(B.T, BT);
+  ge_cached Bc; ge_p3_to_cached(Bc, B);
+  ge_p3 acc; ge_p3_0(acc);
+  ge_p1p1 t;
+  for (int bit = 7; bit >= 0; bit--) {                  /* binary left-to-right: acc = j*B */
+    ge_p2 a2; ge_p3_to_p2(a2, acc);
+    ge_dbl(t, a2); ge_p1p1_to_p3(acc, t);
+    if ((j >> bit) & 1u) { ge_add_cached(t, acc, Bc, false); ge_p1p1_to_p3(acc, t); }
+  }
+  fe zi, x, y, xy, d2, ypx, ymx, xy2d;
+  fe_invert(zi, acc.Z);
+  fe_mul(x, acc.X, zi); fe_mul(y, acc.Y, zi);
+  fe_set(d2, D2);
+  fe_add(ypx, y, x); fe_canon(ypx);
+  fe_sub(ymx, y, x); fe_canon(ymx);
+  fe_mul(xy, x, y); fe_mul(xy2d, xy, d2); fe_canon(xy2d);
+  niels_store(btab + j * FDGPU_BTAB_STRIDE, ypx, ymx, xy2d);
+}
+
+/* ---- per-lane A table in the global workspace ----
+   layout: ws[((wave * 10 + entry) * 40 + word) * 64 + lane]  (dword per lane,
+   a wave's access to one entry-word is one 256-B row).  Entries 0..8 are the
+   table; entry 9 parks (x_R, y_R) across the scalar multiplication. */
+
+FDG_DEV void atab_store(uint32_t *wsl, uint32_t entry, const ge_cached &c) {
+  uint32_t *p = wsl + entry * (FDGPU_ATAB_WORDS * 64u);
+#pragma unroll
+  for (int i = 0; i < 10; i++) {
+    p[(0 + i) * 64] = c.YpX.v[i]; p[(10 + i) * 64] = c.YmX.v[i];
+    p[(20 + i) * 64] = c.Z2.v[i]; p[(30 + i) * 64] = c.T2d.v[i];
+  }
+}
+FDG_DEV int sext4(uint32_t x) { return ((int)(x << 28)) >> 28; }
+FDG_DEV int sext8(uint32_t x) { return ((int)(x << 24)) >> 24; }
+
+/* shift a 256-bit little-endian word vector left by 8 bits */
+FDG_DEV void shl8(uint32_t (&w)[8]) {
+#pragma unroll
+  for (int i = 7; i > 0; i--) w[i] = (w[i] << 8) | (w[i - 1] >> 24);
+  w[0] <<= 8;
+}
+
+/* R' = [S]B + [k](-A) as projective (X:Y:Z).  kd: radix-16 digits of k,
+   sd: radix-256 digits of S; wsl: this lane's A table (entries 0..8). */
+FDG_DEV void dsm(ge_p2 &acc2, uint32_t (&kd)[8], uint32_t (&sd)[8], const uint32_t *wsl,
+                 const uint32_t *s_btab) {
+  ge_p2_0(acc2);
+  ge_p3 acc3;
+  ge_p1p1 t;
+#pragma unroll 1
+  for (int j = 31; j >= 0; j--) {
+    const uint32_t kb = kd[7] >> 24, sb = sd[7] >> 24;
+    shl8(kd); shl8(sd);
+#pragma unroll 1
+    for (int h = 0; h < 2; h++) {
+      const int e = sext4(h == 0 ? (kb >> 4) : (kb & 15u));
+#pragma unroll 1
+      for (int r = 0; r < 4; r++) {
+        ge_dbl(t, acc2);
+        ge_p1p1_to_p2(acc2, t);
+      }
+      /* T of the last doubling (p1p1 -> p3 needs X'Y') */
+      acc3.X = acc2.X; acc3.Y = acc2.Y; acc3.Z = acc2.Z; fe_mul(acc3.T, t.X, t.Y);
+      {
+        const uint32_t *ent = wsl + (uint32_t)(e < 0 ? -e : e) * (FDGPU_ATAB_WORDS * 64u);
+        auto ld = [ent](int c, int w) { return ent[(10 * c + w) * 64]; };
+        ge_add_cached_ld(t, acc3, ld, e < 0);
+      }
+      if (h == 1) {
+        const int d = sext8(sb);
+        ge_p1p1_to_p3(acc3, t);
+        const uint32_t *ent = s_btab + (uint32_t)(d < 0 ? -d : d) * FDGPU_BTAB_STRIDE;
+        auto ld = [ent](int c, int w) { return ent[10 * c + w]; };
+        ge_add_niels_ld(t, acc3, ld, d < 0);
+      }
+      ge_p1p1_to_p2(acc2, t);
+    }
+  }
+}
+
+/* Build this lane's table {O, -A, -2A, ..., -8A} (cached form) in the workspace. */
+FDG_DEV void atab_build(uint32_t *wsl, const ge_p3 &An) {
+  ge_cached c;
+  ge_cached_0(c); atab_store(wsl, 0, c);
+  ge_p3_to_cached(c, An); atab_store(wsl, 1, c);
+  ge_p1p1 t; ge_p2 a2; ge_p3 P;
+  ge_p3_to_p2(a2, An); ge_dbl(t, a2); ge_p1p1_to_p3(P, t);          /* 2(-A) */
+  ge_p3_to_cached(c, P); atab_store(wsl, 2, c);
+  const uint32_t *ent1 = wsl + 1u * (FDGPU_ATAB_WORDS * 64u);
+  auto ld1 = [ent1](int cc, int w) { return ent1[(10 * cc + w) * 64]; };
+#pragma unroll 1
+  for (uint32_t e = 3; e <= 8; e++) {
+    ge_add_cached_ld(t, P, ld1, false); ge_p1p1_to_p3(P, t);
+    ge_p3_to_cached(c, P); atab_store(wsl, e, c);
+  }
+}
+
+/* Full verify of one signature.  Returns the reference's code for the
+   single-signature verify (0 / -1 / -2 / -3).  Phases are ordered so that
+   only the bytes/scalars still needed stay live in VGPRs. */
+FDG_DEV int verify_one(const uint8_t *arena, const fdgpu_sig_desc_t &sd_in, uint32_t nblk_wave,
+                       uint32_t *wsl, const uint32_t *s_btab, bool ref_map) {
+  uint32_t R[8], A[8];
+  load32(R, arena + sd_in.sig_off);
+  load32(A, arena + sd_in.pub_off);
+
+  /* step 5 first (pure function of the bytes): k = SHA-512(R || A || M) mod L */
+  uint32_t k[8];
+  {
+    uint64_t h[8];
+    sha512_hram(h, R, A, arena + sd_in.msg_off, sd_in.msg_sz, nblk_wave);
+    uint32_t kx[16];
+#pragma unroll
+    for (int i = 0; i < 8; i++) { kx[2 * i] = bswap32((uint32_t)(h[i] >> 32)); kx[2 * i + 1] = bswap32((uint32_t)h[i]); }
+    sc_reduce512(k, kx);
+  }
+
+  /* step 1: S < L (fd_ed25519_user.c:159-161) */
+  int code;
+  {
+    uint32_t S[8];
+    load32(S, arena + sd_in.sig_off + 32);
+    code = sc_lt_L(S) ? 0 : -1;
+  }
+
+  /* step 2 (A): decode, small order, then table of -A */
+  bool a_ok, a_small;
+  {
+    ge_p3 Ap;
+    a_ok = ge_decode(Ap, A, ref_map);
+    a_small = ge_is_small_order_affine(Ap);
+    ge_p3 An; ge_p3_neg(An, Ap);
+    atab_build(wsl, An);
+  }
+  /* step 2 (R): decode, small order; keep affine x_R, y_R */
+  bool r_ok, r_small;
+  {
+    ge_p3 Rp;
+    r_ok = ge_decode(Rp, R, ref_map);
+    r_small = ge_is_small_order_affine(Rp);
+    ge_cached park; park.YpX = Rp.X; park.YmX = Rp.Y; fe_0(park.Z2); fe_0(park.T2d);
+    atab_store(wsl, 9, park);      /* x_R, y_R parked in the workspace */
+  }
+  if (code == 0 && !a_ok) code = ref_map ? -2 : -1;    /* decode2 reports A before R */
+  if (code == 0 && !r_ok) code = -1;
+  if (code == 0 && a_small) code = -2;                 /* fd_ed25519_user.c:194-199 */
+  if (code == 0 && r_small) code = -1;
+
+  /* wave-uniform early out when every lane already failed */
+  if (__all(code != 0)) return code;
+
+  /* step 6: [S]B + [k](-A) == R, cofactorless, projective compare */
+  uint32_t kd[8], sdg[8];
+  sc_recode16(kd, k);
+  {
+    uint32_t S[8];
+    load32(S, arena + sd_in.sig_off + 32);
+    sc_recode256(sdg, S);
+  }
+  ge_p2 Rc;
+  dsm(Rc, kd, sdg, wsl, s_btab);
+  fe l, xy;
+  const uint32_t *park = wsl + 9u * (FDGPU_ATAB_WORDS * 64u);
+#pragma unroll
+  for (int i = 0; i < 10; i++) xy.v[i] = park[i * 64];
+  fe_mul(l, xy, Rc.Z);
+  bool eq = fe_eq(Rc.X, l);
+#pragma unroll
+  for (int i = 0; i < 10; i++) xy.v[i] = park[(10 + i) * 64];
+  fe_mul(l, xy, Rc.Z);
+  eq = eq && fe_eq(Rc.Y, l);
+  if (code == 0 && !eq) code = -3;
+  return code;
+}
+
+__global__ void __launch_bounds__(FDGPU_BLOCK, 2)
+fdgpu_verify_sigs_kernel(const uint8_t *__restrict__ arena, const fdgpu_sig_desc_t *__restrict__ sigs,
+                         uint32_t n_sig, const uint32_t *__restrict__ btab, uint32_t *__restrict__ ws,
+                         int8_t *__restrict__ codes, uint32_t flags) {
+  __shared__ __attribute__((aligned(16))) uint32_t s_btab[FDGPU_BTAB_ENTRIES * FDGPU_BTAB_STRIDE];
+  for (uint32_t i = threadIdx.x; i < FDGPU_BTAB_ENTRIES * FDGPU_BTAB_STRIDE; i += blockDim.x) s_btab[i] = btab[i];
+  __syncthreads();
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  uint32_t *wsl = ws + (size_t)(i >> 6) * (FDGPU_WS_ENTRIES * FDGPU_ATAB_WORDS * 64u) + lane;
+  const bool ref_map = (flags & FDGPU_FLAG_REF_MAP) != 0;
+  const bool active = i < n_sig;
+  const fdgpu_sig_desc_t d = sigs[active ? i : n_sig - 1];
+  /* wave-uniform SHA block bound */
+  uint32_t nb = sha512_hram_blocks(d.msg_sz);
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) nb = max(nb, (uint32_t)__shfl_xor((int)nb, off));
+  const int code = verify_one(arena, d, nb, wsl, s_btab, ref_map);
+  if (active) codes[i] = (int8_t)code;
+}
+
+__global__ void fdgpu_combine_kernel(const fdgpu_txn_desc_t *__restrict__ txns, uint32_t n_txn,
+                                     const int8_t *__restrict__ sig_codes, int8_t *__restrict__ txn_codes) {
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= n_txn) return;
+  const fdgpu_txn_desc_t d = txns[t];
+  int code;
+  if (d.sig_cnt == 0 || d.sig_cnt > 16) {
+    code = -1;                                           /* fd_ed25519_user.c:238-241 */
+  } else {
+    int first_struct = 0, any_msg = 0;
+    for (uint32_t j = 0; j < d.sig_cnt; j++) {
+      const int c = sig_codes[d.sig0 + j];
+      if (c == -3) any_msg = 1;
+      else if (c != 0 && first_struct == 0) first_struct = c;
+    }
+    /* pass 1 reports its first failure before any pass-2 (equation) failure */
+    code = first_struct ? first_struct : (any_msg ? -3 : 0);
+  }
+  txn_codes[t] = (int8_t)code;
+}
+
+/* ---------------- test / diagnostic kernels ---------------- */
+
+/* in: n records of 2 x 8 u32 (a, b < 2^255 as LE words); out: n records of
+   8 ops x 8 u32 canonical: a*b, a^2, a+b, a-b, pow22523(a), invert(a), canon(a), -a */
+__global__ void __launch_bounds__(64) fdgpu_test_fe_kernel(const uint32_t *in, uint32_t *out, uint32_t n) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  uint32_t aw[8], bw[8];
+#pragma unroll
+  for (int j = 0; j < 8; j++) { aw[j] = in[16 * i + j]; bw[j] = in[16 * i + 8 + j]; }
+  fe a, b, r;
+  fe_frombytes(a, aw); fe_frombytes(b, bw);
+  uint32_t o[8];
+  uint32_t *dst = out + 64 * i;
+  fe_mul(r, a, b); fe_tobytes(o, r);
+  for (int j = 0; j < 8; j++) dst[j] = o[j];
+  fe_sq(r, a); fe_tobytes(o, r);
+  for (int j = 0; j < 8; j++) dst[8 + j] = o[j];
+  fe_add(r, a, b); fe_tobytes(o, r);
+  for (int j = 0; j < 8; j++) dst[16 + j] = o[j];
+  fe_sub(r, a, b); fe_tobytes(o, r);
+  for (int j = 0; j < 8; j++) dst[24 + j] = o[j];
+  fe_pow22523(r, a); fe_tobytes(o, r);
+  for (int j = 0; j < 8; j++) dst[32 + j] = o[j];
+  fe_invert(r, a); fe_tobytes(o, r);
+  for (int j = 0; j < 8; j++) dst[40 + j] = o[j];
+  fe_tobytes(o, a);
+  for (int j = 0; j < 8; j++) dst[48 + j] = o[j];
+  fe_neg(r, a); fe_tobytes(o, r);
+  for (int j = 0; j < 8; j++) dst[56 + j] = o[j];
+}
+
+/* in: n encodings (8 u32); out: n x 18 u32: [rc, small_order, x(8), y(8)] */
+__global__ void __launch_bounds__(64) fdgpu_test_decode_kernel(const uint32_t *enc, uint32_t *out, uint32_t n, uint32_t flags) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  uint32_t e[8];
+  for (int j = 0; j < 8; j++) e[j] = enc[8 * i + j];
+  ge_p3 P;
+  const bool ok = ge_decode(P, e, (flags & FDGPU_FLAG_REF_MAP) != 0);
+  uint32_t *dst = out + 18 * i;
+  dst[0] = ok ? 0u : 0xffffffffu;
+  dst[1] = ok ? (ge_is_small_order_affine(P) ? 1u : 0u) : 0xffffffffu;
+  uint32_t x[8], y[8];
+  fe_tobytes(x, P.X); fe_tobytes(y, P.Y);
+  for (int j = 0; j < 8; j++) { dst[2 + j] = x[j]; dst[10 + j] = y[j]; }
+}
+
+/* SHA-512 of arena[msg_off .. +msg_sz]; out: n x 16 u32 (digest bytes, LE words) */
+__global__ void __launch_bounds__(64) fdgpu_test_sha512_kernel(const uint8_t *arena, const fdgpu_sig_desc_t *msgs, uint32_t n,
+                                         uint32_t *out) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  const bool active = i < n;
+  const fdgpu_sig_desc_t d = msgs[active ? i : n - 1];
+  uint32_t nb = (d.msg_sz + 16u) / 128u + 1u;
+  for (int off = 32; off > 0; off >>= 1) nb = max(nb, (uint32_t)__shfl_xor((int)nb, off));
+  uint64_t h[8];
+  sha512_plain(h, arena + d.msg_off, d.msg_sz, nb);
+  if (!active) return;
+  for (int j = 0; j < 8; j++) {
+    out[16 * i + 2 * j] = bswap32((uint32_t)(h[j] >> 32));
+    out[16 * i + 2 * j + 1] = bswap32((uint32_t)h[j]);
+  }
+}
+
+/* k = SHA-512(R||A||M) mod L per signature; out: n x 8 u32 */
+__global__ void __launch_bounds__(64) fdgpu_test_hram_kernel(const uint8_t *arena, const fdgpu_sig_desc_t *sigs, uint32_t n,
+                                       uint32_t *out) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  const bool active = i < n;
+  const fdgpu_sig_desc_t d = sigs[active ? i : n - 1];
+  uint32_t nb = sha512_hram_blocks(d.msg_sz);
+  for (int off = 32; off > 0; off >>= 1) nb = max(nb, (uint32_t)__shfl_xor((int)nb, off));
+  uint32_t R[8], A[8];
+  load32(R, arena + d.sig_off);
+  load32(A, arena + d.pub_off);
+  uint64_t h[8];
+  sha512_hram(h, R, A, arena + d.msg_off, d.msg_sz, nb);
+  uint32_t kx[16], k[8];
+  for (int j = 0; j < 8; j++) { kx[2 * j] = bswap32((uint32_t)(h[j] >> 32)); kx[2 * j + 1] = bswap32((uint32_t)h[j]); }
+  sc_reduce512(k, kx);
+  if (!active) return;
+  for (int j = 0; j < 8; j++) out[8 * i + j] = k[j];
+}
+
+__global__ void __launch_bounds__(64) fdgpu_test_sc_reduce_kernel(const uint32_t *in, uint32_t *out, uint32_t n) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  uint32_t x[16], r[8];
+  for (int j = 0; j < 16; j++) x[j] = in[16 * i + j];
+  sc_reduce512(r, x);
+  for (int j = 0; j < 8; j++) out[8 * i + j] = r[j];
+}
+
+}  // namespace
+
+extern "C" {
+
+hipError_t fdgpu_launch_btab_init(uint32_t *d_btab, hipStream_t stream) {
+  hipLaunchKernelGGL(fdgpu_btab_init_kernel, dim3(1), dim3(192), 0, stream, d_btab);
+  return hipGetLastError();
+}
+
+hipError_t fdgpu_verify_occupancy(int *blocks_per_cu) {
+  return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, fdgpu_verify_sigs_kernel, FDGPU_BLOCK, 0);
+}
+
+size_t fdgpu_ws_bytes(uint64_t n_sig) {
+  const uint64_t waves = (n_sig + FDGPU_BLOCK - 1) / FDGPU_BLOCK * (FDGPU_BLOCK / 64u);
+  return (size_t)waves * FDGPU_WS_ENTRIES * FDGPU_ATAB_WORDS * 64u * sizeof(uint32_t);
+}
+
+hipError_t fdgpu_launch_verify_sigs(const uint8_t *d_arena, const fdgpu_sig_desc_t *d_sigs, uint32_t n_sig,
+                                    const uint32_t *d_btab, uint32_t *d_ws, int8_t *d_sig_codes, uint32_t flags,
+                                    hipStream_t stream) {
+  if (!n_sig) return hipSuccess;
+  const uint32_t grid = (n_sig + FDGPU_BLOCK - 1) / FDGPU_BLOCK;
+  hipLaunchKernelGGL(fdgpu_verify_sigs_kernel, dim3(grid), dim3(FDGPU_BLOCK), 0, stream, d_arena, d_sigs, n_sig,
+                     d_btab, d_ws, d_sig_codes, flags);
+  return hipGetLastError();
+}
+
+hipError_t fdgpu_launch_combine(const fdgpu_txn_desc_t *d_txns, uint32_t n_txn, const int8_t *d_sig_codes,
+                                int8_t *d_txn_codes, hipStream_t stream) {
+  if (!n_txn) return hipSuccess;
+  hipLaunchKernelGGL(fdgpu_combine_kernel, dim3((n_txn + 255) / 256), dim3(256), 0, stream, d_txns, n_txn,
+                     d_sig_codes, d_txn_codes);
+  return hipGetLastError();
+}
+
+hipError_t fdgpu_launch_test_fe(const uint32_t *d_in, uint32_t *d_out, uint32_t n, hipStream_t stream) {
+  hipLaunchKernelGGL(fdgpu_test_fe_kernel, dim3((n + 63) / 64), dim3(64), 0, stream, d_in, d_out, n);
+  return hipGetLastError();
+}
+hipError_t fdgpu_launch_test_decode(const uint32_t *d_enc, uint32_t *d_out, uint32_t n, uint32_t flags,
+                                    hipStream_t stream) {
+  hipLaunchKernelGGL(fdgpu_test_decode_kernel, dim3((n + 63) / 64), dim3(64), 0, stream, d_enc, d_out, n, flags);
+  return hipGetLastError();
+}
+hipError_t fdgpu_launch_test_sha512(const uint8_t *d_arena, const fdgpu_sig_desc_t *d_msgs, uint32_t n,
+                                    uint32_t *d_out, hipStream_t stream) {
+  hipLaunchKernelGGL(fdgpu_test_sha512_kernel, dim3((n + 63) / 64), dim3(64), 0, stream, d_arena, d_msgs, n, d_out);
+  return hipGetLastError();
+}
+hipError_t fdgpu_launch_test_hram(const uint8_t *d_arena, const fdgpu_sig_desc_t *d_sigs, uint32_t n,
+                                  uint32_t *d_out, hipStream_t stream) {
+  hipLaunchKernelGGL(fdgpu_test_hram_kernel, dim3((n + 63) / 64), dim3(64), 0, stream, d_arena, d_sigs, n, d_out);
+  return hipGetLastError();
+}
+hipError_t fdgpu_launch_test_sc_reduce(const uint32_t *d_in, uint32_t *d_out, uint32_t n, hipStream_t stream) {
+  hipLaunchKernelGGL(fdgpu_test_sc_reduce_kernel, dim3((n + 63) / 64), dim3(64), 0, stream, d_in, d_out, n);
+  return hipGetLastError();
+}
+
+}  // extern "C"

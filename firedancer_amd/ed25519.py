@@ -1,0 +1,203 @@
+"""Python mirror of the reference's Ed25519 verify interface, served by the
+MI355X engine through the C ABI (include/fd_ed25519_gpu.h).
+
+Reference interface (src/ballet/ed25519/fd_ed25519.h):
+  FD_ED25519_SUCCESS / ERR_SIG / ERR_PUBKEY / ERR_MSG       :11-14
+  fd_ed25519_verify(msg, msg_sz, sig, public_key, sha)      :96-101
+  fd_ed25519_verify_batch_single_msg(msg, msg_sz, signatures, pubkeys, shas, batch_sz)  :124-130
+  fd_ed25519_strerror(err)                                  :132-136
+
+Same names (without the fd_ed25519_ prefix), argument meaning and codes;
+the SHA-512 scratch objects are accepted and ignored (hashing is on the GPU).
+The batched engine (VerifyEngine) is the throughput path used by the verify
+stage; per-transaction results equal fd_ed25519_verify_batch_single_msg.
+"""
+import ctypes
+
+import numpy as np
+
+from . import _lib
+
+SUCCESS, ERR_SIG, ERR_PUBKEY, ERR_MSG = 0, -1, -2, -3
+
+FLAG_REF_MAPPING = 1
+
+# fdgpu_txn_t as a numpy record (msg_off, msg_sz, sig_off, pub_off, sig_cnt)
+TXN_DTYPE = np.dtype([("msg_off", "<u4"), ("msg_sz", "<u4"), ("sig_off", "<u4"),
+                      ("pub_off", "<u4"), ("sig_cnt", "<u4")])
+SIG_DESC_DTYPE = np.dtype([("msg_off", "<u4"), ("msg_sz", "<u4"), ("sig_off", "<u4"), ("pub_off", "<u4")])
+TXN_DESC_DTYPE = np.dtype([("sig0", "<u4"), ("sig_cnt", "<u4")])
+ARENA_SLACK = 160
+
+
+def verify(msg, sig, public_key, sha=None):
+    """fd_ed25519_verify: returns SUCCESS or an ERR_* code."""
+    msg = bytes(msg)
+    sig, public_key = bytes(sig), bytes(public_key)
+    if len(sig) != 64 or len(public_key) != 32:
+        raise ValueError("sig must be 64 bytes and public_key 32 bytes")
+    return _lib.lib().fd_ed25519_verify(msg, len(msg), sig, public_key, None)
+
+
+def verify_batch_single_msg(msg, signatures, pubkeys, shas, batch_sz):
+    """fd_ed25519_verify_batch_single_msg: batch_sz in [1,16] else ERR_SIG."""
+    msg = bytes(msg)
+    signatures, pubkeys = bytes(signatures), bytes(pubkeys)
+    n = int(batch_sz)
+    if n < 0 or n > 255:
+        raise ValueError("batch_sz is a uchar")
+    if 1 <= n <= 16 and (len(signatures) < 64 * n or len(pubkeys) < 32 * n):
+        raise ValueError("signatures/pubkeys shorter than batch_sz records")
+    return _lib.lib().fd_ed25519_verify_batch_single_msg(msg, len(msg), signatures, pubkeys, None, n)
+
+
+def strerror(err):
+    """fd_ed25519_strerror."""
+    return _lib.lib().fd_ed25519_strerror(int(err)).decode()
+
+
+def expand_txns(txns):
+    """Per-signature and per-transaction descriptors for the device path
+    (the same expansion the engine's submit performs on the host)."""
+    txns = np.asarray(txns, dtype=TXN_DTYPE)
+    cnt = txns["sig_cnt"].astype(np.int64)
+    valid = (cnt >= 1) & (cnt <= 16)
+    used = np.where(valid, cnt, 0)
+    sig0 = np.zeros(len(txns), dtype=np.int64)
+    if len(txns):
+        sig0[1:] = np.cumsum(used)[:-1]
+    n_sig = int(used.sum())
+    tdesc = np.zeros(len(txns), dtype=TXN_DESC_DTYPE)
+    tdesc["sig0"] = sig0
+    tdesc["sig_cnt"] = used
+    sdesc = np.zeros(n_sig, dtype=SIG_DESC_DTYPE)
+    t_of_sig = np.repeat(np.arange(len(txns)), used)
+    j = np.arange(n_sig) - sig0[t_of_sig]
+    sdesc["msg_off"] = txns["msg_off"][t_of_sig]
+    sdesc["msg_sz"] = txns["msg_sz"][t_of_sig]
+    sdesc["sig_off"] = txns["sig_off"][t_of_sig] + 64 * j
+    sdesc["pub_off"] = txns["pub_off"][t_of_sig] + 32 * j
+    return sdesc, tdesc
+
+
+class VerifyEngine:
+    """One engine per GPU: pinned double-buffered rings, HIP streams, and the
+    verify kernels.  submit()/poll() is the asynchronous batch API;
+    verify_txns() is submit + blocking poll."""
+
+    def __init__(self, device=0, max_txn=1 << 16, max_sig=None, max_arena=None, ring_depth=2, ref_mapping=False):
+        L = _lib.lib()
+        cfg = _lib.FdgpuCfg(max_txn, max_sig or 2 * max_txn, max_arena or 1232 * max_txn, ring_depth,
+                            FLAG_REF_MAPPING if ref_mapping else 0)
+        self._cfg = cfg
+        self._h = L.fdgpu_engine_open(int(device), ctypes.byref(cfg))
+        if not self._h:
+            raise RuntimeError(f"fdgpu_engine_open({device}) failed: {_lib.last_error()}")
+        self.device = device
+        self._pending = {}
+
+    def close(self):
+        if self._h:
+            _lib.lib().fdgpu_engine_close(self._h)
+            self._h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def info(self):
+        g, b, w = ctypes.c_uint32(), ctypes.c_uint32(), ctypes.c_uint64()
+        _lib.lib().fdgpu_engine_info(self._h, ctypes.byref(g), ctypes.byref(b), ctypes.byref(w))
+        return {"resident_blocks": g.value, "block_threads": b.value, "ws_bytes": w.value}
+
+    def submit(self, arena, txns):
+        arena = np.ascontiguousarray(arena, dtype=np.uint8)
+        txns = np.ascontiguousarray(txns, dtype=TXN_DTYPE)
+        tk = _lib.lib().fdgpu_submit(self._h, arena.ctypes.data, arena.size, txns.ctypes.data, len(txns))
+        if tk < 0:
+            raise RuntimeError(f"fdgpu_submit failed ({tk}): {_lib.last_error()}")
+        self._pending[tk] = len(txns)
+        return tk
+
+    def poll(self, ticket, blocking=True):
+        n = self._pending.get(ticket)
+        if n is None:
+            raise KeyError(ticket)
+        out = np.zeros(max(n, 1), dtype=np.int8)
+        rc = _lib.lib().fdgpu_poll(self._h, ticket, out.ctypes.data, 1 if blocking else 0)
+        if rc == 1:
+            return None
+        if rc != 0:
+            raise RuntimeError(f"fdgpu_poll failed ({rc}): {_lib.last_error()}")
+        del self._pending[ticket]
+        return out[:n]
+
+    def verify_txns(self, arena, txns):
+        return self.poll(self.submit(arena, txns), blocking=True)
+
+    def verify_device(self, d_arena, d_sig_desc, n_sig, d_txn_desc, n_txn, d_sig_codes, d_txn_codes, stream=0):
+        """Device-resident path; all pointers are device addresses (ints)."""
+        rc = _lib.lib().fdgpu_verify_device(self._h, d_arena, d_sig_desc, n_sig, d_txn_desc, n_txn,
+                                            d_sig_codes, d_txn_codes, stream or None)
+        if rc != 0:
+            raise RuntimeError(f"fdgpu_verify_device failed ({rc}): {_lib.last_error()}")
+
+    # ---- per-stage diagnostics (parity tests) ----
+    def _chk(self, rc, what):
+        if rc != 0:
+            raise RuntimeError(f"{what} failed ({rc}): {_lib.last_error()}")
+
+    def debug_fe_ops(self, ab):
+        ab = np.ascontiguousarray(ab, dtype=np.uint8).reshape(-1, 64)
+        out = np.zeros((len(ab), 8, 32), dtype=np.uint8)
+        self._chk(_lib.lib().fdgpu_debug_fe_ops(self._h, ab.ctypes.data, len(ab), out.ctypes.data), "debug_fe_ops")
+        return out
+
+    def debug_decode(self, enc, ref_mapping=False):
+        enc = np.ascontiguousarray(enc, dtype=np.uint8).reshape(-1, 32)
+        out = np.zeros((len(enc), 72), dtype=np.uint8)
+        self._chk(_lib.lib().fdgpu_debug_decode(self._h, enc.ctypes.data, len(enc), 1 if ref_mapping else 0,
+                                                out.ctypes.data), "debug_decode")
+        rc = out[:, 0:4].copy().view(np.int32)[:, 0]
+        so = out[:, 4:8].copy().view(np.int32)[:, 0]
+        return rc, so, out[:, 8:40], out[:, 40:72]
+
+    def debug_sha512(self, arena, txns):
+        arena = np.ascontiguousarray(arena, dtype=np.uint8)
+        txns = np.ascontiguousarray(txns, dtype=TXN_DTYPE)
+        out = np.zeros((len(txns), 64), dtype=np.uint8)
+        self._chk(_lib.lib().fdgpu_debug_sha512(self._h, arena.ctypes.data, arena.size, txns.ctypes.data, len(txns),
+                                                out.ctypes.data), "debug_sha512")
+        return out
+
+    def debug_hram(self, arena, txns):
+        arena = np.ascontiguousarray(arena, dtype=np.uint8)
+        txns = np.ascontiguousarray(txns, dtype=TXN_DTYPE)
+        out = np.zeros((len(txns), 32), dtype=np.uint8)
+        self._chk(_lib.lib().fdgpu_debug_hram(self._h, arena.ctypes.data, arena.size, txns.ctypes.data, len(txns),
+                                              out.ctypes.data), "debug_hram")
+        return out
+
+    def debug_sc_reduce(self, x):
+        x = np.ascontiguousarray(x, dtype=np.uint8).reshape(-1, 64)
+        out = np.zeros((len(x), 32), dtype=np.uint8)
+        self._chk(_lib.lib().fdgpu_debug_sc_reduce(self._h, x.ctypes.data, len(x), out.ctypes.data), "debug_sc_reduce")
+        return out
+
+    def debug_sig_codes(self, arena, txns):
+        arena = np.ascontiguousarray(arena, dtype=np.uint8)
+        txns = np.ascontiguousarray(txns, dtype=TXN_DTYPE)
+        cnt = txns["sig_cnt"].astype(np.int64)
+        n = int(np.where((cnt >= 1) & (cnt <= 16), cnt, 0).sum())
+        out = np.zeros(max(n, 1), dtype=np.int8)
+        self._chk(_lib.lib().fdgpu_debug_sig_codes(self._h, arena.ctypes.data, arena.size, txns.ctypes.data,
+                                                   len(txns), out.ctypes.data), "debug_sig_codes")
+        return out[:n]

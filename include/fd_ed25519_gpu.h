@@ -1,0 +1,168 @@
+/* fd_ed25519_gpu.h -- C ABI of the MI355X batched Ed25519 verify engine
+   (libfd_ed25519_gpu.so).  Plain C types only; no HIP or torch types.
+
+   Two surfaces:
+
+   (i) Drop-in synchronous API with the reference's prototypes and codes:
+         fd_ed25519_verify                  replaces src/ballet/ed25519/fd_ed25519.h:96-101
+                                            (impl fd_ed25519_user.c:135-230)
+         fd_ed25519_verify_batch_single_msg replaces src/ballet/ed25519/fd_ed25519.h:124-130
+                                            (impl fd_ed25519_user.c:232-310)
+         fd_ed25519_strerror                replaces src/ballet/ed25519/fd_ed25519.h:132-136
+                                            (impl fd_ed25519_user.c:312-322)
+       Served by the GPU engine (device 0, opened on first use); results are
+       bit-identical to the reference's AVX-512 build.  Each call is one GPU
+       round trip (tens of microseconds): correct, but the batch API below is
+       the throughput path.
+
+   (ii) Asynchronous batch API for the verify stage (the north-star shim;
+       SURVEY.md §8(b)(ii)).  One engine per GPU; each engine owns pinned,
+       double-buffered host/device rings and HIP streams.  A batch is a flat
+       payload arena plus per-transaction descriptors with
+       fd_ed25519_verify_batch_single_msg semantics per transaction (the
+       verify tile's fd_txn_verify call, src/app/fdctl/run/tiles/fd_verify.h:75).
+       Result per transaction: exactly the code the reference would return.
+
+   Threading: an engine is not thread-safe; use one host thread per engine
+   (one engine per GPU).  The synchronous API serialises on an internal lock. */
+#ifndef FD_ED25519_GPU_H
+#define FD_ED25519_GPU_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Result codes: identical values to src/ballet/ed25519/fd_ed25519.h:11-14 */
+#define FD_ED25519_SUCCESS    ( 0)
+#define FD_ED25519_ERR_SIG    (-1)
+#define FD_ED25519_ERR_PUBKEY (-2)
+#define FD_ED25519_ERR_MSG    (-3)
+
+/* ------------------------------------------------------------------ (i) */
+
+/* Opaque: the reference passes caller-owned SHA-512 scratch objects
+   (fd_sha512_t, src/ballet/sha512/fd_sha512.h:15-31).  The GPU engine hashes
+   on the device and never touches them; any pointer (or NULL) is accepted. */
+typedef struct fd_sha512_private fd_sha512_t;
+
+int fd_ed25519_verify( uint8_t const   msg[],        /* msg_sz bytes; NULL allowed iff msg_sz==0 */
+                       uint64_t        msg_sz,
+                       uint8_t const   sig[ 64 ],
+                       uint8_t const   public_key[ 32 ],
+                       fd_sha512_t *   sha );
+
+int fd_ed25519_verify_batch_single_msg( uint8_t const   msg[],
+                                        uint64_t const  msg_sz,
+                                        uint8_t const   signatures[ 64 ],  /* 64*batch_sz */
+                                        uint8_t const   pubkeys[ 32 ],     /* 32*batch_sz */
+                                        fd_sha512_t *   shas[ 1 ],         /* batch_sz, unused */
+                                        uint8_t const   batch_sz );
+
+char const * fd_ed25519_strerror( int err );
+
+/* ----------------------------------------------------------------- (ii) */
+
+/* One transaction of a batch (same layout as the oracle's test records):
+   signatures and public keys are sig_cnt contiguous 64-B / 32-B records;
+   the message is msg_sz bytes.  All offsets index the batch arena. */
+typedef struct {
+  uint32_t msg_off;
+  uint32_t msg_sz;
+  uint32_t sig_off;
+  uint32_t pub_off;
+  uint32_t sig_cnt;     /* verified iff 1 <= sig_cnt <= 16, else FD_ED25519_ERR_SIG */
+} fdgpu_txn_t;
+
+typedef struct fdgpu_engine fdgpu_engine_t;
+
+typedef struct {
+  uint64_t max_txn;       /* per batch */
+  uint64_t max_sig;       /* per batch (sum of sig_cnt) */
+  uint64_t max_arena;     /* per batch, bytes */
+  uint32_t ring_depth;    /* in-flight batches (pinned staging slots), >= 1; default 2 */
+  uint32_t flags;         /* FDGPU_FLAG_* */
+} fdgpu_cfg_t;
+
+#define FDGPU_FLAG_REF_MAPPING 1u  /* portable-backend (ref) error mapping instead of AVX-512 */
+
+/* Status codes of the engine API (distinct from verify codes). */
+#define FDGPU_OK            ( 0)
+#define FDGPU_PENDING       ( 1)
+#define FDGPU_ERR_INVAL     (-10)
+#define FDGPU_ERR_DEVICE    (-11)
+#define FDGPU_ERR_FULL      (-12)
+#define FDGPU_ERR_TICKET    (-13)
+
+/* Opens an engine on HIP device `device`.  Returns NULL on failure (no
+   device, allocation failure); fdgpu_last_error() describes it. */
+fdgpu_engine_t * fdgpu_engine_open( int device, fdgpu_cfg_t const * cfg );
+void             fdgpu_engine_close( fdgpu_engine_t * e );
+char const *     fdgpu_last_error( void );
+
+/* Stages the batch (copies arena + descriptors into the next pinned slot),
+   enqueues H2D copy, the verify kernels and the D2H copy of the per-txn
+   codes, and returns a ticket >= 0 without waiting for the GPU.  Blocks
+   only if all ring slots are in flight.  Returns < 0 on error. */
+int64_t fdgpu_submit( fdgpu_engine_t *    e,
+                      uint8_t const *     arena,
+                      uint64_t            arena_sz,
+                      fdgpu_txn_t const * txns,
+                      uint64_t            txn_cnt );
+
+/* Polls a ticket.  FDGPU_PENDING if still running (and !blocking);
+   FDGPU_OK when done, with txn_codes[0..txn_cnt) written (one verify code
+   per transaction, in submission order); < 0 on error. */
+int fdgpu_poll( fdgpu_engine_t * e, int64_t ticket, int8_t * txn_codes, int blocking );
+
+/* Device-resident path: inputs already in HBM (device pointers), codes
+   written to device memory, work enqueued on `hip_stream` (a hipStream_t,
+   NULL = the engine's compute stream).  d_sig_desc: per-signature
+   {msg_off, msg_sz, sig_off, pub_off} (16 B each); d_txn_desc: per-txn
+   {sig0, sig_cnt} (8 B each); d_arena must have 160 readable bytes of slack
+   past its last payload byte.  d_sig_codes may be NULL when only the
+   transaction codes are wanted (an engine-owned buffer is used). */
+int fdgpu_verify_device( fdgpu_engine_t * e,
+                         void const *     d_arena,
+                         void const *     d_sig_desc,
+                         uint64_t         sig_cnt,
+                         void const *     d_txn_desc,
+                         uint64_t         txn_cnt,
+                         int8_t *         d_sig_codes,
+                         int8_t *         d_txn_codes,
+                         void *           hip_stream );
+
+/* Engine facts for reporting: persistent grid size and resident lanes. */
+int fdgpu_engine_info( fdgpu_engine_t * e, uint32_t * grid_blocks, uint32_t * block_threads,
+                       uint64_t * ws_bytes );
+
+/* --------------------------------------------------------- diagnostics */
+/* Used by the parity tests to check each stage of the path on the GPU in
+   isolation.  Host pointers; synchronous.  Return FDGPU_OK or < 0. */
+
+/* n records of (a, b) as 2 x 32 LE bytes -> n x 8 x 32 bytes: canonical
+   a*b, a^2, a+b, a-b, a^((p-5)/8), 1/a, a mod p, -a (bit 255 of inputs dropped). */
+int fdgpu_debug_fe_ops( fdgpu_engine_t * e, uint8_t const * ab, uint64_t n, uint8_t * out );
+/* n 32-B encodings -> n x 72 B: int32 rc (0 / -1), int32 small_order (0/1, -1 if rc),
+   x (32 B canonical), y (32 B canonical). */
+int fdgpu_debug_decode( fdgpu_engine_t * e, uint8_t const * enc, uint64_t n, int ref_mapping, uint8_t * out );
+/* SHA-512 of n messages (arena + per-message {off, sz} as fdgpu_txn_t.msg_off/msg_sz) -> n x 64 B */
+int fdgpu_debug_sha512( fdgpu_engine_t * e, uint8_t const * arena, uint64_t arena_sz,
+                        fdgpu_txn_t const * msgs, uint64_t n, uint8_t * out );
+/* k = SHA-512(R || A || M) mod L for n single-signature txns -> n x 32 B */
+int fdgpu_debug_hram( fdgpu_engine_t * e, uint8_t const * arena, uint64_t arena_sz,
+                      fdgpu_txn_t const * txns, uint64_t n, uint8_t * out );
+/* n 64-B little-endian integers -> n x 32 B (x mod L) */
+int fdgpu_debug_sc_reduce( fdgpu_engine_t * e, uint8_t const * in, uint64_t n, uint8_t * out );
+/* per-signature codes of a batch (single-signature verify code of each
+   signature, in txn order) -> sig_codes[sum sig_cnt] */
+int fdgpu_debug_sig_codes( fdgpu_engine_t * e, uint8_t const * arena, uint64_t arena_sz,
+                           fdgpu_txn_t const * txns, uint64_t txn_cnt, int8_t * sig_codes );
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* FD_ED25519_GPU_H */

@@ -1,0 +1,338 @@
+"""GPU parity: every stage of the MI355X path against the CPU oracle / exact
+integer arithmetic, and whole-path result codes against the golden vectors.
+Bit-exact everywhere (integer/byte work; no tolerance applies)."""
+import hashlib
+import random
+
+import numpy as np
+import pytest
+
+import pyref_ed25519 as pyref
+from firedancer_amd import workload
+import firedancer_amd as fa
+
+pytestmark = pytest.mark.gpu
+
+P, L = pyref.P, pyref.L
+
+
+def _le(x, n=32):
+    return int(x % (1 << (8 * n))).to_bytes(n, "little")
+
+
+# ------------------------------------------------------------ field layer
+
+def test_field_ops(engine):
+    rnd = random.Random(11)
+    edge = [0, 1, 2, 19, P - 1, P, P + 1, P + 18, 2**255 - 1, 2**255 - 20, 2**254, 2**26 - 1, 2**51 + 7]
+    vals = edge + [rnd.getrandbits(255) for _ in range(500)]
+    pairs = [(a, b) for a in edge for b in edge] + [(rnd.choice(vals), rnd.choice(vals)) for _ in range(1500)]
+    ab = np.frombuffer(b"".join(_le(a) + _le(b) for a, b in pairs), dtype=np.uint8)
+    out = engine.debug_fe_ops(ab)
+    for i, (a, b) in enumerate(pairs):
+        a %= 2**255; b %= 2**255
+        got = [int.from_bytes(out[i, k].tobytes(), "little") for k in range(8)]
+        exp = [a * b % P, a * a % P, (a + b) % P, (a - b) % P, pow(a, (P - 5) // 8, P),
+               pow(a, P - 2, P), a % P, (-a) % P]
+        assert got == exp, (i, hex(a), hex(b), [g == e for g, e in zip(got, exp)])
+
+
+def test_scalar_reduce(engine):
+    rnd = random.Random(5)
+    xs = [0, 1, L - 1, L, L + 1, 2**512 - 1, L * L, (L - 1) * 2**259, 2**511] + [rnd.getrandbits(512) for _ in range(2000)]
+    xs = [x % 2**512 for x in xs]
+    out = engine.debug_sc_reduce(np.frombuffer(b"".join(_le(x, 64) for x in xs), dtype=np.uint8))
+    for i, x in enumerate(xs):
+        assert int.from_bytes(out[i].tobytes(), "little") == x % L, i
+
+
+# ------------------------------------------------------------ SHA-512
+
+def _msgs_arena(msgs, misalign=0):
+    chunks, txns, off = [], [], misalign
+    for m in msgs:
+        chunks.append(m)
+        txns.append((off, len(m), 0, 0, 1))
+        off += len(m)
+    arena = np.frombuffer(b"\0" * misalign + b"".join(chunks) + b"\0", dtype=np.uint8)
+    return arena, np.array(txns, dtype=fa.TXN_DTYPE)
+
+
+def test_sha512_cavp(engine, sha_vectors):
+    msgs = [bytes.fromhex(v["msg"]) for v in sha_vectors["short"] + sha_vectors["long"]]
+    for mis in (0, 1, 3):
+        arena, txns = _msgs_arena(msgs, mis)
+        out = engine.debug_sha512(arena, txns)
+        for i, v in enumerate(sha_vectors["short"] + sha_vectors["long"]):
+            assert out[i].tobytes().hex() == v["md"], (mis, i, len(msgs[i]))
+
+
+def test_sha512_all_lengths(engine):
+    rnd = random.Random(9)
+    msgs = [rnd.randbytes(n) for n in range(0, 1300)]
+    rnd.shuffle(msgs)                       # mixed block counts inside each wave
+    arena, txns = _msgs_arena(msgs, 2)
+    out = engine.debug_sha512(arena, txns)
+    for i, m in enumerate(msgs):
+        assert out[i].tobytes() == hashlib.sha512(m).digest(), len(m)
+
+
+def test_hram_mod_l(engine):
+    """k = SHA-512(R || A || M) mod L (fd_ed25519_user.c:205-207), all message
+    lengths around the block boundaries, unaligned offsets."""
+    rnd = random.Random(4)
+    recs, chunks, txns, off = [], [], [], 1
+    for n in list(range(0, 300)) + [1232 - 65, 1100, 1167]:
+        R, A, M = rnd.randbytes(32), rnd.randbytes(32), rnd.randbytes(n)
+        chunks += [R + rnd.randbytes(32), A, M]
+        txns.append((off + 96, n, off, off + 64, 1))
+        off += 96 + n
+        recs.append((R, A, M))
+    arena = np.frombuffer(b"\0" + b"".join(chunks), dtype=np.uint8)
+    out = engine.debug_hram(arena, np.array(txns, dtype=fa.TXN_DTYPE))
+    for i, (R, A, M) in enumerate(recs):
+        k = int.from_bytes(hashlib.sha512(R + A + M).digest(), "little") % L
+        assert int.from_bytes(out[i].tobytes(), "little") == k, i
+
+
+# ------------------------------------------------------------ point decoding
+
+def _special_encodings():
+    enc = []
+    ys = [0, 1, 2, P - 1, P - 2, P, P + 1, P + 2, P + 18, 2**255 - 1, 2**255 - 19, 2**255 - 20, 19, 20]
+    y0 = int("26e8958fc2b227b045c3f489f2ef98f0d5dfac05d3c63339b13802886d53fc05", 16)
+    for y in ys:
+        for s in (0, 1):
+            enc.append(_le(y + (s << 255)))
+    for h in ["26e8958fc2b227b045c3f489f2ef98f0d5dfac05d3c63339b13802886d53fc05",
+              "c7176a703d4dd84fba3c0b760d10670f2a2053fa2c39ccc64ec7fd7792ac037a",
+              "5866666666666666666666666666666666666666666666666666666666666666",
+              "b898e00f6f6df758b3f9a05cbf73b15fd392a008a9a417d471c178c1b28c7447"]:
+        b = bytes.fromhex(h)
+        enc += [b, b[:31] + bytes([b[31] ^ 0x80])]
+    del y0
+    return enc
+
+
+def test_decode_and_small_order(engine, oracle, vectors):
+    rnd = random.Random(8)
+    enc = _special_encodings()
+    for v in vectors["vectors"]:
+        enc += [bytes.fromhex(v["pub"]), bytes.fromhex(v["sig"])[:32]]
+    enc += [rnd.randbytes(32) for _ in range(1000)]
+    arr = np.frombuffer(b"".join(enc), dtype=np.uint8)
+    for mapping, refm in ((oracle.MAP_AVX512, False), (oracle.MAP_REF, True)):
+        rc, so, x, y = engine.debug_decode(arr, ref_mapping=refm)
+        for i, e in enumerate(enc):
+            orc_rc, orc_so, xy = oracle.point_decode(e, mapping)
+            assert rc[i] == orc_rc, (mapping, e.hex())
+            if orc_rc == 0:
+                assert so[i] == orc_so, (mapping, e.hex())
+                assert x[i].tobytes() == xy[:32] and y[i].tobytes() == xy[32:], (mapping, e.hex())
+
+
+# ------------------------------------------------------------ whole path
+
+def _vector_batch(vectors, src=None):
+    vs = [v for v in vectors["vectors"] if src is None or v["src"] == src]
+    arena, txns = workload.pack_single((bytes.fromhex(v["msg"]), bytes.fromhex(v["sig"]), bytes.fromhex(v["pub"]))
+                                       for v in vs)
+    return vs, arena, txns
+
+
+def test_golden_vectors_avx512_codes(engine, vectors):
+    vs, arena, txns = _vector_batch(vectors)
+    codes = engine.verify_txns(arena, txns)
+    bad = [(v["src"], v["tc_id"], v["code"], int(c)) for v, c in zip(vs, codes) if c != v["code"]]
+    assert not bad, bad[:20]
+    sig_codes = engine.debug_sig_codes(arena, txns)
+    assert (sig_codes == codes).all()
+
+
+def test_golden_vectors_ref_mapping(engine_ref, vectors):
+    vs, arena, txns = _vector_batch(vectors)
+    codes = engine_ref.verify_txns(arena, txns)
+    bad = [(v["src"], v["tc_id"], v["code_refmap"], int(c)) for v, c in zip(vs, codes) if c != v["code_refmap"]]
+    assert not bad, bad[:20]
+
+
+def test_cctv_batch(engine, vectors):
+    b = vectors["cctv_batch"]
+    msg, sigs, pubs = (bytes.fromhex(b[k]) for k in ("msg", "sigs", "pubs"))
+    cctv = [v for v in vectors["vectors"] if v["src"] == "cctv"]
+    chunks, txns, exp, off = [], [], [], 0
+    for case in b["cases"]:
+        v = cctv[case["cctv_index"]]
+        s = bytearray(sigs); p = bytearray(pubs)
+        s[64:128] = bytes.fromhex(v["sig"]); p[32:64] = bytes.fromhex(v["pub"])
+        for n, code in ((2, case["code2"]), (4, case["code4"])):
+            chunks += [bytes(s[:64 * n]), bytes(p[:32 * n]), msg]
+            txns.append((off + 96 * n, len(msg), off, off + 64 * n, n))
+            off += 96 * n + len(msg)
+            exp.append(code)
+    chunks += [sigs, pubs, msg]
+    txns.append((off + 96 * 16, len(msg), off, off + 64 * 16, 16)); exp.append(0)
+    arena = np.frombuffer(b"".join(chunks), dtype=np.uint8)
+    codes = engine.verify_txns(arena, np.array(txns, dtype=fa.TXN_DTYPE))
+    assert codes.tolist() == exp
+
+
+def test_txn_fixtures(engine, txn_fixtures):
+    chunks, txns, off = [], [], 0
+    for t in txn_fixtures:
+        p = bytes.fromhex(t["payload"])
+        chunks.append(p)
+        txns.append((off + t["msg_off"], len(p) - t["msg_off"], off + t["sig_off"], off + t["pub_off"], t["sig_cnt"]))
+        off += len(p)
+    arena = np.frombuffer(b"".join(chunks), dtype=np.uint8)
+    codes = engine.verify_txns(arena, np.array(txns, dtype=fa.TXN_DTYPE))
+    assert codes.tolist() == [t["code"] for t in txn_fixtures]
+    sig_codes = engine.debug_sig_codes(arena, np.array(txns, dtype=fa.TXN_DTYPE))
+    assert sig_codes.tolist() == [c for t in txn_fixtures for c in t["sig_codes"]]
+
+
+def test_quic_corpus(engine, quic_corpus):
+    arena, txns, codes = quic_corpus
+    assert (engine.verify_txns(arena, txns) == codes).all()
+
+
+def test_cfg1_random_vs_oracle(engine, oracle):
+    arena, txns, modes = workload.cfg1(3000, seed=0x1234)
+    got = engine.verify_txns(arena, txns)
+    exp = oracle.verify_txns(arena, txns, nthreads=8)
+    assert (got == exp).all(), np.nonzero(got != exp)[0][:10]
+    assert (got[modes == 0] == 0).all() and (got[modes != 0] != 0).all()
+
+
+def test_cfg3_multisig_vs_oracle(engine, oracle):
+    arena, txns, modes = workload.cfg3(1500, seed=0x4321)
+    got = engine.verify_txns(arena, txns)
+    exp = oracle.verify_txns(arena, txns, nthreads=8)
+    assert (got == exp).all(), np.nonzero(got != exp)[0][:10]
+
+
+def test_small_order_cross_product(engine, oracle):
+    """small-order encodings (and y+p variants, sign bits) as
+    A x R with S in {0, 1, L-1, L, L+1, 2^253-1, 2^256-1}."""
+    base = ["0100000000000000000000000000000000000000000000000000000000000000",
+            "ecffffffffffffffffffffffffffffffffffffffffffffffffffffffffffff7f",
+            "0000000000000000000000000000000000000000000000000000000000000000",
+            "0000000000000000000000000000000000000000000000000000000000000080",
+            "26e8958fc2b227b045c3f489f2ef98f0d5dfac05d3c63339b13802886d53fc05",
+            "26e8958fc2b227b045c3f489f2ef98f0d5dfac05d3c63339b13802886d53fc85",
+            "c7176a703d4dd84fba3c0b760d10670f2a2053fa2c39ccc64ec7fd7792ac037a",
+            "c7176a703d4dd84fba3c0b760d10670f2a2053fa2c39ccc64ec7fd7792ac03fa"]
+    encs = set()
+    for h in base:
+        b = bytes.fromhex(h)
+        y = int.from_bytes(b, "little") & (2**255 - 1)
+        for yy in (y, y + P):
+            if yy < 2**255:
+                for s in (0, 1):
+                    encs.add(_le(yy + (s << 255)))
+    prv = bytes(range(32))
+    pub_ok, sig_ok = workload.sign(prv, b"cross")
+    encs.add(pub_ok); encs.add(sig_ok[:32])
+    encs = sorted(encs)
+    Ss = [0, 1, L - 1, L, L + 1, 2**253 - 1, 2**256 - 1, int.from_bytes(sig_ok[32:], "little")]
+    recs = [(b"cross", Renc + _le(S), Aenc) for Aenc in encs for Renc in encs for S in Ss]
+    arena, txns = workload.pack_single(recs)
+    got = engine.verify_txns(arena, txns)
+    exp = oracle.verify_txns(arena, txns, nthreads=8)
+    assert len(recs) > 1000
+    assert (got == exp).all(), [recs[i] for i in np.nonzero(got != exp)[0][:3]]
+
+
+def test_batch_edges(engine, oracle):
+    """sig_cnt 0 and 17 -> ERR_SIG; empty and maximal messages; empty batch."""
+    prv = bytes(range(1, 33))
+    recs = []
+    for n in (0, 1, 127, 128, 129, 1232 - 65):
+        msg = bytes((i * 7) & 255 for i in range(n))
+        pub, sig = workload.sign(prv, msg)
+        recs.append((msg, sig, pub))
+    arena, txns = workload.pack_single(recs)
+    txns = np.concatenate([txns, txns[:2].copy(), txns[:1].copy()])
+    txns["sig_cnt"][-3] = 0
+    txns["sig_cnt"][-2] = 17
+    txns["sig_cnt"][-1] = 1
+    codes = engine.verify_txns(arena, txns)
+    assert codes.tolist() == [0] * 6 + [-1, -1, 0]
+    assert engine.verify_txns(arena, txns[:0]).tolist() == []
+
+
+def test_sync_api(vectors):
+    """fd_ed25519_verify / fd_ed25519_verify_batch_single_msg through the C ABI."""
+    vs = vectors["vectors"][:40] + vectors["vectors"][-10:]
+    for v in vs:
+        msg, sig, pub = (bytes.fromhex(v[k]) for k in ("msg", "sig", "pub"))
+        assert fa.verify(msg, sig, pub) == v["code"]
+    prv = bytes(range(32))
+    pub, sig = workload.sign(prv, b"batch")
+    assert fa.verify_batch_single_msg(b"batch", sig * 3, pub * 3, None, 3) == 0
+    assert fa.verify_batch_single_msg(b"batch", sig, pub, None, 0) == -1
+    assert fa.verify_batch_single_msg(b"batch", sig * 17, pub * 17, None, 17) == -1
+
+
+def test_async_ring(engine):
+    a1, t1, m1 = workload.cfg1(700, seed=1)
+    a2, t2, m2 = workload.cfg1(900, seed=2)
+    k1 = engine.submit(a1, t1)
+    k2 = engine.submit(a2, t2)
+    with pytest.raises(RuntimeError):
+        engine.submit(a1, t1)               # both slots hold unpolled batches
+    c2 = engine.poll(k2, blocking=True)
+    c1 = engine.poll(k1, blocking=True)
+    assert ((c1 == 0) == (m1 == 0)).all() and ((c2 == 0) == (m2 == 0)).all()
+    k3 = engine.submit(a1, t1)
+    while True:
+        c3 = engine.poll(k3, blocking=False)
+        if c3 is not None:
+            break
+    assert (c3 == c1).all()
+
+
+def test_device_resident_path(engine):
+    torch = pytest.importorskip("torch")
+    arena, txns, modes = workload.cfg1(5000, seed=77)
+    sdesc, tdesc = fa.ed25519.expand_txns(txns)
+    dev = torch.device("cuda:0")
+    d_arena = torch.zeros(arena.size + fa.ed25519.ARENA_SLACK, dtype=torch.uint8, device=dev)
+    d_arena[: arena.size] = torch.from_numpy(arena).to(dev)
+    d_s = torch.from_numpy(sdesc.view(np.uint8).copy()).to(dev)
+    d_t = torch.from_numpy(tdesc.view(np.uint8).copy()).to(dev)
+    d_sc = torch.zeros(len(sdesc), dtype=torch.int8, device=dev)
+    d_tc = torch.zeros(len(tdesc), dtype=torch.int8, device=dev)
+    stream = torch.cuda.current_stream(dev)
+    engine.verify_device(d_arena.data_ptr(), d_s.data_ptr(), len(sdesc), d_t.data_ptr(), len(tdesc),
+                         d_sc.data_ptr(), d_tc.data_ptr(), stream.cuda_stream)
+    torch.cuda.synchronize()
+    got = d_tc.cpu().numpy()
+    assert (got == engine.verify_txns(arena, txns)).all()
+    assert ((got == 0) == (modes == 0)).all()
+
+
+def test_full_size_cfg1_properties(engine, oracle):
+    """BASELINE cfg2 at full size (1M txns): every untouched transaction
+    verifies, every corrupted one fails, and a random 3000-txn sample matches
+    the oracle code for code."""
+    n = 1_000_000
+    arena, txns, modes = workload.cfg1(n)
+    codes = engine.verify_txns(arena, txns) if n <= engine._cfg.max_txn else _chunked(engine, arena, txns)
+    assert (codes[modes == 0] == 0).all()
+    assert (codes[modes != 0] != 0).all()
+    idx = np.random.default_rng(1).choice(n, 3000, replace=False)
+    exp = oracle.verify_txns(arena, txns[idx], nthreads=8)
+    assert (codes[idx] == exp).all()
+
+
+def _chunked(engine, arena, txns, chunk=1 << 17):
+    out = []
+    for i in range(0, len(txns), chunk):
+        t = txns[i:i + chunk].copy()
+        lo = int(t["sig_off"].min())
+        hi = int((t["msg_off"] + t["msg_sz"]).max())
+        for f in ("msg_off", "sig_off", "pub_off"):
+            t[f] -= lo
+        out.append(engine.verify_txns(arena[lo:hi], t))
+    return np.concatenate(out)

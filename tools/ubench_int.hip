@@ -27,7 +27,7 @@
 #define CHECK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { \
   fprintf(stderr, "HIP error %s at %s:%d\n", hipGetErrorString(e_), __FILE__, __LINE__); exit(1);} } while (0)
 
-constexpr int ITERS = 4096;
+constexpr int ITERS = 32768;
 constexpr int CHAINS = 8;
 
 template <int OP>
@@ -63,6 +63,20 @@ __global__ void __launch_bounds__(256) kbench(uint32_t* out, uint32_t seed) {
         asm volatile("v_add_u32 %0, %0, %1" : "+v"(acc32[k]) : "v"(a));
       } else if constexpr (OP == 7) {
         asm volatile("v_fma_f64 %0, %1, %2, %0" : "+v"(dacc[k]) : "v"(da), "v"(db));
+      } else if constexpr (OP == 8) {
+        asm volatile("v_lshl_add_u64 %0, %0, 0, %1" : "+v"(acc[k]) : "v"((uint64_t)a));
+      } else if constexpr (OP == 9) {
+        asm volatile("v_lshrrev_b64 %0, 3, %0" : "+v"(acc[k]));
+      } else if constexpr (OP == 10) {
+        uint32_t lo = (uint32_t)acc[k]; uint64_t cy;
+        asm volatile("v_add_co_u32 %0, %1, %0, %2" : "+v"(lo), "=s"(cy) : "v"(a));
+        acc[k] = (acc[k] & ~0xffffffffull) | lo;
+      } else if constexpr (OP == 11) {
+        asm volatile("v_alignbit_b32 %0, %0, %1, 7" : "+v"(acc32[k]) : "v"(a));
+      } else if constexpr (OP == 12) {
+        asm volatile("v_cndmask_b32 %0, %0, %1, vcc" : "+v"(acc32[k]) : "v"(a));
+      } else if constexpr (OP == 13) {
+        asm volatile("v_mov_b32 %0, %1" : "=v"(acc32[k]) : "v"(a + k));
       }
     }
   }
@@ -73,8 +87,10 @@ __global__ void __launch_bounds__(256) kbench(uint32_t* out, uint32_t seed) {
 }
 
 static const char* names[] = {"v_mad_u64_u32", "v_mul_lo_u32", "v_mul_hi_u32", "v_mad_u32_u24",
-                              "v_mul_hi_u32_u24", "v_add_co_u32+v_addc_co_u32", "v_add_u32", "v_fma_f64"};
-static const int ops_per_chain[] = {1, 1, 1, 1, 1, 2, 1, 1};
+                              "v_mul_hi_u32_u24", "v_add_co_u32+v_addc_co_u32(vcc chain)", "v_add_u32", "v_fma_f64",
+                              "v_lshl_add_u64", "v_lshrrev_b64", "v_add_co_u32(sgpr carry)", "v_alignbit_b32",
+                              "v_cndmask_b32", "v_mov_b32"};
+static const int ops_per_chain[] = {1, 1, 1, 1, 1, 2, 1, 1, 1, 1, 1, 1, 1, 1};
 
 template <int OP>
 static void run(uint32_t* d, int ncu, double clk_ghz) {
@@ -107,6 +123,8 @@ int main() {
   uint32_t* d; CHECK(hipMalloc(&d, 64));
   run<0>(d, ncu, clk); run<1>(d, ncu, clk); run<2>(d, ncu, clk); run<3>(d, ncu, clk);
   run<4>(d, ncu, clk); run<5>(d, ncu, clk); run<6>(d, ncu, clk); run<7>(d, ncu, clk);
+  run<8>(d, ncu, clk); run<9>(d, ncu, clk); run<10>(d, ncu, clk); run<11>(d, ncu, clk);
+  run<12>(d, ncu, clk); run<13>(d, ncu, clk);
   CHECK(hipFree(d));
   return 0;
 }
