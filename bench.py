@@ -1,0 +1,240 @@
+"""Benchmark: verified Ed25519 signatures/s on MI355X (BASELINE.json metric).
+
+Workload (BASELINE configs[1] = cfg2): 1M synthetic single-signature Solana
+transactions per GPU (msg ~U[180,220] B, 90% valid / 10% with one bit flipped
+in the signature, message or public key; seeded OpenSSL-signed, see
+firedancer_amd/workload.py), staged in HBM before the timed region.  A step
+is one full pass of the hot path over the batch: the signature kernel
+(SHA-512, mod L, decode, small-order, [S]B - [k]A, compare) plus the per-txn
+combine kernel, codes left in HBM.
+
+Multi-GPU: one process per GPU (torch.distributed.run), each rank verifies its
+own independent 1M batch (weak scaling, no data-path collective); CPU-side gloo
+only for the barrier and the max-over-ranks time.
+
+Extras on the JSON line: roofline (INT32 VALU, v_mad_u64_u32 issue peak),
+cpu_baseline (the oracle, a C restatement, on this host's cores, N=1 only),
+p50/p99 batch latency of 65,536-txn batches through the async PCIe path, and
+the PCIe-inclusive pipelined throughput.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+# Algorithmic INT32 multiply-accumulates per signature:
+# 3,300 field multiplications x 64 u32*u32 products (radix-2^32 schoolbook).
+MADS_PER_SIG = 211_200
+# v_mad_u64_u32 issue peak of one MI355X: 256 CU x 4 SIMD x 16 lanes/clk (half
+# rate, measured in tools/ubench_int.hip: profiles/r01_ubench.md) x 2.4 GHz.
+VALU_MAD_PEAK_TOPS = 256 * 64 * 2.4e9 / 1e12
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--txns", type=int, default=1_000_000, help="transactions per GPU")
+    ap.add_argument("--latency-batches", type=int, default=200)
+    ap.add_argument("--latency-batch", type=int, default=65536)
+    ap.add_argument("--cpu-sample", type=int, default=200_000, help="txns timed on the CPU oracle")
+    ap.add_argument("--no-extras", action="store_true", help="only the timed device-resident loop (profiling)")
+    return ap.parse_args()
+
+
+class Dist:
+    """Barrier + max-reduce across ranks (gloo over 127.0.0.1); no GPU collectives."""
+
+    def __init__(self):
+        self.world = int(os.environ.get("WORLD_SIZE", "1"))
+        self.rank = int(os.environ.get("RANK", "0"))
+        self.local_rank = int(os.environ.get("LOCAL_RANK", str(self.rank)))
+        self.dist = None
+        if self.world > 1:
+            import torch.distributed as dist
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            dist.init_process_group("gloo", rank=self.rank, world_size=self.world)
+            self.dist = dist
+
+    def barrier(self):
+        if self.dist:
+            self.dist.barrier()
+
+    def max(self, x):
+        if not self.dist:
+            return x
+        import torch
+        t = torch.tensor([float(x)], dtype=torch.float64)
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
+        return float(t.item())
+
+    def sum(self, x):
+        if not self.dist:
+            return x
+        import torch
+        t = torch.tensor([float(x)], dtype=torch.float64)
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.SUM)
+        return float(t.item())
+
+    def close(self):
+        if self.dist:
+            self.dist.destroy_process_group()
+
+
+def latency_and_pcie(eng, arena, txns, batch, nbatches):
+    """p50/p99 submit->codes-on-host latency of `batch`-txn batches (ring depth
+    2, one in flight at a time for latency), then pipelined throughput with
+    both ring slots busy (PCIe-inclusive)."""
+    n = len(txns)
+    starts = list(range(0, n - batch + 1, batch)) or [0]
+    views = []
+    for s in starts:
+        t = txns[s:s + batch].copy()
+        lo = int(t["sig_off"].min())
+        hi = int((t["msg_off"] + t["msg_sz"]).max())
+        for f in ("msg_off", "sig_off", "pub_off"):
+            t[f] -= lo
+        views.append((np.ascontiguousarray(arena[lo:hi]), t))
+    for i in range(min(10, nbatches)):                     # warm-up
+        a, t = views[i % len(views)]
+        eng.verify_txns(a, t)
+    lat = []
+    for i in range(nbatches):
+        a, t = views[i % len(views)]
+        t0 = time.perf_counter()
+        tk = eng.submit(a, t)
+        eng.poll(tk, blocking=True)
+        lat.append((time.perf_counter() - t0) * 1e3)
+    # pipelined: keep both slots busy
+    sigs = 0
+    t0 = time.perf_counter()
+    inflight = []
+    for i in range(len(views) * 2):
+        a, t = views[i % len(views)]
+        if len(inflight) == 2:
+            eng.poll(inflight.pop(0), blocking=True)
+        inflight.append(eng.submit(a, t))
+        sigs += int(t["sig_cnt"].sum())
+    for tk in inflight:
+        eng.poll(tk, blocking=True)
+    pcie = sigs / (time.perf_counter() - t0)
+    lat = np.array(lat)
+    return float(np.percentile(lat, 50)), float(np.percentile(lat, 99)), pcie
+
+
+def cpu_baseline(arena, txns, sample):
+    from oracle import oracle as orc
+    from firedancer_amd.workload import default_threads
+    cores = default_threads()
+    sub = txns[:sample]
+    t0 = time.perf_counter()
+    codes = orc.verify_txns(arena, sub, nthreads=cores)
+    dt = time.perf_counter() - t0
+    return {"value": round(int(sub["sig_cnt"].sum()) / dt, 1), "unit": "sigs/s", "cores": cores, "kind": "port",
+            "sample": f"first {len(sub)} txns of the rank-0 cfg1 batch, oracle/fd_ed25519_oracle.c "
+                      f"(C restatement, radix-2^51, wNAF) with {cores} threads, {dt:.2f} s wall",
+            "published_ref_per_core": "20-40K sigs/s/core (Icelake, book/guide/tuning.md:75) -- published, not measured",
+            "cpu_codes_nonzero": int((codes != 0).sum())}
+
+
+def pmc_traffic():
+    """HBM bytes per verify-kernel launch from the committed PMC summary
+    (profiles/*_pmc.json written by tools/pmc_summary.py), if present."""
+    import glob
+    files = sorted(glob.glob(os.path.join(REPO, "profiles", "*_pmc.json")))
+    if not files:
+        return None, None
+    d = json.load(open(files[-1]))
+    return d.get("hbm_bytes_per_launch"), os.path.basename(files[-1])
+
+
+def main():
+    args = parse()
+    dist = Dist()
+    from firedancer_amd import VerifyEngine, workload
+
+    t_gen = time.perf_counter()
+    arena, txns, modes = workload.cfg1(args.txns, seed=workload.CFG1_SEED + dist.rank)
+    t_gen = time.perf_counter() - t_gen
+    eng = VerifyEngine(dist.local_rank, max_txn=args.latency_batch, max_sig=2 * args.latency_batch,
+                       max_arena=args.latency_batch * 320)
+    batch = eng.upload(arena, txns)
+    n_sig = batch.n_sig
+
+    for _ in range(args.warmup):
+        batch.verify()
+    eng.sync()
+    codes = batch.codes()
+    self_check = bool(((codes == 0) == (modes == 0)).all())
+
+    dist.barrier()
+    eng.sync()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        batch.verify()
+    eng.sync()
+    dt = time.perf_counter() - t0
+    dist.barrier()
+    dt_max = dist.max(dt)
+    total_sigs = dist.sum(n_sig * args.steps)
+    value = total_sigs / dt_max
+
+    # live HIP-event timing of the dominant kernel (same stream, same batch)
+    wall_ms, kv_ms, kc_ms = batch.time(max(3, min(args.steps, 10)))
+    achieved = n_sig * MADS_PER_SIG / (kv_ms * 1e-3) / 1e12
+    traffic, traffic_src = pmc_traffic()
+
+    extras = {}
+    if not args.no_extras:
+        p50, p99, pcie = latency_and_pcie(eng, arena, txns, args.latency_batch, args.latency_batches)
+        extras = {"p50_batch_latency_ms": round(p50, 3), "p99_batch_latency_ms": round(p99, 3),
+                  "latency_batch_txns": args.latency_batch,
+                  "pcie_inclusive_sigs_per_s_per_gpu": round(pcie, 1)}
+    cpu = None
+    if dist.rank == 0 and dist.world == 1 and not args.no_extras:
+        cpu = cpu_baseline(arena, txns, min(args.cpu_sample, len(txns)))
+    batch.free()
+    eng.close()
+    self_ok = dist.sum(1 if self_check else 0) == dist.world
+
+    if dist.rank == 0:
+        line = {
+            "metric": "verified ed25519 sigs/sec (node)",
+            "value": round(value, 1),
+            "unit": "sigs/s",
+            "n_gpus": dist.world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(dt_max / args.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u32",
+            "data": "synthetic (seeded OpenSSL-signed Solana legacy txns, 10% one-bit corrupted)",
+            "config": {"workload": f"cfg2: {args.txns} single-sig txns/GPU, msg U[180,220] B, 90% valid / 10% "
+                                   "corrupted, device-resident batch, full verify + per-txn combine per step",
+                       "sigs_per_gpu_per_step": n_sig, "parallelism": f"dp{dist.world} (independent per-GPU batches)"},
+            "roofline": {"bound": "valu", "achieved": round(achieved, 3), "peak": round(VALU_MAD_PEAK_TOPS, 2),
+                         "unit": "TOP/s", "frac": round(achieved / VALU_MAD_PEAK_TOPS, 4),
+                         "traffic": traffic,
+                         "note": f"INT32 v_mad_u64_u32 ops: {MADS_PER_SIG} algorithmic mads/sig x {n_sig} sigs / mean "
+                                 f"signature-kernel time {kv_ms:.3f} ms (HIP events, compute stream); combine kernel "
+                                 f"{kc_ms:.4f} ms; traffic source {traffic_src}"},
+            "cpu_baseline": cpu,
+            "self_check_codes": self_ok,
+            "gen_s": round(t_gen, 2),
+        }
+        line.update(extras)
+        print(json.dumps(line), flush=True)
+    dist.close()
+
+
+if __name__ == "__main__":
+    main()

@@ -65,6 +65,21 @@ def lib():
     L.fdgpu_debug_hram.argtypes = [vp, vp, c.c_uint64, vp, c.c_uint64, vp]
     L.fdgpu_debug_sc_reduce.argtypes = [vp, vp, c.c_uint64, vp]
     L.fdgpu_debug_sig_codes.argtypes = [vp, vp, c.c_uint64, vp, c.c_uint64, vp]
+    L.fdgpu_dev_batch_upload.argtypes = [vp, vp, c.c_uint64, vp, c.c_uint64]
+    L.fdgpu_dev_batch_upload.restype = vp
+    L.fdgpu_dev_batch_verify.argtypes = [vp, vp]
+    L.fdgpu_dev_batch_verify.restype = c.c_int
+    L.fdgpu_dev_batch_codes.argtypes = [vp, vp, vp, vp]
+    L.fdgpu_dev_batch_codes.restype = c.c_int
+    L.fdgpu_dev_batch_free.argtypes = [vp, vp]
+    L.fdgpu_dev_batch_free.restype = None
+    L.fdgpu_dev_batch_sig_cnt.argtypes = [vp]
+    L.fdgpu_dev_batch_sig_cnt.restype = c.c_uint64
+    L.fdgpu_dev_batch_time.argtypes = [vp, vp, c.c_int, c.POINTER(c.c_double), c.POINTER(c.c_double),
+                                       c.POINTER(c.c_double)]
+    L.fdgpu_dev_batch_time.restype = c.c_int
+    L.fdgpu_sync.argtypes = [vp]
+    L.fdgpu_sync.restype = c.c_int
     for fn in ("fdgpu_debug_fe_ops", "fdgpu_debug_decode", "fdgpu_debug_sha512", "fdgpu_debug_hram",
                "fdgpu_debug_sc_reduce", "fdgpu_debug_sig_codes"):
         getattr(L, fn).restype = c.c_int

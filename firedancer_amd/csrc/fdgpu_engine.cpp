@@ -293,6 +293,123 @@ int fdgpu_verify_device(fdgpu_engine_t *e, void const *d_arena, void const *d_si
                         (const fdgpu_txn_desc_t *)d_txn_desc, txn_cnt, d_sig_codes, d_txn_codes, st);
 }
 
+/* ----------------------------------------------- device-resident batches */
+
+}  // extern "C"
+
+struct fdgpu_dev_batch {
+  uint8_t *d_arena = nullptr;
+  fdgpu_sig_desc_t *d_sigs = nullptr;
+  fdgpu_txn_desc_t *d_txns = nullptr;
+  int8_t *d_sig_codes = nullptr, *d_txn_codes = nullptr;
+  uint64_t n_sig = 0, n_txn = 0;
+};
+
+extern "C" {
+
+uint64_t fdgpu_dev_batch_sig_cnt(fdgpu_dev_batch_t const *b) { return b ? b->n_sig : 0; }
+
+void fdgpu_dev_batch_free(fdgpu_engine_t *e, fdgpu_dev_batch_t *b) {
+  if (!b) return;
+  if (e) { (void)hipSetDevice(e->device); (void)hipStreamSynchronize(e->compute); }
+  if (b->d_arena) (void)hipFree(b->d_arena);
+  if (b->d_sigs) (void)hipFree(b->d_sigs);
+  if (b->d_txns) (void)hipFree(b->d_txns);
+  if (b->d_sig_codes) (void)hipFree(b->d_sig_codes);
+  if (b->d_txn_codes) (void)hipFree(b->d_txn_codes);
+  delete b;
+}
+
+fdgpu_dev_batch_t *fdgpu_dev_batch_upload(fdgpu_engine_t *e, uint8_t const *arena, uint64_t arena_sz,
+                                          fdgpu_txn_t const *txns, uint64_t txn_cnt) {
+  if (!e || (!arena && arena_sz) || (!txns && txn_cnt)) { set_err("null argument"); return nullptr; }
+  if (arena_sz > 0xFFFFFFF0ull || txn_cnt > 0xFFFFFFF0ull) { set_err("batch exceeds 32-bit offsets"); return nullptr; }
+  HIPCHK(hipSetDevice(e->device), nullptr);
+  uint64_t total = 0;
+  for (uint64_t t = 0; t < txn_cnt; t++) total += (txns[t].sig_cnt >= 1 && txns[t].sig_cnt <= 16) ? txns[t].sig_cnt : 0;
+  std::vector<fdgpu_sig_desc_t> sd(total + 1);
+  std::vector<fdgpu_txn_desc_t> td(txn_cnt + 1);
+  const int64_t ns = expand(arena, arena_sz, txns, txn_cnt, total, sd.data(), td.data());
+  if (ns < 0) return nullptr;
+  fdgpu_dev_batch *b = new fdgpu_dev_batch();
+  b->n_sig = (uint64_t)ns; b->n_txn = txn_cnt;
+  auto fail = [&](const char *what) -> fdgpu_dev_batch_t * { set_err("%s", what); fdgpu_dev_batch_free(e, b); return nullptr; };
+  if (hipMalloc((void **)&b->d_arena, arena_sz + FDGPU_ARENA_SLACK) != hipSuccess) return fail("arena alloc");
+  if (hipMalloc((void **)&b->d_sigs, (ns + 1) * sizeof(fdgpu_sig_desc_t)) != hipSuccess) return fail("sig alloc");
+  if (hipMalloc((void **)&b->d_txns, (txn_cnt + 1) * sizeof(fdgpu_txn_desc_t)) != hipSuccess) return fail("txn alloc");
+  if (hipMalloc((void **)&b->d_sig_codes, ns + 16) != hipSuccess) return fail("code alloc");
+  if (hipMalloc((void **)&b->d_txn_codes, txn_cnt + 16) != hipSuccess) return fail("code alloc");
+  if (hipMemset(b->d_arena, 0, arena_sz + FDGPU_ARENA_SLACK) != hipSuccess) return fail("memset");
+  if (arena_sz && hipMemcpy(b->d_arena, arena, arena_sz, hipMemcpyHostToDevice) != hipSuccess) return fail("h2d");
+  if (ns && hipMemcpy(b->d_sigs, sd.data(), ns * sizeof(fdgpu_sig_desc_t), hipMemcpyHostToDevice) != hipSuccess) return fail("h2d");
+  if (txn_cnt && hipMemcpy(b->d_txns, td.data(), txn_cnt * sizeof(fdgpu_txn_desc_t), hipMemcpyHostToDevice) != hipSuccess) return fail("h2d");
+  if ((uint64_t)ns > e->ws_sig) {
+    if (hipStreamSynchronize(e->compute) != hipSuccess) return fail("sync");
+    if (ensure_ws(e, (uint64_t)ns) != FDGPU_OK) { fdgpu_dev_batch_free(e, b); return nullptr; }
+  }
+  return b;
+}
+
+int fdgpu_dev_batch_verify(fdgpu_engine_t *e, fdgpu_dev_batch_t *b) {
+  if (!e || !b) return FDGPU_ERR_INVAL;
+  HIPCHK(hipSetDevice(e->device), FDGPU_ERR_DEVICE);
+  return enqueue_verify(e, b->d_arena, b->d_sigs, b->n_sig, b->d_txns, b->n_txn, b->d_sig_codes, b->d_txn_codes,
+                        e->compute);
+}
+
+int fdgpu_dev_batch_codes(fdgpu_engine_t *e, fdgpu_dev_batch_t *b, int8_t *txn_codes, int8_t *sig_codes) {
+  if (!e || !b) return FDGPU_ERR_INVAL;
+  HIPCHK(hipSetDevice(e->device), FDGPU_ERR_DEVICE);
+  HIPCHK(hipStreamSynchronize(e->compute), FDGPU_ERR_DEVICE);
+  if (txn_codes && b->n_txn) HIPCHK(hipMemcpy(txn_codes, b->d_txn_codes, b->n_txn, hipMemcpyDeviceToHost), FDGPU_ERR_DEVICE);
+  if (sig_codes && b->n_sig) HIPCHK(hipMemcpy(sig_codes, b->d_sig_codes, b->n_sig, hipMemcpyDeviceToHost), FDGPU_ERR_DEVICE);
+  return FDGPU_OK;
+}
+
+int fdgpu_dev_batch_time(fdgpu_engine_t *e, fdgpu_dev_batch_t *b, int iters, double *wall_ms, double *verify_kernel_ms,
+                         double *combine_kernel_ms) {
+  if (!e || !b || iters < 1) return FDGPU_ERR_INVAL;
+  HIPCHK(hipSetDevice(e->device), FDGPU_ERR_DEVICE);
+  const uint32_t flags = (e->cfg.flags & FDGPU_FLAG_REF_MAPPING) ? FDGPU_FLAG_REF_MAP : 0u;
+  std::vector<hipEvent_t> ev(3 * (size_t)iters + 1);
+  for (auto &x : ev) HIPCHK(hipEventCreate(&x), FDGPU_ERR_DEVICE);
+  int rc = FDGPU_OK;
+  for (int i = 0; i < iters && rc == FDGPU_OK; i++) {
+    if (hipEventRecord(ev[3 * i], e->compute) != hipSuccess) rc = FDGPU_ERR_DEVICE;
+    if (fdgpu_launch_verify_sigs(b->d_arena, b->d_sigs, (uint32_t)b->n_sig, e->d_btab, e->d_ws, b->d_sig_codes, flags,
+                                 e->compute) != hipSuccess) rc = FDGPU_ERR_DEVICE;
+    if (hipEventRecord(ev[3 * i + 1], e->compute) != hipSuccess) rc = FDGPU_ERR_DEVICE;
+    if (fdgpu_launch_combine(b->d_txns, (uint32_t)b->n_txn, b->d_sig_codes, b->d_txn_codes, e->compute) != hipSuccess)
+      rc = FDGPU_ERR_DEVICE;
+    if (hipEventRecord(ev[3 * i + 2], e->compute) != hipSuccess) rc = FDGPU_ERR_DEVICE;
+  }
+  if (rc == FDGPU_OK && hipEventSynchronize(ev[3 * (iters - 1) + 2]) != hipSuccess) rc = FDGPU_ERR_DEVICE;
+  double sv = 0, sc = 0;
+  float ms = 0;
+  for (int i = 0; rc == FDGPU_OK && i < iters; i++) {
+    (void)hipEventElapsedTime(&ms, ev[3 * i], ev[3 * i + 1]); sv += ms;
+    (void)hipEventElapsedTime(&ms, ev[3 * i + 1], ev[3 * i + 2]); sc += ms;
+  }
+  if (rc == FDGPU_OK) {
+    (void)hipEventElapsedTime(&ms, ev[0], ev[3 * (iters - 1) + 2]);
+    if (wall_ms) *wall_ms = ms;
+    if (verify_kernel_ms) *verify_kernel_ms = sv / iters;
+    if (combine_kernel_ms) *combine_kernel_ms = sc / iters;
+  } else {
+    set_err("timing launch failed");
+  }
+  for (auto &x : ev) (void)hipEventDestroy(x);
+  return rc;
+}
+
+int fdgpu_sync(fdgpu_engine_t *e) {
+  if (!e) return FDGPU_ERR_INVAL;
+  HIPCHK(hipSetDevice(e->device), FDGPU_ERR_DEVICE);
+  HIPCHK(hipStreamSynchronize(e->compute), FDGPU_ERR_DEVICE);
+  for (auto &s : e->slots) HIPCHK(hipStreamSynchronize(s.stream), FDGPU_ERR_DEVICE);
+  return FDGPU_OK;
+}
+
 /* ------------------------------------------------------------ sync API */
 
 static std::mutex g_sync_mu;

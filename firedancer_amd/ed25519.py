@@ -150,6 +150,13 @@ class VerifyEngine:
         if rc != 0:
             raise RuntimeError(f"fdgpu_verify_device failed ({rc}): {_lib.last_error()}")
 
+    def upload(self, arena, txns):
+        """Stage a batch in HBM once (DeviceBatch); verify it any number of times."""
+        return DeviceBatch(self, arena, txns)
+
+    def sync(self):
+        self._chk(_lib.lib().fdgpu_sync(self._h), "fdgpu_sync")
+
     # ---- per-stage diagnostics (parity tests) ----
     def _chk(self, rc, what):
         if rc != 0:
@@ -201,3 +208,54 @@ class VerifyEngine:
         self._chk(_lib.lib().fdgpu_debug_sig_codes(self._h, arena.ctypes.data, arena.size, txns.ctypes.data,
                                                    len(txns), out.ctypes.data), "debug_sig_codes")
         return out[:n]
+
+
+class DeviceBatch:
+    """A batch resident in HBM (fdgpu_dev_batch_t)."""
+
+    def __init__(self, engine, arena, txns):
+        arena = np.ascontiguousarray(arena, dtype=np.uint8)
+        txns = np.ascontiguousarray(txns, dtype=TXN_DTYPE)
+        self._e = engine
+        self.n_txn = len(txns)
+        self._b = _lib.lib().fdgpu_dev_batch_upload(engine._h, arena.ctypes.data, arena.size, txns.ctypes.data,
+                                                    len(txns))
+        if not self._b:
+            raise RuntimeError(f"fdgpu_dev_batch_upload failed: {_lib.last_error()}")
+        self.n_sig = int(_lib.lib().fdgpu_dev_batch_sig_cnt(self._b))
+
+    def verify(self):
+        """Enqueue one verify (async on the engine's compute stream)."""
+        rc = _lib.lib().fdgpu_dev_batch_verify(self._e._h, self._b)
+        if rc != 0:
+            raise RuntimeError(f"fdgpu_dev_batch_verify failed ({rc}): {_lib.last_error()}")
+
+    def codes(self, sig_codes=False):
+        t = np.zeros(max(self.n_txn, 1), dtype=np.int8)
+        s = np.zeros(max(self.n_sig, 1), dtype=np.int8) if sig_codes else None
+        rc = _lib.lib().fdgpu_dev_batch_codes(self._e._h, self._b, t.ctypes.data,
+                                              s.ctypes.data if s is not None else None)
+        if rc != 0:
+            raise RuntimeError(f"fdgpu_dev_batch_codes failed ({rc}): {_lib.last_error()}")
+        return (t[:self.n_txn], s[:self.n_sig]) if sig_codes else t[:self.n_txn]
+
+    def time(self, iters):
+        """HIP-event timing of `iters` back-to-back verifies: (wall_ms,
+        mean verify-kernel ms, mean combine-kernel ms)."""
+        import ctypes as c
+        w, v, k = c.c_double(), c.c_double(), c.c_double()
+        rc = _lib.lib().fdgpu_dev_batch_time(self._e._h, self._b, int(iters), c.byref(w), c.byref(v), c.byref(k))
+        if rc != 0:
+            raise RuntimeError(f"fdgpu_dev_batch_time failed ({rc}): {_lib.last_error()}")
+        return w.value, v.value, k.value
+
+    def free(self):
+        if self._b:
+            _lib.lib().fdgpu_dev_batch_free(self._e._h, self._b)
+            self._b = None
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass

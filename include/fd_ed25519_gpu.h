@@ -134,7 +134,32 @@ int fdgpu_verify_device( fdgpu_engine_t * e,
                          int8_t *         d_txn_codes,
                          void *           hip_stream );
 
-/* Engine facts for reporting: persistent grid size and resident lanes. */
+/* Device-resident batches owned by the engine: upload once (host arena +
+   txn descriptors -> HBM, with the per-signature expansion done on the
+   host), then verify any number of times with the inputs already in HBM.
+   This is the path a GPU-side ingest (or a benchmark) uses; codes stay in
+   HBM until fdgpu_dev_batch_codes copies them out. */
+typedef struct fdgpu_dev_batch fdgpu_dev_batch_t;
+
+fdgpu_dev_batch_t * fdgpu_dev_batch_upload( fdgpu_engine_t * e, uint8_t const * arena, uint64_t arena_sz,
+                                            fdgpu_txn_t const * txns, uint64_t txn_cnt );
+/* enqueue one verify of the batch on the engine's compute stream (async) */
+int  fdgpu_dev_batch_verify( fdgpu_engine_t * e, fdgpu_dev_batch_t * b );
+/* wait for the compute stream and copy the per-txn (and optionally per-signature) codes out */
+int  fdgpu_dev_batch_codes( fdgpu_engine_t * e, fdgpu_dev_batch_t * b, int8_t * txn_codes, int8_t * sig_codes );
+void fdgpu_dev_batch_free( fdgpu_engine_t * e, fdgpu_dev_batch_t * b );
+uint64_t fdgpu_dev_batch_sig_cnt( fdgpu_dev_batch_t const * b );
+/* Times `iters` back-to-back verifies of the batch on the compute stream
+   with HIP events: *wall_ms = first-to-last event span (all launches),
+   *verify_kernel_ms = mean duration of the signature kernel alone,
+   *combine_kernel_ms = mean duration of the per-txn combine kernel. */
+int  fdgpu_dev_batch_time( fdgpu_engine_t * e, fdgpu_dev_batch_t * b, int iters, double * wall_ms,
+                           double * verify_kernel_ms, double * combine_kernel_ms );
+/* Blocks until all work enqueued on the engine's streams has finished. */
+int  fdgpu_sync( fdgpu_engine_t * e );
+
+/* Engine facts for reporting: resident workgroups (occupancy x CUs),
+   threads per workgroup, workspace bytes. */
 int fdgpu_engine_info( fdgpu_engine_t * e, uint32_t * grid_blocks, uint32_t * block_threads,
                        uint64_t * ws_bytes );
 
