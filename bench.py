@@ -44,7 +44,7 @@ def parse():
     ap.add_argument("--txns", type=int, default=1_000_000, help="transactions per GPU")
     ap.add_argument("--latency-batches", type=int, default=200)
     ap.add_argument("--latency-batch", type=int, default=65536)
-    ap.add_argument("--cpu-sample", type=int, default=200_000, help="txns timed on the CPU oracle")
+    ap.add_argument("--cpu-sample", type=int, default=1_000_000, help="txns timed on the CPU oracle (bounded sample)")
     ap.add_argument("--no-extras", action="store_true", help="only the timed device-resident loop (profiling)")
     return ap.parse_args()
 
@@ -164,7 +164,7 @@ def main():
     arena, txns, modes = workload.cfg1(args.txns, seed=workload.CFG1_SEED + dist.rank)
     t_gen = time.perf_counter() - t_gen
     eng = VerifyEngine(dist.local_rank, max_txn=args.latency_batch, max_sig=2 * args.latency_batch,
-                       max_arena=args.latency_batch * 320)
+                       max_arena=args.latency_batch * 1232)
     batch = eng.upload(arena, txns)
     n_sig = batch.n_sig
 
