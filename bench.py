@@ -88,6 +88,19 @@ class Dist:
             self.dist.destroy_process_group()
 
 
+def rank_seed(rank):
+    """Each rank verifies its own independent cfg1 shard (weak scaling)."""
+    from firedancer_amd import workload
+    return workload.CFG1_SEED + rank
+
+
+def aggregate(dist, n_sig, steps, dt):
+    """Whole-job throughput: sigs of all ranks / the slowest rank's time."""
+    dt_max = dist.max(dt)
+    total = dist.sum(n_sig * steps)
+    return total / dt_max, dt_max
+
+
 def latency_and_pcie(eng, arena, txns, batch, nbatches):
     """p50/p99 submit->codes-on-host latency of `batch`-txn batches (ring depth
     2, one in flight at a time for latency), then pipelined throughput with
@@ -161,7 +174,7 @@ def main():
     from firedancer_amd import VerifyEngine, workload
 
     t_gen = time.perf_counter()
-    arena, txns, modes = workload.cfg1(args.txns, seed=workload.CFG1_SEED + dist.rank)
+    arena, txns, modes = workload.cfg1(args.txns, seed=rank_seed(dist.rank))
     t_gen = time.perf_counter() - t_gen
     eng = VerifyEngine(dist.local_rank, max_txn=args.latency_batch, max_sig=2 * args.latency_batch,
                        max_arena=args.latency_batch * 1232)
@@ -182,9 +195,7 @@ def main():
     eng.sync()
     dt = time.perf_counter() - t0
     dist.barrier()
-    dt_max = dist.max(dt)
-    total_sigs = dist.sum(n_sig * args.steps)
-    value = total_sigs / dt_max
+    value, dt_max = aggregate(dist, n_sig, args.steps, dt)
 
     # live HIP-event timing of the dominant kernel (same stream, same batch)
     wall_ms, kv_ms, kc_ms = batch.time(max(3, min(args.steps, 10)))
