@@ -8,7 +8,8 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libfd_ed25519_gpu.so")
+# FDGPU_LIB overrides the library path (A/B builds of kernel variants in one tree).
+LIB_PATH = os.environ.get("FDGPU_LIB") or os.path.join(_HERE, "libfd_ed25519_gpu.so")
 HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "fd_ed25519_gpu.h")
 
 _LIB = None

@@ -26,6 +26,13 @@
 
 using namespace fdgpu;
 
+#ifndef FDGPU_PREP_WAVES
+#define FDGPU_PREP_WAVES 2     /* decode/pow chains want ~200 VGPRs */
+#endif
+#ifndef FDGPU_DSM_WAVES
+#define FDGPU_DSM_WAVES 3     /* ~130 VGPRs: 3 waves per SIMD, no spills */
+#endif
+
 namespace {
 
 FDG_DEV void load32(uint32_t (&w)[8], const uint8_t *p) {
@@ -151,35 +158,50 @@ FDG_DEV void atab_build(uint32_t *wsl, const ge_p3 &An) {
   }
 }
 
-/* Full verify of one signature.  Returns the reference's code for the
-   single-signature verify (0 / -1 / -2 / -3).  Phases are ordered so that
-   only the bytes/scalars still needed stay live in VGPRs. */
-FDG_DEV int verify_one(const uint8_t *arena, const fdgpu_sig_desc_t &sd_in, uint32_t nblk_wave,
-                       uint32_t *wsl, const uint32_t *s_btab, bool ref_map) {
+/* Workspace entry 9 ("park") words: 0-9 x_R, 10-19 y_R, 20-27 radix-16
+   digits of k, 28-35 radix-256 digits of S, 36 pass-1 code. */
+#define PARK_XR 0
+#define PARK_YR 10
+#define PARK_KD 20
+#define PARK_SD 28
+#define PARK_CODE 36
+
+FDG_DEV uint32_t *park_ptr(uint32_t *wsl) { return wsl + 9u * (FDGPU_ATAB_WORDS * 64u); }
+
+/* Pass 1 of one signature (fd_ed25519_user.c:158-207; SURVEY Appendix A steps
+   1-5): S < L, k = SHA-512(R||A||M) mod L, decode A then R, small-order
+   tests.  Writes the table {O, -A, .., -8A}, the affine R, both digit
+   strings and the pass-1 code to this lane's workspace; returns the code. */
+FDG_DEV int verify_pass1(const uint8_t *arena, const fdgpu_sig_desc_t &sd_in, uint32_t nblk_wave, uint32_t *wsl,
+                         bool ref_map) {
   uint32_t R[8], A[8];
   load32(R, arena + sd_in.sig_off);
   load32(A, arena + sd_in.pub_off);
+  uint32_t *park = park_ptr(wsl);
 
-  /* step 5 first (pure function of the bytes): k = SHA-512(R || A || M) mod L */
-  uint32_t k[8];
+  /* k = SHA-512(R || A || M) mod L, recoded to signed radix 16 */
   {
     uint64_t h[8];
     sha512_hram(h, R, A, arena + sd_in.msg_off, sd_in.msg_sz, nblk_wave);
-    uint32_t kx[16];
+    uint32_t kx[16], k[8], kd[8];
 #pragma unroll
     for (int i = 0; i < 8; i++) { kx[2 * i] = bswap32((uint32_t)(h[i] >> 32)); kx[2 * i + 1] = bswap32((uint32_t)h[i]); }
     sc_reduce512(k, kx);
+    sc_recode16(kd, k);
+#pragma unroll
+    for (int i = 0; i < 8; i++) park[(PARK_KD + i) * 64] = kd[i];
   }
-
-  /* step 1: S < L (fd_ed25519_user.c:159-161) */
+  /* step 1: S < L (fd_ed25519_user.c:159-161); S recoded to signed radix 256 */
   int code;
   {
-    uint32_t S[8];
+    uint32_t S[8], sd[8];
     load32(S, arena + sd_in.sig_off + 32);
     code = sc_lt_L(S) ? 0 : -1;
+    sc_recode256(sd, S);
+#pragma unroll
+    for (int i = 0; i < 8; i++) park[(PARK_SD + i) * 64] = sd[i];
   }
-
-  /* step 2 (A): decode, small order, then table of -A */
+  /* step 2 (A): decode, small order, table of -A */
   bool a_ok, a_small;
   {
     ge_p3 Ap;
@@ -188,66 +210,74 @@ FDG_DEV int verify_one(const uint8_t *arena, const fdgpu_sig_desc_t &sd_in, uint
     ge_p3 An; ge_p3_neg(An, Ap);
     atab_build(wsl, An);
   }
-  /* step 2 (R): decode, small order; keep affine x_R, y_R */
+  /* step 2 (R): decode, small order; park affine x_R, y_R */
   bool r_ok, r_small;
   {
     ge_p3 Rp;
     r_ok = ge_decode(Rp, R, ref_map);
     r_small = ge_is_small_order_affine(Rp);
-    ge_cached park; park.YpX = Rp.X; park.YmX = Rp.Y; fe_0(park.Z2); fe_0(park.T2d);
-    atab_store(wsl, 9, park);      /* x_R, y_R parked in the workspace */
+#pragma unroll
+    for (int i = 0; i < 10; i++) { park[(PARK_XR + i) * 64] = Rp.X.v[i]; park[(PARK_YR + i) * 64] = Rp.Y.v[i]; }
   }
   if (code == 0 && !a_ok) code = ref_map ? -2 : -1;    /* decode2 reports A before R */
   if (code == 0 && !r_ok) code = -1;
   if (code == 0 && a_small) code = -2;                 /* fd_ed25519_user.c:194-199 */
   if (code == 0 && r_small) code = -1;
-
-  /* wave-uniform early out when every lane already failed */
-  if (__all(code != 0)) return code;
-
-  /* step 6: [S]B + [k](-A) == R, cofactorless, projective compare */
-  uint32_t kd[8], sdg[8];
-  sc_recode16(kd, k);
-  {
-    uint32_t S[8];
-    load32(S, arena + sd_in.sig_off + 32);
-    sc_recode256(sdg, S);
-  }
-  ge_p2 Rc;
-  dsm(Rc, kd, sdg, wsl, s_btab);
-  fe l, xy;
-  const uint32_t *park = wsl + 9u * (FDGPU_ATAB_WORDS * 64u);
-#pragma unroll
-  for (int i = 0; i < 10; i++) xy.v[i] = park[i * 64];
-  fe_mul(l, xy, Rc.Z);
-  bool eq = fe_eq(Rc.X, l);
-#pragma unroll
-  for (int i = 0; i < 10; i++) xy.v[i] = park[(10 + i) * 64];
-  fe_mul(l, xy, Rc.Z);
-  eq = eq && fe_eq(Rc.Y, l);
-  if (code == 0 && !eq) code = -3;
+  park[PARK_CODE * 64] = (uint32_t)code;
   return code;
 }
 
-__global__ void __launch_bounds__(FDGPU_BLOCK, 2)
-fdgpu_verify_sigs_kernel(const uint8_t *__restrict__ arena, const fdgpu_sig_desc_t *__restrict__ sigs,
-                         uint32_t n_sig, const uint32_t *__restrict__ btab, uint32_t *__restrict__ ws,
-                         int8_t *__restrict__ codes, uint32_t flags) {
+/* Pass 2 of one signature (fd_ed25519_user.c:208-229): [S]B + [k](-A) == R,
+   cofactorless, projective compare against the parked affine R. */
+FDG_DEV int verify_pass2(uint32_t *wsl, const uint32_t *s_btab) {
+  uint32_t *park = park_ptr(wsl);
+  const int code = (int)park[PARK_CODE * 64];
+  /* wave-uniform early out when every lane already failed pass 1 */
+  if (__all(code != 0)) return code;
+  uint32_t kd[8], sd[8];
+#pragma unroll
+  for (int i = 0; i < 8; i++) { kd[i] = park[(PARK_KD + i) * 64]; sd[i] = park[(PARK_SD + i) * 64]; }
+  ge_p2 Rc;
+  dsm(Rc, kd, sd, wsl, s_btab);
+  fe l, xy;
+#pragma unroll
+  for (int i = 0; i < 10; i++) xy.v[i] = park[(PARK_XR + i) * 64];
+  fe_mul(l, xy, Rc.Z);
+  bool eq = fe_eq(Rc.X, l);
+#pragma unroll
+  for (int i = 0; i < 10; i++) xy.v[i] = park[(PARK_YR + i) * 64];
+  fe_mul(l, xy, Rc.Z);
+  eq = eq && fe_eq(Rc.Y, l);
+  return (code == 0 && !eq) ? -3 : code;
+}
+
+FDG_DEV uint32_t *lane_ws(uint32_t *ws, uint32_t i) {
+  return ws + (size_t)(i >> 6) * (FDGPU_WS_ENTRIES * FDGPU_ATAB_WORDS * 64u) + (i & 63u);
+}
+
+/* Kernel 1: pass 1 (hash, scalars, decompression, small order, table). */
+__global__ void __launch_bounds__(FDGPU_BLOCK, FDGPU_PREP_WAVES)
+fdgpu_prep_kernel(const uint8_t *__restrict__ arena, const fdgpu_sig_desc_t *__restrict__ sigs, uint32_t n_sig,
+                  uint32_t *__restrict__ ws, uint32_t flags) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  const bool active = i < n_sig;
+  const fdgpu_sig_desc_t d = sigs[active ? i : n_sig - 1];
+  uint32_t nb = sha512_hram_blocks(d.msg_sz);      /* wave-uniform SHA block bound */
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) nb = max(nb, (uint32_t)__shfl_xor((int)nb, off));
+  verify_pass1(arena, d, nb, lane_ws(ws, i), (flags & FDGPU_FLAG_REF_MAP) != 0);
+}
+
+/* Kernel 2: pass 2 (double-scalar multiplication and compare). */
+__global__ void __launch_bounds__(FDGPU_BLOCK, FDGPU_DSM_WAVES)
+fdgpu_dsm_kernel(uint32_t n_sig, const uint32_t *__restrict__ btab, uint32_t *__restrict__ ws,
+                 int8_t *__restrict__ codes) {
   __shared__ __attribute__((aligned(16))) uint32_t s_btab[FDGPU_BTAB_ENTRIES * FDGPU_BTAB_STRIDE];
   for (uint32_t i = threadIdx.x; i < FDGPU_BTAB_ENTRIES * FDGPU_BTAB_STRIDE; i += blockDim.x) s_btab[i] = btab[i];
   __syncthreads();
-  const uint32_t lane = threadIdx.x & 63u;
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  uint32_t *wsl = ws + (size_t)(i >> 6) * (FDGPU_WS_ENTRIES * FDGPU_ATAB_WORDS * 64u) + lane;
-  const bool ref_map = (flags & FDGPU_FLAG_REF_MAP) != 0;
-  const bool active = i < n_sig;
-  const fdgpu_sig_desc_t d = sigs[active ? i : n_sig - 1];
-  /* wave-uniform SHA block bound */
-  uint32_t nb = sha512_hram_blocks(d.msg_sz);
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) nb = max(nb, (uint32_t)__shfl_xor((int)nb, off));
-  const int code = verify_one(arena, d, nb, wsl, s_btab, ref_map);
-  if (active) codes[i] = (int8_t)code;
+  const int code = verify_pass2(lane_ws(ws, i), s_btab);
+  if (i < n_sig) codes[i] = (int8_t)code;
 }
 
 __global__ void fdgpu_combine_kernel(const fdgpu_txn_desc_t *__restrict__ txns, uint32_t n_txn,
@@ -375,7 +405,7 @@ hipError_t fdgpu_launch_btab_init(uint32_t *d_btab, hipStream_t stream) {
 }
 
 hipError_t fdgpu_verify_occupancy(int *blocks_per_cu) {
-  return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, fdgpu_verify_sigs_kernel, FDGPU_BLOCK, 0);
+  return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, fdgpu_dsm_kernel, FDGPU_BLOCK, 0);
 }
 
 size_t fdgpu_ws_bytes(uint64_t n_sig) {
@@ -388,8 +418,10 @@ hipError_t fdgpu_launch_verify_sigs(const uint8_t *d_arena, const fdgpu_sig_desc
                                     hipStream_t stream) {
   if (!n_sig) return hipSuccess;
   const uint32_t grid = (n_sig + FDGPU_BLOCK - 1) / FDGPU_BLOCK;
-  hipLaunchKernelGGL(fdgpu_verify_sigs_kernel, dim3(grid), dim3(FDGPU_BLOCK), 0, stream, d_arena, d_sigs, n_sig,
-                     d_btab, d_ws, d_sig_codes, flags);
+  hipLaunchKernelGGL(fdgpu_prep_kernel, dim3(grid), dim3(FDGPU_BLOCK), 0, stream, d_arena, d_sigs, n_sig, d_ws, flags);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(fdgpu_dsm_kernel, dim3(grid), dim3(FDGPU_BLOCK), 0, stream, n_sig, d_btab, d_ws, d_sig_codes);
   return hipGetLastError();
 }
 
