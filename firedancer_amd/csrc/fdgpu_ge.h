@@ -170,6 +170,34 @@ FDG_DEV void ge_add_niels_ld(ge_p1p1 &r, const ge_p3 &p, const LD &ld, bool neg)
   r.Y = t;
 }
 
+/* ge_add_cached_ld over an entry already in registers (q: the 40 words of a
+   cached entry, coordinate order as above).  The Y+X / Y-X swap for neg is a
+   per-word select, so no register array is indexed dynamically. */
+FDG_DEV void ge_add_cached_regs(ge_p1p1 &r, const ge_p3 &p, const uint32_t (&q)[40], bool neg) {
+  fe t, c;
+#pragma unroll
+  for (int i = 0; i < 10; i++) c.v[i] = q[30 + i];
+  fe_cneg(c, neg);
+  fe_mul(r.Z, p.T, c);             /* C = T1 2dT2 */
+#pragma unroll
+  for (int i = 0; i < 10; i++) c.v[i] = q[20 + i];
+  fe_mul(r.T, p.Z, c);             /* D = Z1 2Z2 */
+#pragma unroll
+  for (int i = 0; i < 10; i++) c.v[i] = neg ? q[10 + i] : q[i];
+  fe_add(t, p.Y, p.X);
+  fe_mul(r.X, t, c);               /* A */
+#pragma unroll
+  for (int i = 0; i < 10; i++) c.v[i] = neg ? q[i] : q[10 + i];
+  fe_sub(t, p.Y, p.X);
+  fe_mul(r.Y, t, c);               /* B */
+  fe_add(t, r.T, r.Z);
+  fe_sub(r.T, r.T, r.Z);
+  r.Z = t;
+  fe_add(t, r.X, r.Y);
+  fe_sub(r.X, r.X, r.Y);
+  r.Y = t;
+}
+
 FDG_DEV void ge_p3_to_cached(ge_cached &r, const ge_p3 &p) {
   constexpr uint32_t D2[10] = FDGPU_FE_D2;
   fe d2; fe_set(d2, D2);

@@ -30,6 +30,8 @@ typedef struct {
 #define FDGPU_ATAB_ENTRIES  9u            /* 0 (identity), 1A .. 8A (A negated) */
 #define FDGPU_ATAB_WORDS    40u           /* u32 per cached entry */
 #define FDGPU_WS_ENTRIES    10u           /* per-lane workspace entries: table + parked (x_R, y_R) */
+#define FDGPU_WS_LANE_WORDS (FDGPU_WS_ENTRIES * FDGPU_ATAB_WORDS)   /* 1600 B per signature */
+#define FDGPU_BTAB_LDS_STRIDE 33u         /* B-table entry stride in LDS (odd: no bank conflicts) */
 #define FDGPU_BLOCK         256u
 #define FDGPU_FLAG_REF_MAP  1u            /* portable-backend error mapping */
 

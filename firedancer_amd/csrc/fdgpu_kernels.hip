@@ -81,17 +81,19 @@ __global__ void fdgpu_btab_init_kernel(uint32_t *btab) {
 }
 
 /* ---- per-lane A table in the global workspace ----
-   layout: ws[((wave * 10 + entry) * 40 + word) * 64 + lane]  (dword per lane,
-   a wave's access to one entry-word is one 256-B row).  Entries 0..8 are the
-   table; entry 9 parks (x_R, y_R) across the scalar multiplication. */
+   layout: lane-contiguous, ws[i * 400 + entry * 40 + word] for signature i:
+   a lane's entry is 160 contiguous bytes (32-B aligned), read whole with ten
+   16-B loads, so a wave's table read touches ~2 cache lines per lane and
+   uses every byte it fetches.  Entries 0..8 are the table; entry 9 parks
+   (x_R, y_R), the digit strings and the pass-1 code across the kernels. */
 
 FDG_DEV void atab_store(uint32_t *wsl, uint32_t entry, const ge_cached &c) {
-  uint32_t *p = wsl + entry * (FDGPU_ATAB_WORDS * 64u);
+  uint4 *p = (uint4 *)(wsl + entry * FDGPU_ATAB_WORDS);
+  uint32_t w[40];
 #pragma unroll
-  for (int i = 0; i < 10; i++) {
-    p[(0 + i) * 64] = c.YpX.v[i]; p[(10 + i) * 64] = c.YmX.v[i];
-    p[(20 + i) * 64] = c.Z2.v[i]; p[(30 + i) * 64] = c.T2d.v[i];
-  }
+  for (int i = 0; i < 10; i++) { w[i] = c.YpX.v[i]; w[10 + i] = c.YmX.v[i]; w[20 + i] = c.Z2.v[i]; w[30 + i] = c.T2d.v[i]; }
+#pragma unroll
+  for (int q = 0; q < 10; q++) p[q] = make_uint4(w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]);
 }
 FDG_DEV int sext4(uint32_t x) { return ((int)(x << 28)) >> 28; }
 FDG_DEV int sext8(uint32_t x) { return ((int)(x << 24)) >> 24; }
@@ -104,7 +106,9 @@ FDG_DEV void shl8(uint32_t (&w)[8]) {
 }
 
 /* R' = [S]B + [k](-A) as projective (X:Y:Z).  kd: radix-16 digits of k,
-   sd: radix-256 digits of S; wsl: this lane's A table (entries 0..8). */
+   sd: radix-256 digits of S; wsl: this lane's A table (entries 0..8).
+   The A entry of each window is loaded (10 x 16 B) before that window's
+   four doublings, so its latency hides behind ~30 field products. */
 FDG_DEV void dsm(ge_p2 &acc2, uint32_t (&kd)[8], uint32_t (&sd)[8], const uint32_t *wsl,
                  const uint32_t *s_btab) {
   ge_p2_0(acc2);
@@ -117,6 +121,15 @@ FDG_DEV void dsm(ge_p2 &acc2, uint32_t (&kd)[8], uint32_t (&sd)[8], const uint32
 #pragma unroll 1
     for (int h = 0; h < 2; h++) {
       const int e = sext4(h == 0 ? (kb >> 4) : (kb & 15u));
+      uint32_t q[40];
+      {
+        const uint4 *ent = (const uint4 *)(wsl + (uint32_t)(e < 0 ? -e : e) * FDGPU_ATAB_WORDS);
+#pragma unroll
+        for (int i = 0; i < 10; i++) {
+          const uint4 v = ent[i];
+          q[4 * i] = v.x; q[4 * i + 1] = v.y; q[4 * i + 2] = v.z; q[4 * i + 3] = v.w;
+        }
+      }
 #pragma unroll 1
       for (int r = 0; r < 4; r++) {
         ge_dbl(t, acc2);
@@ -124,15 +137,11 @@ FDG_DEV void dsm(ge_p2 &acc2, uint32_t (&kd)[8], uint32_t (&sd)[8], const uint32
       }
       /* T of the last doubling (p1p1 -> p3 needs X'Y') */
       acc3.X = acc2.X; acc3.Y = acc2.Y; acc3.Z = acc2.Z; fe_mul(acc3.T, t.X, t.Y);
-      {
-        const uint32_t *ent = wsl + (uint32_t)(e < 0 ? -e : e) * (FDGPU_ATAB_WORDS * 64u);
-        auto ld = [ent](int c, int w) { return ent[(10 * c + w) * 64]; };
-        ge_add_cached_ld(t, acc3, ld, e < 0);
-      }
+      ge_add_cached_regs(t, acc3, q, e < 0);
       if (h == 1) {
         const int d = sext8(sb);
         ge_p1p1_to_p3(acc3, t);
-        const uint32_t *ent = s_btab + (uint32_t)(d < 0 ? -d : d) * FDGPU_BTAB_STRIDE;
+        const uint32_t *ent = s_btab + (uint32_t)(d < 0 ? -d : d) * FDGPU_BTAB_LDS_STRIDE;
         auto ld = [ent](int c, int w) { return ent[10 * c + w]; };
         ge_add_niels_ld(t, acc3, ld, d < 0);
       }
@@ -149,8 +158,8 @@ FDG_DEV void atab_build(uint32_t *wsl, const ge_p3 &An) {
   ge_p1p1 t; ge_p2 a2; ge_p3 P;
   ge_p3_to_p2(a2, An); ge_dbl(t, a2); ge_p1p1_to_p3(P, t);          /* 2(-A) */
   ge_p3_to_cached(c, P); atab_store(wsl, 2, c);
-  const uint32_t *ent1 = wsl + 1u * (FDGPU_ATAB_WORDS * 64u);
-  auto ld1 = [ent1](int cc, int w) { return ent1[(10 * cc + w) * 64]; };
+  const uint32_t *ent1 = wsl + 1u * FDGPU_ATAB_WORDS;
+  auto ld1 = [ent1](int cc, int w) { return ent1[10 * cc + w]; };
 #pragma unroll 1
   for (uint32_t e = 3; e <= 8; e++) {
     ge_add_cached_ld(t, P, ld1, false); ge_p1p1_to_p3(P, t);
@@ -166,7 +175,7 @@ FDG_DEV void atab_build(uint32_t *wsl, const ge_p3 &An) {
 #define PARK_SD 28
 #define PARK_CODE 36
 
-FDG_DEV uint32_t *park_ptr(uint32_t *wsl) { return wsl + 9u * (FDGPU_ATAB_WORDS * 64u); }
+FDG_DEV uint32_t *park_ptr(uint32_t *wsl) { return wsl + 9u * FDGPU_ATAB_WORDS; }
 
 /* Pass 1 of one signature (fd_ed25519_user.c:158-207; SURVEY Appendix A steps
    1-5): S < L, k = SHA-512(R||A||M) mod L, decode A then R, small-order
@@ -189,7 +198,7 @@ FDG_DEV int verify_pass1(const uint8_t *arena, const fdgpu_sig_desc_t &sd_in, ui
     sc_reduce512(k, kx);
     sc_recode16(kd, k);
 #pragma unroll
-    for (int i = 0; i < 8; i++) park[(PARK_KD + i) * 64] = kd[i];
+    for (int i = 0; i < 8; i++) park[PARK_KD + i] = kd[i];
   }
   /* step 1: S < L (fd_ed25519_user.c:159-161); S recoded to signed radix 256 */
   int code;
@@ -199,7 +208,7 @@ FDG_DEV int verify_pass1(const uint8_t *arena, const fdgpu_sig_desc_t &sd_in, ui
     code = sc_lt_L(S) ? 0 : -1;
     sc_recode256(sd, S);
 #pragma unroll
-    for (int i = 0; i < 8; i++) park[(PARK_SD + i) * 64] = sd[i];
+    for (int i = 0; i < 8; i++) park[PARK_SD + i] = sd[i];
   }
   /* step 2 (A): decode, small order, table of -A */
   bool a_ok, a_small;
@@ -217,13 +226,13 @@ FDG_DEV int verify_pass1(const uint8_t *arena, const fdgpu_sig_desc_t &sd_in, ui
     r_ok = ge_decode(Rp, R, ref_map);
     r_small = ge_is_small_order_affine(Rp);
 #pragma unroll
-    for (int i = 0; i < 10; i++) { park[(PARK_XR + i) * 64] = Rp.X.v[i]; park[(PARK_YR + i) * 64] = Rp.Y.v[i]; }
+    for (int i = 0; i < 10; i++) { park[PARK_XR + i] = Rp.X.v[i]; park[PARK_YR + i] = Rp.Y.v[i]; }
   }
   if (code == 0 && !a_ok) code = ref_map ? -2 : -1;    /* decode2 reports A before R */
   if (code == 0 && !r_ok) code = -1;
   if (code == 0 && a_small) code = -2;                 /* fd_ed25519_user.c:194-199 */
   if (code == 0 && r_small) code = -1;
-  park[PARK_CODE * 64] = (uint32_t)code;
+  park[PARK_CODE] = (uint32_t)code;
   return code;
 }
 
@@ -231,28 +240,28 @@ FDG_DEV int verify_pass1(const uint8_t *arena, const fdgpu_sig_desc_t &sd_in, ui
    cofactorless, projective compare against the parked affine R. */
 FDG_DEV int verify_pass2(uint32_t *wsl, const uint32_t *s_btab) {
   uint32_t *park = park_ptr(wsl);
-  const int code = (int)park[PARK_CODE * 64];
+  const int code = (int)park[PARK_CODE];
   /* wave-uniform early out when every lane already failed pass 1 */
   if (__all(code != 0)) return code;
   uint32_t kd[8], sd[8];
 #pragma unroll
-  for (int i = 0; i < 8; i++) { kd[i] = park[(PARK_KD + i) * 64]; sd[i] = park[(PARK_SD + i) * 64]; }
+  for (int i = 0; i < 8; i++) { kd[i] = park[PARK_KD + i]; sd[i] = park[PARK_SD + i]; }
   ge_p2 Rc;
   dsm(Rc, kd, sd, wsl, s_btab);
   fe l, xy;
 #pragma unroll
-  for (int i = 0; i < 10; i++) xy.v[i] = park[(PARK_XR + i) * 64];
+  for (int i = 0; i < 10; i++) xy.v[i] = park[PARK_XR + i];
   fe_mul(l, xy, Rc.Z);
   bool eq = fe_eq(Rc.X, l);
 #pragma unroll
-  for (int i = 0; i < 10; i++) xy.v[i] = park[(PARK_YR + i) * 64];
+  for (int i = 0; i < 10; i++) xy.v[i] = park[PARK_YR + i];
   fe_mul(l, xy, Rc.Z);
   eq = eq && fe_eq(Rc.Y, l);
   return (code == 0 && !eq) ? -3 : code;
 }
 
 FDG_DEV uint32_t *lane_ws(uint32_t *ws, uint32_t i) {
-  return ws + (size_t)(i >> 6) * (FDGPU_WS_ENTRIES * FDGPU_ATAB_WORDS * 64u) + (i & 63u);
+  return ws + (size_t)i * FDGPU_WS_LANE_WORDS;
 }
 
 /* Kernel 1: pass 1 (hash, scalars, decompression, small order, table). */
@@ -272,8 +281,10 @@ fdgpu_prep_kernel(const uint8_t *__restrict__ arena, const fdgpu_sig_desc_t *__r
 __global__ void __launch_bounds__(FDGPU_BLOCK, FDGPU_DSM_WAVES)
 fdgpu_dsm_kernel(uint32_t n_sig, const uint32_t *__restrict__ btab, uint32_t *__restrict__ ws,
                  int8_t *__restrict__ codes) {
-  __shared__ __attribute__((aligned(16))) uint32_t s_btab[FDGPU_BTAB_ENTRIES * FDGPU_BTAB_STRIDE];
-  for (uint32_t i = threadIdx.x; i < FDGPU_BTAB_ENTRIES * FDGPU_BTAB_STRIDE; i += blockDim.x) s_btab[i] = btab[i];
+  /* odd LDS stride: lanes reading word w of different entries hit different banks */
+  __shared__ uint32_t s_btab[FDGPU_BTAB_ENTRIES * FDGPU_BTAB_LDS_STRIDE];
+  for (uint32_t i = threadIdx.x; i < FDGPU_BTAB_ENTRIES * FDGPU_BTAB_STRIDE; i += blockDim.x)
+    s_btab[(i / FDGPU_BTAB_STRIDE) * FDGPU_BTAB_LDS_STRIDE + i % FDGPU_BTAB_STRIDE] = btab[i];
   __syncthreads();
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   const int code = verify_pass2(lane_ws(ws, i), s_btab);
@@ -409,8 +420,8 @@ hipError_t fdgpu_verify_occupancy(int *blocks_per_cu) {
 }
 
 size_t fdgpu_ws_bytes(uint64_t n_sig) {
-  const uint64_t waves = (n_sig + FDGPU_BLOCK - 1) / FDGPU_BLOCK * (FDGPU_BLOCK / 64u);
-  return (size_t)waves * FDGPU_WS_ENTRIES * FDGPU_ATAB_WORDS * 64u * sizeof(uint32_t);
+  const uint64_t lanes = (n_sig + FDGPU_BLOCK - 1) / FDGPU_BLOCK * FDGPU_BLOCK;
+  return (size_t)lanes * FDGPU_WS_LANE_WORDS * sizeof(uint32_t);
 }
 
 hipError_t fdgpu_launch_verify_sigs(const uint8_t *d_arena, const fdgpu_sig_desc_t *d_sigs, uint32_t n_sig,
