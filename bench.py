@@ -157,15 +157,18 @@ def cpu_baseline(arena, txns, sample):
             "cpu_codes_nonzero": int((codes != 0).sum())}
 
 
+VERIFY_KERNEL = "fdgpu_fused_kernel"
+
+
 def pmc_traffic():
-    """HBM bytes per verify-kernel launch from the committed PMC summary
-    (profiles/*_pmc.json written by tools/pmc_summary.py), if present."""
+    """HBM bytes per verify-kernel launch from the newest committed PMC summary
+    of the current kernel (profiles/rNN_pmc.json, tools/pmc_summary.py)."""
     import glob
-    files = sorted(glob.glob(os.path.join(REPO, "profiles", "*_pmc.json")))
-    if not files:
-        return None, None
-    d = json.load(open(files[-1]))
-    return d.get("hbm_bytes_per_launch"), os.path.basename(files[-1])
+    for f in sorted(glob.glob(os.path.join(REPO, "profiles", "r[0-9][0-9]_pmc.json")), reverse=True):
+        d = json.load(open(f))
+        if d.get("kernel") == VERIFY_KERNEL:
+            return d.get("hbm_bytes_per_launch"), os.path.basename(f)
+    return None, None
 
 
 def main():
@@ -236,7 +239,7 @@ def main():
                          "unit": "TOP/s", "frac": round(achieved / VALU_MAD_PEAK_TOPS, 4),
                          "traffic": traffic,
                          "note": f"INT32 v_mad_u64_u32 ops: {MADS_PER_SIG} algorithmic mads/sig x {n_sig} sigs / mean "
-                                 f"signature-kernel time {kv_ms:.3f} ms (HIP events, compute stream); combine kernel "
+                                 f"{VERIFY_KERNEL} time {kv_ms:.3f} ms (HIP events, compute stream); combine kernel "
                                  f"{kc_ms:.4f} ms; traffic source {traffic_src}"},
             "cpu_baseline": cpu,
             "self_check_codes": self_ok,

@@ -1,19 +1,22 @@
 /* fdgpu_kernels.hip -- MI355X (gfx950) kernels of the batched Ed25519
    verify engine.
 
-   fdgpu_verify_sigs: one signature per lane, whole verify in one pass
-     (fd_ed25519_user.c:135-230):
-       S < L  ->  SHA-512(R||A||M) mod L  ->  decode A, R  ->  small-order
-       tests  ->  [S]B + [k](-A) == R  ->  per-signature code.
+   fdgpu_fused_kernel (default): one signature per lane, whole verify in one
+     launch (fd_ed25519_user.c:135-230):
+       pass 1: S < L -> SHA-512(R||A||M) mod L -> decode A, R -> small-order
+               tests -> table {O, -A, .., -8A} into the lane's workspace;
+       pass 2: [S]B + [k](-A) == R -> per-signature code.
      Every lane executes the same instruction stream (failures are masked,
      not branched on; a wave whose lanes all failed pass 1 skips the scalar
      multiplication).  The double-scalar multiplication uses fixed signed
-     windows: radix 16 for k over a per-lane table {O, -A, ..., -8A} kept
-     in a global workspace laid out lane-interleaved, and radix 256 for S
-     over the fixed table {O, B, ..., 128B} staged into LDS once per
-     workgroup (the reference's wNAF-4 / wNAF-8 split,
-     fd_curve25519.c:109-153, made divergence-free).
-     Persistent grid: grid = resident workgroups, grid-stride over the batch.
+     windows: radix 16 for k over the per-lane A table (lane-contiguous
+     160-B entries in a global workspace, each window's entry prefetched
+     ahead of its doublings), and radix 256 for S over the fixed table
+     {O, B, ..., 128B} staged into LDS once per workgroup at an odd stride
+     (the reference's wNAF-4 / wNAF-8 split, fd_curve25519.c:109-153, made
+     divergence-free).  One thread per signature, grid = ceil(n / 256).
+   fdgpu_prep_kernel + fdgpu_dsm_kernel (FDGPU_FUSED=0): the same two passes
+     as separate launches (measured equal speed; kept for A/B).
    fdgpu_combine: per transaction, batch_single_msg first-error semantics
      (fd_ed25519_user.c:232-310).
    fdgpu_btab_init: builds the B table on the device at engine open. */
@@ -28,6 +31,9 @@ using namespace fdgpu;
 
 #ifndef FDGPU_PREP_WAVES
 #define FDGPU_PREP_WAVES 2     /* decode/pow chains want ~200 VGPRs */
+#endif
+#ifndef FDGPU_FUSED
+#define FDGPU_FUSED 1         /* 1: one launch runs both passes; 0: prep + dsm kernels (same speed) */
 #endif
 #ifndef FDGPU_DSM_WAVES
 #define FDGPU_DSM_WAVES 3     /* ~130 VGPRs: 3 waves per SIMD, no spills */
@@ -291,6 +297,27 @@ fdgpu_dsm_kernel(uint32_t n_sig, const uint32_t *__restrict__ btab, uint32_t *__
   if (i < n_sig) codes[i] = (int8_t)code;
 }
 
+/* Fused variant (FDGPU_FUSED=1): both passes in one launch, B table in LDS. */
+__global__ void __launch_bounds__(FDGPU_BLOCK, FDGPU_PREP_WAVES)
+fdgpu_fused_kernel(const uint8_t *__restrict__ arena, const fdgpu_sig_desc_t *__restrict__ sigs, uint32_t n_sig,
+                   const uint32_t *__restrict__ btab, uint32_t *__restrict__ ws, int8_t *__restrict__ codes,
+                   uint32_t flags) {
+  __shared__ uint32_t s_btab[FDGPU_BTAB_ENTRIES * FDGPU_BTAB_LDS_STRIDE];
+  for (uint32_t i = threadIdx.x; i < FDGPU_BTAB_ENTRIES * FDGPU_BTAB_STRIDE; i += blockDim.x)
+    s_btab[(i / FDGPU_BTAB_STRIDE) * FDGPU_BTAB_LDS_STRIDE + i % FDGPU_BTAB_STRIDE] = btab[i];
+  __syncthreads();
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  const bool active = i < n_sig;
+  const fdgpu_sig_desc_t d = sigs[active ? i : n_sig - 1];
+  uint32_t nb = sha512_hram_blocks(d.msg_sz);
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) nb = max(nb, (uint32_t)__shfl_xor((int)nb, off));
+  uint32_t *wsl = lane_ws(ws, i);
+  verify_pass1(arena, d, nb, wsl, (flags & FDGPU_FLAG_REF_MAP) != 0);
+  const int code = verify_pass2(wsl, s_btab);
+  if (active) codes[i] = (int8_t)code;
+}
+
 __global__ void fdgpu_combine_kernel(const fdgpu_txn_desc_t *__restrict__ txns, uint32_t n_txn,
                                      const int8_t *__restrict__ sig_codes, int8_t *__restrict__ txn_codes) {
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
@@ -416,7 +443,11 @@ hipError_t fdgpu_launch_btab_init(uint32_t *d_btab, hipStream_t stream) {
 }
 
 hipError_t fdgpu_verify_occupancy(int *blocks_per_cu) {
+#if FDGPU_FUSED
+  return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, fdgpu_fused_kernel, FDGPU_BLOCK, 0);
+#else
   return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, fdgpu_dsm_kernel, FDGPU_BLOCK, 0);
+#endif
 }
 
 size_t fdgpu_ws_bytes(uint64_t n_sig) {
@@ -429,6 +460,11 @@ hipError_t fdgpu_launch_verify_sigs(const uint8_t *d_arena, const fdgpu_sig_desc
                                     hipStream_t stream) {
   if (!n_sig) return hipSuccess;
   const uint32_t grid = (n_sig + FDGPU_BLOCK - 1) / FDGPU_BLOCK;
+#if FDGPU_FUSED
+  hipLaunchKernelGGL(fdgpu_fused_kernel, dim3(grid), dim3(FDGPU_BLOCK), 0, stream, d_arena, d_sigs, n_sig, d_btab, d_ws,
+                     d_sig_codes, flags);
+  return hipGetLastError();
+#endif
   hipLaunchKernelGGL(fdgpu_prep_kernel, dim3(grid), dim3(FDGPU_BLOCK), 0, stream, d_arena, d_sigs, n_sig, d_ws, flags);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;

@@ -1,8 +1,9 @@
 """Summarise rocprofv3 --pmc passes of the verify kernel into profiles/<tag>_pmc.json.
 
 Usage: python tools/pmc_summary.py <tag> <dir_pass1> [<dir_pass2> ...]
+(env PMC_OUT_DIR overrides the output directory, default profiles/)
 Each dir holds one rocprofv3 `--pmc ... -o run --output-format csv` pass.
-Reports per launch of fdgpu_verify_sigs_kernel: FETCH_SIZE / WRITE_SIZE (KB as
+Reports per launch of the verify kernel (KERNEL): FETCH_SIZE / WRITE_SIZE (KB as
 rocprofv3 reports them, and HBM bytes with the gfx950 FETCH_SIZE x2
 correction of MI355X_MICROARCH.md §HBM), VALU instruction mix and busy
 fractions.  The per-launch HBM bytes feed bench.py's roofline.traffic.
@@ -14,7 +15,7 @@ import os
 import sys
 from collections import defaultdict
 
-KERNEL = "fdgpu_verify_sigs_kernel"
+KERNEL = "fdgpu_fused_kernel"
 
 
 def read_pass(d):
@@ -55,7 +56,9 @@ def main():
         out["valu_int32_share"] = agg["SQ_INSTS_VALU_INT32"] / max(agg["SQ_INSTS_VALU"], 1)
     if "SQ_ACTIVE_INST_VALU" in agg and "SQ_WAVE_CYCLES" in agg:
         out["valu_active_per_wave_cycle"] = agg["SQ_ACTIVE_INST_VALU"] / max(agg["SQ_WAVE_CYCLES"], 1)
-    path = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "profiles", f"{tag}_pmc.json")
+    out_dir = os.environ.get("PMC_OUT_DIR") or os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                                           "profiles")
+    path = os.path.join(out_dir, f"{tag}_pmc.json")
     json.dump(out, open(path, "w"), indent=1)
     print(json.dumps(out, indent=1))
 
