@@ -1,0 +1,431 @@
+/* fdt_base.cpp -- host-side wire formats around the verify stage:
+   tango frag metadata / mcache / compact dcache, tcache, fd_hash and the
+   transaction parser (include/fd_verify_tile.h lists the reference lines
+   each one restates).  Plain C++17, no GPU code. */
+#include <atomic>
+#include <cstring>
+
+#include "../../../include/fd_verify_tile.h"
+
+namespace {
+
+inline uint64_t ld_acq(const uint64_t *p) { return __atomic_load_n(p, __ATOMIC_ACQUIRE); }
+inline void st_rel(uint64_t *p, uint64_t v) { __atomic_store_n(p, v, __ATOMIC_RELEASE); }
+
+}  // namespace
+
+extern "C" {
+
+/* ------------------------------------------------------------ mcache */
+
+uint64_t fdt_frag_meta_ctl(uint64_t orig, int som, int eom, int err) {
+  return (uint64_t)(som != 0) | ((uint64_t)(eom != 0) << 1) | ((uint64_t)(err != 0) << 2) | (orig << 3);
+}
+
+/* fd_mcache.c:64-69: the line of seq s starts out holding s-1 (so a
+   consumer waiting for s sees "not yet") with ctl = som|eom|err. */
+void fdt_mcache_init(fdt_frag_meta_t *mcache, uint64_t depth, uint64_t seq0) {
+  std::memset(mcache, 0, depth * sizeof(fdt_frag_meta_t));
+  for (uint64_t i = 0; i < depth; i++) {
+    const uint64_t s = seq0 + i;
+    fdt_frag_meta_t &m = mcache[s & (depth - 1)];
+    m.seq = s - 1;
+    m.ctl = (uint16_t)fdt_frag_meta_ctl(0, 1, 1, 1);
+  }
+  std::atomic_thread_fence(std::memory_order_release);
+}
+
+/* fd_mcache.h:299-322: mark the line as being rewritten (seq-1), write the
+   body, then expose seq.  Release ordering makes the body visible before
+   the final seq on any consumer that acquires it. */
+void fdt_mcache_publish(fdt_frag_meta_t *mcache, uint64_t depth, uint64_t seq, uint64_t sig, uint64_t chunk,
+                        uint64_t sz, uint64_t ctl, uint64_t tsorig, uint64_t tspub) {
+  fdt_frag_meta_t *m = mcache + (seq & (depth - 1));
+  st_rel(&m->seq, seq - 1);
+  std::atomic_thread_fence(std::memory_order_release);
+  m->sig = sig;
+  m->chunk = (uint32_t)chunk;
+  m->sz = (uint16_t)sz;
+  m->ctl = (uint16_t)ctl;
+  m->tsorig = (uint32_t)tsorig;
+  m->tspub = (uint32_t)tspub;
+  st_rel(&m->seq, seq);
+}
+
+/* One poll of FD_MCACHE_WAIT (fd_mcache.h:574-601): read seq, copy the
+   line, re-read seq; the copy is trusted only when both reads agree. */
+int fdt_mcache_poll(const fdt_frag_meta_t *mcache, uint64_t depth, uint64_t seq, fdt_frag_meta_t *meta,
+                    uint64_t *seq_found) {
+  const fdt_frag_meta_t *m = mcache + (seq & (depth - 1));
+  const uint64_t s0 = ld_acq(&m->seq);
+  fdt_frag_meta_t copy;
+  std::memcpy(&copy, (const void *)m, sizeof copy);
+  std::atomic_thread_fence(std::memory_order_acquire);
+  const uint64_t s1 = ld_acq(&m->seq);
+  if (seq_found) *seq_found = s0;
+  const int64_t diff = (int64_t)(s0 - seq);
+  if (s0 != s1 || diff < 0) return 0;    /* being written, or not yet published */
+  if (diff > 0) return -1;               /* overrun */
+  copy.seq = s0;
+  *meta = copy;
+  return 1;
+}
+
+uint64_t fdt_mcache_query(const fdt_frag_meta_t *mcache, uint64_t depth, uint64_t seq) {
+  return ld_acq(&mcache[seq & (depth - 1)].seq);
+}
+
+/* ------------------------------------------------------------ dcache */
+
+/* fd_dcache.h:214: chunks for a worst-case frag, rounded to a chunk pair */
+uint64_t fdt_dcache_chunk_mtu(uint64_t mtu) { return ((mtu + 2 * FDT_CHUNK_SZ - 1) >> (1 + FDT_CHUNK_LG_SZ)) << 1; }
+
+/* room for chunk_mtu*(depth+2)-1 chunks (fd_dcache.h:220-260), rounded up */
+uint64_t fdt_dcache_data_sz(uint64_t mtu, uint64_t depth) {
+  return fdt_dcache_chunk_mtu(mtu) * (depth + 2) * FDT_CHUNK_SZ;
+}
+
+uint64_t fdt_dcache_wmark(uint64_t chunk0, uint64_t chunk1, uint64_t mtu) {
+  (void)chunk0;
+  return chunk1 - fdt_dcache_chunk_mtu(mtu);
+}
+
+/* fd_dcache.h:262-269 */
+uint64_t fdt_dcache_compact_next(uint64_t chunk, uint64_t sz, uint64_t chunk0, uint64_t wmark) {
+  chunk += ((sz + 2 * FDT_CHUNK_SZ - 1) >> (1 + FDT_CHUNK_LG_SZ)) << 1;
+  return chunk > wmark ? chunk0 : chunk;
+}
+
+/* ------------------------------------------------------------ tcache */
+
+namespace {
+constexpr uint64_t TCACHE_MAGIC = 0xf17eda2c377ca540ULL;   /* fd_tcache.h:63 */
+struct tcache_view {
+  uint64_t *hdr;
+  uint64_t depth() const { return hdr[1]; }
+  uint64_t map_cnt() const { return hdr[2]; }
+  uint64_t &oldest() const { return hdr[3]; }
+  uint64_t *ring() const { return hdr + 4; }
+  uint64_t *map() const { return hdr + 4 + hdr[1]; }
+};
+inline int msb64(uint64_t x) { return 63 - __builtin_clzll(x); }
+
+/* linear probe from tag & (map_cnt-1) to the tag or the first null slot
+   (FD_TCACHE_QUERY, fd_tcache.h:281-295) */
+inline bool map_find(const uint64_t *map, uint64_t map_cnt, uint64_t tag, uint64_t &slot) {
+  slot = tag & (map_cnt - 1);
+  for (;;) {
+    const uint64_t t = map[slot];
+    if (t == tag) return true;
+    if (t == FDT_TCACHE_TAG_NULL) return false;
+    slot = (slot + 1) & (map_cnt - 1);
+  }
+}
+
+/* backward-shift deletion of tag (fd_tcache_remove, fd_tcache.h:306-342):
+   after emptying a slot, walk the probe run and pull back every entry
+   whose home slot is not cyclically within (hole, slot]. */
+void map_remove(uint64_t *map, uint64_t map_cnt, uint64_t tag) {
+  if (tag == FDT_TCACHE_TAG_NULL) return;
+  uint64_t slot;
+  if (!map_find(map, map_cnt, tag, slot)) return;
+  const uint64_t mask = map_cnt - 1;
+  for (;;) {
+    map[slot] = FDT_TCACHE_TAG_NULL;
+    const uint64_t hole = slot;
+    uint64_t t;
+    for (;;) {
+      slot = (slot + 1) & mask;
+      t = map[slot];
+      if (t == FDT_TCACHE_TAG_NULL) return;
+      const uint64_t home = t & mask;
+      /* stays iff home lies cyclically in (hole, slot] */
+      const bool stays = (hole < slot) ? (hole < home && home <= slot) : (hole < home || home <= slot);
+      if (!stays) break;
+    }
+    map[hole] = t;
+  }
+}
+}  // namespace
+
+uint64_t fdt_tcache_map_cnt_default(uint64_t depth) {
+  if (!depth || depth == UINT64_MAX) return 0;
+  const int lg = msb64(depth + 1) + 2;                    /* FD_TCACHE_SPARSE_DEFAULT = 2 */
+  if (lg > 63) return 0;
+  return 1ULL << lg;
+}
+
+uint64_t fdt_tcache_footprint(uint64_t depth, uint64_t map_cnt) {
+  if (!map_cnt) map_cnt = fdt_tcache_map_cnt_default(depth);
+  if (!depth || !map_cnt || (map_cnt & (map_cnt - 1)) || map_cnt < depth + 2) return 0;
+  uint64_t words = 4 + depth;                              /* overflow guards as fd_tcache.c:15-19 */
+  if (words < depth) return 0;
+  words += map_cnt;
+  if (words < map_cnt || words > UINT64_MAX / 8) return 0;
+  const uint64_t bytes = words * 8, fp = (bytes + 127) & ~127ULL;
+  return fp < bytes ? 0 : fp;
+}
+
+void *fdt_tcache_new(void *mem, uint64_t depth, uint64_t map_cnt) {
+  if (!map_cnt) map_cnt = fdt_tcache_map_cnt_default(depth);
+  if (!mem || !fdt_tcache_footprint(depth, map_cnt)) return nullptr;
+  uint64_t *h = (uint64_t *)mem;
+  h[0] = TCACHE_MAGIC; h[1] = depth; h[2] = map_cnt; h[3] = 0;
+  fdt_tcache_reset(mem);
+  return mem;
+}
+
+void fdt_tcache_reset(void *tc) {
+  tcache_view v{(uint64_t *)tc};
+  std::memset(v.ring(), 0, v.depth() * 8);
+  std::memset(v.map(), 0, v.map_cnt() * 8);
+  v.oldest() = 0;
+}
+
+int fdt_tcache_query(const void *tc, uint64_t tag) {
+  tcache_view v{(uint64_t *)tc};
+  uint64_t slot;
+  return map_find(v.map(), v.map_cnt(), tag, slot) ? 1 : 0;
+}
+
+/* FD_TCACHE_INSERT (fd_tcache.h:373-404): not LRU -- a duplicate leaves
+   the cache untouched; a new tag takes the oldest ring slot and the
+   evicted tag leaves the map. */
+int fdt_tcache_insert(void *tc, uint64_t tag) {
+  tcache_view v{(uint64_t *)tc};
+  uint64_t slot;
+  if (map_find(v.map(), v.map_cnt(), tag, slot)) return 1;
+  v.map()[slot] = tag;
+  uint64_t &old = v.oldest();
+  const uint64_t evict = v.ring()[old];
+  v.ring()[old] = tag;
+  old = (old + 1 >= v.depth()) ? 0 : old + 1;
+  map_remove(v.map(), v.map_cnt(), evict);
+  return 0;
+}
+
+/* -------------------------------------------------------------- hash */
+
+/* xxhash-r39 over 64-bit lanes (fd_hash.c:12-73). */
+namespace {
+constexpr uint64_t P1 = 11400714785074694791ULL, P2 = 14029467366897019727ULL, P3 = 1609587929392839161ULL,
+                   P4 = 9650029242287828579ULL, P5 = 2870177450012600261ULL;
+inline uint64_t rotl(uint64_t x, int r) { return (x << r) | (x >> (64 - r)); }
+inline uint64_t rd64(const uint8_t *p) { uint64_t v; std::memcpy(&v, p, 8); return v; }
+inline uint32_t rd32(const uint8_t *p) { uint32_t v; std::memcpy(&v, p, 4); return v; }
+inline uint64_t lane_round(uint64_t acc, uint64_t in) { return rotl(acc + in * P2, 31) * P1; }
+inline uint64_t merge(uint64_t h, uint64_t acc) { return (h ^ lane_round(0, acc)) * P1 + P4; }
+}  // namespace
+
+uint64_t fdt_hash(uint64_t seed, const void *buf, uint64_t sz) {
+  const uint8_t *p = (const uint8_t *)buf, *end = p + sz;
+  uint64_t h;
+  if (sz >= 32) {
+    uint64_t a = seed + P1 + P2, b = seed + P2, c = seed, d = seed - P1;
+    do {
+      a = lane_round(a, rd64(p)); b = lane_round(b, rd64(p + 8));
+      c = lane_round(c, rd64(p + 16)); d = lane_round(d, rd64(p + 24));
+      p += 32;
+    } while (p + 32 <= end);
+    h = rotl(a, 1) + rotl(b, 7) + rotl(c, 12) + rotl(d, 18);
+    h = merge(h, a); h = merge(h, b); h = merge(h, c); h = merge(h, d);
+  } else {
+    h = seed + P5;
+  }
+  h += sz;
+  for (; p + 8 <= end; p += 8) h = rotl(h ^ lane_round(0, rd64(p)), 27) * P1 + P4;
+  if (p + 4 <= end) { h = rotl(h ^ ((uint64_t)rd32(p) * P1), 23) * P2 + P3; p += 4; }
+  for (; p < end; p++) h = rotl(h ^ ((uint64_t)*p * P5), 11) * P1;
+  h ^= h >> 33; h *= P2; h ^= h >> 29; h *= P3; h ^= h >> 32;
+  return h;
+}
+
+/* --------------------------------------------------------------- txn */
+
+uint64_t fdt_txn_footprint(uint64_t instr_cnt, uint64_t lut_cnt) {
+  return sizeof(fdt_txn_t) + instr_cnt * sizeof(fdt_txn_instr_t) + lut_cnt * sizeof(fdt_txn_acct_addr_lut_t);
+}
+
+}  // extern "C"
+
+static_assert(sizeof(fdt_frag_meta_t) == 32, "fd_frag_meta_t is 32 B");
+static_assert(sizeof(fdt_txn_t) == 20, "fd_txn_t header is 20 B");
+static_assert(sizeof(fdt_txn_instr_t) == 10, "fd_txn_instr_t is 10 B");
+static_assert(sizeof(fdt_txn_acct_addr_lut_t) == 8, "fd_txn_acct_addr_lut_t is 8 B");
+
+namespace {
+
+/* Failure reasons recorded in the counters' ring (the reference records
+   the source line of the failed check; any non-zero token serves). */
+enum ParseFail : uint64_t {
+  PF_MTU = 1, PF_SHORT, PF_SIG_CNT, PF_VERSION, PF_HDR_SIG_CNT, PF_RO_SIGNED, PF_CU16, PF_ACCT_CNT,
+  PF_ACCT_SIGNERS, PF_INSTR_CNT, PF_NO_PROGRAM_ACCT, PF_PROGRAM_ID, PF_LUT_CNT, PF_LUT_WRITABLE, PF_LUT_READONLY,
+  PF_LUT_EMPTY, PF_TRAILING, PF_TOTAL_ACCTS, PF_ACCT_IDX
+};
+
+/* Bounds-checked reader over an untrusted payload (fd_txn_parse.c:12-75:
+   check that n bytes remain before every read; compact-u16 must be
+   minimally encoded and fit 16 bits). */
+struct Reader {
+  const uint8_t *p;
+  uint64_t sz, i = 0;
+  uint64_t fail = 0;
+  bool need(uint64_t n, uint64_t why = PF_SHORT) {
+    if (fail) return false;
+    if (n > sz - i) { fail = why; return false; }
+    return true;
+  }
+  bool u8(uint8_t &v) { if (!need(1)) return false; v = p[i++]; return true; }
+  bool skip(uint64_t n) { if (!need(n)) return false; i += n; return true; }
+  /* fd_compact_u16.h:60-75 */
+  bool cu16(uint16_t &v) {
+    if (fail) return false;
+    const uint64_t avail = sz - i;
+    const uint8_t *b = p + i;
+    if (avail >= 1 && !(b[0] & 0x80)) { v = b[0]; i += 1; return true; }
+    if (avail >= 2 && !(b[1] & 0x80)) {
+      if (!b[1]) { fail = PF_CU16; return false; }
+      v = (uint16_t)((b[0] & 0x7f) | (b[1] << 7)); i += 2; return true;
+    }
+    if (avail >= 3 && !(b[2] & 0xfc)) {
+      if (!b[2]) { fail = PF_CU16; return false; }
+      v = (uint16_t)((b[0] & 0x7f) | ((b[1] & 0x7f) << 7) | (b[2] << 14)); i += 3; return true;
+    }
+    fail = PF_CU16;
+    return false;
+  }
+  bool check(bool ok, uint64_t why) { if (!fail && !ok) fail = why; return !fail; }
+};
+
+}  // namespace
+
+extern "C" uint64_t fdt_txn_parse(const uint8_t *payload, uint64_t payload_sz, void *out_buf,
+                                  fdt_txn_parse_counters_t *counters) {
+  Reader r{payload, payload_sz};
+  fdt_txn_t *t = (fdt_txn_t *)out_buf;
+  auto bail = [&]() -> uint64_t {
+    if (counters) counters->failure_ring[counters->failure_cnt++ % 32] = r.fail ? r.fail : PF_SHORT;
+    return 0;
+  };
+  if (!r.check(payload_sz <= FDT_TXN_MTU, PF_MTU)) return bail();
+
+  /* signatures: count (u8 == compact-u16 below 128), at least one signer */
+  uint8_t sig_cnt;
+  if (!r.u8(sig_cnt) || !r.check(sig_cnt >= 1 && sig_cnt <= FDT_TXN_SIG_MAX, PF_SIG_CNT)) return bail();
+  const uint64_t sig_off = r.i;
+  if (!r.skip(64ULL * sig_cnt)) return bail();
+
+  /* message header: optional version prefix, then the signer count again */
+  const uint64_t msg_off = r.i;
+  uint8_t b0;
+  if (!r.u8(b0)) return bail();
+  uint8_t version;
+  if (b0 & 0x80) {
+    version = b0 & 0x7f;
+    uint8_t n;
+    if (!r.check(version == FDT_TXN_V0, PF_VERSION) || !r.u8(n) || !r.check(n == sig_cnt, PF_HDR_SIG_CNT))
+      return bail();
+  } else {
+    version = FDT_TXN_VLEGACY;
+    if (!r.check(b0 == sig_cnt, PF_HDR_SIG_CNT)) return bail();
+  }
+  uint8_t ro_signed, ro_unsigned;
+  if (!r.u8(ro_signed) || !r.check(ro_signed < sig_cnt, PF_RO_SIGNED) || !r.u8(ro_unsigned)) return bail();
+
+  /* account addresses and the recent blockhash */
+  uint16_t acct_cnt;
+  if (!r.cu16(acct_cnt)) return bail();
+  if (!r.check(sig_cnt <= acct_cnt && acct_cnt <= FDT_TXN_ACCT_ADDR_MAX, PF_ACCT_CNT) ||
+      !r.check((uint64_t)sig_cnt + ro_unsigned <= acct_cnt, PF_ACCT_SIGNERS))
+    return bail();
+  const uint64_t acct_off = r.i;
+  if (!r.skip(32ULL * acct_cnt)) return bail();
+  const uint64_t blockhash_off = r.i;
+  if (!r.skip(32)) return bail();
+
+  /* instructions: each at least 3 bytes (program id, two empty lists) */
+  uint16_t instr_cnt;
+  if (!r.cu16(instr_cnt) || !r.check(instr_cnt <= FDT_TXN_INSTR_MAX, PF_INSTR_CNT) || !r.need(3ULL * instr_cnt) ||
+      !r.check(acct_cnt > (instr_cnt ? 1 : 0), PF_NO_PROGRAM_ACCT))
+    return bail();
+  if (t) {
+    t->transaction_version = version;
+    t->signature_cnt = sig_cnt;
+    t->signature_off = (uint16_t)sig_off;
+    t->message_off = (uint16_t)msg_off;
+    t->readonly_signed_cnt = ro_signed;
+    t->readonly_unsigned_cnt = ro_unsigned;
+    t->acct_addr_cnt = acct_cnt;
+    t->acct_addr_off = (uint16_t)acct_off;
+    t->recent_blockhash_off = (uint16_t)blockhash_off;
+    t->instr_cnt = instr_cnt;
+  }
+  uint8_t max_acct = 0;
+  for (uint16_t j = 0; j < instr_cnt; j++) {
+    uint8_t program_id;
+    uint16_t n_acct, data_sz;
+    if (!r.need(3) || !r.u8(program_id) || !r.cu16(n_acct) || !r.need(n_acct)) return bail();
+    const uint64_t a_off = r.i;
+    for (uint16_t k = 0; k < n_acct; k++) max_acct = payload[a_off + k] > max_acct ? payload[a_off + k] : max_acct;
+    r.i += n_acct;
+    if (!r.cu16(data_sz) || !r.need(data_sz)) return bail();
+    const uint64_t d_off = r.i;
+    r.i += data_sz;
+    /* the program is neither the fee payer nor outside the static keys */
+    if (!r.check(program_id > 0 && program_id < acct_cnt, PF_PROGRAM_ID)) return bail();
+    if (t) {
+      fdt_txn_instr_t &ins = t->instr[j];
+      ins.program_id = program_id;
+      ins._padding_reserved_1 = 0;
+      ins.acct_cnt = n_acct;
+      ins.data_sz = data_sz;
+      ins.acct_off = (uint16_t)a_off;
+      ins.data_off = (uint16_t)d_off;
+    }
+  }
+
+  /* v0 address lookup tables: each >= 34 bytes (key + two lists) */
+  uint16_t lut_cnt = 0;
+  uint64_t adtl_w = 0, adtl = 0;
+  fdt_txn_acct_addr_lut_t *luts = t ? (fdt_txn_acct_addr_lut_t *)(t->instr + instr_cnt) : nullptr;
+  if (version == FDT_TXN_V0) {
+    if (!r.cu16(lut_cnt) || !r.check(lut_cnt <= FDT_TXN_ADDR_TABLE_LOOKUP_MAX, PF_LUT_CNT) ||
+        !r.need(34ULL * lut_cnt))
+      return bail();
+    for (uint16_t j = 0; j < lut_cnt; j++) {
+      uint16_t nw, nr;
+      const uint64_t addr_off = r.i;
+      if (!r.skip(32) || !r.cu16(nw) || !r.need(nw)) return bail();
+      const uint64_t w_off = r.i;
+      r.i += nw;
+      if (!r.cu16(nr) || !r.need(nr)) return bail();
+      const uint64_t ro_off = r.i;
+      r.i += nr;
+      if (!r.check(nw <= FDT_TXN_ACCT_ADDR_MAX - acct_cnt, PF_LUT_WRITABLE) ||
+          !r.check(nr <= FDT_TXN_ACCT_ADDR_MAX - acct_cnt, PF_LUT_READONLY) ||
+          !r.check(nw + nr >= 1, PF_LUT_EMPTY))
+        return bail();
+      if (luts) {
+        luts[j].addr_off = (uint16_t)addr_off;
+        luts[j].writable_cnt = (uint8_t)nw;
+        luts[j].readonly_cnt = (uint8_t)nr;
+        luts[j].writable_off = (uint16_t)w_off;
+        luts[j].readonly_off = (uint16_t)ro_off;
+      }
+      adtl_w += nw;
+      adtl += (uint64_t)nw + nr;
+    }
+  }
+  if (!r.check(r.i == payload_sz, PF_TRAILING) ||
+      !r.check(acct_cnt + adtl <= FDT_TXN_ACCT_ADDR_MAX, PF_TOTAL_ACCTS) ||
+      !r.check(max_acct < acct_cnt + adtl, PF_ACCT_IDX))
+    return bail();
+  if (t) {
+    t->addr_table_lookup_cnt = (uint8_t)lut_cnt;
+    t->addr_table_adtl_writable_cnt = (uint8_t)adtl_w;
+    t->addr_table_adtl_cnt = (uint8_t)adtl;
+    t->_padding_reserved_1 = 0;
+  }
+  if (counters) counters->success_cnt++;
+  return fdt_txn_footprint(instr_cnt, lut_cnt);
+}

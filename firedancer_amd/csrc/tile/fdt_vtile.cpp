@@ -1,0 +1,545 @@
+/* fdt_vtile.cpp -- the verify tile around the GPU engine, the multi-GPU
+   dispatcher, the dedup tile and a line-rate frag producer
+   (include/fd_verify_tile.h).
+
+   Verify tile (src/app/fdctl/run/tiles/fd_verify.c:36-148 and
+   fd_verify.h:45-89 restated for batched, asynchronous verification):
+
+     ingest   FD_MCACHE_WAIT-style polls of the in mcache; a frag outside
+              this tile's round-robin share is skipped (fd_verify.c:46); the
+              payload is copied into the open batch, the line re-checked for
+              overrun (fd_mux.c:641-647), then fd_txn_parse'd into the
+              batch's trailer area; parse failures are filtered
+              (fd_verify.c:117-121).
+     verify   the batch's per-transaction descriptors {msg, sigs, pubkeys,
+              sig_cnt} (fd_verify.h:53-61) go to the verifier as one
+              fd_ed25519_verify_batch_single_msg job per txn; up to
+              inflight_max batches are outstanding at once.
+     resolve  strictly in ingest order, one txn at a time: tag =
+              fd_hash(seed, sig0, 64); tcache hit -> DEDUP; verify code != 0
+              -> FAILED; else tcache insert and publish
+              [payload][pad][fd_txn_t][u16 payload_sz] with sig = tag
+              (fd_verify.c:93-147).  Because every earlier txn is resolved
+              first, the tcache sees exactly the insert sequence of the
+              reference's one-frag-at-a-time loop, so each txn's outcome is
+              identical; duplicates are still sent to the GPU (harmless
+              extra work) since whether they are duplicates is only known at
+              resolution.
+   Out-link flow control: with out_fseq set, publishing stops while the
+   consumer is a full mcache depth behind (the mux credit check,
+   fd_mux.c:548). */
+#include <time.h>
+
+#include <algorithm>
+#include <atomic>
+#include <cstdlib>
+#include <cstring>
+#include <deque>
+#include <new>
+#include <thread>
+#include <vector>
+
+#include "../../../include/fd_verify_tile.h"
+
+namespace {
+
+inline uint64_t now_ns() {
+  timespec ts;
+  clock_gettime(CLOCK_MONOTONIC, &ts);
+  return (uint64_t)ts.tv_sec * 1000000000ull + (uint64_t)ts.tv_nsec;
+}
+
+inline uint64_t align2(uint64_t x) { return (x + 1) & ~1ull; }
+
+}  // namespace
+
+/* ----------------------------------------------------------- dispatch */
+
+struct fdgpu_dispatch {
+  std::vector<fdgpu_engine_t *> eng;
+  uint32_t next = 0;
+};
+
+namespace {
+
+/* ticket = engine_ticket * n + engine index */
+int64_t dispatch_submit(void *ctx, const uint8_t *arena, uint64_t arena_sz, const fdgpu_txn_t *txns, uint64_t n_txn) {
+  auto *d = (fdgpu_dispatch *)ctx;
+  const uint32_t n = (uint32_t)d->eng.size();
+  for (uint32_t k = 0; k < n; k++) {
+    const uint32_t idx = (d->next + k) % n;
+    const int64_t t = fdgpu_submit(d->eng[idx], arena, arena_sz, txns, n_txn);
+    if (t == FDGPU_ERR_FULL) continue;
+    if (t < 0) return t;
+    d->next = (idx + 1) % n;
+    return t * n + idx;
+  }
+  return FDGPU_ERR_FULL;
+}
+
+int dispatch_poll(void *ctx, int64_t ticket, int8_t *codes, int blocking) {
+  auto *d = (fdgpu_dispatch *)ctx;
+  const int64_t n = (int64_t)d->eng.size();
+  if (ticket < 0) return FDGPU_ERR_TICKET;
+  return fdgpu_poll(d->eng[ticket % n], ticket / n, codes, blocking);
+}
+
+}  // namespace
+
+extern "C" {
+
+fdgpu_dispatch_t *fdgpu_dispatch_new(fdgpu_engine_t *const *engines, uint32_t engine_cnt) {
+  if (!engines || !engine_cnt) return nullptr;
+  auto *d = new (std::nothrow) fdgpu_dispatch;
+  if (!d) return nullptr;
+  d->eng.assign(engines, engines + engine_cnt);
+  for (auto *e : d->eng) if (!e) { delete d; return nullptr; }
+  return d;
+}
+
+void fdgpu_dispatch_delete(fdgpu_dispatch_t *d) { delete d; }
+
+fdgpu_verifier_t fdgpu_dispatch_verifier(fdgpu_dispatch_t *d) {
+  fdgpu_verifier_t v;
+  v.ctx = d;
+  v.submit = dispatch_submit;
+  v.poll = dispatch_poll;
+  return v;
+}
+
+}  // extern "C"
+
+/* -------------------------------------------------------- verify tile */
+
+namespace {
+
+struct Item {
+  uint64_t seq;
+  uint32_t pay_off;     /* payload offset in the batch arena */
+  uint16_t pay_sz;
+  uint16_t txn_sz;      /* parsed fd_txn_t footprint */
+  uint32_t txn_off;     /* in the batch trailer area */
+  uint32_t tsorig;
+};
+
+struct Batch {
+  std::vector<uint8_t> arena;       /* payload copies, back to back */
+  std::vector<uint8_t> trailer;     /* parsed fd_txn_t of each item */
+  std::vector<fdgpu_txn_t> txns;    /* one per item */
+  std::vector<Item> items;
+  std::vector<int8_t> codes;
+  uint64_t arena_used = 0, trailer_used = 0;
+  int64_t ticket = -1;
+  bool done = false;
+  size_t next = 0;                  /* next item to resolve */
+  uint64_t t_first = 0;
+
+  void reset() {
+    arena_used = trailer_used = 0;
+    txns.clear(); items.clear();
+    ticket = -1; done = false; next = 0; t_first = 0;
+  }
+};
+
+}  // namespace
+
+struct fdgpu_vtile {
+  fdgpu_vtile_cfg_t cfg{};
+  fdgpu_verifier_t ver{};
+  std::vector<uint64_t> tcache_mem;
+  void *tcache = nullptr;
+  uint64_t rx_seq = 0, out_seq = 0, out_chunk = 0;
+  std::vector<Batch *> pool;         /* free batches */
+  std::deque<Batch *> inflight;      /* submitted, resolved in order */
+  Batch *open = nullptr;             /* being filled */
+  std::vector<Batch> storage;
+  fdgpu_vtile_stats_t st{};
+  std::vector<uint64_t> lat;
+  uint64_t log_max = 0;
+  std::vector<uint64_t> log_seq;
+  std::vector<int8_t> log_code;
+
+  void log(uint64_t seq, int code) {
+    if (log_seq.size() < log_max) { log_seq.push_back(seq); log_code.push_back((int8_t)code); }
+  }
+
+  int64_t credits() const {
+    if (!cfg.out_fseq) return INT64_MAX;
+    const uint64_t fseq = __atomic_load_n(cfg.out_fseq, __ATOMIC_ACQUIRE);
+    return (int64_t)cfg.out_depth - (int64_t)(out_seq - fseq);
+  }
+
+  /* publish one verified txn downstream (fd_verify.c:93-147) */
+  void publish(const Batch &b, const Item &it, uint64_t tag) {
+    uint8_t *dst = cfg.out_base + (out_chunk << FDT_CHUNK_LG_SZ);
+    std::memcpy(dst, b.arena.data() + it.pay_off, it.pay_sz);
+    const uint64_t toff = align2(it.pay_sz);
+    if (toff != it.pay_sz) dst[it.pay_sz] = 0;
+    std::memcpy(dst + toff, b.trailer.data() + it.txn_off, it.txn_sz);
+    const uint16_t psz = it.pay_sz;
+    std::memcpy(dst + toff + it.txn_sz, &psz, 2);
+    const uint64_t new_sz = toff + it.txn_sz + 2;
+    fdt_mcache_publish(cfg.out_mcache, cfg.out_depth, out_seq, tag, out_chunk, new_sz, 0, it.tsorig,
+                       (uint32_t)now_ns());
+    out_seq++;
+    out_chunk = fdt_dcache_compact_next(out_chunk, new_sz, cfg.out_chunk0, cfg.out_wmark);
+    st.published++;
+  }
+
+  /* resolve completed batches in order; returns txns resolved, < 0 on error */
+  int64_t resolve() {
+    int64_t n = 0;
+    while (!inflight.empty()) {
+      Batch *b = inflight.front();
+      if (!b->done) {
+        const int rc = ver.poll(ver.ctx, b->ticket, b->codes.data(), 0);
+        if (rc == FDGPU_PENDING) break;
+        if (rc != FDGPU_OK) return rc;
+        b->done = true;
+      }
+      while (b->next < b->items.size()) {
+        if (credits() <= 0) { st.backpressure++; return n; }
+        const Item &it = b->items[b->next];
+        const uint64_t tag = fdt_hash(cfg.hashmap_seed, b->arena.data() + it.pay_off +
+                                      ((const fdt_txn_t *)(b->trailer.data() + it.txn_off))->signature_off, 64);
+        int outcome;
+        if (fdt_tcache_query(tcache, tag)) outcome = FD_TXN_VERIFY_DEDUP;
+        else if (b->codes[b->next] != FD_ED25519_SUCCESS) outcome = FD_TXN_VERIFY_FAILED;
+        else outcome = fdt_tcache_insert(tcache, tag) ? FD_TXN_VERIFY_DEDUP : FD_TXN_VERIFY_SUCCESS;
+        if (outcome == FD_TXN_VERIFY_SUCCESS) publish(*b, it, tag);
+        else if (outcome == FD_TXN_VERIFY_DEDUP) st.dedup++;
+        else st.verify_failed++;
+        log(it.seq, outcome);
+        b->next++;
+        n++;
+      }
+      if (lat.size() < (1u << 22) && !b->items.empty()) lat.push_back(now_ns() - b->t_first);
+      inflight.pop_front();
+      b->reset();
+      pool.push_back(b);
+    }
+    return n;
+  }
+
+  /* ingest available frags into the open batch (stops when it is full) */
+  void ingest() {
+    if (!open) {
+      if (pool.empty()) return;
+      open = pool.back(); pool.pop_back();
+    }
+    Batch &b = *open;
+    while (b.items.size() < cfg.batch_txn_max) {
+      fdt_frag_meta_t m;
+      uint64_t found;
+      const int rc = fdt_mcache_poll(cfg.in_mcache, cfg.in_depth, rx_seq, &m, &found);
+      if (rc == 0) break;
+      if (rc < 0) {                                     /* overrun: skip to the producer */
+        for (uint64_t s = rx_seq; s != found; s++) log(s, FDGPU_VTILE_LOG_LOST);
+        st.overrun += found - rx_seq;
+        rx_seq = found;
+        continue;
+      }
+      const uint64_t seq = rx_seq++;
+      st.in_frags++;
+      if (cfg.round_robin_cnt > 1 && seq % cfg.round_robin_cnt != cfg.round_robin_idx) {
+        st.filtered_rr++; log(seq, FDGPU_VTILE_LOG_FILTERED); continue;
+      }
+      if (m.chunk < cfg.in_chunk0 || m.chunk > cfg.in_wmark || m.sz > FDT_TPU_MTU) {
+        st.corrupt++; log(seq, FDGPU_VTILE_LOG_LOST); continue;
+      }
+      uint8_t *pay = b.arena.data() + b.arena_used;
+      std::memcpy(pay, cfg.in_base + ((uint64_t)m.chunk << FDT_CHUNK_LG_SZ), m.sz);
+      if (fdt_mcache_query(cfg.in_mcache, cfg.in_depth, seq) != seq) {   /* overwritten while copying */
+        st.overrun++; log(seq, FDGPU_VTILE_LOG_LOST); continue;
+      }
+      uint8_t *txn = b.trailer.data() + b.trailer_used;
+      const uint64_t tsz = fdt_txn_parse(pay, m.sz, txn, nullptr);
+      if (!tsz) { st.parse_fail++; log(seq, FDGPU_VTILE_LOG_PARSE_FAIL); continue; }
+      const fdt_txn_t *t = (const fdt_txn_t *)txn;
+      fdgpu_txn_t d;
+      d.sig_off = (uint32_t)(b.arena_used + t->signature_off);
+      d.pub_off = (uint32_t)(b.arena_used + t->acct_addr_off);
+      d.msg_off = (uint32_t)(b.arena_used + t->message_off);
+      d.msg_sz = (uint32_t)(m.sz - t->message_off);
+      d.sig_cnt = t->signature_cnt;
+      if (b.items.empty()) b.t_first = now_ns();
+      b.items.push_back(Item{seq, (uint32_t)b.arena_used, m.sz, (uint16_t)tsz, (uint32_t)b.trailer_used, m.tsorig});
+      b.txns.push_back(d);
+      b.arena_used += m.sz;
+      b.trailer_used += (tsz + 7) & ~7ull;
+      st.sigs += t->signature_cnt;
+    }
+  }
+
+  /* submit the open batch when full or when its first frag has waited long enough */
+  int submit(bool force) {
+    if (!open || open->items.empty()) return 0;
+    const bool full = open->items.size() >= cfg.batch_txn_max;
+    if (!full && !force && now_ns() - open->t_first < cfg.batch_wait_ns) return 0;
+    if (inflight.size() >= cfg.inflight_max) return 0;
+    const int64_t t = ver.submit(ver.ctx, open->arena.data(), open->arena_used, open->txns.data(),
+                                 open->txns.size());
+    if (t == FDGPU_ERR_FULL) return 0;
+    if (t < 0) return (int)t;
+    open->ticket = t;
+    inflight.push_back(open);
+    open = nullptr;
+    st.batches++;
+    return 1;
+  }
+};
+
+extern "C" {
+
+fdgpu_vtile_t *fdgpu_vtile_new(const fdgpu_vtile_cfg_t *cfg, fdgpu_verifier_t ver) {
+  if (!cfg || !ver.submit || !ver.poll || !cfg->in_mcache || !cfg->out_mcache || !cfg->in_base || !cfg->out_base)
+    return nullptr;
+  if (!cfg->in_depth || (cfg->in_depth & (cfg->in_depth - 1)) || !cfg->out_depth ||
+      (cfg->out_depth & (cfg->out_depth - 1)) || !cfg->batch_txn_max || cfg->out_wmark < cfg->out_chunk0)
+    return nullptr;
+  auto *t = new (std::nothrow) fdgpu_vtile;
+  if (!t) return nullptr;
+  t->cfg = *cfg;
+  if (!t->cfg.round_robin_cnt) t->cfg.round_robin_cnt = 1;
+  if (!t->cfg.inflight_max) t->cfg.inflight_max = 2;
+  if (!t->cfg.tcache_depth) t->cfg.tcache_depth = FDT_VERIFY_TCACHE_DEPTH;
+  if (!cfg->tcache_depth && !t->cfg.tcache_map_cnt) t->cfg.tcache_map_cnt = FDT_VERIFY_TCACHE_MAP_CNT;
+  const uint64_t fp = fdt_tcache_footprint(t->cfg.tcache_depth, t->cfg.tcache_map_cnt);
+  if (!fp) { delete t; return nullptr; }
+  t->tcache_mem.assign(fp / 8, 0);
+  t->tcache = fdt_tcache_new(t->tcache_mem.data(), t->cfg.tcache_depth, t->cfg.tcache_map_cnt);
+  t->ver = ver;
+  t->rx_seq = cfg->in_seq0;
+  t->out_seq = cfg->out_seq0;
+  t->out_chunk = cfg->out_chunk0;
+  const uint32_t nb = t->cfg.inflight_max + 1;
+  t->storage.resize(nb);
+  for (auto &b : t->storage) {
+    b.arena.resize((size_t)t->cfg.batch_txn_max * FDT_TPU_MTU + 256);
+    b.trailer.resize((size_t)t->cfg.batch_txn_max * (FDT_TXN_MAX_SZ + 8));
+    b.codes.resize(t->cfg.batch_txn_max);
+    b.txns.reserve(t->cfg.batch_txn_max);
+    b.items.reserve(t->cfg.batch_txn_max);
+    t->pool.push_back(&b);
+  }
+  return t;
+}
+
+void fdgpu_vtile_delete(fdgpu_vtile_t *t) {
+  if (!t) return;
+  /* drain: the verifier may still write codes into in-flight batches */
+  for (Batch *b : t->inflight) if (!b->done) t->ver.poll(t->ver.ctx, b->ticket, b->codes.data(), 1);
+  delete t;
+}
+
+int64_t fdgpu_vtile_step(fdgpu_vtile_t *t) {
+  const int64_t n = t->resolve();
+  if (n < 0) return n;
+  t->ingest();
+  const int rc = t->submit(false);
+  if (rc < 0) return rc;
+  return n;
+}
+
+int fdgpu_vtile_flush(fdgpu_vtile_t *t) {
+  int rc = t->submit(true);
+  while (rc == 0 && t->open && !t->open->items.empty()) {   /* wait for a free in-flight slot */
+    const int64_t n = t->resolve();
+    if (n < 0) return (int)n;
+    rc = t->submit(true);
+  }
+  if (rc < 0) return rc;
+  while (!t->inflight.empty()) {
+    Batch *b = t->inflight.front();
+    if (!b->done) {
+      const int r = t->ver.poll(t->ver.ctx, b->ticket, b->codes.data(), 1);
+      if (r != FDGPU_OK) return r;
+      b->done = true;
+    }
+    const int64_t n = t->resolve();
+    if (n < 0) return (int)n;
+    if (!t->inflight.empty() && t->inflight.front() == b) return FDGPU_ERR_FULL;   /* out-link credits exhausted */
+  }
+  return 0;
+}
+
+int fdgpu_vtile_run(fdgpu_vtile_t *t, uint64_t in_frags, double timeout_s) {
+  const uint64_t t0 = now_ns(), lim = (uint64_t)(timeout_s * 1e9);
+  uint64_t idle = 0;
+  while (t->rx_seq - t->cfg.in_seq0 < in_frags) {
+    const uint64_t before = t->rx_seq;
+    const int64_t n = fdgpu_vtile_step(t);
+    if (n < 0) return (int)n;
+    if (t->rx_seq == before && n == 0) {
+      /* nothing new: push out a partial batch rather than wait */
+      if (++idle > 64) { const int rc = t->submit(true); if (rc < 0) return rc; idle = 0; }
+      if (now_ns() - t0 > lim) return FDGPU_ERR_FULL;
+    } else {
+      idle = 0;
+    }
+  }
+  return fdgpu_vtile_flush(t);
+}
+
+void fdgpu_vtile_stats(const fdgpu_vtile_t *t, fdgpu_vtile_stats_t *out) {
+  *out = t->st;
+  out->lat_cnt = t->lat.size();
+}
+
+uint64_t fdgpu_vtile_latencies(const fdgpu_vtile_t *t, uint64_t *out, uint64_t max) {
+  const uint64_t n = std::min<uint64_t>(max, t->lat.size());
+  std::memcpy(out, t->lat.data(), n * 8);
+  return n;
+}
+
+void *fdgpu_vtile_tcache(fdgpu_vtile_t *t) { return t->tcache; }
+
+void fdgpu_vtile_log_enable(fdgpu_vtile_t *t, uint64_t log_max) {
+  t->log_max = log_max;
+  t->log_seq.reserve(log_max);
+  t->log_code.reserve(log_max);
+}
+
+uint64_t fdgpu_vtile_log(const fdgpu_vtile_t *t, uint64_t *seqs, int8_t *codes, uint64_t max) {
+  const uint64_t n = std::min<uint64_t>(max, t->log_seq.size());
+  std::memcpy(seqs, t->log_seq.data(), n * 8);
+  std::memcpy(codes, t->log_code.data(), n);
+  return n;
+}
+
+}  // extern "C"
+
+/* --------------------------------------------------------- dedup tile */
+
+struct fdgpu_dtile {
+  fdgpu_dtile_cfg_t cfg{};
+  std::vector<uint64_t> tcache_mem;
+  void *tcache = nullptr;
+  uint64_t rx_seq[16] = {};
+  uint64_t out_seq = 0, out_chunk = 0;
+  uint32_t next_in = 0;
+  fdgpu_dtile_stats_t st{};
+};
+
+extern "C" {
+
+fdgpu_dtile_t *fdgpu_dtile_new(const fdgpu_dtile_cfg_t *cfg) {
+  if (!cfg || !cfg->in_cnt || cfg->in_cnt > 16 || !cfg->out_mcache || !cfg->out_base || !cfg->tcache_depth)
+    return nullptr;
+  auto *t = new (std::nothrow) fdgpu_dtile;
+  if (!t) return nullptr;
+  t->cfg = *cfg;
+  const uint64_t fp = fdt_tcache_footprint(cfg->tcache_depth, cfg->tcache_map_cnt);
+  if (!fp) { delete t; return nullptr; }
+  t->tcache_mem.assign(fp / 8, 0);
+  t->tcache = fdt_tcache_new(t->tcache_mem.data(), cfg->tcache_depth, cfg->tcache_map_cnt);
+  for (uint32_t i = 0; i < cfg->in_cnt; i++) t->rx_seq[i] = cfg->in_seq0[i];
+  t->out_seq = cfg->out_seq0;
+  t->out_chunk = cfg->out_chunk0;
+  return t;
+}
+
+void fdgpu_dtile_delete(fdgpu_dtile_t *t) { delete t; }
+
+/* One pass over the in links, at most one frag from each (the mux's
+   round-robin service order), fd_dedup.c:89-205. */
+int64_t fdgpu_dtile_step(fdgpu_dtile_t *t) {
+  const fdgpu_dtile_cfg_t &c = t->cfg;
+  int64_t n = 0;
+  for (uint32_t k = 0; k < c.in_cnt; k++) {
+    const uint32_t i = (t->next_in + k) % c.in_cnt;
+    fdt_frag_meta_t m;
+    uint64_t found;
+    const int rc = fdt_mcache_poll(c.in_mcache[i], c.in_depth[i], t->rx_seq[i], &m, &found);
+    if (rc == 0) continue;
+    if (rc < 0) { t->st.overrun += found - t->rx_seq[i]; t->rx_seq[i] = found; continue; }
+    const uint64_t seq = t->rx_seq[i]++;
+    t->st.in_frags++;
+    n++;
+    if (m.chunk < c.in_chunk0[i] || m.chunk > c.in_wmark[i] || m.sz > FDT_TPU_DCACHE_MTU) { t->st.corrupt++; continue; }
+    uint8_t *dst = c.out_base + (t->out_chunk << FDT_CHUNK_LG_SZ);
+    std::memcpy(dst, c.in_base[i] + ((uint64_t)m.chunk << FDT_CHUNK_LG_SZ), m.sz);
+    if (fdt_mcache_query(c.in_mcache[i], c.in_depth[i], seq) != seq) { t->st.overrun++; continue; }
+    uint64_t sz = m.sz;
+    const fdt_txn_t *txn;
+    if (i < c.unparsed_in_cnt) {
+      /* raw txn (gossip): parse into the trailer like the verify tile */
+      const uint64_t toff = align2(sz);
+      if (toff > FDT_TPU_DCACHE_MTU - FDT_TXN_MAX_SZ - 2) { t->st.parse_fail++; continue; }
+      const uint64_t tsz = fdt_txn_parse(dst, sz, dst + toff, nullptr);
+      if (!tsz) { t->st.parse_fail++; continue; }
+      const uint16_t psz = (uint16_t)sz;
+      std::memcpy(dst + toff + tsz, &psz, 2);
+      txn = (const fdt_txn_t *)(dst + toff);
+      sz = toff + tsz + 2;
+    } else {
+      if (sz < 2) { t->st.corrupt++; continue; }
+      uint16_t psz;
+      std::memcpy(&psz, dst + sz - 2, 2);
+      if (align2(psz) + sizeof(fdt_txn_t) + 2 > sz) { t->st.corrupt++; continue; }
+      txn = (const fdt_txn_t *)(dst + align2(psz));
+    }
+    if ((uint64_t)txn->signature_off + 64 > sz) { t->st.corrupt++; continue; }
+    const uint64_t tag = fdt_hash(c.hashmap_seed, dst + txn->signature_off, 64);
+    if (fdt_tcache_insert(t->tcache, tag)) { t->st.dup++; continue; }
+    fdt_mcache_publish(c.out_mcache, c.out_depth, t->out_seq, 0, t->out_chunk, sz, m.ctl, m.tsorig,
+                       (uint32_t)now_ns());
+    t->out_seq++;
+    t->out_chunk = fdt_dcache_compact_next(t->out_chunk, sz, c.out_chunk0, c.out_wmark);
+    t->st.published++;
+  }
+  t->next_in = (t->next_in + 1) % c.in_cnt;
+  return n;
+}
+
+void fdgpu_dtile_stats(const fdgpu_dtile_t *t, fdgpu_dtile_stats_t *out) { *out = t->st; }
+
+}  // extern "C"
+
+/* ------------------------------------------------------------ producer */
+
+struct fdgpu_producer {
+  std::thread th;
+  std::atomic<uint64_t> published{0};
+  double elapsed = 0;
+};
+
+extern "C" {
+
+fdgpu_producer_t *fdgpu_producer_start(fdt_frag_meta_t *mcache, uint64_t depth, uint64_t seq0, uint8_t *base,
+                                       uint64_t chunk0, uint64_t wmark, const uint8_t *arena, const uint64_t *off,
+                                       const uint32_t *sz, uint64_t cnt, double rate_tps) {
+  if (!mcache || !base || !arena || !off || !sz || !depth || (depth & (depth - 1))) return nullptr;
+  auto *p = new (std::nothrow) fdgpu_producer;
+  if (!p) return nullptr;
+  p->th = std::thread([=]() {
+    const uint64_t t0 = now_ns();
+    uint64_t chunk = chunk0;
+    const uint16_t ctl = (uint16_t)fdt_frag_meta_ctl(0, 1, 1, 0);
+    for (uint64_t i = 0; i < cnt; i++) {
+      if (rate_tps > 0) {
+        const uint64_t due = t0 + (uint64_t)((double)i * 1e9 / rate_tps);
+        while (now_ns() < due) { /* spin: sub-microsecond pacing */ }
+      }
+      const uint32_t n = std::min<uint32_t>(sz[i], (uint32_t)FDT_TPU_MTU);
+      std::memcpy(base + (chunk << FDT_CHUNK_LG_SZ), arena + off[i], n);
+      const uint32_t ts = (uint32_t)now_ns();
+      fdt_mcache_publish(mcache, depth, seq0 + i, 0, chunk, n, ctl, ts, ts);
+      chunk = fdt_dcache_compact_next(chunk, n, chunk0, wmark);
+      p->published.store(i + 1, std::memory_order_relaxed);
+    }
+    p->elapsed = (double)(now_ns() - t0) * 1e-9;
+  });
+  return p;
+}
+
+uint64_t fdgpu_producer_join(fdgpu_producer_t *p, double *elapsed_s) {
+  if (!p) return 0;
+  p->th.join();
+  const uint64_t n = p->published.load();
+  if (elapsed_s) *elapsed_s = p->elapsed;
+  delete p;
+  return n;
+}
+
+}  // extern "C"

@@ -1,0 +1,543 @@
+"""Python mirror of the verify-stage integration (libfd_verify_tile.so,
+include/fd_verify_tile.h): tango links (mcache + compact dcache), tcache,
+fd_hash, fd_txn_parse, the verify tile over the GPU engine(s), the dedup
+tile and a line-rate frag producer.
+
+Reference interfaces restated (names follow the reference):
+  fd_frag_meta_t / fd_mcache / fd_dcache   src/tango/fd_tango_base.h:146-203,
+                                           mcache/fd_mcache.h:299-322,574-601,
+                                           dcache/fd_dcache.h:198-269
+  fd_tcache                                src/tango/tcache/fd_tcache.h:237-404
+  fd_hash                                  src/util/fd_hash.c:12-73
+  fd_txn_t / fd_txn_parse                  src/ballet/txn/fd_txn.h:122-335,
+                                           fd_txn_parse.c:7-243
+  fd_txn_verify + verify tile              src/app/fdctl/run/tiles/fd_verify.h:45-89,
+                                           fd_verify.c:36-148
+  dedup tile                               src/app/fdctl/run/tiles/fd_dedup.c:89-205
+The library is required: there is no Python fallback for any of it.
+"""
+import ctypes
+import os
+
+import numpy as np
+
+from . import _lib
+from .ed25519 import TXN_DTYPE
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+TILE_LIB_PATH = os.environ.get("FDGPU_TILE_LIB") or os.path.join(_HERE, "libfd_verify_tile.so")
+TILE_HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "fd_verify_tile.h")
+
+CHUNK_SZ = 64
+TPU_MTU = 1232
+TXN_MAX_SZ = 852
+TPU_DCACHE_MTU = TPU_MTU + TXN_MAX_SZ + 2
+TXN_VLEGACY, TXN_V0 = 0xFF, 0x00
+VERIFY_SUCCESS, VERIFY_FAILED, VERIFY_DEDUP = 0, -1, -2
+LOG_PARSE_FAIL, LOG_FILTERED, LOG_LOST = 1, 2, 3
+VERIFY_TCACHE_DEPTH, VERIFY_TCACHE_MAP_CNT = 16, 64
+
+FRAG_META_DTYPE = np.dtype([("seq", "<u8"), ("sig", "<u8"), ("chunk", "<u4"), ("sz", "<u2"), ("ctl", "<u2"),
+                            ("tsorig", "<u4"), ("tspub", "<u4")])
+assert FRAG_META_DTYPE.itemsize == 32
+
+_TL = None
+c = ctypes
+vp = c.c_void_p
+
+
+class FragMeta(c.Structure):
+    _fields_ = [("seq", c.c_uint64), ("sig", c.c_uint64), ("chunk", c.c_uint32), ("sz", c.c_uint16),
+                ("ctl", c.c_uint16), ("tsorig", c.c_uint32), ("tspub", c.c_uint32)]
+
+
+class TxnInstr(c.Structure):
+    _fields_ = [("program_id", c.c_uint8), ("_padding_reserved_1", c.c_uint8), ("acct_cnt", c.c_uint16),
+                ("data_sz", c.c_uint16), ("acct_off", c.c_uint16), ("data_off", c.c_uint16)]
+
+
+class TxnLut(c.Structure):
+    _fields_ = [("addr_off", c.c_uint16), ("writable_cnt", c.c_uint8), ("readonly_cnt", c.c_uint8),
+                ("writable_off", c.c_uint16), ("readonly_off", c.c_uint16)]
+
+
+class TxnHdr(c.Structure):
+    _fields_ = [("transaction_version", c.c_uint8), ("signature_cnt", c.c_uint8), ("signature_off", c.c_uint16),
+                ("message_off", c.c_uint16), ("readonly_signed_cnt", c.c_uint8),
+                ("readonly_unsigned_cnt", c.c_uint8), ("acct_addr_cnt", c.c_uint16), ("acct_addr_off", c.c_uint16),
+                ("recent_blockhash_off", c.c_uint16), ("addr_table_lookup_cnt", c.c_uint8),
+                ("addr_table_adtl_writable_cnt", c.c_uint8), ("addr_table_adtl_cnt", c.c_uint8),
+                ("_padding_reserved_1", c.c_uint8), ("instr_cnt", c.c_uint16)]
+
+
+class ParseCounters(c.Structure):
+    _fields_ = [("success_cnt", c.c_uint64), ("failure_cnt", c.c_uint64), ("failure_ring", c.c_uint64 * 32)]
+
+
+SUBMIT_FN = c.CFUNCTYPE(c.c_int64, vp, vp, c.c_uint64, vp, c.c_uint64)
+POLL_FN = c.CFUNCTYPE(c.c_int, vp, c.c_int64, vp, c.c_int)
+
+
+class Verifier(c.Structure):
+    _fields_ = [("ctx", vp), ("submit", SUBMIT_FN), ("poll", POLL_FN)]
+
+
+class VTileCfg(c.Structure):
+    _fields_ = [("in_mcache", vp), ("in_depth", c.c_uint64), ("in_seq0", c.c_uint64), ("in_base", vp),
+                ("in_chunk0", c.c_uint64), ("in_wmark", c.c_uint64),
+                ("out_mcache", vp), ("out_depth", c.c_uint64), ("out_seq0", c.c_uint64), ("out_base", vp),
+                ("out_chunk0", c.c_uint64), ("out_wmark", c.c_uint64), ("out_fseq", vp),
+                ("round_robin_idx", c.c_uint64), ("round_robin_cnt", c.c_uint64), ("hashmap_seed", c.c_uint64),
+                ("tcache_depth", c.c_uint64), ("tcache_map_cnt", c.c_uint64), ("batch_txn_max", c.c_uint32),
+                ("inflight_max", c.c_uint32), ("batch_wait_ns", c.c_uint64)]
+
+
+class VTileStats(c.Structure):
+    _fields_ = [(n, c.c_uint64) for n in ("in_frags", "filtered_rr", "corrupt", "overrun", "parse_fail",
+                                          "verify_failed", "dedup", "published", "batches", "sigs",
+                                          "backpressure", "lat_cnt")]
+
+    def as_dict(self):
+        return {n: getattr(self, n) for n, _ in self._fields_}
+
+
+class DTileCfg(c.Structure):
+    _fields_ = [("in_cnt", c.c_uint32), ("in_mcache", vp * 16), ("in_depth", c.c_uint64 * 16),
+                ("in_seq0", c.c_uint64 * 16), ("in_base", vp * 16), ("in_chunk0", c.c_uint64 * 16),
+                ("in_wmark", c.c_uint64 * 16), ("unparsed_in_cnt", c.c_uint32),
+                ("out_mcache", vp), ("out_depth", c.c_uint64), ("out_seq0", c.c_uint64), ("out_base", vp),
+                ("out_chunk0", c.c_uint64), ("out_wmark", c.c_uint64), ("hashmap_seed", c.c_uint64),
+                ("tcache_depth", c.c_uint64), ("tcache_map_cnt", c.c_uint64)]
+
+
+class DTileStats(c.Structure):
+    _fields_ = [(n, c.c_uint64) for n in ("in_frags", "dup", "published", "overrun", "corrupt", "parse_fail")]
+
+    def as_dict(self):
+        return {n: getattr(self, n) for n, _ in self._fields_}
+
+
+def lib():
+    """Load libfd_verify_tile.so (and through it libfd_ed25519_gpu.so). Raises if absent."""
+    global _TL
+    if _TL is not None:
+        return _TL
+    if not os.path.exists(TILE_LIB_PATH):
+        raise RuntimeError(f"firedancer_amd: tile library not built: {TILE_LIB_PATH} "
+                           "(run `make -C firedancer_amd/csrc`)")
+    _lib.lib()      # the engine library first (the tile library links it)
+    L = ctypes.CDLL(TILE_LIB_PATH)
+    u64, i64 = c.c_uint64, c.c_int64
+    sig = {
+        "fdt_frag_meta_ctl": (u64, [u64, c.c_int, c.c_int, c.c_int]),
+        "fdt_mcache_init": (None, [vp, u64, u64]),
+        "fdt_mcache_publish": (None, [vp, u64, u64, u64, u64, u64, u64, u64, u64]),
+        "fdt_mcache_poll": (c.c_int, [vp, u64, u64, vp, c.POINTER(u64)]),
+        "fdt_mcache_query": (u64, [vp, u64, u64]),
+        "fdt_dcache_chunk_mtu": (u64, [u64]),
+        "fdt_dcache_data_sz": (u64, [u64, u64]),
+        "fdt_dcache_wmark": (u64, [u64, u64, u64]),
+        "fdt_dcache_compact_next": (u64, [u64, u64, u64, u64]),
+        "fdt_tcache_map_cnt_default": (u64, [u64]),
+        "fdt_tcache_footprint": (u64, [u64, u64]),
+        "fdt_tcache_new": (vp, [vp, u64, u64]),
+        "fdt_tcache_reset": (None, [vp]),
+        "fdt_tcache_query": (c.c_int, [vp, u64]),
+        "fdt_tcache_insert": (c.c_int, [vp, u64]),
+        "fdt_hash": (u64, [u64, vp, u64]),
+        "fdt_txn_footprint": (u64, [u64, u64]),
+        "fdt_txn_parse": (u64, [vp, u64, vp, c.POINTER(ParseCounters)]),
+        "fdgpu_dispatch_new": (vp, [c.POINTER(vp), c.c_uint32]),
+        "fdgpu_dispatch_delete": (None, [vp]),
+        "fdgpu_dispatch_verifier": (Verifier, [vp]),
+        "fdgpu_vtile_new": (vp, [c.POINTER(VTileCfg), Verifier]),
+        "fdgpu_vtile_delete": (None, [vp]),
+        "fdgpu_vtile_step": (i64, [vp]),
+        "fdgpu_vtile_run": (c.c_int, [vp, u64, c.c_double]),
+        "fdgpu_vtile_flush": (c.c_int, [vp]),
+        "fdgpu_vtile_stats": (None, [vp, c.POINTER(VTileStats)]),
+        "fdgpu_vtile_latencies": (u64, [vp, vp, u64]),
+        "fdgpu_vtile_tcache": (vp, [vp]),
+        "fdgpu_vtile_log_enable": (None, [vp, u64]),
+        "fdgpu_vtile_log": (u64, [vp, vp, vp, u64]),
+        "fdgpu_dtile_new": (vp, [c.POINTER(DTileCfg)]),
+        "fdgpu_dtile_delete": (None, [vp]),
+        "fdgpu_dtile_step": (i64, [vp]),
+        "fdgpu_dtile_stats": (None, [vp, c.POINTER(DTileStats)]),
+        "fdgpu_producer_start": (vp, [vp, u64, u64, vp, u64, u64, vp, vp, vp, u64, c.c_double]),
+        "fdgpu_producer_join": (u64, [vp, c.POINTER(c.c_double)]),
+    }
+    for name, (res, args) in sig.items():
+        f = getattr(L, name)
+        f.restype, f.argtypes = res, args
+    _TL = L
+    return L
+
+
+def header_functions():
+    import re
+    text = open(TILE_HEADER_PATH).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    names = re.findall(r"^[A-Za-z_][\w \t\*]*?\b(fd\w+)\s*\(", text, flags=re.M)
+    return sorted(set(n for n in names if not n.startswith("FD_")))
+
+
+def _aligned(nbytes, align):
+    buf = np.zeros(nbytes + align, dtype=np.uint8)
+    off = (-buf.ctypes.data) % align
+    return buf[off:off + nbytes]
+
+
+# ---------------------------------------------------------------- basics
+
+def fd_hash(seed, data):
+    data = bytes(data)
+    return lib().fdt_hash(seed & (2**64 - 1), data, len(data))
+
+
+def frag_meta_ctl(orig, som, eom, err):
+    return lib().fdt_frag_meta_ctl(orig, som, eom, err)
+
+
+def dcache_compact_next(chunk, sz, chunk0, wmark):
+    return lib().fdt_dcache_compact_next(chunk, sz, chunk0, wmark)
+
+
+class TCache:
+    """fd_tcache: ring of the last `depth` unique tags + linear-probed map."""
+
+    def __init__(self, depth, map_cnt=0):
+        L = lib()
+        fp = L.fdt_tcache_footprint(depth, map_cnt)
+        if not fp:
+            raise ValueError("bad tcache depth / map_cnt")
+        self._mem = _aligned(fp, 128)
+        self._p = L.fdt_tcache_new(self._mem.ctypes.data, depth, map_cnt)
+        self.depth = depth
+        self.map_cnt = int(self._mem[16:24].view("<u8")[0])
+
+    @classmethod
+    def attach(cls, ptr, owner):
+        self = cls.__new__(cls)
+        self._mem, self._p = owner, ptr
+        hdr = (c.c_uint64 * 4).from_address(ptr)
+        self.depth, self.map_cnt = hdr[1], hdr[2]
+        return self
+
+    def reset(self):
+        lib().fdt_tcache_reset(self._p)
+
+    def query(self, tag):
+        return bool(lib().fdt_tcache_query(self._p, tag))
+
+    def insert(self, tag):
+        """returns True if tag was a duplicate (tcache unchanged)"""
+        return bool(lib().fdt_tcache_insert(self._p, tag))
+
+    def words(self):
+        n = 4 + self.depth + self.map_cnt
+        return np.ctypeslib.as_array((c.c_uint64 * n).from_address(self._p)).copy()
+
+
+def txn_parse(payload, counters=None):
+    """fd_txn_parse: returns (footprint, raw fd_txn_t bytes) or (0, None)."""
+    payload = bytes(payload)
+    out = c.create_string_buffer(TXN_MAX_SZ + 16)
+    sz = lib().fdt_txn_parse(payload, len(payload), out, c.byref(counters) if counters is not None else None)
+    return (sz, out.raw[:sz]) if sz else (0, None)
+
+
+def txn_decode(raw):
+    """fd_txn_t bytes -> dict (header fields, instr list, address tables)."""
+    hdr = TxnHdr.from_buffer_copy(raw[:c.sizeof(TxnHdr)])
+    d = {n: getattr(hdr, n) for n, _ in TxnHdr._fields_}
+    off = c.sizeof(TxnHdr)
+    d["instr"] = []
+    for _ in range(hdr.instr_cnt):
+        ins = TxnInstr.from_buffer_copy(raw[off:off + 10])
+        d["instr"].append({n: getattr(ins, n) for n, _ in TxnInstr._fields_})
+        off += 10
+    d["luts"] = []
+    for _ in range(hdr.addr_table_lookup_cnt):
+        lut = TxnLut.from_buffer_copy(raw[off:off + 8])
+        d["luts"].append({n: getattr(lut, n) for n, _ in TxnLut._fields_})
+        off += 8
+    return d
+
+
+# ---------------------------------------------------------------- links
+
+class Link:
+    """One tango link: an mcache of `depth` frag metas and a compact dcache
+    sized for `depth` frags of up to `mtu` bytes (chunk 0 = dcache start)."""
+
+    def __init__(self, depth, mtu, seq0=0):
+        L = lib()
+        if depth & (depth - 1):
+            raise ValueError("depth must be a power of 2")
+        self.depth, self.mtu, self.seq0 = depth, mtu, seq0
+        self.mcache = _aligned(depth * 32, 128).view(FRAG_META_DTYPE)
+        data_sz = L.fdt_dcache_data_sz(mtu, depth)
+        self.dcache = _aligned(data_sz, 4096)
+        self.chunk0 = 0
+        self.chunk1 = data_sz // CHUNK_SZ
+        self.wmark = L.fdt_dcache_wmark(self.chunk0, self.chunk1, mtu)
+        self.fseq = np.zeros(1, dtype=np.uint64)
+        self.fseq[0] = seq0
+        L.fdt_mcache_init(self.mcache.ctypes.data, depth, seq0)
+        self._pub_seq, self._pub_chunk = seq0, 0
+
+    @property
+    def mcache_ptr(self):
+        return self.mcache.ctypes.data
+
+    @property
+    def base_ptr(self):
+        return self.dcache.ctypes.data
+
+    def publish(self, payload, sig=0, ctl=None):
+        """Producer side (single-threaded): payload into the dcache, meta into the mcache."""
+        L = lib()
+        payload = bytes(payload)
+        ch = self._pub_chunk
+        self.dcache[ch * CHUNK_SZ: ch * CHUNK_SZ + len(payload)] = np.frombuffer(payload, dtype=np.uint8)
+        ctl = frag_meta_ctl(0, 1, 1, 0) if ctl is None else ctl
+        L.fdt_mcache_publish(self.mcache_ptr, self.depth, self._pub_seq, sig, ch, len(payload), ctl, 0, 0)
+        self._pub_seq += 1
+        self._pub_chunk = L.fdt_dcache_compact_next(ch, len(payload), self.chunk0, self.wmark)
+        return self._pub_seq - 1
+
+    def poll(self, seq):
+        """Consumer side: (status, meta dict or None, seq_found)."""
+        m = FragMeta()
+        found = c.c_uint64()
+        rc = lib().fdt_mcache_poll(self.mcache_ptr, self.depth, seq, c.byref(m), c.byref(found))
+        meta = {n: getattr(m, n) for n, _ in FragMeta._fields_} if rc == 1 else None
+        return rc, meta, found.value
+
+    def payload(self, meta):
+        o = meta["chunk"] * CHUNK_SZ
+        return bytes(self.dcache[o:o + meta["sz"]])
+
+    def drain(self, seq=None, max_frags=1 << 30):
+        """Reads frags from `seq` (default seq0) until none is available: list of (meta, payload)."""
+        seq = self.seq0 if seq is None else seq
+        out = []
+        while len(out) < max_frags:
+            rc, meta, found = self.poll(seq)
+            if rc != 1:
+                break
+            out.append((meta, self.payload(meta)))
+            seq += 1
+        return out
+
+
+def split_verify_output(frag_payload):
+    """[payload][pad][fd_txn_t][u16 payload_sz] -> (payload, fd_txn_t bytes)."""
+    b = bytes(frag_payload)
+    psz = int.from_bytes(b[-2:], "little")
+    toff = (psz + 1) & ~1
+    return b[:psz], b[toff:-2]
+
+
+# -------------------------------------------------------------- verifiers
+
+class PyVerifier:
+    """A verifier backed by a Python callable fn(arena uint8[], txns TXN_DTYPE[]) -> int8 codes.
+    For tests of the tile logic without a GPU (the callable is the test's
+    checker); `lag` makes each batch report PENDING for that many polls."""
+
+    def __init__(self, fn, slots=2, lag=0):
+        self.fn, self.slots, self.lag = fn, slots, lag
+        self.results, self.polls, self.next = {}, {}, 0
+        self.batches = []
+
+        def submit(ctx, arena, arena_sz, txns, n):
+            if len(self.results) >= self.slots:
+                return -12                                    # FDGPU_ERR_FULL
+            a = np.ctypeslib.as_array((c.c_uint8 * max(arena_sz, 1)).from_address(arena))[:arena_sz].copy()
+            t = np.frombuffer((c.c_uint8 * (20 * n)).from_address(txns), dtype=TXN_DTYPE).copy() if n else \
+                np.zeros(0, dtype=TXN_DTYPE)
+            self.batches.append(len(t))
+            k = self.next
+            self.next += 1
+            self.results[k] = np.asarray(self.fn(a, t), dtype=np.int8)
+            self.polls[k] = 0
+            return k
+
+        def poll(ctx, ticket, codes, blocking):
+            if ticket not in self.results:
+                return -13
+            if not blocking and self.polls[ticket] < self.lag:
+                self.polls[ticket] += 1
+                return 1                                      # FDGPU_PENDING
+            r = self.results.pop(ticket)
+            self.polls.pop(ticket)
+            if len(r):
+                c.memmove(codes, r.ctypes.data, len(r))
+            return 0
+
+        self._submit, self._poll = SUBMIT_FN(submit), POLL_FN(poll)
+        self.struct = Verifier(None, self._submit, self._poll)
+
+
+class EngineVerifier:
+    """Round-robin over GPU engines (fdgpu_dispatch; one engine per GPU)."""
+
+    def __init__(self, engines):
+        L = lib()
+        self.engines = list(engines)
+        arr = (vp * len(self.engines))(*[e._h for e in self.engines])
+        self._d = L.fdgpu_dispatch_new(arr, len(self.engines))
+        if not self._d:
+            raise RuntimeError("fdgpu_dispatch_new failed")
+        self.struct = L.fdgpu_dispatch_verifier(self._d)
+
+    def close(self):
+        if self._d:
+            lib().fdgpu_dispatch_delete(self._d)
+            self._d = None
+
+
+# ------------------------------------------------------------------ tiles
+
+class VerifyTile:
+    """The verify tile (fd_verify.c) over a verifier (GPU engines in the product)."""
+
+    def __init__(self, in_link, out_link, verifier, hashmap_seed=0x5EEDF00D, batch_txn_max=4096, inflight_max=2,
+                 batch_wait_us=200, round_robin_idx=0, round_robin_cnt=1, tcache_depth=0, tcache_map_cnt=0,
+                 flow_control=False, log_max=0):
+        L = lib()
+        self.verifier, self.in_link, self.out_link = verifier, in_link, out_link
+        cfg = VTileCfg()
+        cfg.in_mcache, cfg.in_depth, cfg.in_seq0 = in_link.mcache_ptr, in_link.depth, in_link.seq0
+        cfg.in_base, cfg.in_chunk0, cfg.in_wmark = in_link.base_ptr, in_link.chunk0, in_link.wmark
+        cfg.out_mcache, cfg.out_depth, cfg.out_seq0 = out_link.mcache_ptr, out_link.depth, out_link.seq0
+        cfg.out_base, cfg.out_chunk0, cfg.out_wmark = out_link.base_ptr, out_link.chunk0, out_link.wmark
+        cfg.out_fseq = out_link.fseq.ctypes.data if flow_control else None
+        cfg.round_robin_idx, cfg.round_robin_cnt = round_robin_idx, round_robin_cnt
+        cfg.hashmap_seed = hashmap_seed
+        cfg.tcache_depth, cfg.tcache_map_cnt = tcache_depth, tcache_map_cnt
+        cfg.batch_txn_max, cfg.inflight_max = batch_txn_max, inflight_max
+        cfg.batch_wait_ns = int(batch_wait_us * 1000)
+        self.cfg = cfg
+        self._t = L.fdgpu_vtile_new(c.byref(cfg), verifier.struct)
+        if not self._t:
+            raise RuntimeError("fdgpu_vtile_new: bad configuration")
+        if log_max:
+            L.fdgpu_vtile_log_enable(self._t, log_max)
+        self.tcache = TCache.attach(L.fdgpu_vtile_tcache(self._t), self)
+
+    def step(self):
+        r = lib().fdgpu_vtile_step(self._t)
+        if r < 0:
+            raise RuntimeError(f"verify tile step failed: {r} ({_lib.last_error()})")
+        return r
+
+    def run(self, in_frags, timeout_s=60.0):
+        r = lib().fdgpu_vtile_run(self._t, in_frags, timeout_s)
+        if r < 0:
+            raise RuntimeError(f"verify tile run failed: {r} ({_lib.last_error()})")
+
+    def flush(self):
+        r = lib().fdgpu_vtile_flush(self._t)
+        if r < 0:
+            raise RuntimeError(f"verify tile flush failed: {r}")
+
+    def stats(self):
+        s = VTileStats()
+        lib().fdgpu_vtile_stats(self._t, c.byref(s))
+        return s.as_dict()
+
+    def latencies_ns(self):
+        n = self.stats()["lat_cnt"]
+        out = np.zeros(max(n, 1), dtype=np.uint64)
+        n = lib().fdgpu_vtile_latencies(self._t, out.ctypes.data, n)
+        return out[:n]
+
+    def log(self, max_entries=1 << 24):
+        seqs = np.zeros(max_entries, dtype=np.uint64)
+        codes = np.zeros(max_entries, dtype=np.int8)
+        n = lib().fdgpu_vtile_log(self._t, seqs.ctypes.data, codes.ctypes.data, max_entries)
+        order = np.argsort(seqs[:n], kind="stable")
+        return seqs[:n][order], codes[:n][order]
+
+    def close(self):
+        if self._t:
+            lib().fdgpu_vtile_delete(self._t)
+            self._t = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class DedupTile:
+    """The dedup tile (fd_dedup.c) over one or more verify outputs."""
+
+    def __init__(self, in_links, out_link, hashmap_seed=0xDED0, tcache_depth=4194302, tcache_map_cnt=0,
+                 unparsed_in_cnt=0):
+        L = lib()
+        cfg = DTileCfg()
+        cfg.in_cnt = len(in_links)
+        for i, lk in enumerate(in_links):
+            cfg.in_mcache[i], cfg.in_depth[i], cfg.in_seq0[i] = lk.mcache_ptr, lk.depth, lk.seq0
+            cfg.in_base[i], cfg.in_chunk0[i], cfg.in_wmark[i] = lk.base_ptr, lk.chunk0, lk.wmark
+        cfg.unparsed_in_cnt = unparsed_in_cnt
+        cfg.out_mcache, cfg.out_depth, cfg.out_seq0 = out_link.mcache_ptr, out_link.depth, out_link.seq0
+        cfg.out_base, cfg.out_chunk0, cfg.out_wmark = out_link.base_ptr, out_link.chunk0, out_link.wmark
+        cfg.hashmap_seed, cfg.tcache_depth, cfg.tcache_map_cnt = hashmap_seed, tcache_depth, tcache_map_cnt
+        self.cfg, self.links = cfg, (in_links, out_link)
+        self._t = L.fdgpu_dtile_new(c.byref(cfg))
+        if not self._t:
+            raise RuntimeError("fdgpu_dtile_new: bad configuration")
+
+    def step(self):
+        return lib().fdgpu_dtile_step(self._t)
+
+    def run_until_idle(self, max_idle=4):
+        idle, n = 0, 0
+        while idle < max_idle:
+            k = self.step()
+            n += k
+            idle = idle + 1 if k == 0 else 0
+        return n
+
+    def stats(self):
+        s = DTileStats()
+        lib().fdgpu_dtile_stats(self._t, c.byref(s))
+        return s.as_dict()
+
+    def close(self):
+        if self._t:
+            lib().fdgpu_dtile_delete(self._t)
+            self._t = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class Producer:
+    """Line-rate producer thread (stands in for the quic tile)."""
+
+    def __init__(self, link, payloads_arena, offs, sizes, rate_tps=0.0):
+        L = lib()
+        self._keep = (np.ascontiguousarray(payloads_arena, dtype=np.uint8),
+                      np.ascontiguousarray(offs, dtype=np.uint64), np.ascontiguousarray(sizes, dtype=np.uint32))
+        a, o, s = self._keep
+        self._p = L.fdgpu_producer_start(link.mcache_ptr, link.depth, link.seq0, link.base_ptr, link.chunk0,
+                                         link.wmark, a.ctypes.data, o.ctypes.data, s.ctypes.data, len(o),
+                                         float(rate_tps))
+        if not self._p:
+            raise RuntimeError("fdgpu_producer_start failed")
+
+    def join(self):
+        el = c.c_double()
+        n = lib().fdgpu_producer_join(self._p, c.byref(el))
+        self._p = None
+        return n, el.value

@@ -83,3 +83,72 @@ def pack_single(records):
         off += 96 + len(msg)
     arena = np.frombuffer(b"".join(chunks) or b"\0", dtype=np.uint8).copy()
     return arena, np.array(txns, dtype=TXN_DTYPE)
+
+
+_P = 2**255 - 19
+_L = 2**252 + 27742317777372353535851937790883648493
+
+# The eight small-order encodings (fd_curve25519.h:87-94 lists the points;
+# these are their canonical encodings with both sign bits where x == 0).
+SMALL_ORDER_ENC = [
+    "0100000000000000000000000000000000000000000000000000000000000000",
+    "ecffffffffffffffffffffffffffffffffffffffffffffffffffffffffffff7f",
+    "0000000000000000000000000000000000000000000000000000000000000000",
+    "0000000000000000000000000000000000000000000000000000000000000080",
+    "26e8958fc2b227b045c3f489f2ef98f0d5dfac05d3c63339b13802886d53fc05",
+    "26e8958fc2b227b045c3f489f2ef98f0d5dfac05d3c63339b13802886d53fc85",
+    "c7176a703d4dd84fba3c0b760d10670f2a2053fa2c39ccc64ec7fd7792ac037a",
+    "c7176a703d4dd84fba3c0b760d10670f2a2053fa2c39ccc64ec7fd7792ac03fa"]
+
+
+def small_order_cross_product(msg=b"cross"):
+    """SURVEY §8(d) cfg4 adversarial set: the small-order encodings, their
+    y+p variants (where y+p < 2^255) with both sign bits, plus one valid
+    (R, A), as A x R, with S in {0, 1, L-1, L, L+1, 2^253-1, 2^256-1, valid S}.
+    Returns a list of (msg, sig, pub) records."""
+    le = lambda x: int(x % (1 << 256)).to_bytes(32, "little")  # noqa: E731
+    encs = set()
+    for h in SMALL_ORDER_ENC:
+        y = int.from_bytes(bytes.fromhex(h), "little") & (2**255 - 1)
+        for yy in (y, y + _P):
+            if yy < 2**255:
+                for s in (0, 1):
+                    encs.add(le(yy + (s << 255)))
+    pub_ok, sig_ok = sign(bytes(range(32)), msg)
+    encs.add(pub_ok)
+    encs.add(sig_ok[:32])
+    encs = sorted(encs)
+    Ss = [0, 1, _L - 1, _L, _L + 1, 2**253 - 1, 2**256 - 1, int.from_bytes(sig_ok[32:], "little")]
+    return [(msg, Renc + le(S), Aenc) for Aenc in encs for Renc in encs for S in Ss]
+
+
+def explode_sigs(txns):
+    """One single-signature descriptor per signature of each transaction (the
+    signature's own R||S and public key, the transaction's shared message):
+    the per-signature view of fd_ed25519_verify_batch_single_msg's inputs."""
+    cnt = txns["sig_cnt"].astype(np.int64)
+    cnt = np.where((cnt >= 1) & (cnt <= 16), cnt, 0)
+    owner = np.repeat(np.arange(len(txns)), cnt)
+    j = np.arange(len(owner)) - np.repeat(np.cumsum(cnt) - cnt, cnt)
+    out = np.zeros(len(owner), dtype=TXN_DTYPE)
+    t = txns[owner]
+    out["msg_off"], out["msg_sz"] = t["msg_off"], t["msg_sz"]
+    out["sig_off"] = t["sig_off"] + 64 * j
+    out["pub_off"] = t["pub_off"] + 32 * j
+    out["sig_cnt"] = 1
+    return out, owner
+
+
+def payloads(arena, txns):
+    """Raw Solana wire payloads ([sig_cnt][sigs][message]) of generated txns."""
+    return [bytes(arena[int(t["sig_off"]) - 1: int(t["msg_off"]) + int(t["msg_sz"])]) for t in txns]
+
+
+def pack_payloads(payload_list):
+    """payload bytes list -> (arena uint8, offs uint64, sizes uint32) for the frag producer."""
+    sizes = np.array([len(p) for p in payload_list], dtype=np.uint32)
+    offs = np.zeros(len(payload_list), dtype=np.uint64)
+    if len(payload_list):
+        offs[1:] = np.cumsum(sizes.astype(np.uint64))[:-1]
+    arena = np.frombuffer(b"".join(payload_list) or b"\0", dtype=np.uint8).copy()
+    return arena, offs, sizes

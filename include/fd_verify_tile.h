@@ -1,0 +1,320 @@
+/* fd_verify_tile.h -- C ABI of the verify-stage integration around the
+   MI355X Ed25519 engine (libfd_verify_tile.so).
+
+   What the reference's verify tile does per frag (src/app/fdctl/run/tiles/
+   fd_verify.c:36-148, fd_verify.h:45-89): filter by round robin, copy the
+   payload, fd_txn_parse it, check a tcache of recent signature tags, call
+   fd_ed25519_verify_batch_single_msg, insert the tag on success, and publish
+   [payload][pad to 2][fd_txn_t][u16 payload_sz] downstream with the tag as
+   the frag signature.  Here the same contract is met with the signature
+   work batched onto one or more GPUs:
+
+     ingest   frags are read off a tango mcache/dcache pair with the
+              reference's overrun protocol and parsed on the host into a
+              batch arena;
+     verify   whole batches go to the GPU engine(s) (fdgpu_submit), several
+              batches in flight, round-robin over the engines of a node;
+     publish  completed batches are resolved strictly in ingest order: for
+              each txn the tcache is queried, a verify failure filters it,
+              a success inserts the tag and publishes -- exactly the outcome
+              sequence the reference's per-frag fd_txn_verify produces (the
+              tcache decision only depends on earlier txns' outcomes, which
+              are final by the time a txn is resolved).
+
+   Restated wire formats (bit-compatible with the reference, so the tile can
+   sit between the reference's quic and dedup tiles):
+     fdt_frag_meta_t      fd_frag_meta_t          src/tango/fd_tango_base.h:146-203
+     fdt_mcache_*         fd_mcache publish/wait  src/tango/mcache/fd_mcache.h:265-322,574-601
+                                                  fd_mcache.c:64-69 (line init)
+     fdt_dcache_*         compact chunk ring      src/tango/dcache/fd_dcache.h:198-269
+     fdt_tcache_*         fd_tcache               src/tango/tcache/fd_tcache.h:34-404
+     fdt_hash             fd_hash (xxhash-r39)    src/util/fd_hash.c:12-73
+     fdt_txn_t/_parse     fd_txn_t, fd_txn_parse  src/ballet/txn/fd_txn.h:122-335,437-440
+                                                  src/ballet/txn/fd_txn_parse.c:7-243
+                                                  src/ballet/txn/fd_compact_u16.h:29-75
+   Everything here is plain host C/C++; only the verify step touches the GPU
+   (through libfd_ed25519_gpu.so). */
+#ifndef FD_VERIFY_TILE_H
+#define FD_VERIFY_TILE_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#include "fd_ed25519_gpu.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ------------------------------------------------------------ constants */
+
+#define FDT_CHUNK_LG_SZ        (6)
+#define FDT_CHUNK_SZ           (64UL)
+#define FDT_TPU_MTU            (1232UL)                    /* src/disco/fd_disco_base.h:34 */
+#define FDT_TXN_MTU            (1232UL)                    /* src/ballet/txn/fd_txn.h:103 */
+#define FDT_TXN_MAX_SZ         (852UL)                     /* fd_txn.h:98 */
+#define FDT_TPU_DCACHE_MTU     (FDT_TPU_MTU + FDT_TXN_MAX_SZ + 2UL)   /* fd_disco_base.h:41 */
+#define FDT_TXN_SIG_MAX        (127UL)                     /* fd_txn.h:67 */
+#define FDT_TXN_ACCT_ADDR_MAX  (128UL)                     /* fd_txn.h:76 */
+#define FDT_TXN_ADDR_TABLE_LOOKUP_MAX (127UL)              /* fd_txn.h:85 */
+#define FDT_TXN_INSTR_MAX      (64UL)                      /* fd_txn.h:89 */
+#define FDT_TXN_VLEGACY        ((uint8_t)0xFF)
+#define FDT_TXN_V0             ((uint8_t)0x00)
+
+#define FD_TXN_VERIFY_SUCCESS  ( 0)                        /* fd_verify.h:9-11 */
+#define FD_TXN_VERIFY_FAILED   (-1)
+#define FD_TXN_VERIFY_DEDUP    (-2)
+
+#define FDT_VERIFY_TCACHE_DEPTH   (16UL)                   /* fd_verify.h:6-7 */
+#define FDT_VERIFY_TCACHE_MAP_CNT (64UL)
+#define FDT_TCACHE_TAG_NULL       (0UL)
+
+/* ------------------------------------------------------- frag metadata */
+
+typedef struct __attribute__((aligned(32))) {
+  uint64_t seq;
+  uint64_t sig;
+  uint32_t chunk;
+  uint16_t sz;
+  uint16_t ctl;       /* som | eom<<1 | err<<2 | orig<<3 */
+  uint32_t tsorig;
+  uint32_t tspub;
+} fdt_frag_meta_t;
+
+uint64_t fdt_frag_meta_ctl( uint64_t orig, int som, int eom, int err );
+
+/* mcache: `depth` (power of 2) lines; line of seq = seq & (depth-1).
+   init marks every line as not-yet-published for seq0 .. seq0+depth-1. */
+void     fdt_mcache_init   ( fdt_frag_meta_t * mcache, uint64_t depth, uint64_t seq0 );
+void     fdt_mcache_publish( fdt_frag_meta_t * mcache, uint64_t depth, uint64_t seq, uint64_t sig,
+                             uint64_t chunk, uint64_t sz, uint64_t ctl, uint64_t tsorig, uint64_t tspub );
+/* One poll of FD_MCACHE_WAIT: returns 0 if seq is not yet published,
+   1 with *meta filled when it is, -1 if the consumer was overrun (then
+   *seq_found is a lower bound of the producer position). */
+int      fdt_mcache_poll   ( fdt_frag_meta_t const * mcache, uint64_t depth, uint64_t seq,
+                             fdt_frag_meta_t * meta, uint64_t * seq_found );
+/* Sequence number currently in seq's line (re-check after reading a payload). */
+uint64_t fdt_mcache_query  ( fdt_frag_meta_t const * mcache, uint64_t depth, uint64_t seq );
+
+/* compact dcache addressing (chunk = 64-B units from a base address) */
+uint64_t fdt_dcache_chunk_mtu ( uint64_t mtu );
+uint64_t fdt_dcache_data_sz   ( uint64_t mtu, uint64_t depth );  /* bytes for depth frags of <= mtu */
+uint64_t fdt_dcache_wmark     ( uint64_t chunk0, uint64_t chunk1, uint64_t mtu );
+uint64_t fdt_dcache_compact_next( uint64_t chunk, uint64_t sz, uint64_t chunk0, uint64_t wmark );
+
+/* -------------------------------------------------------------- tcache */
+
+uint64_t fdt_tcache_map_cnt_default( uint64_t depth );
+/* Footprint in bytes of a tcache (header 4 words + ring + map), same
+   layout as fd_tcache_private: {magic, depth, map_cnt, oldest, ring[depth],
+   map[map_cnt]}.  map_cnt 0 = default. 0 on bad parameters. */
+uint64_t fdt_tcache_footprint( uint64_t depth, uint64_t map_cnt );
+void *   fdt_tcache_new      ( void * mem, uint64_t depth, uint64_t map_cnt );
+void     fdt_tcache_reset    ( void * tcache );
+/* 1 if tag is present */
+int      fdt_tcache_query    ( void const * tcache, uint64_t tag );
+/* returns dup (1: already present, unchanged; 0: inserted, oldest evicted) */
+int      fdt_tcache_insert   ( void * tcache, uint64_t tag );
+
+/* ---------------------------------------------------------------- hash */
+
+uint64_t fdt_hash( uint64_t seed, void const * buf, uint64_t sz );
+
+/* ----------------------------------------------------------------- txn */
+
+typedef struct {
+  uint8_t  program_id;
+  uint8_t  _padding_reserved_1;
+  uint16_t acct_cnt;
+  uint16_t data_sz;
+  uint16_t acct_off;
+  uint16_t data_off;
+} fdt_txn_instr_t;
+
+typedef struct {
+  uint16_t addr_off;
+  uint8_t  writable_cnt;
+  uint8_t  readonly_cnt;
+  uint16_t writable_off;
+  uint16_t readonly_off;
+} fdt_txn_acct_addr_lut_t;
+
+typedef struct {
+  uint8_t  transaction_version;
+  uint8_t  signature_cnt;
+  uint16_t signature_off;
+  uint16_t message_off;
+  uint8_t  readonly_signed_cnt;
+  uint8_t  readonly_unsigned_cnt;
+  uint16_t acct_addr_cnt;
+  uint16_t acct_addr_off;
+  uint16_t recent_blockhash_off;
+  uint8_t  addr_table_lookup_cnt;
+  uint8_t  addr_table_adtl_writable_cnt;
+  uint8_t  addr_table_adtl_cnt;
+  uint8_t  _padding_reserved_1;
+  uint16_t instr_cnt;
+  fdt_txn_instr_t instr[];
+} fdt_txn_t;
+
+typedef struct {
+  uint64_t success_cnt;
+  uint64_t failure_cnt;
+  uint64_t failure_ring[ 32 ];
+} fdt_txn_parse_counters_t;
+
+uint64_t fdt_txn_footprint( uint64_t instr_cnt, uint64_t addr_table_lookup_cnt );
+/* Parses payload[0,payload_sz) into out_buf (>= FDT_TXN_MAX_SZ bytes, or
+   NULL to validate only).  Returns the fdt_txn_t footprint, 0 if the
+   payload is not a valid transaction.  counters_opt as the reference
+   (failure_ring records a reason code per failure). */
+uint64_t fdt_txn_parse( uint8_t const * payload, uint64_t payload_sz, void * out_buf,
+                        fdt_txn_parse_counters_t * counters_opt );
+
+/* ----------------------------------------------------------- verifiers */
+
+/* A verifier runs fd_ed25519_verify_batch_single_msg over whole batches,
+   asynchronously.  submit returns a ticket >= 0 or < 0 (FDGPU_ERR_FULL when
+   no slot is free); poll returns FDGPU_OK with codes written,
+   FDGPU_PENDING, or < 0. */
+typedef struct {
+  void *  ctx;
+  int64_t (*submit)( void * ctx, uint8_t const * arena, uint64_t arena_sz, fdgpu_txn_t const * txns,
+                     uint64_t txn_cnt );
+  int     (*poll)  ( void * ctx, int64_t ticket, int8_t * txn_codes, int blocking );
+} fdgpu_verifier_t;
+
+/* Multi-GPU dispatcher: batches go round-robin over `engine_cnt` engines
+   (one per GPU, independent queues, no collective). */
+typedef struct fdgpu_dispatch fdgpu_dispatch_t;
+fdgpu_dispatch_t * fdgpu_dispatch_new( fdgpu_engine_t * const * engines, uint32_t engine_cnt );
+void               fdgpu_dispatch_delete( fdgpu_dispatch_t * d );
+fdgpu_verifier_t   fdgpu_dispatch_verifier( fdgpu_dispatch_t * d );
+
+/* --------------------------------------------------------- verify tile */
+
+typedef struct {
+  /* in link (quic -> verify): mcache + payload region */
+  fdt_frag_meta_t const * in_mcache;
+  uint64_t                in_depth;
+  uint64_t                in_seq0;
+  uint8_t const *         in_base;      /* address of chunk 0 */
+  uint64_t                in_chunk0;    /* valid chunk range [chunk0, wmark] */
+  uint64_t                in_wmark;
+  /* out link (verify -> dedup) */
+  fdt_frag_meta_t *       out_mcache;
+  uint64_t                out_depth;
+  uint64_t                out_seq0;
+  uint8_t *               out_base;
+  uint64_t                out_chunk0;
+  uint64_t                out_wmark;
+  uint64_t const *        out_fseq;     /* reliable consumer's next seq (NULL: no flow control) */
+  /* tile */
+  uint64_t round_robin_idx;
+  uint64_t round_robin_cnt;
+  uint64_t hashmap_seed;
+  uint64_t tcache_depth;                /* 0: FDT_VERIFY_TCACHE_DEPTH */
+  uint64_t tcache_map_cnt;              /* 0: FDT_VERIFY_TCACHE_MAP_CNT */
+  uint32_t batch_txn_max;               /* txns per GPU batch */
+  uint32_t inflight_max;                /* batches in flight (<= the verifier's slots) */
+  uint64_t batch_wait_ns;               /* a partial batch is submitted after this long */
+} fdgpu_vtile_cfg_t;
+
+typedef struct {
+  uint64_t in_frags;        /* frags seen on the in link */
+  uint64_t filtered_rr;     /* not this tile's round-robin share */
+  uint64_t corrupt;         /* chunk/sz out of range (reference: FD_LOG_ERR) */
+  uint64_t overrun;         /* frags lost to producer overrun */
+  uint64_t parse_fail;      /* fd_txn_parse rejected */
+  uint64_t verify_failed;   /* FD_TXN_VERIFY_FAILED */
+  uint64_t dedup;           /* FD_TXN_VERIFY_DEDUP */
+  uint64_t published;       /* FD_TXN_VERIFY_SUCCESS, published downstream */
+  uint64_t batches;
+  uint64_t sigs;            /* signatures sent to the GPU */
+  uint64_t backpressure;    /* steps that stalled on out-link credits */
+  uint64_t lat_cnt;         /* batch latencies recorded (ingest of first frag -> publish) */
+} fdgpu_vtile_stats_t;
+
+typedef struct fdgpu_vtile fdgpu_vtile_t;
+
+fdgpu_vtile_t * fdgpu_vtile_new   ( fdgpu_vtile_cfg_t const * cfg, fdgpu_verifier_t verifier );
+void            fdgpu_vtile_delete( fdgpu_vtile_t * t );
+/* One run-loop iteration: ingest what is available (up to one batch),
+   submit due batches, resolve and publish completed ones in order.
+   Returns the number of frags resolved this step, < 0 on a verifier error. */
+int64_t         fdgpu_vtile_step  ( fdgpu_vtile_t * t );
+/* Runs steps until `in_frags` frags have been seen on the in link and every
+   batch is resolved, or timeout_s passes.  Returns 0, or < 0. */
+int             fdgpu_vtile_run   ( fdgpu_vtile_t * t, uint64_t in_frags, double timeout_s );
+/* Submits a partial batch and resolves everything in flight (blocking). */
+int             fdgpu_vtile_flush ( fdgpu_vtile_t * t );
+void            fdgpu_vtile_stats ( fdgpu_vtile_t const * t, fdgpu_vtile_stats_t * out );
+/* Copies up to max recorded batch latencies (ns) into out; returns count. */
+uint64_t        fdgpu_vtile_latencies( fdgpu_vtile_t const * t, uint64_t * out, uint64_t max );
+/* The tile's tcache (e.g. to reset it between test phases). */
+void *          fdgpu_vtile_tcache( fdgpu_vtile_t * t );
+/* Per-frag outcome log (tests): for every in-link seq the tile saw, the
+   FD_TXN_VERIFY_* code, or FDGPU_VTILE_LOG_* below.  Enabled by
+   fdgpu_vtile_log_enable(t, max) before the first step; entries are in the
+   order outcomes became final (filtered frags at ingest, verified ones at
+   resolution), so sort by seq to compare with a sequential model. */
+#define FDGPU_VTILE_LOG_PARSE_FAIL (1)
+#define FDGPU_VTILE_LOG_FILTERED   (2)
+#define FDGPU_VTILE_LOG_LOST       (3)   /* overrun or corrupt */
+void            fdgpu_vtile_log_enable( fdgpu_vtile_t * t, uint64_t log_max );
+uint64_t        fdgpu_vtile_log( fdgpu_vtile_t const * t, uint64_t * seqs, int8_t * codes, uint64_t max );
+
+/* ---------------------------------------------------------- dedup tile */
+
+/* src/app/fdctl/run/tiles/fd_dedup.c:89-205: consumes verify outputs (the
+   parsed trailer locates signature 0), tags with fd_hash(seed, sig0, 64),
+   tcache-inserts, publishes non-duplicates with sig 0. */
+typedef struct {
+  uint32_t                in_cnt;
+  fdt_frag_meta_t const * in_mcache[ 16 ];
+  uint64_t                in_depth [ 16 ];
+  uint64_t                in_seq0  [ 16 ];
+  uint8_t const *         in_base  [ 16 ];
+  uint64_t                in_chunk0[ 16 ];
+  uint64_t                in_wmark [ 16 ];
+  uint32_t                unparsed_in_cnt;   /* first links carry raw txns (gossip) */
+  fdt_frag_meta_t *       out_mcache;
+  uint64_t                out_depth;
+  uint64_t                out_seq0;
+  uint8_t *               out_base;
+  uint64_t                out_chunk0;
+  uint64_t                out_wmark;
+  uint64_t                hashmap_seed;
+  uint64_t                tcache_depth;     /* reference default 4194302 (default.toml:910) */
+  uint64_t                tcache_map_cnt;   /* 0: default */
+} fdgpu_dtile_cfg_t;
+
+typedef struct {
+  uint64_t in_frags, dup, published, overrun, corrupt, parse_fail;
+} fdgpu_dtile_stats_t;
+
+typedef struct fdgpu_dtile fdgpu_dtile_t;
+fdgpu_dtile_t * fdgpu_dtile_new   ( fdgpu_dtile_cfg_t const * cfg );
+void            fdgpu_dtile_delete( fdgpu_dtile_t * t );
+int64_t         fdgpu_dtile_step  ( fdgpu_dtile_t * t );   /* frags consumed this step */
+void            fdgpu_dtile_stats ( fdgpu_dtile_t const * t, fdgpu_dtile_stats_t * out );
+
+/* ------------------------------------------------------- frag producer */
+
+/* A line-rate producer thread standing in for the quic tile: publishes
+   payload i (arena + off[i], sz[i] bytes) as frag seq0+i into an mcache /
+   compact dcache at `rate_tps` frags per second (0 = as fast as possible),
+   without backpressure (the quic -> verify link has none, fd_tpu.h:52-68). */
+typedef struct fdgpu_producer fdgpu_producer_t;
+fdgpu_producer_t * fdgpu_producer_start( fdt_frag_meta_t * mcache, uint64_t depth, uint64_t seq0,
+                                         uint8_t * base, uint64_t chunk0, uint64_t wmark,
+                                         uint8_t const * arena, uint64_t const * off, uint32_t const * sz,
+                                         uint64_t cnt, double rate_tps );
+/* Waits for the producer; returns frags published, *elapsed_s its wall time. */
+uint64_t           fdgpu_producer_join ( fdgpu_producer_t * p, double * elapsed_s );
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* FD_VERIFY_TILE_H */

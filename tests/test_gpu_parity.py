@@ -214,28 +214,7 @@ def test_cfg3_multisig_vs_oracle(engine, oracle):
 def test_small_order_cross_product(engine, oracle):
     """small-order encodings (and y+p variants, sign bits) as
     A x R with S in {0, 1, L-1, L, L+1, 2^253-1, 2^256-1}."""
-    base = ["0100000000000000000000000000000000000000000000000000000000000000",
-            "ecffffffffffffffffffffffffffffffffffffffffffffffffffffffffffff7f",
-            "0000000000000000000000000000000000000000000000000000000000000000",
-            "0000000000000000000000000000000000000000000000000000000000000080",
-            "26e8958fc2b227b045c3f489f2ef98f0d5dfac05d3c63339b13802886d53fc05",
-            "26e8958fc2b227b045c3f489f2ef98f0d5dfac05d3c63339b13802886d53fc85",
-            "c7176a703d4dd84fba3c0b760d10670f2a2053fa2c39ccc64ec7fd7792ac037a",
-            "c7176a703d4dd84fba3c0b760d10670f2a2053fa2c39ccc64ec7fd7792ac03fa"]
-    encs = set()
-    for h in base:
-        b = bytes.fromhex(h)
-        y = int.from_bytes(b, "little") & (2**255 - 1)
-        for yy in (y, y + P):
-            if yy < 2**255:
-                for s in (0, 1):
-                    encs.add(_le(yy + (s << 255)))
-    prv = bytes(range(32))
-    pub_ok, sig_ok = workload.sign(prv, b"cross")
-    encs.add(pub_ok); encs.add(sig_ok[:32])
-    encs = sorted(encs)
-    Ss = [0, 1, L - 1, L, L + 1, 2**253 - 1, 2**256 - 1, int.from_bytes(sig_ok[32:], "little")]
-    recs = [(b"cross", Renc + _le(S), Aenc) for Aenc in encs for Renc in encs for S in Ss]
+    recs = workload.small_order_cross_product()
     arena, txns = workload.pack_single(recs)
     got = engine.verify_txns(arena, txns)
     exp = oracle.verify_txns(arena, txns, nthreads=8)

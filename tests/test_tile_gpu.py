@@ -1,0 +1,98 @@
+"""Verify tile over the real GPU engine(s): the reference's test_verify.c
+sequences, a mixed stream against the sequential model (oracle verdicts),
+the multi-engine dispatcher, and the concurrent producer path."""
+import numpy as np
+import pytest
+
+import firedancer_amd as fa
+from firedancer_amd import tile, workload
+import tile_model
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def fixtures(txn_fixtures):
+    return {t["name"]: bytes.fromhex(t["payload"]) for t in txn_fixtures}
+
+
+@pytest.fixture(scope="module")
+def engines():
+    es = [fa.VerifyEngine(0, max_txn=4096, max_sig=4096 * 12, max_arena=4096 * 1232, ring_depth=2)
+          for _ in range(2)]
+    yield es
+    for e in es:
+        e.close()
+
+
+def _tile(engs, inl, outl, **kw):
+    ver = tile.EngineVerifier(engs)
+    vt = tile.VerifyTile(inl, outl, ver, **kw)
+    vt._ver_keep = ver
+    return vt
+
+
+def test_reference_sequences_on_gpu(engines, fixtures):
+    v1, v2 = fixtures["test_verify.valid_txn_1sig"], fixtures["test_verify.valid_txn_2sigs"]
+    i2, same1 = fixtures["test_verify.invalid_txn_2sigs"], fixtures["test_verify.invalid_txn_same_1sig"]
+    same64 = fixtures["test_verify.invalid_txn_1sig_same_64bit"]
+    seq = [v2, v2, v2, v1, v1, v1, i2, i2, same64]
+    inl, outl = tile.Link(64, 1232), tile.Link(64, tile.TPU_DCACHE_MTU)
+    vt = _tile(engines[:1], inl, outl, batch_txn_max=4, log_max=64)
+    for p in seq:
+        inl.publish(p)
+    vt.run(len(seq), timeout_s=30)
+    assert vt.log()[1].tolist() == [0, -2, -2, 0, -2, -2, -1, -1, -1]
+    inl2, outl2 = tile.Link(64, 1232), tile.Link(64, tile.TPU_DCACHE_MTU)
+    vt2 = _tile(engines[:1], inl2, outl2, batch_txn_max=4, log_max=64)
+    for p in (same1, v1, same1):
+        inl2.publish(p)
+    vt2.run(3, timeout_s=30)
+    assert vt2.log()[1].tolist() == [-1, 0, -2]
+
+
+def test_mixed_stream_two_engines_vs_model(engines, oracle):
+    from test_tile import _mixed_stream
+    ps = _mixed_stream(3000, seed=99)
+    seed = 0xFEED
+    inl, outl = tile.Link(1 << 13, 1232), tile.Link(1 << 13, tile.TPU_DCACHE_MTU)
+    vt = _tile(engines, inl, outl, hashmap_seed=seed, batch_txn_max=97, inflight_max=4, log_max=1 << 14)
+    for p in ps:
+        inl.publish(p)
+    vt.run(len(ps), timeout_s=60)
+    exp, pub = tile_model.verify_tile_model(ps, seed, lambda a, t: oracle.verify_txns(a, t))
+    seqs, codes = vt.log()
+    assert codes.tolist() == exp
+    outs = outl.drain()
+    assert [(m["sig"], tile.split_verify_output(f)[0]) for m, f in outs] == [(t, p) for p, _, t in pub]
+    assert vt.stats()["batches"] >= len(ps) // 97
+
+
+def test_quic_corpus_through_tile(engines, quic_corpus, oracle):
+    arena, txns, codes = quic_corpus
+    ps = [bytes(arena[int(t["sig_off"]) - 1: int(t["msg_off"]) + int(t["msg_sz"])]) for t in txns]
+    inl, outl = tile.Link(1 << 11, 1232), tile.Link(1 << 11, tile.TPU_DCACHE_MTU)
+    vt = _tile(engines, inl, outl, batch_txn_max=256, inflight_max=2)
+    for p in ps:
+        inl.publish(p)
+    vt.run(len(ps), timeout_s=60)
+    st = vt.stats()
+    exp, pub = tile_model.verify_tile_model(ps, 0x5EEDF00D, lambda a, t: oracle.verify_txns(a, t))
+    assert st["published"] == len(pub) == exp.count(0) and st["verify_failed"] == 0
+
+
+def test_producer_at_rate_no_overrun(engines):
+    """Producer thread at 500K frags/s into a 2^16-deep link, tile keeping up."""
+    a, t, modes = workload.cfg3(20000, seed=7)
+    ps = workload.payloads(a, t)
+    arena, offs, sizes = workload.pack_payloads(ps)
+    inl, outl = tile.Link(1 << 16, 1232), tile.Link(1 << 16, tile.TPU_DCACHE_MTU)
+    vt = _tile(engines, inl, outl, batch_txn_max=2048, inflight_max=4, batch_wait_us=100)
+    prod = tile.Producer(inl, arena, offs, sizes, rate_tps=500000)
+    vt.run(len(ps), timeout_s=60)
+    prod.join()
+    st = vt.stats()
+    assert st["overrun"] == 0 and st["in_frags"] == len(ps)
+    assert st["published"] == int((modes == 0).sum())
+    lat = vt.latencies_ns()
+    assert len(lat) == st["batches"] and np.percentile(lat, 99) < 50e6

@@ -1,0 +1,113 @@
+"""Config-5 line-rate bench (BASELINE.json configs[4]):
+tango-framed cfg3 transactions (1-12 signatures, msgs up to the MTU) are
+published by a producer thread into the quic->verify link; T verify tiles
+(one host thread each, round-robin shares of the stream as in
+fd_verify.c:46) batch them onto G GPU engines, resolve tcache/dedup in order
+and publish the verify->dedup frags.  Reports end-to-end transactions/s and
+signatures/s (producer start -> last frag resolved), per-batch latency
+(first frag ingested -> batch published) and per-tile counters.
+
+    python tools/bench_tile.py --gpus 1 --tiles 1 --txns 200000
+"""
+import argparse
+import json
+import os
+import sys
+import threading
+import time
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+
+import firedancer_amd as fa  # noqa: E402
+from firedancer_amd import tile, workload  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--txns", type=int, default=200_000)
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--tiles", type=int, default=0, help="verify tile threads (default: one per GPU)")
+    ap.add_argument("--rate", type=float, default=0.0, help="producer frags/s (0: as fast as possible)")
+    ap.add_argument("--batch", type=int, default=4096)
+    ap.add_argument("--inflight", type=int, default=3)
+    ap.add_argument("--wait-us", type=float, default=200.0)
+    ap.add_argument("--depth-lg", type=int, default=19, help="log2 of the quic->verify mcache depth")
+    ap.add_argument("--multi", type=int, default=1, help="1: cfg3 multi-sig txns, 0: cfg1 single-sig")
+    ap.add_argument("--out", default="")
+    args = ap.parse_args()
+    tiles_n = args.tiles or args.gpus
+
+    t0 = time.time()
+    gen = workload.cfg3 if args.multi else workload.cfg1
+    a, t, modes = gen(args.txns, seed=0x5EED0005)
+    ps = workload.payloads(a, t)
+    arena, offs, sizes = workload.pack_payloads(ps)
+    n_sig = int(t["sig_cnt"].sum())
+    print(f"[bench_tile] generated {len(ps)} txns / {n_sig} sigs in {time.time() - t0:.1f}s", flush=True)
+    del a, t
+
+    # one engine per tile thread (an engine is single-threaded), tiles spread over the GPUs
+    engines = [fa.VerifyEngine(k % args.gpus, max_txn=args.batch, max_sig=args.batch * 12,
+                               max_arena=args.batch * 1232, ring_depth=args.inflight) for k in range(tiles_n)]
+    inl = tile.Link(1 << args.depth_lg, 1232)
+    vts, vers = [], []
+    for k in range(tiles_n):
+        ver = tile.EngineVerifier([engines[k]])
+        outl = tile.Link(1 << 12, tile.TPU_DCACHE_MTU)
+        vts.append(tile.VerifyTile(inl, outl, ver, batch_txn_max=args.batch, inflight_max=args.inflight,
+                                   batch_wait_us=args.wait_us, round_robin_idx=k, round_robin_cnt=tiles_n))
+        vers.append((ver, outl))
+
+    errs = []
+
+    def run(vt):
+        try:
+            vt.run(len(ps), timeout_s=300)
+        except Exception as e:  # noqa: BLE001
+            errs.append(repr(e))
+
+    ths = [threading.Thread(target=run, args=(vt,)) for vt in vts]
+    start = time.perf_counter()
+    prod = tile.Producer(inl, arena, offs, sizes, rate_tps=args.rate)
+    for th in ths:
+        th.start()
+    for th in ths:
+        th.join()
+    wall = time.perf_counter() - start
+    n_pub, prod_s = prod.join()
+    if errs:
+        raise SystemExit(f"tile errors: {errs}")
+
+    stats = [vt.stats() for vt in vts]
+    lat = np.concatenate([vt.latencies_ns() for vt in vts]) / 1e6
+    agg = {k: int(sum(s[k] for s in stats)) for k in stats[0]}
+    res = {
+        "metric": "verify tile end-to-end transactions/s (tango in -> GPU verify -> tango out)",
+        "txns_per_s": round(len(ps) / wall, 1),
+        "sigs_per_s": round(agg["sigs"] / wall, 1),
+        "wall_s": round(wall, 4), "producer_s": round(prod_s, 4), "producer_published": int(n_pub),
+        "gpus": args.gpus, "tiles": tiles_n, "batch_txn_max": args.batch, "inflight": args.inflight,
+        "rate_target": args.rate, "workload": "cfg3 (1-12 sigs/txn, payload <= 1232 B, 10% corrupted)"
+        if args.multi else "cfg1 (1 sig, msg U[180,220] B, 10% corrupted)",
+        "txns": len(ps), "sigs": n_sig,
+        "batch_latency_ms": {"p50": round(float(np.percentile(lat, 50)), 3),
+                             "p99": round(float(np.percentile(lat, 99)), 3), "n": int(len(lat))},
+        "counters": agg,
+        "expected_published": int((modes == 0).sum()),
+    }
+    line = json.dumps(res)
+    print(line, flush=True)
+    if args.out:
+        with open(args.out, "w") as f:
+            f.write(line + "\n")
+    for e in engines:
+        e.close()
+    ok = agg["published"] == res["expected_published"] and agg["overrun"] == 0
+    return 0 if ok else 1
+
+
+if __name__ == "__main__":
+    sys.exit(main())
