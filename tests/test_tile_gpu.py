@@ -36,19 +36,15 @@ def test_reference_sequences_on_gpu(engines, fixtures):
     v1, v2 = fixtures["test_verify.valid_txn_1sig"], fixtures["test_verify.valid_txn_2sigs"]
     i2, same1 = fixtures["test_verify.invalid_txn_2sigs"], fixtures["test_verify.invalid_txn_same_1sig"]
     same64 = fixtures["test_verify.invalid_txn_1sig_same_64bit"]
-    seq = [v2, v2, v2, v1, v1, v1, i2, i2, same64]
-    inl, outl = tile.Link(64, 1232), tile.Link(64, tile.TPU_DCACHE_MTU)
-    vt = _tile(engines[:1], inl, outl, batch_txn_max=4, log_max=64)
-    for p in seq:
-        inl.publish(p)
-    vt.run(len(seq), timeout_s=30)
-    assert vt.log()[1].tolist() == [0, -2, -2, 0, -2, -2, -1, -1, -1]
-    inl2, outl2 = tile.Link(64, 1232), tile.Link(64, tile.TPU_DCACHE_MTU)
-    vt2 = _tile(engines[:1], inl2, outl2, batch_txn_max=4, log_max=64)
-    for p in (same1, v1, same1):
-        inl2.publish(p)
-    vt2.run(3, timeout_s=30)
-    assert vt2.log()[1].tolist() == [-1, 0, -2]
+    S, F, D = 0, -1, -2
+    for seq, exp in (([v2, v2, v2, v1, v1, v1], [S, D, D, S, D, D]), ([i2, i2], [F, F]),
+                     ([same1, v1, same1], [F, S, D]), ([v1, same64], [S, F])):
+        inl, outl = tile.Link(64, 1232), tile.Link(64, tile.TPU_DCACHE_MTU)
+        vt = _tile(engines[:1], inl, outl, batch_txn_max=4, log_max=64)
+        for p in seq:
+            inl.publish(p)
+        vt.run(len(seq), timeout_s=30)
+        assert vt.log()[1].tolist() == exp
 
 
 def test_mixed_stream_two_engines_vs_model(engines, oracle):

@@ -37,8 +37,8 @@ def main():
     ap.add_argument("--depth-lg", type=int, default=19, help="log2 of the quic->verify mcache depth")
     ap.add_argument("--multi", type=int, default=1, help="1: cfg3 multi-sig txns, 0: cfg1 single-sig")
     ap.add_argument("--out", default="")
+    ap.add_argument("--sweep", default="", help="';'-separated runs of 'tiles,batch,inflight,rate' over the same txns")
     args = ap.parse_args()
-    tiles_n = args.tiles or args.gpus
 
     t0 = time.time()
     gen = workload.cfg3 if args.multi else workload.cfg1
@@ -49,15 +49,32 @@ def main():
     print(f"[bench_tile] generated {len(ps)} txns / {n_sig} sigs in {time.time() - t0:.1f}s", flush=True)
     del a, t
 
+    runs = [tuple(float(x) for x in r.split(",")) for r in args.sweep.split(";") if r] or \
+        [(args.tiles or args.gpus, args.batch, args.inflight, args.rate)]
+    ok = True
+    lines = []
+    for tiles_n, batch, inflight, rate in runs:
+        res = run_once(args, ps, arena, offs, sizes, n_sig, modes, int(tiles_n), int(batch), int(inflight), rate)
+        line = json.dumps(res)
+        print(line, flush=True)
+        lines.append(line)
+        ok &= res["counters"]["published"] == res["expected_published"] and res["counters"]["overrun"] == 0
+    if args.out:
+        with open(args.out, "w") as f:
+            f.write("\n".join(lines) + "\n")
+    return 0 if ok else 1
+
+
+def run_once(args, ps, arena, offs, sizes, n_sig, modes, tiles_n, batch, inflight, rate):
     # one engine per tile thread (an engine is single-threaded), tiles spread over the GPUs
-    engines = [fa.VerifyEngine(k % args.gpus, max_txn=args.batch, max_sig=args.batch * 12,
-                               max_arena=args.batch * 1232, ring_depth=args.inflight) for k in range(tiles_n)]
+    engines = [fa.VerifyEngine(k % args.gpus, max_txn=batch, max_sig=batch * 12,
+                               max_arena=batch * 1232, ring_depth=inflight) for k in range(tiles_n)]
     inl = tile.Link(1 << args.depth_lg, 1232)
     vts, vers = [], []
     for k in range(tiles_n):
         ver = tile.EngineVerifier([engines[k]])
         outl = tile.Link(1 << 12, tile.TPU_DCACHE_MTU)
-        vts.append(tile.VerifyTile(inl, outl, ver, batch_txn_max=args.batch, inflight_max=args.inflight,
+        vts.append(tile.VerifyTile(inl, outl, ver, batch_txn_max=batch, inflight_max=inflight,
                                    batch_wait_us=args.wait_us, round_robin_idx=k, round_robin_cnt=tiles_n))
         vers.append((ver, outl))
 
@@ -71,7 +88,7 @@ def main():
 
     ths = [threading.Thread(target=run, args=(vt,)) for vt in vts]
     start = time.perf_counter()
-    prod = tile.Producer(inl, arena, offs, sizes, rate_tps=args.rate)
+    prod = tile.Producer(inl, arena, offs, sizes, rate_tps=rate)
     for th in ths:
         th.start()
     for th in ths:
@@ -89,8 +106,8 @@ def main():
         "txns_per_s": round(len(ps) / wall, 1),
         "sigs_per_s": round(agg["sigs"] / wall, 1),
         "wall_s": round(wall, 4), "producer_s": round(prod_s, 4), "producer_published": int(n_pub),
-        "gpus": args.gpus, "tiles": tiles_n, "batch_txn_max": args.batch, "inflight": args.inflight,
-        "rate_target": args.rate, "workload": "cfg3 (1-12 sigs/txn, payload <= 1232 B, 10% corrupted)"
+        "gpus": args.gpus, "tiles": tiles_n, "batch_txn_max": batch, "inflight": inflight,
+        "rate_target": rate, "workload": "cfg3 (1-12 sigs/txn, payload <= 1232 B, 10% corrupted)"
         if args.multi else "cfg1 (1 sig, msg U[180,220] B, 10% corrupted)",
         "txns": len(ps), "sigs": n_sig,
         "batch_latency_ms": {"p50": round(float(np.percentile(lat, 50)), 3),
@@ -98,15 +115,13 @@ def main():
         "counters": agg,
         "expected_published": int((modes == 0).sum()),
     }
-    line = json.dumps(res)
-    print(line, flush=True)
-    if args.out:
-        with open(args.out, "w") as f:
-            f.write(line + "\n")
+    for vt in vts:
+        vt.close()
+    for ver, _ in vers:
+        ver.close()
     for e in engines:
         e.close()
-    ok = agg["published"] == res["expected_published"] and agg["overrun"] == 0
-    return 0 if ok else 1
+    return res
 
 
 if __name__ == "__main__":
