@@ -173,10 +173,8 @@ fdgpu_engine_t *fdgpu_engine_open(int device, fdgpu_cfg_t const *cfg_in) {
   e->cfg = cfg;
   auto fail = [&]() -> fdgpu_engine_t * { fdgpu_engine_close(e); return nullptr; };
   if (hipStreamCreateWithFlags(&e->compute, hipStreamNonBlocking) != hipSuccess) { set_err("stream"); return fail(); }
-  if (hipMalloc((void **)&e->d_btab, FDGPU_BTAB_ENTRIES * FDGPU_BTAB_STRIDE * sizeof(uint32_t)) != hipSuccess) {
-    set_err("btab alloc"); return fail();
-  }
-  if (fdgpu_launch_btab_init(e->d_btab, e->compute) != hipSuccess) { set_err("btab init launch"); return fail(); }
+  if (hipMalloc((void **)&e->d_btab, fdgpu_btab_bytes()) != hipSuccess) { set_err("btab alloc"); return fail(); }
+  if (fdgpu_btab_build(e->d_btab, e->compute) != hipSuccess) { set_err("fixed-base table build failed"); return fail(); }
   int bpcu = 0;
   hipDeviceProp_t prop;
   if (fdgpu_verify_occupancy(&bpcu) != hipSuccess || bpcu < 1) bpcu = 1;

@@ -198,6 +198,32 @@ FDG_DEV void ge_add_cached_regs(ge_p1p1 &r, const ge_p3 &p, const uint32_t (&q)[
   r.Y = t;
 }
 
+/* P + Q with Q an affine niels entry in registers (q[0..9] = y+x,
+   q[10..19] = y-x, q[20..29] = 2dxy, canonical): 3M.  neg selects P - Q. */
+FDG_DEV void ge_add_niels_regs(ge_p1p1 &r, const ge_p3 &p, const uint32_t (&q)[32], bool neg) {
+  fe t, c;
+#pragma unroll
+  for (int i = 0; i < 10; i++) c.v[i] = q[20 + i];
+  fe_cneg(c, neg);
+  fe_mul(r.Z, p.T, c);             /* C = T1 2dxy */
+  fe_add(r.T, p.Z, p.Z);           /* D = 2 Z1 */
+#pragma unroll
+  for (int i = 0; i < 10; i++) c.v[i] = neg ? q[10 + i] : q[i];
+  fe_add(t, p.Y, p.X);
+  fe_mul(r.X, t, c);               /* A */
+#pragma unroll
+  for (int i = 0; i < 10; i++) c.v[i] = neg ? q[i] : q[10 + i];
+  fe_sub(t, p.Y, p.X);
+  fe_mul(r.Y, t, c);               /* B */
+  fe_add(t, r.T, r.Z);
+  fe_sub(r.T, r.T, r.Z);
+  fe_carry(r.T);
+  r.Z = t;
+  fe_add(t, r.X, r.Y);
+  fe_sub(r.X, r.X, r.Y);
+  r.Y = t;
+}
+
 FDG_DEV void ge_p3_to_cached(ge_cached &r, const ge_p3 &p) {
   constexpr uint32_t D2[10] = FDGPU_FE_D2;
   fe d2; fe_set(d2, D2);

@@ -29,8 +29,23 @@ typedef struct {
 #define FDGPU_BTAB_STRIDE   32u           /* u32 per niels entry (30 used) */
 #define FDGPU_ATAB_ENTRIES  9u            /* 0 (identity), 1A .. 8A (A negated) */
 #define FDGPU_ATAB_WORDS    40u           /* u32 per cached entry */
-#define FDGPU_WS_ENTRIES    10u           /* per-lane workspace entries: table + parked (x_R, y_R) */
-#define FDGPU_WS_LANE_WORDS (FDGPU_WS_ENTRIES * FDGPU_ATAB_WORDS)   /* 1600 B per signature */
+/* Fixed-base comb for [S]B (FDGPU_BCOMB=1): S in signed radix 2^W, digit i
+   looked up in table i = {0, 1, .., 2^(W-1)} x 2^(W i) B (affine niels, one
+   128-B line per entry), so [S]B costs NDIG mixed additions and no
+   doublings.  Tables live in HBM (W=16: 16 x 32769 x 128 B = 67 MB, resident
+   in the 256 MB Infinity Cache). */
+#ifndef FDGPU_BCOMB
+#define FDGPU_BCOMB 1
+#endif
+#ifndef FDGPU_BCOMB_BITS
+#define FDGPU_BCOMB_BITS 16u
+#endif
+#define FDGPU_BCOMB_NDIG    ((254u + FDGPU_BCOMB_BITS - 1u) / FDGPU_BCOMB_BITS)   /* covers S < 2^253 + carry */
+#define FDGPU_BCOMB_ENTRIES ((1u << (FDGPU_BCOMB_BITS - 1u)) + 1u)
+#define FDGPU_BCOMB_STRIDE  32u           /* u32 per entry (30 used): one 128-B line */
+#define FDGPU_BCOMB_CHUNK   64u           /* entries per lane in the table build (one batch inversion) */
+#define FDGPU_WS_ENTRIES    11u           /* per-lane workspace: A table, parked (x_R, y_R, digits), cached [S]B */
+#define FDGPU_WS_LANE_WORDS (FDGPU_WS_ENTRIES * FDGPU_ATAB_WORDS)   /* 1760 B per signature */
 #define FDGPU_BTAB_LDS_STRIDE 33u         /* B-table entry stride in LDS (odd: no bank conflicts) */
 #define FDGPU_BLOCK         256u
 #define FDGPU_FLAG_REF_MAP  1u            /* portable-backend error mapping */
@@ -39,8 +54,10 @@ typedef struct {
 extern "C" {
 #endif
 
-/* launchers (fdgpu_kernels.hip); all asynchronous on `stream` */
-hipError_t fdgpu_launch_btab_init(uint32_t *d_btab, hipStream_t stream);
+/* launchers (fdgpu_kernels.hip); all asynchronous on `stream` unless noted */
+size_t     fdgpu_btab_bytes(void);                                   /* fixed-base table size */
+/* builds the fixed-base table into d_btab (fdgpu_btab_bytes()); synchronous */
+hipError_t fdgpu_btab_build(uint32_t *d_btab, hipStream_t stream);
 /* one signature per lane; d_ws must hold fdgpu_ws_bytes(n_sig) bytes */
 hipError_t fdgpu_launch_verify_sigs(const uint8_t *d_arena, const fdgpu_sig_desc_t *d_sigs, uint32_t n_sig,
                                     const uint32_t *d_btab, uint32_t *d_ws, int8_t *d_sig_codes, uint32_t flags,

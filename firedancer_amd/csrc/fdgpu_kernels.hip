@@ -35,6 +35,21 @@ using namespace fdgpu;
 #ifndef FDGPU_FUSED
 #define FDGPU_FUSED 1         /* 1: one launch runs both passes; 0: prep + dsm kernels (same speed) */
 #endif
+/* Cost-breakdown experiments (timing only -- results are wrong when set):
+   FDGPU_EXP_NO_RDEC skip decompressing R, FDGPU_EXP_NO_BADD skip the B adds,
+   FDGPU_EXP_NO_AADD skip the A adds, FDGPU_EXP_NO_SHA skip SHA-512. */
+#ifndef FDGPU_EXP_NO_RDEC
+#define FDGPU_EXP_NO_RDEC 0
+#endif
+#ifndef FDGPU_EXP_NO_BADD
+#define FDGPU_EXP_NO_BADD 0
+#endif
+#ifndef FDGPU_EXP_NO_AADD
+#define FDGPU_EXP_NO_AADD 0
+#endif
+#ifndef FDGPU_EXP_NO_SHA
+#define FDGPU_EXP_NO_SHA 0
+#endif
 #ifndef FDGPU_DSM_WAVES
 #define FDGPU_DSM_WAVES 3     /* ~130 VGPRs: 3 waves per SIMD, no spills */
 #endif
@@ -84,6 +99,86 @@ __global__ void fdgpu_btab_init_kernel(uint32_t *btab) {
   fe_sub(ymx, y, x); fe_canon(ymx);
   fe_mul(xy, x, y); fe_mul(xy2d, xy, d2); fe_canon(xy2d);
   niels_store(btab + j * FDGPU_BTAB_STRIDE, ypx, ymx, xy2d);
+}
+
+/* ---- fixed-base comb tables (FDGPU_BCOMB) ----
+   table i, entry j = j * 2^(W i) B as affine niels (y+x, y-x, 2dxy),
+   canonical limbs, word offset ((i * ENTRIES) + j) * STRIDE. */
+
+constexpr uint32_t BC_W = FDGPU_BCOMB_BITS, BC_NDIG = FDGPU_BCOMB_NDIG, BC_ENT = FDGPU_BCOMB_ENTRIES;
+constexpr uint32_t BC_CHUNKS = (BC_ENT + FDGPU_BCOMB_CHUNK - 1) / FDGPU_BCOMB_CHUNK;
+
+/* bases[i] = 2^(W i) B (p3, 40 words), one lane per table */
+__global__ void fdgpu_bcomb_base_kernel(uint32_t *bases) {
+  const uint32_t i = threadIdx.x;
+  if (i >= BC_NDIG) return;
+  constexpr uint32_t BX[10] = FDGPU_FE_BX, BY[10] = FDGPU_FE_BY, BT[10] = FDGPU_FE_BT;
+  ge_p3 P; fe_set(P.X, BX); fe_set(P.Y, BY); fe_1(P.Z); fe_set(P.T, BT);
+  ge_p1p1 t;
+  for (uint32_t n = 0; n < BC_W * i; n++) {
+    ge_p2 a; ge_p3_to_p2(a, P); ge_dbl(t, a); ge_p1p1_to_p3(P, t);
+  }
+  uint32_t *o = bases + 40 * i;
+#pragma unroll
+  for (int w = 0; w < 10; w++) { o[w] = P.X.v[w]; o[10 + w] = P.Y.v[w]; o[20 + w] = P.Z.v[w]; o[30 + w] = P.T.v[w]; }
+}
+
+/* One lane per (table, chunk of 64 entries): j0 * base by double-and-add,
+   then 63 consecutive additions, then one inversion for the whole chunk
+   (Montgomery's trick over the Z coordinates, prefix products in scratch). */
+__global__ void __launch_bounds__(64) fdgpu_bcomb_fill_kernel(const uint32_t *bases, uint32_t *tab,
+                                                              uint32_t *scratch) {
+  const uint32_t lane = blockIdx.x * blockDim.x + threadIdx.x;
+  if (lane >= BC_NDIG * BC_CHUNKS) return;
+  const uint32_t ti = lane / BC_CHUNKS, j0 = (lane % BC_CHUNKS) * FDGPU_BCOMB_CHUNK;
+  const uint32_t cnt = min(FDGPU_BCOMB_CHUNK, BC_ENT - j0);
+  ge_p3 base;
+  const uint32_t *b = bases + 40 * ti;
+#pragma unroll
+  for (int w = 0; w < 10; w++) { base.X.v[w] = b[w]; base.Y.v[w] = b[10 + w]; base.Z.v[w] = b[20 + w]; base.T.v[w] = b[30 + w]; }
+  ge_cached bc; ge_p3_to_cached(bc, base);
+  ge_p3 P; ge_p3_0(P);
+  ge_p1p1 t;
+  for (int bit = 15; bit >= 0; bit--) {
+    ge_p2 a; ge_p3_to_p2(a, P); ge_dbl(t, a); ge_p1p1_to_p3(P, t);
+    if ((j0 >> bit) & 1u) { ge_add_cached(t, P, bc, false); ge_p1p1_to_p3(P, t); }
+  }
+  uint32_t *pre = scratch + (size_t)lane * FDGPU_BCOMB_CHUNK * 10;
+  uint32_t *ent0 = tab + ((size_t)ti * BC_ENT + j0) * FDGPU_BCOMB_STRIDE;
+  fe acc; fe_1(acc);
+  for (uint32_t k = 0; k < cnt; k++) {
+    uint32_t *e = ent0 + (size_t)k * FDGPU_BCOMB_STRIDE;
+#pragma unroll
+    for (int w = 0; w < 10; w++) { e[w] = P.X.v[w]; e[10 + w] = P.Y.v[w]; e[20 + w] = P.Z.v[w]; }
+    fe_mul(acc, acc, P.Z);
+#pragma unroll
+    for (int w = 0; w < 10; w++) pre[10 * k + w] = acc.v[w];
+    ge_add_cached(t, P, bc, false); ge_p1p1_to_p3(P, t);
+  }
+  fe inv; fe_invert(inv, acc);
+  constexpr uint32_t D2[10] = FDGPU_FE_D2;
+  fe d2; fe_set(d2, D2);
+  for (int k = (int)cnt - 1; k >= 0; k--) {
+    uint32_t *e = ent0 + (size_t)k * FDGPU_BCOMB_STRIDE;
+    fe X, Y, Z, zi;
+#pragma unroll
+    for (int w = 0; w < 10; w++) { X.v[w] = e[w]; Y.v[w] = e[10 + w]; Z.v[w] = e[20 + w]; }
+    if (k > 0) {
+      fe pk;
+#pragma unroll
+      for (int w = 0; w < 10; w++) pk.v[w] = pre[10 * (k - 1) + w];
+      fe_mul(zi, inv, pk);
+    } else {
+      zi = inv;
+    }
+    fe_mul(inv, inv, Z);
+    fe x, y, xy, ypx, ymx, xy2d;
+    fe_mul(x, X, zi); fe_mul(y, Y, zi);
+    fe_add(ypx, y, x); fe_canon(ypx);
+    fe_sub(ymx, y, x); fe_canon(ymx);
+    fe_mul(xy, x, y); fe_mul(xy2d, xy, d2); fe_canon(xy2d);
+    niels_store(e, ypx, ymx, xy2d);
+  }
 }
 
 /* ---- per-lane A table in the global workspace ----
@@ -143,8 +238,8 @@ FDG_DEV void dsm(ge_p2 &acc2, uint32_t (&kd)[8], uint32_t (&sd)[8], const uint32
       }
       /* T of the last doubling (p1p1 -> p3 needs X'Y') */
       acc3.X = acc2.X; acc3.Y = acc2.Y; acc3.Z = acc2.Z; fe_mul(acc3.T, t.X, t.Y);
-      ge_add_cached_regs(t, acc3, q, e < 0);
-      if (h == 1) {
+      if (!FDGPU_EXP_NO_AADD) ge_add_cached_regs(t, acc3, q, e < 0);
+      if (h == 1 && !FDGPU_EXP_NO_BADD) {
         const int d = sext8(sb);
         ge_p1p1_to_p3(acc3, t);
         const uint32_t *ent = s_btab + (uint32_t)(d < 0 ? -d : d) * FDGPU_BTAB_LDS_STRIDE;
@@ -153,6 +248,96 @@ FDG_DEV void dsm(ge_p2 &acc2, uint32_t (&kd)[8], uint32_t (&sd)[8], const uint32
       }
       ge_p1p1_to_p2(acc2, t);
     }
+  }
+}
+
+/* FDGPU_BCOMB variant: R' = [k](-A) + [S]B with [S]B precomputed by the
+   comb in pass 1 and parked (cached form) in workspace entry 10.  The chain
+   only serves k: 64 windows of 4 doublings + one A-table addition; the last
+   window's sum is converted to p3 and the parked [S]B added. */
+FDG_DEV void dsm_k(ge_p2 &acc2, uint32_t (&kd)[8], const uint32_t *wsl) {
+  ge_p2_0(acc2);
+  ge_p3 acc3;
+  ge_p1p1 t;
+#pragma unroll 1
+  for (int j = 31; j >= 0; j--) {
+    const uint32_t kb = kd[7] >> 24;
+    shl8(kd);
+#pragma unroll 1
+    for (int h = 0; h < 2; h++) {
+      const int e = sext4(h == 0 ? (kb >> 4) : (kb & 15u));
+      uint32_t q[40];
+      {
+        const uint4 *ent = (const uint4 *)(wsl + (uint32_t)(e < 0 ? -e : e) * FDGPU_ATAB_WORDS);
+#pragma unroll
+        for (int i = 0; i < 10; i++) {
+          const uint4 v = ent[i];
+          q[4 * i] = v.x; q[4 * i + 1] = v.y; q[4 * i + 2] = v.z; q[4 * i + 3] = v.w;
+        }
+      }
+#pragma unroll 1
+      for (int r = 0; r < 4; r++) {
+        ge_dbl(t, acc2);
+        ge_p1p1_to_p2(acc2, t);
+      }
+      acc3.X = acc2.X; acc3.Y = acc2.Y; acc3.Z = acc2.Z; fe_mul(acc3.T, t.X, t.Y);
+      ge_add_cached_regs(t, acc3, q, e < 0);
+      if (j == 0 && h == 1) break;
+      ge_p1p1_to_p2(acc2, t);
+    }
+  }
+  /* + [S]B (parked cached form) */
+  ge_p1p1_to_p3(acc3, t);
+  uint32_t q[40];
+  {
+    const uint4 *ent = (const uint4 *)(wsl + 10u * FDGPU_ATAB_WORDS);
+#pragma unroll
+    for (int i = 0; i < 10; i++) {
+      const uint4 v = ent[i];
+      q[4 * i] = v.x; q[4 * i + 1] = v.y; q[4 * i + 2] = v.z; q[4 * i + 3] = v.w;
+    }
+  }
+  ge_add_cached_regs(t, acc3, q, false);
+  ge_p1p1_to_p2(acc2, t);
+}
+
+/* [S]B by the fixed-base comb: S (< L, or 0 for rejected lanes) in signed
+   radix 2^W; one mixed addition per digit from table i; each entry (one
+   128-B line, random across the 67-MB table) is loaded one digit ahead of
+   its use so the load latency hides behind the previous addition. */
+FDG_DEV void comb_sb(ge_p3 &acc, const uint32_t (&S)[8], const uint32_t *__restrict__ btab) {
+  constexpr int NW = (BC_NDIG + 1) / 2;
+  uint32_t dg[NW];
+  sc_recode_comb<(int)BC_W, (int)BC_NDIG>(dg, S);
+  auto next_digit = [&dg]() {
+    const int d = (int)(int16_t)(dg[0] & 0xffffu);
+#pragma unroll
+    for (int i = 0; i < NW - 1; i++) dg[i] = (dg[i] >> 16) | (dg[i + 1] << 16);
+    dg[NW - 1] >>= 16;
+    return d;
+  };
+  auto load_entry = [btab](uint32_t (&q)[32], uint32_t ti, int d) {
+    const uint4 *ent = (const uint4 *)(btab + ((size_t)ti * BC_ENT + (uint32_t)(d < 0 ? -d : d)) * FDGPU_BCOMB_STRIDE);
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+      const uint4 v = ent[i];
+      q[4 * i] = v.x; q[4 * i + 1] = v.y; q[4 * i + 2] = v.z; q[4 * i + 3] = v.w;
+    }
+  };
+  ge_p3_0(acc);
+  uint32_t qa[32], qb[32];
+  int d = next_digit();
+  load_entry(qa, 0, d);
+  ge_p1p1 t;
+#pragma unroll 1
+  for (uint32_t i = 0; i < BC_NDIG; i++) {
+    const int dn = next_digit();
+    if (i + 1 < BC_NDIG) load_entry(qb, i + 1, dn);
+    ge_add_niels_regs(t, acc, qa, d < 0);
+    ge_p1p1_to_p3(acc, t);
+#pragma unroll
+    for (int w = 0; w < 32; w++) qa[w] = qb[w];
+    d = dn;
   }
 }
 
@@ -188,7 +373,7 @@ FDG_DEV uint32_t *park_ptr(uint32_t *wsl) { return wsl + 9u * FDGPU_ATAB_WORDS; 
    tests.  Writes the table {O, -A, .., -8A}, the affine R, both digit
    strings and the pass-1 code to this lane's workspace; returns the code. */
 FDG_DEV int verify_pass1(const uint8_t *arena, const fdgpu_sig_desc_t &sd_in, uint32_t nblk_wave, uint32_t *wsl,
-                         bool ref_map) {
+                         const uint32_t *__restrict__ btab, bool ref_map) {
   uint32_t R[8], A[8];
   load32(R, arena + sd_in.sig_off);
   load32(A, arena + sd_in.pub_off);
@@ -197,7 +382,12 @@ FDG_DEV int verify_pass1(const uint8_t *arena, const fdgpu_sig_desc_t &sd_in, ui
   /* k = SHA-512(R || A || M) mod L, recoded to signed radix 16 */
   {
     uint64_t h[8];
-    sha512_hram(h, R, A, arena + sd_in.msg_off, sd_in.msg_sz, nblk_wave);
+    if (FDGPU_EXP_NO_SHA) {
+#pragma unroll
+      for (int i = 0; i < 8; i++) h[i] = ((uint64_t)R[i] << 32) | A[i];
+    } else {
+      sha512_hram(h, R, A, arena + sd_in.msg_off, sd_in.msg_sz, nblk_wave);
+    }
     uint32_t kx[16], k[8], kd[8];
 #pragma unroll
     for (int i = 0; i < 8; i++) { kx[2 * i] = bswap32((uint32_t)(h[i] >> 32)); kx[2 * i + 1] = bswap32((uint32_t)h[i]); }
@@ -209,12 +399,23 @@ FDG_DEV int verify_pass1(const uint8_t *arena, const fdgpu_sig_desc_t &sd_in, ui
   /* step 1: S < L (fd_ed25519_user.c:159-161); S recoded to signed radix 256 */
   int code;
   {
-    uint32_t S[8], sd[8];
+    uint32_t S[8];
     load32(S, arena + sd_in.sig_off + 32);
     code = sc_lt_L(S) ? 0 : -1;
+#if FDGPU_BCOMB
+    /* [S]B by the comb, parked in cached form for pass 2 (rejected S -> 0) */
+#pragma unroll
+    for (int i = 0; i < 8; i++) S[i] = code ? 0u : S[i];
+    ge_p3 SB;
+    comb_sb(SB, S, btab);
+    ge_cached c; ge_p3_to_cached(c, SB);
+    atab_store(wsl, 10, c);
+#else
+    uint32_t sd[8];
     sc_recode256(sd, S);
 #pragma unroll
     for (int i = 0; i < 8; i++) park[PARK_SD + i] = sd[i];
+#endif
   }
   /* step 2 (A): decode, small order, table of -A */
   bool a_ok, a_small;
@@ -229,7 +430,11 @@ FDG_DEV int verify_pass1(const uint8_t *arena, const fdgpu_sig_desc_t &sd_in, ui
   bool r_ok, r_small;
   {
     ge_p3 Rp;
-    r_ok = ge_decode(Rp, R, ref_map);
+    if (FDGPU_EXP_NO_RDEC) {
+      fe_frombytes(Rp.X, R); fe_frombytes(Rp.Y, A); r_ok = true;
+    } else {
+      r_ok = ge_decode(Rp, R, ref_map);
+    }
     r_small = ge_is_small_order_affine(Rp);
 #pragma unroll
     for (int i = 0; i < 10; i++) { park[PARK_XR + i] = Rp.X.v[i]; park[PARK_YR + i] = Rp.Y.v[i]; }
@@ -249,11 +454,18 @@ FDG_DEV int verify_pass2(uint32_t *wsl, const uint32_t *s_btab) {
   const int code = (int)park[PARK_CODE];
   /* wave-uniform early out when every lane already failed pass 1 */
   if (__all(code != 0)) return code;
+  ge_p2 Rc;
+#if FDGPU_BCOMB
+  uint32_t kd[8];
+#pragma unroll
+  for (int i = 0; i < 8; i++) kd[i] = park[PARK_KD + i];
+  dsm_k(Rc, kd, wsl);
+#else
   uint32_t kd[8], sd[8];
 #pragma unroll
   for (int i = 0; i < 8; i++) { kd[i] = park[PARK_KD + i]; sd[i] = park[PARK_SD + i]; }
-  ge_p2 Rc;
   dsm(Rc, kd, sd, wsl, s_btab);
+#endif
   fe l, xy;
 #pragma unroll
   for (int i = 0; i < 10; i++) xy.v[i] = park[PARK_XR + i];
@@ -273,14 +485,14 @@ FDG_DEV uint32_t *lane_ws(uint32_t *ws, uint32_t i) {
 /* Kernel 1: pass 1 (hash, scalars, decompression, small order, table). */
 __global__ void __launch_bounds__(FDGPU_BLOCK, FDGPU_PREP_WAVES)
 fdgpu_prep_kernel(const uint8_t *__restrict__ arena, const fdgpu_sig_desc_t *__restrict__ sigs, uint32_t n_sig,
-                  uint32_t *__restrict__ ws, uint32_t flags) {
+                  const uint32_t *__restrict__ btab, uint32_t *__restrict__ ws, uint32_t flags) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   const bool active = i < n_sig;
   const fdgpu_sig_desc_t d = sigs[active ? i : n_sig - 1];
   uint32_t nb = sha512_hram_blocks(d.msg_sz);      /* wave-uniform SHA block bound */
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) nb = max(nb, (uint32_t)__shfl_xor((int)nb, off));
-  verify_pass1(arena, d, nb, lane_ws(ws, i), (flags & FDGPU_FLAG_REF_MAP) != 0);
+  verify_pass1(arena, d, nb, lane_ws(ws, i), btab, (flags & FDGPU_FLAG_REF_MAP) != 0);
 }
 
 /* Kernel 2: pass 2 (double-scalar multiplication and compare). */
@@ -288,10 +500,14 @@ __global__ void __launch_bounds__(FDGPU_BLOCK, FDGPU_DSM_WAVES)
 fdgpu_dsm_kernel(uint32_t n_sig, const uint32_t *__restrict__ btab, uint32_t *__restrict__ ws,
                  int8_t *__restrict__ codes) {
   /* odd LDS stride: lanes reading word w of different entries hit different banks */
+#if FDGPU_BCOMB
+  const uint32_t *s_btab = nullptr;                   /* [S]B comes from the comb (pass 1) */
+#else
   __shared__ uint32_t s_btab[FDGPU_BTAB_ENTRIES * FDGPU_BTAB_LDS_STRIDE];
   for (uint32_t i = threadIdx.x; i < FDGPU_BTAB_ENTRIES * FDGPU_BTAB_STRIDE; i += blockDim.x)
     s_btab[(i / FDGPU_BTAB_STRIDE) * FDGPU_BTAB_LDS_STRIDE + i % FDGPU_BTAB_STRIDE] = btab[i];
   __syncthreads();
+#endif
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   const int code = verify_pass2(lane_ws(ws, i), s_btab);
   if (i < n_sig) codes[i] = (int8_t)code;
@@ -302,10 +518,14 @@ __global__ void __launch_bounds__(FDGPU_BLOCK, FDGPU_PREP_WAVES)
 fdgpu_fused_kernel(const uint8_t *__restrict__ arena, const fdgpu_sig_desc_t *__restrict__ sigs, uint32_t n_sig,
                    const uint32_t *__restrict__ btab, uint32_t *__restrict__ ws, int8_t *__restrict__ codes,
                    uint32_t flags) {
+#if FDGPU_BCOMB
+  const uint32_t *s_btab = nullptr;                   /* [S]B comes from the comb (pass 1) */
+#else
   __shared__ uint32_t s_btab[FDGPU_BTAB_ENTRIES * FDGPU_BTAB_LDS_STRIDE];
   for (uint32_t i = threadIdx.x; i < FDGPU_BTAB_ENTRIES * FDGPU_BTAB_STRIDE; i += blockDim.x)
     s_btab[(i / FDGPU_BTAB_STRIDE) * FDGPU_BTAB_LDS_STRIDE + i % FDGPU_BTAB_STRIDE] = btab[i];
   __syncthreads();
+#endif
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   const bool active = i < n_sig;
   const fdgpu_sig_desc_t d = sigs[active ? i : n_sig - 1];
@@ -313,7 +533,7 @@ fdgpu_fused_kernel(const uint8_t *__restrict__ arena, const fdgpu_sig_desc_t *__
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) nb = max(nb, (uint32_t)__shfl_xor((int)nb, off));
   uint32_t *wsl = lane_ws(ws, i);
-  verify_pass1(arena, d, nb, wsl, (flags & FDGPU_FLAG_REF_MAP) != 0);
+  verify_pass1(arena, d, nb, wsl, btab, (flags & FDGPU_FLAG_REF_MAP) != 0);
   const int code = verify_pass2(wsl, s_btab);
   if (active) codes[i] = (int8_t)code;
 }
@@ -437,9 +657,37 @@ __global__ void __launch_bounds__(64) fdgpu_test_sc_reduce_kernel(const uint32_t
 
 extern "C" {
 
-hipError_t fdgpu_launch_btab_init(uint32_t *d_btab, hipStream_t stream) {
+size_t fdgpu_btab_bytes(void) {
+#if FDGPU_BCOMB
+  return (size_t)BC_NDIG * BC_ENT * FDGPU_BCOMB_STRIDE * sizeof(uint32_t);
+#else
+  return (size_t)FDGPU_BTAB_ENTRIES * FDGPU_BTAB_STRIDE * sizeof(uint32_t);
+#endif
+}
+
+hipError_t fdgpu_btab_build(uint32_t *d_btab, hipStream_t stream) {
+#if FDGPU_BCOMB
+  uint32_t *bases = nullptr, *scratch = nullptr;
+  const uint32_t lanes = BC_NDIG * BC_CHUNKS;
+  hipError_t e = hipMalloc((void **)&bases, BC_NDIG * 40 * sizeof(uint32_t));
+  if (e == hipSuccess) e = hipMalloc((void **)&scratch, (size_t)lanes * FDGPU_BCOMB_CHUNK * 10 * sizeof(uint32_t));
+  if (e == hipSuccess) {
+    hipLaunchKernelGGL(fdgpu_bcomb_base_kernel, dim3(1), dim3(64), 0, stream, bases);
+    e = hipGetLastError();
+  }
+  if (e == hipSuccess) {
+    hipLaunchKernelGGL(fdgpu_bcomb_fill_kernel, dim3((lanes + 63) / 64), dim3(64), 0, stream, bases, d_btab, scratch);
+    e = hipGetLastError();
+  }
+  if (e == hipSuccess) e = hipStreamSynchronize(stream);
+  if (bases) (void)hipFree(bases);
+  if (scratch) (void)hipFree(scratch);
+  return e;
+#else
   hipLaunchKernelGGL(fdgpu_btab_init_kernel, dim3(1), dim3(192), 0, stream, d_btab);
-  return hipGetLastError();
+  hipError_t e = hipGetLastError();
+  return e == hipSuccess ? hipStreamSynchronize(stream) : e;
+#endif
 }
 
 hipError_t fdgpu_verify_occupancy(int *blocks_per_cu) {
@@ -465,7 +713,8 @@ hipError_t fdgpu_launch_verify_sigs(const uint8_t *d_arena, const fdgpu_sig_desc
                      d_sig_codes, flags);
   return hipGetLastError();
 #endif
-  hipLaunchKernelGGL(fdgpu_prep_kernel, dim3(grid), dim3(FDGPU_BLOCK), 0, stream, d_arena, d_sigs, n_sig, d_ws, flags);
+  hipLaunchKernelGGL(fdgpu_prep_kernel, dim3(grid), dim3(FDGPU_BLOCK), 0, stream, d_arena, d_sigs, n_sig, d_btab, d_ws,
+                     flags);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(fdgpu_dsm_kernel, dim3(grid), dim3(FDGPU_BLOCK), 0, stream, n_sig, d_btab, d_ws, d_sig_codes);

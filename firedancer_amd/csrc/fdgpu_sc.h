@@ -128,4 +128,25 @@ FDG_DEV void sc_recode256(uint32_t (&out)[8], const uint32_t (&s)[8]) {
   }
 }
 
+/* Signed radix-2^W digits of S for the fixed-base comb (W = FDGPU_BCOMB_BITS):
+   NDIG digits d_i in [-2^(W-1), 2^(W-1)], S = sum d_i 2^(W i), packed as
+   int16 slots (two per word, digit 0 in the low half of word 0).  Needs
+   S < 2^(W NDIG - 1) (callers pass S < L or 0). */
+template <int W, int NDIG>
+FDG_DEV void sc_recode_comb(uint32_t (&out)[(NDIG + 1) / 2], const uint32_t (&s)[8]) {
+  uint32_t carry = 0;
+#pragma unroll
+  for (int i = 0; i < (NDIG + 1) / 2; i++) out[i] = 0;
+#pragma unroll
+  for (int i = 0; i < NDIG; i++) {
+    const int bit = W * i, wd = bit >> 5, sh = bit & 31;
+    uint64_t x = wd < 8 ? s[wd] : 0u;
+    if (wd + 1 < 8) x |= (uint64_t)s[wd + 1] << 32;
+    const uint32_t e = (uint32_t)((x >> sh) & ((1ull << W) - 1)) + carry;
+    carry = e >= (1u << (W - 1)) ? 1u : 0u;
+    const uint32_t d = (e - (carry << W)) & 0xffffu;   /* int16 two's complement */
+    out[i >> 1] |= d << (16 * (i & 1));
+  }
+}
+
 }  // namespace fdgpu
