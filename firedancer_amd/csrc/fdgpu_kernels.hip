@@ -50,6 +50,9 @@ using namespace fdgpu;
 #ifndef FDGPU_EXP_NO_SHA
 #define FDGPU_EXP_NO_SHA 0
 #endif
+#ifndef FDGPU_RAVOID
+#define FDGPU_RAVOID 1        /* 1: compare R' with R's encoding (batched inversion), decode R only for failures */
+#endif
 #ifndef FDGPU_DSM_WAVES
 #define FDGPU_DSM_WAVES 3     /* ~130 VGPRs: 3 waves per SIMD, no spills */
 #endif
@@ -365,6 +368,9 @@ FDG_DEV void atab_build(uint32_t *wsl, const ge_p3 &An) {
 #define PARK_KD 20
 #define PARK_SD 28
 #define PARK_CODE 36
+/* R-avoiding path (FDGPU_RAVOID): flag bits above the int8 code in PARK_CODE */
+#define RA_ASMALL (1u << 8)
+#define RA_YMATCH (1u << 9)
 
 FDG_DEV uint32_t *park_ptr(uint32_t *wsl) { return wsl + 9u * FDGPU_ATAB_WORDS; }
 
@@ -372,6 +378,7 @@ FDG_DEV uint32_t *park_ptr(uint32_t *wsl) { return wsl + 9u * FDGPU_ATAB_WORDS; 
    1-5): S < L, k = SHA-512(R||A||M) mod L, decode A then R, small-order
    tests.  Writes the table {O, -A, .., -8A}, the affine R, both digit
    strings and the pass-1 code to this lane's workspace; returns the code. */
+template <bool DECODE_R = true>
 FDG_DEV int verify_pass1(const uint8_t *arena, const fdgpu_sig_desc_t &sd_in, uint32_t nblk_wave, uint32_t *wsl,
                          const uint32_t *__restrict__ btab, bool ref_map) {
   uint32_t R[8], A[8];
@@ -425,6 +432,13 @@ FDG_DEV int verify_pass1(const uint8_t *arena, const fdgpu_sig_desc_t &sd_in, ui
     a_small = ge_is_small_order_affine(Ap);
     ge_p3 An; ge_p3_neg(An, Ap);
     atab_build(wsl, An);
+  }
+  if (!DECODE_R) {
+    /* R is resolved after the scalar multiplication (fdgpu_finish_kernel):
+       park the S / A verdict and A's small-order bit only */
+    if (code == 0 && !a_ok) code = ref_map ? -2 : -1;
+    park[PARK_CODE] = ((uint32_t)code & 0xffu) | (a_small ? RA_ASMALL : 0u);
+    return code;
   }
   /* step 2 (R): decode, small order; park affine x_R, y_R */
   bool r_ok, r_small;
@@ -536,6 +550,234 @@ fdgpu_fused_kernel(const uint8_t *__restrict__ arena, const fdgpu_sig_desc_t *__
   verify_pass1(arena, d, nb, wsl, btab, (flags & FDGPU_FLAG_REF_MAP) != 0);
   const int code = verify_pass2(wsl, s_btab);
   if (active) codes[i] = (int8_t)code;
+}
+
+/* ---------------- R-avoiding verify (FDGPU_RAVOID) ----------------
+   The reference decompresses R (a 2^252-3 exponentiation) only to compare it
+   with R' = [S]B - [k]A (fd_ed25519_user.c:164-229).  Here R' is compared on
+   its encoding instead: y_R (the encoded y, reduced mod p) must equal Y/Z,
+   and the parity of the canonical x = X/Z must equal R's sign bit.  The
+   one inversion of Z this needs is batched (Montgomery's trick): a
+   workgroup-wide product scan of Z in the verify kernel, one inversion per
+   workgroup in fdgpu_wginv_kernel, and 3 products per signature in
+   fdgpu_finish_kernel.  Equal y determines the decoded R up to the sign of
+   x, so every code of fd_ed25519_user.c follows without decompressing R:
+     y match, parity match      -> R = R' (x = 0 included):  small(R) ? ERR_SIG : SUCCESS
+     y match, parity mismatch   -> x = 0: decode fails (AVX) / R small (ref): ERR_SIG
+                                   else R = -R':             small(R) ? ERR_SIG : ERR_MSG
+   Signatures whose y differs, or whose A is small order (the R decode verdict
+   then outranks ERR_PUBKEY), are queued and finished by fdgpu_slow_kernel
+   with the full R decode, as the reference does. */
+
+FDG_DEV void fe_shfl_up(fe &o, const fe &a, int off) {
+#pragma unroll
+  for (int i = 0; i < 10; i++) o.v[i] = (uint32_t)__shfl_up((int)a.v[i], off, 64);
+}
+FDG_DEV void fe_shfl_down(fe &o, const fe &a, int off) {
+#pragma unroll
+  for (int i = 0; i < 10; i++) o.v[i] = (uint32_t)__shfl_down((int)a.v[i], off, 64);
+}
+
+/* Exclusive prefix and suffix products of z over the workgroup (256 lanes =
+   4 waves): within a wave by log-step shuffles, across waves through LDS.
+   Thread 0 writes the workgroup's total product. */
+FDG_DEV void wg_scan(const fe &z, fe &pex, fe &sex, uint32_t *tot_out) {
+  __shared__ uint32_t s_tot[FDGPU_BLOCK / 64][10];
+  const int lane = (int)(threadIdx.x & 63u), wv = (int)(threadIdx.x >> 6);
+  fe p = z, q = z, t, m;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    fe_shfl_up(t, p, off);
+    fe_mul(m, p, t);
+    fe_cmov(p, m, p, lane >= off);
+    fe_shfl_down(t, q, off);
+    fe_mul(m, q, t);
+    fe_cmov(q, m, q, lane + off < 64);
+  }
+  fe one; fe_1(one);
+  fe_shfl_up(t, p, 1);   fe_cmov(pex, one, t, lane == 0);
+  fe_shfl_down(t, q, 1); fe_cmov(sex, one, t, lane == 63);
+  if (lane == 63) {
+#pragma unroll
+    for (int i = 0; i < 10; i++) s_tot[wv][i] = p.v[i];
+  }
+  __syncthreads();
+  fe pre, suf, w;
+  fe_1(pre); fe_1(suf);
+#pragma unroll
+  for (int v = 0; v < (int)(FDGPU_BLOCK / 64); v++) {
+#pragma unroll
+    for (int i = 0; i < 10; i++) w.v[i] = s_tot[v][i];
+    if (v < wv) fe_mul(pre, pre, w);          /* wave-uniform branches */
+    if (v > wv) fe_mul(suf, suf, w);
+  }
+  fe_mul(pex, pex, pre);
+  fe_mul(sex, sex, suf);
+  if (threadIdx.x == 63) {                    /* wave 0's inclusive total x waves 1..3 */
+    fe all; fe_mul(all, p, suf);
+#pragma unroll
+    for (int i = 0; i < 10; i++) tot_out[i] = all.v[i];
+  }
+}
+
+/* Kernel A: pass 1 without R, [S]B - [k]A, y check, Z scan; parks
+   X, Y, Z (entry 9 words 0-29), the exclusive prefix (entry 9 words 30-39)
+   and suffix (entry 10 words 0-9) products and the flags (entry 10 word 10). */
+__global__ void __launch_bounds__(FDGPU_BLOCK, FDGPU_PREP_WAVES)
+fdgpu_verify_ra_kernel(const uint8_t *__restrict__ arena, const fdgpu_sig_desc_t *__restrict__ sigs, uint32_t n_sig,
+                       const uint32_t *__restrict__ btab, uint32_t *__restrict__ ws, uint32_t *__restrict__ wg_tot,
+                       uint32_t *__restrict__ queue, uint32_t *__restrict__ queue_cnt, uint32_t flags) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  const bool active = i < n_sig;
+  const fdgpu_sig_desc_t d = sigs[active ? i : n_sig - 1];
+  uint32_t nb = sha512_hram_blocks(d.msg_sz);
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) nb = max(nb, (uint32_t)__shfl_xor((int)nb, off));
+  uint32_t *wsl = lane_ws(ws, i);
+  uint32_t *park = park_ptr(wsl);
+  const int code1 = verify_pass1<false>(arena, d, nb, wsl, btab, (flags & FDGPU_FLAG_REF_MAP) != 0);
+  const bool need = active && code1 == 0;
+  ge_p2 Rc;
+  if (__any(need)) {
+    uint32_t kd[8];
+#pragma unroll
+    for (int k = 0; k < 8; k++) kd[k] = park[PARK_KD + k];
+    dsm_k(Rc, kd, wsl);
+  } else {
+    ge_p2_0(Rc);
+  }
+  uint32_t Renc[8];
+  load32(Renc, arena + d.sig_off);
+  fe yR, t;
+  fe_frombytes(yR, Renc);
+  fe_mul(t, yR, Rc.Z);
+  const bool ymatch = fe_eq(Rc.Y, t);
+  fe z, one; fe_1(one);
+  fe_cmov(z, Rc.Z, one, need && !fe_iszero(Rc.Z));
+  const uint32_t fl = park[PARK_CODE] | (ymatch ? RA_YMATCH : 0u);
+  const bool slow = need && ((fl & RA_ASMALL) || !ymatch);
+  if (slow) {                                  /* only the slow path needs R' itself */
+#pragma unroll
+    for (int k = 0; k < 10; k++) { park[k] = Rc.X.v[k]; park[10 + k] = Rc.Y.v[k]; park[20 + k] = Rc.Z.v[k]; }
+  }
+  /* queue the slow signatures (one atomic per wave; waves finish spread over
+     the kernel's lifetime, so the counter is not contended) */
+  {
+    const uint64_t m = __ballot(slow);
+    if (m) {
+      const int lane = (int)(threadIdx.x & 63u);
+      const int leader = __ffsll((long long)m) - 1;
+      uint32_t base = 0;
+      if (lane == leader) base = atomicAdd(queue_cnt, (uint32_t)__popcll(m));
+      base = (uint32_t)__shfl((int)base, leader, 64);
+      if (slow) queue[base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull))] = i;
+    }
+  }
+  fe pex, sex;
+  wg_scan(z, pex, sex, wg_tot + (size_t)blockIdx.x * 10);
+  /* U = X * (product of every other Z in the workgroup): x = U / (all Z) */
+  fe U;
+  fe_mul(U, Rc.X, pex);
+  fe_mul(U, U, sex);
+  uint4 *o = (uint4 *)(park + 32);             /* words 32-43 (16-B aligned): U, flags */
+  o[0] = make_uint4(U.v[0], U.v[1], U.v[2], U.v[3]);
+  o[1] = make_uint4(U.v[4], U.v[5], U.v[6], U.v[7]);
+  o[2] = make_uint4(U.v[8], U.v[9], fl, 0u);
+}
+
+/* Inverse of one workgroup's Z product (Kernel B's work, run by the extra
+   blocks of fdgpu_tail_kernel). */
+FDG_DEV void wg_invert(const uint32_t *__restrict__ wg_tot, uint32_t *__restrict__ wg_inv, uint32_t g) {
+  fe a, r;
+#pragma unroll
+  for (int k = 0; k < 10; k++) a.v[k] = wg_tot[10 * g + k];
+  fe_invert(r, a);
+#pragma unroll
+  for (int k = 0; k < 10; k++) wg_inv[10 * g + k] = r.v[k];
+}
+
+/* Kernel C: finish each signature from its y check and the parity of
+   x = X / Z (Z^-1 = workgroup inverse x prefix x suffix); queue the rest. */
+__global__ void __launch_bounds__(FDGPU_BLOCK) fdgpu_finish_kernel(
+    const uint8_t *__restrict__ arena, const fdgpu_sig_desc_t *__restrict__ sigs, uint32_t n_sig,
+    const uint32_t *__restrict__ ws, const uint32_t *__restrict__ wg_inv, int8_t *__restrict__ codes) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  const bool active = i < n_sig;
+  const uint32_t *park = ws + (size_t)(active ? i : 0) * FDGPU_WS_LANE_WORDS + 9u * FDGPU_ATAB_WORDS;
+  const uint4 *pv = (const uint4 *)(park + 32);
+  const uint4 u0 = pv[0], u1 = pv[1], u2 = pv[2];
+  const uint32_t fl = u2.z;
+  const int code1 = (int)(int8_t)(fl & 0xffu);
+  const bool slow = active && code1 == 0 && ((fl & RA_ASMALL) || !(fl & RA_YMATCH));
+  int code = code1;
+  if (__any(active && code1 == 0 && !slow)) {
+    fe U, inv, x;
+    U.v[0] = u0.x; U.v[1] = u0.y; U.v[2] = u0.z; U.v[3] = u0.w; U.v[4] = u1.x; U.v[5] = u1.y; U.v[6] = u1.z;
+    U.v[7] = u1.w; U.v[8] = u2.x; U.v[9] = u2.y;
+#pragma unroll
+    for (int k = 0; k < 10; k++) inv.v[k] = wg_inv[10 * blockIdx.x + k];
+    fe_mul(x, U, inv);
+    fe_canon(x);
+    uint32_t xnz = 0;
+#pragma unroll
+    for (int k = 0; k < 10; k++) xnz |= x.v[k];
+    uint32_t Renc[8];
+    load32(Renc, arena + sigs[active ? i : 0].sig_off);
+    ge_p3 Rp;                                  /* affine (x, y) with y = y_R: only x==0 and y feed the test */
+    Rp.X = x; fe_frombytes(Rp.Y, Renc);
+    const bool small = ge_is_small_order_affine(Rp);
+    const uint32_t sign = Renc[7] >> 31;
+    int c;
+    if ((x.v[0] & 1u) == sign) c = small ? -1 : 0;
+    else if (xnz == 0) c = -1;
+    else c = small ? -1 : -3;
+    if (active && code1 == 0 && !slow) code = c;
+  }
+  if (active && !slow) codes[i] = (int8_t)code;
+}
+
+/* Kernel D: the queued signatures, with the reference's full R decode
+   (fd_ed25519_user.c:164-229 order: R decode failure, A small, R small,
+   equation). */
+/* Kernel B+D (one launch, both latency-bound): blocks [0, slow_blocks) run
+   the queued signatures grid-stride; the remaining blocks invert the
+   workgroup Z products, one per thread. */
+__global__ void __launch_bounds__(FDGPU_BLOCK, FDGPU_PREP_WAVES) fdgpu_tail_kernel(
+    const uint8_t *__restrict__ arena, const fdgpu_sig_desc_t *__restrict__ sigs, const uint32_t *__restrict__ ws,
+    int8_t *__restrict__ codes, const uint32_t *__restrict__ queue, const uint32_t *__restrict__ queue_cnt,
+    const uint32_t *__restrict__ wg_tot, uint32_t *__restrict__ wg_inv, uint32_t n_wg, uint32_t slow_blocks,
+    uint32_t flags) {
+  if (blockIdx.x >= slow_blocks) {
+    const uint32_t g = (blockIdx.x - slow_blocks) * blockDim.x + threadIdx.x;
+    if (g < n_wg) wg_invert(wg_tot, wg_inv, g);
+    return;
+  }
+  const uint32_t cnt = *queue_cnt;
+  for (uint32_t q = blockIdx.x * blockDim.x + threadIdx.x; q < cnt; q += slow_blocks * blockDim.x) {
+  const uint32_t i = queue[q];
+  const uint32_t *wsl = ws + (size_t)i * FDGPU_WS_LANE_WORDS;
+  const uint32_t *park = wsl + 9u * FDGPU_ATAB_WORDS;
+  const uint32_t fl = park[42];
+  uint32_t Renc[8];
+  load32(Renc, arena + sigs[i].sig_off);
+  ge_p3 Rp;
+  const bool r_ok = ge_decode(Rp, Renc, (flags & FDGPU_FLAG_REF_MAP) != 0);
+  int code;
+  if (!r_ok) code = -1;
+  else if (fl & RA_ASMALL) code = -2;
+  else if (ge_is_small_order_affine(Rp)) code = -1;
+  else {
+    fe X, Y, Z, l;
+#pragma unroll
+    for (int k = 0; k < 10; k++) { X.v[k] = park[k]; Y.v[k] = park[10 + k]; Z.v[k] = park[20 + k]; }
+    fe_mul(l, Rp.X, Z);
+    bool eq = fe_eq(X, l);
+    fe_mul(l, Rp.Y, Z);
+    eq = eq && fe_eq(Y, l);
+    code = eq ? 0 : -3;
+  }
+  codes[i] = (int8_t)code;
+  }
 }
 
 __global__ void fdgpu_combine_kernel(const fdgpu_txn_desc_t *__restrict__ txns, uint32_t n_txn,
@@ -698,9 +940,11 @@ hipError_t fdgpu_verify_occupancy(int *blocks_per_cu) {
 #endif
 }
 
+/* workspace: per-lane words, then (FDGPU_RAVOID) per-workgroup Z products
+   and their inverses, the slow-path queue and its counter */
 size_t fdgpu_ws_bytes(uint64_t n_sig) {
-  const uint64_t lanes = (n_sig + FDGPU_BLOCK - 1) / FDGPU_BLOCK * FDGPU_BLOCK;
-  return (size_t)lanes * FDGPU_WS_LANE_WORDS * sizeof(uint32_t);
+  const uint64_t grid = (n_sig + FDGPU_BLOCK - 1) / FDGPU_BLOCK, lanes = grid * FDGPU_BLOCK;
+  return (size_t)(lanes * FDGPU_WS_LANE_WORDS + 20 * grid + lanes + 16) * sizeof(uint32_t);
 }
 
 hipError_t fdgpu_launch_verify_sigs(const uint8_t *d_arena, const fdgpu_sig_desc_t *d_sigs, uint32_t n_sig,
@@ -708,6 +952,24 @@ hipError_t fdgpu_launch_verify_sigs(const uint8_t *d_arena, const fdgpu_sig_desc
                                     hipStream_t stream) {
   if (!n_sig) return hipSuccess;
   const uint32_t grid = (n_sig + FDGPU_BLOCK - 1) / FDGPU_BLOCK;
+#if FDGPU_RAVOID
+  {
+    const size_t lanes = (size_t)grid * FDGPU_BLOCK;
+    uint32_t *wg_tot = d_ws + lanes * FDGPU_WS_LANE_WORDS, *wg_inv = wg_tot + 10 * (size_t)grid;
+    uint32_t *queue = wg_inv + 10 * (size_t)grid, *cnt = queue + lanes;
+    hipError_t e = hipMemsetAsync(cnt, 0, sizeof(uint32_t), stream);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(fdgpu_verify_ra_kernel, dim3(grid), dim3(FDGPU_BLOCK), 0, stream, d_arena, d_sigs, n_sig, d_btab,
+                       d_ws, wg_tot, queue, cnt, flags);
+    /* slow path sized for ~1/8 of the signatures per pass (grid-stride beyond) */
+    const uint32_t slow_blocks = (grid + 7) / 8, inv_blocks = (grid + FDGPU_BLOCK - 1) / FDGPU_BLOCK;
+    hipLaunchKernelGGL(fdgpu_tail_kernel, dim3(slow_blocks + inv_blocks), dim3(FDGPU_BLOCK), 0, stream, d_arena,
+                       d_sigs, d_ws, d_sig_codes, queue, cnt, wg_tot, wg_inv, grid, slow_blocks, flags);
+    hipLaunchKernelGGL(fdgpu_finish_kernel, dim3(grid), dim3(FDGPU_BLOCK), 0, stream, d_arena, d_sigs, n_sig, d_ws,
+                       wg_inv, d_sig_codes);
+    return hipGetLastError();
+  }
+#endif
 #if FDGPU_FUSED
   hipLaunchKernelGGL(fdgpu_fused_kernel, dim3(grid), dim3(FDGPU_BLOCK), 0, stream, d_arena, d_sigs, n_sig, d_btab, d_ws,
                      d_sig_codes, flags);
