@@ -3,7 +3,8 @@
 Usage: python tools/pmc_summary.py <tag> <dir_pass1> [<dir_pass2> ...]
 (env PMC_OUT_DIR overrides the output directory, default profiles/)
 Each dir holds one rocprofv3 `--pmc ... -o run --output-format csv` pass.
-Reports per launch of the verify kernel (KERNEL): FETCH_SIZE / WRITE_SIZE (KB as
+Reports per launch of the verify pipeline (KERNELS: the main verify kernel
+and its tail kernels, summed; per-kernel medians kept): FETCH_SIZE / WRITE_SIZE (KB as
 rocprofv3 reports them, and HBM bytes with the gfx950 FETCH_SIZE x2
 correction of MI355X_MICROARCH.md §HBM), VALU instruction mix and busy
 fractions.  The per-launch HBM bytes feed bench.py's roofline.traffic.
@@ -15,35 +16,47 @@ import os
 import sys
 from collections import defaultdict
 
-KERNEL = "fdgpu_fused_kernel"
+PIPELINE = "verify pipeline"
+# the launches of one fdgpu_launch_verify_sigs (R-avoiding path), or the single
+# fused kernel of the FDGPU_RAVOID=0 build
+KERNELS = ("fdgpu_verify_ra_kernel", "fdgpu_tail_kernel", "fdgpu_finish_kernel", "fdgpu_fused_kernel")
 
 
 def read_pass(d):
     files = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
-    vals = defaultdict(list)
+    vals = defaultdict(lambda: defaultdict(list))      # kernel -> counter -> per-dispatch values
     meta = {}
     for f in files:
         with open(f) as fh:
             for row in csv.DictReader(fh):
-                if KERNEL not in row.get("Kernel_Name", ""):
+                name = next((k for k in KERNELS if k in row.get("Kernel_Name", "")), None)
+                if name is None:
                     continue
-                vals[row["Counter_Name"]].append(float(row["Counter_Value"]))
-                meta = {k: row.get(k) for k in ("Grid_Size", "Workgroup_Size", "LDS_Block_Size", "Scratch_Size",
-                                                "VGPR_Count", "Accum_VGPR_Count", "SGPR_Count") if k in row}
+                vals[name][row["Counter_Name"]].append(float(row["Counter_Value"]))
+                if name in ("fdgpu_verify_ra_kernel", "fdgpu_fused_kernel"):
+                    meta = {k: row.get(k) for k in ("Grid_Size", "Workgroup_Size", "LDS_Block_Size", "Scratch_Size",
+                                                    "VGPR_Count", "Accum_VGPR_Count", "SGPR_Count") if k in row}
     return vals, meta
 
 
 def main():
     tag, dirs = sys.argv[1], sys.argv[2:]
-    agg, meta = {}, {}
+    per_kernel, meta = defaultdict(dict), {}
     for d in dirs:
         v, m = read_pass(d)
         meta.update(m)
-        for k, xs in v.items():
-            # several dispatches (warmup + steps): keep the median per launch
-            xs = sorted(xs)
-            agg[k] = xs[len(xs) // 2]
-    out = {"kernel": KERNEL, "counters_per_launch_median": agg, "dispatch": meta}
+        for kern, cs in v.items():
+            for k, xs in cs.items():
+                # several dispatches (warmup + steps): keep the median per launch
+                xs = sorted(xs)
+                per_kernel[kern][k] = xs[len(xs) // 2]
+    agg = defaultdict(float)
+    for cs in per_kernel.values():
+        for k, x in cs.items():
+            agg[k] += x
+    agg = dict(agg)
+    out = {"kernel": PIPELINE, "kernels": sorted(per_kernel), "counters_per_launch_median": agg,
+           "per_kernel": per_kernel, "dispatch": meta}
     if "FETCH_SIZE" in agg:
         out["fetch_kb_reported"] = agg["FETCH_SIZE"]
         out["read_bytes_corrected"] = agg["FETCH_SIZE"] * 1024 * 2
