@@ -27,7 +27,11 @@ typedef struct {
 #define FDGPU_ARENA_SLACK   160u          /* readable bytes past the arena (SHA block loads) */
 #define FDGPU_BTAB_ENTRIES  129u          /* 0 (identity), 1B .. 128B */
 #define FDGPU_BTAB_STRIDE   32u           /* u32 per niels entry (30 used) */
-#define FDGPU_ATAB_ENTRIES  9u            /* 0 (identity), 1A .. 8A (A negated) */
+/* k in signed radix 2^FDGPU_KWIN (4: 64 windows over {O,..,8A}; 5: 51 windows over {O,..,16A}) */
+#ifndef FDGPU_KWIN
+#define FDGPU_KWIN 4
+#endif
+#define FDGPU_ATAB_ENTRIES  ((1u << (FDGPU_KWIN - 1)) + 1u)   /* 0 (identity), 1A .. 2^(w-1) A (A negated) */
 #define FDGPU_ATAB_WORDS    40u           /* u32 per cached entry */
 /* Fixed-base comb for [S]B (FDGPU_BCOMB=1): S in signed radix 2^W, digit i
    looked up in table i = {0, 1, .., 2^(W-1)} x 2^(W i) B (affine niels, one
@@ -44,8 +48,10 @@ typedef struct {
 #define FDGPU_BCOMB_ENTRIES ((1u << (FDGPU_BCOMB_BITS - 1u)) + 1u)
 #define FDGPU_BCOMB_STRIDE  32u           /* u32 per entry (30 used): one 128-B line */
 #define FDGPU_BCOMB_CHUNK   64u           /* entries per lane in the table build (one batch inversion) */
-#define FDGPU_WS_ENTRIES    11u           /* per-lane workspace: A table, parked (x_R, y_R, digits), cached [S]B */
-#define FDGPU_WS_LANE_WORDS (FDGPU_WS_ENTRIES * FDGPU_ATAB_WORDS)   /* 1760 B per signature */
+#define FDGPU_WS_PARK       FDGPU_ATAB_ENTRIES          /* entry: digits, codes, R', U */
+#define FDGPU_WS_SB         (FDGPU_ATAB_ENTRIES + 1u)   /* entry: [S]B in cached form */
+#define FDGPU_WS_ENTRIES    (FDGPU_ATAB_ENTRIES + 2u)   /* per-lane workspace: A table, park, [S]B */
+#define FDGPU_WS_LANE_WORDS (FDGPU_WS_ENTRIES * FDGPU_ATAB_WORDS)   /* 1760 B per signature (w = 4) */
 #define FDGPU_BTAB_LDS_STRIDE 33u         /* B-table entry stride in LDS (odd: no bank conflicts) */
 #define FDGPU_BLOCK         256u
 #define FDGPU_FLAG_REF_MAP  1u            /* portable-backend error mapping */

@@ -202,6 +202,12 @@ FDG_DEV void atab_store(uint32_t *wsl, uint32_t entry, const ge_cached &c) {
 FDG_DEV int sext4(uint32_t x) { return ((int)(x << 28)) >> 28; }
 FDG_DEV int sext8(uint32_t x) { return ((int)(x << 24)) >> 24; }
 
+#if FDGPU_KWIN == 5
+#define KD_WORDS 13       /* 51 signed radix-32 digits, one per byte (byte j+1) */
+#else
+#define KD_WORDS 8        /* 64 signed radix-16 digits, one per nibble */
+#endif
+
 /* shift a 256-bit little-endian word vector left by 8 bits */
 FDG_DEV void shl8(uint32_t (&w)[8]) {
 #pragma unroll
@@ -258,7 +264,40 @@ FDG_DEV void dsm(ge_p2 &acc2, uint32_t (&kd)[8], uint32_t (&sd)[8], const uint32
    comb in pass 1 and parked (cached form) in workspace entry 10.  The chain
    only serves k: 64 windows of 4 doublings + one A-table addition; the last
    window's sum is converted to p3 and the parked [S]B added. */
-FDG_DEV void dsm_k(ge_p2 &acc2, uint32_t (&kd)[8], const uint32_t *wsl) {
+#if FDGPU_KWIN == 5
+FDG_DEV void dsm_k(ge_p2 &acc2, uint32_t (&kd)[KD_WORDS], const uint32_t *wsl) {
+  ge_p2_0(acc2);
+  ge_p3 acc3;
+  ge_p1p1 t;
+  /* digit j (0..50) sits in byte j + 1; the top byte of the top word is read
+     and the string shifted left by one byte per window */
+#pragma unroll 1
+  for (int j = 50; j >= 0; j--) {
+    const int e = ((int)kd[KD_WORDS - 1]) >> 24;
+#pragma unroll
+    for (int w = KD_WORDS - 1; w > 0; w--) kd[w] = (kd[w] << 8) | (kd[w - 1] >> 24);
+    kd[0] <<= 8;
+    uint32_t q[40];
+    {
+      const uint4 *ent = (const uint4 *)(wsl + (uint32_t)(e < 0 ? -e : e) * FDGPU_ATAB_WORDS);
+#pragma unroll
+      for (int i = 0; i < 10; i++) {
+        const uint4 v = ent[i];
+        q[4 * i] = v.x; q[4 * i + 1] = v.y; q[4 * i + 2] = v.z; q[4 * i + 3] = v.w;
+      }
+    }
+#pragma unroll 1
+    for (int r = 0; r < 5; r++) {
+      ge_dbl(t, acc2);
+      ge_p1p1_to_p2(acc2, t);
+    }
+    acc3.X = acc2.X; acc3.Y = acc2.Y; acc3.Z = acc2.Z; fe_mul(acc3.T, t.X, t.Y);
+    ge_add_cached_regs(t, acc3, q, e < 0);
+    if (j == 0) break;
+    ge_p1p1_to_p2(acc2, t);
+  }
+#else
+FDG_DEV void dsm_k(ge_p2 &acc2, uint32_t (&kd)[KD_WORDS], const uint32_t *wsl) {
   ge_p2_0(acc2);
   ge_p3 acc3;
   ge_p1p1 t;
@@ -289,11 +328,12 @@ FDG_DEV void dsm_k(ge_p2 &acc2, uint32_t (&kd)[8], const uint32_t *wsl) {
       ge_p1p1_to_p2(acc2, t);
     }
   }
+#endif
   /* + [S]B (parked cached form) */
   ge_p1p1_to_p3(acc3, t);
   uint32_t q[40];
   {
-    const uint4 *ent = (const uint4 *)(wsl + 10u * FDGPU_ATAB_WORDS);
+    const uint4 *ent = (const uint4 *)(wsl + FDGPU_WS_SB * FDGPU_ATAB_WORDS);
 #pragma unroll
     for (int i = 0; i < 10; i++) {
       const uint4 v = ent[i];
@@ -355,7 +395,7 @@ FDG_DEV void atab_build(uint32_t *wsl, const ge_p3 &An) {
   const uint32_t *ent1 = wsl + 1u * FDGPU_ATAB_WORDS;
   auto ld1 = [ent1](int cc, int w) { return ent1[10 * cc + w]; };
 #pragma unroll 1
-  for (uint32_t e = 3; e <= 8; e++) {
+  for (uint32_t e = 3; e < FDGPU_ATAB_ENTRIES; e++) {
     ge_add_cached_ld(t, P, ld1, false); ge_p1p1_to_p3(P, t);
     ge_p3_to_cached(c, P); atab_store(wsl, e, c);
   }
@@ -365,14 +405,14 @@ FDG_DEV void atab_build(uint32_t *wsl, const ge_p3 &An) {
    digits of k, 28-35 radix-256 digits of S, 36 pass-1 code. */
 #define PARK_XR 0
 #define PARK_YR 10
-#define PARK_KD 20
+#define PARK_KD 20      /* radix-16: 8 words; radix-32: 13 words (20-32) */
 #define PARK_SD 28
 #define PARK_CODE 36
 /* R-avoiding path (FDGPU_RAVOID): flag bits above the int8 code in PARK_CODE */
 #define RA_ASMALL (1u << 8)
 #define RA_YMATCH (1u << 9)
 
-FDG_DEV uint32_t *park_ptr(uint32_t *wsl) { return wsl + 9u * FDGPU_ATAB_WORDS; }
+FDG_DEV uint32_t *park_ptr(uint32_t *wsl) { return wsl + FDGPU_WS_PARK * FDGPU_ATAB_WORDS; }
 
 /* Pass 1 of one signature (fd_ed25519_user.c:158-207; SURVEY Appendix A steps
    1-5): S < L, k = SHA-512(R||A||M) mod L, decode A then R, small-order
@@ -395,13 +435,17 @@ FDG_DEV int verify_pass1(const uint8_t *arena, const fdgpu_sig_desc_t &sd_in, ui
     } else {
       sha512_hram(h, R, A, arena + sd_in.msg_off, sd_in.msg_sz, nblk_wave);
     }
-    uint32_t kx[16], k[8], kd[8];
+    uint32_t kx[16], k[8], kd[KD_WORDS];
 #pragma unroll
     for (int i = 0; i < 8; i++) { kx[2 * i] = bswap32((uint32_t)(h[i] >> 32)); kx[2 * i + 1] = bswap32((uint32_t)h[i]); }
     sc_reduce512(k, kx);
+#if FDGPU_KWIN == 5
+    sc_recode32(kd, k);
+#else
     sc_recode16(kd, k);
+#endif
 #pragma unroll
-    for (int i = 0; i < 8; i++) park[PARK_KD + i] = kd[i];
+    for (int i = 0; i < KD_WORDS; i++) park[PARK_KD + i] = kd[i];
   }
   /* step 1: S < L (fd_ed25519_user.c:159-161); S recoded to signed radix 256 */
   int code;
@@ -416,7 +460,7 @@ FDG_DEV int verify_pass1(const uint8_t *arena, const fdgpu_sig_desc_t &sd_in, ui
     ge_p3 SB;
     comb_sb(SB, S, btab);
     ge_cached c; ge_p3_to_cached(c, SB);
-    atab_store(wsl, 10, c);
+    atab_store(wsl, FDGPU_WS_SB, c);
 #else
     uint32_t sd[8];
     sc_recode256(sd, S);
@@ -470,9 +514,9 @@ FDG_DEV int verify_pass2(uint32_t *wsl, const uint32_t *s_btab) {
   if (__all(code != 0)) return code;
   ge_p2 Rc;
 #if FDGPU_BCOMB
-  uint32_t kd[8];
+  uint32_t kd[KD_WORDS];
 #pragma unroll
-  for (int i = 0; i < 8; i++) kd[i] = park[PARK_KD + i];
+  for (int i = 0; i < KD_WORDS; i++) kd[i] = park[PARK_KD + i];
   dsm_k(Rc, kd, wsl);
 #else
   uint32_t kd[8], sd[8];
@@ -639,9 +683,9 @@ fdgpu_verify_ra_kernel(const uint8_t *__restrict__ arena, const fdgpu_sig_desc_t
   const bool need = active && code1 == 0;
   ge_p2 Rc;
   if (__any(need)) {
-    uint32_t kd[8];
+    uint32_t kd[KD_WORDS];
 #pragma unroll
-    for (int k = 0; k < 8; k++) kd[k] = park[PARK_KD + k];
+    for (int k = 0; k < KD_WORDS; k++) kd[k] = park[PARK_KD + k];
     dsm_k(Rc, kd, wsl);
   } else {
     ge_p2_0(Rc);
@@ -703,7 +747,7 @@ __global__ void __launch_bounds__(FDGPU_BLOCK) fdgpu_finish_kernel(
     const uint32_t *__restrict__ ws, const uint32_t *__restrict__ wg_inv, int8_t *__restrict__ codes) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   const bool active = i < n_sig;
-  const uint32_t *park = ws + (size_t)(active ? i : 0) * FDGPU_WS_LANE_WORDS + 9u * FDGPU_ATAB_WORDS;
+  const uint32_t *park = ws + (size_t)(active ? i : 0) * FDGPU_WS_LANE_WORDS + FDGPU_WS_PARK * FDGPU_ATAB_WORDS;
   const uint4 *pv = (const uint4 *)(park + 32);
   const uint4 u0 = pv[0], u1 = pv[1], u2 = pv[2];
   const uint32_t fl = u2.z;
@@ -756,7 +800,7 @@ __global__ void __launch_bounds__(FDGPU_BLOCK, FDGPU_PREP_WAVES) fdgpu_tail_kern
   for (uint32_t q = blockIdx.x * blockDim.x + threadIdx.x; q < cnt; q += slow_blocks * blockDim.x) {
   const uint32_t i = queue[q];
   const uint32_t *wsl = ws + (size_t)i * FDGPU_WS_LANE_WORDS;
-  const uint32_t *park = wsl + 9u * FDGPU_ATAB_WORDS;
+  const uint32_t *park = wsl + FDGPU_WS_PARK * FDGPU_ATAB_WORDS;
   const uint32_t fl = park[42];
   uint32_t Renc[8];
   load32(Renc, arena + sigs[i].sig_off);

@@ -329,3 +329,31 @@ def _chunked(engine, arena, txns, chunk=1 << 17):
             t[f] -= lo
         out.append(engine.verify_txns(arena[lo:hi], t))
     return np.concatenate(out)
+
+
+def test_r_sign_and_equation_edges(engine, oracle):
+    """Edges of the R-avoiding compare (fdgpu_kernels.hip): R's
+    sign bit flipped on valid signatures (decoded R = -R': ERR_MSG), R
+    replaced by A or by B's encoding, S + L (out of range), and every lane of
+    a batch failing (the whole batch takes the slow path)."""
+    arena, txns, modes = workload.cfg1(2000, seed=0x5157)
+    recs = []
+    for t in txns[modes == 0][:600]:
+        msg = bytes(arena[int(t["msg_off"]): int(t["msg_off"]) + int(t["msg_sz"])])
+        sig = bytearray(arena[int(t["sig_off"]): int(t["sig_off"]) + 64])
+        pub = bytes(arena[int(t["pub_off"]): int(t["pub_off"]) + 32])
+        flipped = bytearray(sig); flipped[31] ^= 0x80
+        recs.append((msg, bytes(flipped), pub))                        # R -> -R
+        recs.append((msg, pub + bytes(sig[32:]), pub))                 # R = A
+        s_plus_l = (int.from_bytes(sig[32:], "little") + L) % 2**256
+        recs.append((msg, bytes(sig[:32]) + _le(s_plus_l), pub))       # S >= L
+        recs.append((msg, bytes(sig), pub))                            # untouched
+    a2, t2 = workload.pack_single(recs)
+    got = engine.verify_txns(a2, t2)
+    exp = oracle.verify_txns(a2, t2, nthreads=8)
+    assert (got == exp).all(), np.nonzero(got != exp)[0][:10]
+    assert (exp[0::4] == -3).sum() > 590 and (exp[3::4] == 0).all()
+    bad = np.nonzero(exp != 0)[0]                                      # an all-failing batch
+    sub = t2[bad]
+    got_bad = engine.verify_txns(a2, sub)
+    assert (got_bad == exp[bad]).all()
