@@ -46,6 +46,8 @@ def parse():
     ap.add_argument("--latency-batch", type=int, default=65536)
     ap.add_argument("--cpu-sample", type=int, default=1_000_000, help="txns timed on the CPU oracle (bounded sample)")
     ap.add_argument("--no-extras", action="store_true", help="only the timed device-resident loop (profiling)")
+    ap.add_argument("--cfg3-txns", type=int, default=150_000,
+                    help="multi-signature (cfg3) txns for the secondary device-resident line (0: skip)")
     return ap.parse_args()
 
 
@@ -174,6 +176,22 @@ def pmc_traffic():
     return None, None
 
 
+def cfg3_rate(eng, n_txn, seed):
+    """BASELINE configs[2] (cfg3): 1-12 signatures sharing one message, msg up
+    to the 1232-B MTU, 10% with one corrupted signature or message bit;
+    device-resident, mean of HIP-event-timed verifies (secondary line, not
+    `value`)."""
+    from firedancer_amd import workload
+    arena, txns, modes = workload.cfg3(n_txn, seed=seed)
+    b = eng.upload(arena, txns)
+    b.verify()
+    wall, kv, kc = b.time(5)
+    n_sig = b.n_sig
+    b.free()
+    return {"cfg3_txns": n_txn, "cfg3_sigs": n_sig, "cfg3_sigs_per_s": round(n_sig / ((kv + kc) * 1e-3), 1),
+            "cfg3_txns_per_s": round(n_txn / ((kv + kc) * 1e-3), 1), "cfg3_ms_per_batch": round(kv + kc, 3)}
+
+
 def main():
     args = parse()
     dist = Dist()
@@ -214,6 +232,8 @@ def main():
         extras = {"p50_batch_latency_ms": round(p50, 3), "p99_batch_latency_ms": round(p99, 3),
                   "latency_batch_txns": args.latency_batch,
                   "pcie_inclusive_sigs_per_s_per_gpu": round(pcie, 1)}
+        if args.cfg3_txns:
+            extras.update(cfg3_rate(eng, args.cfg3_txns, workload.CFG3_SEED + dist.rank))
     cpu = None
     if dist.rank == 0 and dist.world == 1 and not args.no_extras:
         cpu = cpu_baseline(arena, txns, min(args.cpu_sample, len(txns)))
