@@ -50,6 +50,11 @@ using namespace fdgpu;
 #ifndef FDGPU_EXP_NO_SHA
 #define FDGPU_EXP_NO_SHA 0
 #endif
+/* FDGPU_EXP_LDS_PAD: bytes of dummy LDS per workgroup of the main kernel, to
+   cap residency (occupancy experiments; 0 = off) */
+#ifndef FDGPU_EXP_LDS_PAD
+#define FDGPU_EXP_LDS_PAD 0
+#endif
 #ifndef FDGPU_RAVOID
 #define FDGPU_RAVOID 1        /* 1: compare R' with R's encoding (batched inversion), decode R only for failures */
 #endif
@@ -679,6 +684,11 @@ fdgpu_verify_ra_kernel(const uint8_t *__restrict__ arena, const fdgpu_sig_desc_t
   for (int off = 32; off > 0; off >>= 1) nb = max(nb, (uint32_t)__shfl_xor((int)nb, off));
   uint32_t *wsl = lane_ws(ws, i);
   uint32_t *park = park_ptr(wsl);
+#if FDGPU_EXP_LDS_PAD
+  __shared__ uint32_t s_pad[FDGPU_EXP_LDS_PAD / 4];
+  if (threadIdx.x == 0 && nb == 12345u) s_pad[blockIdx.x % (FDGPU_EXP_LDS_PAD / 4)] = 1u;
+  if (nb == 12346u) park[0] = s_pad[threadIdx.x];
+#endif
   const int code1 = verify_pass1<false>(arena, d, nb, wsl, btab, (flags & FDGPU_FLAG_REF_MAP) != 0);
   const bool need = active && code1 == 0;
   ge_p2 Rc;
