@@ -56,6 +56,16 @@ def lib():
     L.fdgpu_submit.restype = c.c_int64
     L.fdgpu_poll.argtypes = [vp, c.c_int64, vp, c.c_int]
     L.fdgpu_poll.restype = c.c_int
+    L.fdgpu_stage_acquire.argtypes = [vp, c.POINTER(c.c_uint64)]
+    L.fdgpu_stage_acquire.restype = vp
+    L.fdgpu_stage_submit.argtypes = [vp, c.c_uint64, vp, c.c_uint64]
+    L.fdgpu_stage_submit.restype = c.c_int64
+    L.fdgpu_poll_keep.argtypes = [vp, c.c_int64, vp, c.c_int]
+    L.fdgpu_poll_keep.restype = c.c_int
+    L.fdgpu_release.argtypes = [vp, c.c_int64]
+    L.fdgpu_release.restype = c.c_int
+    L.fdgpu_stage_cancel.argtypes = [vp]
+    L.fdgpu_stage_cancel.restype = c.c_int
     L.fdgpu_verify_device.argtypes = [vp, vp, vp, c.c_uint64, vp, c.c_uint64, vp, vp, vp]
     L.fdgpu_verify_device.restype = c.c_int
     L.fdgpu_engine_info.argtypes = [vp, c.POINTER(c.c_uint32), c.POINTER(c.c_uint32), c.POINTER(c.c_uint64)]

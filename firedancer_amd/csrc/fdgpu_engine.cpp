@@ -2,13 +2,14 @@
    exported C ABI (include/fd_ed25519_gpu.h).
 
    Per engine (one per GPU):
-     - one compute stream running the verify + combine kernels in order
-       (they share the per-lane A-table workspace);
      - `ring_depth` staging slots, each with pinned host buffers, device
-       buffers, a copy stream and events, so the PCIe copies of batch i+1
-       and the D2H of batch i-1 overlap the kernels of batch i;
-     - the B table (built on the device at open) and the workspace sized for
-       the persistent grid (resident workgroups x 256 lanes).
+       buffers, its own stream and its own workspace: a slot's H2D copy,
+       verify kernels and D2H of the codes run in order on its stream, and
+       the slots' batches overlap each other on the GPU (copies of one batch
+       under the kernels of another; two small batches sharing the CUs);
+     - one compute stream + workspace for the device-resident path
+       (fdgpu_dev_batch_*, fdgpu_verify_device) and the diagnostics;
+     - the fixed-base comb table (built on the device at open).
    Untrusted descriptors are bounds-checked on the host before anything is
    handed to the GPU (offsets + sizes must lie inside the arena). */
 #include <hip/hip_runtime.h>
@@ -45,7 +46,10 @@ struct Slot {
   fdgpu_sig_desc_t *h_sigs = nullptr, *d_sigs = nullptr;
   fdgpu_txn_desc_t *h_txns = nullptr, *d_txns = nullptr;
   int8_t *h_codes = nullptr, *d_txn_codes = nullptr, *d_sig_codes = nullptr;
+  uint32_t *d_ws = nullptr;   /* this slot's workspace: slots run concurrently on their own streams */
   int64_t ticket = -1;      /* -1: free */
+  bool staged = false;      /* reserved by fdgpu_stage_acquire, not yet submitted */
+  bool held = false;        /* polled with fdgpu_poll_keep, awaiting fdgpu_release */
   uint64_t txn_cnt = 0;
 };
 
@@ -82,6 +86,7 @@ void slot_free(Slot &s) {
   if (s.d_txns) (void)hipFree(s.d_txns);
   if (s.d_txn_codes) (void)hipFree(s.d_txn_codes);
   if (s.d_sig_codes) (void)hipFree(s.d_sig_codes);
+  if (s.d_ws) (void)hipFree(s.d_ws);
   s = Slot{};
 }
 
@@ -100,6 +105,7 @@ bool slot_alloc(Slot &s, const fdgpu_cfg_t &c) {
   HIPCHK(hipMalloc((void **)&s.d_txns, c.max_txn * sizeof(fdgpu_txn_desc_t) + 16), false);
   HIPCHK(hipMalloc((void **)&s.d_txn_codes, c.max_txn + 16), false);
   HIPCHK(hipMalloc((void **)&s.d_sig_codes, c.max_sig + 16), false);
+  HIPCHK(hipMalloc((void **)&s.d_ws, fdgpu_ws_bytes(c.max_sig ? c.max_sig : 1)), false);
   return true;
 }
 
@@ -207,20 +213,53 @@ int fdgpu_engine_info(fdgpu_engine_t *e, uint32_t *grid_blocks, uint32_t *block_
   return FDGPU_OK;
 }
 
+/* ws: a workspace for n_sig signatures, or NULL for the engine's compute
+   workspace (grown on demand; callers on other streams synchronise first). */
 static int enqueue_verify(fdgpu_engine_t *e, const uint8_t *d_arena, const fdgpu_sig_desc_t *d_sigs, uint64_t n_sig,
                           const fdgpu_txn_desc_t *d_txns, uint64_t n_txn, int8_t *d_sig_codes, int8_t *d_txn_codes,
-                          hipStream_t st) {
+                          hipStream_t st, uint32_t *ws = nullptr) {
   const uint32_t flags = (e->cfg.flags & FDGPU_FLAG_REF_MAPPING) ? FDGPU_FLAG_REF_MAP : 0u;
-  if (n_sig > e->ws_sig) {
+  if (!ws && n_sig > e->ws_sig) {
     HIPCHK(hipStreamSynchronize(st), FDGPU_ERR_DEVICE);
     HIPCHK(hipStreamSynchronize(e->compute), FDGPU_ERR_DEVICE);
     int rc = ensure_ws(e, n_sig);
     if (rc) return rc;
   }
-  HIPCHK(fdgpu_launch_verify_sigs(d_arena, d_sigs, (uint32_t)n_sig, e->d_btab, e->d_ws, d_sig_codes, flags, st),
+  HIPCHK(fdgpu_launch_verify_sigs(d_arena, d_sigs, (uint32_t)n_sig, e->d_btab, ws ? ws : e->d_ws, d_sig_codes, flags,
+                                  st),
          FDGPU_ERR_DEVICE);
   HIPCHK(fdgpu_launch_combine(d_txns, (uint32_t)n_txn, d_sig_codes, d_txn_codes, st), FDGPU_ERR_DEVICE);
   return FDGPU_OK;
+}
+
+/* Enqueue the batch already in slot s's pinned arena (arena_sz bytes). */
+static int64_t submit_slot(fdgpu_engine_t *e, Slot *s, uint64_t arena_sz, fdgpu_txn_t const *txns, uint64_t txn_cnt) {
+  const int64_t ns = expand(s->h_arena, arena_sz, txns, txn_cnt, e->cfg.max_sig, s->h_sigs, s->h_txns);
+  if (ns < 0) return FDGPU_ERR_INVAL;
+  memset(s->h_arena + arena_sz, 0, FDGPU_ARENA_SLACK);
+  const size_t asz = arena_sz + FDGPU_ARENA_SLACK;
+  HIPCHK(hipMemcpyAsync(s->d_arena, s->h_arena, asz, hipMemcpyHostToDevice, s->stream), FDGPU_ERR_DEVICE);
+  if (ns) HIPCHK(hipMemcpyAsync(s->d_sigs, s->h_sigs, (size_t)ns * sizeof(fdgpu_sig_desc_t), hipMemcpyHostToDevice, s->stream), FDGPU_ERR_DEVICE);
+  if (txn_cnt) HIPCHK(hipMemcpyAsync(s->d_txns, s->h_txns, txn_cnt * sizeof(fdgpu_txn_desc_t), hipMemcpyHostToDevice, s->stream), FDGPU_ERR_DEVICE);
+  /* copies, kernels and the code read-back of a slot run in order on the
+     slot's own stream with the slot's own workspace, so the ring's batches
+     overlap each other on the GPU (a 64K-signature batch fills only half of
+     the resident wave slots) */
+  int rc = enqueue_verify(e, s->d_arena, s->d_sigs, (uint64_t)ns, s->d_txns, txn_cnt, s->d_sig_codes, s->d_txn_codes,
+                          s->stream, s->d_ws);
+  if (rc) return rc;
+  if (txn_cnt) HIPCHK(hipMemcpyAsync(s->h_codes, s->d_txn_codes, txn_cnt, hipMemcpyDeviceToHost, s->stream), FDGPU_ERR_DEVICE);
+  HIPCHK(hipEventRecord(s->done, s->stream), FDGPU_ERR_DEVICE);
+  s->staged = false;
+  s->held = false;
+  s->ticket = e->next_ticket++;
+  s->txn_cnt = txn_cnt;
+  return s->ticket;
+}
+
+static Slot *free_slot(fdgpu_engine_t *e) {
+  for (auto &c : e->slots) if (c.ticket < 0 && !c.staged) return &c;
+  return nullptr;
 }
 
 int64_t fdgpu_submit(fdgpu_engine_t *e, uint8_t const *arena, uint64_t arena_sz, fdgpu_txn_t const *txns,
@@ -228,36 +267,37 @@ int64_t fdgpu_submit(fdgpu_engine_t *e, uint8_t const *arena, uint64_t arena_sz,
   if (!e || (!arena && arena_sz) || (!txns && txn_cnt)) { set_err("null argument"); return FDGPU_ERR_INVAL; }
   if (arena_sz > e->cfg.max_arena || txn_cnt > e->cfg.max_txn) { set_err("batch exceeds engine limits"); return FDGPU_ERR_INVAL; }
   HIPCHK(hipSetDevice(e->device), FDGPU_ERR_DEVICE);
-  Slot *s = nullptr;
-  for (auto &c : e->slots) if (c.ticket < 0) { s = &c; break; }
+  Slot *s = free_slot(e);
   if (!s) { set_err("all ring slots hold unpolled batches"); return FDGPU_ERR_FULL; }
   /* the slot's previous batch was polled, so its copies are complete */
-  const int64_t ns = expand(arena, arena_sz, txns, txn_cnt, e->cfg.max_sig, s->h_sigs, s->h_txns);
-  if (ns < 0) return FDGPU_ERR_INVAL;
   if (arena_sz) memcpy(s->h_arena, arena, arena_sz);
-  memset(s->h_arena + arena_sz, 0, FDGPU_ARENA_SLACK);
-  const size_t asz = arena_sz + FDGPU_ARENA_SLACK;
-  HIPCHK(hipMemcpyAsync(s->d_arena, s->h_arena, asz, hipMemcpyHostToDevice, s->stream), FDGPU_ERR_DEVICE);
-  if (ns) HIPCHK(hipMemcpyAsync(s->d_sigs, s->h_sigs, (size_t)ns * sizeof(fdgpu_sig_desc_t), hipMemcpyHostToDevice, s->stream), FDGPU_ERR_DEVICE);
-  if (txn_cnt) HIPCHK(hipMemcpyAsync(s->d_txns, s->h_txns, txn_cnt * sizeof(fdgpu_txn_desc_t), hipMemcpyHostToDevice, s->stream), FDGPU_ERR_DEVICE);
-  HIPCHK(hipEventRecord(s->h2d_done, s->stream), FDGPU_ERR_DEVICE);
-  HIPCHK(hipStreamWaitEvent(e->compute, s->h2d_done, 0), FDGPU_ERR_DEVICE);
-  int rc = enqueue_verify(e, s->d_arena, s->d_sigs, (uint64_t)ns, s->d_txns, txn_cnt, s->d_sig_codes, s->d_txn_codes,
-                          e->compute);
-  if (rc) return rc;
-  HIPCHK(hipEventRecord(s->comp_done, e->compute), FDGPU_ERR_DEVICE);
-  HIPCHK(hipStreamWaitEvent(s->stream, s->comp_done, 0), FDGPU_ERR_DEVICE);
-  if (txn_cnt) HIPCHK(hipMemcpyAsync(s->h_codes, s->d_txn_codes, txn_cnt, hipMemcpyDeviceToHost, s->stream), FDGPU_ERR_DEVICE);
-  HIPCHK(hipEventRecord(s->done, s->stream), FDGPU_ERR_DEVICE);
-  s->ticket = e->next_ticket++;
-  s->txn_cnt = txn_cnt;
-  return s->ticket;
+  return submit_slot(e, s, arena_sz, txns, txn_cnt);
 }
 
-int fdgpu_poll(fdgpu_engine_t *e, int64_t ticket, int8_t *txn_codes, int blocking) {
+uint8_t *fdgpu_stage_acquire(fdgpu_engine_t *e, uint64_t *cap) {
+  if (!e) return nullptr;
+  for (auto &c : e->slots) if (c.staged) { set_err("a slot is already staged"); return nullptr; }
+  Slot *s = free_slot(e);
+  if (!s) { set_err("all ring slots hold unpolled batches"); return nullptr; }
+  s->staged = true;
+  if (cap) *cap = e->cfg.max_arena;
+  return s->h_arena;
+}
+
+int64_t fdgpu_stage_submit(fdgpu_engine_t *e, uint64_t arena_sz, fdgpu_txn_t const *txns, uint64_t txn_cnt) {
+  if (!e || (!txns && txn_cnt)) { set_err("null argument"); return FDGPU_ERR_INVAL; }
+  Slot *s = nullptr;
+  for (auto &c : e->slots) if (c.staged) { s = &c; break; }
+  if (!s) { set_err("no staged slot"); return FDGPU_ERR_INVAL; }
+  if (arena_sz > e->cfg.max_arena || txn_cnt > e->cfg.max_txn) { set_err("batch exceeds engine limits"); return FDGPU_ERR_INVAL; }
+  HIPCHK(hipSetDevice(e->device), FDGPU_ERR_DEVICE);
+  return submit_slot(e, s, arena_sz, txns, txn_cnt);
+}
+
+static int poll_slot(fdgpu_engine_t *e, int64_t ticket, int8_t *txn_codes, int blocking, bool keep) {
   if (!e) return FDGPU_ERR_INVAL;
   Slot *s = nullptr;
-  for (auto &c : e->slots) if (c.ticket == ticket && ticket >= 0) { s = &c; break; }
+  for (auto &c : e->slots) if (c.ticket == ticket && ticket >= 0 && !c.held) { s = &c; break; }
   if (!s) { set_err("unknown ticket %lld", (long long)ticket); return FDGPU_ERR_TICKET; }
   HIPCHK(hipSetDevice(e->device), FDGPU_ERR_DEVICE);
   if (blocking) {
@@ -268,8 +308,31 @@ int fdgpu_poll(fdgpu_engine_t *e, int64_t ticket, int8_t *txn_codes, int blockin
     HIPCHK(q, FDGPU_ERR_DEVICE);
   }
   if (txn_codes && s->txn_cnt) memcpy(txn_codes, s->h_codes, s->txn_cnt);
-  s->ticket = -1;
+  if (keep) s->held = true;
+  else s->ticket = -1;
   return FDGPU_OK;
+}
+
+int fdgpu_poll(fdgpu_engine_t *e, int64_t ticket, int8_t *txn_codes, int blocking) {
+  return poll_slot(e, ticket, txn_codes, blocking, false);
+}
+
+int fdgpu_poll_keep(fdgpu_engine_t *e, int64_t ticket, int8_t *txn_codes, int blocking) {
+  return poll_slot(e, ticket, txn_codes, blocking, true);
+}
+
+int fdgpu_stage_cancel(fdgpu_engine_t *e) {
+  if (!e) return FDGPU_ERR_INVAL;
+  for (auto &c : e->slots) if (c.staged) { c.staged = false; return FDGPU_OK; }
+  return FDGPU_ERR_INVAL;
+}
+
+int fdgpu_release(fdgpu_engine_t *e, int64_t ticket) {
+  if (!e) return FDGPU_ERR_INVAL;
+  for (auto &c : e->slots)
+    if (c.ticket == ticket && ticket >= 0 && c.held) { c.held = false; c.ticket = -1; return FDGPU_OK; }
+  set_err("ticket %lld not held", (long long)ticket);
+  return FDGPU_ERR_TICKET;
 }
 
 int fdgpu_verify_device(fdgpu_engine_t *e, void const *d_arena, void const *d_sig_desc, uint64_t sig_cnt,

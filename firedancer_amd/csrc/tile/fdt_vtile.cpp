@@ -58,6 +58,7 @@ inline uint64_t align2(uint64_t x) { return (x + 1) & ~1ull; }
 struct fdgpu_dispatch {
   std::vector<fdgpu_engine_t *> eng;
   uint32_t next = 0;
+  int staged = -1;          /* engine holding the staged slot */
 };
 
 namespace {
@@ -84,6 +85,50 @@ int dispatch_poll(void *ctx, int64_t ticket, int8_t *codes, int blocking) {
   return fdgpu_poll(d->eng[ticket % n], ticket / n, codes, blocking);
 }
 
+uint8_t *dispatch_stage(void *ctx, uint64_t *cap) {
+  auto *d = (fdgpu_dispatch *)ctx;
+  if (d->staged >= 0) return nullptr;
+  const uint32_t n = (uint32_t)d->eng.size();
+  for (uint32_t k = 0; k < n; k++) {
+    const uint32_t idx = (d->next + k) % n;
+    uint8_t *p = fdgpu_stage_acquire(d->eng[idx], cap);
+    if (p) { d->staged = (int)idx; d->next = (idx + 1) % n; return p; }
+  }
+  return nullptr;
+}
+
+int64_t dispatch_submit_staged(void *ctx, uint64_t arena_sz, const fdgpu_txn_t *txns, uint64_t n_txn) {
+  auto *d = (fdgpu_dispatch *)ctx;
+  if (d->staged < 0) return FDGPU_ERR_INVAL;
+  const int idx = d->staged;
+  const int64_t t = fdgpu_stage_submit(d->eng[idx], arena_sz, txns, n_txn);
+  if (t < 0) return t;
+  d->staged = -1;
+  return t * (int64_t)d->eng.size() + idx;
+}
+
+int dispatch_poll_keep(void *ctx, int64_t ticket, int8_t *codes, int blocking) {
+  auto *d = (fdgpu_dispatch *)ctx;
+  const int64_t n = (int64_t)d->eng.size();
+  if (ticket < 0) return FDGPU_ERR_TICKET;
+  return fdgpu_poll_keep(d->eng[ticket % n], ticket / n, codes, blocking);
+}
+
+int dispatch_release(void *ctx, int64_t ticket) {
+  auto *d = (fdgpu_dispatch *)ctx;
+  const int64_t n = (int64_t)d->eng.size();
+  if (ticket < 0) return FDGPU_ERR_TICKET;
+  return fdgpu_release(d->eng[ticket % n], ticket / n);
+}
+
+int dispatch_stage_cancel(void *ctx) {
+  auto *d = (fdgpu_dispatch *)ctx;
+  if (d->staged < 0) return FDGPU_ERR_INVAL;
+  const int rc = fdgpu_stage_cancel(d->eng[d->staged]);
+  d->staged = -1;
+  return rc;
+}
+
 }  // namespace
 
 extern "C" {
@@ -100,10 +145,15 @@ fdgpu_dispatch_t *fdgpu_dispatch_new(fdgpu_engine_t *const *engines, uint32_t en
 void fdgpu_dispatch_delete(fdgpu_dispatch_t *d) { delete d; }
 
 fdgpu_verifier_t fdgpu_dispatch_verifier(fdgpu_dispatch_t *d) {
-  fdgpu_verifier_t v;
+  fdgpu_verifier_t v{};
   v.ctx = d;
   v.submit = dispatch_submit;
   v.poll = dispatch_poll;
+  v.stage = dispatch_stage;
+  v.submit_staged = dispatch_submit_staged;
+  v.poll_keep = dispatch_poll_keep;
+  v.release = dispatch_release;
+  v.stage_cancel = dispatch_stage_cancel;
   return v;
 }
 
@@ -123,7 +173,10 @@ struct Item {
 };
 
 struct Batch {
-  std::vector<uint8_t> arena;       /* payload copies, back to back */
+  std::vector<uint8_t> arena;       /* payload copies, back to back (when not staged) */
+  uint8_t *ap = nullptr;            /* the arena in use: arena.data() or a staged pinned slot */
+  uint64_t cap = 0;                 /* its capacity */
+  bool staged = false;
   std::vector<uint8_t> trailer;     /* parsed fd_txn_t of each item */
   std::vector<fdgpu_txn_t> txns;    /* one per item */
   std::vector<Item> items;
@@ -138,6 +191,7 @@ struct Batch {
     arena_used = trailer_used = 0;
     txns.clear(); items.clear();
     ticket = -1; done = false; next = 0; t_first = 0;
+    ap = nullptr; cap = 0; staged = false;
   }
 };
 
@@ -172,7 +226,7 @@ struct fdgpu_vtile {
   /* publish one verified txn downstream (fd_verify.c:93-147) */
   void publish(const Batch &b, const Item &it, uint64_t tag) {
     uint8_t *dst = cfg.out_base + (out_chunk << FDT_CHUNK_LG_SZ);
-    std::memcpy(dst, b.arena.data() + it.pay_off, it.pay_sz);
+    std::memcpy(dst, b.ap + it.pay_off, it.pay_sz);
     const uint64_t toff = align2(it.pay_sz);
     if (toff != it.pay_sz) dst[it.pay_sz] = 0;
     std::memcpy(dst + toff, b.trailer.data() + it.txn_off, it.txn_sz);
@@ -192,7 +246,8 @@ struct fdgpu_vtile {
     while (!inflight.empty()) {
       Batch *b = inflight.front();
       if (!b->done) {
-        const int rc = ver.poll(ver.ctx, b->ticket, b->codes.data(), 0);
+        const int rc = b->staged ? ver.poll_keep(ver.ctx, b->ticket, b->codes.data(), 0)
+                                 : ver.poll(ver.ctx, b->ticket, b->codes.data(), 0);
         if (rc == FDGPU_PENDING) break;
         if (rc != FDGPU_OK) return rc;
         b->done = true;
@@ -200,7 +255,7 @@ struct fdgpu_vtile {
       while (b->next < b->items.size()) {
         if (credits() <= 0) { st.backpressure++; return n; }
         const Item &it = b->items[b->next];
-        const uint64_t tag = fdt_hash(cfg.hashmap_seed, b->arena.data() + it.pay_off +
+        const uint64_t tag = fdt_hash(cfg.hashmap_seed, b->ap + it.pay_off +
                                       ((const fdt_txn_t *)(b->trailer.data() + it.txn_off))->signature_off, 64);
         int outcome;
         if (fdt_tcache_query(tcache, tag)) outcome = FD_TXN_VERIFY_DEDUP;
@@ -214,6 +269,7 @@ struct fdgpu_vtile {
         n++;
       }
       if (lat.size() < (1u << 22) && !b->items.empty()) lat.push_back(now_ns() - b->t_first);
+      if (b->staged) ver.release(ver.ctx, b->ticket);
       inflight.pop_front();
       b->reset();
       pool.push_back(b);
@@ -225,10 +281,20 @@ struct fdgpu_vtile {
   void ingest() {
     if (!open) {
       if (pool.empty()) return;
-      open = pool.back(); pool.pop_back();
+      Batch *nb = pool.back();
+      if (ver.stage) {                                  /* zero-copy: frags go straight to pinned memory */
+        uint64_t cap = 0;
+        uint8_t *p = ver.stage(ver.ctx, &cap);
+        if (!p) return;                                 /* every slot busy: resolve first */
+        nb->ap = p; nb->cap = cap; nb->staged = true;
+      } else {
+        nb->ap = nb->arena.data(); nb->cap = nb->arena.size();
+      }
+      pool.pop_back();
+      open = nb;
     }
     Batch &b = *open;
-    while (b.items.size() < cfg.batch_txn_max) {
+    while (b.items.size() < cfg.batch_txn_max && b.arena_used + FDT_TPU_MTU <= b.cap) {
       fdt_frag_meta_t m;
       uint64_t found;
       const int rc = fdt_mcache_poll(cfg.in_mcache, cfg.in_depth, rx_seq, &m, &found);
@@ -247,7 +313,7 @@ struct fdgpu_vtile {
       if (m.chunk < cfg.in_chunk0 || m.chunk > cfg.in_wmark || m.sz > FDT_TPU_MTU) {
         st.corrupt++; log(seq, FDGPU_VTILE_LOG_LOST); continue;
       }
-      uint8_t *pay = b.arena.data() + b.arena_used;
+      uint8_t *pay = b.ap + b.arena_used;
       std::memcpy(pay, cfg.in_base + ((uint64_t)m.chunk << FDT_CHUNK_LG_SZ), m.sz);
       if (fdt_mcache_query(cfg.in_mcache, cfg.in_depth, seq) != seq) {   /* overwritten while copying */
         st.overrun++; log(seq, FDGPU_VTILE_LOG_LOST); continue;
@@ -274,11 +340,12 @@ struct fdgpu_vtile {
   /* submit the open batch when full or when its first frag has waited long enough */
   int submit(bool force) {
     if (!open || open->items.empty()) return 0;
-    const bool full = open->items.size() >= cfg.batch_txn_max;
+    const bool full = open->items.size() >= cfg.batch_txn_max || open->arena_used + FDT_TPU_MTU > open->cap;
     if (!full && !force && now_ns() - open->t_first < cfg.batch_wait_ns) return 0;
     if (inflight.size() >= cfg.inflight_max) return 0;
-    const int64_t t = ver.submit(ver.ctx, open->arena.data(), open->arena_used, open->txns.data(),
-                                 open->txns.size());
+    const int64_t t = open->staged
+        ? ver.submit_staged(ver.ctx, open->arena_used, open->txns.data(), open->txns.size())
+        : ver.submit(ver.ctx, open->ap, open->arena_used, open->txns.data(), open->txns.size());
     if (t == FDGPU_ERR_FULL) return 0;
     if (t < 0) return (int)t;
     open->ticket = t;
@@ -294,6 +361,7 @@ extern "C" {
 fdgpu_vtile_t *fdgpu_vtile_new(const fdgpu_vtile_cfg_t *cfg, fdgpu_verifier_t ver) {
   if (!cfg || !ver.submit || !ver.poll || !cfg->in_mcache || !cfg->out_mcache || !cfg->in_base || !cfg->out_base)
     return nullptr;
+  if (ver.stage && (!ver.submit_staged || !ver.poll_keep || !ver.release)) return nullptr;
   if (!cfg->in_depth || (cfg->in_depth & (cfg->in_depth - 1)) || !cfg->out_depth ||
       (cfg->out_depth & (cfg->out_depth - 1)) || !cfg->batch_txn_max || cfg->out_wmark < cfg->out_chunk0)
     return nullptr;
@@ -328,7 +396,14 @@ fdgpu_vtile_t *fdgpu_vtile_new(const fdgpu_vtile_cfg_t *cfg, fdgpu_verifier_t ve
 void fdgpu_vtile_delete(fdgpu_vtile_t *t) {
   if (!t) return;
   /* drain: the verifier may still write codes into in-flight batches */
-  for (Batch *b : t->inflight) if (!b->done) t->ver.poll(t->ver.ctx, b->ticket, b->codes.data(), 1);
+  for (Batch *b : t->inflight) {
+    if (!b->done) {
+      if (b->staged) t->ver.poll_keep(t->ver.ctx, b->ticket, b->codes.data(), 1);
+      else t->ver.poll(t->ver.ctx, b->ticket, b->codes.data(), 1);
+    }
+    if (b->staged) t->ver.release(t->ver.ctx, b->ticket);
+  }
+  if (t->open && t->open->staged && t->ver.stage_cancel) t->ver.stage_cancel(t->ver.ctx);
   delete t;
 }
 
@@ -352,7 +427,8 @@ int fdgpu_vtile_flush(fdgpu_vtile_t *t) {
   while (!t->inflight.empty()) {
     Batch *b = t->inflight.front();
     if (!b->done) {
-      const int r = t->ver.poll(t->ver.ctx, b->ticket, b->codes.data(), 1);
+      const int r = b->staged ? t->ver.poll_keep(t->ver.ctx, b->ticket, b->codes.data(), 1)
+                              : t->ver.poll(t->ver.ctx, b->ticket, b->codes.data(), 1);
       if (r != FDGPU_OK) return r;
       b->done = true;
     }

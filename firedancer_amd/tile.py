@@ -79,7 +79,10 @@ POLL_FN = c.CFUNCTYPE(c.c_int, vp, c.c_int64, vp, c.c_int)
 
 
 class Verifier(c.Structure):
-    _fields_ = [("ctx", vp), ("submit", SUBMIT_FN), ("poll", POLL_FN)]
+    """fdgpu_verifier_t: submit/poll, plus the optional zero-copy staging
+    hooks (left NULL by PyVerifier; set by the GPU dispatcher)."""
+    _fields_ = [("ctx", vp), ("submit", SUBMIT_FN), ("poll", POLL_FN), ("stage", vp), ("submit_staged", vp),
+                ("poll_keep", vp), ("release", vp), ("stage_cancel", vp)]
 
 
 class VTileCfg(c.Structure):

@@ -117,6 +117,24 @@ int64_t fdgpu_submit( fdgpu_engine_t *    e,
    per transaction, in submission order); < 0 on error. */
 int fdgpu_poll( fdgpu_engine_t * e, int64_t ticket, int8_t * txn_codes, int blocking );
 
+/* Zero-copy staging (the verify tile's path): the caller writes the batch
+   payload straight into a ring slot's pinned arena instead of handing over
+   its own buffer, saving one host copy per byte.
+     fdgpu_stage_acquire reserves a free slot and returns its pinned arena
+       (capacity *cap bytes), or NULL when every slot is busy or one is
+       already staged (one staged slot per engine);
+     fdgpu_stage_submit submits the staged slot (arena_sz bytes written) with
+       its descriptors -> ticket, as fdgpu_submit;
+     fdgpu_poll_keep is fdgpu_poll but keeps the slot (and the payload bytes
+       in its arena) reserved until fdgpu_release, so results can be
+       published from the staged bytes after the codes are known. */
+uint8_t * fdgpu_stage_acquire( fdgpu_engine_t * e, uint64_t * cap );
+int64_t   fdgpu_stage_submit( fdgpu_engine_t * e, uint64_t arena_sz, fdgpu_txn_t const * txns, uint64_t txn_cnt );
+int       fdgpu_poll_keep( fdgpu_engine_t * e, int64_t ticket, int8_t * txn_codes, int blocking );
+int       fdgpu_release( fdgpu_engine_t * e, int64_t ticket );
+/* Returns a staged (acquired, not submitted) slot to the ring. */
+int       fdgpu_stage_cancel( fdgpu_engine_t * e );
+
 /* Device-resident path: inputs already in HBM (device pointers), codes
    written to device memory, work enqueued on `hip_stream` (a hipStream_t,
    NULL = the engine's compute stream).  d_sig_desc: per-signature

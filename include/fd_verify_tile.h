@@ -182,6 +182,14 @@ typedef struct {
   int64_t (*submit)( void * ctx, uint8_t const * arena, uint64_t arena_sz, fdgpu_txn_t const * txns,
                      uint64_t txn_cnt );
   int     (*poll)  ( void * ctx, int64_t ticket, int8_t * txn_codes, int blocking );
+  /* Optional zero-copy staging (NULL when unsupported): the tile copies
+     frags straight into the returned (pinned) arena; a staged batch is
+     polled with poll_keep and handed back with release once published. */
+  uint8_t * (*stage)        ( void * ctx, uint64_t * cap );
+  int64_t   (*submit_staged)( void * ctx, uint64_t arena_sz, fdgpu_txn_t const * txns, uint64_t txn_cnt );
+  int       (*poll_keep)    ( void * ctx, int64_t ticket, int8_t * txn_codes, int blocking );
+  int       (*release)      ( void * ctx, int64_t ticket );
+  int       (*stage_cancel) ( void * ctx );
 } fdgpu_verifier_t;
 
 /* Multi-GPU dispatcher: batches go round-robin over `engine_cnt` engines

@@ -357,3 +357,29 @@ def test_r_sign_and_equation_edges(engine, oracle):
     sub = t2[bad]
     got_bad = engine.verify_txns(a2, sub)
     assert (got_bad == exp[bad]).all()
+
+
+def test_zero_copy_staging(engine):
+    """fdgpu_stage_acquire / stage_submit / poll_keep / release: payloads
+    written straight into the pinned slot verify like fdgpu_submit, the slot
+    stays reserved until released, one staged slot at a time."""
+    import ctypes
+    L = fa._lib.lib() if hasattr(fa, "_lib") else __import__("firedancer_amd._lib", fromlist=["lib"]).lib()
+    arena, txns, modes = workload.cfg1(500, seed=91)
+    cap = ctypes.c_uint64()
+    p = L.fdgpu_stage_acquire(engine._h, ctypes.byref(cap))
+    assert p and cap.value >= len(arena)
+    assert not L.fdgpu_stage_acquire(engine._h, ctypes.byref(cap))      # one staged slot per engine
+    ctypes.memmove(p, arena.ctypes.data, len(arena))
+    t = np.ascontiguousarray(txns)
+    tk = L.fdgpu_stage_submit(engine._h, len(arena), t.ctypes.data, len(t))
+    assert tk >= 0
+    codes = np.zeros(len(t), dtype=np.int8)
+    assert L.fdgpu_poll_keep(engine._h, tk, codes.ctypes.data, 1) == 0
+    assert ((codes == 0) == (modes == 0)).all()
+    assert bytes((ctypes.c_uint8 * 64).from_address(p)) == bytes(arena[:64])   # still reserved, intact
+    assert (engine.verify_txns(arena, txns) == codes).all()
+    assert L.fdgpu_release(engine._h, tk) == 0
+    assert L.fdgpu_release(engine._h, tk) != 0
+    p2 = L.fdgpu_stage_acquire(engine._h, ctypes.byref(cap))
+    assert p2 and L.fdgpu_stage_cancel(engine._h) == 0
