@@ -103,10 +103,13 @@ def aggregate(dist, n_sig, steps, dt):
     return total / dt_max, dt_max
 
 
+RING_DEPTH = 4        # ring slots (one stream + workspace each) of the latency/PCIe engine
+
+
 def latency_and_pcie(eng, arena, txns, batch, nbatches):
-    """p50/p99 submit->codes-on-host latency of `batch`-txn batches (ring depth
-    2, one in flight at a time for latency), then pipelined throughput with
-    both ring slots busy (PCIe-inclusive)."""
+    """p50/p99 submit->codes-on-host latency of `batch`-txn batches (one in
+    flight at a time), then pipelined throughput with every ring slot busy
+    (PCIe-inclusive: host staging memcpy, uploads, kernels, code read-back)."""
     n = len(txns)
     starts = list(range(0, n - batch + 1, batch)) or [0]
     views = []
@@ -131,9 +134,9 @@ def latency_and_pcie(eng, arena, txns, batch, nbatches):
     sigs = 0
     t0 = time.perf_counter()
     inflight = []
-    for i in range(len(views) * 2):
+    for i in range(max(len(views), 4 * RING_DEPTH) * 2):
         a, t = views[i % len(views)]
-        if len(inflight) == 2:
+        if len(inflight) == RING_DEPTH:
             eng.poll(inflight.pop(0), blocking=True)
         inflight.append(eng.submit(a, t))
         sigs += int(t["sig_cnt"].sum())
@@ -201,7 +204,7 @@ def main():
     arena, txns, modes = workload.cfg1(args.txns, seed=rank_seed(dist.rank))
     t_gen = time.perf_counter() - t_gen
     eng = VerifyEngine(dist.local_rank, max_txn=args.latency_batch, max_sig=2 * args.latency_batch,
-                       max_arena=args.latency_batch * 1232)
+                       max_arena=args.latency_batch * 1232, ring_depth=RING_DEPTH)
     batch = eng.upload(arena, txns)
     n_sig = batch.n_sig
 

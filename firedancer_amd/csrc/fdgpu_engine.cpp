@@ -21,6 +21,7 @@
 #include <cstring>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/fd_ed25519_gpu.h"
@@ -233,12 +234,16 @@ static int enqueue_verify(fdgpu_engine_t *e, const uint8_t *d_arena, const fdgpu
 }
 
 /* Enqueue the batch already in slot s's pinned arena (arena_sz bytes). */
-static int64_t submit_slot(fdgpu_engine_t *e, Slot *s, uint64_t arena_sz, fdgpu_txn_t const *txns, uint64_t txn_cnt) {
+/* `uploaded` = bytes of the arena whose host->device copy is already queued on
+   the slot's stream (fdgpu_submit overlaps its staging memcpy with the copy) */
+static int64_t submit_slot(fdgpu_engine_t *e, Slot *s, uint64_t arena_sz, fdgpu_txn_t const *txns, uint64_t txn_cnt,
+                           uint64_t uploaded = 0) {
   const int64_t ns = expand(s->h_arena, arena_sz, txns, txn_cnt, e->cfg.max_sig, s->h_sigs, s->h_txns);
   if (ns < 0) return FDGPU_ERR_INVAL;
   memset(s->h_arena + arena_sz, 0, FDGPU_ARENA_SLACK);
-  const size_t asz = arena_sz + FDGPU_ARENA_SLACK;
-  HIPCHK(hipMemcpyAsync(s->d_arena, s->h_arena, asz, hipMemcpyHostToDevice, s->stream), FDGPU_ERR_DEVICE);
+  const size_t asz = arena_sz + FDGPU_ARENA_SLACK - uploaded;
+  HIPCHK(hipMemcpyAsync(s->d_arena + uploaded, s->h_arena + uploaded, asz, hipMemcpyHostToDevice, s->stream),
+         FDGPU_ERR_DEVICE);
   if (ns) HIPCHK(hipMemcpyAsync(s->d_sigs, s->h_sigs, (size_t)ns * sizeof(fdgpu_sig_desc_t), hipMemcpyHostToDevice, s->stream), FDGPU_ERR_DEVICE);
   if (txn_cnt) HIPCHK(hipMemcpyAsync(s->d_txns, s->h_txns, txn_cnt * sizeof(fdgpu_txn_desc_t), hipMemcpyHostToDevice, s->stream), FDGPU_ERR_DEVICE);
   /* copies, kernels and the code read-back of a slot run in order on the
@@ -262,6 +267,42 @@ static Slot *free_slot(fdgpu_engine_t *e) {
   return nullptr;
 }
 
+/* Copy a caller's arena into the slot's pinned buffer.  Large arenas are
+   split over FDGPU_COPY_THREADS host threads; each queues its part's upload on
+   the slot stream as soon as its memcpy is done, so the PCIe copy runs under
+   the rest of the staging (one core's memcpy bandwidth, ~15 GB/s, otherwise
+   bounds submit()).  Returns the bytes already queued for upload, or
+   UINT64_MAX on a HIP error.  An arena that expand() later rejects leaves the
+   slot free; its stale upload is overwritten by the next batch's copies,
+   which are ordered after it on the same stream. */
+static constexpr unsigned FDGPU_COPY_THREADS = 4;
+static constexpr uint64_t FDGPU_COPY_SPLIT_MIN = 4ull << 20;
+
+static uint64_t stage_arena(fdgpu_engine_t *e, Slot *s, uint8_t const *arena, uint64_t sz) {
+  if (sz < FDGPU_COPY_SPLIT_MIN) {
+    memcpy(s->h_arena, arena, sz);
+    return 0;
+  }
+  const uint64_t part = ((sz + FDGPU_COPY_THREADS - 1) / FDGPU_COPY_THREADS + 63) & ~63ull;
+  int err[FDGPU_COPY_THREADS] = {};
+  auto work = [&](unsigned i) {
+    const uint64_t off = (uint64_t)i * part;
+    if (off >= sz) return;
+    const uint64_t n = sz - off < part ? sz - off : part;
+    memcpy(s->h_arena + off, arena + off, n);
+    if (hipSetDevice(e->device) != hipSuccess ||
+        hipMemcpyAsync(s->d_arena + off, s->h_arena + off, n, hipMemcpyHostToDevice, s->stream) != hipSuccess)
+      err[i] = 1;
+  };
+  std::thread th[FDGPU_COPY_THREADS - 1];
+  for (unsigned i = 1; i < FDGPU_COPY_THREADS; i++) th[i - 1] = std::thread(work, i);
+  work(0);
+  for (auto &t : th) t.join();
+  for (unsigned i = 0; i < FDGPU_COPY_THREADS; i++)
+    if (err[i]) { set_err("staging upload failed"); return UINT64_MAX; }
+  return sz;
+}
+
 int64_t fdgpu_submit(fdgpu_engine_t *e, uint8_t const *arena, uint64_t arena_sz, fdgpu_txn_t const *txns,
                      uint64_t txn_cnt) {
   if (!e || (!arena && arena_sz) || (!txns && txn_cnt)) { set_err("null argument"); return FDGPU_ERR_INVAL; }
@@ -270,8 +311,9 @@ int64_t fdgpu_submit(fdgpu_engine_t *e, uint8_t const *arena, uint64_t arena_sz,
   Slot *s = free_slot(e);
   if (!s) { set_err("all ring slots hold unpolled batches"); return FDGPU_ERR_FULL; }
   /* the slot's previous batch was polled, so its copies are complete */
-  if (arena_sz) memcpy(s->h_arena, arena, arena_sz);
-  return submit_slot(e, s, arena_sz, txns, txn_cnt);
+  const uint64_t up = stage_arena(e, s, arena, arena_sz);
+  if (up == UINT64_MAX) return FDGPU_ERR_DEVICE;
+  return submit_slot(e, s, arena_sz, txns, txn_cnt, up);
 }
 
 uint8_t *fdgpu_stage_acquire(fdgpu_engine_t *e, uint64_t *cap) {
