@@ -42,7 +42,7 @@ def parse():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--txns", type=int, default=1_000_000, help="transactions per GPU")
-    ap.add_argument("--latency-batches", type=int, default=200)
+    ap.add_argument("--latency-batches", type=int, default=1000)   # >=1000 after 100 warm-up
     ap.add_argument("--latency-batch", type=int, default=65536)
     ap.add_argument("--cpu-sample", type=int, default=1_000_000, help="txns timed on the CPU oracle (bounded sample)")
     ap.add_argument("--no-extras", action="store_true", help="only the timed device-resident loop (profiling)")
@@ -120,7 +120,7 @@ def latency_and_pcie(eng, arena, txns, batch, nbatches):
         for f in ("msg_off", "sig_off", "pub_off"):
             t[f] -= lo
         views.append((np.ascontiguousarray(arena[lo:hi]), t))
-    for i in range(min(10, nbatches)):                     # warm-up
+    for i in range(100):                                   # warm-up
         a, t = views[i % len(views)]
         eng.verify_txns(a, t)
     lat = []
@@ -147,6 +147,16 @@ def latency_and_pcie(eng, arena, txns, batch, nbatches):
     return float(np.percentile(lat, 50)), float(np.percentile(lat, 99)), pcie
 
 
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
 def cpu_baseline(arena, txns, sample):
     from oracle import oracle as orc
     from firedancer_amd.workload import default_threads
@@ -155,7 +165,9 @@ def cpu_baseline(arena, txns, sample):
     t0 = time.perf_counter()
     codes = orc.verify_txns(arena, sub, nthreads=cores)
     dt = time.perf_counter() - t0
-    return {"value": round(int(sub["sig_cnt"].sum()) / dt, 1), "unit": "sigs/s", "cores": cores, "kind": "port",
+    rate = int(sub["sig_cnt"].sum()) / dt
+    return {"value": round(rate, 1), "unit": "sigs/s", "cores": cores, "kind": "port",
+            "per_core": round(rate / cores, 1), "cpu_model": cpu_model(),
             "sample": f"first {len(sub)} txns of the rank-0 cfg1 batch, oracle/fd_ed25519_oracle.c "
                       f"(C restatement, radix-2^51, wNAF) with {cores} threads, {dt:.2f} s wall",
             "published_ref_per_core": "20-40K sigs/s/core (Icelake, book/guide/tuning.md:75) -- published, not measured",
