@@ -271,6 +271,22 @@ def test_async_ring(engine):
     assert (c3 == c1).all()
 
 
+def test_threaded_staging_large_arena(engine, oracle):
+    """Arenas >= 4 MB are staged by 4 host threads, each queuing its part's
+    upload (fdgpu_engine.cpp stage_arena); sizes straddle the part rounding."""
+    arena, txns, _ = workload.cfg1(24000, seed=0x5151)
+    exp = oracle.verify_txns(arena, txns, nthreads=8)
+    dev = engine.upload(arena, txns)
+    dev.verify()
+    assert (dev.codes() == exp).all()
+    for n in (13000, 13001, 24000):          # 4.3 MB .. 7.9 MB arenas
+        t = txns[:n]
+        hi = int((t["msg_off"] + t["msg_sz"]).max())
+        assert hi >= 4 << 20
+        got = engine.verify_txns(np.ascontiguousarray(arena[:hi]), t)
+        assert (got == exp[:n]).all(), (n, np.nonzero(got != exp[:n])[0][:10])
+
+
 def test_device_resident_batch(engine):
     """Batch staged in HBM once, verified repeatedly (the benchmark path)."""
     arena, txns, modes = workload.cfg3(3000, seed=77)

@@ -83,6 +83,9 @@ def main():
                                   "pipelined_sigs_per_s": round(rate, 1),
                                   "submit_host_ms": round(t_sub / nsub * 1e3, 3),
                                   "submit_idle_ms": round(float(np.median(lsub)), 3),
+                                  "submit_idle_p99_ms": round(float(np.percentile(lsub, 99)), 3),
+                                  "p999_ms": round(float(np.percentile(lat, 99.9)), 3),
+                                  "n_over_2x_p50": int((lat > 2 * np.percentile(lat, 50)).sum()),
                                   "arena_mb": round(sum(v[0].size for v in vs) / len(vs) / 1e6, 2)}), flush=True)
 
 
