@@ -198,6 +198,20 @@ FDG_DEV void ge_add_cached_regs(ge_p1p1 &r, const ge_p3 &p, const uint32_t (&q)[
   r.Y = t;
 }
 
+/* A cached entry in registers (Y+X, Y-X, 2Z, 2dT) as a p2 point:
+   (Y+X) - (Y-X) = 2X and (Y+X) + (Y-X) = 2Y over 2Z are the same projective
+   point.  neg gives -P (Y+X and Y-X swapped).  X, Y carried to R; Z = the
+   entry's 2Z (R). */
+FDG_DEV void ge_cached_regs_to_p2(ge_p2 &r, const uint32_t (&q)[40], bool neg) {
+  fe a, b;
+#pragma unroll
+  for (int i = 0; i < 10; i++) { a.v[i] = neg ? q[10 + i] : q[i]; b.v[i] = neg ? q[i] : q[10 + i]; }
+  fe_sub(r.X, a, b); fe_carry(r.X);
+  fe_add(r.Y, a, b); fe_carry(r.Y);
+#pragma unroll
+  for (int i = 0; i < 10; i++) r.Z.v[i] = q[20 + i];
+}
+
 /* P + Q with Q an affine niels entry in registers (q[0..9] = y+x,
    q[10..19] = y-x, q[20..29] = 2dxy, canonical): 3M.  neg selects P - Q. */
 FDG_DEV void ge_add_niels_regs(ge_p1p1 &r, const ge_p3 &p, const uint32_t (&q)[32], bool neg) {

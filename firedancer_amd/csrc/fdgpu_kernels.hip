@@ -265,6 +265,22 @@ FDG_DEV void dsm(ge_p2 &acc2, uint32_t (&kd)[8], uint32_t (&sd)[8], const uint32
   }
 }
 
+FDG_DEV void atab_load(uint32_t (&q)[40], const uint32_t *wsl, int e) {
+  const uint4 *ent = (const uint4 *)(wsl + (uint32_t)(e < 0 ? -e : e) * FDGPU_ATAB_WORDS);
+#pragma unroll
+  for (int i = 0; i < 10; i++) {
+    const uint4 v = ent[i];
+    q[4 * i] = v.x; q[4 * i + 1] = v.y; q[4 * i + 2] = v.z; q[4 * i + 3] = v.w;
+  }
+}
+
+/* shift a 256-bit little-endian word vector left by 4 bits */
+FDG_DEV void shl4(uint32_t (&w)[8]) {
+#pragma unroll
+  for (int i = 7; i > 0; i--) w[i] = (w[i] << 4) | (w[i - 1] >> 28);
+  w[0] <<= 4;
+}
+
 /* FDGPU_BCOMB variant: R' = [k](-A) + [S]B with [S]B precomputed by the
    comb in pass 1 and parked (cached form) in workspace entry 10.  The chain
    only serves k: 64 windows of 4 doublings + one A-table addition; the last
@@ -303,49 +319,38 @@ FDG_DEV void dsm_k(ge_p2 &acc2, uint32_t (&kd)[KD_WORDS], const uint32_t *wsl) {
   }
 #else
 FDG_DEV void dsm_k(ge_p2 &acc2, uint32_t (&kd)[KD_WORDS], const uint32_t *wsl) {
-  ge_p2_0(acc2);
   ge_p3 acc3;
   ge_p1p1 t;
+  uint32_t q[40];
+  /* the top window would double the identity four times and then add its
+     entry: start from the entry itself (Horner's first step) */
+  {
+    const int e = sext4(kd[7] >> 28);
+    shl4(kd);
+    atab_load(q, wsl, e);
+    ge_cached_regs_to_p2(acc2, q, e < 0);
+  }
 #pragma unroll 1
-  for (int j = 31; j >= 0; j--) {
-    const uint32_t kb = kd[7] >> 24;
-    shl8(kd);
+  for (int j = 62; j >= 0; j--) {
+    const int e = sext4(kd[7] >> 28);
+    shl4(kd);
+    atab_load(q, wsl, e);
 #pragma unroll 1
-    for (int h = 0; h < 2; h++) {
-      const int e = sext4(h == 0 ? (kb >> 4) : (kb & 15u));
-      uint32_t q[40];
-      {
-        const uint4 *ent = (const uint4 *)(wsl + (uint32_t)(e < 0 ? -e : e) * FDGPU_ATAB_WORDS);
-#pragma unroll
-        for (int i = 0; i < 10; i++) {
-          const uint4 v = ent[i];
-          q[4 * i] = v.x; q[4 * i + 1] = v.y; q[4 * i + 2] = v.z; q[4 * i + 3] = v.w;
-        }
-      }
-#pragma unroll 1
-      for (int r = 0; r < 4; r++) {
-        ge_dbl(t, acc2);
-        ge_p1p1_to_p2(acc2, t);
-      }
-      acc3.X = acc2.X; acc3.Y = acc2.Y; acc3.Z = acc2.Z; fe_mul(acc3.T, t.X, t.Y);
-      ge_add_cached_regs(t, acc3, q, e < 0);
-      if (j == 0 && h == 1) break;
+    for (int r = 0; r < 4; r++) {
+      ge_dbl(t, acc2);
       ge_p1p1_to_p2(acc2, t);
     }
+    acc3.X = acc2.X; acc3.Y = acc2.Y; acc3.Z = acc2.Z; fe_mul(acc3.T, t.X, t.Y);
+    ge_add_cached_regs(t, acc3, q, e < 0);
+    if (j == 0) break;
+    ge_p1p1_to_p2(acc2, t);
   }
 #endif
   /* + [S]B (parked cached form) */
   ge_p1p1_to_p3(acc3, t);
-  uint32_t q[40];
-  {
-    const uint4 *ent = (const uint4 *)(wsl + FDGPU_WS_SB * FDGPU_ATAB_WORDS);
-#pragma unroll
-    for (int i = 0; i < 10; i++) {
-      const uint4 v = ent[i];
-      q[4 * i] = v.x; q[4 * i + 1] = v.y; q[4 * i + 2] = v.z; q[4 * i + 3] = v.w;
-    }
-  }
-  ge_add_cached_regs(t, acc3, q, false);
+  uint32_t qs[40];
+  atab_load(qs, wsl, FDGPU_WS_SB);
+  ge_add_cached_regs(t, acc3, qs, false);
   ge_p1p1_to_p2(acc2, t);
 }
 
