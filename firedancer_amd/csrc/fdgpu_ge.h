@@ -212,6 +212,21 @@ FDG_DEV void ge_cached_regs_to_p2(ge_p2 &r, const uint32_t (&q)[40], bool neg) {
   for (int i = 0; i < 10; i++) r.Z.v[i] = q[20 + i];
 }
 
+/* An affine niels entry in registers (y+x, y-x, 2dxy) as a p3 point:
+   X' = (y+x) - (y-x) = 2x, Y' = 2y, and (2X', 2Y', 4, X'Y') = 4 (x, y, 1, xy).
+   neg gives -P.  1M; X, Y carried to R. */
+FDG_DEV void ge_niels_regs_to_p3(ge_p3 &r, const uint32_t (&q)[32], bool neg) {
+  fe a, b, x2, y2;
+#pragma unroll
+  for (int i = 0; i < 10; i++) { a.v[i] = neg ? q[10 + i] : q[i]; b.v[i] = neg ? q[i] : q[10 + i]; }
+  fe_sub(x2, a, b); fe_carry(x2);
+  fe_add(y2, a, b); fe_carry(y2);
+  fe_mul(r.T, x2, y2);
+  fe_add(r.X, x2, x2); fe_carry(r.X);
+  fe_add(r.Y, y2, y2); fe_carry(r.Y);
+  fe_0(r.Z); r.Z.v[0] = 4;
+}
+
 /* P + Q with Q an affine niels entry in registers (q[0..9] = y+x,
    q[10..19] = y-x, q[20..29] = 2dxy, canonical): 3M.  neg selects P - Q. */
 FDG_DEV void ge_add_niels_regs(ge_p1p1 &r, const ge_p3 &p, const uint32_t (&q)[32], bool neg) {

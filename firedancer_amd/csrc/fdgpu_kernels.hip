@@ -377,13 +377,21 @@ FDG_DEV void comb_sb(ge_p3 &acc, const uint32_t (&S)[8], const uint32_t *__restr
       q[4 * i] = v.x; q[4 * i + 1] = v.y; q[4 * i + 2] = v.z; q[4 * i + 3] = v.w;
     }
   };
-  ge_p3_0(acc);
   uint32_t qa[32], qb[32];
   int d = next_digit();
   load_entry(qa, 0, d);
+  /* the first digit's entry is the starting point (no addition to O) */
+  {
+    const int dn = next_digit();
+    load_entry(qb, 1, dn);
+    ge_niels_regs_to_p3(acc, qa, d < 0);
+#pragma unroll
+    for (int w = 0; w < 32; w++) qa[w] = qb[w];
+    d = dn;
+  }
   ge_p1p1 t;
 #pragma unroll 1
-  for (uint32_t i = 0; i < BC_NDIG; i++) {
+  for (uint32_t i = 1; i < BC_NDIG; i++) {
     const int dn = next_digit();
     if (i + 1 < BC_NDIG) load_entry(qb, i + 1, dn);
     ge_add_niels_regs(t, acc, qa, d < 0);
