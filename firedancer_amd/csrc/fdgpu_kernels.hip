@@ -287,26 +287,27 @@ FDG_DEV void shl4(uint32_t (&w)[8]) {
    window's sum is converted to p3 and the parked [S]B added. */
 #if FDGPU_KWIN == 5
 FDG_DEV void dsm_k(ge_p2 &acc2, uint32_t (&kd)[KD_WORDS], const uint32_t *wsl) {
-  ge_p2_0(acc2);
   ge_p3 acc3;
   ge_p1p1 t;
+  uint32_t q[40];
   /* digit j (0..50) sits in byte j + 1; the top byte of the top word is read
      and the string shifted left by one byte per window */
-#pragma unroll 1
-  for (int j = 50; j >= 0; j--) {
+  auto next = [&kd]() {
     const int e = ((int)kd[KD_WORDS - 1]) >> 24;
 #pragma unroll
     for (int w = KD_WORDS - 1; w > 0; w--) kd[w] = (kd[w] << 8) | (kd[w - 1] >> 24);
     kd[0] <<= 8;
-    uint32_t q[40];
-    {
-      const uint4 *ent = (const uint4 *)(wsl + (uint32_t)(e < 0 ? -e : e) * FDGPU_ATAB_WORDS);
-#pragma unroll
-      for (int i = 0; i < 10; i++) {
-        const uint4 v = ent[i];
-        q[4 * i] = v.x; q[4 * i + 1] = v.y; q[4 * i + 2] = v.z; q[4 * i + 3] = v.w;
-      }
-    }
+    return e;
+  };
+  {                                    /* top window: start from its entry */
+    const int e = next();
+    atab_load(q, wsl, e);
+    ge_cached_regs_to_p2(acc2, q, e < 0);
+  }
+#pragma unroll 1
+  for (int j = 49; j >= 0; j--) {
+    const int e = next();
+    atab_load(q, wsl, e);
 #pragma unroll 1
     for (int r = 0; r < 5; r++) {
       ge_dbl(t, acc2);
@@ -412,11 +413,29 @@ FDG_DEV void atab_build(uint32_t *wsl, const ge_p3 &An) {
   ge_p3_to_cached(c, P); atab_store(wsl, 2, c);
   const uint32_t *ent1 = wsl + 1u * FDGPU_ATAB_WORDS;
   auto ld1 = [ent1](int cc, int w) { return ent1[10 * cc + w]; };
+#if FDGPU_KWIN == 4
+  /* even multiples by doubling the stored half (4S + 4M) instead of adding
+     -A (8M): 3 = 2 + 1, 4 = 2*2, 5 = 4 + 1, 6 = 2*3, 7 = 6 + 1, 8 = 2*4 */
+#pragma unroll 1
+  for (uint32_t e = 3; e < FDGPU_ATAB_ENTRIES; e++) {
+    if (e & 1u) {
+      ge_add_cached_ld(t, P, ld1, false);
+    } else {
+      uint32_t q[40];
+      atab_load(q, wsl, (int)(e >> 1));
+      ge_cached_regs_to_p2(a2, q, false);
+      ge_dbl(t, a2);
+    }
+    ge_p1p1_to_p3(P, t);
+    ge_p3_to_cached(c, P); atab_store(wsl, e, c);
+  }
+#else
 #pragma unroll 1
   for (uint32_t e = 3; e < FDGPU_ATAB_ENTRIES; e++) {
     ge_add_cached_ld(t, P, ld1, false); ge_p1p1_to_p3(P, t);
     ge_p3_to_cached(c, P); atab_store(wsl, e, c);
   }
+#endif
 }
 
 /* Workspace entry 9 ("park") words: 0-9 x_R, 10-19 y_R, 20-27 radix-16
