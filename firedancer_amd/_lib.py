@@ -80,6 +80,8 @@ def lib():
     L.fdgpu_dev_batch_upload.restype = vp
     L.fdgpu_dev_batch_verify.argtypes = [vp, vp]
     L.fdgpu_dev_batch_verify.restype = c.c_int
+    L.fdgpu_dev_batch_own_queue.argtypes = [vp, vp]
+    L.fdgpu_dev_batch_own_queue.restype = c.c_int
     L.fdgpu_dev_batch_codes.argtypes = [vp, vp, vp, vp]
     L.fdgpu_dev_batch_codes.restype = c.c_int
     L.fdgpu_dev_batch_free.argtypes = [vp, vp]

@@ -69,6 +69,7 @@ struct fdgpu_engine {
   int64_t next_ticket = 0;
   int8_t *d_scratch_codes = nullptr;   /* for fdgpu_verify_device with d_sig_codes == NULL */
   uint64_t scratch_cap = 0;
+  std::vector<hipStream_t> batch_streams;   /* streams of device batches with their own queue */
 };
 
 namespace {
@@ -199,6 +200,7 @@ void fdgpu_engine_close(fdgpu_engine_t *e) {
   (void)hipSetDevice(e->device);
   if (e->compute) (void)hipStreamSynchronize(e->compute);
   for (auto &s : e->slots) { if (s.stream) (void)hipStreamSynchronize(s.stream); slot_free(s); }
+  for (auto st : e->batch_streams) (void)hipStreamSynchronize(st);   /* btab is read there */
   if (e->d_btab) (void)hipFree(e->d_btab);
   if (e->d_ws) (void)hipFree(e->d_ws);
   if (e->d_scratch_codes) (void)hipFree(e->d_scratch_codes);
@@ -406,15 +408,48 @@ struct fdgpu_dev_batch {
   fdgpu_txn_desc_t *d_txns = nullptr;
   int8_t *d_sig_codes = nullptr, *d_txn_codes = nullptr;
   uint64_t n_sig = 0, n_txn = 0;
+  /* fdgpu_dev_batch_own_queue: a private stream + workspace, so verifies of
+     different batches run concurrently (the next batch's waves fill the CUs
+     the previous one's last, partial round leaves idle) */
+  hipStream_t stream = nullptr;
+  uint32_t *d_ws = nullptr;
 };
+
+namespace {
+hipStream_t batch_stream(fdgpu_engine_t *e, fdgpu_dev_batch_t *b) { return b->stream ? b->stream : e->compute; }
+uint32_t *batch_ws(fdgpu_engine_t *e, fdgpu_dev_batch_t *b) { return b->d_ws ? b->d_ws : e->d_ws; }
+}  // namespace
 
 extern "C" {
 
 uint64_t fdgpu_dev_batch_sig_cnt(fdgpu_dev_batch_t const *b) { return b ? b->n_sig : 0; }
 
+int fdgpu_dev_batch_own_queue(fdgpu_engine_t *e, fdgpu_dev_batch_t *b) {
+  if (!e || !b) return FDGPU_ERR_INVAL;
+  if (b->stream) return FDGPU_OK;
+  HIPCHK(hipSetDevice(e->device), FDGPU_ERR_DEVICE);
+  if (hipMalloc((void **)&b->d_ws, fdgpu_ws_bytes(b->n_sig ? b->n_sig : 1)) != hipSuccess) {
+    b->d_ws = nullptr; set_err("batch workspace alloc"); return FDGPU_ERR_DEVICE;
+  }
+  if (hipStreamCreateWithFlags(&b->stream, hipStreamNonBlocking) != hipSuccess) {
+    (void)hipFree(b->d_ws); b->d_ws = nullptr; b->stream = nullptr; set_err("batch stream"); return FDGPU_ERR_DEVICE;
+  }
+  e->batch_streams.push_back(b->stream);
+  return FDGPU_OK;
+}
+
 void fdgpu_dev_batch_free(fdgpu_engine_t *e, fdgpu_dev_batch_t *b) {
   if (!b) return;
   if (e) { (void)hipSetDevice(e->device); (void)hipStreamSynchronize(e->compute); }
+  if (b->stream) {
+    (void)hipStreamSynchronize(b->stream);
+    if (e) {
+      auto &v = e->batch_streams;
+      for (size_t i = 0; i < v.size(); i++) if (v[i] == b->stream) { v.erase(v.begin() + (long)i); break; }
+    }
+    (void)hipStreamDestroy(b->stream);
+  }
+  if (b->d_ws) (void)hipFree(b->d_ws);
   if (b->d_arena) (void)hipFree(b->d_arena);
   if (b->d_sigs) (void)hipFree(b->d_sigs);
   if (b->d_txns) (void)hipFree(b->d_txns);
@@ -457,13 +492,13 @@ int fdgpu_dev_batch_verify(fdgpu_engine_t *e, fdgpu_dev_batch_t *b) {
   if (!e || !b) return FDGPU_ERR_INVAL;
   HIPCHK(hipSetDevice(e->device), FDGPU_ERR_DEVICE);
   return enqueue_verify(e, b->d_arena, b->d_sigs, b->n_sig, b->d_txns, b->n_txn, b->d_sig_codes, b->d_txn_codes,
-                        e->compute);
+                        batch_stream(e, b), b->d_ws);
 }
 
 int fdgpu_dev_batch_codes(fdgpu_engine_t *e, fdgpu_dev_batch_t *b, int8_t *txn_codes, int8_t *sig_codes) {
   if (!e || !b) return FDGPU_ERR_INVAL;
   HIPCHK(hipSetDevice(e->device), FDGPU_ERR_DEVICE);
-  HIPCHK(hipStreamSynchronize(e->compute), FDGPU_ERR_DEVICE);
+  HIPCHK(hipStreamSynchronize(batch_stream(e, b)), FDGPU_ERR_DEVICE);
   if (txn_codes && b->n_txn) HIPCHK(hipMemcpy(txn_codes, b->d_txn_codes, b->n_txn, hipMemcpyDeviceToHost), FDGPU_ERR_DEVICE);
   if (sig_codes && b->n_sig) HIPCHK(hipMemcpy(sig_codes, b->d_sig_codes, b->n_sig, hipMemcpyDeviceToHost), FDGPU_ERR_DEVICE);
   return FDGPU_OK;
@@ -474,17 +509,23 @@ int fdgpu_dev_batch_time(fdgpu_engine_t *e, fdgpu_dev_batch_t *b, int iters, dou
   if (!e || !b || iters < 1) return FDGPU_ERR_INVAL;
   HIPCHK(hipSetDevice(e->device), FDGPU_ERR_DEVICE);
   const uint32_t flags = (e->cfg.flags & FDGPU_FLAG_REF_MAPPING) ? FDGPU_FLAG_REF_MAP : 0u;
+  const hipStream_t st = batch_stream(e, b);
+  if (!b->d_ws && b->n_sig > e->ws_sig) {
+    HIPCHK(hipStreamSynchronize(e->compute), FDGPU_ERR_DEVICE);
+    const int wrc = ensure_ws(e, b->n_sig);
+    if (wrc) return wrc;
+  }
   std::vector<hipEvent_t> ev(3 * (size_t)iters + 1);
   for (auto &x : ev) HIPCHK(hipEventCreate(&x), FDGPU_ERR_DEVICE);
   int rc = FDGPU_OK;
   for (int i = 0; i < iters && rc == FDGPU_OK; i++) {
-    if (hipEventRecord(ev[3 * i], e->compute) != hipSuccess) rc = FDGPU_ERR_DEVICE;
-    if (fdgpu_launch_verify_sigs(b->d_arena, b->d_sigs, (uint32_t)b->n_sig, e->d_btab, e->d_ws, b->d_sig_codes, flags,
-                                 e->compute) != hipSuccess) rc = FDGPU_ERR_DEVICE;
-    if (hipEventRecord(ev[3 * i + 1], e->compute) != hipSuccess) rc = FDGPU_ERR_DEVICE;
-    if (fdgpu_launch_combine(b->d_txns, (uint32_t)b->n_txn, b->d_sig_codes, b->d_txn_codes, e->compute) != hipSuccess)
+    if (hipEventRecord(ev[3 * i], st) != hipSuccess) rc = FDGPU_ERR_DEVICE;
+    if (fdgpu_launch_verify_sigs(b->d_arena, b->d_sigs, (uint32_t)b->n_sig, e->d_btab, batch_ws(e, b), b->d_sig_codes,
+                                 flags, st) != hipSuccess) rc = FDGPU_ERR_DEVICE;
+    if (hipEventRecord(ev[3 * i + 1], st) != hipSuccess) rc = FDGPU_ERR_DEVICE;
+    if (fdgpu_launch_combine(b->d_txns, (uint32_t)b->n_txn, b->d_sig_codes, b->d_txn_codes, st) != hipSuccess)
       rc = FDGPU_ERR_DEVICE;
-    if (hipEventRecord(ev[3 * i + 2], e->compute) != hipSuccess) rc = FDGPU_ERR_DEVICE;
+    if (hipEventRecord(ev[3 * i + 2], st) != hipSuccess) rc = FDGPU_ERR_DEVICE;
   }
   if (rc == FDGPU_OK && hipEventSynchronize(ev[3 * (iters - 1) + 2]) != hipSuccess) rc = FDGPU_ERR_DEVICE;
   double sv = 0, sc = 0;
@@ -510,6 +551,7 @@ int fdgpu_sync(fdgpu_engine_t *e) {
   HIPCHK(hipSetDevice(e->device), FDGPU_ERR_DEVICE);
   HIPCHK(hipStreamSynchronize(e->compute), FDGPU_ERR_DEVICE);
   for (auto &s : e->slots) HIPCHK(hipStreamSynchronize(s.stream), FDGPU_ERR_DEVICE);
+  for (auto st : e->batch_streams) HIPCHK(hipStreamSynchronize(st), FDGPU_ERR_DEVICE);
   return FDGPU_OK;
 }
 

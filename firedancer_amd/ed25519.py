@@ -224,8 +224,17 @@ class DeviceBatch:
             raise RuntimeError(f"fdgpu_dev_batch_upload failed: {_lib.last_error()}")
         self.n_sig = int(_lib.lib().fdgpu_dev_batch_sig_cnt(self._b))
 
+    def own_queue(self):
+        """Give this batch its own HIP stream + workspace (verifies of
+        different batches then overlap on the GPU, like ring slots)."""
+        rc = _lib.lib().fdgpu_dev_batch_own_queue(self._e._h, self._b)
+        if rc != 0:
+            raise RuntimeError(f"fdgpu_dev_batch_own_queue failed ({rc}): {_lib.last_error()}")
+        return self
+
     def verify(self):
-        """Enqueue one verify (async on the engine's compute stream)."""
+        """Enqueue one verify (async on the batch's queue: the engine's
+        compute stream unless own_queue() was called)."""
         rc = _lib.lib().fdgpu_dev_batch_verify(self._e._h, self._b)
         if rc != 0:
             raise RuntimeError(f"fdgpu_dev_batch_verify failed ({rc}): {_lib.last_error()}")

@@ -161,9 +161,14 @@ typedef struct fdgpu_dev_batch fdgpu_dev_batch_t;
 
 fdgpu_dev_batch_t * fdgpu_dev_batch_upload( fdgpu_engine_t * e, uint8_t const * arena, uint64_t arena_sz,
                                             fdgpu_txn_t const * txns, uint64_t txn_cnt );
-/* enqueue one verify of the batch on the engine's compute stream (async) */
+/* enqueue one verify of the batch on its queue (async): the engine's compute
+   stream, or the batch's own stream after fdgpu_dev_batch_own_queue */
 int  fdgpu_dev_batch_verify( fdgpu_engine_t * e, fdgpu_dev_batch_t * b );
-/* wait for the compute stream and copy the per-txn (and optionally per-signature) codes out */
+/* gives the batch a private HIP stream and workspace (fdgpu_ws_bytes of its
+   signature count), so verifies of different batches overlap on the GPU the
+   way the ring slots of fdgpu_submit do; idempotent */
+int  fdgpu_dev_batch_own_queue( fdgpu_engine_t * e, fdgpu_dev_batch_t * b );
+/* wait for the batch's queue and copy the per-txn (and optionally per-signature) codes out */
 int  fdgpu_dev_batch_codes( fdgpu_engine_t * e, fdgpu_dev_batch_t * b, int8_t * txn_codes, int8_t * sig_codes );
 void fdgpu_dev_batch_free( fdgpu_engine_t * e, fdgpu_dev_batch_t * b );
 uint64_t fdgpu_dev_batch_sig_cnt( fdgpu_dev_batch_t const * b );

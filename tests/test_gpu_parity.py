@@ -304,6 +304,28 @@ def test_device_resident_batch(engine):
     b.free()
 
 
+def test_device_batches_own_queues(engine, oracle):
+    """Batches on their own streams + workspaces (the bench's overlapped
+    steps): concurrent verifies of different batches and of the compute-stream
+    path give the oracle's codes, and engine.sync() covers every queue."""
+    sets = [workload.cfg1(70000, seed=0x0A01), workload.cfg3(4000, seed=0x0A02), workload.cfg1(3001, seed=0x0A03)]
+    exp = [oracle.verify_txns(a, t, nthreads=8) for a, t, _ in sets]
+    bs = [engine.upload(a, t).own_queue() for a, t, _ in sets]
+    shared = engine.upload(*sets[2][:2])                 # engine compute stream, engine workspace
+    for _ in range(3):
+        for b in bs:
+            b.verify()
+        shared.verify()
+    engine.sync()
+    for b, e in zip(bs, exp):
+        assert (b.codes() == e).all()
+    assert (shared.codes() == exp[2]).all()
+    wall, kv, kc = bs[0].time(2)
+    assert wall > 0 and 0 < kv <= wall
+    for b in bs + [shared]:
+        b.free()
+
+
 def test_raw_device_pointer_api(engine):
     """fdgpu_verify_device with caller-owned device buffers (pointers taken
     from an engine-owned DeviceBatch; no torch involvement)."""
