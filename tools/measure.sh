@@ -13,7 +13,7 @@ timeout -k 10 300 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout
 tail -1 $out/tests.log
 step kernel-trace
 timeout -k 10 240 rocprofv3 --kernel-trace --stats -d $out/trace -o run --output-format csv \
-  -- python3 bench.py --no-extras --steps 10 --warmup 2 > $out/trace_bench.json 2>$out/trace.err || { tail $out/trace.err; exit 1; }
+  -- python3 bench.py --no-extras --queues 1 --steps 10 --warmup 2 > $out/trace_bench.json 2>$out/trace.err || { tail $out/trace.err; exit 1; }
 cp $(find $out/trace -name '*kernel_stats.csv' | head -1) $out/kernel_stats.csv
 P=(FETCH_SIZE WRITE_SIZE
    "SQ_INSTS_VALU SQ_INSTS_VALU_INT32 SQ_INSTS_VALU_INT64 SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_LDS_BANK_CONFLICT"
@@ -22,7 +22,7 @@ dirs=()
 for i in "${!P[@]}"; do
   step pmc pass $i: ${P[$i]}
   timeout -s KILL 120 rocprofv3 --pmc ${P[$i]} -d $out/pmc_$i -o run --output-format csv \
-    -- python3 bench.py --no-extras --steps 3 --warmup 1 > $out/pmc_$i.json 2>$out/pmc_$i.err || { tail $out/pmc_$i.err; exit 1; }
+    -- python3 bench.py --no-extras --queues 1 --steps 3 --warmup 1 > $out/pmc_$i.json 2>$out/pmc_$i.err || { tail $out/pmc_$i.err; exit 1; }
   dirs+=($out/pmc_$i)
 done
 PMC_OUT_DIR=profiles python3 tools/pmc_summary.py $tag "${dirs[@]}" > /dev/null && cp profiles/${tag}_pmc.json $out/
