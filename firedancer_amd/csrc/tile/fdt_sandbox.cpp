@@ -1,0 +1,156 @@
+/* fdt_sandbox.cpp -- process separation for the verify stage (SURVEY.md
+   §8(f) row 1, last bullet): tango links laid out in one shared-memory
+   region that independent processes join, and the tiles' seccomp sandbox.
+
+   Why: the reference's tiles run one per process and, after privileged init,
+   inside a seccomp policy that allows only write(2 or logfile_fd) and
+   fsync(logfile_fd) (src/app/fdctl/run/tiles/verify.seccomppolicy:1-19,
+   dedup.seccomppolicy; entered at src/disco/topo/fd_topo_run.c:96-103).  A
+   GPU engine needs ioctls on /dev/kfd for every submission, so the GPU side
+   runs as its own (unsandboxed) engine process, fed over tango links in
+   shared memory -- the wiredancer precedent (src/wiredancer/c/wd_f1.h:71-112)
+   -- while the tiles around it (dedup, and anything else that only touches
+   links) keep the reference's sandbox.
+
+   Link region layout (fdt_link_new / fdt_link_join; offsets from the region
+   base, every part 4 KiB aligned so the region can be mapped anywhere):
+     [0, 4096)        header: magic, depth, mtu, seq0, data_sz, mcache_off,
+                      dcache_off; the consumer fseq on its own 128-B line
+     [4096, ...)      mcache: depth x fdt_frag_meta_t (fd_mcache.h:265-322)
+     [dcache_off, ..) compact dcache for depth frags of <= mtu (fd_dcache.h) */
+#include <errno.h>
+#include <linux/audit.h>
+#include <linux/filter.h>
+#include <linux/seccomp.h>
+#include <stddef.h>
+#include <string.h>
+#include <sys/prctl.h>
+#include <sys/syscall.h>
+#include <time.h>
+#include <unistd.h>
+
+#include "../../../include/fd_verify_tile.h"
+
+namespace {
+
+constexpr uint64_t LINK_MAGIC = 0xFD7A960114C0DE01ull;
+constexpr uint64_t LINK_HDR = 4096;
+constexpr uint64_t FSEQ_OFF = 128;
+
+struct link_hdr {
+  uint64_t magic, depth, mtu, seq0, data_sz, mcache_off, dcache_off;
+};
+
+uint64_t align_up(uint64_t x, uint64_t a) { return (x + a - 1) & ~(a - 1); }
+
+uint64_t mono_ns() {
+  timespec ts;
+  clock_gettime(CLOCK_MONOTONIC, &ts);
+  return (uint64_t)ts.tv_sec * 1000000000ull + (uint64_t)ts.tv_nsec;
+}
+
+}  // namespace
+
+extern "C" {
+
+uint64_t fdt_link_footprint(uint64_t depth, uint64_t mtu) {
+  if (!depth || (depth & (depth - 1)) || !mtu) return 0;
+  const uint64_t dc_off = align_up(LINK_HDR + depth * sizeof(fdt_frag_meta_t), 4096);
+  return align_up(dc_off + fdt_dcache_data_sz(mtu, depth), 4096);
+}
+
+int fdt_link_new(void *mem, uint64_t depth, uint64_t mtu, uint64_t seq0) {
+  const uint64_t fp = fdt_link_footprint(depth, mtu);
+  if (!mem || !fp || ((uintptr_t)mem & 4095)) return -1;
+  auto *h = (link_hdr *)mem;
+  h->magic = 0;                                   /* not joinable until fully formatted */
+  h->depth = depth;
+  h->mtu = mtu;
+  h->seq0 = seq0;
+  h->data_sz = fdt_dcache_data_sz(mtu, depth);
+  h->mcache_off = LINK_HDR;
+  h->dcache_off = align_up(LINK_HDR + depth * sizeof(fdt_frag_meta_t), 4096);
+  *(volatile uint64_t *)((uint8_t *)mem + FSEQ_OFF) = seq0;
+  fdt_mcache_init((fdt_frag_meta_t *)((uint8_t *)mem + h->mcache_off), depth, seq0);
+  __atomic_store_n(&h->magic, LINK_MAGIC, __ATOMIC_RELEASE);
+  return 0;
+}
+
+int fdt_link_join(void *mem, fdt_link_t *out) {
+  if (!mem || !out) return -1;
+  auto *h = (link_hdr *)mem;
+  if (__atomic_load_n(&h->magic, __ATOMIC_ACQUIRE) != LINK_MAGIC) return -1;
+  auto *base = (uint8_t *)mem;
+  out->mcache = (fdt_frag_meta_t *)(base + h->mcache_off);
+  out->depth = h->depth;
+  out->seq0 = h->seq0;
+  out->mtu = h->mtu;
+  out->base = base + h->dcache_off;
+  out->chunk0 = 0;
+  out->wmark = fdt_dcache_wmark(0, h->data_sz >> FDT_CHUNK_LG_SZ, h->mtu);
+  out->fseq = (uint64_t *)(base + FSEQ_OFF);
+  return 0;
+}
+
+/* The tiles' policy, restated as a classic-BPF seccomp filter:
+     write   iff fd == 2 or fd == logfile_fd   (verify.seccomppolicy:11-12)
+     fsync   iff fd == logfile_fd              (:17)
+     exit, exit_group                          (leaving the loop)
+     clock_gettime                             (only reached when the vDSO
+                                                falls back to the syscall)
+   anything else kills the process (SECCOMP_RET_KILL_PROCESS), as the
+   reference's generated filters do. */
+int fdt_sandbox_enter(int logfile_fd) {
+  const uint32_t lfd = (uint32_t)(logfile_fd < 0 ? 2 : logfile_fd);
+  struct sock_filter f[] = {
+    BPF_STMT(BPF_LD | BPF_W | BPF_ABS, offsetof(struct seccomp_data, arch)),
+    BPF_JUMP(BPF_JMP | BPF_JEQ | BPF_K, AUDIT_ARCH_X86_64, 1, 0),
+    BPF_STMT(BPF_RET | BPF_K, SECCOMP_RET_KILL_PROCESS),
+    BPF_STMT(BPF_LD | BPF_W | BPF_ABS, offsetof(struct seccomp_data, nr)),
+    BPF_JUMP(BPF_JMP | BPF_JEQ | BPF_K, __NR_write, 0, 4),
+    /* write: fd in {2, logfile_fd} */
+    BPF_STMT(BPF_LD | BPF_W | BPF_ABS, offsetof(struct seccomp_data, args[0])),
+    BPF_JUMP(BPF_JMP | BPF_JEQ | BPF_K, 2, 10, 0),
+    BPF_JUMP(BPF_JMP | BPF_JEQ | BPF_K, lfd, 9, 0),
+    BPF_STMT(BPF_RET | BPF_K, SECCOMP_RET_KILL_PROCESS),
+    BPF_JUMP(BPF_JMP | BPF_JEQ | BPF_K, __NR_fsync, 0, 3),
+    /* fsync: fd == logfile_fd */
+    BPF_STMT(BPF_LD | BPF_W | BPF_ABS, offsetof(struct seccomp_data, args[0])),
+    BPF_JUMP(BPF_JMP | BPF_JEQ | BPF_K, lfd, 5, 0),
+    BPF_STMT(BPF_RET | BPF_K, SECCOMP_RET_KILL_PROCESS),
+    BPF_JUMP(BPF_JMP | BPF_JEQ | BPF_K, __NR_exit_group, 3, 0),
+    BPF_JUMP(BPF_JMP | BPF_JEQ | BPF_K, __NR_exit, 2, 0),
+    BPF_JUMP(BPF_JMP | BPF_JEQ | BPF_K, __NR_clock_gettime, 1, 0),
+    BPF_STMT(BPF_RET | BPF_K, SECCOMP_RET_KILL_PROCESS),
+    BPF_STMT(BPF_RET | BPF_K, SECCOMP_RET_ALLOW),
+  };
+  struct sock_fprog prog = {(unsigned short)(sizeof(f) / sizeof(f[0])), f};
+  if (prctl(PR_SET_NO_NEW_PRIVS, 1, 0, 0, 0)) return -errno;
+  if (syscall(__NR_seccomp, SECCOMP_SET_MODE_FILTER, 0, &prog)) return -errno;
+  return 0;
+}
+
+/* Dedup tile main loop inside the sandbox (a child process of whoever set
+   up the links): steps until frag_target frags were consumed or nothing
+   arrived for idle_ns_max, stores the final stats into stats_out (shared
+   memory the parent reads) and exits the process: 0 target reached, 1 idle
+   timeout, 3 sandbox could not be entered.  Never returns. */
+void fdgpu_dtile_run_sandboxed(fdgpu_dtile_t *t, uint64_t frag_target, uint64_t idle_ns_max,
+                               fdgpu_dtile_stats_t *stats_out, int logfile_fd) {
+  if (fdt_sandbox_enter(logfile_fd)) syscall(__NR_exit_group, 3);
+  fdgpu_dtile_stats_t st;
+  uint64_t last = mono_ns();
+  int rc = 0;
+  for (;;) {
+    if (fdgpu_dtile_step(t) > 0) last = mono_ns();
+    fdgpu_dtile_stats(t, &st);
+    if (st.in_frags + st.overrun >= frag_target) break;
+    if (mono_ns() - last > idle_ns_max) { rc = 1; break; }
+  }
+  memcpy(stats_out, &st, sizeof(st));
+  __atomic_thread_fence(__ATOMIC_SEQ_CST);
+  syscall(__NR_exit_group, rc);
+  for (;;) {}
+}
+
+}  // extern "C"

@@ -17,6 +17,7 @@ Reference interfaces restated (names follow the reference):
 The library is required: there is no Python fallback for any of it.
 """
 import ctypes
+import mmap
 import os
 
 import numpy as np
@@ -120,6 +121,11 @@ class DTileStats(c.Structure):
         return {n: getattr(self, n) for n, _ in self._fields_}
 
 
+class LinkT(c.Structure):
+    _fields_ = [("mcache", vp), ("depth", c.c_uint64), ("seq0", c.c_uint64), ("mtu", c.c_uint64),
+                ("base", vp), ("chunk0", c.c_uint64), ("wmark", c.c_uint64), ("fseq", vp)]
+
+
 def lib():
     """Load libfd_verify_tile.so (and through it libfd_ed25519_gpu.so). Raises if absent."""
     global _TL
@@ -168,6 +174,11 @@ def lib():
         "fdgpu_dtile_step": (i64, [vp]),
         "fdgpu_dtile_stats": (None, [vp, c.POINTER(DTileStats)]),
         "fdgpu_producer_start": (vp, [vp, u64, u64, vp, u64, u64, vp, vp, vp, u64, c.c_double]),
+        "fdt_link_footprint": (u64, [u64, u64]),
+        "fdt_link_new": (c.c_int, [vp, u64, u64, u64]),
+        "fdt_link_join": (c.c_int, [vp, c.POINTER(LinkT)]),
+        "fdt_sandbox_enter": (c.c_int, [c.c_int]),
+        "fdgpu_dtile_run_sandboxed": (None, [vp, u64, u64, c.POINTER(DTileStats), c.c_int]),
         "fdgpu_producer_join": (u64, [vp, c.POINTER(c.c_double)]),
     }
     for name, (res, args) in sig.items():
@@ -183,6 +194,14 @@ def header_functions():
     text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
     names = re.findall(r"^[A-Za-z_][\w \t\*]*?\b(fd\w+)\s*\(", text, flags=re.M)
     return sorted(set(n for n in names if not n.startswith("FD_")))
+
+
+def sandbox_enter(logfile_fd=2):
+    """Enters the tiles' seccomp policy in this process (irreversible; only
+    write to fd 2 / logfile_fd, fsync, clock_gettime and exit remain)."""
+    r = lib().fdt_sandbox_enter(logfile_fd)
+    if r:
+        raise OSError(-r, "fdt_sandbox_enter failed")
 
 
 def _aligned(nbytes, align):
@@ -289,6 +308,52 @@ class Link:
         self.fseq[0] = seq0
         L.fdt_mcache_init(self.mcache.ctypes.data, depth, seq0)
         self._pub_seq, self._pub_chunk = seq0, 0
+
+    @classmethod
+    def shm_create(cls, path, depth, mtu, seq0=0):
+        """A link formatted in a shared-memory file (fdt_link_new), joinable
+        by other processes with shm_join(path): the engine process and the
+        sandboxed tiles share links this way (fd_wksp's role)."""
+        fp = lib().fdt_link_footprint(depth, mtu)
+        if not fp:
+            raise ValueError("bad link parameters")
+        fd = os.open(path, os.O_RDWR | os.O_CREAT | os.O_TRUNC, 0o600)
+        try:
+            os.ftruncate(fd, fp)
+            mm = mmap.mmap(fd, fp, mmap.MAP_SHARED, mmap.PROT_READ | mmap.PROT_WRITE)
+        finally:
+            os.close(fd)
+        region = np.frombuffer(mm, dtype=np.uint8)
+        if lib().fdt_link_new(region.ctypes.data, depth, mtu, seq0):
+            raise RuntimeError("fdt_link_new failed")
+        return cls._from_region(mm, region)
+
+    @classmethod
+    def shm_join(cls, path):
+        fd = os.open(path, os.O_RDWR)
+        try:
+            mm = mmap.mmap(fd, os.fstat(fd).st_size, mmap.MAP_SHARED, mmap.PROT_READ | mmap.PROT_WRITE)
+        finally:
+            os.close(fd)
+        return cls._from_region(mm, np.frombuffer(mm, dtype=np.uint8))
+
+    @classmethod
+    def _from_region(cls, mm, region):
+        v = LinkT()
+        if lib().fdt_link_join(region.ctypes.data, c.byref(v)):
+            raise RuntimeError("not a formatted link region")
+        base = region.ctypes.data
+        self = cls.__new__(cls)
+        self._mm, self._region = mm, region
+        self.depth, self.mtu, self.seq0 = v.depth, v.mtu, v.seq0
+        mo, do, fo = v.mcache - base, v.base - base, v.fseq - base
+        self.mcache = region[mo:mo + v.depth * 32].view(FRAG_META_DTYPE)
+        self.dcache = region[do:]
+        self.fseq = region[fo:fo + 8].view(np.uint64)
+        self.chunk0, self.wmark = v.chunk0, v.wmark
+        self.chunk1 = len(self.dcache) // CHUNK_SZ
+        self._pub_seq, self._pub_chunk = v.seq0, v.chunk0
+        return self
 
     @property
     def mcache_ptr(self):
@@ -512,6 +577,24 @@ class DedupTile:
         s = DTileStats()
         lib().fdgpu_dtile_stats(self._t, c.byref(s))
         return s.as_dict()
+
+    def fork_sandboxed(self, frag_target, idle_s=10.0, logfile_fd=2):
+        """Runs this tile in a forked child process inside the tiles' seccomp
+        sandbox (fdgpu_dtile_run_sandboxed).  Its links must live in shared
+        memory (Link.shm_create).  Returns (pid, stats_fn): stats_fn() reads
+        the stats the child left behind once it has exited."""
+        shared = mmap.mmap(-1, c.sizeof(DTileStats), mmap.MAP_SHARED, mmap.PROT_READ | mmap.PROT_WRITE)
+        st = DTileStats.from_buffer(shared)
+        pid = os.fork()
+        if pid == 0:                                             # child: never returns
+            try:
+                lib().fdgpu_dtile_run_sandboxed(self._t, frag_target, int(idle_s * 1e9), c.byref(st), logfile_fd)
+            finally:
+                os._exit(4)
+
+        def stats():
+            return DTileStats.from_buffer_copy(shared).as_dict()
+        return pid, stats
 
     def close(self):
         if self._t:

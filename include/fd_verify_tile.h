@@ -307,6 +307,40 @@ void            fdgpu_dtile_delete( fdgpu_dtile_t * t );
 int64_t         fdgpu_dtile_step  ( fdgpu_dtile_t * t );   /* frags consumed this step */
 void            fdgpu_dtile_stats ( fdgpu_dtile_t const * t, fdgpu_dtile_stats_t * out );
 
+/* --------------------------------------- process separation (§8(f) row 1) */
+
+/* A link (mcache + compact dcache + consumer fseq) formatted inside one
+   caller-mapped region (e.g. a /dev/shm file), so that the engine process
+   and sandboxed tiles in other processes can join it -- the role fd_wksp
+   plays for the reference's tango objects.  mem must be 4096-aligned. */
+typedef struct {
+  fdt_frag_meta_t * mcache;
+  uint64_t          depth;
+  uint64_t          seq0;
+  uint64_t          mtu;
+  uint8_t *         base;      /* chunk 0 */
+  uint64_t          chunk0;
+  uint64_t          wmark;
+  uint64_t *        fseq;      /* reliable consumer's next seq */
+} fdt_link_t;
+
+uint64_t fdt_link_footprint( uint64_t depth, uint64_t mtu );   /* 0 on bad parameters */
+int      fdt_link_new      ( void * mem, uint64_t depth, uint64_t mtu, uint64_t seq0 );
+int      fdt_link_join     ( void * mem, fdt_link_t * out );   /* 0, or -1 if not a formatted link */
+
+/* Enters the tiles' seccomp policy (src/app/fdctl/run/tiles/
+   verify.seccomppolicy, dedup.seccomppolicy): from here on only write to fd
+   2 / logfile_fd, fsync(logfile_fd), clock_gettime and exit are allowed;
+   any other syscall kills the process.  Returns 0 or -errno. */
+int      fdt_sandbox_enter ( int logfile_fd );
+/* Runs a dedup tile inside the sandbox until frag_target frags were
+   consumed (or lost to overrun) or none arrived for idle_ns_max; writes the
+   final stats to stats_out (shared memory) and exits the calling process
+   with 0 (target reached), 1 (idle) or 3 (sandbox failed).  Never returns:
+   call it in a child process. */
+void     fdgpu_dtile_run_sandboxed( fdgpu_dtile_t * t, uint64_t frag_target, uint64_t idle_ns_max,
+                                    fdgpu_dtile_stats_t * stats_out, int logfile_fd );
+
 /* ------------------------------------------------------- frag producer */
 
 /* A line-rate producer thread standing in for the quic tile: publishes
