@@ -174,6 +174,8 @@ def lib():
         "fdgpu_dtile_step": (i64, [vp]),
         "fdgpu_dtile_stats": (None, [vp, c.POINTER(DTileStats)]),
         "fdgpu_producer_start": (vp, [vp, u64, u64, vp, u64, u64, vp, vp, vp, u64, c.c_double]),
+        "fdgpu_replay_verify": (c.c_int, [Verifier, vp, vp, vp, u64, u64, u64, vp]),
+        "fdgpu_fec_roots_verify": (c.c_int, [Verifier, vp, vp, vp, c.c_int, u64, u64, vp]),
         "fdt_link_footprint": (u64, [u64, u64]),
         "fdt_link_new": (c.c_int, [vp, u64, u64, u64]),
         "fdt_link_join": (c.c_int, [vp, c.POINTER(LinkT)]),
@@ -465,6 +467,46 @@ class EngineVerifier:
         if self._d:
             lib().fdgpu_dispatch_delete(self._d)
             self._d = None
+
+
+# ------------------------------------------------------- other callers
+
+REPLAY_PARSE_FAIL = 1
+
+
+def replay_verify(verifier, payloads, batch_txn_max=4096, batch_bytes_max=4096 * 1232):
+    """fd_executor_txn_verify over a block's raw txns, batched
+    (fdgpu_replay_verify): one fd_ed25519 code per payload, or
+    REPLAY_PARSE_FAIL."""
+    n = len(payloads)
+    sizes = np.array([len(p) for p in payloads], dtype=np.uint32)
+    offs = np.zeros(n, dtype=np.uint64)
+    if n:
+        offs[1:] = np.cumsum(sizes[:-1], dtype=np.uint64)
+    arena = np.frombuffer(b"".join(payloads) + b"\0", dtype=np.uint8)
+    codes = np.zeros(max(n, 1), dtype=np.int8)
+    r = lib().fdgpu_replay_verify(verifier.struct, arena.ctypes.data, offs.ctypes.data, sizes.ctypes.data, n,
+                                  batch_txn_max, batch_bytes_max, codes.ctypes.data)
+    if r:
+        raise RuntimeError(f"fdgpu_replay_verify failed: {r}")
+    return codes[:n]
+
+
+def fec_roots_verify(verifier, roots, sigs, pubkeys, batch_max=65536):
+    """fd_ed25519_verify(root, 32, sig, leader_pubkey) per FEC set
+    (fdgpu_fec_roots_verify); pubkeys: one 32-B key (shared) or one per set."""
+    roots = np.ascontiguousarray(np.frombuffer(bytes(roots), dtype=np.uint8))
+    sigs = np.ascontiguousarray(np.frombuffer(bytes(sigs), dtype=np.uint8))
+    pubkeys = np.ascontiguousarray(np.frombuffer(bytes(pubkeys), dtype=np.uint8))
+    n = len(roots) // 32
+    if len(sigs) != 64 * n or len(pubkeys) not in (32, 32 * n):
+        raise ValueError("roots/sigs/pubkeys sizes disagree")
+    codes = np.zeros(max(n, 1), dtype=np.int8)
+    r = lib().fdgpu_fec_roots_verify(verifier.struct, roots.ctypes.data, sigs.ctypes.data, pubkeys.ctypes.data,
+                                     1 if len(pubkeys) == 32 and n != 1 else 0, n, batch_max, codes.ctypes.data)
+    if r:
+        raise RuntimeError(f"fdgpu_fec_roots_verify failed: {r}")
+    return codes[:n]
 
 
 # ------------------------------------------------------------------ tiles

@@ -307,6 +307,28 @@ void            fdgpu_dtile_delete( fdgpu_dtile_t * t );
 int64_t         fdgpu_dtile_step  ( fdgpu_dtile_t * t );   /* frags consumed this step */
 void            fdgpu_dtile_stats ( fdgpu_dtile_t const * t, fdgpu_dtile_stats_t * out );
 
+/* ------------------------------------- other callers (§8(f) row 4) */
+
+/* Replay: fd_executor_txn_verify (src/flamenco/runtime/fd_executor.c:
+   1157-1185) for every raw transaction payloads[off[i], off[i]+sz[i]) of a
+   block, batched: each is parsed (fdt_txn_parse) and verified with
+   fd_ed25519_verify_batch_single_msg semantics over the verifier, in
+   batches of <= batch_txn_max txns / batch_bytes_max (>= FDT_TXN_MTU)
+   payload bytes, two in flight.  codes[i] = the fd_ed25519 code (0 =
+   verified; fd_executor_txn_verify returns -1 for any other) or
+   FDGPU_REPLAY_PARSE_FAIL.  Returns 0, or < 0 on a verifier error. */
+#define FDGPU_REPLAY_PARSE_FAIL (1)
+int fdgpu_replay_verify( fdgpu_verifier_t v, uint8_t const * payloads, uint64_t const * off, uint32_t const * sz,
+                         uint64_t n, uint64_t batch_txn_max, uint64_t batch_bytes_max, int8_t * codes );
+
+/* Shred FEC-set roots: fd_ed25519_verify( roots+32i, 32, sigs+64i, pub )
+   (src/disco/shred/fd_fec_resolver.c:438) for n sets in batches of
+   <= batch_max; pub = pubkeys (shared_pubkey: one leader key) or
+   pubkeys+32i.  codes[i] = the fd_ed25519 code.  Returns 0 or < 0. */
+int fdgpu_fec_roots_verify( fdgpu_verifier_t v, uint8_t const * roots, uint8_t const * sigs,
+                            uint8_t const * pubkeys, int shared_pubkey, uint64_t n, uint64_t batch_max,
+                            int8_t * codes );
+
 /* --------------------------------------- process separation (§8(f) row 1) */
 
 /* A link (mcache + compact dcache + consumer fseq) formatted inside one
