@@ -176,6 +176,16 @@ def lib():
         "fdgpu_producer_start": (vp, [vp, u64, u64, vp, u64, u64, vp, vp, vp, u64, c.c_double]),
         "fdgpu_replay_verify": (c.c_int, [Verifier, vp, vp, vp, u64, u64, u64, vp]),
         "fdgpu_fec_roots_verify": (c.c_int, [Verifier, vp, vp, vp, c.c_int, u64, u64, vp]),
+        "fdt_tpu_reasm_footprint": (u64, [u64, u64]),
+        "fdt_tpu_reasm_new": (vp, [vp, u64, u64, u64]),
+        "fdt_tpu_reasm_reset": (None, [vp]),
+        "fdt_tpu_reasm_chunk0": (u64, [vp, vp]),
+        "fdt_tpu_reasm_wmark": (u64, [vp, vp]),
+        "fdt_tpu_reasm_prepare": (c.c_uint32, [vp, u64]),
+        "fdt_tpu_reasm_append": (c.c_int, [vp, c.c_uint32, vp, u64, u64]),
+        "fdt_tpu_reasm_publish": (c.c_int, [vp, c.c_uint32, vp, vp, u64, u64]),
+        "fdt_tpu_reasm_cancel": (None, [vp, c.c_uint32]),
+        "fdt_tpu_reasm_slot_state": (c.c_int, [vp, c.c_uint32]),
         "fdt_link_footprint": (u64, [u64, u64]),
         "fdt_link_new": (c.c_int, [vp, u64, u64, u64]),
         "fdt_link_join": (c.c_int, [vp, c.POINTER(LinkT)]),
@@ -400,6 +410,74 @@ class Link:
             out.append((meta, self.payload(meta)))
             seq += 1
         return out
+
+
+REASM_SUCCESS, REASM_ERR_SZ, REASM_ERR_SKIP, REASM_ERR_STATE = 0, 1, 2, 3
+REASM_FREE, REASM_BUSY, REASM_PUB = 0, 1, 2
+TPU_REASM_MTU = 1280
+
+
+class TpuReasm:
+    """The quic -> verify link as the reference builds it: TPU stream
+    reassembly slots (fdt_tpu_reasm_*, fd_tpu.h:20-246) publishing into an
+    mcache.  Has the attributes VerifyTile reads from a link (mcache_ptr,
+    depth, seq0, base_ptr, chunk0, wmark): base is the region start, chunk0
+    the first slot's chunk, wmark per fd_verify.c:186-191."""
+
+    def __init__(self, depth, burst, orig=0, seq0=0):
+        L = lib()
+        fp = L.fdt_tpu_reasm_footprint(depth, burst)
+        if not fp:
+            raise ValueError("bad reasm parameters")
+        self.depth, self.burst, self.seq0, self.mtu = depth, burst, seq0, TPU_REASM_MTU
+        self.region = _aligned(fp, 4096)
+        self._r = L.fdt_tpu_reasm_new(self.region.ctypes.data, depth, burst, orig)
+        if not self._r:
+            raise RuntimeError("fdt_tpu_reasm_new failed")
+        self.mcache = _aligned(depth * 32, 128).view(FRAG_META_DTYPE)
+        L.fdt_mcache_init(self.mcache.ctypes.data, depth, seq0)
+        self.chunk0 = L.fdt_tpu_reasm_chunk0(self._r, self.base_ptr)
+        self.wmark = L.fdt_tpu_reasm_wmark(self._r, self.base_ptr)
+        self.fseq = np.zeros(1, dtype=np.uint64)
+        self.next_seq = seq0
+
+    @property
+    def mcache_ptr(self):
+        return self.mcache.ctypes.data
+
+    @property
+    def base_ptr(self):
+        return self.region.ctypes.data
+
+    def prepare(self, tsorig=0):
+        return lib().fdt_tpu_reasm_prepare(self._r, tsorig)
+
+    def append(self, slot, data, off):
+        data = bytes(data)
+        return lib().fdt_tpu_reasm_append(self._r, slot, data, len(data), off)
+
+    def publish(self, slot, tspub=0):
+        rc = lib().fdt_tpu_reasm_publish(self._r, slot, self.mcache_ptr, self.base_ptr, self.next_seq, tspub)
+        if rc == REASM_SUCCESS:
+            self.next_seq += 1
+        return rc
+
+    def cancel(self, slot):
+        lib().fdt_tpu_reasm_cancel(self._r, slot)
+
+    def state(self, slot):
+        return lib().fdt_tpu_reasm_slot_state(self._r, slot)
+
+    def poll(self, seq):
+        m = FragMeta()
+        found = c.c_uint64()
+        rc = lib().fdt_mcache_poll(self.mcache_ptr, self.depth, seq, c.byref(m), c.byref(found))
+        meta = {n: getattr(m, n) for n, _ in FragMeta._fields_} if rc == 1 else None
+        return rc, meta, found.value
+
+    def payload(self, meta):
+        o = meta["chunk"] * CHUNK_SZ
+        return bytes(self.region[o:o + meta["sz"]])
 
 
 def split_verify_output(frag_payload):

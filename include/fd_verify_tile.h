@@ -307,6 +307,39 @@ void            fdgpu_dtile_delete( fdgpu_dtile_t * t );
 int64_t         fdgpu_dtile_step  ( fdgpu_dtile_t * t );   /* frags consumed this step */
 void            fdgpu_dtile_stats ( fdgpu_dtile_t const * t, fdgpu_dtile_stats_t * out );
 
+/* ------------------------------------ TPU reassembly (§8(f) row 2) */
+
+/* The quic -> verify link's producer (src/disco/quic/fd_tpu.h:20-246):
+   QUIC stream data is reassembled into one of depth + burst slots of
+   FDT_TPU_REASM_MTU bytes and published to an mcache of `depth` lines,
+   the frag's chunk pointing into the slot.  Slots are identified by index
+   (the reference hands out slot pointers).  The verify tile's in-link chunk
+   range is [fdt_tpu_reasm_chunk0, fdt_tpu_reasm_wmark] (fd_verify.c:186-191). */
+#define FDT_TPU_REASM_CHUNK_MTU   ((FDT_TPU_MTU + FDT_CHUNK_SZ - 1) / FDT_CHUNK_SZ)   /* 20 */
+#define FDT_TPU_REASM_MTU         (FDT_TPU_REASM_CHUNK_MTU * FDT_CHUNK_SZ)             /* 1280 */
+#define FDT_TPU_REASM_SUCCESS     (0)
+#define FDT_TPU_REASM_ERR_SZ      (1)     /* message over FDT_TXN_MTU */
+#define FDT_TPU_REASM_ERR_SKIP    (2)     /* gap in the stream data */
+#define FDT_TPU_REASM_ERR_STATE   (3)     /* slot not being reassembled */
+#define FDT_TPU_REASM_STATE_FREE  (0)
+#define FDT_TPU_REASM_STATE_BUSY  (1)
+#define FDT_TPU_REASM_STATE_PUB   (2)
+
+uint64_t fdt_tpu_reasm_footprint( uint64_t depth, uint64_t burst );   /* 0 on bad parameters */
+void *   fdt_tpu_reasm_new      ( void * mem, uint64_t depth, uint64_t burst, uint64_t orig );  /* mem 64-aligned */
+void     fdt_tpu_reasm_reset    ( void * reasm );
+uint64_t fdt_tpu_reasm_chunk0   ( void * reasm, void const * base );
+uint64_t fdt_tpu_reasm_wmark    ( void * reasm, void const * base );
+/* new stream: a FREE slot, or the least recently prepared BUSY one (cancelled) */
+uint32_t fdt_tpu_reasm_prepare  ( void * reasm, uint64_t tsorig );
+int      fdt_tpu_reasm_append   ( void * reasm, uint32_t slot, uint8_t const * data, uint64_t data_sz,
+                                  uint64_t data_off );
+/* BUSY -> PUB as frag seq; the slot mcache line seq held goes back to FREE */
+int      fdt_tpu_reasm_publish  ( void * reasm, uint32_t slot, fdt_frag_meta_t * mcache, void const * base,
+                                  uint64_t seq, uint64_t tspub );
+void     fdt_tpu_reasm_cancel   ( void * reasm, uint32_t slot );
+int      fdt_tpu_reasm_slot_state( void * reasm, uint32_t slot );     /* FDT_TPU_REASM_STATE_*, -1 */
+
 /* ------------------------------------- other callers (§8(f) row 4) */
 
 /* Replay: fd_executor_txn_verify (src/flamenco/runtime/fd_executor.c:
