@@ -94,7 +94,7 @@ def _reasm_tile_run(oracle, depth, burst, batch, verifier, n=600):
     ps = [p for p in _mixed_stream(n, seed=depth + burst) if len(p) <= 1232]
     rnd = random.Random(depth)
     r = tile.TpuReasm(depth, burst)
-    outl = tile.Link(1 << 11, tile.TPU_DCACHE_MTU)
+    outl = tile.Link(1 << 13, tile.TPU_DCACHE_MTU)          # holds every output (drained at the end)
     vt = tile.VerifyTile(r, outl, verifier, batch_txn_max=batch, log_max=1 << 14)
     i, open_, pub_order = 0, [], []                  # open_: streams in progress [slot, payload, sent]
     while i < len(ps) or open_:
