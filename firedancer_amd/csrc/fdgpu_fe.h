@@ -214,14 +214,19 @@ FDG_DEV void fe_mul(fe &h, const fe &f, const fe &g) {
   FDG_SCHED_FENCE();
 }
 
-/* h = f^2 using the symmetric terms once (55 products).  Coefficient of
-   f_i f_j (i <= j) in column (i+j) mod 10: (i!=j ? 2 : 1) * (i,j odd ? 2 : 1)
-   * (i+j >= 10 ? 19 : 1), applied as (a f_i)(b f_j) with a in {1,2,4} and
-   b in {1,19} so both factors stay below 2^32 for inputs up to A/S. */
-FDG_DEV void fe_sq(fe &h, const fe &f) {
-  uint32_t f2[10], f4[10], f19[10];
+/* h = 2^SH * f^2 using the symmetric terms once (55 products).  Coefficient
+   of f_i f_j (i <= j) in column (i+j) mod 10: (i!=j ? 2 : 1) * (i,j odd ? 2
+   : 1) * (i+j >= 10 ? 19 : 1) * 2^SH, applied as (a f_i)(b f_j) with a in
+   {1,2,4,8} and b in {1,19} so both factors stay below 2^32 for inputs up to
+   A/S (SH = 1 only for R inputs: 8 f_i < 2^30, column sums < 2^62). */
+template <int SH>
+FDG_DEV void fe_sq_sh(fe &h, const fe &f) {
+  uint32_t f2[10], f4[10], f8[10], f19[10];
 #pragma unroll
-  for (int i = 0; i < 10; i++) { f2[i] = f.v[i] << 1; f4[i] = f.v[i] << 2; f19[i] = 19u * f.v[i]; }
+  for (int i = 0; i < 10; i++) {
+    f2[i] = f.v[i] << 1; f4[i] = f.v[i] << 2; f8[i] = f.v[i] << 3; f19[i] = 19u * f.v[i];
+  }
+  auto pick = [&](int m, int i) { return m == 0 ? f.v[i] : m == 1 ? f2[i] : m == 2 ? f4[i] : f8[i]; };
 #if FDGPU_FE_FF
   uint32_t r[10];
   uint64_t carry = 0;
@@ -233,9 +238,8 @@ FDG_DEV void fe_sq(fe &h, const fe &f) {
 #pragma unroll
       for (int j = i; j < 10; j++) {
         if ((i + j) % 10 != k) continue;
-        const int mul2 = (i != j ? 1 : 0) + (((i & 1) && (j & 1)) ? 1 : 0);
-        const uint32_t a = mul2 == 0 ? f.v[i] : (mul2 == 1 ? f2[i] : f4[i]);
-        mad_acc(s, a, (i + j) >= 10 ? f19[j] : f.v[j]);
+        const int mul2 = (i != j ? 1 : 0) + (((i & 1) && (j & 1)) ? 1 : 0) + SH;
+        mad_acc(s, pick(mul2, i), (i + j) >= 10 ? f19[j] : f.v[j]);
       }
     }
     const int bits = (k & 1) ? 25 : 26;
@@ -253,16 +257,18 @@ FDG_DEV void fe_sq(fe &h, const fe &f) {
     for (int j = i; j < 10; j++) {
       const int k = (i + j) % 10;
       const bool wrap = (i + j) >= 10;
-      int mul2 = (i != j ? 1 : 0) + (((i & 1) && (j & 1)) ? 1 : 0);  /* power of two: 0,1,2 */
-      const uint32_t a = mul2 == 0 ? f.v[i] : (mul2 == 1 ? f2[i] : f4[i]);
-      const uint32_t b = wrap ? f19[j] : f.v[j];
-      c[k] += (uint64_t)a * b;
+      const int mul2 = (i != j ? 1 : 0) + (((i & 1) && (j & 1)) ? 1 : 0) + SH;
+      c[k] += (uint64_t)pick(mul2, i) * (wrap ? f19[j] : f.v[j]);
     }
   }
   fe_carry64(h, c);
 #endif
   FDG_SCHED_FENCE();
 }
+
+FDG_DEV void fe_sq(fe &h, const fe &f) { fe_sq_sh<0>(h, f); }
+/* h = 2 f^2 (f <= R) */
+FDG_DEV void fe_sq2(fe &h, const fe &f) { fe_sq_sh<1>(h, f); }
 
 FDG_DEV void fe_sqn(fe &h, const fe &f, int n) {
   fe_sq(h, f);
