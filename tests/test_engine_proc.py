@@ -136,3 +136,32 @@ def test_engine_process_pipeline_gpu(oracle):
     ps = _mixed_stream(3000, seed=72)
     exp_out = _pipeline(ps, True, oracle, batch=512)
     assert exp_out.count(0) > 1000
+
+
+@pytest.mark.gpu
+def test_engine_process_cli_gpu(oracle):
+    """`python -m firedancer_amd.engine_proc` as an operator starts it: joins
+    the links by path, verifies on the GPU, prints the tile's stats."""
+    import json
+    import subprocess
+    import sys
+    ps = _mixed_stream(1500, seed=73)
+    paths = [_shm_path(n) for n in ("qv", "vd")]
+    try:
+        inl = tile.Link.shm_create(paths[0], 1 << 12, 1232)
+        vd = tile.Link.shm_create(paths[1], 1 << 12, tile.TPU_DCACHE_MTU)
+        for p in ps:
+            inl.publish(p)
+        r = subprocess.run([sys.executable, "-m", "firedancer_amd.engine_proc", "--in", paths[0], "--out", paths[1],
+                            "--frags", str(len(ps)), "--batch", "512", "--timeout", "60"],
+                           capture_output=True, text=True, timeout=120,
+                           cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+        assert r.returncode == 0, r.stderr[-2000:]
+        st = json.loads(r.stdout.strip().splitlines()[-1])
+        exp_out, exp_pub = tile_model.verify_tile_model(ps, 0x5EEDF00D, lambda a, t: oracle.verify_txns(a, t))
+        assert st["published"] == exp_out.count(0) and st["verify_failed"] == exp_out.count(-1)
+        assert [m["sig"] for m, _ in vd.drain()] == [t for _, _, t in exp_pub]
+    finally:
+        for p in paths:
+            if os.path.exists(p):
+                os.unlink(p)
