@@ -31,9 +31,15 @@ sys.path.insert(0, REPO)
 # Algorithmic INT32 multiply-accumulates per signature:
 # 3,300 field multiplications x 64 u32*u32 products (radix-2^32 schoolbook).
 MADS_PER_SIG = 211_200
-# v_mad_u64_u32 issue peak of one MI355X: 256 CU x 4 SIMD x 16 lanes/clk (half
-# rate, measured in tools/ubench_int.hip: profiles/r01_ubench.md) x 2.4 GHz.
+# v_mad_u64_u32 issue peak of one MI355X (the headline `peak`): 256 CU x 4
+# SIMD x 16 lanes/clk (the instruction issues at half the 32-lane rate) x
+# 2.4 GHz = 39.32 T/s.
 VALU_MAD_PEAK_TOPS = 256 * 64 * 2.4e9 / 1e12
+# The same instruction's measured throughput on MI355X (tools/ubench_int.hip,
+# profiles/r01_ubench_int.jsonl: 55.15 lane-ops/CU/clk at 2.4 GHz, 8 waves
+# per SIMD of independent chains) -- BASELINE.md's r_mad; `frac_measured`
+# prices against it.
+VALU_MAD_MEASURED_TOPS = 33.881
 
 
 def parse():
@@ -50,6 +56,8 @@ def parse():
                     help="device batches verified round-robin, each on its own HIP stream (1: one stream)")
     ap.add_argument("--cfg3-txns", type=int, default=150_000,
                     help="multi-signature (cfg3) txns for the secondary device-resident line (0: skip)")
+    ap.add_argument("--adv-txns", type=int, default=1_000_000,
+                    help="txns of each adversarial batch (all equation failures / all corrupted R; 0: skip)")
     return ap.parse_args()
 
 
@@ -160,20 +168,50 @@ def cpu_model():
 
 
 def cpu_baseline(arena, txns, sample):
+    """The oracle (C restatement) on one pinned thread per physical core of
+    this host (at most the GPU box's 16-CPU share), inputs statically
+    partitioned.  Returns (baseline record, the CPU codes of the sample)."""
     from oracle import oracle as orc
-    from firedancer_amd.workload import default_threads
-    cores = default_threads()
+    from firedancer_amd.workload import physical_cpus
+    cpus = physical_cpus()
     sub = txns[:sample]
     t0 = time.perf_counter()
-    codes = orc.verify_txns(arena, sub, nthreads=cores)
+    codes = orc.verify_txns(arena, sub, cpus=cpus)
     dt = time.perf_counter() - t0
     rate = int(sub["sig_cnt"].sum()) / dt
-    return {"value": round(rate, 1), "unit": "sigs/s", "cores": cores, "kind": "port",
-            "per_core": round(rate / cores, 1), "cpu_model": cpu_model(),
-            "sample": f"first {len(sub)} txns of the rank-0 cfg1 batch, oracle/fd_ed25519_oracle.c "
-                      f"(C restatement, radix-2^51, wNAF) with {cores} threads, {dt:.2f} s wall",
-            "published_ref_per_core": "20-40K sigs/s/core (Icelake, book/guide/tuning.md:75) -- published, not measured",
-            "cpu_codes_nonzero": int((codes != 0).sum())}
+    rec = {"value": round(rate, 1), "unit": "sigs/s", "cores": len(cpus), "kind": "port",
+           "per_core": round(rate / len(cpus), 1), "cpu_model": cpu_model(), "cpus_pinned": cpus,
+           "sample": f"first {len(sub)} txns of the rank-0 cfg1 batch, oracle/fd_ed25519_oracle.c "
+                     f"(C restatement, radix-2^51, wNAF), one pinned thread per physical core on "
+                     f"{len(cpus)} cores (the box's CPU share), {dt:.2f} s wall",
+           "published_ref_per_core": "20-40K sigs/s/core (Icelake, book/guide/tuning.md:75) -- published, not measured"}
+    return rec, codes
+
+
+def adversarial(eng, n_txn, seed, ref_ms_per_sig):
+    """SURVEY §8(d) / test_ed25519.c:920-951 bad-sig/msg modes at batch
+    scale: 1M single-signature txns where EVERY signature fails the
+    equation (one message bit flipped -> ERR_MSG), and where every R is
+    corrupted (one bit of R -> decode failure or a wrong point).  Timed with
+    HIP events like the headline's isolated launch; codes checked against
+    the oracle on all txns."""
+    from firedancer_amd import workload
+    from oracle import oracle as orc
+    out = {}
+    for name, mode in (("eq_fail", workload.MODE_MSG), ("bad_r", workload.MODE_R)):
+        arena, txns, _ = workload.make_txns(n_txn, seed, corrupt=1.0, corrupt_mode=mode)
+        b = eng.upload(arena, txns)
+        b.verify()
+        got = b.codes()
+        _, kv, kc = b.time(5)
+        exp = orc.verify_txns(arena, txns, cpus=workload.physical_cpus())
+        sigs_per_s = b.n_sig / ((kv + kc) * 1e-3)
+        out[f"adv_{name}_sigs_per_s"] = round(sigs_per_s, 1)
+        out[f"adv_{name}_vs_cfg2_isolated"] = round(ref_ms_per_sig / ((kv + kc) / b.n_sig), 4)   # throughput ratio
+        out[f"adv_{name}_parity_mismatches"] = int((got != exp).sum())
+        out[f"adv_{name}_codes"] = {int(c): int(k) for c, k in zip(*np.unique(exp, return_counts=True))}
+        b.free()
+    return out
 
 
 # one verify = fdgpu_verify_ra_kernel (everything but the last inversion) +
@@ -193,20 +231,30 @@ def pmc_traffic():
     return None, None
 
 
-def cfg3_rate(eng, n_txn, seed):
+def cfg3_rate(eng, eng_nobucket, n_txn, seed):
     """BASELINE configs[2] (cfg3): 1-12 signatures sharing one message, msg up
     to the 1232-B MTU, 10% with one corrupted signature or message bit;
     device-resident, mean of HIP-event-timed verifies (secondary line, not
-    `value`)."""
+    `value`).  Timed with the signatures grouped by SHA-512 block count (the
+    engine default) and in transaction order (FDGPU_FLAG_NO_BUCKET)."""
     from firedancer_amd import workload
     arena, txns, modes = workload.cfg3(n_txn, seed=seed)
-    b = eng.upload(arena, txns)
-    b.verify()
-    wall, kv, kc = b.time(5)
-    n_sig = b.n_sig
-    b.free()
-    return {"cfg3_txns": n_txn, "cfg3_sigs": n_sig, "cfg3_sigs_per_s": round(n_sig / ((kv + kc) * 1e-3), 1),
-            "cfg3_txns_per_s": round(n_txn / ((kv + kc) * 1e-3), 1), "cfg3_ms_per_batch": round(kv + kc, 3)}
+    out = {}
+    for tag, e in (("", eng), ("_unbucketed", eng_nobucket)):
+        b = e.upload(arena, txns)
+        b.verify()
+        wall, kv, kc = b.time(5)
+        n_sig = b.n_sig
+        if not tag:
+            codes = b.codes()
+        else:
+            out["cfg3_bucketing_codes_equal"] = bool((b.codes() == codes).all())
+        b.free()
+        out[f"cfg3{tag}_sigs_per_s"] = round(n_sig / ((kv + kc) * 1e-3), 1)
+        out[f"cfg3{tag}_ms_per_batch"] = round(kv + kc, 3)
+    out.update({"cfg3_txns": n_txn, "cfg3_sigs": n_sig,
+                "cfg3_txns_per_s": round(n_txn / (out["cfg3_ms_per_batch"] * 1e-3), 1)})
+    return out
 
 
 def main():
@@ -257,10 +305,27 @@ def main():
                   "latency_batch_txns": args.latency_batch,
                   "pcie_inclusive_sigs_per_s_per_gpu": round(pcie, 1)}
         if args.cfg3_txns:
-            extras.update(cfg3_rate(eng, args.cfg3_txns, workload.CFG3_SEED + dist.rank))
+            eng_nb = VerifyEngine(dist.local_rank, max_txn=1024, ring_depth=1, bucket=False)
+            extras.update(cfg3_rate(eng, eng_nb, args.cfg3_txns, workload.CFG3_SEED + dist.rank))
+            eng_nb.close()
+        if args.adv_txns:
+            extras.update(adversarial(eng, args.adv_txns, workload.CFG1_SEED + 0x400 + dist.rank,
+                                      (kv_ms + kc_ms) / n_sig))
     cpu = None
-    if dist.rank == 0 and dist.world == 1 and not args.no_extras:
-        cpu = cpu_baseline(arena, txns, min(args.cpu_sample, len(txns)))
+    parity = {}
+    if not args.no_extras:
+        # full-size cfg2 parity: every GPU code of this rank's batch against the
+        # oracle (rank 0 also times that oracle run as the CPU baseline)
+        gpu_codes = batch.codes()
+        n_chk = min(args.cpu_sample, len(txns))
+        if dist.rank == 0 and dist.world == 1:
+            cpu, cpu_codes = cpu_baseline(arena, txns, n_chk)
+        else:
+            from oracle import oracle as orc
+            cpu_codes = orc.verify_txns(arena, txns[:n_chk], cpus=workload.physical_cpus())
+        mism = int((gpu_codes[:n_chk] != cpu_codes).sum())
+        parity = {"parity_checked_txns": int(dist.sum(n_chk)), "parity_mismatches": int(dist.sum(mism)),
+                  "parity_codes": {int(c): int(k) for c, k in zip(*np.unique(cpu_codes, return_counts=True))}}
     for b in batches:
         b.free()
     eng.close()
@@ -287,6 +352,10 @@ def main():
             "roofline": {"bound": "valu", "achieved": round(achieved, 3), "peak": round(VALU_MAD_PEAK_TOPS, 2),
                          "unit": "TOP/s", "frac": round(achieved / VALU_MAD_PEAK_TOPS, 4),
                          "traffic": traffic,
+                         "peak_measured": VALU_MAD_MEASURED_TOPS,
+                         "frac_measured": round(achieved / VALU_MAD_MEASURED_TOPS, 4),
+                         "peak_note": "frac uses the nominal v_mad_u64_u32 issue peak (39.32 T/s); frac_measured "
+                                      "the instruction's measured rate (33.88 T/s, profiles/r01_ubench_int.jsonl)",
                          "frac_overlapped": round(value / dist.world * MADS_PER_SIG / 1e12 / VALU_MAD_PEAK_TOPS, 4),
                          "note": f"INT32 v_mad_u64_u32 ops: {MADS_PER_SIG} algorithmic mads/sig x {n_sig} sigs / mean "
                                  f"{VERIFY_KERNEL} (fdgpu_verify_ra_kernel + fdgpu_tail_kernel + fdgpu_finish_kernel) time "
@@ -296,9 +365,13 @@ def main():
             "self_check_codes": self_ok,
             "gen_s": round(t_gen, 2),
         }
+        line.update(parity)
         line.update(extras)
         print(json.dumps(line), flush=True)
     dist.close()
+    # a parity failure fails the run (after the line is printed)
+    if parity.get("parity_mismatches") or any(v for k, v in extras.items() if k.endswith("parity_mismatches")):
+        sys.exit(3)
 
 
 if __name__ == "__main__":

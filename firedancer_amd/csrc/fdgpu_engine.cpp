@@ -45,6 +45,7 @@ struct Slot {
   hipEvent_t h2d_done = nullptr, comp_done = nullptr, done = nullptr;
   uint8_t *h_arena = nullptr, *d_arena = nullptr;
   fdgpu_sig_desc_t *h_sigs = nullptr, *d_sigs = nullptr;
+  uint32_t *h_perm = nullptr, *d_perm = nullptr;   /* block-count grouping: descriptor i -> signature perm[i] */
   fdgpu_txn_desc_t *h_txns = nullptr, *d_txns = nullptr;
   int8_t *h_codes = nullptr, *d_txn_codes = nullptr, *d_sig_codes = nullptr;
   uint32_t *d_ws = nullptr;   /* this slot's workspace: slots run concurrently on their own streams */
@@ -81,6 +82,8 @@ void slot_free(Slot &s) {
   if (s.done) (void)hipEventDestroy(s.done);
   if (s.h_arena) (void)hipHostFree(s.h_arena);
   if (s.h_sigs) (void)hipHostFree(s.h_sigs);
+  if (s.h_perm) (void)hipHostFree(s.h_perm);
+  if (s.d_perm) (void)hipFree(s.d_perm);
   if (s.h_txns) (void)hipHostFree(s.h_txns);
   if (s.h_codes) (void)hipHostFree(s.h_codes);
   if (s.d_arena) (void)hipFree(s.d_arena);
@@ -100,10 +103,12 @@ bool slot_alloc(Slot &s, const fdgpu_cfg_t &c) {
   HIPCHK(hipEventCreateWithFlags(&s.done, hipEventDisableTiming), false);
   HIPCHK(hipHostMalloc((void **)&s.h_arena, arena, hipHostMallocDefault), false);
   HIPCHK(hipHostMalloc((void **)&s.h_sigs, c.max_sig * sizeof(fdgpu_sig_desc_t) + 16, hipHostMallocDefault), false);
+  HIPCHK(hipHostMalloc((void **)&s.h_perm, c.max_sig * sizeof(uint32_t) + 16, hipHostMallocDefault), false);
   HIPCHK(hipHostMalloc((void **)&s.h_txns, c.max_txn * sizeof(fdgpu_txn_desc_t) + 16, hipHostMallocDefault), false);
   HIPCHK(hipHostMalloc((void **)&s.h_codes, c.max_txn + 16, hipHostMallocDefault), false);
   HIPCHK(hipMalloc((void **)&s.d_arena, arena), false);
   HIPCHK(hipMalloc((void **)&s.d_sigs, c.max_sig * sizeof(fdgpu_sig_desc_t) + 16), false);
+  HIPCHK(hipMalloc((void **)&s.d_perm, c.max_sig * sizeof(uint32_t) + 16), false);
   HIPCHK(hipMalloc((void **)&s.d_txns, c.max_txn * sizeof(fdgpu_txn_desc_t) + 16), false);
   HIPCHK(hipMalloc((void **)&s.d_txn_codes, c.max_txn + 16), false);
   HIPCHK(hipMalloc((void **)&s.d_sig_codes, c.max_sig + 16), false);
@@ -111,12 +116,22 @@ bool slot_alloc(Slot &s, const fdgpu_cfg_t &c) {
   return true;
 }
 
+/* SHA-512 blocks of R || A || M (fdgpu_sha512.h sha512_hram_blocks) */
+inline uint32_t hram_blocks(uint32_t msg_sz) { return (64u + msg_sz + 16u) / 128u + 1u; }
+
 /* Validate and expand transactions into per-signature work items.
-   Returns the number of signatures or -1 on invalid input. */
-int64_t expand(const uint8_t *arena_unused, uint64_t arena_sz, const fdgpu_txn_t *txns, uint64_t txn_cnt,
-               uint64_t max_sig, fdgpu_sig_desc_t *sigs, fdgpu_txn_desc_t *tds) {
-  (void)arena_unused;
+   Returns the number of signatures or -1 on invalid input.
+
+   perm != NULL: the descriptors are grouped by SHA-512 block count (a
+   stable counting sort; the SHA loop of a wave runs to its longest
+   message, so mixed message sizes in one wave cost the longest one's
+   blocks) and perm[i] is the signature index (in transaction order, the
+   combine kernel's sig0 + j) of descriptor i.  perm == NULL: transaction
+   order, no permutation. */
+int64_t expand(uint64_t arena_sz, const fdgpu_txn_t *txns, uint64_t txn_cnt, uint64_t max_sig,
+               fdgpu_sig_desc_t *sigs, fdgpu_txn_desc_t *tds, uint32_t *perm) {
   uint64_t ns = 0;
+  uint64_t cnt_by_grp[FDGPU_NBLK_GROUPS] = {};
   for (uint64_t t = 0; t < txn_cnt; t++) {
     const fdgpu_txn_t &x = txns[t];
     const uint32_t cnt = x.sig_cnt;
@@ -128,20 +143,38 @@ int64_t expand(const uint8_t *arena_unused, uint64_t arena_sz, const fdgpu_txn_t
       set_err("txn %llu: descriptor out of arena bounds", (unsigned long long)t);
       return -1;
     }
-    if (ns + cnt > max_sig) { set_err("batch exceeds max_sig"); return -1; }
-    for (uint32_t j = 0; j < cnt; j++) {
-      sigs[ns + j].msg_off = x.msg_off;
-      sigs[ns + j].msg_sz = x.msg_sz;
-      sigs[ns + j].sig_off = x.sig_off + 64u * j;
-      sigs[ns + j].pub_off = x.pub_off + 32u * j;
-    }
+    if (ns + cnt > max_sig) { set_err("batch exceeds max_sig (%llu)", (unsigned long long)max_sig); return -1; }
+    if (perm) cnt_by_grp[std::min(hram_blocks(x.msg_sz), FDGPU_NBLK_GROUPS) - 1] += cnt;
     ns += cnt;
+  }
+  uint64_t next[FDGPU_NBLK_GROUPS];
+  if (perm) {
+    uint64_t o = 0;
+    for (uint32_t g = 0; g < FDGPU_NBLK_GROUPS; g++) { next[g] = o; o += cnt_by_grp[g]; }
+  }
+  for (uint64_t t = 0; t < txn_cnt; t++) {
+    const fdgpu_txn_t &x = txns[t];
+    const uint32_t cnt = tds[t].sig_cnt;
+    if (!cnt) continue;
+    const uint32_t s0 = tds[t].sig0;
+    uint64_t *slot = perm ? &next[std::min(hram_blocks(x.msg_sz), FDGPU_NBLK_GROUPS) - 1] : nullptr;
+    for (uint32_t j = 0; j < cnt; j++) {
+      const uint64_t i = slot ? (*slot)++ : (uint64_t)s0 + j;
+      sigs[i].msg_off = x.msg_off;
+      sigs[i].msg_sz = x.msg_sz;
+      sigs[i].sig_off = x.sig_off + 64u * j;
+      sigs[i].pub_off = x.pub_off + 32u * j;
+      if (perm) perm[i] = s0 + j;
+    }
   }
   return (int64_t)ns;
 }
 
-template <typename T>
-T *dalloc(size_t n) { T *p = nullptr; if (hipMalloc((void **)&p, n * sizeof(T) + 64) != hipSuccess) return nullptr; return p; }
+/* RAII device buffer (diagnostics) */
+struct DevBuf {
+  void *p = nullptr;
+  ~DevBuf() { if (p) (void)hipFree(p); }
+};
 
 /* (Re)size the per-lane workspace to cover n_sig signatures. */
 int ensure_ws(fdgpu_engine *e, uint64_t n_sig) {
@@ -157,6 +190,8 @@ int ensure_ws(fdgpu_engine *e, uint64_t n_sig) {
 
 }  // namespace
 
+static bool bucket(const fdgpu_engine_t *e) { return !(e->cfg.flags & FDGPU_FLAG_NO_BUCKET); }
+
 extern "C" {
 
 char const *fdgpu_last_error(void) { return g_err.c_str(); }
@@ -165,7 +200,9 @@ fdgpu_engine_t *fdgpu_engine_open(int device, fdgpu_cfg_t const *cfg_in) {
   fdgpu_cfg_t cfg{};
   if (cfg_in) cfg = *cfg_in;
   if (!cfg.max_txn) cfg.max_txn = 1u << 16;
-  if (!cfg.max_sig) cfg.max_sig = cfg.max_txn * 2;
+  /* a parsed transaction carries at most 12 signatures (FD_TXN_ACTUAL_SIG_MAX,
+     fd_txn.h:68); batches whose signatures exceed max_sig are rejected */
+  if (!cfg.max_sig) cfg.max_sig = cfg.max_txn * 12;
   if (!cfg.max_arena) cfg.max_arena = cfg.max_txn * 1232ull;
   if (!cfg.ring_depth) cfg.ring_depth = 2;
   if (cfg.max_arena > 0xFFFFFFF0ull || cfg.max_sig > 0xFFFFFFF0ull || cfg.max_txn > 0xFFFFFFF0ull) {
@@ -218,9 +255,9 @@ int fdgpu_engine_info(fdgpu_engine_t *e, uint32_t *grid_blocks, uint32_t *block_
 
 /* ws: a workspace for n_sig signatures, or NULL for the engine's compute
    workspace (grown on demand; callers on other streams synchronise first). */
-static int enqueue_verify(fdgpu_engine_t *e, const uint8_t *d_arena, const fdgpu_sig_desc_t *d_sigs, uint64_t n_sig,
-                          const fdgpu_txn_desc_t *d_txns, uint64_t n_txn, int8_t *d_sig_codes, int8_t *d_txn_codes,
-                          hipStream_t st, uint32_t *ws = nullptr) {
+static int enqueue_verify(fdgpu_engine_t *e, const uint8_t *d_arena, const fdgpu_sig_desc_t *d_sigs,
+                          const uint32_t *d_perm, uint64_t n_sig, const fdgpu_txn_desc_t *d_txns, uint64_t n_txn,
+                          int8_t *d_sig_codes, int8_t *d_txn_codes, hipStream_t st, uint32_t *ws = nullptr) {
   const uint32_t flags = (e->cfg.flags & FDGPU_FLAG_REF_MAPPING) ? FDGPU_FLAG_REF_MAP : 0u;
   if (!ws && n_sig > e->ws_sig) {
     HIPCHK(hipStreamSynchronize(st), FDGPU_ERR_DEVICE);
@@ -228,10 +265,10 @@ static int enqueue_verify(fdgpu_engine_t *e, const uint8_t *d_arena, const fdgpu
     int rc = ensure_ws(e, n_sig);
     if (rc) return rc;
   }
-  HIPCHK(fdgpu_launch_verify_sigs(d_arena, d_sigs, (uint32_t)n_sig, e->d_btab, ws ? ws : e->d_ws, d_sig_codes, flags,
-                                  st),
+  HIPCHK(fdgpu_launch_verify_sigs(d_arena, d_sigs, (uint32_t)n_sig, d_perm, e->d_btab, ws ? ws : e->d_ws, d_sig_codes,
+                                  flags, st),
          FDGPU_ERR_DEVICE);
-  HIPCHK(fdgpu_launch_combine(d_txns, (uint32_t)n_txn, d_sig_codes, d_txn_codes, st), FDGPU_ERR_DEVICE);
+  HIPCHK(fdgpu_launch_combine(d_txns, (uint32_t)n_txn, d_sig_codes, d_txn_codes, nullptr, st), FDGPU_ERR_DEVICE);
   return FDGPU_OK;
 }
 
@@ -240,20 +277,22 @@ static int enqueue_verify(fdgpu_engine_t *e, const uint8_t *d_arena, const fdgpu
    the slot's stream (fdgpu_submit overlaps its staging memcpy with the copy) */
 static int64_t submit_slot(fdgpu_engine_t *e, Slot *s, uint64_t arena_sz, fdgpu_txn_t const *txns, uint64_t txn_cnt,
                            uint64_t uploaded = 0) {
-  const int64_t ns = expand(s->h_arena, arena_sz, txns, txn_cnt, e->cfg.max_sig, s->h_sigs, s->h_txns);
+  uint32_t *perm = bucket(e) ? s->h_perm : nullptr;
+  const int64_t ns = expand(arena_sz, txns, txn_cnt, e->cfg.max_sig, s->h_sigs, s->h_txns, perm);
   if (ns < 0) return FDGPU_ERR_INVAL;
   memset(s->h_arena + arena_sz, 0, FDGPU_ARENA_SLACK);
   const size_t asz = arena_sz + FDGPU_ARENA_SLACK - uploaded;
   HIPCHK(hipMemcpyAsync(s->d_arena + uploaded, s->h_arena + uploaded, asz, hipMemcpyHostToDevice, s->stream),
          FDGPU_ERR_DEVICE);
   if (ns) HIPCHK(hipMemcpyAsync(s->d_sigs, s->h_sigs, (size_t)ns * sizeof(fdgpu_sig_desc_t), hipMemcpyHostToDevice, s->stream), FDGPU_ERR_DEVICE);
+  if (ns && perm) HIPCHK(hipMemcpyAsync(s->d_perm, perm, (size_t)ns * sizeof(uint32_t), hipMemcpyHostToDevice, s->stream), FDGPU_ERR_DEVICE);
   if (txn_cnt) HIPCHK(hipMemcpyAsync(s->d_txns, s->h_txns, txn_cnt * sizeof(fdgpu_txn_desc_t), hipMemcpyHostToDevice, s->stream), FDGPU_ERR_DEVICE);
   /* copies, kernels and the code read-back of a slot run in order on the
      slot's own stream with the slot's own workspace, so the ring's batches
      overlap each other on the GPU (a 64K-signature batch fills only half of
      the resident wave slots) */
-  int rc = enqueue_verify(e, s->d_arena, s->d_sigs, (uint64_t)ns, s->d_txns, txn_cnt, s->d_sig_codes, s->d_txn_codes,
-                          s->stream, s->d_ws);
+  int rc = enqueue_verify(e, s->d_arena, s->d_sigs, perm ? s->d_perm : nullptr, (uint64_t)ns, s->d_txns, txn_cnt,
+                          s->d_sig_codes, s->d_txn_codes, s->stream, s->d_ws);
   if (rc) return rc;
   if (txn_cnt) HIPCHK(hipMemcpyAsync(s->h_codes, s->d_txn_codes, txn_cnt, hipMemcpyDeviceToHost, s->stream), FDGPU_ERR_DEVICE);
   HIPCHK(hipEventRecord(s->done, s->stream), FDGPU_ERR_DEVICE);
@@ -394,7 +433,7 @@ int fdgpu_verify_device(fdgpu_engine_t *e, void const *d_arena, void const *d_si
     }
     d_sig_codes = e->d_scratch_codes;
   }
-  return enqueue_verify(e, (const uint8_t *)d_arena, (const fdgpu_sig_desc_t *)d_sig_desc, sig_cnt,
+  return enqueue_verify(e, (const uint8_t *)d_arena, (const fdgpu_sig_desc_t *)d_sig_desc, nullptr, sig_cnt,
                         (const fdgpu_txn_desc_t *)d_txn_desc, txn_cnt, d_sig_codes, d_txn_codes, st);
 }
 
@@ -405,6 +444,7 @@ int fdgpu_verify_device(fdgpu_engine_t *e, void const *d_arena, void const *d_si
 struct fdgpu_dev_batch {
   uint8_t *d_arena = nullptr;
   fdgpu_sig_desc_t *d_sigs = nullptr;
+  uint32_t *d_perm = nullptr;               /* NULL: descriptors in transaction order */
   fdgpu_txn_desc_t *d_txns = nullptr;
   int8_t *d_sig_codes = nullptr, *d_txn_codes = nullptr;
   uint64_t n_sig = 0, n_txn = 0;
@@ -452,6 +492,7 @@ void fdgpu_dev_batch_free(fdgpu_engine_t *e, fdgpu_dev_batch_t *b) {
   if (b->d_ws) (void)hipFree(b->d_ws);
   if (b->d_arena) (void)hipFree(b->d_arena);
   if (b->d_sigs) (void)hipFree(b->d_sigs);
+  if (b->d_perm) (void)hipFree(b->d_perm);
   if (b->d_txns) (void)hipFree(b->d_txns);
   if (b->d_sig_codes) (void)hipFree(b->d_sig_codes);
   if (b->d_txn_codes) (void)hipFree(b->d_txn_codes);
@@ -467,7 +508,8 @@ fdgpu_dev_batch_t *fdgpu_dev_batch_upload(fdgpu_engine_t *e, uint8_t const *aren
   for (uint64_t t = 0; t < txn_cnt; t++) total += (txns[t].sig_cnt >= 1 && txns[t].sig_cnt <= 16) ? txns[t].sig_cnt : 0;
   std::vector<fdgpu_sig_desc_t> sd(total + 1);
   std::vector<fdgpu_txn_desc_t> td(txn_cnt + 1);
-  const int64_t ns = expand(arena, arena_sz, txns, txn_cnt, total, sd.data(), td.data());
+  std::vector<uint32_t> pm(bucket(e) ? total + 1 : 0);
+  const int64_t ns = expand(arena_sz, txns, txn_cnt, total, sd.data(), td.data(), bucket(e) ? pm.data() : nullptr);
   if (ns < 0) return nullptr;
   fdgpu_dev_batch *b = new fdgpu_dev_batch();
   b->n_sig = (uint64_t)ns; b->n_txn = txn_cnt;
@@ -480,6 +522,10 @@ fdgpu_dev_batch_t *fdgpu_dev_batch_upload(fdgpu_engine_t *e, uint8_t const *aren
   if (hipMemset(b->d_arena, 0, arena_sz + FDGPU_ARENA_SLACK) != hipSuccess) return fail("memset");
   if (arena_sz && hipMemcpy(b->d_arena, arena, arena_sz, hipMemcpyHostToDevice) != hipSuccess) return fail("h2d");
   if (ns && hipMemcpy(b->d_sigs, sd.data(), ns * sizeof(fdgpu_sig_desc_t), hipMemcpyHostToDevice) != hipSuccess) return fail("h2d");
+  if (ns && !pm.empty()) {
+    if (hipMalloc((void **)&b->d_perm, ns * sizeof(uint32_t)) != hipSuccess) return fail("perm alloc");
+    if (hipMemcpy(b->d_perm, pm.data(), ns * sizeof(uint32_t), hipMemcpyHostToDevice) != hipSuccess) return fail("h2d");
+  }
   if (txn_cnt && hipMemcpy(b->d_txns, td.data(), txn_cnt * sizeof(fdgpu_txn_desc_t), hipMemcpyHostToDevice) != hipSuccess) return fail("h2d");
   if ((uint64_t)ns > e->ws_sig) {
     if (hipStreamSynchronize(e->compute) != hipSuccess) return fail("sync");
@@ -491,8 +537,8 @@ fdgpu_dev_batch_t *fdgpu_dev_batch_upload(fdgpu_engine_t *e, uint8_t const *aren
 int fdgpu_dev_batch_verify(fdgpu_engine_t *e, fdgpu_dev_batch_t *b) {
   if (!e || !b) return FDGPU_ERR_INVAL;
   HIPCHK(hipSetDevice(e->device), FDGPU_ERR_DEVICE);
-  return enqueue_verify(e, b->d_arena, b->d_sigs, b->n_sig, b->d_txns, b->n_txn, b->d_sig_codes, b->d_txn_codes,
-                        batch_stream(e, b), b->d_ws);
+  return enqueue_verify(e, b->d_arena, b->d_sigs, b->d_perm, b->n_sig, b->d_txns, b->n_txn, b->d_sig_codes,
+                        b->d_txn_codes, batch_stream(e, b), b->d_ws);
 }
 
 int fdgpu_dev_batch_codes(fdgpu_engine_t *e, fdgpu_dev_batch_t *b, int8_t *txn_codes, int8_t *sig_codes) {
@@ -520,10 +566,10 @@ int fdgpu_dev_batch_time(fdgpu_engine_t *e, fdgpu_dev_batch_t *b, int iters, dou
   int rc = FDGPU_OK;
   for (int i = 0; i < iters && rc == FDGPU_OK; i++) {
     if (hipEventRecord(ev[3 * i], st) != hipSuccess) rc = FDGPU_ERR_DEVICE;
-    if (fdgpu_launch_verify_sigs(b->d_arena, b->d_sigs, (uint32_t)b->n_sig, e->d_btab, batch_ws(e, b), b->d_sig_codes,
-                                 flags, st) != hipSuccess) rc = FDGPU_ERR_DEVICE;
+    if (fdgpu_launch_verify_sigs(b->d_arena, b->d_sigs, (uint32_t)b->n_sig, b->d_perm, e->d_btab, batch_ws(e, b),
+                                 b->d_sig_codes, flags, st) != hipSuccess) rc = FDGPU_ERR_DEVICE;
     if (hipEventRecord(ev[3 * i + 1], st) != hipSuccess) rc = FDGPU_ERR_DEVICE;
-    if (fdgpu_launch_combine(b->d_txns, (uint32_t)b->n_txn, b->d_sig_codes, b->d_txn_codes, st) != hipSuccess)
+    if (fdgpu_launch_combine(b->d_txns, (uint32_t)b->n_txn, b->d_sig_codes, b->d_txn_codes, nullptr, st) != hipSuccess)
       rc = FDGPU_ERR_DEVICE;
     if (hipEventRecord(ev[3 * i + 2], st) != hipSuccess) rc = FDGPU_ERR_DEVICE;
   }
@@ -557,44 +603,52 @@ int fdgpu_sync(fdgpu_engine_t *e) {
 
 /* ------------------------------------------------------------ sync API */
 
+/* Compatibility shim for the reference's synchronous per-call API: one
+   process-wide engine on device 0, one GPU round trip per call, serialised
+   on a lock.  The batch API is the throughput path; hot callers (the verify
+   tile, replay, FEC roots) use it.  The caller's current HIP device is saved
+   and restored.  The reference API has no error channel besides the verify
+   codes, so an engine failure (no device, a HIP error) aborts the process
+   (documented in fd_ed25519_gpu.h): answering ERR_SIG for a signature that
+   was never checked would silently drop valid traffic. */
 static std::mutex g_sync_mu;
 static fdgpu_engine_t *g_sync_engine = nullptr;
 
-static fdgpu_engine_t *sync_engine() {
-  if (!g_sync_engine) {
-    fdgpu_cfg_t cfg{};
-    cfg.max_txn = 1; cfg.max_sig = 16; cfg.max_arena = 64 * 16 + 32 * 16 + 65536; cfg.ring_depth = 1;
-    g_sync_engine = fdgpu_engine_open(0, &cfg);
-    if (!g_sync_engine) {
-      fprintf(stderr, "fd_ed25519_gpu: cannot open the GPU engine: %s\n", fdgpu_last_error());
-      abort();   /* no silent CPU fallback */
-    }
-  }
+[[noreturn]] static void sync_fatal(const char *what) {
+  fprintf(stderr, "fd_ed25519_gpu: %s: %s\n", what, fdgpu_last_error());
+  abort();   /* no silent CPU fallback, no unchecked verdict */
+}
+
+static fdgpu_engine_t *sync_engine(uint64_t need) {
+  if (g_sync_engine && need <= g_sync_engine->cfg.max_arena) return g_sync_engine;
+  /* first use, or a message longer than the engine's arena: (re)open */
+  if (g_sync_engine) fdgpu_engine_close(g_sync_engine);
+  fdgpu_cfg_t cfg{};
+  cfg.max_txn = 1; cfg.max_sig = 16; cfg.ring_depth = 1;
+  cfg.max_arena = std::max<uint64_t>(64 * 16 + 32 * 16 + 65536, need * 2);
+  g_sync_engine = fdgpu_engine_open(0, &cfg);
+  if (!g_sync_engine) sync_fatal("cannot open the GPU engine");
   return g_sync_engine;
 }
 
 static int sync_verify(const uint8_t *msg, uint64_t msg_sz, const uint8_t *sigs, const uint8_t *pubs, uint32_t n) {
   if (n == 0 || n > 16) return FD_ED25519_ERR_SIG;
   std::lock_guard<std::mutex> lk(g_sync_mu);
-  fdgpu_engine_t *e = sync_engine();
+  int prev_dev = -1;
+  if (hipGetDevice(&prev_dev) != hipSuccess) prev_dev = -1;
   const uint64_t need = 64ull * n + 32ull * n + msg_sz;
+  fdgpu_engine_t *e = sync_engine(need);
   std::vector<uint8_t> arena(need);
   memcpy(arena.data(), sigs, 64ull * n);
   memcpy(arena.data() + 64ull * n, pubs, 32ull * n);
   if (msg_sz) memcpy(arena.data() + 96ull * n, msg, msg_sz);
-  if (need > e->cfg.max_arena) {
-    /* grow the sync engine for long messages */
-    fdgpu_engine_close(e);
-    fdgpu_cfg_t cfg{}; cfg.max_txn = 1; cfg.max_sig = 16; cfg.max_arena = need * 2; cfg.ring_depth = 1;
-    g_sync_engine = e = fdgpu_engine_open(0, &cfg);
-    if (!e) { fprintf(stderr, "fd_ed25519_gpu: %s\n", fdgpu_last_error()); abort(); }
-  }
   fdgpu_txn_t t;
   t.sig_off = 0; t.pub_off = 64u * n; t.msg_off = 96u * n; t.msg_sz = (uint32_t)msg_sz; t.sig_cnt = n;
   const int64_t tk = fdgpu_submit(e, arena.data(), need, &t, 1);
-  if (tk < 0) { fprintf(stderr, "fd_ed25519_gpu: submit failed: %s\n", fdgpu_last_error()); abort(); }
+  if (tk < 0) sync_fatal("submit failed");
   int8_t code = 0;
-  if (fdgpu_poll(e, tk, &code, 1) != FDGPU_OK) { fprintf(stderr, "fd_ed25519_gpu: %s\n", fdgpu_last_error()); abort(); }
+  if (fdgpu_poll(e, tk, &code, 1) != FDGPU_OK) sync_fatal("poll failed");
+  if (prev_dev >= 0) (void)hipSetDevice(prev_dev);
   return code;
 }
 
@@ -623,29 +677,34 @@ char const *fd_ed25519_strerror(int err) {
 
 /* --------------------------------------------------------- diagnostics */
 
+#define DALLOC(buf, T, n) do { if (hipMalloc(&(buf).p, (size_t)(n) * sizeof(T) + 64) != hipSuccess) { \
+  (buf).p = nullptr; set_err("alloc"); return FDGPU_ERR_DEVICE; } } while (0)
+
 int fdgpu_debug_fe_ops(fdgpu_engine_t *e, uint8_t const *ab, uint64_t n, uint8_t *out) {
   if (!e || !n) return FDGPU_ERR_INVAL;
   HIPCHK(hipSetDevice(e->device), FDGPU_ERR_DEVICE);
-  uint32_t *din = dalloc<uint32_t>(n * 16), *dout = dalloc<uint32_t>(n * 64);
-  if (!din || !dout) { set_err("alloc"); return FDGPU_ERR_DEVICE; }
-  HIPCHK(hipMemcpy(din, ab, n * 64, hipMemcpyHostToDevice), FDGPU_ERR_DEVICE);
-  HIPCHK(fdgpu_launch_test_fe(din, dout, (uint32_t)n, e->compute), FDGPU_ERR_DEVICE);
+  DevBuf din, dout;
+  DALLOC(din, uint32_t, n * 16);
+  DALLOC(dout, uint32_t, n * 64);
+  HIPCHK(hipMemcpy(din.p, ab, n * 64, hipMemcpyHostToDevice), FDGPU_ERR_DEVICE);
+  HIPCHK(fdgpu_launch_test_fe((uint32_t *)din.p, (uint32_t *)dout.p, (uint32_t)n, e->compute), FDGPU_ERR_DEVICE);
   HIPCHK(hipStreamSynchronize(e->compute), FDGPU_ERR_DEVICE);
-  HIPCHK(hipMemcpy(out, dout, n * 256, hipMemcpyDeviceToHost), FDGPU_ERR_DEVICE);
-  (void)hipFree(din); (void)hipFree(dout);
+  HIPCHK(hipMemcpy(out, dout.p, n * 256, hipMemcpyDeviceToHost), FDGPU_ERR_DEVICE);
   return FDGPU_OK;
 }
 
 int fdgpu_debug_decode(fdgpu_engine_t *e, uint8_t const *enc, uint64_t n, int ref_mapping, uint8_t *out) {
   if (!e || !n) return FDGPU_ERR_INVAL;
   HIPCHK(hipSetDevice(e->device), FDGPU_ERR_DEVICE);
-  uint32_t *din = dalloc<uint32_t>(n * 8), *dout = dalloc<uint32_t>(n * 18);
-  if (!din || !dout) { set_err("alloc"); return FDGPU_ERR_DEVICE; }
-  HIPCHK(hipMemcpy(din, enc, n * 32, hipMemcpyHostToDevice), FDGPU_ERR_DEVICE);
-  HIPCHK(fdgpu_launch_test_decode(din, dout, (uint32_t)n, ref_mapping ? FDGPU_FLAG_REF_MAP : 0u, e->compute), FDGPU_ERR_DEVICE);
+  DevBuf din, dout;
+  DALLOC(din, uint32_t, n * 8);
+  DALLOC(dout, uint32_t, n * 18);
+  HIPCHK(hipMemcpy(din.p, enc, n * 32, hipMemcpyHostToDevice), FDGPU_ERR_DEVICE);
+  HIPCHK(fdgpu_launch_test_decode((uint32_t *)din.p, (uint32_t *)dout.p, (uint32_t)n,
+                                  ref_mapping ? FDGPU_FLAG_REF_MAP : 0u, e->compute),
+         FDGPU_ERR_DEVICE);
   HIPCHK(hipStreamSynchronize(e->compute), FDGPU_ERR_DEVICE);
-  HIPCHK(hipMemcpy(out, dout, n * 72, hipMemcpyDeviceToHost), FDGPU_ERR_DEVICE);
-  (void)hipFree(din); (void)hipFree(dout);
+  HIPCHK(hipMemcpy(out, dout.p, n * 72, hipMemcpyDeviceToHost), FDGPU_ERR_DEVICE);
   return FDGPU_OK;
 }
 
@@ -662,18 +721,23 @@ static int debug_msgs(fdgpu_engine_t *e, uint8_t const *arena, uint64_t arena_sz
     d[i].msg_off = txns[i].msg_off; d[i].msg_sz = txns[i].msg_sz;
     d[i].sig_off = txns[i].sig_off; d[i].pub_off = txns[i].pub_off;
   }
-  uint8_t *da = dalloc<uint8_t>(arena_sz + FDGPU_ARENA_SLACK);
-  fdgpu_sig_desc_t *dd = dalloc<fdgpu_sig_desc_t>(n);
-  uint32_t *dout = dalloc<uint32_t>(n * 16);
-  if (!da || !dd || !dout) { set_err("alloc"); return FDGPU_ERR_DEVICE; }
-  HIPCHK(hipMemset(da, 0, arena_sz + FDGPU_ARENA_SLACK), FDGPU_ERR_DEVICE);
-  if (arena_sz) HIPCHK(hipMemcpy(da, arena, arena_sz, hipMemcpyHostToDevice), FDGPU_ERR_DEVICE);
-  HIPCHK(hipMemcpy(dd, d.data(), n * sizeof(fdgpu_sig_desc_t), hipMemcpyHostToDevice), FDGPU_ERR_DEVICE);
-  if (hram) HIPCHK(fdgpu_launch_test_hram(da, dd, (uint32_t)n, dout, e->compute), FDGPU_ERR_DEVICE);
-  else HIPCHK(fdgpu_launch_test_sha512(da, dd, (uint32_t)n, dout, e->compute), FDGPU_ERR_DEVICE);
+  DevBuf da, dd, dout;
+  DALLOC(da, uint8_t, arena_sz + FDGPU_ARENA_SLACK);
+  DALLOC(dd, fdgpu_sig_desc_t, n);
+  DALLOC(dout, uint32_t, n * 16);
+  HIPCHK(hipMemset(da.p, 0, arena_sz + FDGPU_ARENA_SLACK), FDGPU_ERR_DEVICE);
+  if (arena_sz) HIPCHK(hipMemcpy(da.p, arena, arena_sz, hipMemcpyHostToDevice), FDGPU_ERR_DEVICE);
+  HIPCHK(hipMemcpy(dd.p, d.data(), n * sizeof(fdgpu_sig_desc_t), hipMemcpyHostToDevice), FDGPU_ERR_DEVICE);
+  if (hram)
+    HIPCHK(fdgpu_launch_test_hram((uint8_t *)da.p, (fdgpu_sig_desc_t *)dd.p, (uint32_t)n, (uint32_t *)dout.p,
+                                  e->compute),
+           FDGPU_ERR_DEVICE);
+  else
+    HIPCHK(fdgpu_launch_test_sha512((uint8_t *)da.p, (fdgpu_sig_desc_t *)dd.p, (uint32_t)n, (uint32_t *)dout.p,
+                                    e->compute),
+           FDGPU_ERR_DEVICE);
   HIPCHK(hipStreamSynchronize(e->compute), FDGPU_ERR_DEVICE);
-  HIPCHK(hipMemcpy(out, dout, n * (hram ? 32 : 64), hipMemcpyDeviceToHost), FDGPU_ERR_DEVICE);
-  (void)hipFree(da); (void)hipFree(dd); (void)hipFree(dout);
+  HIPCHK(hipMemcpy(out, dout.p, n * (hram ? 32 : 64), hipMemcpyDeviceToHost), FDGPU_ERR_DEVICE);
   return FDGPU_OK;
 }
 
@@ -690,13 +754,14 @@ int fdgpu_debug_hram(fdgpu_engine_t *e, uint8_t const *arena, uint64_t arena_sz,
 int fdgpu_debug_sc_reduce(fdgpu_engine_t *e, uint8_t const *in, uint64_t n, uint8_t *out) {
   if (!e || !n) return FDGPU_ERR_INVAL;
   HIPCHK(hipSetDevice(e->device), FDGPU_ERR_DEVICE);
-  uint32_t *din = dalloc<uint32_t>(n * 16), *dout = dalloc<uint32_t>(n * 8);
-  if (!din || !dout) { set_err("alloc"); return FDGPU_ERR_DEVICE; }
-  HIPCHK(hipMemcpy(din, in, n * 64, hipMemcpyHostToDevice), FDGPU_ERR_DEVICE);
-  HIPCHK(fdgpu_launch_test_sc_reduce(din, dout, (uint32_t)n, e->compute), FDGPU_ERR_DEVICE);
+  DevBuf din, dout;
+  DALLOC(din, uint32_t, n * 16);
+  DALLOC(dout, uint32_t, n * 8);
+  HIPCHK(hipMemcpy(din.p, in, n * 64, hipMemcpyHostToDevice), FDGPU_ERR_DEVICE);
+  HIPCHK(fdgpu_launch_test_sc_reduce((uint32_t *)din.p, (uint32_t *)dout.p, (uint32_t)n, e->compute),
+         FDGPU_ERR_DEVICE);
   HIPCHK(hipStreamSynchronize(e->compute), FDGPU_ERR_DEVICE);
-  HIPCHK(hipMemcpy(out, dout, n * 32, hipMemcpyDeviceToHost), FDGPU_ERR_DEVICE);
-  (void)hipFree(din); (void)hipFree(dout);
+  HIPCHK(hipMemcpy(out, dout.p, n * 32, hipMemcpyDeviceToHost), FDGPU_ERR_DEVICE);
   return FDGPU_OK;
 }
 
@@ -704,27 +769,32 @@ int fdgpu_debug_sig_codes(fdgpu_engine_t *e, uint8_t const *arena, uint64_t aren
                           uint64_t txn_cnt, int8_t *sig_codes) {
   if (!e) return FDGPU_ERR_INVAL;
   HIPCHK(hipSetDevice(e->device), FDGPU_ERR_DEVICE);
-  std::vector<fdgpu_sig_desc_t> sd;
-  std::vector<fdgpu_txn_desc_t> td(txn_cnt);
   uint64_t total = 0;
   for (uint64_t t = 0; t < txn_cnt; t++) total += (txns[t].sig_cnt >= 1 && txns[t].sig_cnt <= 16) ? txns[t].sig_cnt : 0;
-  sd.resize(total + 1);
-  const int64_t ns = expand(arena, arena_sz, txns, txn_cnt, total, sd.data(), td.data());
+  std::vector<fdgpu_sig_desc_t> sd(total + 1);
+  std::vector<fdgpu_txn_desc_t> td(txn_cnt + 1);
+  std::vector<uint32_t> pm(total + 1);
+  uint32_t *perm = bucket(e) ? pm.data() : nullptr;
+  const int64_t ns = expand(arena_sz, txns, txn_cnt, total, sd.data(), td.data(), perm);
   if (ns < 0) return FDGPU_ERR_INVAL;
   if (!ns) return FDGPU_OK;
-  uint8_t *da = dalloc<uint8_t>(arena_sz + FDGPU_ARENA_SLACK);
-  fdgpu_sig_desc_t *dd = dalloc<fdgpu_sig_desc_t>(ns);
-  int8_t *dc = dalloc<int8_t>(ns);
-  if (!da || !dd || !dc) { set_err("alloc"); return FDGPU_ERR_DEVICE; }
-  HIPCHK(hipMemset(da, 0, arena_sz + FDGPU_ARENA_SLACK), FDGPU_ERR_DEVICE);
-  HIPCHK(hipMemcpy(da, arena, arena_sz, hipMemcpyHostToDevice), FDGPU_ERR_DEVICE);
-  HIPCHK(hipMemcpy(dd, sd.data(), ns * sizeof(fdgpu_sig_desc_t), hipMemcpyHostToDevice), FDGPU_ERR_DEVICE);
+  DevBuf da, dd, dp, dc;
+  DALLOC(da, uint8_t, arena_sz + FDGPU_ARENA_SLACK);
+  DALLOC(dd, fdgpu_sig_desc_t, ns);
+  DALLOC(dp, uint32_t, ns);
+  DALLOC(dc, int8_t, ns);
+  HIPCHK(hipMemset(da.p, 0, arena_sz + FDGPU_ARENA_SLACK), FDGPU_ERR_DEVICE);
+  HIPCHK(hipMemcpy(da.p, arena, arena_sz, hipMemcpyHostToDevice), FDGPU_ERR_DEVICE);
+  HIPCHK(hipMemcpy(dd.p, sd.data(), ns * sizeof(fdgpu_sig_desc_t), hipMemcpyHostToDevice), FDGPU_ERR_DEVICE);
+  if (perm) HIPCHK(hipMemcpy(dp.p, perm, ns * sizeof(uint32_t), hipMemcpyHostToDevice), FDGPU_ERR_DEVICE);
   const uint32_t flags = (e->cfg.flags & FDGPU_FLAG_REF_MAPPING) ? FDGPU_FLAG_REF_MAP : 0u;
   if ((uint64_t)ns > e->ws_sig) { int rc = ensure_ws(e, (uint64_t)ns); if (rc) return rc; }
-  HIPCHK(fdgpu_launch_verify_sigs(da, dd, (uint32_t)ns, e->d_btab, e->d_ws, dc, flags, e->compute), FDGPU_ERR_DEVICE);
+  HIPCHK(fdgpu_launch_verify_sigs((uint8_t *)da.p, (fdgpu_sig_desc_t *)dd.p, (uint32_t)ns,
+                                  perm ? (uint32_t *)dp.p : nullptr, e->d_btab, e->d_ws, (int8_t *)dc.p, flags,
+                                  e->compute),
+         FDGPU_ERR_DEVICE);
   HIPCHK(hipStreamSynchronize(e->compute), FDGPU_ERR_DEVICE);
-  HIPCHK(hipMemcpy(sig_codes, dc, ns, hipMemcpyDeviceToHost), FDGPU_ERR_DEVICE);
-  (void)hipFree(da); (void)hipFree(dd); (void)hipFree(dc);
+  HIPCHK(hipMemcpy(sig_codes, dc.p, ns, hipMemcpyDeviceToHost), FDGPU_ERR_DEVICE);
   return FDGPU_OK;
 }
 

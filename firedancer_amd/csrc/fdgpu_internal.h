@@ -25,36 +25,28 @@ typedef struct {
 } fdgpu_txn_desc_t;
 
 #define FDGPU_ARENA_SLACK   160u          /* readable bytes past the arena (SHA block loads) */
-#define FDGPU_BTAB_ENTRIES  129u          /* 0 (identity), 1B .. 128B */
-#define FDGPU_BTAB_STRIDE   32u           /* u32 per niels entry (30 used) */
-/* k in signed radix 2^FDGPU_KWIN (4: 64 windows over {O,..,8A}; 5: 51 windows over {O,..,16A}) */
-#ifndef FDGPU_KWIN
-#define FDGPU_KWIN 4
-#endif
-#define FDGPU_ATAB_ENTRIES  ((1u << (FDGPU_KWIN - 1)) + 1u)   /* 0 (identity), 1A .. 2^(w-1) A (A negated) */
+/* k in signed radix 16: 64 windows over the per-lane table {O, -A, .., -8A} */
+#define FDGPU_ATAB_ENTRIES  9u            /* 0 (identity), 1A .. 8A (A negated) */
 #define FDGPU_ATAB_WORDS    40u           /* u32 per cached entry */
-/* Fixed-base comb for [S]B (FDGPU_BCOMB=1): S in signed radix 2^W, digit i
-   looked up in table i = {0, 1, .., 2^(W-1)} x 2^(W i) B (affine niels, one
-   128-B line per entry), so [S]B costs NDIG mixed additions and no
-   doublings.  Tables live in HBM (W=16: 16 x 32769 x 128 B = 67 MB, resident
-   in the 256 MB Infinity Cache). */
-#ifndef FDGPU_BCOMB
-#define FDGPU_BCOMB 1
-#endif
-#ifndef FDGPU_BCOMB_BITS
-#define FDGPU_BCOMB_BITS 16u
-#endif
+/* Fixed-base comb for [S]B: S in signed radix 2^W, digit i looked up in
+   table i = {0, 1, .., 2^(W-1)} x 2^(W i) B (affine niels, one 128-B line per
+   entry), so [S]B costs NDIG mixed additions and no doublings.  Tables live
+   in HBM (W=16: 16 x 32769 x 128 B = 67 MB, resident in the 256 MB Infinity
+   Cache). */
+#define FDGPU_BCOMB_BITS    16u
 #define FDGPU_BCOMB_NDIG    ((254u + FDGPU_BCOMB_BITS - 1u) / FDGPU_BCOMB_BITS)   /* covers S < 2^253 + carry */
 #define FDGPU_BCOMB_ENTRIES ((1u << (FDGPU_BCOMB_BITS - 1u)) + 1u)
 #define FDGPU_BCOMB_STRIDE  32u           /* u32 per entry (30 used): one 128-B line */
 #define FDGPU_BCOMB_CHUNK   64u           /* entries per lane in the table build (one batch inversion) */
-#define FDGPU_WS_PARK       FDGPU_ATAB_ENTRIES          /* entry: digits, codes, R', U */
-#define FDGPU_WS_SB         (FDGPU_ATAB_ENTRIES + 1u)   /* entry: [S]B in cached form */
+#define FDGPU_WS_PARK       FDGPU_ATAB_ENTRIES          /* entry: digits, code, R' (slow path) */
+#define FDGPU_WS_SB         (FDGPU_ATAB_ENTRIES + 1u)   /* entry: [S]B in cached form, then U + flags */
 #define FDGPU_WS_ENTRIES    (FDGPU_ATAB_ENTRIES + 2u)   /* per-lane workspace: A table, park, [S]B */
-#define FDGPU_WS_LANE_WORDS (FDGPU_WS_ENTRIES * FDGPU_ATAB_WORDS)   /* 1760 B per signature (w = 4) */
-#define FDGPU_BTAB_LDS_STRIDE 33u         /* B-table entry stride in LDS (odd: no bank conflicts) */
+#define FDGPU_WS_LANE_WORDS (FDGPU_WS_ENTRIES * FDGPU_ATAB_WORDS)   /* 1760 B per signature */
 #define FDGPU_BLOCK         256u
 #define FDGPU_FLAG_REF_MAP  1u            /* portable-backend error mapping */
+/* SHA-512 block-count groups of the host-side bucketing (expand): messages of
+   more blocks than this share the last group */
+#define FDGPU_NBLK_GROUPS   32u
 
 #ifdef __cplusplus
 extern "C" {
@@ -65,11 +57,15 @@ size_t     fdgpu_btab_bytes(void);                                   /* fixed-ba
 /* builds the fixed-base table into d_btab (fdgpu_btab_bytes()); synchronous */
 hipError_t fdgpu_btab_build(uint32_t *d_btab, hipStream_t stream);
 /* one signature per lane; d_ws must hold fdgpu_ws_bytes(n_sig) bytes */
+/* d_perm (NULL = identity): d_sig_codes[d_perm[i]] receives the code of
+   descriptor i (descriptors grouped by SHA-512 block count, codes in the
+   caller's order) */
 hipError_t fdgpu_launch_verify_sigs(const uint8_t *d_arena, const fdgpu_sig_desc_t *d_sigs, uint32_t n_sig,
-                                    const uint32_t *d_btab, uint32_t *d_ws, int8_t *d_sig_codes, uint32_t flags,
-                                    hipStream_t stream);
+                                    const uint32_t *d_perm, const uint32_t *d_btab, uint32_t *d_ws,
+                                    int8_t *d_sig_codes, uint32_t flags, hipStream_t stream);
+/* d_accept (NULL: not written): ceil(n_txn / 64) words, bit t = txn t verified */
 hipError_t fdgpu_launch_combine(const fdgpu_txn_desc_t *d_txns, uint32_t n_txn, const int8_t *d_sig_codes,
-                                int8_t *d_txn_codes, hipStream_t stream);
+                                int8_t *d_txn_codes, uint64_t *d_accept, hipStream_t stream);
 hipError_t fdgpu_verify_occupancy(int *blocks_per_cu);
 size_t     fdgpu_ws_bytes(uint64_t n_sig);
 

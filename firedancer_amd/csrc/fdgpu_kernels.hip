@@ -1,25 +1,23 @@
 /* fdgpu_kernels.hip -- MI355X (gfx950) kernels of the batched Ed25519
-   verify engine.
+   verify engine.  One signature per lane, 256-thread workgroups; integer /
+   bignum work only (no MFMA).  Per batch, on one stream:
 
-   fdgpu_fused_kernel (default): one signature per lane, whole verify in one
-     launch (fd_ed25519_user.c:135-230):
-       pass 1: S < L -> SHA-512(R||A||M) mod L -> decode A, R -> small-order
-               tests -> table {O, -A, .., -8A} into the lane's workspace;
-       pass 2: [S]B + [k](-A) == R -> per-signature code.
-     Every lane executes the same instruction stream (failures are masked,
-     not branched on; a wave whose lanes all failed pass 1 skips the scalar
-     multiplication).  The double-scalar multiplication uses fixed signed
-     windows: radix 16 for k over the per-lane A table (lane-contiguous
-     160-B entries in a global workspace, each window's entry prefetched
-     ahead of its doublings), and radix 256 for S over the fixed table
-     {O, B, ..., 128B} staged into LDS once per workgroup at an odd stride
-     (the reference's wNAF-4 / wNAF-8 split, fd_curve25519.c:109-153, made
-     divergence-free).  One thread per signature, grid = ceil(n / 256).
-   fdgpu_prep_kernel + fdgpu_dsm_kernel (FDGPU_FUSED=0): the same two passes
-     as separate launches (measured equal speed; kept for A/B).
-   fdgpu_combine: per transaction, batch_single_msg first-error semantics
-     (fd_ed25519_user.c:232-310).
-   fdgpu_btab_init: builds the B table on the device at engine open. */
+   fdgpu_verify_ra_kernel  everything but the last inversion: S < L,
+       k = SHA-512(R||A||M) mod L, [S]B by a fixed-base comb, decode A and its
+       small-order test, the per-lane table {O, -A, .., -8A}, [k](-A) + [S]B
+       by signed radix-16 windows (the reference's wNAF double-scalar
+       multiplication, fd_curve25519.c:109-153, made divergence-free), then
+       R' is compared with R's encoding (y, sign) without decompressing R,
+       using one batched inversion per workgroup.
+   fdgpu_tail_kernel       the workgroup inversions, and the signatures whose
+       y did not match (or whose A is small order) with the reference's
+       full R decode and projective compare.
+   fdgpu_finish_kernel     per signature: x = U / (Z product) -> code.
+   fdgpu_combine_kernel    per transaction, batch_single_msg first-error
+       semantics (fd_ed25519_user.c:232-310), plus a ballot-compacted
+       accept bitmap.
+   fdgpu_bcomb_*           build the comb tables at engine open.
+   fdgpu_test_*            per-stage diagnostics for the parity tests. */
 #include <hip/hip_runtime.h>
 
 #include "fdgpu_ge.h"
@@ -29,37 +27,8 @@
 
 using namespace fdgpu;
 
-#ifndef FDGPU_PREP_WAVES
-#define FDGPU_PREP_WAVES 2     /* decode/pow chains want ~200 VGPRs */
-#endif
-#ifndef FDGPU_FUSED
-#define FDGPU_FUSED 1         /* 1: one launch runs both passes; 0: prep + dsm kernels (same speed) */
-#endif
-/* Cost-breakdown experiments (timing only -- results are wrong when set):
-   FDGPU_EXP_NO_RDEC skip decompressing R, FDGPU_EXP_NO_BADD skip the B adds,
-   FDGPU_EXP_NO_AADD skip the A adds, FDGPU_EXP_NO_SHA skip SHA-512. */
-#ifndef FDGPU_EXP_NO_RDEC
-#define FDGPU_EXP_NO_RDEC 0
-#endif
-#ifndef FDGPU_EXP_NO_BADD
-#define FDGPU_EXP_NO_BADD 0
-#endif
-#ifndef FDGPU_EXP_NO_AADD
-#define FDGPU_EXP_NO_AADD 0
-#endif
-#ifndef FDGPU_EXP_NO_SHA
-#define FDGPU_EXP_NO_SHA 0
-#endif
-/* FDGPU_EXP_LDS_PAD: bytes of dummy LDS per workgroup of the main kernel, to
-   cap residency (occupancy experiments; 0 = off) */
-#ifndef FDGPU_EXP_LDS_PAD
-#define FDGPU_EXP_LDS_PAD 0
-#endif
-#ifndef FDGPU_RAVOID
-#define FDGPU_RAVOID 1        /* 1: compare R' with R's encoding (batched inversion), decode R only for failures */
-#endif
-#ifndef FDGPU_DSM_WAVES
-#define FDGPU_DSM_WAVES 3     /* ~130 VGPRs: 3 waves per SIMD, no spills */
+#ifndef FDGPU_VERIFY_WAVES
+#define FDGPU_VERIFY_WAVES 2  /* waves per SIMD of the verify kernel: decode/pow chains want ~190 VGPRs */
 #endif
 
 namespace {
@@ -76,40 +45,13 @@ FDG_DEV void load32(uint32_t (&w)[8], const uint8_t *p) {
   }
 }
 
-/* ---- B table: entry j = j*B in affine niels form, canonical limbs ---- */
-
 FDG_DEV void niels_store(uint32_t *dst, const fe &ypx, const fe &ymx, const fe &xy2d) {
 #pragma unroll
   for (int i = 0; i < 10; i++) { dst[i] = ypx.v[i]; dst[10 + i] = ymx.v[i]; dst[20 + i] = xy2d.v[i]; }
   dst[30] = 0; dst[31] = 0;
 }
 
-__global__ void fdgpu_btab_init_kernel(uint32_t *btab) {
-  const uint32_t j = threadIdx.x;                       /* 0 .. 128 */
-  if (j >= FDGPU_BTAB_ENTRIES) return;
-  fe one; fe_1(one);
-  if (j == 0) { fe z; fe_0(z); niels_store(btab, one, one, z); return; }
-  constexpr uint32_t BX[10] = FDGPU_FE_BX, BY[10] = FDGPU_FE_BY, BT[10] = FDGPU_FE_BT, D2[10] = FDGPU_FE_D2;
-  ge_p3 B; fe_set(B.X, BX); fe_set(B.Y, BY); fe_1(B.Z); fe_set(B.T, BT);
-  ge_cached Bc; ge_p3_to_cached(Bc, B);
-  ge_p3 acc; ge_p3_0(acc);
-  ge_p1p1 t;
-  for (int bit = 7; bit >= 0; bit--) {                  /* binary left-to-right: acc = j*B */
-    ge_p2 a2; ge_p3_to_p2(a2, acc);
-    ge_dbl(t, a2); ge_p1p1_to_p3(acc, t);
-    if ((j >> bit) & 1u) { ge_add_cached(t, acc, Bc, false); ge_p1p1_to_p3(acc, t); }
-  }
-  fe zi, x, y, xy, d2, ypx, ymx, xy2d;
-  fe_invert(zi, acc.Z);
-  fe_mul(x, acc.X, zi); fe_mul(y, acc.Y, zi);
-  fe_set(d2, D2);
-  fe_add(ypx, y, x); fe_canon(ypx);
-  fe_sub(ymx, y, x); fe_canon(ymx);
-  fe_mul(xy, x, y); fe_mul(xy2d, xy, d2); fe_canon(xy2d);
-  niels_store(btab + j * FDGPU_BTAB_STRIDE, ypx, ymx, xy2d);
-}
-
-/* ---- fixed-base comb tables (FDGPU_BCOMB) ----
+/* ---- fixed-base comb tables ----
    table i, entry j = j * 2^(W i) B as affine niels (y+x, y-x, 2dxy),
    canonical limbs, word offset ((i * ENTRIES) + j) * STRIDE. */
 
@@ -205,65 +147,8 @@ FDG_DEV void atab_store(uint32_t *wsl, uint32_t entry, const ge_cached &c) {
   for (int q = 0; q < 10; q++) p[q] = make_uint4(w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]);
 }
 FDG_DEV int sext4(uint32_t x) { return ((int)(x << 28)) >> 28; }
-FDG_DEV int sext8(uint32_t x) { return ((int)(x << 24)) >> 24; }
 
-#if FDGPU_KWIN == 5
-#define KD_WORDS 13       /* 51 signed radix-32 digits, one per byte (byte j+1) */
-#else
-#define KD_WORDS 8        /* 64 signed radix-16 digits, one per nibble */
-#endif
-
-/* shift a 256-bit little-endian word vector left by 8 bits */
-FDG_DEV void shl8(uint32_t (&w)[8]) {
-#pragma unroll
-  for (int i = 7; i > 0; i--) w[i] = (w[i] << 8) | (w[i - 1] >> 24);
-  w[0] <<= 8;
-}
-
-/* R' = [S]B + [k](-A) as projective (X:Y:Z).  kd: radix-16 digits of k,
-   sd: radix-256 digits of S; wsl: this lane's A table (entries 0..8).
-   The A entry of each window is loaded (10 x 16 B) before that window's
-   four doublings, so its latency hides behind ~30 field products. */
-FDG_DEV void dsm(ge_p2 &acc2, uint32_t (&kd)[8], uint32_t (&sd)[8], const uint32_t *wsl,
-                 const uint32_t *s_btab) {
-  ge_p2_0(acc2);
-  ge_p3 acc3;
-  ge_p1p1 t;
-#pragma unroll 1
-  for (int j = 31; j >= 0; j--) {
-    const uint32_t kb = kd[7] >> 24, sb = sd[7] >> 24;
-    shl8(kd); shl8(sd);
-#pragma unroll 1
-    for (int h = 0; h < 2; h++) {
-      const int e = sext4(h == 0 ? (kb >> 4) : (kb & 15u));
-      uint32_t q[40];
-      {
-        const uint4 *ent = (const uint4 *)(wsl + (uint32_t)(e < 0 ? -e : e) * FDGPU_ATAB_WORDS);
-#pragma unroll
-        for (int i = 0; i < 10; i++) {
-          const uint4 v = ent[i];
-          q[4 * i] = v.x; q[4 * i + 1] = v.y; q[4 * i + 2] = v.z; q[4 * i + 3] = v.w;
-        }
-      }
-#pragma unroll 1
-      for (int r = 0; r < 4; r++) {
-        ge_dbl(t, acc2);
-        ge_p1p1_to_p2(acc2, t);
-      }
-      /* T of the last doubling (p1p1 -> p3 needs X'Y') */
-      acc3.X = acc2.X; acc3.Y = acc2.Y; acc3.Z = acc2.Z; fe_mul(acc3.T, t.X, t.Y);
-      if (!FDGPU_EXP_NO_AADD) ge_add_cached_regs(t, acc3, q, e < 0);
-      if (h == 1 && !FDGPU_EXP_NO_BADD) {
-        const int d = sext8(sb);
-        ge_p1p1_to_p3(acc3, t);
-        const uint32_t *ent = s_btab + (uint32_t)(d < 0 ? -d : d) * FDGPU_BTAB_LDS_STRIDE;
-        auto ld = [ent](int c, int w) { return ent[10 * c + w]; };
-        ge_add_niels_ld(t, acc3, ld, d < 0);
-      }
-      ge_p1p1_to_p2(acc2, t);
-    }
-  }
-}
+#define KD_WORDS 8        /* 64 signed radix-16 digits of k, one per nibble */
 
 FDG_DEV void atab_load(uint32_t (&q)[40], const uint32_t *wsl, int e) {
   const uint4 *ent = (const uint4 *)(wsl + (uint32_t)(e < 0 ? -e : e) * FDGPU_ATAB_WORDS);
@@ -281,44 +166,10 @@ FDG_DEV void shl4(uint32_t (&w)[8]) {
   w[0] <<= 4;
 }
 
-/* FDGPU_BCOMB variant: R' = [k](-A) + [S]B with [S]B precomputed by the
+/* R' = [k](-A) + [S]B with [S]B precomputed by the
    comb in pass 1 and parked (cached form) in workspace entry 10.  The chain
    only serves k: 64 windows of 4 doublings + one A-table addition; the last
    window's sum is converted to p3 and the parked [S]B added. */
-#if FDGPU_KWIN == 5
-FDG_DEV void dsm_k(ge_p2 &acc2, uint32_t (&kd)[KD_WORDS], const uint32_t *wsl) {
-  ge_p3 acc3;
-  ge_p1p1 t;
-  uint32_t q[40];
-  /* digit j (0..50) sits in byte j + 1; the top byte of the top word is read
-     and the string shifted left by one byte per window */
-  auto next = [&kd]() {
-    const int e = ((int)kd[KD_WORDS - 1]) >> 24;
-#pragma unroll
-    for (int w = KD_WORDS - 1; w > 0; w--) kd[w] = (kd[w] << 8) | (kd[w - 1] >> 24);
-    kd[0] <<= 8;
-    return e;
-  };
-  {                                    /* top window: start from its entry */
-    const int e = next();
-    atab_load(q, wsl, e);
-    ge_cached_regs_to_p2(acc2, q, e < 0);
-  }
-#pragma unroll 1
-  for (int j = 49; j >= 0; j--) {
-    const int e = next();
-    atab_load(q, wsl, e);
-#pragma unroll 1
-    for (int r = 0; r < 5; r++) {
-      ge_dbl(t, acc2);
-      ge_p1p1_to_p2(acc2, t);
-    }
-    acc3.X = acc2.X; acc3.Y = acc2.Y; acc3.Z = acc2.Z; fe_mul(acc3.T, t.X, t.Y);
-    ge_add_cached_regs(t, acc3, q, e < 0);
-    if (j == 0) break;
-    ge_p1p1_to_p2(acc2, t);
-  }
-#else
 FDG_DEV void dsm_k(ge_p2 &acc2, uint32_t (&kd)[KD_WORDS], const uint32_t *wsl) {
   ge_p3 acc3;
   ge_p1p1 t;
@@ -346,7 +197,6 @@ FDG_DEV void dsm_k(ge_p2 &acc2, uint32_t (&kd)[KD_WORDS], const uint32_t *wsl) {
     if (j == 0) break;
     ge_p1p1_to_p2(acc2, t);
   }
-#endif
   /* + [S]B (parked cached form) */
   ge_p1p1_to_p3(acc3, t);
   uint32_t qs[40];
@@ -403,7 +253,10 @@ FDG_DEV void comb_sb(ge_p3 &acc, const uint32_t (&S)[8], const uint32_t *__restr
   }
 }
 
-/* Build this lane's table {O, -A, -2A, ..., -8A} (cached form) in the workspace. */
+/* Build this lane's table {O, -A, -2A, ..., -8A} (cached form) in the
+   workspace.  Even multiples by doubling the stored half (4S + 4M) instead
+   of adding -A (8M): 3 = 2 + 1, 4 = 2*2, 5 = 4 + 1, 6 = 2*3, 7 = 6 + 1,
+   8 = 2*4. */
 FDG_DEV void atab_build(uint32_t *wsl, const ge_p3 &An) {
   ge_cached c;
   ge_cached_0(c); atab_store(wsl, 0, c);
@@ -413,9 +266,6 @@ FDG_DEV void atab_build(uint32_t *wsl, const ge_p3 &An) {
   ge_p3_to_cached(c, P); atab_store(wsl, 2, c);
   const uint32_t *ent1 = wsl + 1u * FDGPU_ATAB_WORDS;
   auto ld1 = [ent1](int cc, int w) { return ent1[10 * cc + w]; };
-#if FDGPU_KWIN == 4
-  /* even multiples by doubling the stored half (4S + 4M) instead of adding
-     -A (8M): 3 = 2 + 1, 4 = 2*2, 5 = 4 + 1, 6 = 2*3, 7 = 6 + 1, 8 = 2*4 */
 #pragma unroll 1
   for (uint32_t e = 3; e < FDGPU_ATAB_ENTRIES; e++) {
     if (e & 1u) {
@@ -429,33 +279,37 @@ FDG_DEV void atab_build(uint32_t *wsl, const ge_p3 &An) {
     ge_p1p1_to_p3(P, t);
     ge_p3_to_cached(c, P); atab_store(wsl, e, c);
   }
-#else
-#pragma unroll 1
-  for (uint32_t e = 3; e < FDGPU_ATAB_ENTRIES; e++) {
-    ge_add_cached_ld(t, P, ld1, false); ge_p1p1_to_p3(P, t);
-    ge_p3_to_cached(c, P); atab_store(wsl, e, c);
-  }
-#endif
 }
 
-/* Workspace entry 9 ("park") words: 0-9 x_R, 10-19 y_R, 20-27 radix-16
-   digits of k, 28-35 radix-256 digits of S, 36 pass-1 code. */
-#define PARK_XR 0
-#define PARK_YR 10
-#define PARK_KD 20      /* radix-16: 8 words; radix-32: 13 words (20-32) */
-#define PARK_SD 28
+/* Per-lane workspace words beyond the A table (entries 0..8):
+   entry FDGPU_WS_PARK ("park"):
+     words 20-27  radix-16 digits of k (pass 1 -> dsm_k; dead once dsm_k
+                  has read them)
+     word  36     pass-1 code (low byte) | RA_ASMALL
+     words  0-29  X, Y, Z of R' (slow-path lanes only, after dsm_k)
+   entry FDGPU_WS_SB ("post" once dsm_k has consumed [S]B):
+     words  0-39  [S]B in cached form (pass 1 -> the last addition of dsm_k)
+     words  0-9   U = X * (product of the workgroup's other Z)  } written after
+     word  10     pass-1 code | RA_* flags                       } dsm_k */
+#define PARK_KD 20
 #define PARK_CODE 36
-/* R-avoiding path (FDGPU_RAVOID): flag bits above the int8 code in PARK_CODE */
+#define POST_U 0
+#define POST_FLAGS 10
+static_assert(PARK_KD + KD_WORDS <= PARK_CODE, "digit string overlaps the pass-1 code");
+static_assert(PARK_CODE < (int)FDGPU_ATAB_WORDS && POST_FLAGS + 2 <= (int)FDGPU_ATAB_WORDS, "park layout");
+static_assert(POST_U == 0 && POST_FLAGS == 10, "U and flags are written as three dwordx4 at the entry start");
+/* flag bits above the int8 pass-1 code */
 #define RA_ASMALL (1u << 8)
 #define RA_YMATCH (1u << 9)
 
 FDG_DEV uint32_t *park_ptr(uint32_t *wsl) { return wsl + FDGPU_WS_PARK * FDGPU_ATAB_WORDS; }
+FDG_DEV uint32_t *post_ptr(uint32_t *wsl) { return wsl + FDGPU_WS_SB * FDGPU_ATAB_WORDS; }
 
-/* Pass 1 of one signature (fd_ed25519_user.c:158-207; SURVEY Appendix A steps
-   1-5): S < L, k = SHA-512(R||A||M) mod L, decode A then R, small-order
-   tests.  Writes the table {O, -A, .., -8A}, the affine R, both digit
-   strings and the pass-1 code to this lane's workspace; returns the code. */
-template <bool DECODE_R = true>
+/* Pass 1 of one signature without R (fd_ed25519_user.c:158-207; SURVEY
+   Appendix A steps 1-5): S < L, k = SHA-512(R||A||M) mod L, [S]B by the
+   comb, decode A and its small-order test, the table {O, -A, .., -8A}.  R is
+   resolved after the scalar multiplication (fdgpu_finish_kernel / the slow
+   path).  Returns the S / A verdict; parks k's digits and the flags. */
 FDG_DEV int verify_pass1(const uint8_t *arena, const fdgpu_sig_desc_t &sd_in, uint32_t nblk_wave, uint32_t *wsl,
                          const uint32_t *__restrict__ btab, bool ref_map) {
   uint32_t R[8], A[8];
@@ -466,44 +320,28 @@ FDG_DEV int verify_pass1(const uint8_t *arena, const fdgpu_sig_desc_t &sd_in, ui
   /* k = SHA-512(R || A || M) mod L, recoded to signed radix 16 */
   {
     uint64_t h[8];
-    if (FDGPU_EXP_NO_SHA) {
-#pragma unroll
-      for (int i = 0; i < 8; i++) h[i] = ((uint64_t)R[i] << 32) | A[i];
-    } else {
-      sha512_hram(h, R, A, arena + sd_in.msg_off, sd_in.msg_sz, nblk_wave);
-    }
+    sha512_hram(h, R, A, arena + sd_in.msg_off, sd_in.msg_sz, nblk_wave);
     uint32_t kx[16], k[8], kd[KD_WORDS];
 #pragma unroll
     for (int i = 0; i < 8; i++) { kx[2 * i] = bswap32((uint32_t)(h[i] >> 32)); kx[2 * i + 1] = bswap32((uint32_t)h[i]); }
     sc_reduce512(k, kx);
-#if FDGPU_KWIN == 5
-    sc_recode32(kd, k);
-#else
     sc_recode16(kd, k);
-#endif
 #pragma unroll
     for (int i = 0; i < KD_WORDS; i++) park[PARK_KD + i] = kd[i];
   }
-  /* step 1: S < L (fd_ed25519_user.c:159-161); S recoded to signed radix 256 */
+  /* step 1: S < L (fd_ed25519_user.c:159-161); [S]B by the comb, parked in
+     cached form for dsm_k (rejected S -> 0) */
   int code;
   {
     uint32_t S[8];
     load32(S, arena + sd_in.sig_off + 32);
     code = sc_lt_L(S) ? 0 : -1;
-#if FDGPU_BCOMB
-    /* [S]B by the comb, parked in cached form for pass 2 (rejected S -> 0) */
 #pragma unroll
     for (int i = 0; i < 8; i++) S[i] = code ? 0u : S[i];
     ge_p3 SB;
     comb_sb(SB, S, btab);
     ge_cached c; ge_p3_to_cached(c, SB);
     atab_store(wsl, FDGPU_WS_SB, c);
-#else
-    uint32_t sd[8];
-    sc_recode256(sd, S);
-#pragma unroll
-    for (int i = 0; i < 8; i++) park[PARK_SD + i] = sd[i];
-#endif
   }
   /* step 2 (A): decode, small order, table of -A */
   bool a_ok, a_small;
@@ -514,126 +352,16 @@ FDG_DEV int verify_pass1(const uint8_t *arena, const fdgpu_sig_desc_t &sd_in, ui
     ge_p3 An; ge_p3_neg(An, Ap);
     atab_build(wsl, An);
   }
-  if (!DECODE_R) {
-    /* R is resolved after the scalar multiplication (fdgpu_finish_kernel):
-       park the S / A verdict and A's small-order bit only */
-    if (code == 0 && !a_ok) code = ref_map ? -2 : -1;
-    park[PARK_CODE] = ((uint32_t)code & 0xffu) | (a_small ? RA_ASMALL : 0u);
-    return code;
-  }
-  /* step 2 (R): decode, small order; park affine x_R, y_R */
-  bool r_ok, r_small;
-  {
-    ge_p3 Rp;
-    if (FDGPU_EXP_NO_RDEC) {
-      fe_frombytes(Rp.X, R); fe_frombytes(Rp.Y, A); r_ok = true;
-    } else {
-      r_ok = ge_decode(Rp, R, ref_map);
-    }
-    r_small = ge_is_small_order_affine(Rp);
-#pragma unroll
-    for (int i = 0; i < 10; i++) { park[PARK_XR + i] = Rp.X.v[i]; park[PARK_YR + i] = Rp.Y.v[i]; }
-  }
   if (code == 0 && !a_ok) code = ref_map ? -2 : -1;    /* decode2 reports A before R */
-  if (code == 0 && !r_ok) code = -1;
-  if (code == 0 && a_small) code = -2;                 /* fd_ed25519_user.c:194-199 */
-  if (code == 0 && r_small) code = -1;
-  park[PARK_CODE] = (uint32_t)code;
+  park[PARK_CODE] = ((uint32_t)code & 0xffu) | (a_small ? RA_ASMALL : 0u);
   return code;
-}
-
-/* Pass 2 of one signature (fd_ed25519_user.c:208-229): [S]B + [k](-A) == R,
-   cofactorless, projective compare against the parked affine R. */
-FDG_DEV int verify_pass2(uint32_t *wsl, const uint32_t *s_btab) {
-  uint32_t *park = park_ptr(wsl);
-  const int code = (int)park[PARK_CODE];
-  /* wave-uniform early out when every lane already failed pass 1 */
-  if (__all(code != 0)) return code;
-  ge_p2 Rc;
-#if FDGPU_BCOMB
-  uint32_t kd[KD_WORDS];
-#pragma unroll
-  for (int i = 0; i < KD_WORDS; i++) kd[i] = park[PARK_KD + i];
-  dsm_k(Rc, kd, wsl);
-#else
-  uint32_t kd[8], sd[8];
-#pragma unroll
-  for (int i = 0; i < 8; i++) { kd[i] = park[PARK_KD + i]; sd[i] = park[PARK_SD + i]; }
-  dsm(Rc, kd, sd, wsl, s_btab);
-#endif
-  fe l, xy;
-#pragma unroll
-  for (int i = 0; i < 10; i++) xy.v[i] = park[PARK_XR + i];
-  fe_mul(l, xy, Rc.Z);
-  bool eq = fe_eq(Rc.X, l);
-#pragma unroll
-  for (int i = 0; i < 10; i++) xy.v[i] = park[PARK_YR + i];
-  fe_mul(l, xy, Rc.Z);
-  eq = eq && fe_eq(Rc.Y, l);
-  return (code == 0 && !eq) ? -3 : code;
 }
 
 FDG_DEV uint32_t *lane_ws(uint32_t *ws, uint32_t i) {
   return ws + (size_t)i * FDGPU_WS_LANE_WORDS;
 }
 
-/* Kernel 1: pass 1 (hash, scalars, decompression, small order, table). */
-__global__ void __launch_bounds__(FDGPU_BLOCK, FDGPU_PREP_WAVES)
-fdgpu_prep_kernel(const uint8_t *__restrict__ arena, const fdgpu_sig_desc_t *__restrict__ sigs, uint32_t n_sig,
-                  const uint32_t *__restrict__ btab, uint32_t *__restrict__ ws, uint32_t flags) {
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  const bool active = i < n_sig;
-  const fdgpu_sig_desc_t d = sigs[active ? i : n_sig - 1];
-  uint32_t nb = sha512_hram_blocks(d.msg_sz);      /* wave-uniform SHA block bound */
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) nb = max(nb, (uint32_t)__shfl_xor((int)nb, off));
-  verify_pass1(arena, d, nb, lane_ws(ws, i), btab, (flags & FDGPU_FLAG_REF_MAP) != 0);
-}
-
-/* Kernel 2: pass 2 (double-scalar multiplication and compare). */
-__global__ void __launch_bounds__(FDGPU_BLOCK, FDGPU_DSM_WAVES)
-fdgpu_dsm_kernel(uint32_t n_sig, const uint32_t *__restrict__ btab, uint32_t *__restrict__ ws,
-                 int8_t *__restrict__ codes) {
-  /* odd LDS stride: lanes reading word w of different entries hit different banks */
-#if FDGPU_BCOMB
-  const uint32_t *s_btab = nullptr;                   /* [S]B comes from the comb (pass 1) */
-#else
-  __shared__ uint32_t s_btab[FDGPU_BTAB_ENTRIES * FDGPU_BTAB_LDS_STRIDE];
-  for (uint32_t i = threadIdx.x; i < FDGPU_BTAB_ENTRIES * FDGPU_BTAB_STRIDE; i += blockDim.x)
-    s_btab[(i / FDGPU_BTAB_STRIDE) * FDGPU_BTAB_LDS_STRIDE + i % FDGPU_BTAB_STRIDE] = btab[i];
-  __syncthreads();
-#endif
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  const int code = verify_pass2(lane_ws(ws, i), s_btab);
-  if (i < n_sig) codes[i] = (int8_t)code;
-}
-
-/* Fused variant (FDGPU_FUSED=1): both passes in one launch, B table in LDS. */
-__global__ void __launch_bounds__(FDGPU_BLOCK, FDGPU_PREP_WAVES)
-fdgpu_fused_kernel(const uint8_t *__restrict__ arena, const fdgpu_sig_desc_t *__restrict__ sigs, uint32_t n_sig,
-                   const uint32_t *__restrict__ btab, uint32_t *__restrict__ ws, int8_t *__restrict__ codes,
-                   uint32_t flags) {
-#if FDGPU_BCOMB
-  const uint32_t *s_btab = nullptr;                   /* [S]B comes from the comb (pass 1) */
-#else
-  __shared__ uint32_t s_btab[FDGPU_BTAB_ENTRIES * FDGPU_BTAB_LDS_STRIDE];
-  for (uint32_t i = threadIdx.x; i < FDGPU_BTAB_ENTRIES * FDGPU_BTAB_STRIDE; i += blockDim.x)
-    s_btab[(i / FDGPU_BTAB_STRIDE) * FDGPU_BTAB_LDS_STRIDE + i % FDGPU_BTAB_STRIDE] = btab[i];
-  __syncthreads();
-#endif
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  const bool active = i < n_sig;
-  const fdgpu_sig_desc_t d = sigs[active ? i : n_sig - 1];
-  uint32_t nb = sha512_hram_blocks(d.msg_sz);
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) nb = max(nb, (uint32_t)__shfl_xor((int)nb, off));
-  uint32_t *wsl = lane_ws(ws, i);
-  verify_pass1(arena, d, nb, wsl, btab, (flags & FDGPU_FLAG_REF_MAP) != 0);
-  const int code = verify_pass2(wsl, s_btab);
-  if (active) codes[i] = (int8_t)code;
-}
-
-/* ---------------- R-avoiding verify (FDGPU_RAVOID) ----------------
+/* ---------------- R-avoiding verify ----------------
    The reference decompresses R (a 2^252-3 exponentiation) only to compare it
    with R' = [S]B - [k]A (fd_ed25519_user.c:164-229).  Here R' is compared on
    its encoding instead: y_R (the encoded y, reduced mod p) must equal Y/Z,
@@ -701,10 +429,9 @@ FDG_DEV void wg_scan(const fe &z, fe &pex, fe &sex, uint32_t *tot_out) {
   }
 }
 
-/* Kernel A: pass 1 without R, [S]B - [k]A, y check, Z scan; parks
-   X, Y, Z (entry 9 words 0-29), the exclusive prefix (entry 9 words 30-39)
-   and suffix (entry 10 words 0-9) products and the flags (entry 10 word 10). */
-__global__ void __launch_bounds__(FDGPU_BLOCK, FDGPU_PREP_WAVES)
+/* Kernel A: pass 1 without R, [S]B - [k]A, y check, Z scan.  Parks R'
+   (slow-path lanes, park words 0-29) and U + flags (post entry). */
+__global__ void __launch_bounds__(FDGPU_BLOCK, FDGPU_VERIFY_WAVES)
 fdgpu_verify_ra_kernel(const uint8_t *__restrict__ arena, const fdgpu_sig_desc_t *__restrict__ sigs, uint32_t n_sig,
                        const uint32_t *__restrict__ btab, uint32_t *__restrict__ ws, uint32_t *__restrict__ wg_tot,
                        uint32_t *__restrict__ queue, uint32_t *__restrict__ queue_cnt, uint32_t flags) {
@@ -716,12 +443,7 @@ fdgpu_verify_ra_kernel(const uint8_t *__restrict__ arena, const fdgpu_sig_desc_t
   for (int off = 32; off > 0; off >>= 1) nb = max(nb, (uint32_t)__shfl_xor((int)nb, off));
   uint32_t *wsl = lane_ws(ws, i);
   uint32_t *park = park_ptr(wsl);
-#if FDGPU_EXP_LDS_PAD
-  __shared__ uint32_t s_pad[FDGPU_EXP_LDS_PAD / 4];
-  if (threadIdx.x == 0 && nb == 12345u) s_pad[blockIdx.x % (FDGPU_EXP_LDS_PAD / 4)] = 1u;
-  if (nb == 12346u) park[0] = s_pad[threadIdx.x];
-#endif
-  const int code1 = verify_pass1<false>(arena, d, nb, wsl, btab, (flags & FDGPU_FLAG_REF_MAP) != 0);
+  const int code1 = verify_pass1(arena, d, nb, wsl, btab, (flags & FDGPU_FLAG_REF_MAP) != 0);
   const bool need = active && code1 == 0;
   ge_p2 Rc;
   if (__any(need)) {
@@ -765,14 +487,14 @@ fdgpu_verify_ra_kernel(const uint8_t *__restrict__ arena, const fdgpu_sig_desc_t
   fe U;
   fe_mul(U, Rc.X, pex);
   fe_mul(U, U, sex);
-  uint4 *o = (uint4 *)(park + 32);             /* words 32-43 (16-B aligned): U, flags */
+  uint4 *o = (uint4 *)(post_ptr(wsl) + POST_U);   /* [S]B is dead here: dsm_k added it */
   o[0] = make_uint4(U.v[0], U.v[1], U.v[2], U.v[3]);
   o[1] = make_uint4(U.v[4], U.v[5], U.v[6], U.v[7]);
   o[2] = make_uint4(U.v[8], U.v[9], fl, 0u);
 }
 
-/* Inverse of one workgroup's Z product (Kernel B's work, run by the extra
-   blocks of fdgpu_tail_kernel). */
+/* Inverse of one workgroup's Z product (run by the extra blocks of
+   fdgpu_tail_kernel). */
 FDG_DEV void wg_invert(const uint32_t *__restrict__ wg_tot, uint32_t *__restrict__ wg_inv, uint32_t g) {
   fe a, r;
 #pragma unroll
@@ -782,15 +504,22 @@ FDG_DEV void wg_invert(const uint32_t *__restrict__ wg_tot, uint32_t *__restrict
   for (int k = 0; k < 10; k++) wg_inv[10 * g + k] = r.v[k];
 }
 
+/* Output slot of lane i: signatures may be verified in an order grouped by
+   SHA-512 block count (perm[i] = the signature's index in the caller's
+   order); codes are always written in the caller's order. */
+FDG_DEV uint32_t out_idx(const uint32_t *__restrict__ perm, uint32_t i) { return perm ? perm[i] : i; }
+
 /* Kernel C: finish each signature from its y check and the parity of
-   x = X / Z (Z^-1 = workgroup inverse x prefix x suffix); queue the rest. */
+   x = X / Z (Z^-1 = workgroup inverse x prefix x suffix); slow-path lanes
+   are left to fdgpu_tail_kernel. */
 __global__ void __launch_bounds__(FDGPU_BLOCK) fdgpu_finish_kernel(
     const uint8_t *__restrict__ arena, const fdgpu_sig_desc_t *__restrict__ sigs, uint32_t n_sig,
-    const uint32_t *__restrict__ ws, const uint32_t *__restrict__ wg_inv, int8_t *__restrict__ codes) {
+    const uint32_t *__restrict__ ws, const uint32_t *__restrict__ wg_inv, const uint32_t *__restrict__ perm,
+    int8_t *__restrict__ codes) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   const bool active = i < n_sig;
-  const uint32_t *park = ws + (size_t)(active ? i : 0) * FDGPU_WS_LANE_WORDS + FDGPU_WS_PARK * FDGPU_ATAB_WORDS;
-  const uint4 *pv = (const uint4 *)(park + 32);
+  const uint32_t *post = ws + (size_t)(active ? i : 0) * FDGPU_WS_LANE_WORDS + FDGPU_WS_SB * FDGPU_ATAB_WORDS;
+  const uint4 *pv = (const uint4 *)(post + POST_U);
   const uint4 u0 = pv[0], u1 = pv[1], u2 = pv[2];
   const uint32_t fl = u2.z;
   const int code1 = (int)(int8_t)(fl & 0xffu);
@@ -819,72 +548,82 @@ __global__ void __launch_bounds__(FDGPU_BLOCK) fdgpu_finish_kernel(
     else c = small ? -1 : -3;
     if (active && code1 == 0 && !slow) code = c;
   }
-  if (active && !slow) codes[i] = (int8_t)code;
+  if (active && !slow) codes[out_idx(perm, i)] = (int8_t)code;
 }
 
-/* Kernel D: the queued signatures, with the reference's full R decode
-   (fd_ed25519_user.c:164-229 order: R decode failure, A small, R small,
-   equation). */
 /* Kernel B+D (one launch, both latency-bound): blocks [0, slow_blocks) run
-   the queued signatures grid-stride; the remaining blocks invert the
-   workgroup Z products, one per thread. */
-__global__ void __launch_bounds__(FDGPU_BLOCK, FDGPU_PREP_WAVES) fdgpu_tail_kernel(
+   the queued signatures grid-stride with the reference's full R decode
+   (fd_ed25519_user.c:164-229 order: R decode failure, A small, R small,
+   equation); the remaining blocks invert the workgroup Z products, one per
+   thread.  slow_blocks covers every resident wave slot the batch's grid
+   has, so a batch where every signature fails the equation (all queued)
+   spreads the decodes over the whole GPU. */
+__global__ void __launch_bounds__(FDGPU_BLOCK, FDGPU_VERIFY_WAVES) fdgpu_tail_kernel(
     const uint8_t *__restrict__ arena, const fdgpu_sig_desc_t *__restrict__ sigs, const uint32_t *__restrict__ ws,
-    int8_t *__restrict__ codes, const uint32_t *__restrict__ queue, const uint32_t *__restrict__ queue_cnt,
-    const uint32_t *__restrict__ wg_tot, uint32_t *__restrict__ wg_inv, uint32_t n_wg, uint32_t slow_blocks,
-    uint32_t flags) {
+    const uint32_t *__restrict__ perm, int8_t *__restrict__ codes, const uint32_t *__restrict__ queue,
+    const uint32_t *__restrict__ queue_cnt, const uint32_t *__restrict__ wg_tot, uint32_t *__restrict__ wg_inv,
+    uint32_t n_wg, uint32_t slow_blocks, uint32_t flags) {
   if (blockIdx.x >= slow_blocks) {
     const uint32_t g = (blockIdx.x - slow_blocks) * blockDim.x + threadIdx.x;
     if (g < n_wg) wg_invert(wg_tot, wg_inv, g);
     return;
   }
   const uint32_t cnt = *queue_cnt;
+  if (blockIdx.x * blockDim.x >= cnt) return;            /* nothing queued for this block */
   for (uint32_t q = blockIdx.x * blockDim.x + threadIdx.x; q < cnt; q += slow_blocks * blockDim.x) {
-  const uint32_t i = queue[q];
-  const uint32_t *wsl = ws + (size_t)i * FDGPU_WS_LANE_WORDS;
-  const uint32_t *park = wsl + FDGPU_WS_PARK * FDGPU_ATAB_WORDS;
-  const uint32_t fl = park[42];
-  uint32_t Renc[8];
-  load32(Renc, arena + sigs[i].sig_off);
-  ge_p3 Rp;
-  const bool r_ok = ge_decode(Rp, Renc, (flags & FDGPU_FLAG_REF_MAP) != 0);
-  int code;
-  if (!r_ok) code = -1;
-  else if (fl & RA_ASMALL) code = -2;
-  else if (ge_is_small_order_affine(Rp)) code = -1;
-  else {
-    fe X, Y, Z, l;
+    const uint32_t i = queue[q];
+    const uint32_t *wsl = ws + (size_t)i * FDGPU_WS_LANE_WORDS;
+    const uint32_t *park = wsl + FDGPU_WS_PARK * FDGPU_ATAB_WORDS;
+    const uint32_t fl = wsl[FDGPU_WS_SB * FDGPU_ATAB_WORDS + POST_FLAGS];
+    uint32_t Renc[8];
+    load32(Renc, arena + sigs[i].sig_off);
+    ge_p3 Rp;
+    const bool r_ok = ge_decode(Rp, Renc, (flags & FDGPU_FLAG_REF_MAP) != 0);
+    int code;
+    if (!r_ok) code = -1;
+    else if (fl & RA_ASMALL) code = -2;
+    else if (ge_is_small_order_affine(Rp)) code = -1;
+    else {
+      fe X, Y, Z, l;
 #pragma unroll
-    for (int k = 0; k < 10; k++) { X.v[k] = park[k]; Y.v[k] = park[10 + k]; Z.v[k] = park[20 + k]; }
-    fe_mul(l, Rp.X, Z);
-    bool eq = fe_eq(X, l);
-    fe_mul(l, Rp.Y, Z);
-    eq = eq && fe_eq(Y, l);
-    code = eq ? 0 : -3;
-  }
-  codes[i] = (int8_t)code;
+      for (int k = 0; k < 10; k++) { X.v[k] = park[k]; Y.v[k] = park[10 + k]; Z.v[k] = park[20 + k]; }
+      fe_mul(l, Rp.X, Z);
+      bool eq = fe_eq(X, l);
+      fe_mul(l, Rp.Y, Z);
+      eq = eq && fe_eq(Y, l);
+      code = eq ? 0 : -3;
+    }
+    codes[out_idx(perm, i)] = (int8_t)code;
   }
 }
 
-__global__ void fdgpu_combine_kernel(const fdgpu_txn_desc_t *__restrict__ txns, uint32_t n_txn,
-                                     const int8_t *__restrict__ sig_codes, int8_t *__restrict__ txn_codes) {
+/* Per transaction: fd_ed25519_verify_batch_single_msg's first-error order
+   (fd_ed25519_user.c:232-310) over its signatures' codes, plus the batch's
+   accept/reject results compacted by wavefront ballot: bit t of accept[]
+   is set iff transaction t verified (one 64-bit word per wave; the verify
+   tile only needs accept/reject, so it can read n/8 bytes instead of n). */
+__global__ void __launch_bounds__(256) fdgpu_combine_kernel(const fdgpu_txn_desc_t *__restrict__ txns, uint32_t n_txn,
+                                                            const int8_t *__restrict__ sig_codes,
+                                                            int8_t *__restrict__ txn_codes,
+                                                            uint64_t *__restrict__ accept) {
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= n_txn) return;
-  const fdgpu_txn_desc_t d = txns[t];
-  int code;
-  if (d.sig_cnt == 0 || d.sig_cnt > 16) {
-    code = -1;                                           /* fd_ed25519_user.c:238-241 */
-  } else {
-    int first_struct = 0, any_msg = 0;
-    for (uint32_t j = 0; j < d.sig_cnt; j++) {
-      const int c = sig_codes[d.sig0 + j];
-      if (c == -3) any_msg = 1;
-      else if (c != 0 && first_struct == 0) first_struct = c;
+  int code = -1;
+  if (t < n_txn) {
+    const fdgpu_txn_desc_t d = txns[t];
+    if (d.sig_cnt >= 1 && d.sig_cnt <= 16) {             /* else ERR_SIG (fd_ed25519_user.c:238-241) */
+      int first_struct = 0, any_msg = 0;
+      for (uint32_t j = 0; j < d.sig_cnt; j++) {
+        const int c = sig_codes[d.sig0 + j];
+        if (c == -3) any_msg = 1;
+        else if (c != 0 && first_struct == 0) first_struct = c;
+      }
+      /* pass 1 reports its first failure before any pass-2 (equation) failure */
+      code = first_struct ? first_struct : (any_msg ? -3 : 0);
     }
-    /* pass 1 reports its first failure before any pass-2 (equation) failure */
-    code = first_struct ? first_struct : (any_msg ? -3 : 0);
+    txn_codes[t] = (int8_t)code;
   }
-  txn_codes[t] = (int8_t)code;
+  const uint64_t ok = __ballot(t < n_txn && code == 0);   /* every lane of the wave takes part */
+  if (accept && (threadIdx.x & 63u) == 0 && t < n_txn) accept[t >> 6] = ok;
 }
 
 /* ---------------- test / diagnostic kernels ---------------- */
@@ -985,16 +724,9 @@ __global__ void __launch_bounds__(64) fdgpu_test_sc_reduce_kernel(const uint32_t
 
 extern "C" {
 
-size_t fdgpu_btab_bytes(void) {
-#if FDGPU_BCOMB
-  return (size_t)BC_NDIG * BC_ENT * FDGPU_BCOMB_STRIDE * sizeof(uint32_t);
-#else
-  return (size_t)FDGPU_BTAB_ENTRIES * FDGPU_BTAB_STRIDE * sizeof(uint32_t);
-#endif
-}
+size_t fdgpu_btab_bytes(void) { return (size_t)BC_NDIG * BC_ENT * FDGPU_BCOMB_STRIDE * sizeof(uint32_t); }
 
 hipError_t fdgpu_btab_build(uint32_t *d_btab, hipStream_t stream) {
-#if FDGPU_BCOMB
   uint32_t *bases = nullptr, *scratch = nullptr;
   const uint32_t lanes = BC_NDIG * BC_CHUNKS;
   hipError_t e = hipMalloc((void **)&bases, BC_NDIG * 40 * sizeof(uint32_t));
@@ -1011,69 +743,57 @@ hipError_t fdgpu_btab_build(uint32_t *d_btab, hipStream_t stream) {
   if (bases) (void)hipFree(bases);
   if (scratch) (void)hipFree(scratch);
   return e;
-#else
-  hipLaunchKernelGGL(fdgpu_btab_init_kernel, dim3(1), dim3(192), 0, stream, d_btab);
-  hipError_t e = hipGetLastError();
-  return e == hipSuccess ? hipStreamSynchronize(stream) : e;
-#endif
 }
 
 hipError_t fdgpu_verify_occupancy(int *blocks_per_cu) {
-#if FDGPU_FUSED
-  return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, fdgpu_fused_kernel, FDGPU_BLOCK, 0);
-#else
-  return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, fdgpu_dsm_kernel, FDGPU_BLOCK, 0);
-#endif
+  return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, fdgpu_verify_ra_kernel, FDGPU_BLOCK, 0);
 }
 
-/* workspace: per-lane words, then (FDGPU_RAVOID) per-workgroup Z products
-   and their inverses, the slow-path queue and its counter */
+/* workspace: per-lane words, then per-workgroup Z products and their
+   inverses, the slow-path queue and its counter */
 size_t fdgpu_ws_bytes(uint64_t n_sig) {
   const uint64_t grid = (n_sig + FDGPU_BLOCK - 1) / FDGPU_BLOCK, lanes = grid * FDGPU_BLOCK;
   return (size_t)(lanes * FDGPU_WS_LANE_WORDS + 20 * grid + lanes + 16) * sizeof(uint32_t);
 }
 
 hipError_t fdgpu_launch_verify_sigs(const uint8_t *d_arena, const fdgpu_sig_desc_t *d_sigs, uint32_t n_sig,
-                                    const uint32_t *d_btab, uint32_t *d_ws, int8_t *d_sig_codes, uint32_t flags,
-                                    hipStream_t stream) {
+                                    const uint32_t *d_perm, const uint32_t *d_btab, uint32_t *d_ws,
+                                    int8_t *d_sig_codes, uint32_t flags, hipStream_t stream) {
   if (!n_sig) return hipSuccess;
   const uint32_t grid = (n_sig + FDGPU_BLOCK - 1) / FDGPU_BLOCK;
-#if FDGPU_RAVOID
-  {
-    const size_t lanes = (size_t)grid * FDGPU_BLOCK;
-    uint32_t *wg_tot = d_ws + lanes * FDGPU_WS_LANE_WORDS, *wg_inv = wg_tot + 10 * (size_t)grid;
-    uint32_t *queue = wg_inv + 10 * (size_t)grid, *cnt = queue + lanes;
-    hipError_t e = hipMemsetAsync(cnt, 0, sizeof(uint32_t), stream);
-    if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(fdgpu_verify_ra_kernel, dim3(grid), dim3(FDGPU_BLOCK), 0, stream, d_arena, d_sigs, n_sig, d_btab,
-                       d_ws, wg_tot, queue, cnt, flags);
-    /* slow path sized for ~1/8 of the signatures per pass (grid-stride beyond) */
-    const uint32_t slow_blocks = (grid + 7) / 8, inv_blocks = (grid + FDGPU_BLOCK - 1) / FDGPU_BLOCK;
-    hipLaunchKernelGGL(fdgpu_tail_kernel, dim3(slow_blocks + inv_blocks), dim3(FDGPU_BLOCK), 0, stream, d_arena,
-                       d_sigs, d_ws, d_sig_codes, queue, cnt, wg_tot, wg_inv, grid, slow_blocks, flags);
-    hipLaunchKernelGGL(fdgpu_finish_kernel, dim3(grid), dim3(FDGPU_BLOCK), 0, stream, d_arena, d_sigs, n_sig, d_ws,
-                       wg_inv, d_sig_codes);
-    return hipGetLastError();
-  }
-#endif
-#if FDGPU_FUSED
-  hipLaunchKernelGGL(fdgpu_fused_kernel, dim3(grid), dim3(FDGPU_BLOCK), 0, stream, d_arena, d_sigs, n_sig, d_btab, d_ws,
-                     d_sig_codes, flags);
-  return hipGetLastError();
-#endif
-  hipLaunchKernelGGL(fdgpu_prep_kernel, dim3(grid), dim3(FDGPU_BLOCK), 0, stream, d_arena, d_sigs, n_sig, d_btab, d_ws,
-                     flags);
-  hipError_t e = hipGetLastError();
+  const size_t lanes = (size_t)grid * FDGPU_BLOCK;
+  uint32_t *wg_tot = d_ws + lanes * FDGPU_WS_LANE_WORDS, *wg_inv = wg_tot + 10 * (size_t)grid;
+  uint32_t *queue = wg_inv + 10 * (size_t)grid, *cnt = queue + lanes;
+  hipError_t e = hipMemsetAsync(cnt, 0, sizeof(uint32_t), stream);
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(fdgpu_dsm_kernel, dim3(grid), dim3(FDGPU_BLOCK), 0, stream, n_sig, d_btab, d_ws, d_sig_codes);
+  hipLaunchKernelGGL(fdgpu_verify_ra_kernel, dim3(grid), dim3(FDGPU_BLOCK), 0, stream, d_arena, d_sigs, n_sig, d_btab,
+                     d_ws, wg_tot, queue, cnt, flags);
+  /* slow path: as many blocks as the batch's grid could keep resident (all of
+     them, up to every wave slot of the GPU), each exiting at once when the
+     queue holds nothing for it; one block per 256 workgroup inversions */
+  static int resident = 0;
+  if (!resident) {
+    int bpcu = 0, dev = 0, cus = 0;
+    if (fdgpu_verify_occupancy(&bpcu) != hipSuccess || bpcu < 1) bpcu = 1;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) !=
+                                                hipSuccess || cus < 1)
+      cus = 256;
+    resident = bpcu * cus;
+  }
+  const uint32_t slow_blocks = grid < (uint32_t)resident ? grid : (uint32_t)resident;
+  const uint32_t inv_blocks = (grid + FDGPU_BLOCK - 1) / FDGPU_BLOCK;
+  hipLaunchKernelGGL(fdgpu_tail_kernel, dim3(slow_blocks + inv_blocks), dim3(FDGPU_BLOCK), 0, stream, d_arena,
+                     d_sigs, d_ws, d_perm, d_sig_codes, queue, cnt, wg_tot, wg_inv, grid, slow_blocks, flags);
+  hipLaunchKernelGGL(fdgpu_finish_kernel, dim3(grid), dim3(FDGPU_BLOCK), 0, stream, d_arena, d_sigs, n_sig, d_ws,
+                     wg_inv, d_perm, d_sig_codes);
   return hipGetLastError();
 }
 
 hipError_t fdgpu_launch_combine(const fdgpu_txn_desc_t *d_txns, uint32_t n_txn, const int8_t *d_sig_codes,
-                                int8_t *d_txn_codes, hipStream_t stream) {
+                                int8_t *d_txn_codes, uint64_t *d_accept, hipStream_t stream) {
   if (!n_txn) return hipSuccess;
   hipLaunchKernelGGL(fdgpu_combine_kernel, dim3((n_txn + 255) / 256), dim3(256), 0, stream, d_txns, n_txn,
-                     d_sig_codes, d_txn_codes);
+                     d_sig_codes, d_txn_codes, d_accept);
   return hipGetLastError();
 }
 

@@ -111,41 +111,6 @@ FDG_DEV void sc_recode16(uint32_t (&out)[8], const uint32_t (&k)[8]) {
   }
 }
 
-/* Signed radix-32 digits of k < 2^253: 51 digits in [-16, 15] as int8,
-   digit j in byte j + 1 of the 13-word string (byte 0 and 51 zero). */
-FDG_DEV void sc_recode32(uint32_t (&out)[13], const uint32_t (&k)[8]) {
-  uint32_t carry = 0;
-#pragma unroll
-  for (int i = 0; i < 13; i++) out[i] = 0;
-#pragma unroll
-  for (int j = 0; j < 51; j++) {
-    const int bit = 5 * j, wd = bit >> 5, sh = bit & 31;
-    uint64_t x = k[wd];
-    if (wd + 1 < 8) x |= (uint64_t)k[wd + 1] << 32;
-    uint32_t e = (uint32_t)((x >> sh) & 31u) + carry;
-    carry = e >= 16u;
-    e = (e - (carry << 5)) & 255u;
-    out[(j + 1) >> 2] |= e << (8 * ((j + 1) & 3));
-  }
-}
-
-/* Signed radix-256 digits of S: 32 digits in [-128, 127] as int8 bytes. */
-FDG_DEV void sc_recode256(uint32_t (&out)[8], const uint32_t (&s)[8]) {
-  uint32_t carry = 0;
-#pragma unroll
-  for (int w = 0; w < 8; w++) {
-    uint32_t o = 0;
-#pragma unroll
-    for (int n = 0; n < 4; n++) {
-      uint32_t e = ((s[w] >> (8 * n)) & 255u) + carry;
-      carry = e >= 128u;
-      e = (e - (carry << 8)) & 255u;
-      o |= e << (8 * n);
-    }
-    out[w] = o;
-  }
-}
-
 /* Signed radix-2^W digits of S for the fixed-base comb (W = FDGPU_BCOMB_BITS):
    NDIG digits d_i in [-2^(W-1), 2^(W-1)], S = sum d_i 2^(W i), packed as
    int16 slots (two per word, digit 0 in the low half of word 0).  Needs

@@ -182,6 +182,7 @@ struct Batch {
   std::vector<Item> items;
   std::vector<int8_t> codes;
   uint64_t arena_used = 0, trailer_used = 0;
+  uint64_t sig_cnt = 0;             /* signatures the verifier will check (sig_cnt in [1,16] per txn) */
   int64_t ticket = -1;
   bool done = false;
   size_t next = 0;                  /* next item to resolve */
@@ -189,6 +190,7 @@ struct Batch {
 
   void reset() {
     arena_used = trailer_used = 0;
+    sig_cnt = 0;
     txns.clear(); items.clear();
     ticket = -1; done = false; next = 0; t_first = 0;
     ap = nullptr; cap = 0; staged = false;
@@ -294,7 +296,10 @@ struct fdgpu_vtile {
       open = nb;
     }
     Batch &b = *open;
-    while (b.items.size() < cfg.batch_txn_max && b.arena_used + FDT_TPU_MTU <= b.cap) {
+    /* room for one more frag: payload bytes, and signatures (a txn sends at
+       most 16 to the verifier; more make batch_single_msg fail unverified) */
+    while (b.items.size() < cfg.batch_txn_max && b.arena_used + FDT_TPU_MTU <= b.cap &&
+           b.sig_cnt + 16 <= cfg.batch_sig_max) {
       fdt_frag_meta_t m;
       uint64_t found;
       const int rc = fdt_mcache_poll(cfg.in_mcache, cfg.in_depth, rx_seq, &m, &found);
@@ -333,20 +338,36 @@ struct fdgpu_vtile {
       b.txns.push_back(d);
       b.arena_used += m.sz;
       b.trailer_used += (tsz + 7) & ~7ull;
-      st.sigs += t->signature_cnt;
+      if (t->signature_cnt <= 16) { b.sig_cnt += t->signature_cnt; st.sigs += t->signature_cnt; }
     }
+  }
+
+  /* The verifier refused the batch as malformed (e.g. more signatures than
+     the engine was opened for): its transactions are failed -- logged as
+     FAILED and counted in verify_errors, nothing published -- and the batch
+     returns to the pool, so the tile keeps running.  Device errors stay
+     fatal (returned from step). */
+  void reject_open() {
+    Batch *b = open;
+    for (const Item &it : b->items) { st.verify_errors++; log(it.seq, FD_TXN_VERIFY_FAILED); }
+    if (b->staged && ver.stage_cancel) ver.stage_cancel(ver.ctx);
+    b->reset();
+    pool.push_back(b);
+    open = nullptr;
   }
 
   /* submit the open batch when full or when its first frag has waited long enough */
   int submit(bool force) {
     if (!open || open->items.empty()) return 0;
-    const bool full = open->items.size() >= cfg.batch_txn_max || open->arena_used + FDT_TPU_MTU > open->cap;
+    const bool full = open->items.size() >= cfg.batch_txn_max || open->arena_used + FDT_TPU_MTU > open->cap ||
+                      open->sig_cnt + 16 > cfg.batch_sig_max;
     if (!full && !force && now_ns() - open->t_first < cfg.batch_wait_ns) return 0;
     if (inflight.size() >= cfg.inflight_max) return 0;
     const int64_t t = open->staged
         ? ver.submit_staged(ver.ctx, open->arena_used, open->txns.data(), open->txns.size())
         : ver.submit(ver.ctx, open->ap, open->arena_used, open->txns.data(), open->txns.size());
     if (t == FDGPU_ERR_FULL) return 0;
+    if (t == FDGPU_ERR_INVAL) { reject_open(); return 0; }
     if (t < 0) return (int)t;
     open->ticket = t;
     inflight.push_back(open);
@@ -371,6 +392,9 @@ fdgpu_vtile_t *fdgpu_vtile_new(const fdgpu_vtile_cfg_t *cfg, fdgpu_verifier_t ve
   if (!t->cfg.round_robin_cnt) t->cfg.round_robin_cnt = 1;
   if (!t->cfg.inflight_max) t->cfg.inflight_max = 2;
   if (!t->cfg.tcache_depth) t->cfg.tcache_depth = FDT_VERIFY_TCACHE_DEPTH;
+  /* default: the engine's default max_sig (12 per txn), at least one txn's 16 */
+  if (!t->cfg.batch_sig_max) t->cfg.batch_sig_max = std::max<uint64_t>(16, (uint64_t)t->cfg.batch_txn_max * 12);
+  if (t->cfg.batch_sig_max < 16) { delete t; return nullptr; }
   if (!cfg->tcache_depth && !t->cfg.tcache_map_cnt) t->cfg.tcache_map_cnt = FDT_VERIFY_TCACHE_MAP_CNT;
   const uint64_t fp = fdt_tcache_footprint(t->cfg.tcache_depth, t->cfg.tcache_map_cnt);
   if (!fp) { delete t; return nullptr; }

@@ -93,13 +93,13 @@ class VTileCfg(c.Structure):
                 ("out_chunk0", c.c_uint64), ("out_wmark", c.c_uint64), ("out_fseq", vp),
                 ("round_robin_idx", c.c_uint64), ("round_robin_cnt", c.c_uint64), ("hashmap_seed", c.c_uint64),
                 ("tcache_depth", c.c_uint64), ("tcache_map_cnt", c.c_uint64), ("batch_txn_max", c.c_uint32),
-                ("inflight_max", c.c_uint32), ("batch_wait_ns", c.c_uint64)]
+                ("inflight_max", c.c_uint32), ("batch_wait_ns", c.c_uint64), ("batch_sig_max", c.c_uint64)]
 
 
 class VTileStats(c.Structure):
     _fields_ = [(n, c.c_uint64) for n in ("in_frags", "filtered_rr", "corrupt", "overrun", "parse_fail",
                                           "verify_failed", "dedup", "published", "batches", "sigs",
-                                          "backpressure", "lat_cnt")]
+                                          "backpressure", "lat_cnt", "verify_errors")]
 
     def as_dict(self):
         return {n: getattr(self, n) for n, _ in self._fields_}
@@ -535,6 +535,7 @@ class EngineVerifier:
     def __init__(self, engines):
         L = lib()
         self.engines = list(engines)
+        self.sig_max = min(e.max_sig for e in self.engines)     # signatures per batch every engine accepts
         arr = (vp * len(self.engines))(*[e._h for e in self.engines])
         self._d = L.fdgpu_dispatch_new(arr, len(self.engines))
         if not self._d:
@@ -594,7 +595,7 @@ class VerifyTile:
 
     def __init__(self, in_link, out_link, verifier, hashmap_seed=0x5EEDF00D, batch_txn_max=4096, inflight_max=2,
                  batch_wait_us=200, round_robin_idx=0, round_robin_cnt=1, tcache_depth=0, tcache_map_cnt=0,
-                 flow_control=False, log_max=0):
+                 flow_control=False, log_max=0, batch_sig_max=0):
         L = lib()
         self.verifier, self.in_link, self.out_link = verifier, in_link, out_link
         cfg = VTileCfg()
@@ -608,6 +609,7 @@ class VerifyTile:
         cfg.tcache_depth, cfg.tcache_map_cnt = tcache_depth, tcache_map_cnt
         cfg.batch_txn_max, cfg.inflight_max = batch_txn_max, inflight_max
         cfg.batch_wait_ns = int(batch_wait_us * 1000)
+        cfg.batch_sig_max = batch_sig_max or getattr(verifier, "sig_max", 0)
         self.cfg = cfg
         self._t = L.fdgpu_vtile_new(c.byref(cfg), verifier.struct)
         if not self._t:

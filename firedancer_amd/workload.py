@@ -30,10 +30,18 @@ def gen():
         g.fdgen_txns.argtypes = [c.c_uint64, c.c_uint64, c.c_int, c.c_uint32, c.c_uint32, c.c_uint32, c.c_double,
                                  c.c_uint32, c.c_void_p, c.c_void_p, c.c_void_p, c.c_int]
         g.fdgen_txns.restype = c.c_int
+        g.fdgen_txns_ex.argtypes = [c.c_uint64, c.c_uint64, c.c_int, c.c_uint32, c.c_uint32, c.c_uint32, c.c_double,
+                                    c.c_int, c.c_uint64, c.c_uint32, c.c_void_p, c.c_void_p, c.c_void_p, c.c_int]
+        g.fdgen_txns_ex.restype = c.c_int
         g.fdgen_sign.argtypes = [c.c_char_p, c.c_char_p, c.c_uint64, c.c_char_p, c.c_char_p]
         g.fdgen_sign.restype = c.c_int
         _GEN = g
     return _GEN
+
+
+# A GPU box gives one GPU's share of the host, 16 CPUs (os.cpu_count() and
+# the affinity mask show the whole machine there): worker pools stay within it.
+BOX_CPU_SHARE = 16
 
 
 def default_threads():
@@ -41,17 +49,52 @@ def default_threads():
         n = len(os.sched_getaffinity(0))
     except AttributeError:
         n = os.cpu_count() or 1
-    return max(1, min(n, 16))
+    return max(1, min(n, BOX_CPU_SHARE))
 
 
-def make_txns(n, seed, multi=False, msg_lo=180, msg_hi=220, max_sigs=12, corrupt=0.10, nthreads=None):
-    """Returns (arena uint8[n*stride + slack], txns TXN_DTYPE[n], modes uint8[n])."""
+def physical_cpus(limit=BOX_CPU_SHARE):
+    """One logical CPU per physical core among the CPUs this process may run
+    on (SMT siblings skipped; /sys topology), at most `limit`: the CPU
+    baseline pins one thread to each (BASELINE.md "one pinned thread per
+    physical core", within the box's CPU share)."""
+    try:
+        allowed = sorted(os.sched_getaffinity(0))
+    except AttributeError:
+        allowed = list(range(os.cpu_count() or 1))
+    seen, out = set(), []
+    for cpu in allowed:
+        base = f"/sys/devices/system/cpu/cpu{cpu}/topology/"
+        try:
+            key = (open(base + "physical_package_id").read().strip(), open(base + "core_id").read().strip())
+        except OSError:
+            key = ("cpu", str(cpu))
+        if key in seen:
+            continue
+        seen.add(key)
+        out.append(cpu)
+        if len(out) >= limit:
+            break
+    return out or [0]
+
+
+# corruption modes (modes[i]): which bit the generator flipped
+MODE_NONE, MODE_SIG, MODE_MSG, MODE_PUB, MODE_R = 0, 1, 2, 3, 4
+
+
+def make_txns(n, seed, multi=False, msg_lo=180, msg_hi=220, max_sigs=12, corrupt=0.10, nthreads=None,
+              corrupt_mode=0, key_pool=0):
+    """Returns (arena uint8[n*stride + slack], txns TXN_DTYPE[n], modes uint8[n]).
+    corrupt_mode 0 flips a bit of a random one of signature / message /
+    public key (test_ed25519.c:920-951's bad-sig/msg/pub modes); MODE_* forces
+    one (MODE_R: a bit of R).  key_pool K > 0 draws signers from K seeded key
+    pairs instead of a fresh pair per signer."""
     stride = 1232 + 16 if multi else ((1 + 64 + max(msg_hi, 256) + 15) // 16) * 16
     arena = np.zeros(n * stride + 256, dtype=np.uint8)
     txns = np.zeros(n, dtype=TXN_DTYPE)
     modes = np.zeros(n, dtype=np.uint8)
-    rc = gen().fdgen_txns(n, seed, 1 if multi else 0, msg_lo, msg_hi, max_sigs, corrupt, stride,
-                          arena.ctypes.data, txns.ctypes.data, modes.ctypes.data, nthreads or default_threads())
+    rc = gen().fdgen_txns_ex(n, seed, 1 if multi else 0, msg_lo, msg_hi, max_sigs, corrupt, corrupt_mode, key_pool,
+                             stride, arena.ctypes.data, txns.ctypes.data, modes.ctypes.data,
+                             nthreads or default_threads())
     if rc != 0:
         raise RuntimeError(f"fdgen_txns failed: {rc}")
     return arena[: n * stride], txns, modes

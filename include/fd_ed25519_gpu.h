@@ -10,10 +10,14 @@
                                             (impl fd_ed25519_user.c:232-310)
          fd_ed25519_strerror                replaces src/ballet/ed25519/fd_ed25519.h:132-136
                                             (impl fd_ed25519_user.c:312-322)
-       Served by the GPU engine (device 0, opened on first use); results are
-       bit-identical to the reference's AVX-512 build.  Each call is one GPU
-       round trip (tens of microseconds): correct, but the batch API below is
-       the throughput path.
+       A compatibility shim served by the GPU engine (device 0, opened on
+       first use); results are bit-identical to the reference's AVX-512
+       build.  Each call is one serialised GPU round trip (tens of
+       microseconds): correct, but hot callers belong on the batch API below.
+       The caller thread's current HIP device is preserved.  The reference
+       API returns verify codes only, so an engine failure (no GPU, a HIP
+       error) ABORTS the process rather than return a verdict nothing
+       computed.
 
    (ii) Asynchronous batch API for the verify stage (the north-star shim;
        SURVEY.md §8(b)(ii)).  One engine per GPU; each engine owns pinned,
@@ -80,13 +84,16 @@ typedef struct fdgpu_engine fdgpu_engine_t;
 
 typedef struct {
   uint64_t max_txn;       /* per batch */
-  uint64_t max_sig;       /* per batch (sum of sig_cnt) */
+  uint64_t max_sig;       /* per batch (sum of sig_cnt); 0 = 12 x max_txn (FD_TXN_ACTUAL_SIG_MAX);
+                             a batch with more signatures is rejected with FDGPU_ERR_INVAL */
   uint64_t max_arena;     /* per batch, bytes */
   uint32_t ring_depth;    /* in-flight batches (pinned staging slots), >= 1; default 2 */
   uint32_t flags;         /* FDGPU_FLAG_* */
 } fdgpu_cfg_t;
 
 #define FDGPU_FLAG_REF_MAPPING 1u  /* portable-backend (ref) error mapping instead of AVX-512 */
+#define FDGPU_FLAG_NO_BUCKET   2u  /* verify signatures in transaction order (default: grouped by
+                                      SHA-512 block count, codes still returned in order) */
 
 /* Status codes of the engine API (distinct from verify codes). */
 #define FDGPU_OK            ( 0)

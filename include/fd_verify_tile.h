@@ -226,6 +226,8 @@ typedef struct {
   uint32_t batch_txn_max;               /* txns per GPU batch */
   uint32_t inflight_max;                /* batches in flight (<= the verifier's slots) */
   uint64_t batch_wait_ns;               /* a partial batch is submitted after this long */
+  uint64_t batch_sig_max;               /* signatures per batch (<= the engines' max_sig);
+                                           0: 12 x batch_txn_max, the engine's default */
 } fdgpu_vtile_cfg_t;
 
 typedef struct {
@@ -241,6 +243,7 @@ typedef struct {
   uint64_t sigs;            /* signatures sent to the GPU */
   uint64_t backpressure;    /* steps that stalled on out-link credits */
   uint64_t lat_cnt;         /* batch latencies recorded (ingest of first frag -> publish) */
+  uint64_t verify_errors;   /* txns of batches the verifier rejected as malformed (failed, not published) */
 } fdgpu_vtile_stats_t;
 
 typedef struct fdgpu_vtile fdgpu_vtile_t;

@@ -32,6 +32,7 @@
  * init time (d = -121665/121666, sqrt(-1) = 2^((p-1)/4), B decoded from
  * its RFC 8032 encoding, mu = floor(2^512/L) by long division).
  */
+#define _GNU_SOURCE
 #include "fd_ed25519_oracle.h"
 
 #include <pthread.h>
@@ -750,10 +751,15 @@ typedef struct {
   int                          mapping;
   int                          nthreads;
   int                          tid;
+  int                          cpu;      /* pin to this CPU (-1: no pinning) */
 } bulk_arg_t;
 
 static void * bulk_worker( void * _a ) {
   bulk_arg_t * a = (bulk_arg_t *)_a;
+  if( a->cpu >= 0 ) {
+    cpu_set_t set; CPU_ZERO( &set ); CPU_SET( a->cpu, &set );
+    (void)pthread_setaffinity_np( pthread_self(), sizeof(set), &set );
+  }
   uint64_t lo = a->n * (uint64_t)a->tid / (uint64_t)a->nthreads;
   uint64_t hi = a->n * (uint64_t)(a->tid+1) / (uint64_t)a->nthreads;
   for( uint64_t i=lo; i<hi; i++ ) {
@@ -765,18 +771,25 @@ static void * bulk_worker( void * _a ) {
   return NULL;
 }
 
-void oracle_verify_txns( uint8_t const * arena, oracle_txn_t const * txns, uint64_t n,
-                         int8_t * codes, int mapping, int nthreads ) {
+/* cpus: NULL, or nthreads CPU ids -- worker t is pinned to cpus[t] (the
+   CPU baseline: one pinned thread per physical core, static partition) */
+void oracle_verify_txns_pinned( uint8_t const * arena, oracle_txn_t const * txns, uint64_t n,
+                                int8_t * codes, int mapping, int nthreads, int const * cpus ) {
   oracle_init();
   if( nthreads < 1 ) nthreads = 1;
   if( nthreads > 256 ) nthreads = 256;
   pthread_t th[256]; bulk_arg_t args[256];
   for( int t=0; t<nthreads; t++ ) {
-    args[t] = (bulk_arg_t){ arena, txns, n, codes, mapping, nthreads, t };
-    if( nthreads==1 ) { bulk_worker( &args[t] ); return; }
+    args[t] = (bulk_arg_t){ arena, txns, n, codes, mapping, nthreads, t, cpus ? cpus[t] : -1 };
+    if( nthreads==1 && !cpus ) { bulk_worker( &args[t] ); return; }
     pthread_create( &th[t], NULL, bulk_worker, &args[t] );
   }
   for( int t=0; t<nthreads; t++ ) pthread_join( th[t], NULL );
+}
+
+void oracle_verify_txns( uint8_t const * arena, oracle_txn_t const * txns, uint64_t n,
+                         int8_t * codes, int mapping, int nthreads ) {
+  oracle_verify_txns_pinned( arena, txns, n, codes, mapping, nthreads, NULL );
 }
 
 /* ===================================================================

@@ -42,6 +42,8 @@ void oracle_verify_detail( uint8_t const * msg, uint64_t msg_sz, uint8_t const s
                            int mapping, int * pass1_code, int * eq, uint8_t k_out[32] );
 void oracle_verify_txns( uint8_t const * arena, oracle_txn_t const * txns, uint64_t n,
                          int8_t * codes, int mapping, int nthreads );
+void oracle_verify_txns_pinned( uint8_t const * arena, oracle_txn_t const * txns, uint64_t n,
+                                int8_t * codes, int mapping, int nthreads, int const * cpus );
 
 void oracle_public_from_private( uint8_t pub[32], uint8_t const prv[32] );
 void oracle_sign( uint8_t sig[64], uint8_t const * msg, uint64_t sz, uint8_t const pub[32], uint8_t const prv[32] );

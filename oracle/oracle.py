@@ -38,6 +38,8 @@ def lib():
         L.oracle_verify_detail.argtypes = [u8p, c.c_uint64, u8p, u8p, c.c_int,
                                            c.POINTER(c.c_int), c.POINTER(c.c_int), c.c_char_p]
         L.oracle_verify_txns.argtypes = [c.c_void_p, c.c_void_p, c.c_uint64, c.c_void_p, c.c_int, c.c_int]
+        L.oracle_verify_txns_pinned.argtypes = [c.c_void_p, c.c_void_p, c.c_uint64, c.c_void_p, c.c_int, c.c_int,
+                                                c.c_void_p]
         L.oracle_point_decode.argtypes = [u8p, c.c_int, c.POINTER(c.c_int), c.c_char_p]
         L.oracle_sha512.argtypes = [u8p, c.c_uint64, c.c_char_p]
         L.oracle_scalar_reduce.argtypes = [c.c_char_p, u8p]
@@ -100,11 +102,17 @@ def sign(msg, pub, prv):
     return out.raw
 
 
-def verify_txns(arena, txns, mapping=MAP_AVX512, nthreads=1):
-    """arena: uint8 ndarray; txns: ndarray of TXN_DTYPE. Returns int8 codes."""
+def verify_txns(arena, txns, mapping=MAP_AVX512, nthreads=1, cpus=None):
+    """arena: uint8 ndarray; txns: ndarray of TXN_DTYPE. Returns int8 codes.
+    cpus: list of CPU ids, one pinned worker thread each (overrides nthreads)."""
     arena = np.ascontiguousarray(arena, dtype=np.uint8)
     txns = np.ascontiguousarray(txns, dtype=TXN_DTYPE)
     codes = np.zeros(len(txns), dtype=np.int8)
-    lib().oracle_verify_txns(arena.ctypes.data, txns.ctypes.data, len(txns), codes.ctypes.data,
-                             mapping, nthreads)
+    if cpus:
+        cp = np.ascontiguousarray(cpus, dtype=np.int32)
+        lib().oracle_verify_txns_pinned(arena.ctypes.data, txns.ctypes.data, len(txns), codes.ctypes.data,
+                                        mapping, len(cp), cp.ctypes.data)
+    else:
+        lib().oracle_verify_txns(arena.ctypes.data, txns.ctypes.data, len(txns), codes.ctypes.data,
+                                 mapping, nthreads)
     return codes

@@ -421,3 +421,48 @@ def test_zero_copy_staging(engine):
     assert L.fdgpu_release(engine._h, tk) != 0
     p2 = L.fdgpu_stage_acquire(engine._h, ctypes.byref(cap))
     assert p2 and L.fdgpu_stage_cancel(engine._h) == 0
+
+
+def test_block_count_grouping_keeps_codes(engine, oracle):
+    """Signatures are verified grouped by SHA-512 block count (engine
+    default) yet every code lands in the caller's order: transaction and
+    per-signature codes equal the ungrouped engine's and the oracle's, over
+    messages of 0 to 1100+ bytes (1 to 10 blocks) interleaved at random."""
+    import firedancer_amd as fa
+    a3, t3, _ = workload.cfg3(1200, seed=0xB0C)
+    a1, t1, _ = workload.make_txns(1200, 0xB0D, msg_lo=0, msg_hi=1100)
+    a1 = a1.copy()
+    off = len(a3)
+    t1 = t1.copy()
+    for f in ("msg_off", "sig_off", "pub_off"):
+        t1[f] += off
+    arena = np.concatenate([a3, a1])
+    txns = np.concatenate([t3, t1])[np.random.default_rng(5).permutation(len(t3) + len(t1))]
+    flat = fa.VerifyEngine(0, max_txn=1 << 13, bucket=False)
+    try:
+        got, got_flat = engine.verify_txns(arena, txns), flat.verify_txns(arena, txns)
+        sig, sig_flat = engine.debug_sig_codes(arena, txns), flat.debug_sig_codes(arena, txns)
+        b = engine.upload(arena, txns)
+        b.verify()
+        dev_t, dev_s = b.codes(sig_codes=True)
+        b.free()
+    finally:
+        flat.close()
+    exp = oracle.verify_txns(arena, txns, nthreads=8)
+    st, _ = workload.explode_sigs(txns)
+    exp_s = oracle.verify_txns(arena, st, nthreads=8)
+    assert (got == exp).all() and (got_flat == exp).all() and (dev_t == exp).all()
+    assert (sig == exp_s).all() and (sig_flat == exp_s).all() and (dev_s == exp_s).all()
+
+
+@pytest.mark.parametrize("mode", [workload.MODE_MSG, workload.MODE_R])
+def test_all_failing_batches(engine, oracle, mode):
+    """test_ed25519.c:920-951 bad-msg / bad-sig modes at batch scale: every
+    signature of a 65,536-txn batch fails (all queued for the slow path's R
+    decode, spread over the whole grid); codes vs the oracle."""
+    arena, txns, modes = workload.make_txns(65536, 0xAD0 + mode, corrupt=1.0, corrupt_mode=mode)
+    assert (modes == mode).all()
+    got = engine.verify_txns(arena, txns)
+    exp = oracle.verify_txns(arena, txns, nthreads=8)
+    assert (got == exp).all(), np.nonzero(got != exp)[0][:10]
+    assert (got != 0).all()

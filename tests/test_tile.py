@@ -396,6 +396,64 @@ def test_verify_tile_vs_sequential_model(oracle, batch, inflight, lag, rr):
     assert exp_out.count(-2) > 10 and exp_out.count(-1) > 10 and exp_out.count(1) > 5
 
 
+def test_verify_tile_signature_cap(oracle):
+    """Batches close before their signature count can exceed batch_sig_max
+    (the engines' max_sig), so a stream of 12-signature transactions never
+    builds a batch the engine rejects; outcomes still match the model."""
+    a3, t3, _ = workload.make_txns(120, seed=0xCA9, multi=True, max_sigs=12)
+    ps = workload.payloads(a3, t3)
+    cap = 40
+    seen = []
+
+    def fn(arena, txns):
+        cnt = txns["sig_cnt"].astype(np.int64)
+        seen.append(int(np.where((cnt >= 1) & (cnt <= 16), cnt, 0).sum()))
+        return oracle_fn(oracle)(arena, txns)
+
+    inl, outl = tile.Link(1 << 10, 1232), tile.Link(1 << 10, tile.TPU_DCACHE_MTU)
+    vt = tile.VerifyTile(inl, outl, tile.PyVerifier(fn), batch_txn_max=64, batch_sig_max=cap, log_max=1 << 12)
+    for q in ps:
+        inl.publish(q)
+    vt.run(len(ps), timeout_s=30)
+    assert max(seen) <= cap and sum(seen) == int(t3["sig_cnt"].sum())
+    exp_out, _ = tile_model.verify_tile_model(ps, 0x5EEDF00D, oracle_fn(oracle))
+    assert vt.log()[1].tolist() == exp_out
+
+
+def test_verify_tile_recovers_from_rejected_batch(oracle, fixtures):
+    """A batch the verifier rejects as malformed (FDGPU_ERR_INVAL) fails its
+    transactions (verify_errors, nothing published) and the tile keeps
+    running: the next batches verify normally."""
+    v1, v2 = fixtures["test_verify.valid_txn_1sig"], fixtures["test_verify.valid_txn_2sigs"]
+    state = {"n": 0}
+    inner = tile.PyVerifier(oracle_fn(oracle))
+
+    def fn(arena, txns):
+        return oracle_fn(oracle)(arena, txns)
+
+    ver = tile.PyVerifier(fn)
+    orig_submit = ver._submit
+
+    def submit(ctx, arena, arena_sz, txns, n):
+        state["n"] += 1
+        if state["n"] == 1:
+            return -10                                            # FDGPU_ERR_INVAL
+        return orig_submit(ctx, arena, arena_sz, txns, n)
+
+    ver._submit = tile.SUBMIT_FN(submit)
+    ver.struct = tile.Verifier(None, ver._submit, ver._poll)
+    inl, outl = tile.Link(64, 1232), tile.Link(64, tile.TPU_DCACHE_MTU)
+    vt = tile.VerifyTile(inl, outl, ver, batch_txn_max=2, log_max=64)
+    for q in (v1, v2, v1, v2):
+        inl.publish(q)
+    vt.run(4, timeout_s=10)
+    st = vt.stats()
+    F, S, D = tile.VERIFY_FAILED, tile.VERIFY_SUCCESS, tile.VERIFY_DEDUP
+    assert vt.log()[1].tolist() == [F, F, S, S]                   # first batch rejected, tcache untouched
+    assert st["verify_errors"] == 2 and st["published"] == 2
+    del inner
+
+
 def test_verify_tile_out_flow_control(oracle):
     """With a reliable consumer (out fseq), the tile never runs more than
     out_depth frags ahead of it and resumes when it advances."""

@@ -92,3 +92,30 @@ def test_producer_at_rate_no_overrun(engines):
     assert st["published"] == int((modes == 0).sum())
     lat = vt.latencies_ns()
     assert len(lat) == st["batches"] and np.percentile(lat, 99) < 50e6
+
+
+def test_twelve_signature_txns_default_config():
+    """Engines opened with the default max_sig (12 per txn) and a tile with
+    the default signature cap: a stream of 12-signature transactions never
+    builds a batch the engine rejects, and matches the sequential model."""
+    a3, t3, _ = workload.make_txns(3000, 0x12, multi=True, max_sigs=12, key_pool=4096)
+    keep = t3["sig_cnt"] >= 10
+    ps = [p for p, k in zip(workload.payloads(a3, t3), keep) if k]
+    eng = fa.VerifyEngine(0, max_txn=256, ring_depth=2)
+    try:
+        inl, outl = tile.Link(1 << 12, 1232), tile.Link(1 << 12, tile.TPU_DCACHE_MTU)
+        vt = _tile([eng], inl, outl, batch_txn_max=256, log_max=1 << 13)
+        for p in ps:
+            inl.publish(p)
+        vt.run(len(ps), timeout_s=60)
+        from oracle import oracle as orc
+
+        def ofn(arena, txns):
+            return orc.verify_txns(arena, txns, nthreads=8)
+        exp_out, _ = tile_model.verify_tile_model(ps, 0x5EEDF00D, ofn)
+        st = vt.stats()
+        assert vt.log()[1].tolist() == exp_out
+        assert st["verify_errors"] == 0 and st["sigs"] >= 10 * len(ps)
+        vt.close()
+    finally:
+        eng.close()

@@ -54,10 +54,20 @@ static int sign_only(const uint8_t prv[32], const uint8_t *msg, size_t msg_sz, u
   return ok ? 0 : -1;
 }
 
-/* Build one transaction at p (capacity `stride`).  Returns payload size or 0. */
+/* Optional key pool: signers drawn from `cnt` precomputed key pairs
+   (recurring signers, as fee payers and vote authorities are in real
+   traffic; also halves the signing cost of large parity sets). */
+typedef struct {
+  uint64_t cnt;
+  const uint8_t *prv, *pub;   /* cnt x 32 B each */
+} key_pool_t;
+
+/* Build one transaction at p (capacity `stride`).  Returns payload size or 0.
+   corrupt_mode 0: a random one of 1-3; 1 signature bit, 2 message bit,
+   3 public-key bit, 4 a bit of R (the signature's first 32 bytes). */
 static uint32_t build_txn(uint64_t seed, uint64_t idx, int multi, uint32_t msg_lo, uint32_t msg_hi, uint32_t max_sigs,
-                          double corrupt_frac, uint8_t *p, uint32_t stride, fdgen_txn_t *t, uint64_t base_off,
-                          uint8_t *mode_out) {
+                          double corrupt_frac, int corrupt_mode, const key_pool_t *pool, uint8_t *p, uint32_t stride,
+                          fdgen_txn_t *t, uint64_t base_off, uint8_t *mode_out) {
   uint64_t s = seed ^ (idx * 0xd1342543de82ef95ULL);
   splitmix64(&s);
   const uint32_t n = multi ? 1u + rng_below(&s, max_sigs) : 1u;
@@ -84,8 +94,14 @@ static uint32_t build_txn(uint64_t seed, uint64_t idx, int multi, uint32_t msg_l
   msg[o++] = (uint8_t)n; msg[o++] = 0; msg[o++] = 1;
   msg[o++] = (uint8_t)acct;
   for (uint32_t j = 0; j < n; j++) {
-    rng_bytes(&s, prv[j], 32);
-    if (derive_pub(prv[j], msg + o)) return 0;
+    if (pool && pool->cnt) {
+      const uint64_t k = splitmix64(&s) % pool->cnt;
+      memcpy(prv[j], pool->prv + 32 * k, 32);
+      memcpy(msg + o, pool->pub + 32 * k, 32);
+    } else {
+      rng_bytes(&s, prv[j], 32);
+      if (derive_pub(prv[j], msg + o)) return 0;
+    }
     o += 32;
   }
   for (uint32_t j = n; j < acct; j++) {
@@ -117,11 +133,12 @@ sign:
   /* corruption: exactly one bit flip in a signature, the message or a public key */
   uint8_t mode = 0;
   if ((double)(splitmix64(&s) >> 11) * (1.0 / 9007199254740992.0) < corrupt_frac) {
-    mode = (uint8_t)(1 + rng_below(&s, 3));
+    mode = corrupt_mode ? (uint8_t)corrupt_mode : (uint8_t)(1 + rng_below(&s, 3));
     const uint32_t j = rng_below(&s, n);
     if (mode == 1) { uint32_t b = rng_below(&s, 512); sigs[64 * j + b / 8] ^= (uint8_t)(1u << (b & 7)); }
     if (mode == 2) { uint32_t b = rng_below(&s, 8 * msg_sz); msg[b / 8] ^= (uint8_t)(1u << (b & 7)); }
     if (mode == 3) { uint32_t b = rng_below(&s, 256); msg[4 + 32 * j + b / 8] ^= (uint8_t)(1u << (b & 7)); }
+    if (mode == 4) { uint32_t b = rng_below(&s, 256); sigs[64 * j + b / 8] ^= (uint8_t)(1u << (b & 7)); }
   }
   const uint32_t payload = 1 + 64 * n + msg_sz;
   t->sig_cnt = n;
@@ -138,6 +155,8 @@ typedef struct {
   int multi;
   uint32_t msg_lo, msg_hi, max_sigs, stride;
   double corrupt;
+  int corrupt_mode;
+  const key_pool_t *pool;
   uint8_t *arena;
   fdgen_txn_t *txns;
   uint8_t *modes;
@@ -148,8 +167,26 @@ static void *worker(void *a) {
   job_t *j = (job_t *)a;
   for (uint64_t i = j->lo; i < j->hi; i++) {
     uint8_t *p = j->arena + i * (uint64_t)j->stride;
-    if (!build_txn(j->seed, i, j->multi, j->msg_lo, j->msg_hi, j->max_sigs, j->corrupt, p, j->stride, &j->txns[i],
-                   i * (uint64_t)j->stride, j->modes ? &j->modes[i] : NULL)) { j->err = 1; return NULL; }
+    if (!build_txn(j->seed, i, j->multi, j->msg_lo, j->msg_hi, j->max_sigs, j->corrupt, j->corrupt_mode, j->pool, p,
+                   j->stride, &j->txns[i], i * (uint64_t)j->stride, j->modes ? &j->modes[i] : NULL)) {
+      j->err = 1; return NULL;
+    }
+  }
+  return NULL;
+}
+
+typedef struct {
+  uint64_t lo, hi, seed;
+  uint8_t *prv, *pub;
+  int err;
+} pool_job_t;
+
+static void *pool_worker(void *a) {
+  pool_job_t *j = (pool_job_t *)a;
+  for (uint64_t k = j->lo; k < j->hi; k++) {
+    uint64_t s = j->seed ^ (k * 0x9e3779b97f4a7c15ULL) ^ 0x6b65795f706f6f6cULL;
+    rng_bytes(&s, j->prv + 32 * k, 32);
+    if (derive_pub(j->prv + 32 * k, j->pub + 32 * k)) { j->err = 1; return NULL; }
   }
   return NULL;
 }
@@ -158,24 +195,52 @@ static void *worker(void *a) {
    (capacity n*stride).  multi=0: one signature, msg_sz ~ U[msg_lo, msg_hi]
    (cfg1); multi=1: sig_cnt ~ U{1..max_sigs}, payload <= 1232 B (cfg3).
    corrupt_frac of the transactions get one bit flipped (modes[i]: 0 none,
-   1 signature, 2 message, 3 public key).  Returns 0 on success. */
-int fdgen_txns(uint64_t n, uint64_t seed, int multi, uint32_t msg_lo, uint32_t msg_hi, uint32_t max_sigs,
-               double corrupt_frac, uint32_t stride, uint8_t *arena, fdgen_txn_t *txns, uint8_t *modes,
-               int nthreads) {
+   1 signature, 2 message, 3 public key, 4 R; corrupt_mode 0 picks one of
+   1-3 at random, else forces it).  key_pool 0: a fresh key pair per signer;
+   K > 0: signers drawn from K seeded key pairs.  Returns 0 on success. */
+int fdgen_txns_ex(uint64_t n, uint64_t seed, int multi, uint32_t msg_lo, uint32_t msg_hi, uint32_t max_sigs,
+                  double corrupt_frac, int corrupt_mode, uint64_t key_pool, uint32_t stride, uint8_t *arena,
+                  fdgen_txn_t *txns, uint8_t *modes, int nthreads) {
   if (nthreads < 1) nthreads = 1;
   if (nthreads > 128) nthreads = 128;
-  if (max_sigs < 1 || max_sigs > 16 || (!multi && msg_hi < msg_lo)) return -1;
-  memset(arena, 0, n * (uint64_t)stride);
+  if (max_sigs < 1 || max_sigs > 16 || (!multi && msg_hi < msg_lo) || corrupt_mode < 0 || corrupt_mode > 4 ||
+      key_pool > (1ull << 24))
+    return -1;
+  key_pool_t pool = {0, NULL, NULL};
   pthread_t th[128];
+  if (key_pool) {
+    uint8_t *prv = malloc(32 * key_pool), *pub = malloc(32 * key_pool);
+    if (!prv || !pub) { free(prv); free(pub); return -3; }
+    pool_job_t pj[128];
+    int perr = 0;
+    for (int t = 0; t < nthreads; t++) {
+      pj[t] = (pool_job_t){key_pool * (uint64_t)t / (uint64_t)nthreads, key_pool * (uint64_t)(t + 1) / (uint64_t)nthreads,
+                           seed, prv, pub, 0};
+      pthread_create(&th[t], NULL, pool_worker, &pj[t]);
+    }
+    for (int t = 0; t < nthreads; t++) { pthread_join(th[t], NULL); perr |= pj[t].err; }
+    if (perr) { free(prv); free(pub); return -2; }
+    pool = (key_pool_t){key_pool, prv, pub};
+  }
+  memset(arena, 0, n * (uint64_t)stride);
   job_t jobs[128];
   for (int t = 0; t < nthreads; t++) {
     jobs[t] = (job_t){n, seed, n * (uint64_t)t / (uint64_t)nthreads, n * (uint64_t)(t + 1) / (uint64_t)nthreads,
-                      multi, msg_lo, msg_hi, max_sigs, stride, corrupt_frac, arena, txns, modes, 0};
+                      multi, msg_lo, msg_hi, max_sigs, stride, corrupt_frac, corrupt_mode, &pool, arena, txns, modes,
+                      0};
     pthread_create(&th[t], NULL, worker, &jobs[t]);
   }
   int err = 0;
   for (int t = 0; t < nthreads; t++) { pthread_join(th[t], NULL); err |= jobs[t].err; }
+  free((void *)pool.prv); free((void *)pool.pub);
   return err ? -2 : 0;
+}
+
+int fdgen_txns(uint64_t n, uint64_t seed, int multi, uint32_t msg_lo, uint32_t msg_hi, uint32_t max_sigs,
+               double corrupt_frac, uint32_t stride, uint8_t *arena, fdgen_txn_t *txns, uint8_t *modes,
+               int nthreads) {
+  return fdgen_txns_ex(n, seed, multi, msg_lo, msg_hi, max_sigs, corrupt_frac, 0, 0, stride, arena, txns, modes,
+                       nthreads);
 }
 
 /* Plain RFC 8032 keygen + sign of caller-provided messages (test fixtures). */
