@@ -88,6 +88,8 @@ def lib():
     L.fdgpu_dev_batch_free.restype = None
     L.fdgpu_dev_batch_sig_cnt.argtypes = [vp]
     L.fdgpu_dev_batch_sig_cnt.restype = c.c_uint64
+    L.fdgpu_dev_batch_device_ptrs.argtypes = [vp] + [vp] * 6
+    L.fdgpu_dev_batch_device_ptrs.restype = c.c_int
     L.fdgpu_dev_batch_time.argtypes = [vp, vp, c.c_int, c.POINTER(c.c_double), c.POINTER(c.c_double),
                                        c.POINTER(c.c_double)]
     L.fdgpu_dev_batch_time.restype = c.c_int

@@ -464,6 +464,18 @@ extern "C" {
 
 uint64_t fdgpu_dev_batch_sig_cnt(fdgpu_dev_batch_t const *b) { return b ? b->n_sig : 0; }
 
+int fdgpu_dev_batch_device_ptrs(fdgpu_dev_batch_t const *b, void **d_arena, void **d_sig_desc, void **d_perm,
+                                void **d_txn_desc, int8_t **d_sig_codes, int8_t **d_txn_codes) {
+  if (!b) return FDGPU_ERR_INVAL;
+  if (d_arena) *d_arena = b->d_arena;
+  if (d_sig_desc) *d_sig_desc = b->d_sigs;
+  if (d_perm) *d_perm = b->d_perm;
+  if (d_txn_desc) *d_txn_desc = b->d_txns;
+  if (d_sig_codes) *d_sig_codes = b->d_sig_codes;
+  if (d_txn_codes) *d_txn_codes = b->d_txn_codes;
+  return FDGPU_OK;
+}
+
 int fdgpu_dev_batch_own_queue(fdgpu_engine_t *e, fdgpu_dev_batch_t *b) {
   if (!e || !b) return FDGPU_ERR_INVAL;
   if (b->stream) return FDGPU_OK;

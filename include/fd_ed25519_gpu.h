@@ -178,6 +178,15 @@ int  fdgpu_dev_batch_own_queue( fdgpu_engine_t * e, fdgpu_dev_batch_t * b );
 /* wait for the batch's queue and copy the per-txn (and optionally per-signature) codes out */
 int  fdgpu_dev_batch_codes( fdgpu_engine_t * e, fdgpu_dev_batch_t * b, int8_t * txn_codes, int8_t * sig_codes );
 void fdgpu_dev_batch_free( fdgpu_engine_t * e, fdgpu_dev_batch_t * b );
+/* The batch's device buffers, in the layout fdgpu_verify_device takes (any
+   out pointer may be NULL).  *d_perm is NULL unless the engine groups
+   signatures by SHA-512 block count (the default): then descriptor i's code
+   belongs at signature perm[i], and only the engine's own verify
+   (fdgpu_dev_batch_verify) applies it -- pass such descriptors to
+   fdgpu_verify_device only from an engine opened with FDGPU_FLAG_NO_BUCKET. */
+int  fdgpu_dev_batch_device_ptrs( fdgpu_dev_batch_t const * b, void ** d_arena, void ** d_sig_desc,
+                                  void ** d_perm, void ** d_txn_desc, int8_t ** d_sig_codes,
+                                  int8_t ** d_txn_codes );
 uint64_t fdgpu_dev_batch_sig_cnt( fdgpu_dev_batch_t const * b );
 /* Times `iters` back-to-back verifies of the batch on the compute stream
    with HIP events: *wall_ms = first-to-last event span (all launches),

@@ -326,21 +326,27 @@ def test_device_batches_own_queues(engine, oracle):
         b.free()
 
 
-def test_raw_device_pointer_api(engine):
-    """fdgpu_verify_device with caller-owned device buffers (pointers taken
-    from an engine-owned DeviceBatch; no torch involvement)."""
+def test_raw_device_pointer_api():
+    """fdgpu_verify_device with device buffers the caller owns (here: an
+    engine-owned DeviceBatch's, via fdgpu_dev_batch_device_ptrs; no torch
+    involvement).  Descriptors in transaction order (FDGPU_FLAG_NO_BUCKET)."""
     import ctypes
+    import firedancer_amd as fa
+    from firedancer_amd import _lib
     arena, txns, modes = workload.cfg1(2000, seed=78)
-    b = engine.upload(arena, txns)
-    class _DB(ctypes.Structure):
-        _fields_ = [("d_arena", ctypes.c_void_p), ("d_sigs", ctypes.c_void_p), ("d_txns", ctypes.c_void_p),
-                    ("d_sig_codes", ctypes.c_void_p), ("d_txn_codes", ctypes.c_void_p),
-                    ("n_sig", ctypes.c_uint64), ("n_txn", ctypes.c_uint64)]
-    db = _DB.from_address(b._b)
-    engine.verify_device(db.d_arena, db.d_sigs, db.n_sig, db.d_txns, db.n_txn, db.d_sig_codes, db.d_txn_codes, 0)
-    engine.sync()
-    assert ((b.codes() == 0) == (modes == 0)).all()
-    b.free()
+    eng = fa.VerifyEngine(0, max_txn=4096, bucket=False)
+    try:
+        b = eng.upload(arena, txns)
+        p = [ctypes.c_void_p() for _ in range(6)]
+        assert _lib.lib().fdgpu_dev_batch_device_ptrs(b._b, *[ctypes.byref(x) for x in p]) == 0
+        d_arena, d_sigs, d_perm, d_txns, d_sc, d_tc = [x.value for x in p]
+        assert d_perm is None
+        eng.verify_device(d_arena, d_sigs, b.n_sig, d_txns, b.n_txn, d_sc, d_tc, 0)
+        eng.sync()
+        assert ((b.codes() == 0) == (modes == 0)).all()
+        b.free()
+    finally:
+        eng.close()
 
 
 def test_full_size_cfg1_properties(engine, oracle):
