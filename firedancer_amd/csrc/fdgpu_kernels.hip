@@ -24,6 +24,7 @@
 #include "fdgpu_internal.h"
 #include "fdgpu_sc.h"
 #include "fdgpu_sha512.h"
+#include "fdgpu_stamps.h"
 
 using namespace fdgpu;
 
@@ -321,6 +322,7 @@ FDG_DEV int verify_pass1(const uint8_t *arena, const fdgpu_sig_desc_t &sd_in, ui
   {
     uint64_t h[8];
     sha512_hram(h, R, A, arena + sd_in.msg_off, sd_in.msg_sz, nblk_wave);
+    FDGPU_STAMP(1);
     uint32_t kx[16], k[8], kd[KD_WORDS];
 #pragma unroll
     for (int i = 0; i < 8; i++) { kx[2 * i] = bswap32((uint32_t)(h[i] >> 32)); kx[2 * i + 1] = bswap32((uint32_t)h[i]); }
@@ -339,16 +341,19 @@ FDG_DEV int verify_pass1(const uint8_t *arena, const fdgpu_sig_desc_t &sd_in, ui
 #pragma unroll
     for (int i = 0; i < 8; i++) S[i] = code ? 0u : S[i];
     ge_p3 SB;
+    FDGPU_STAMP(2);
     comb_sb(SB, S, btab);
     ge_cached c; ge_p3_to_cached(c, SB);
     atab_store(wsl, FDGPU_WS_SB, c);
   }
+  FDGPU_STAMP(3);
   /* step 2 (A): decode, small order, table of -A */
   bool a_ok, a_small;
   {
     ge_p3 Ap;
     a_ok = ge_decode(Ap, A, ref_map);
     a_small = ge_is_small_order_affine(Ap);
+    FDGPU_STAMP(4);
     ge_p3 An; ge_p3_neg(An, Ap);
     atab_build(wsl, An);
   }
@@ -443,7 +448,9 @@ fdgpu_verify_ra_kernel(const uint8_t *__restrict__ arena, const fdgpu_sig_desc_t
   for (int off = 32; off > 0; off >>= 1) nb = max(nb, (uint32_t)__shfl_xor((int)nb, off));
   uint32_t *wsl = lane_ws(ws, i);
   uint32_t *park = park_ptr(wsl);
+  FDGPU_STAMP(0);
   const int code1 = verify_pass1(arena, d, nb, wsl, btab, (flags & FDGPU_FLAG_REF_MAP) != 0);
+  FDGPU_STAMP(5);
   const bool need = active && code1 == 0;
   ge_p2 Rc;
   if (__any(need)) {
@@ -454,6 +461,7 @@ fdgpu_verify_ra_kernel(const uint8_t *__restrict__ arena, const fdgpu_sig_desc_t
   } else {
     ge_p2_0(Rc);
   }
+  FDGPU_STAMP(6);
   uint32_t Renc[8];
   load32(Renc, arena + d.sig_off);
   fe yR, t;
@@ -491,6 +499,7 @@ fdgpu_verify_ra_kernel(const uint8_t *__restrict__ arena, const fdgpu_sig_desc_t
   o[0] = make_uint4(U.v[0], U.v[1], U.v[2], U.v[3]);
   o[1] = make_uint4(U.v[4], U.v[5], U.v[6], U.v[7]);
   o[2] = make_uint4(U.v[8], U.v[9], fl, 0u);
+  FDGPU_STAMP(7);
 }
 
 /* Inverse of one workgroup's Z product (run by the extra blocks of
@@ -796,6 +805,15 @@ hipError_t fdgpu_launch_combine(const fdgpu_txn_desc_t *d_txns, uint32_t n_txn, 
                      d_sig_codes, d_txn_codes, d_accept);
   return hipGetLastError();
 }
+
+#if FDGPU_PHASE_STAMPS
+/* diagnostic builds: copy out the per-wave phase stamps */
+int fdgpu_debug_stamps(uint64_t *out, uint64_t n_waves) {
+  if (n_waves > FDGPU_STAMP_WAVES) n_waves = FDGPU_STAMP_WAVES;
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_fdgpu_stamps), n_waves * FDGPU_STAMP_SLOTS * sizeof(uint64_t)) ==
+                 hipSuccess ? 0 : -1;
+}
+#endif
 
 hipError_t fdgpu_launch_test_fe(const uint32_t *d_in, uint32_t *d_out, uint32_t n, hipStream_t stream) {
   hipLaunchKernelGGL(fdgpu_test_fe_kernel, dim3((n + 63) / 64), dim3(64), 0, stream, d_in, d_out, n);

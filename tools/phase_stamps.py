@@ -1,0 +1,65 @@
+"""Per-phase cycle breakdown of fdgpu_verify_ra_kernel (diagnostic build).
+
+    bash tools/build_variant.sh stamps -DFDGPU_PHASE_STAMPS=1
+    FDGPU_LIB=build/stamps/libfd_ed25519_gpu.so python tools/phase_stamps.py [--txns N] [--out f.json]
+
+Lane 0 of every wave stamps the shader clock at the phase boundaries of
+fdgpu_kernels.hip (FDGPU_STAMP 0..7, fdgpu_stamps.h).  Reported: the mean
+cycles each wave spends per phase (two waves share a SIMD, so a phase's
+cycles include the time the partner wave held the VALU), the share of the
+wave's lifetime, and the kernel's HIP-event time.
+"""
+import argparse
+import ctypes
+import json
+import os
+import sys
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+
+PHASES = ["sha512 + loads", "mod L + recode + S check", "comb [S]B", "decode A + small order",
+          "A table", "dsm_k ([k](-A) + [S]B)", "y check + Z scan + park"]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--txns", type=int, default=1_000_000)
+    ap.add_argument("--out", default=None)
+    args = ap.parse_args()
+    import firedancer_amd as fa
+    from firedancer_amd import _lib, workload
+    L = _lib.lib()
+    if not hasattr(L, "fdgpu_debug_stamps"):
+        raise SystemExit("not a stamps build: set FDGPU_LIB=build/stamps/libfd_ed25519_gpu.so")
+    L.fdgpu_debug_stamps.argtypes = [ctypes.c_void_p, ctypes.c_uint64]
+    arena, txns, modes = workload.cfg1(args.txns)
+    eng = fa.VerifyEngine(0, max_txn=4096)
+    b = eng.upload(arena, txns)
+    b.verify()
+    _, kv, kc = b.time(2)                       # the last of these verifies leaves its stamps
+    n_waves = (b.n_sig + 63) // 64
+    st = np.zeros(n_waves * 8, dtype=np.uint64)
+    assert L.fdgpu_debug_stamps(st.ctypes.data, n_waves) == 0
+    st = st.reshape(n_waves, 8).astype(np.int64)
+    d = np.diff(st, axis=1)
+    ok = (d >= 0).all(axis=1)
+    d = d[ok]
+    life = (st[ok, 7] - st[ok, 0])
+    out = {"waves": int(n_waves), "waves_used": int(ok.sum()), "verify_ms": round(kv, 3),
+           "wave_life_cycles_mean": round(float(life.mean()), 1),
+           "phases": {p: {"cycles_mean": round(float(d[:, i].mean()), 1),
+                          "share": round(float(d[:, i].mean() / life.mean()), 4)} for i, p in enumerate(PHASES)},
+           "note": "cycles per wave between FDGPU_STAMP boundaries (s_memtime, shader clock); 2 waves share a SIMD"}
+    b.free()
+    eng.close()
+    js = json.dumps(out, indent=1)
+    print(js)
+    if args.out:
+        open(args.out, "w").write(js + "\n")
+
+
+if __name__ == "__main__":
+    main()
