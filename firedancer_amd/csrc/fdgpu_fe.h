@@ -3,7 +3,7 @@
    weight 2^(25 i + ceil(i/2)) (widths 26,25,26,...,25; 255 bits in all).
 
    Why this representation (tools/ubench_int.hip, tools/ubench_fe.hip, run on
-   MI355X, profiles/r01_ubench.md): every 32-bit integer multiply form on
+   MI355X, profiles/r01_ubench_int.jsonl and r01_ubench_fe.jsonl): every 32-bit integer multiply form on
    gfx950 issues at half rate (~61 lane-ops/CU/clk) and so do VOP3 adds with
    a carry-out, while plain v_add_u32/v_mov_b32 issue at full rate.  Radix
    2^25.5 needs no carries inside a product (64-bit column sums), makes

@@ -38,10 +38,24 @@ typedef struct {
 #define FDGPU_BCOMB_ENTRIES ((1u << (FDGPU_BCOMB_BITS - 1u)) + 1u)
 #define FDGPU_BCOMB_STRIDE  32u           /* u32 per entry (30 used): one 128-B line */
 #define FDGPU_BCOMB_CHUNK   64u           /* entries per lane in the table build (one batch inversion) */
+/* FDGPU_HALFSIZE=1 (default): the verify equation with half-size scalars
+   (fdgpu_lattice.h); 0: the full-length chain with R compared on its
+   encoding (R-avoiding path). */
+#ifndef FDGPU_HALFSIZE
+#define FDGPU_HALFSIZE 1
+#endif
+#define HS_MAX_WIN          34u           /* radix-16 windows of |u|, |v| (< 2^135) */
+#if FDGPU_HALFSIZE
+#define FDGPU_WS_RTAB       FDGPU_ATAB_ENTRIES          /* entries 9..17: the -R table */
+#define FDGPU_WS_PARK       (2u * FDGPU_ATAB_ENTRIES)   /* entry: k digits, decoded R, code (full path) */
+#define FDGPU_WS_SB         (FDGPU_WS_PARK + 1u)        /* entry: [w]B (or [S]B) in cached form */
+#define FDGPU_WS_ENTRIES    (FDGPU_WS_SB + 1u)          /* 20 entries: 3200 B per signature */
+#else
 #define FDGPU_WS_PARK       FDGPU_ATAB_ENTRIES          /* entry: digits, code, R' (slow path) */
 #define FDGPU_WS_SB         (FDGPU_ATAB_ENTRIES + 1u)   /* entry: [S]B in cached form, then U + flags */
-#define FDGPU_WS_ENTRIES    (FDGPU_ATAB_ENTRIES + 2u)   /* per-lane workspace: A table, park, [S]B */
-#define FDGPU_WS_LANE_WORDS (FDGPU_WS_ENTRIES * FDGPU_ATAB_WORDS)   /* 1760 B per signature */
+#define FDGPU_WS_ENTRIES    (FDGPU_ATAB_ENTRIES + 2u)   /* per-lane workspace: A table, park, [S]B: 1760 B */
+#endif
+#define FDGPU_WS_LANE_WORDS (FDGPU_WS_ENTRIES * FDGPU_ATAB_WORDS)
 #define FDGPU_BLOCK         256u
 #define FDGPU_FLAG_REF_MAP  1u            /* portable-backend error mapping */
 /* SHA-512 block-count groups of the host-side bucketing (expand): messages of

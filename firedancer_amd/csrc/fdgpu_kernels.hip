@@ -24,6 +24,7 @@
 #include "fdgpu_internal.h"
 #include "fdgpu_sc.h"
 #include "fdgpu_sha512.h"
+#include "fdgpu_lattice.h"
 #include "fdgpu_stamps.h"
 
 using namespace fdgpu;
@@ -171,7 +172,7 @@ FDG_DEV void shl4(uint32_t (&w)[8]) {
    comb in pass 1 and parked (cached form) in workspace entry 10.  The chain
    only serves k: 64 windows of 4 doublings + one A-table addition; the last
    window's sum is converted to p3 and the parked [S]B added. */
-FDG_DEV void dsm_k(ge_p2 &acc2, uint32_t (&kd)[KD_WORDS], const uint32_t *wsl) {
+FDG_DEV void dsm_k(ge_p2 &acc2, uint32_t (&kd)[KD_WORDS], const uint32_t *wsl, uint32_t sb_entry = FDGPU_WS_SB) {
   ge_p3 acc3;
   ge_p1p1 t;
   uint32_t q[40];
@@ -201,7 +202,7 @@ FDG_DEV void dsm_k(ge_p2 &acc2, uint32_t (&kd)[KD_WORDS], const uint32_t *wsl) {
   /* + [S]B (parked cached form) */
   ge_p1p1_to_p3(acc3, t);
   uint32_t qs[40];
-  atab_load(qs, wsl, FDGPU_WS_SB);
+  atab_load(qs, wsl, (int)sb_entry);
   ge_add_cached_regs(t, acc3, qs, false);
   ge_p1p1_to_p2(acc2, t);
 }
@@ -606,6 +607,293 @@ __global__ void __launch_bounds__(FDGPU_BLOCK, FDGPU_VERIFY_WAVES) fdgpu_tail_ke
   }
 }
 
+/* ---------------- half-size verify (FDGPU_HALFSIZE) ----------------
+   fdgpu_lattice.h: with u = v k (mod 8L), v odd and |u|, |v| < 2^135,
+   [S]B - [k]A == R  <=>  [w]B - [u]A - [v]R == O  (w = v S mod L), decided
+   with ~132 doublings instead of ~252.  Per lane:
+     pass 1   S < L, k = SHA-512(R||A||M) mod L, decode A and R (the
+              reference's decode2, both codes settled here in the
+              reference's order), the tables {O, -A, .., -8A} and
+              {O, -R, .., -8R};
+     split    (u, v) = hs_split(k);  w = v S mod L;  [w]B by the comb;
+     chain    [|u|](+-A table) + [|v|](+-R table) over the wave's longest
+              digit string (signed radix 16: 4 doublings + 2 additions per
+              window, every lane at the same positions);
+     check    chain == -[w]B, projectively (4 products).
+   A lane whose split fails (hs_split_t.ok == false) keeps k's digits and
+   [S]B and is finished by fdgpu_full_kernel with the full-length chain. */
+
+/* park words (entry FDGPU_WS_PARK) */
+#define HPARK_KD 0        /* 8 words: radix-16 digits of k (full-path lanes) */
+#define HPARK_XR 10       /* decoded R, affine x (10 words) */
+#define HPARK_YR 20       /* and y */
+#define HPARK_CODE 30     /* pass-1 code */
+static_assert(HPARK_KD + KD_WORDS <= HPARK_XR && HPARK_CODE < (int)FDGPU_ATAB_WORDS, "park layout");
+
+/* Signed radix-16 digits of a magnitude m < 2^160 (5 limbs): 40 nibbles in
+   [-8, 7] (two's complement, digit i at bits 4(i%8) of word i/8); nd = the
+   number of digits up to the highest nonzero one (41 if a carry is left). */
+FDG_DEV void recode16_160(uint32_t (&out)[5], uint32_t &nd, const uint32_t (&m)[5]) {
+  uint32_t carry = 0;
+  nd = 0;
+#pragma unroll
+  for (int w = 0; w < 5; w++) {
+    uint32_t o = 0;
+#pragma unroll
+    for (int n = 0; n < 8; n++) {
+      uint32_t e = ((m[w] >> (4 * n)) & 15u) + carry;
+      carry = e >= 8u;
+      e = (e - (carry << 4)) & 15u;
+      o |= e << (4 * n);
+      nd = e ? (uint32_t)(8 * w + n + 1) : nd;
+    }
+    out[w] = o;
+  }
+  nd = carry ? 41u : nd;
+}
+
+FDG_DEV void shl4_5(uint32_t (&w)[5]) {
+#pragma unroll
+  for (int i = 4; i > 0; i--) w[i] = (w[i] << 4) | (w[i - 1] >> 28);
+  w[0] <<= 4;
+}
+
+/* w = v S mod L for |v| < 2^160 (5 limbs), S < L (8 limbs); negated mod L
+   when v < 0 */
+FDG_DEV void hs_wscalar(uint32_t (&w)[8], const uint32_t (&v)[5], bool v_neg, const uint32_t (&S)[8]) {
+  uint32_t x[16];
+#pragma unroll
+  for (int i = 0; i < 16; i++) x[i] = 0;
+#pragma unroll
+  for (int i = 0; i < 5; i++) {
+    uint64_t c = 0;
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+      const uint64_t t = (uint64_t)v[i] * S[j] + x[i + j] + c;
+      x[i + j] = (uint32_t)t;
+      c = t >> 32;
+    }
+    x[i + 8] = (uint32_t)c;
+  }
+  uint32_t r[8];
+  sc_reduce512(r, x);
+  constexpr uint32_t L[8] = FDGPU_SC_L;
+  uint32_t nz = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) nz |= r[i];
+  const bool flip = v_neg && nz != 0;
+  uint32_t bw = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) {                 /* L - r */
+    const uint64_t d = (uint64_t)L[i] - r[i] - bw;
+    w[i] = flip ? (uint32_t)d : r[i];
+    bw = (uint32_t)(d >> 63);
+  }
+}
+
+/* [|u|](T_A) + [|v|](T_R), digit strings pre-shifted so that digit nwin-1
+   sits in the top nibble; u_neg / v_neg flip every digit's sign (the tables
+   hold -A, -R).  Leaves the completed sum of the last addition in t. */
+FDG_DEV void hs_chain(ge_p1p1 &t, uint32_t (&ud)[5], uint32_t (&vd)[5], bool u_neg, bool v_neg, uint32_t nwin,
+                      const uint32_t *wsl) {
+  const uint32_t *ta = wsl, *tr = wsl + FDGPU_WS_RTAB * FDGPU_ATAB_WORDS;
+  ge_p2 acc2;
+  ge_p3 acc3;
+  uint32_t qa[40], qr[40];
+  {                                             /* top window: O + T_A[du] + T_R[dv] */
+    const int du = sext4(ud[4] >> 28), dv = sext4(vd[4] >> 28);
+    shl4_5(ud); shl4_5(vd);
+    atab_load(qa, ta, du);
+    atab_load(qr, tr, dv);
+    /* the entry as a p3 point needs T = XY/Z (its 2dT would need 1/d): add
+       it to the identity instead */
+    ge_p3_0(acc3);
+    ge_add_cached_regs(t, acc3, qa, (du < 0) != u_neg);
+    ge_p1p1_to_p3(acc3, t);
+    ge_add_cached_regs(t, acc3, qr, (dv < 0) != v_neg);
+  }
+#pragma unroll 1
+  for (uint32_t j = 1; j < nwin; j++) {
+    ge_p1p1_to_p2(acc2, t);
+    const int du = sext4(ud[4] >> 28), dv = sext4(vd[4] >> 28);
+    shl4_5(ud); shl4_5(vd);
+    atab_load(qa, ta, du);                     /* both entries land behind the doublings */
+    atab_load(qr, tr, dv);
+#pragma unroll 1
+    for (int r = 0; r < 4; r++) {
+      ge_dbl(t, acc2);
+      ge_p1p1_to_p2(acc2, t);
+    }
+    acc3.X = acc2.X; acc3.Y = acc2.Y; acc3.Z = acc2.Z; fe_mul(acc3.T, t.X, t.Y);
+    ge_add_cached_regs(t, acc3, qa, (du < 0) != u_neg);
+    ge_p1p1_to_p3(acc3, t);
+    ge_add_cached_regs(t, acc3, qr, (dv < 0) != v_neg);
+  }
+}
+
+/* The verify kernel of the half-size path; codes of lanes it settles are
+   written here, lanes whose split failed are queued for fdgpu_full_kernel. */
+__global__ void __launch_bounds__(FDGPU_BLOCK, FDGPU_VERIFY_WAVES)
+fdgpu_verify_hs_kernel(const uint8_t *__restrict__ arena, const fdgpu_sig_desc_t *__restrict__ sigs, uint32_t n_sig,
+                       const uint32_t *__restrict__ btab, uint32_t *__restrict__ ws, const uint32_t *__restrict__ perm,
+                       int8_t *__restrict__ codes, uint32_t *__restrict__ queue, uint32_t *__restrict__ queue_cnt,
+                       uint32_t flags) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  const bool active = i < n_sig;
+  const bool ref_map = (flags & FDGPU_FLAG_REF_MAP) != 0;
+  const fdgpu_sig_desc_t d = sigs[active ? i : n_sig - 1];
+  uint32_t nb = sha512_hram_blocks(d.msg_sz);
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) nb = max(nb, (uint32_t)__shfl_xor((int)nb, off));
+  uint32_t *wsl = lane_ws(ws, i);
+  uint32_t *park = wsl + FDGPU_WS_PARK * FDGPU_ATAB_WORDS;
+  FDGPU_STAMP(0);
+  uint32_t Renc[8], Aenc[8];
+  load32(Renc, arena + d.sig_off);
+  load32(Aenc, arena + d.pub_off);
+  /* k = SHA-512(R || A || M) mod L */
+  uint32_t k[8];
+  {
+    uint64_t h[8];
+    sha512_hram(h, Renc, Aenc, arena + d.msg_off, d.msg_sz, nb);
+    FDGPU_STAMP(1);
+    uint32_t kx[16];
+#pragma unroll
+    for (int j = 0; j < 8; j++) { kx[2 * j] = bswap32((uint32_t)(h[j] >> 32)); kx[2 * j + 1] = bswap32((uint32_t)h[j]); }
+    sc_reduce512(k, kx);
+  }
+  /* step 1: S < L (fd_ed25519_user.c:159-161) */
+  uint32_t S[8];
+  load32(S, arena + d.sig_off + 32);
+  int code = sc_lt_L(S) ? 0 : -1;
+#pragma unroll
+  for (int j = 0; j < 8; j++) S[j] = code ? 0u : S[j];
+  FDGPU_STAMP(2);
+  /* step 2: decode A then R (decode2 reports A first), small-order tests,
+     tables of -A and -R */
+  {
+    ge_p3 P, Pn;
+    const bool a_ok = ge_decode(P, Aenc, ref_map);
+    const bool a_small = ge_is_small_order_affine(P);
+    ge_p3_neg(Pn, P);
+    atab_build(wsl, Pn);
+    FDGPU_STAMP(3);
+    const bool r_ok = ge_decode(P, Renc, ref_map);
+    const bool r_small = ge_is_small_order_affine(P);
+#pragma unroll
+    for (int j = 0; j < 10; j++) { park[HPARK_XR + j] = P.X.v[j]; park[HPARK_YR + j] = P.Y.v[j]; }
+    ge_p3_neg(Pn, P);
+    atab_build(wsl + FDGPU_WS_RTAB * FDGPU_ATAB_WORDS, Pn);
+    if (code == 0 && !a_ok) code = ref_map ? -2 : -1;
+    if (code == 0 && !r_ok) code = -1;
+    if (code == 0 && a_small) code = -2;                 /* fd_ed25519_user.c:194-199 */
+    if (code == 0 && r_small) code = -1;
+  }
+  FDGPU_STAMP(4);
+  const bool need = active && code == 0;
+  /* split k (lanes already failed run no Euclid steps: k = 0) */
+  hs_split_t hs;
+  {
+    uint32_t ke[8];
+#pragma unroll
+    for (int j = 0; j < 8; j++) ke[j] = need ? k[j] : 0u;
+    hs_split(hs, ke);
+  }
+  uint32_t ud[5], vd[5], ndu = 0, ndv = 0;
+  recode16_160(ud, ndu, hs.u);
+  recode16_160(vd, ndv, hs.v);
+  const uint32_t nd_lane = max(max(ndu, ndv), 1u);
+  const bool full = need && (!hs.ok || nd_lane > HS_MAX_WIN);
+  const bool half = need && !full;
+  FDGPU_STAMP(5);
+  /* [w]B (w = v S mod L), or [S]B for the full-length path; parked cached */
+  {
+    uint32_t w[8];
+    hs_wscalar(w, hs.v, hs.v_neg, S);
+#pragma unroll
+    for (int j = 0; j < 8; j++) w[j] = half ? w[j] : S[j];
+    ge_p3 WB;
+    comb_sb(WB, w, btab);
+    ge_cached c; ge_p3_to_cached(c, WB);
+    atab_store(wsl, FDGPU_WS_SB, c);
+  }
+  if (full) {
+    uint32_t kd[KD_WORDS];
+    sc_recode16(kd, k);
+#pragma unroll
+    for (int j = 0; j < KD_WORDS; j++) park[HPARK_KD + j] = kd[j];
+    park[HPARK_CODE] = 0u;
+  }
+  FDGPU_STAMP(6);
+  bool eq = false;
+  if (__any(half)) {
+    /* the wave's digit count; every lane runs it (shorter strings lead with zeros) */
+    uint32_t nwin = half ? nd_lane : 1u;
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) nwin = max(nwin, (uint32_t)__shfl_xor((int)nwin, off));
+#pragma unroll 1
+    for (uint32_t s = nwin; s < 40; s++) { shl4_5(ud); shl4_5(vd); }
+    ge_p1p1 t;
+    hs_chain(t, ud, vd, hs.u_neg, hs.v_neg, nwin, wsl);
+    /* chain == -[w]B:  x = X/Z = -(YpX - YmX)/Z2,  y = Y/T = (YpX + YmX)/Z2 */
+    uint32_t q[40];
+    atab_load(q, wsl, (int)FDGPU_WS_SB);
+    fe ypx, ymx, z2, xw, yw, l1, l2;
+#pragma unroll
+    for (int j = 0; j < 10; j++) { ypx.v[j] = q[j]; ymx.v[j] = q[10 + j]; z2.v[j] = q[20 + j]; }
+    fe_sub(xw, ypx, ymx);
+    fe_add(yw, ypx, ymx);
+    fe_mul(l1, t.X, z2);
+    fe_mul(l2, t.Z, xw);
+    fe_add(l1, l1, l2);
+    const bool ex = fe_iszero(l1);
+    fe_mul(l1, t.Y, z2);
+    fe_mul(l2, t.T, yw);
+    fe_sub(l1, l1, l2);
+    eq = ex && fe_iszero(l1);
+  }
+  FDGPU_STAMP(7);
+  if (active && !full) codes[out_idx(perm, i)] = (int8_t)(code ? code : (eq ? 0 : -3));
+  {                                             /* queue the full-length lanes (rare) */
+    const uint64_t m = __ballot(full);
+    if (m) {
+      const int lane = (int)(threadIdx.x & 63u);
+      const int leader = __ffsll((long long)m) - 1;
+      uint32_t base = 0;
+      if (lane == leader) base = atomicAdd(queue_cnt, (uint32_t)__popcll(m));
+      base = (uint32_t)__shfl((int)base, leader, 64);
+      if (full) queue[base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull))] = i;
+    }
+  }
+}
+
+/* The queued lanes of fdgpu_verify_hs_kernel: [S]B + [k](-A) with k's 64
+   windows (dsm_k), compared with the decoded R (affine, parked). */
+__global__ void __launch_bounds__(FDGPU_BLOCK, FDGPU_VERIFY_WAVES)
+fdgpu_full_kernel(uint32_t *__restrict__ ws, const uint32_t *__restrict__ perm, int8_t *__restrict__ codes,
+                  const uint32_t *__restrict__ queue, const uint32_t *__restrict__ queue_cnt, uint32_t slots) {
+  const uint32_t cnt = *queue_cnt;
+  if (blockIdx.x * blockDim.x >= cnt) return;
+  for (uint32_t q = blockIdx.x * blockDim.x + threadIdx.x; q < cnt; q += slots) {
+    const uint32_t i = queue[q];
+    uint32_t *wsl = ws + (size_t)i * FDGPU_WS_LANE_WORDS;
+    const uint32_t *park = wsl + FDGPU_WS_PARK * FDGPU_ATAB_WORDS;
+    uint32_t kd[KD_WORDS];
+#pragma unroll
+    for (int j = 0; j < KD_WORDS; j++) kd[j] = park[HPARK_KD + j];
+    ge_p2 Rc;
+    dsm_k(Rc, kd, wsl, FDGPU_WS_SB);
+    fe x, y, l;
+#pragma unroll
+    for (int j = 0; j < 10; j++) { x.v[j] = park[HPARK_XR + j]; y.v[j] = park[HPARK_YR + j]; }
+    fe_mul(l, x, Rc.Z);
+    bool eq = fe_eq(Rc.X, l);
+    fe_mul(l, y, Rc.Z);
+    eq = eq && fe_eq(Rc.Y, l);
+    codes[out_idx(perm, i)] = (int8_t)(eq ? 0 : -3);
+  }
+}
+
 /* Per transaction: fd_ed25519_verify_batch_single_msg's first-error order
    (fd_ed25519_user.c:232-310) over its signatures' codes, plus the batch's
    accept/reject results compacted by wavefront ballot: bit t of accept[]
@@ -755,7 +1043,11 @@ hipError_t fdgpu_btab_build(uint32_t *d_btab, hipStream_t stream) {
 }
 
 hipError_t fdgpu_verify_occupancy(int *blocks_per_cu) {
+#if FDGPU_HALFSIZE
+  return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, fdgpu_verify_hs_kernel, FDGPU_BLOCK, 0);
+#else
   return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, fdgpu_verify_ra_kernel, FDGPU_BLOCK, 0);
+#endif
 }
 
 /* workspace: per-lane words, then per-workgroup Z products and their
@@ -775,11 +1067,9 @@ hipError_t fdgpu_launch_verify_sigs(const uint8_t *d_arena, const fdgpu_sig_desc
   uint32_t *queue = wg_inv + 10 * (size_t)grid, *cnt = queue + lanes;
   hipError_t e = hipMemsetAsync(cnt, 0, sizeof(uint32_t), stream);
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(fdgpu_verify_ra_kernel, dim3(grid), dim3(FDGPU_BLOCK), 0, stream, d_arena, d_sigs, n_sig, d_btab,
-                     d_ws, wg_tot, queue, cnt, flags);
-  /* slow path: as many blocks as the batch's grid could keep resident (all of
-     them, up to every wave slot of the GPU), each exiting at once when the
-     queue holds nothing for it; one block per 256 workgroup inversions */
+  /* the queued (slow / full-length) lanes get as many blocks as the batch's
+     grid could keep resident (all of them, up to every wave slot of the
+     GPU), each exiting at once when the queue holds nothing for it */
   static int resident = 0;
   if (!resident) {
     int bpcu = 0, dev = 0, cus = 0;
@@ -790,6 +1080,16 @@ hipError_t fdgpu_launch_verify_sigs(const uint8_t *d_arena, const fdgpu_sig_desc
     resident = bpcu * cus;
   }
   const uint32_t slow_blocks = grid < (uint32_t)resident ? grid : (uint32_t)resident;
+#if FDGPU_HALFSIZE
+  (void)wg_tot; (void)wg_inv;
+  hipLaunchKernelGGL(fdgpu_verify_hs_kernel, dim3(grid), dim3(FDGPU_BLOCK), 0, stream, d_arena, d_sigs, n_sig, d_btab,
+                     d_ws, d_perm, d_sig_codes, queue, cnt, flags);
+  hipLaunchKernelGGL(fdgpu_full_kernel, dim3(slow_blocks), dim3(FDGPU_BLOCK), 0, stream, d_ws, d_perm, d_sig_codes,
+                     queue, cnt, slow_blocks * FDGPU_BLOCK);
+  return hipGetLastError();
+#endif
+  hipLaunchKernelGGL(fdgpu_verify_ra_kernel, dim3(grid), dim3(FDGPU_BLOCK), 0, stream, d_arena, d_sigs, n_sig, d_btab,
+                     d_ws, wg_tot, queue, cnt, flags);
   const uint32_t inv_blocks = (grid + FDGPU_BLOCK - 1) / FDGPU_BLOCK;
   hipLaunchKernelGGL(fdgpu_tail_kernel, dim3(slow_blocks + inv_blocks), dim3(FDGPU_BLOCK), 0, stream, d_arena,
                      d_sigs, d_ws, d_perm, d_sig_codes, queue, cnt, wg_tot, wg_inv, grid, slow_blocks, flags);

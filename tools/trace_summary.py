@@ -21,14 +21,19 @@ import os
 import sys
 
 PIPE = ("fdgpu_verify_ra_kernel", "fdgpu_tail_kernel", "fdgpu_finish_kernel", "fdgpu_combine_kernel")
+PIPE_HS = ("fdgpu_verify_hs_kernel", "fdgpu_full_kernel", "fdgpu_combine_kernel")
 
 
 def load(trace_dir):
+    global PIPE
     f = glob.glob(os.path.join(trace_dir, "**", "*kernel_trace.csv"), recursive=True)
     if not f:
         raise SystemExit(f"no kernel_trace.csv under {trace_dir}")
     rows = []
-    for r in csv.DictReader(open(f[0])):
+    recs = list(csv.DictReader(open(f[0])))
+    if any(PIPE_HS[0] in r["Kernel_Name"] for r in recs):
+        PIPE = PIPE_HS
+    for r in recs:
         name = next((k for k in PIPE if k in r["Kernel_Name"]), None)
         if name:
             rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), name,
@@ -44,6 +49,7 @@ def main():
     rows = load(trace_dir)
     ra = [r for r in rows if r[2] == PIPE[0]]
     per = {k: [(e - s) / 1e6 for s, e, n, _ in rows if n == k] for k in PIPE}
+    last = PIPE[-1]
     # group each verify_ra launch with the tail/finish/combine that follow it
     # on the same queue
     pipes = []
@@ -51,12 +57,15 @@ def main():
         end = e
         for s2, e2, n2, q2 in rows:
             if q2 == q and s2 >= s and n2 != PIPE[0] and s2 < s + 60e6:
-                if n2 == PIPE[3]:
+                if n2 == last:
                     end = max(end, e2)
                     break
                 end = max(end, e2)
         pipes.append((s, end, q))
-    timed = pipes[-steps:]
+    # bench.py: max(warmup, queues) warm-up verifies, the `steps` timed ones,
+    # then batch.time()'s max(3, min(steps, 10)) single-stream launches
+    w = max(int(bench["warmup"]), int(bench["config"].get("queues") or 1))
+    timed = pipes[w:w + steps]
     span = (max(e for _, e, _ in timed) - min(s for s, _, _ in timed)) / 1e6
     busy = 0.0
     ev = sorted([(s, 1) for s, _, _ in timed] + [(e, -1) for _, e, _ in timed])
@@ -76,8 +85,9 @@ def main():
         "kernel_calls": {k: len(v) for k, v in per.items()},
         "span_ms": round(span, 3), "gpu_busy_ms": round(busy, 3), "two_pipelines_concurrent_ms": round(conc, 3),
         "queues_seen": sorted({q for _, _, q in timed}),
-        "note": "trace_ms_per_step = span of the last `steps` verify pipelines / steps; pipeline_ms_mean = one "
-                "step's verify_ra start to combine end (overlapping its neighbours when queues > 1)",
+        "note": "trace_ms_per_step = span of the timed region's `steps` verify pipelines (after the warm-up ones) / "
+                "steps; pipeline_ms_mean = one step's verify start to combine end (overlapping its neighbours when "
+                "queues > 1); kernel_ms_mean covers every launch in the trace",
     }
     js = json.dumps(out, indent=1)
     print(js)
