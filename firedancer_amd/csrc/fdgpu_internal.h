@@ -42,7 +42,7 @@ typedef struct {
    (fdgpu_lattice.h); 0: the full-length chain with R compared on its
    encoding (R-avoiding path). */
 #ifndef FDGPU_HALFSIZE
-#define FDGPU_HALFSIZE 1
+#define FDGPU_HALFSIZE 0
 #endif
 #define HS_MAX_WIN          34u           /* radix-16 windows of |u|, |v| (< 2^135) */
 #if FDGPU_HALFSIZE

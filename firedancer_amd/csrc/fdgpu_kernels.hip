@@ -691,43 +691,85 @@ FDG_DEV void hs_wscalar(uint32_t (&w)[8], const uint32_t (&v)[5], bool v_neg, co
   }
 }
 
+/* Table entries of the chain are staged through LDS by LDS-DMA
+   (global_load_lds_dwordx4: no VGPR destination), issued at the start of a
+   window and read back after its doublings, so no 40-word entry stays live
+   in VGPRs across the doublings.  One wave-instruction moves 16 B for each
+   of the 64 lanes into 1 KiB of LDS (wave-uniform base + 16 B x lane).
+   HS_STAGE 1: the R entry through LDS, the A entry in VGPRs (prefetched);
+   2: both through LDS (20 KiB per wave). */
+#ifndef HS_STAGE
+#define HS_STAGE 2
+#endif
+typedef __attribute__((address_space(3))) void lds_void_t;
+
+FDG_DEV void stage_entry(uint32_t *lds_wave, const uint32_t *tab, int e) {
+  const uint32_t *src = tab + (uint32_t)(e < 0 ? -e : e) * FDGPU_ATAB_WORDS;
+#pragma unroll
+  for (int c = 0; c < 10; c++)
+    __builtin_amdgcn_global_load_lds((const void *)(src + 4 * c), (lds_void_t *)(lds_wave + 256 * c), 16, 0, 0);
+}
+
+FDG_DEV void unstage_entry(uint32_t (&q)[40], const uint32_t *lds_wave) {
+  const uint32_t lane = threadIdx.x & 63u;
+#pragma unroll
+  for (int c = 0; c < 10; c++) {
+    const uint4 v = *(const uint4 *)(lds_wave + 256 * c + 4 * lane);
+    q[4 * c] = v.x; q[4 * c + 1] = v.y; q[4 * c + 2] = v.z; q[4 * c + 3] = v.w;
+  }
+}
+
 /* [|u|](T_A) + [|v|](T_R), digit strings pre-shifted so that digit nwin-1
    sits in the top nibble; u_neg / v_neg flip every digit's sign (the tables
    hold -A, -R).  Leaves the completed sum of the last addition in t. */
 FDG_DEV void hs_chain(ge_p1p1 &t, uint32_t (&ud)[5], uint32_t (&vd)[5], bool u_neg, bool v_neg, uint32_t nwin,
                       const uint32_t *wsl) {
   const uint32_t *ta = wsl, *tr = wsl + FDGPU_WS_RTAB * FDGPU_ATAB_WORDS;
+  __shared__ uint32_t s_stage[FDGPU_BLOCK / 64][HS_STAGE][10 * 256];
+  uint32_t *st_r = &s_stage[threadIdx.x >> 6][0][0];
+#if HS_STAGE == 2
+  uint32_t *st_a = &s_stage[threadIdx.x >> 6][1][0];
+#endif
   ge_p2 acc2;
   ge_p3 acc3;
-  uint32_t qa[40], qr[40];
+  uint32_t q[40];
   {                                             /* top window: O + T_A[du] + T_R[dv] */
     const int du = sext4(ud[4] >> 28), dv = sext4(vd[4] >> 28);
     shl4_5(ud); shl4_5(vd);
-    atab_load(qa, ta, du);
-    atab_load(qr, tr, dv);
     /* the entry as a p3 point needs T = XY/Z (its 2dT would need 1/d): add
        it to the identity instead */
+    atab_load(q, ta, du);
     ge_p3_0(acc3);
-    ge_add_cached_regs(t, acc3, qa, (du < 0) != u_neg);
+    ge_add_cached_regs(t, acc3, q, (du < 0) != u_neg);
     ge_p1p1_to_p3(acc3, t);
-    ge_add_cached_regs(t, acc3, qr, (dv < 0) != v_neg);
+    atab_load(q, tr, dv);
+    ge_add_cached_regs(t, acc3, q, (dv < 0) != v_neg);
   }
 #pragma unroll 1
   for (uint32_t j = 1; j < nwin; j++) {
     ge_p1p1_to_p2(acc2, t);
     const int du = sext4(ud[4] >> 28), dv = sext4(vd[4] >> 28);
     shl4_5(ud); shl4_5(vd);
-    atab_load(qa, ta, du);                     /* both entries land behind the doublings */
-    atab_load(qr, tr, dv);
+#if HS_STAGE == 2
+    stage_entry(st_a, ta, du);
+#else
+    atab_load(q, ta, du);
+#endif
+    stage_entry(st_r, tr, dv);
 #pragma unroll 1
     for (int r = 0; r < 4; r++) {
       ge_dbl(t, acc2);
       ge_p1p1_to_p2(acc2, t);
     }
     acc3.X = acc2.X; acc3.Y = acc2.Y; acc3.Z = acc2.Z; fe_mul(acc3.T, t.X, t.Y);
-    ge_add_cached_regs(t, acc3, qa, (du < 0) != u_neg);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   /* the window's LDS-DMA has landed */
+#if HS_STAGE == 2
+    unstage_entry(q, st_a);
+#endif
+    ge_add_cached_regs(t, acc3, q, (du < 0) != u_neg);
     ge_p1p1_to_p3(acc3, t);
-    ge_add_cached_regs(t, acc3, qr, (dv < 0) != v_neg);
+    unstage_entry(q, st_r);
+    ge_add_cached_regs(t, acc3, q, (dv < 0) != v_neg);
   }
 }
 

@@ -20,14 +20,17 @@ import numpy as np
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, REPO)
 
-PHASES = ["sha512 + loads", "mod L + recode + S check", "comb [S]B", "decode A + small order",
-          "A table", "dsm_k ([k](-A) + [S]B)", "y check + Z scan + park"]
+PHASES = {"ra": ["sha512 + loads", "mod L + recode + S check", "comb [S]B", "decode A + small order",
+                  "A table", "dsm_k ([k](-A) + [S]B)", "y check + Z scan + park"],
+          "hs": ["sha512 + loads", "mod L + S check", "decode A + A table", "decode R + R table",
+                 "lattice split + recode", "w = vS mod L + comb [w]B", "chain + check"]}
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--txns", type=int, default=1_000_000)
     ap.add_argument("--out", default=None)
+    ap.add_argument("--path", choices=("ra", "hs"), default="hs", help="kernel path of the stamped build")
     args = ap.parse_args()
     import firedancer_amd as fa
     from firedancer_amd import _lib, workload
@@ -51,7 +54,8 @@ def main():
     out = {"waves": int(n_waves), "waves_used": int(ok.sum()), "verify_ms": round(kv, 3),
            "wave_life_cycles_mean": round(float(life.mean()), 1),
            "phases": {p: {"cycles_mean": round(float(d[:, i].mean()), 1),
-                          "share": round(float(d[:, i].mean() / life.mean()), 4)} for i, p in enumerate(PHASES)},
+                          "share": round(float(d[:, i].mean() / life.mean()), 4)}
+                      for i, p in enumerate(PHASES[args.path])},
            "note": "cycles per wave between FDGPU_STAMP boundaries (s_memtime, shader clock); 2 waves share a SIMD"}
     b.free()
     eng.close()
