@@ -607,6 +607,7 @@ __global__ void __launch_bounds__(FDGPU_BLOCK, FDGPU_VERIFY_WAVES) fdgpu_tail_ke
   }
 }
 
+#if FDGPU_HALFSIZE
 /* ---------------- half-size verify (FDGPU_HALFSIZE) ----------------
    fdgpu_lattice.h: with u = v k (mod 8L), v odd and |u|, |v| < 2^135,
    [S]B - [k]A == R  <=>  [w]B - [u]A - [v]R == O  (w = v S mod L), decided
@@ -935,6 +936,8 @@ fdgpu_full_kernel(uint32_t *__restrict__ ws, const uint32_t *__restrict__ perm, 
     codes[out_idx(perm, i)] = (int8_t)(eq ? 0 : -3);
   }
 }
+
+#endif  /* FDGPU_HALFSIZE */
 
 /* Per transaction: fd_ed25519_verify_batch_single_msg's first-error order
    (fd_ed25519_user.c:232-310) over its signatures' codes, plus the batch's
