@@ -214,9 +214,9 @@ def adversarial(eng, n_txn, seed, ref_ms_per_sig):
     return out
 
 
-# one verify = fdgpu_verify_ra_kernel (everything but the last inversion) +
-# fdgpu_tail_kernel (batched inversions, queued slow-path signatures) +
-# fdgpu_finish_kernel; timed together with HIP events around the launches
+# one verify = the launches of fdgpu_launch_verify_sigs (fdgpu_kernel_path():
+# the half-size kernel + its full-length fallback, or the R-avoiding kernels),
+# timed together with HIP events around the launches
 VERIFY_KERNEL = "verify pipeline"
 
 
@@ -260,7 +260,7 @@ def cfg3_rate(eng, eng_nobucket, n_txn, seed):
 def main():
     args = parse()
     dist = Dist()
-    from firedancer_amd import VerifyEngine, workload
+    from firedancer_amd import VerifyEngine, _lib, workload
 
     t_gen = time.perf_counter()
     arena, txns, modes = workload.cfg1(args.txns, seed=rank_seed(dist.rank))
@@ -358,7 +358,7 @@ def main():
                                       "the instruction's measured rate (33.88 T/s, profiles/r01_ubench_int.jsonl)",
                          "frac_overlapped": round(value / dist.world * MADS_PER_SIG / 1e12 / VALU_MAD_PEAK_TOPS, 4),
                          "note": f"INT32 v_mad_u64_u32 ops: {MADS_PER_SIG} algorithmic mads/sig x {n_sig} sigs / mean "
-                                 f"{VERIFY_KERNEL} (fdgpu_verify_ra_kernel + fdgpu_tail_kernel + fdgpu_finish_kernel) time "
+                                 f"{VERIFY_KERNEL} ({_lib.lib().fdgpu_kernel_path().decode()}) time "
                                  f"{kv_ms:.3f} ms (HIP events, compute stream); combine kernel "
                                  f"{kc_ms:.4f} ms; traffic source {traffic_src}"},
             "cpu_baseline": cpu,

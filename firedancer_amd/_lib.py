@@ -52,6 +52,8 @@ def lib():
     L.fdgpu_engine_close.restype = None
     L.fdgpu_last_error.argtypes = []
     L.fdgpu_last_error.restype = c.c_char_p
+    L.fdgpu_kernel_path.argtypes = []
+    L.fdgpu_kernel_path.restype = c.c_char_p
     L.fdgpu_submit.argtypes = [vp, vp, c.c_uint64, vp, c.c_uint64]
     L.fdgpu_submit.restype = c.c_int64
     L.fdgpu_poll.argtypes = [vp, c.c_int64, vp, c.c_int]

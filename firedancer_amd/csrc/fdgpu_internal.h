@@ -42,9 +42,9 @@ typedef struct {
    (fdgpu_lattice.h); 0: the full-length chain with R compared on its
    encoding (R-avoiding path). */
 #ifndef FDGPU_HALFSIZE
-#define FDGPU_HALFSIZE 0
+#define FDGPU_HALFSIZE 1
 #endif
-#define HS_MAX_WIN          34u           /* radix-16 windows of |u|, |v| (< 2^135) */
+#define HS_MAX_WIN          40u           /* radix-16 windows of |u|, |v| (< 2^159) */
 #if FDGPU_HALFSIZE
 #define FDGPU_WS_RTAB       FDGPU_ATAB_ENTRIES          /* entries 9..17: the -R table */
 #define FDGPU_WS_PARK       (2u * FDGPU_ATAB_ENTRIES)   /* entry: k digits, decoded R, code (full path) */

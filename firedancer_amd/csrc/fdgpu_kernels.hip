@@ -609,7 +609,7 @@ __global__ void __launch_bounds__(FDGPU_BLOCK, FDGPU_VERIFY_WAVES) fdgpu_tail_ke
 
 #if FDGPU_HALFSIZE
 /* ---------------- half-size verify (FDGPU_HALFSIZE) ----------------
-   fdgpu_lattice.h: with u = v k (mod 8L), v odd and |u|, |v| < 2^135,
+   fdgpu_lattice.h: with u = v k (mod 8L), v odd and |u|, |v| < 2^159,
    [S]B - [k]A == R  <=>  [w]B - [u]A - [v]R == O  (w = v S mod L), decided
    with ~132 doublings instead of ~252.  Per lane:
      pass 1   S < L, k = SHA-512(R||A||M) mod L, decode A and R (the
@@ -1065,6 +1065,14 @@ __global__ void __launch_bounds__(64) fdgpu_test_sc_reduce_kernel(const uint32_t
 }  // namespace
 
 extern "C" {
+
+char const *fdgpu_kernel_path(void) {
+#if FDGPU_HALFSIZE
+  return "halfsize: fdgpu_verify_hs_kernel + fdgpu_full_kernel";
+#else
+  return "r-avoiding: fdgpu_verify_ra_kernel + fdgpu_tail_kernel + fdgpu_finish_kernel";
+#endif
+}
 
 size_t fdgpu_btab_bytes(void) { return (size_t)BC_NDIG * BC_ENT * FDGPU_BCOMB_STRIDE * sizeof(uint32_t); }
 

@@ -22,15 +22,19 @@
    |t_i| <= N / r_{i-1} < 2^127.  Of (r_i, t_i), (r_{i-1}, t_{i-1}),
    (r_{i+1}, t_{i+1}), (r_{i-1} - r_i, ...), (r_{i-1} + r_i, ...) the one with
    odd t and the fewest bits is taken (consecutive t are coprime, so an odd
-   one exists).  Over random k: 99.7% need <= 131 bits (33 radix-16
-   windows), 1e-5 more than 135 bits (34 windows); those lanes, and any lane
-   whose Euclid meets a quotient >= 2^31 (probability ~2^-30 per step), take
-   the full-length path instead (fdgpu_kernels.hip, the slow kernel).
+   one exists).  Over 400,000 random k (tests/test_lattice.py's harness):
+   99.7% need <= 131 bits (33 radix-16 windows), 5 needed 136-137 bits, none
+   more; up to 159 bits (40 windows) run in the verify kernel, and only a
+   lane whose Euclid needs a full-precision step with a quotient >= 2^31
+   (probability ~2^-30 per step) takes the full-length path
+   (fdgpu_kernels.hip, fdgpu_full_kernel).  The Euclid itself runs as
+   Lehmer's algorithm (hs_split below).
 
    Per lane, 32-bit limbs; __host__ __device__ so tests/test_lattice.py can
    check it against Python integers on the CPU. */
 #pragma once
 
+#include <math.h>
 #include <stdint.h>
 
 #if defined(__HIPCC__)
@@ -42,7 +46,7 @@
 
 namespace fdgpu {
 
-#define HS_MAX_BITS 135u          /* |u|, |v| < 2^135: 34 signed radix-16 windows */
+#define HS_MAX_BITS 159u          /* |u|, |v| < 2^159: at most 40 signed radix-16 windows */
 #define HS_MAX_ITERS 192u         /* Euclid steps (random k: 43-101; all-ones quotients: ~184) */
 #define HS_LIMBS 5u               /* |u|, |v| as 5 x u32 */
 
@@ -215,8 +219,66 @@ FDG_HD void hs_take(hs_split_t &o, const uint32_t (&x)[8], const uint32_t (&t)[6
   o.bits = bits;
 }
 
-/* (u, v) for k < L (8 limbs) -- see the file comment. */
-FDG_HD void hs_split(hs_split_t &o, const uint32_t (&k)[8]) {
+/* The split from the stopping point of Euclid: ar = r_{i-1} >= 2^128 > br =
+   r_i with their cofactors (see the file comment for the candidates). */
+FDG_HD void hs_finish(hs_split_t &o, const uint32_t (&ar)[8], const uint32_t (&br)[8], const uint32_t (&ta)[6],
+                      const uint32_t (&tb)[6]) {
+  o.ok = false;
+  o.bits = 0xffffffffu;
+  o.u_neg = o.v_neg = false;
+#pragma unroll
+  for (int i = 0; i < (int)HS_LIMBS; i++) o.u[i] = o.v[i] = 0;
+  uint32_t best = HS_MAX_BITS + 1;
+  hs_take(o, br, tb, best, true);                                /* (r_i, t_i) */
+  hs_take(o, ar, ta, best, true);                                /* (r_{i-1}, t_{i-1}) */
+  {                                                              /* (r_{i-1} - r_i, t_{i-1} - t_i) */
+    uint32_t x[8], t[6];
+#pragma unroll
+    for (int i = 0; i < 8; i++) x[i] = ar[i];
+    hs_sub8(x, br);
+    hs_tadd(t, ta, tb, true);
+    hs_take(o, x, t, best, true);
+    uint32_t y[8];                                               /* (r_{i-1} + r_i, t_{i-1} + t_i) */
+#pragma unroll
+    for (int i = 0; i < 8; i++) y[i] = ar[i];
+    hs_add8(y, br);
+    hs_tadd(t, ta, tb, false);
+    hs_take(o, y, t, best, (ar[7] >> 31) == 0);                  /* no 2^256 wrap */
+  }
+  {                                                              /* (r_{i+1}, t_{i+1}): one more step */
+    bool nz = false;
+#pragma unroll
+    for (int i = 0; i < 8; i++) nz = nz || br[i] != 0;
+    if (nz) {
+      /* q = floor(a / b) with b < 2^128: normalise a copy so a's top limb is set */
+      uint32_t an[8], bn[8];
+#pragma unroll
+      for (int i = 0; i < 8; i++) { an[i] = ar[i]; bn[i] = br[i]; }
+#pragma unroll 1
+      for (int s = 0; s < 7; s++) {
+        const bool m = an[7] == 0;
+#pragma unroll
+        for (int i = 7; i > 0; i--) { an[i] = m ? an[i - 1] : an[i]; bn[i] = m ? bn[i - 1] : bn[i]; }
+        an[0] = m ? 0u : an[0];
+        bn[0] = m ? 0u : bn[0];
+      }
+      uint32_t r[8], q = 0;
+      if (an[7] != 0 && hs_divstep(r, q, an, bn)) {
+        /* r is the normalised remainder; recompute it unshifted: c = a - q b */
+        uint32_t c[8], t[6];
+        const bool neg = hs_submul(c, ar, q, br);
+        hs_tsubmul(t, ta, q, tb);
+        hs_take(o, c, t, best, !neg);
+      }
+    }
+  }
+  o.ok = best <= HS_MAX_BITS;
+}
+
+/* (u, v) for k < L (8 limbs), one full-precision Euclid step per iteration
+   -- the definition hs_split (Lehmer) must reproduce; kept for the host
+   tests (tests/test_lattice.py). */
+FDG_HD void hs_split_euclid(hs_split_t &o, const uint32_t (&k)[8]) {
   constexpr uint32_t NL[8] = FDGPU_SC_8L;
   uint32_t a[8], b[8], ta[6], tb[6];
 #pragma unroll
@@ -280,51 +342,158 @@ FDG_HD void hs_split(hs_split_t &o, const uint32_t (&k)[8]) {
     ar[i] = xa;
     br[i] = xb;
   }
-  uint32_t best = HS_MAX_BITS + 1;
-  hs_take(o, br, tb, best, true);                                /* (r_i, t_i) */
-  hs_take(o, ar, ta, best, true);                                /* (r_{i-1}, t_{i-1}) */
-  {                                                              /* (r_{i-1} - r_i, t_{i-1} - t_i) */
-    uint32_t x[8], t[6];
+  hs_finish(o, ar, br, ta, tb);
+}
+
+/* ---- Lehmer's algorithm (Knuth, TAOCP vol. 2, 4.5.2, Algorithm L) ----
+   The Euclid steps are simulated on the leading 52 bits of a and b in
+   doubles (exact: every value stays below 2^53), collecting the 2x2
+   cofactor matrix; a quotient is taken only when both bracketing ratios
+   (U + A)/(V + C) and (U + B)/(V + D) agree on it, so the simulated steps
+   are exactly Euclid's.  The matrix is then applied to the full values
+   (about 26 bits of reduction per application instead of ~1.2 per
+   full-width step).  The stop rule is Euclid's too: a step is taken inside
+   the simulation only when its remainder is known to be >= 2^128 or known
+   to be < 2^128 (then it is the last); an undecided step, or a first step
+   the brackets cannot settle, is taken at full precision.  So hs_split
+   ends at the same (r_{i-1}, r_i) as hs_split_euclid and returns the same
+   split (tests/test_lattice.py checks this). */
+#define HS_MAX_OUTER 200u     /* matrix applications + full steps (random k: ~6-10) */
+#define HS_MAX_INNER 48u      /* simulated steps per application (cofactors < 2^31) */
+
+/* floor(x / y) for integers 0 <= x < 2^53, 0 < y < 2^53 held in doubles:
+   the rounded quotient is never below the true floor (integers are
+   representable, rounding is monotonic), and the remainder is exact */
+FDG_HD double hs_fdivf(double x, double y) {
+  const double q = floor(x / y);
+  return fma(-q, y, x) < 0.0 ? q - 1.0 : q;
+}
+
+/* (x >> s) for an 8-limb x < 2^(s + 64), s < 256 (selects, no dynamic
+   register indexing) */
+FDG_HD uint64_t hs_window(const uint32_t (&x)[8], uint32_t s) {
+  const uint32_t w = s >> 5, o = s & 31u;
+  uint32_t l0 = 0, l1 = 0, l2 = 0;
 #pragma unroll
-    for (int i = 0; i < 8; i++) x[i] = ar[i];
-    hs_sub8(x, br);
-    hs_tadd(t, ta, tb, true);
-    hs_take(o, x, t, best, true);
-    uint32_t y[8];                                               /* (r_{i-1} + r_i, t_{i-1} + t_i) */
-#pragma unroll
-    for (int i = 0; i < 8; i++) y[i] = ar[i];
-    hs_add8(y, br);
-    hs_tadd(t, ta, tb, false);
-    hs_take(o, y, t, best, (ar[7] >> 31) == 0);                  /* no 2^256 wrap */
+  for (uint32_t i = 0; i < 8; i++) {
+    l0 = i == w ? x[i] : l0;
+    l1 = i == w + 1u ? x[i] : l1;
+    l2 = i == w + 2u ? x[i] : l2;
   }
-  {                                                              /* (r_{i+1}, t_{i+1}): one more step */
-    bool nz = false;
+  const uint64_t lo = ((uint64_t)l1 << 32) | l0;
+  return o ? (lo >> o) | ((uint64_t)l2 << (64u - o)) : lo;
+}
+
+/* o = cx x + cy y over N limbs (mod 2^(32N)), cx and cy of opposite signs
+   (or one of them 0) with magnitudes < 2^31: o = +-(|cx| x - |cy| y).  For
+   remainders the true value is in [0, 2^256); for the two's complement
+   cofactors it fits N limbs. */
+template <int N>
+FDG_HD void hs_lin(uint32_t (&o)[N], const uint32_t (&x)[N], double cx, const uint32_t (&y)[N], double cy) {
+  const bool flip = cx < 0.0 || (cx == 0.0 && cy > 0.0);
+  const uint32_t mx = (uint32_t)fabs(cx), my = (uint32_t)fabs(cy);
+  uint64_t cp = 0, cq = 0;
+  uint32_t bw = 0;
 #pragma unroll
-    for (int i = 0; i < 8; i++) nz = nz || br[i] != 0;
-    if (nz) {
-      /* q = floor(a / b) with b < 2^128: normalise a copy so a's top limb is set */
-      uint32_t an[8], bn[8];
+  for (int j = 0; j < N; j++) {
+    const uint64_t p = (uint64_t)mx * x[j] + cp, q = (uint64_t)my * y[j] + cq;
+    cp = p >> 32;
+    cq = q >> 32;
+    const uint32_t pos = flip ? (uint32_t)q : (uint32_t)p, neg = flip ? (uint32_t)p : (uint32_t)q;
+    const uint64_t d = (uint64_t)pos - neg - bw;
+    o[j] = (uint32_t)d;
+    bw = (uint32_t)(d >> 63);
+  }
+}
+
+/* One full-precision Euclid step (a, b, ta, tb) <- (b, a - q b, tb, ta - q tb);
+   false when the quotient may reach 2^31 (the lane takes the full path). */
+FDG_HD bool hs_fullstep(uint32_t (&a)[8], uint32_t (&b)[8], uint32_t (&ta)[6], uint32_t (&tb)[6]) {
+  uint32_t an[8], bn[8];
 #pragma unroll
-      for (int i = 0; i < 8; i++) { an[i] = ar[i]; bn[i] = br[i]; }
+  for (int i = 0; i < 8; i++) { an[i] = a[i]; bn[i] = b[i]; }
 #pragma unroll 1
-      for (int s = 0; s < 7; s++) {
-        const bool m = an[7] == 0;
+  for (int s = 0; s < 7; s++) {                 /* normalise copies: a's top limb set */
+    const bool m = an[7] == 0;
 #pragma unroll
-        for (int i = 7; i > 0; i--) { an[i] = m ? an[i - 1] : an[i]; bn[i] = m ? bn[i - 1] : bn[i]; }
-        an[0] = m ? 0u : an[0];
-        bn[0] = m ? 0u : bn[0];
-      }
-      uint32_t r[8], q = 0;
-      if (an[7] != 0 && hs_divstep(r, q, an, bn)) {
-        /* r is the normalised remainder; recompute it unshifted: c = a - q b */
-        uint32_t c[8], t[6];
-        const bool neg = hs_submul(c, ar, q, br);
-        hs_tsubmul(t, ta, q, tb);
-        hs_take(o, c, t, best, !neg);
+    for (int i = 7; i > 0; i--) { an[i] = m ? an[i - 1] : an[i]; bn[i] = m ? bn[i - 1] : bn[i]; }
+    an[0] = m ? 0u : an[0];
+    bn[0] = m ? 0u : bn[0];
+  }
+  uint32_t r[8], q = 0;
+  if (an[7] == 0 || !hs_divstep(r, q, an, bn)) return false;
+  uint32_t c[8], t[6];
+  (void)hs_submul(c, a, q, b);                  /* q is exact: c = a mod b >= 0 */
+  hs_tsubmul(t, ta, q, tb);
+#pragma unroll
+  for (int i = 0; i < 8; i++) { a[i] = b[i]; b[i] = c[i]; }
+#pragma unroll
+  for (int i = 0; i < 6; i++) { ta[i] = tb[i]; tb[i] = t[i]; }
+  return true;
+}
+
+/* (u, v) for k < L (8 limbs) -- see the file comment. */
+FDG_HD void hs_split(hs_split_t &o, const uint32_t (&k)[8]) {
+  constexpr uint32_t NL[8] = FDGPU_SC_8L;
+  uint32_t a[8], b[8], ta[6], tb[6];
+#pragma unroll
+  for (int i = 0; i < 8; i++) { a[i] = NL[i]; b[i] = k[i]; }
+#pragma unroll
+  for (int i = 0; i < 6; i++) { ta[i] = 0; tb[i] = 0; }
+  tb[0] = 1;
+  bool fail = false, done = false;
+#pragma unroll 1
+  for (uint32_t it = 0; it < HS_MAX_OUTER; it++) {
+    if (!done && !fail) {
+      done = (b[4] | b[5] | b[6] | b[7]) == 0;   /* r_i < 2^128 (a = r_{i-1} >= 2^128) */
+      if (!done) {
+        const uint32_t s = hs_bitlen<8>(a) - 52u;   /* a >= 2^128: s >= 77 */
+        double U = (double)hs_window(a, s), V = (double)hs_window(b, s);
+        const double T = ldexp(1.0, 128 - (int)s);   /* 2^128 in units of 2^s */
+        double A = 1.0, B = 0.0, C = 0.0, D = 1.0;
+#pragma unroll 1
+        for (uint32_t j = 0; j < HS_MAX_INNER; j++) {
+          if (V + C <= 0.0 || V + D <= 0.0) break;
+          const double q = hs_fdivf(U + A, V + C);
+          if (q != hs_fdivf(U + B, V + D)) break;
+          const double Vn = fma(-q, V, U), Cn = fma(-q, C, A), Dn = fma(-q, D, B);
+          if (fmax(fabs(Cn), fabs(Dn)) >= 2147483648.0) break;
+          /* the true remainder / 2^s lies in (Vn + min(Cn, Dn), Vn + max(Cn, Dn)) */
+          const double lo = Vn + fmin(Cn, Dn), hi = Vn + fmax(Cn, Dn);
+          if (hi > T && lo < T) break;            /* undecided: take it at full precision */
+          U = V; V = Vn; A = C; C = Cn; B = D; D = Dn;
+          if (hi <= T) break;                     /* the first remainder below 2^128: stop */
+        }
+        if (B == 0.0) {
+          fail = !hs_fullstep(a, b, ta, tb);
+        } else {
+          uint32_t a2[8], b2[8], ta2[6], tb2[6];
+          hs_lin<8>(a2, a, A, b, B);
+          hs_lin<8>(b2, a, C, b, D);
+          hs_lin<6>(ta2, ta, A, tb, B);
+          hs_lin<6>(tb2, ta, C, tb, D);
+#pragma unroll
+          for (int i = 0; i < 8; i++) { a[i] = a2[i]; b[i] = b2[i]; }
+#pragma unroll
+          for (int i = 0; i < 6; i++) { ta[i] = ta2[i]; tb[i] = tb2[i]; }
+        }
       }
     }
+#if defined(__HIP_DEVICE_COMPILE__)
+    if (__all(done || fail)) break;
+#else
+    if (done || fail) break;
+#endif
   }
-  o.ok = best <= HS_MAX_BITS;
+  if (fail || !done) {
+    o.ok = false;
+    o.bits = 0xffffffffu;
+    o.u_neg = o.v_neg = false;
+#pragma unroll
+    for (int i = 0; i < (int)HS_LIMBS; i++) o.u[i] = o.v[i] = 0;
+    return;
+  }
+  hs_finish(o, a, b, ta, tb);
 }
 
 }  // namespace fdgpu

@@ -201,6 +201,9 @@ int  fdgpu_sync( fdgpu_engine_t * e );
    threads per workgroup, workspace bytes. */
 int fdgpu_engine_info( fdgpu_engine_t * e, uint32_t * grid_blocks, uint32_t * block_threads,
                        uint64_t * ws_bytes );
+/* The kernels one verify launches, as a static string, e.g.
+   "halfsize: fdgpu_verify_hs_kernel + fdgpu_full_kernel" (the build's path). */
+char const * fdgpu_kernel_path( void );
 
 /* --------------------------------------------------------- diagnostics */
 /* Used by the parity tests to check each stage of the path on the GPU in

@@ -1,6 +1,6 @@
 """fdgpu_lattice.h (half-size scalars for the verify equation) on the CPU,
 against Python integers: for every k the split (u, v) must satisfy
-u = v k (mod 8L), v odd, 0 < |v| < L and |u|, |v| < 2^bits <= 2^135 whenever
+u = v k (mod 8L), v odd, 0 < |v| < L and |u|, |v| < 2^bits <= 2^159 whenever
 it reports ok -- the conditions under which [w]B - [u]A - [v]R = O decides
 the reference's cofactorless [S]B - [k]A == R exactly (file comment)."""
 import ctypes
@@ -21,12 +21,12 @@ def hs(tmp_path_factory):
     subprocess.run(["g++", "-O2", "-std=c++17", "-fPIC", "-shared", "-Wno-unknown-pragmas",
                     os.path.join(REPO, "tests", "native", "lattice_host.cpp"), "-o", so], check=True)
     lib = ctypes.CDLL(so)
-    lib.hs_split_host.argtypes = [ctypes.c_void_p] * 4
+    lib.hs_split_host.argtypes = [ctypes.c_void_p] * 4 + [ctypes.c_int]
 
-    def split(k):
+    def split(k, which=0):
         kb = (ctypes.c_uint32 * 8)(*[(k >> (32 * i)) & 0xffffffff for i in range(8)])
         u, v, f = (ctypes.c_uint32 * 5)(), (ctypes.c_uint32 * 5)(), (ctypes.c_uint32 * 4)()
-        lib.hs_split_host(kb, u, v, f)
+        lib.hs_split_host(kb, u, v, f, which)
         uu = sum(x << (32 * i) for i, x in enumerate(u))
         vv = sum(x << (32 * i) for i, x in enumerate(v))
         return (-uu if f[1] else uu), (-vv if f[2] else vv), bool(f[0]), f[3]
@@ -39,7 +39,7 @@ def _check(split, k):
         return False
     assert (u - v * k) % N == 0, k
     assert v % 2 == 1 and 0 < abs(v) < L
-    assert max(abs(u).bit_length(), abs(v).bit_length()) == bits <= 135
+    assert max(abs(u).bit_length(), abs(v).bit_length()) == bits <= 159
     return True
 
 
@@ -72,3 +72,23 @@ def test_scalars_with_large_quotients(hs):
         m = rnd.randrange(1, n + 1)
         k = (N * m // n + rnd.randrange(-1000, 1000)) % L
         _check(hs, k)
+
+
+def test_lehmer_matches_euclid(hs):
+    """hs_split (Lehmer: Euclid simulated on 52-bit leading parts, matrix
+    applied to the full values) stops where the one-step-at-a-time Euclid
+    stops, so both return the same split -- except that a quotient >= 2^31
+    inside a simulated run is exact in Lehmer (ok) where the full-precision
+    step gives up (not ok)."""
+    rnd = random.Random(0x1E4)
+    ks = [rnd.randrange(L) for _ in range(20000)]
+    ks += [rnd.randrange(2**128, 2**140) for _ in range(500)]          # short runs, the stop near the top
+    ks += [(N * m // n + rnd.randrange(-50, 50)) % L                    # large partial quotients
+           for n, m in ((rnd.randrange(1, 1 << 36), rnd.randrange(1, 1 << 20)) for _ in range(3000)) if m < n]
+    ks += [2**128 + i for i in range(50)] + [2**129 - i for i in range(1, 50)] + [L - i for i in range(1, 50)]
+    for k in ks:
+        a, b = hs(k, 0), hs(k, 1)
+        if b[2]:
+            assert a == b, k
+        elif a[2]:
+            _check(hs, k)

@@ -17,9 +17,10 @@ import sys
 from collections import defaultdict
 
 PIPELINE = "verify pipeline"
-# the launches of one fdgpu_launch_verify_sigs (R-avoiding path), or the single
-# fused kernel of the FDGPU_RAVOID=0 build
-KERNELS = ("fdgpu_verify_ra_kernel", "fdgpu_tail_kernel", "fdgpu_finish_kernel", "fdgpu_fused_kernel")
+# the launches of one fdgpu_launch_verify_sigs (half-size path, or the
+# R-avoiding path of FDGPU_HALFSIZE=0 builds)
+KERNELS = ("fdgpu_verify_hs_kernel", "fdgpu_full_kernel",
+           "fdgpu_verify_ra_kernel", "fdgpu_tail_kernel", "fdgpu_finish_kernel", "fdgpu_fused_kernel")
 
 
 def read_pass(d):
@@ -33,7 +34,7 @@ def read_pass(d):
                 if name is None:
                     continue
                 vals[name][row["Counter_Name"]].append(float(row["Counter_Value"]))
-                if name in ("fdgpu_verify_ra_kernel", "fdgpu_fused_kernel"):
+                if name in ("fdgpu_verify_hs_kernel", "fdgpu_verify_ra_kernel", "fdgpu_fused_kernel"):
                     meta = {k: row.get(k) for k in ("Grid_Size", "Workgroup_Size", "LDS_Block_Size", "Scratch_Size",
                                                     "VGPR_Count", "Accum_VGPR_Count", "SGPR_Count") if k in row}
     return vals, meta
