@@ -191,6 +191,11 @@ int ensure_ws(fdgpu_engine *e, uint64_t n_sig) {
 }  // namespace
 
 static bool bucket(const fdgpu_engine_t *e) { return !(e->cfg.flags & FDGPU_FLAG_NO_BUCKET); }
+/* the kernels' flags for this engine's configuration */
+static uint32_t kflags(const fdgpu_engine_t *e) {
+  return ((e->cfg.flags & FDGPU_FLAG_REF_MAPPING) ? FDGPU_FLAG_REF_MAP : 0u) |
+         ((e->cfg.flags & FDGPU_FLAG_FULL_PATH) ? FDGPU_FLAG_KFULL : 0u);
+}
 
 extern "C" {
 
@@ -258,7 +263,7 @@ int fdgpu_engine_info(fdgpu_engine_t *e, uint32_t *grid_blocks, uint32_t *block_
 static int enqueue_verify(fdgpu_engine_t *e, const uint8_t *d_arena, const fdgpu_sig_desc_t *d_sigs,
                           const uint32_t *d_perm, uint64_t n_sig, const fdgpu_txn_desc_t *d_txns, uint64_t n_txn,
                           int8_t *d_sig_codes, int8_t *d_txn_codes, hipStream_t st, uint32_t *ws = nullptr) {
-  const uint32_t flags = (e->cfg.flags & FDGPU_FLAG_REF_MAPPING) ? FDGPU_FLAG_REF_MAP : 0u;
+  const uint32_t flags = kflags(e);
   if (!ws && n_sig > e->ws_sig) {
     HIPCHK(hipStreamSynchronize(st), FDGPU_ERR_DEVICE);
     HIPCHK(hipStreamSynchronize(e->compute), FDGPU_ERR_DEVICE);
@@ -566,7 +571,7 @@ int fdgpu_dev_batch_time(fdgpu_engine_t *e, fdgpu_dev_batch_t *b, int iters, dou
                          double *combine_kernel_ms) {
   if (!e || !b || iters < 1) return FDGPU_ERR_INVAL;
   HIPCHK(hipSetDevice(e->device), FDGPU_ERR_DEVICE);
-  const uint32_t flags = (e->cfg.flags & FDGPU_FLAG_REF_MAPPING) ? FDGPU_FLAG_REF_MAP : 0u;
+  const uint32_t flags = kflags(e);
   const hipStream_t st = batch_stream(e, b);
   if (!b->d_ws && b->n_sig > e->ws_sig) {
     HIPCHK(hipStreamSynchronize(e->compute), FDGPU_ERR_DEVICE);
@@ -799,7 +804,7 @@ int fdgpu_debug_sig_codes(fdgpu_engine_t *e, uint8_t const *arena, uint64_t aren
   HIPCHK(hipMemcpy(da.p, arena, arena_sz, hipMemcpyHostToDevice), FDGPU_ERR_DEVICE);
   HIPCHK(hipMemcpy(dd.p, sd.data(), ns * sizeof(fdgpu_sig_desc_t), hipMemcpyHostToDevice), FDGPU_ERR_DEVICE);
   if (perm) HIPCHK(hipMemcpy(dp.p, perm, ns * sizeof(uint32_t), hipMemcpyHostToDevice), FDGPU_ERR_DEVICE);
-  const uint32_t flags = (e->cfg.flags & FDGPU_FLAG_REF_MAPPING) ? FDGPU_FLAG_REF_MAP : 0u;
+  const uint32_t flags = kflags(e);
   if ((uint64_t)ns > e->ws_sig) { int rc = ensure_ws(e, (uint64_t)ns); if (rc) return rc; }
   HIPCHK(fdgpu_launch_verify_sigs((uint8_t *)da.p, (fdgpu_sig_desc_t *)dd.p, (uint32_t)ns,
                                   perm ? (uint32_t *)dp.p : nullptr, e->d_btab, e->d_ws, (int8_t *)dc.p, flags,

@@ -147,6 +147,98 @@ FDG_DEV void fe_carry(fe &h) {
 #define FDGPU_FE_FF 1
 #endif
 
+#ifndef FDGPU_FE_ASMCOL
+#define FDGPU_FE_ASMCOL 1
+#endif
+
+/* FDGPU_FE_ASMCOL=1: each column's v_mad_u64_u32 chain is ONE inline-asm
+   block.  With one block per mad the compiler's hazard recognizer cannot see
+   inside the asm and pads every block with an s_nop; compiler-generated
+   back-to-back mads writing the same carry SGPR need none, so a block of N
+   dependent mads is as safe as N separate ones.  madc<N>::run(s, a, b):
+   s += a[0] b[0] + ... + a[N-1] b[N-1], in that order. */
+template <int N> struct madc;
+template <> struct madc<1> {
+  static FDG_DEV void run(uint64_t &s, const uint32_t *a, const uint32_t *b) {
+    uint64_t cc;
+    asm("v_mad_u64_u32 %0, %1, %2, %3, %0\n"
+        : "+v"(s), "=&s"(cc) : "v"(a[0]), "v"(b[0]));
+    (void)cc;
+  }
+};
+template <> struct madc<2> {
+  static FDG_DEV void run(uint64_t &s, const uint32_t *a, const uint32_t *b) {
+    uint64_t cc;
+    asm("v_mad_u64_u32 %0, %1, %2, %3, %0\n" "v_mad_u64_u32 %0, %1, %4, %5, %0\n"
+        : "+v"(s), "=&s"(cc) : "v"(a[0]), "v"(b[0]), "v"(a[1]), "v"(b[1]));
+    (void)cc;
+  }
+};
+template <> struct madc<3> {
+  static FDG_DEV void run(uint64_t &s, const uint32_t *a, const uint32_t *b) {
+    uint64_t cc;
+    asm("v_mad_u64_u32 %0, %1, %2, %3, %0\n" "v_mad_u64_u32 %0, %1, %4, %5, %0\n" "v_mad_u64_u32 %0, %1, %6, %7, %0\n"
+        : "+v"(s), "=&s"(cc) : "v"(a[0]), "v"(b[0]), "v"(a[1]), "v"(b[1]), "v"(a[2]), "v"(b[2]));
+    (void)cc;
+  }
+};
+template <> struct madc<4> {
+  static FDG_DEV void run(uint64_t &s, const uint32_t *a, const uint32_t *b) {
+    uint64_t cc;
+    asm("v_mad_u64_u32 %0, %1, %2, %3, %0\n" "v_mad_u64_u32 %0, %1, %4, %5, %0\n" "v_mad_u64_u32 %0, %1, %6, %7, %0\n" "v_mad_u64_u32 %0, %1, %8, %9, %0\n"
+        : "+v"(s), "=&s"(cc) : "v"(a[0]), "v"(b[0]), "v"(a[1]), "v"(b[1]), "v"(a[2]), "v"(b[2]), "v"(a[3]), "v"(b[3]));
+    (void)cc;
+  }
+};
+template <> struct madc<5> {
+  static FDG_DEV void run(uint64_t &s, const uint32_t *a, const uint32_t *b) {
+    uint64_t cc;
+    asm("v_mad_u64_u32 %0, %1, %2, %3, %0\n" "v_mad_u64_u32 %0, %1, %4, %5, %0\n" "v_mad_u64_u32 %0, %1, %6, %7, %0\n" "v_mad_u64_u32 %0, %1, %8, %9, %0\n" "v_mad_u64_u32 %0, %1, %10, %11, %0\n"
+        : "+v"(s), "=&s"(cc) : "v"(a[0]), "v"(b[0]), "v"(a[1]), "v"(b[1]), "v"(a[2]), "v"(b[2]), "v"(a[3]), "v"(b[3]), "v"(a[4]), "v"(b[4]));
+    (void)cc;
+  }
+};
+template <> struct madc<6> {
+  static FDG_DEV void run(uint64_t &s, const uint32_t *a, const uint32_t *b) {
+    uint64_t cc;
+    asm("v_mad_u64_u32 %0, %1, %2, %3, %0\n" "v_mad_u64_u32 %0, %1, %4, %5, %0\n" "v_mad_u64_u32 %0, %1, %6, %7, %0\n" "v_mad_u64_u32 %0, %1, %8, %9, %0\n" "v_mad_u64_u32 %0, %1, %10, %11, %0\n" "v_mad_u64_u32 %0, %1, %12, %13, %0\n"
+        : "+v"(s), "=&s"(cc) : "v"(a[0]), "v"(b[0]), "v"(a[1]), "v"(b[1]), "v"(a[2]), "v"(b[2]), "v"(a[3]), "v"(b[3]), "v"(a[4]), "v"(b[4]), "v"(a[5]), "v"(b[5]));
+    (void)cc;
+  }
+};
+template <> struct madc<7> {
+  static FDG_DEV void run(uint64_t &s, const uint32_t *a, const uint32_t *b) {
+    uint64_t cc;
+    asm("v_mad_u64_u32 %0, %1, %2, %3, %0\n" "v_mad_u64_u32 %0, %1, %4, %5, %0\n" "v_mad_u64_u32 %0, %1, %6, %7, %0\n" "v_mad_u64_u32 %0, %1, %8, %9, %0\n" "v_mad_u64_u32 %0, %1, %10, %11, %0\n" "v_mad_u64_u32 %0, %1, %12, %13, %0\n" "v_mad_u64_u32 %0, %1, %14, %15, %0\n"
+        : "+v"(s), "=&s"(cc) : "v"(a[0]), "v"(b[0]), "v"(a[1]), "v"(b[1]), "v"(a[2]), "v"(b[2]), "v"(a[3]), "v"(b[3]), "v"(a[4]), "v"(b[4]), "v"(a[5]), "v"(b[5]), "v"(a[6]), "v"(b[6]));
+    (void)cc;
+  }
+};
+template <> struct madc<8> {
+  static FDG_DEV void run(uint64_t &s, const uint32_t *a, const uint32_t *b) {
+    uint64_t cc;
+    asm("v_mad_u64_u32 %0, %1, %2, %3, %0\n" "v_mad_u64_u32 %0, %1, %4, %5, %0\n" "v_mad_u64_u32 %0, %1, %6, %7, %0\n" "v_mad_u64_u32 %0, %1, %8, %9, %0\n" "v_mad_u64_u32 %0, %1, %10, %11, %0\n" "v_mad_u64_u32 %0, %1, %12, %13, %0\n" "v_mad_u64_u32 %0, %1, %14, %15, %0\n" "v_mad_u64_u32 %0, %1, %16, %17, %0\n"
+        : "+v"(s), "=&s"(cc) : "v"(a[0]), "v"(b[0]), "v"(a[1]), "v"(b[1]), "v"(a[2]), "v"(b[2]), "v"(a[3]), "v"(b[3]), "v"(a[4]), "v"(b[4]), "v"(a[5]), "v"(b[5]), "v"(a[6]), "v"(b[6]), "v"(a[7]), "v"(b[7]));
+    (void)cc;
+  }
+};
+template <> struct madc<9> {
+  static FDG_DEV void run(uint64_t &s, const uint32_t *a, const uint32_t *b) {
+    uint64_t cc;
+    asm("v_mad_u64_u32 %0, %1, %2, %3, %0\n" "v_mad_u64_u32 %0, %1, %4, %5, %0\n" "v_mad_u64_u32 %0, %1, %6, %7, %0\n" "v_mad_u64_u32 %0, %1, %8, %9, %0\n" "v_mad_u64_u32 %0, %1, %10, %11, %0\n" "v_mad_u64_u32 %0, %1, %12, %13, %0\n" "v_mad_u64_u32 %0, %1, %14, %15, %0\n" "v_mad_u64_u32 %0, %1, %16, %17, %0\n" "v_mad_u64_u32 %0, %1, %18, %19, %0\n"
+        : "+v"(s), "=&s"(cc) : "v"(a[0]), "v"(b[0]), "v"(a[1]), "v"(b[1]), "v"(a[2]), "v"(b[2]), "v"(a[3]), "v"(b[3]), "v"(a[4]), "v"(b[4]), "v"(a[5]), "v"(b[5]), "v"(a[6]), "v"(b[6]), "v"(a[7]), "v"(b[7]), "v"(a[8]), "v"(b[8]));
+    (void)cc;
+  }
+};
+template <> struct madc<10> {
+  static FDG_DEV void run(uint64_t &s, const uint32_t *a, const uint32_t *b) {
+    uint64_t cc;
+    asm("v_mad_u64_u32 %0, %1, %2, %3, %0\n" "v_mad_u64_u32 %0, %1, %4, %5, %0\n" "v_mad_u64_u32 %0, %1, %6, %7, %0\n" "v_mad_u64_u32 %0, %1, %8, %9, %0\n" "v_mad_u64_u32 %0, %1, %10, %11, %0\n" "v_mad_u64_u32 %0, %1, %12, %13, %0\n" "v_mad_u64_u32 %0, %1, %14, %15, %0\n" "v_mad_u64_u32 %0, %1, %16, %17, %0\n" "v_mad_u64_u32 %0, %1, %18, %19, %0\n" "v_mad_u64_u32 %0, %1, %20, %21, %0\n"
+        : "+v"(s), "=&s"(cc) : "v"(a[0]), "v"(b[0]), "v"(a[1]), "v"(b[1]), "v"(a[2]), "v"(b[2]), "v"(a[3]), "v"(b[3]), "v"(a[4]), "v"(b[4]), "v"(a[5]), "v"(b[5]), "v"(a[6]), "v"(b[6]), "v"(a[7]), "v"(b[7]), "v"(a[8]), "v"(b[8]), "v"(a[9]), "v"(b[9]));
+    (void)cc;
+  }
+};
+
 /* s += a * b as one v_mad_u64_u32 (carry-out SGPR pair unused) */
 FDG_DEV void mad_acc(uint64_t &s, uint32_t a, uint32_t b) {
   uint64_t cc;
@@ -179,6 +271,19 @@ FDG_DEV void fe_mul(fe &h, const fe &f, const fe &g) {
 #pragma unroll
   for (int k = 0; k < 10; k++) {
     uint64_t s = carry;
+#if FDGPU_FE_ASMCOL
+    uint32_t ca[10], cb[10];
+#pragma unroll
+    for (int i = 0; i < 10; i++) {
+      int j = k - i;
+      const bool wrap = j < 0;
+      if (wrap) j += 10;
+      const bool dbl = (i & 1) && (j & 1);
+      ca[i] = dbl ? f2[i] : f.v[i];
+      cb[i] = wrap ? g19[j] : g.v[j];
+    }
+    madc<10>::run(s, ca, cb);
+#else
 #pragma unroll
     for (int i = 0; i < 10; i++) {
       int j = k - i;
@@ -187,6 +292,7 @@ FDG_DEV void fe_mul(fe &h, const fe &f, const fe &g) {
       const bool dbl = (i & 1) && (j & 1);
       mad_acc(s, dbl ? f2[i] : f.v[i], wrap ? g19[j] : g.v[j]);
     }
+#endif
     const int bits = (k & 1) ? 25 : 26;
     r[k] = (uint32_t)s & ((1u << bits) - 1);
     carry = s >> bits;
@@ -233,6 +339,23 @@ FDG_DEV void fe_sq_sh(fe &h, const fe &f) {
 #pragma unroll
   for (int k = 0; k < 10; k++) {
     uint64_t s = carry;
+#if FDGPU_FE_ASMCOL
+    uint32_t ca[6], cb[6];
+    int n = 0;
+#pragma unroll
+    for (int i = 0; i < 10; i++) {
+#pragma unroll
+      for (int j = i; j < 10; j++) {
+        if ((i + j) % 10 != k) continue;
+        const int mul2 = (i != j ? 1 : 0) + (((i & 1) && (j & 1)) ? 1 : 0) + SH;
+        ca[n] = pick(mul2, i);
+        cb[n] = (i + j) >= 10 ? f19[j] : f.v[j];
+        n++;
+      }
+    }
+    if (k & 1) madc<5>::run(s, ca, cb);             /* odd columns: 5 symmetric terms, even: 6 */
+    else madc<6>::run(s, ca, cb);
+#else
 #pragma unroll
     for (int i = 0; i < 10; i++) {
 #pragma unroll
@@ -242,6 +365,7 @@ FDG_DEV void fe_sq_sh(fe &h, const fe &f) {
         mad_acc(s, pick(mul2, i), (i + j) >= 10 ? f19[j] : f.v[j]);
       }
     }
+#endif
     const int bits = (k & 1) ? 25 : 26;
     r[k] = (uint32_t)s & ((1u << bits) - 1);
     carry = s >> bits;

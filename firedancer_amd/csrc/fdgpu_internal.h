@@ -58,6 +58,7 @@ typedef struct {
 #define FDGPU_WS_LANE_WORDS (FDGPU_WS_ENTRIES * FDGPU_ATAB_WORDS)
 #define FDGPU_BLOCK         256u
 #define FDGPU_FLAG_REF_MAP  1u            /* portable-backend error mapping */
+#define FDGPU_FLAG_KFULL    2u            /* half-size path: every lane takes the full-length fallback */
 /* SHA-512 block-count groups of the host-side bucketing (expand): messages of
    more blocks than this share the last group */
 #define FDGPU_NBLK_GROUPS   32u

@@ -846,7 +846,7 @@ fdgpu_verify_hs_kernel(const uint8_t *__restrict__ arena, const fdgpu_sig_desc_t
   recode16_160(ud, ndu, hs.u);
   recode16_160(vd, ndv, hs.v);
   const uint32_t nd_lane = max(max(ndu, ndv), 1u);
-  const bool full = need && (!hs.ok || nd_lane > HS_MAX_WIN);
+  const bool full = need && (!hs.ok || nd_lane > HS_MAX_WIN || (flags & FDGPU_FLAG_KFULL));
   const bool half = need && !full;
   FDGPU_STAMP(5);
   /* [w]B (w = v S mod L), or [S]B for the full-length path; parked cached */

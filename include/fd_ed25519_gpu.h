@@ -94,6 +94,8 @@ typedef struct {
 #define FDGPU_FLAG_REF_MAPPING 1u  /* portable-backend (ref) error mapping instead of AVX-512 */
 #define FDGPU_FLAG_NO_BUCKET   2u  /* verify signatures in transaction order (default: grouped by
                                       SHA-512 block count, codes still returned in order) */
+#define FDGPU_FLAG_FULL_PATH  4u  /* diagnostics: every signature takes the full-length fallback chain
+                                      (fdgpu_full_kernel), so the parity tests cover that path */
 
 /* Status codes of the engine API (distinct from verify codes). */
 #define FDGPU_OK            ( 0)

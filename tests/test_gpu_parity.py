@@ -472,3 +472,28 @@ def test_all_failing_batches(engine, oracle, mode):
     exp = oracle.verify_txns(arena, txns, nthreads=8)
     assert (got == exp).all(), np.nonzero(got != exp)[0][:10]
     assert (got != 0).all()
+
+
+def test_full_length_fallback_path(vectors, oracle):
+    """The half-size kernel hands a lane whose lattice split fails (a Euclid
+    quotient >= 2^31: ~2^-30 per step, no input reaches it on purpose) to
+    fdgpu_full_kernel, the full-length [S]B + [k](-A) chain.  FDGPU_FLAG_FULL_PATH
+    sends every signature there, so that path is held to the same parity bar:
+    the golden vectors (reference codes), random cfg1/cfg3 sets and the
+    small-order x S-edge cross product against the oracle."""
+    import firedancer_amd as fa
+    eng = fa.VerifyEngine(0, max_txn=8192, full_path=True)
+    try:
+        vs, arena, txns = _vector_batch(vectors)
+        codes = eng.verify_txns(arena, txns)
+        bad = [(v["src"], v["tc_id"], v["code"], int(c)) for v, c in zip(vs, codes) if c != v["code"]]
+        assert not bad, bad[:20]
+        for arena, txns, _ in (workload.cfg1(2000, seed=0xF011), workload.cfg3(600, seed=0xF012)):
+            got = eng.verify_txns(arena, txns)
+            exp = oracle.verify_txns(arena, txns, nthreads=8)
+            assert (got == exp).all(), np.nonzero(got != exp)[0][:10]
+        arena, txns = workload.pack_single(workload.small_order_cross_product())
+        got = eng.verify_txns(arena, txns)
+        assert (got == oracle.verify_txns(arena, txns, nthreads=8)).all()
+    finally:
+        eng.close()
