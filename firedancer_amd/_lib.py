@@ -68,6 +68,10 @@ def lib():
     L.fdgpu_release.restype = c.c_int
     L.fdgpu_stage_cancel.argtypes = [vp]
     L.fdgpu_stage_cancel.restype = c.c_int
+    L.fdgpu_host_register.argtypes = [vp, vp, c.c_uint64]
+    L.fdgpu_host_register.restype = c.c_int
+    L.fdgpu_host_unregister.argtypes = [vp, vp]
+    L.fdgpu_host_unregister.restype = c.c_int
     L.fdgpu_verify_device.argtypes = [vp, vp, vp, c.c_uint64, vp, c.c_uint64, vp, vp, vp]
     L.fdgpu_verify_device.restype = c.c_int
     L.fdgpu_engine_info.argtypes = [vp, c.POINTER(c.c_uint32), c.POINTER(c.c_uint32), c.POINTER(c.c_uint64)]

@@ -19,6 +19,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <map>
 #include <mutex>
 #include <string>
 #include <thread>
@@ -71,6 +72,10 @@ struct fdgpu_engine {
   int8_t *d_scratch_codes = nullptr;   /* for fdgpu_verify_device with d_sig_codes == NULL */
   uint64_t scratch_cap = 0;
   std::vector<hipStream_t> batch_streams;   /* streams of device batches with their own queue */
+  /* the ring API (submit / stage / poll / release) may be called from several
+     host threads (verify tiles sharing the node's engines) */
+  std::mutex ring_mu;
+  std::vector<std::pair<uintptr_t, uint64_t>> regions;   /* fdgpu_host_register'ed [p, p + sz) */
 };
 
 namespace {
@@ -190,6 +195,31 @@ int ensure_ws(fdgpu_engine *e, uint64_t n_sig) {
 
 }  // namespace
 
+/* Host regions registered for direct DMA (hipHostRegister, portable to every
+   device), reference-counted across the engines that registered them. */
+namespace {
+std::mutex g_reg_mu;
+std::map<uintptr_t, std::pair<uint64_t, int>> g_regions;   /* page-aligned base -> (bytes, engines) */
+
+bool region_covers(const fdgpu_engine *e, const uint8_t *p, uint64_t sz) {
+  const uintptr_t a = (uintptr_t)p;
+  for (const auto &r : e->regions)
+    if (a >= r.first && a + sz <= r.first + r.second) return true;
+  return false;
+}
+
+void unregister_one(fdgpu_engine *e, uintptr_t a) {
+  std::lock_guard<std::mutex> rk(g_reg_mu);
+  auto it = g_regions.find(a);
+  if (it == g_regions.end()) return;
+  if (--it->second.second == 0) {
+    (void)hipSetDevice(e->device);
+    (void)hipHostUnregister((void *)a);
+    g_regions.erase(it);
+  }
+}
+}  // namespace
+
 static bool bucket(const fdgpu_engine_t *e) { return !(e->cfg.flags & FDGPU_FLAG_NO_BUCKET); }
 /* the kernels' flags for this engine's configuration */
 static uint32_t kflags(const fdgpu_engine_t *e) {
@@ -242,6 +272,7 @@ void fdgpu_engine_close(fdgpu_engine_t *e) {
   (void)hipSetDevice(e->device);
   if (e->compute) (void)hipStreamSynchronize(e->compute);
   for (auto &s : e->slots) { if (s.stream) (void)hipStreamSynchronize(s.stream); slot_free(s); }
+  for (auto &r : e->regions) unregister_one(e, r.first);
   for (auto st : e->batch_streams) (void)hipStreamSynchronize(st);   /* btab is read there */
   if (e->d_btab) (void)hipFree(e->d_btab);
   if (e->d_ws) (void)hipFree(e->d_ws);
@@ -280,15 +311,23 @@ static int enqueue_verify(fdgpu_engine_t *e, const uint8_t *d_arena, const fdgpu
 /* Enqueue the batch already in slot s's pinned arena (arena_sz bytes). */
 /* `uploaded` = bytes of the arena whose host->device copy is already queued on
    the slot's stream (fdgpu_submit overlaps its staging memcpy with the copy) */
+/* src != NULL: the arena lies in a registered host region and is uploaded
+   straight from there (no staging copy); its bytes must stay unchanged until
+   the batch is polled. */
 static int64_t submit_slot(fdgpu_engine_t *e, Slot *s, uint64_t arena_sz, fdgpu_txn_t const *txns, uint64_t txn_cnt,
-                           uint64_t uploaded = 0) {
+                           uint64_t uploaded = 0, const uint8_t *src = nullptr) {
   uint32_t *perm = bucket(e) ? s->h_perm : nullptr;
   const int64_t ns = expand(arena_sz, txns, txn_cnt, e->cfg.max_sig, s->h_sigs, s->h_txns, perm);
   if (ns < 0) return FDGPU_ERR_INVAL;
-  memset(s->h_arena + arena_sz, 0, FDGPU_ARENA_SLACK);
-  const size_t asz = arena_sz + FDGPU_ARENA_SLACK - uploaded;
-  HIPCHK(hipMemcpyAsync(s->d_arena + uploaded, s->h_arena + uploaded, asz, hipMemcpyHostToDevice, s->stream),
-         FDGPU_ERR_DEVICE);
+  if (src) {
+    if (arena_sz) HIPCHK(hipMemcpyAsync(s->d_arena, src, arena_sz, hipMemcpyHostToDevice, s->stream), FDGPU_ERR_DEVICE);
+    HIPCHK(hipMemsetAsync(s->d_arena + arena_sz, 0, FDGPU_ARENA_SLACK, s->stream), FDGPU_ERR_DEVICE);
+  } else {
+    memset(s->h_arena + arena_sz, 0, FDGPU_ARENA_SLACK);
+    const size_t asz = arena_sz + FDGPU_ARENA_SLACK - uploaded;
+    HIPCHK(hipMemcpyAsync(s->d_arena + uploaded, s->h_arena + uploaded, asz, hipMemcpyHostToDevice, s->stream),
+           FDGPU_ERR_DEVICE);
+  }
   if (ns) HIPCHK(hipMemcpyAsync(s->d_sigs, s->h_sigs, (size_t)ns * sizeof(fdgpu_sig_desc_t), hipMemcpyHostToDevice, s->stream), FDGPU_ERR_DEVICE);
   if (ns && perm) HIPCHK(hipMemcpyAsync(s->d_perm, perm, (size_t)ns * sizeof(uint32_t), hipMemcpyHostToDevice, s->stream), FDGPU_ERR_DEVICE);
   if (txn_cnt) HIPCHK(hipMemcpyAsync(s->d_txns, s->h_txns, txn_cnt * sizeof(fdgpu_txn_desc_t), hipMemcpyHostToDevice, s->stream), FDGPU_ERR_DEVICE);
@@ -353,9 +392,11 @@ int64_t fdgpu_submit(fdgpu_engine_t *e, uint8_t const *arena, uint64_t arena_sz,
                      uint64_t txn_cnt) {
   if (!e || (!arena && arena_sz) || (!txns && txn_cnt)) { set_err("null argument"); return FDGPU_ERR_INVAL; }
   if (arena_sz > e->cfg.max_arena || txn_cnt > e->cfg.max_txn) { set_err("batch exceeds engine limits"); return FDGPU_ERR_INVAL; }
+  std::lock_guard<std::mutex> lk(e->ring_mu);
   HIPCHK(hipSetDevice(e->device), FDGPU_ERR_DEVICE);
   Slot *s = free_slot(e);
   if (!s) { set_err("all ring slots hold unpolled batches"); return FDGPU_ERR_FULL; }
+  if (region_covers(e, arena, arena_sz)) return submit_slot(e, s, arena_sz, txns, txn_cnt, 0, arena);
   /* the slot's previous batch was polled, so its copies are complete */
   const uint64_t up = stage_arena(e, s, arena, arena_sz);
   if (up == UINT64_MAX) return FDGPU_ERR_DEVICE;
@@ -364,6 +405,7 @@ int64_t fdgpu_submit(fdgpu_engine_t *e, uint8_t const *arena, uint64_t arena_sz,
 
 uint8_t *fdgpu_stage_acquire(fdgpu_engine_t *e, uint64_t *cap) {
   if (!e) return nullptr;
+  std::lock_guard<std::mutex> lk(e->ring_mu);
   for (auto &c : e->slots) if (c.staged) { set_err("a slot is already staged"); return nullptr; }
   Slot *s = free_slot(e);
   if (!s) { set_err("all ring slots hold unpolled batches"); return nullptr; }
@@ -374,6 +416,7 @@ uint8_t *fdgpu_stage_acquire(fdgpu_engine_t *e, uint64_t *cap) {
 
 int64_t fdgpu_stage_submit(fdgpu_engine_t *e, uint64_t arena_sz, fdgpu_txn_t const *txns, uint64_t txn_cnt) {
   if (!e || (!txns && txn_cnt)) { set_err("null argument"); return FDGPU_ERR_INVAL; }
+  std::lock_guard<std::mutex> lk(e->ring_mu);
   Slot *s = nullptr;
   for (auto &c : e->slots) if (c.staged) { s = &c; break; }
   if (!s) { set_err("no staged slot"); return FDGPU_ERR_INVAL; }
@@ -384,12 +427,15 @@ int64_t fdgpu_stage_submit(fdgpu_engine_t *e, uint64_t arena_sz, fdgpu_txn_t con
 
 static int poll_slot(fdgpu_engine_t *e, int64_t ticket, int8_t *txn_codes, int blocking, bool keep) {
   if (!e) return FDGPU_ERR_INVAL;
+  std::unique_lock<std::mutex> lk(e->ring_mu);
   Slot *s = nullptr;
   for (auto &c : e->slots) if (c.ticket == ticket && ticket >= 0 && !c.held) { s = &c; break; }
   if (!s) { set_err("unknown ticket %lld", (long long)ticket); return FDGPU_ERR_TICKET; }
   HIPCHK(hipSetDevice(e->device), FDGPU_ERR_DEVICE);
   if (blocking) {
+    lk.unlock();                               /* the slot is this caller's until it is polled */
     HIPCHK(hipEventSynchronize(s->done), FDGPU_ERR_DEVICE);
+    lk.lock();
   } else {
     hipError_t q = hipEventQuery(s->done);
     if (q == hipErrorNotReady) return FDGPU_PENDING;
@@ -411,16 +457,53 @@ int fdgpu_poll_keep(fdgpu_engine_t *e, int64_t ticket, int8_t *txn_codes, int bl
 
 int fdgpu_stage_cancel(fdgpu_engine_t *e) {
   if (!e) return FDGPU_ERR_INVAL;
+  std::lock_guard<std::mutex> lk(e->ring_mu);
   for (auto &c : e->slots) if (c.staged) { c.staged = false; return FDGPU_OK; }
   return FDGPU_ERR_INVAL;
 }
 
 int fdgpu_release(fdgpu_engine_t *e, int64_t ticket) {
   if (!e) return FDGPU_ERR_INVAL;
+  std::lock_guard<std::mutex> lk(e->ring_mu);
   for (auto &c : e->slots)
     if (c.ticket == ticket && ticket >= 0 && c.held) { c.held = false; c.ticket = -1; return FDGPU_OK; }
   set_err("ticket %lld not held", (long long)ticket);
   return FDGPU_ERR_TICKET;
+}
+
+int fdgpu_host_register(fdgpu_engine_t *e, void *p, uint64_t sz) {
+  if (!e || !p || !sz) { set_err("null argument"); return FDGPU_ERR_INVAL; }
+  const uintptr_t a = (uintptr_t)p & ~(uintptr_t)4095, b = ((uintptr_t)p + sz + 4095) & ~(uintptr_t)4095;
+  std::lock_guard<std::mutex> lk(e->ring_mu);
+  if (region_covers(e, (const uint8_t *)p, sz)) return FDGPU_OK;
+  std::lock_guard<std::mutex> rk(g_reg_mu);
+  auto it = g_regions.find(a);
+  if (it != g_regions.end() && it->second.first >= b - a) {
+    it->second.second++;
+  } else {
+    if (it != g_regions.end()) { set_err("region overlaps a smaller registered one"); return FDGPU_ERR_INVAL; }
+    HIPCHK(hipSetDevice(e->device), FDGPU_ERR_DEVICE);
+    HIPCHK(hipHostRegister((void *)a, b - a, hipHostRegisterPortable), FDGPU_ERR_DEVICE);
+    g_regions[a] = {b - a, 1};
+    it = g_regions.find(a);
+  }
+  e->regions.push_back({a, it->second.first});
+  return FDGPU_OK;
+}
+
+int fdgpu_host_unregister(fdgpu_engine_t *e, void *p) {
+  if (!e || !p) return FDGPU_ERR_INVAL;
+  const uintptr_t a = (uintptr_t)p & ~(uintptr_t)4095;
+  std::lock_guard<std::mutex> lk(e->ring_mu);
+  for (size_t i = 0; i < e->regions.size(); i++) {
+    if (e->regions[i].first != a) continue;
+    for (auto &sl : e->slots) if (sl.stream) (void)hipStreamSynchronize(sl.stream);   /* no DMA still reads it */
+    unregister_one(e, a);
+    e->regions.erase(e->regions.begin() + (long)i);
+    return FDGPU_OK;
+  }
+  set_err("region not registered with this engine");
+  return FDGPU_ERR_INVAL;
 }
 
 int fdgpu_verify_device(fdgpu_engine_t *e, void const *d_arena, void const *d_sig_desc, uint64_t sig_cnt,

@@ -1,0 +1,512 @@
+/* fdt_mux.cpp -- the reference's mux tile API restated (fdt_mux_run,
+   fdt_mux_publish: src/disco/mux/fd_mux.h:106-299,484-496 and the run loop
+   of fd_mux.c:387-699), and the batched GPU verify tile written as mux
+   callbacks (fdgpu_vmux_*: fd_verify.c:36-148,232-246).  See
+   include/fd_verify_tile.h for the contract. */
+#include <time.h>
+
+#include <algorithm>
+#include <atomic>
+#include <cstring>
+#include <deque>
+#include <new>
+#include <vector>
+
+#include "../../../include/fd_verify_tile.h"
+
+namespace {
+
+inline uint64_t now_ns() {
+  timespec ts;
+  clock_gettime(CLOCK_MONOTONIC, &ts);
+  return (uint64_t)ts.tv_sec * 1000000000ull + (uint64_t)ts.tv_nsec;
+}
+inline uint64_t ld_acq(const uint64_t *p) { return __atomic_load_n(p, __ATOMIC_ACQUIRE); }
+inline void st_rel(uint64_t *p, uint64_t v) { __atomic_store_n(p, v, __ATOMIC_RELEASE); }
+inline bool pow2(uint64_t x) { return x && !(x & (x - 1)); }
+inline uint64_t align2(uint64_t x) { return (x + 1) & ~1ull; }
+
+}  // namespace
+
+/* ------------------------------------------------------------------ mux */
+
+extern "C" {
+
+void fdt_mux_publish(fdt_mux_context_t *ctx, uint64_t sig, uint64_t chunk, uint64_t sz, uint64_t ctl,
+                     uint64_t tsorig, uint64_t tspub) {
+  const uint64_t seq = *ctx->seq;
+  fdt_mcache_publish(ctx->mcache, ctx->depth, seq, sig, chunk, sz, ctl, tsorig, tspub);
+  *ctx->cr_avail -= ctx->cr_decrement_amount;
+  *ctx->seq = seq + 1;
+}
+
+int fdt_mux_run(const fdt_mux_cfg_t *cfg, const fdt_mux_callbacks_t *cb, void *ctx, const volatile uint64_t *halt,
+                fdt_mux_stats_t *stats_out) {
+  if (!cfg || !cb || cfg->in_cnt > FDT_MUX_IN_MAX || cfg->out_cnt > FDT_MUX_OUT_MAX) return -1;
+  const uint64_t in_cnt = cfg->in_cnt, out_cnt = cfg->out_cnt, flags = cfg->flags;
+  const bool copy = (flags & FDT_MUX_FLAG_COPY) != 0;
+  uint64_t min_in_depth = UINT64_MAX;
+  for (uint64_t i = 0; i < in_cnt; i++) {
+    if (!cfg->in_mcache[i] || !pow2(cfg->in_depth[i])) return -1;
+    min_in_depth = std::min(min_in_depth, cfg->in_depth[i]);
+  }
+  /* out stream (fd_mux.c:209-219: no mcache -> a 128-deep dummy, no consumers) */
+  fdt_frag_meta_t *mcache = cfg->out_mcache;
+  const uint64_t depth = mcache ? cfg->out_depth : 128;
+  if (mcache && !pow2(depth)) return -1;
+  if (!mcache && out_cnt) return -1;
+  for (uint64_t j = 0; j < out_cnt; j++) if (!cfg->out_fseq[j]) return -1;
+  /* credits (fd_mux.c:326-335) */
+  const uint64_t cr_max_max = copy ? depth : std::min(min_in_depth, depth);
+  const uint64_t cr_max = cfg->cr_max ? cfg->cr_max : cr_max_max;
+  if (cr_max < 1 || cr_max > cr_max_max) return -1;
+  const uint64_t burst = cfg->burst ? cfg->burst : 1;
+  const uint64_t lazy = cfg->lazy_iters ? cfg->lazy_iters : 16;
+
+  uint64_t in_seq[FDT_MUX_IN_MAX], out_seq[FDT_MUX_OUT_MAX];
+  for (uint64_t i = 0; i < in_cnt; i++) in_seq[i] = cfg->in_seq0[i];
+  for (uint64_t j = 0; j < out_cnt; j++) out_seq[j] = ld_acq(cfg->out_fseq[j]);
+  uint64_t seq = cfg->out_seq0, cr_avail = 0, cr_filt = 0, in_rr = 0;
+  fdt_mux_stats_t st{};
+  for (uint64_t it = 0;; it++) {
+    st.loops++;
+    if (it % lazy == 0) {
+      /* housekeeping (fd_mux.c:391-491): receive credits from the outs, send
+         our position to the ins, user callbacks, halt (the cnc signal) */
+      for (uint64_t j = 0; j < out_cnt; j++) out_seq[j] = ld_acq(cfg->out_fseq[j]);
+      const uint64_t exposed = copy ? 0 : cr_max - cr_avail + cr_filt;
+      for (uint64_t i = 0; i < in_cnt; i++) if (cfg->in_fseq[i]) st_rel(cfg->in_fseq[i], in_seq[i] - exposed);
+      if (cb->metrics_write) cb->metrics_write(ctx);
+      if (halt && *halt) break;
+      if (cr_avail < cr_max) {
+        cr_avail = cr_max;
+        for (uint64_t j = 0; j < out_cnt; j++) {
+          const int64_t lag = std::max<int64_t>((int64_t)(seq - out_seq[j]), 0);
+          const uint64_t out_cr = (uint64_t)std::max<int64_t>((int64_t)cr_max - lag, 0);
+          cr_avail = std::min(cr_avail, out_cr);
+        }
+        if (cr_avail == cr_max) cr_filt = 0;
+      }
+      if (cb->during_housekeeping) cb->during_housekeeping(ctx);
+    }
+
+    fdt_mux_context_t mux = {mcache, depth, &cr_avail, &seq, out_cnt ? 1ull : 0ull};
+    if (cb->before_credit) cb->before_credit(ctx, &mux);
+    if (cr_avail < cr_filt + burst) { st.backpressure++; continue; }   /* fd_mux.c:548-556 */
+    int poll_in = 1;
+    if (cb->after_credit) cb->after_credit(ctx, &mux, &poll_in);
+    if (!poll_in || !in_cnt) continue;
+
+    const uint64_t i = in_rr;
+    in_rr = in_rr + 1 == in_cnt ? 0 : in_rr + 1;
+    const fdt_frag_meta_t *line = cfg->in_mcache[i] + (in_seq[i] & (cfg->in_depth[i] - 1));
+    const uint64_t seq_found = ld_acq(&line->seq);
+    const int64_t diff = (int64_t)(in_seq[i] - seq_found);
+    if (diff) {                                     /* caught up, or overrun (fd_mux.c:595-609) */
+      if (diff < 0) { st.overrun_polling += (uint64_t)(-diff); in_seq[i] = seq_found; }
+      continue;
+    }
+    uint64_t sig = line->sig;
+    st.in_frags++;
+    if (cb->before_frag) {
+      int filter = 0;
+      cb->before_frag(ctx, i, seq_found, sig, &filter);
+      if (filter) {
+        if (!copy) cr_filt += (uint64_t)(cr_avail < cr_max);
+        in_seq[i]++;
+        st.filtered_before++;
+        continue;
+      }
+    }
+    std::atomic_thread_fence(std::memory_order_acquire);
+    uint64_t chunk = line->chunk, sz = line->sz;
+    const uint64_t ctl = line->ctl, tsorig = line->tsorig;
+    std::atomic_thread_fence(std::memory_order_acquire);
+    const uint64_t seq_test = ld_acq(&line->seq);
+    int filter = 0;
+    if (cb->during_frag) cb->during_frag(ctx, i, seq_found, sig, chunk, sz, &filter);
+    /* the reference checks the seq read before during_frag (fd_mux.c:641-655);
+       the quic -> verify link has no backpressure, so the payload copy is
+       checked too */
+    const uint64_t seq_test2 = ld_acq(&line->seq);
+    if (seq_test != seq_found || seq_test2 != seq_found) {
+      st.overrun_reading++;
+      in_seq[i] = seq_test2;
+      continue;
+    }
+    uint64_t out_sz = sz, out_tsorig = tsorig;
+    if (!filter && cb->after_frag) cb->after_frag(ctx, i, seq_found, &sig, &chunk, &out_sz, &out_tsorig, &filter, &mux);
+    if (filter) {
+      if (!copy) cr_filt += (uint64_t)(cr_avail < cr_max);
+      st.filtered_after++;
+    } else if (!(flags & FDT_MUX_FLAG_MANUAL_PUBLISH)) {
+      fdt_mux_publish(&mux, sig, chunk, out_sz, ctl, out_tsorig, (uint32_t)now_ns());
+      st.published++;
+    }
+    in_seq[i]++;
+  }
+  /* halting (fd_mux.c:701-714): every exposed frag counts as consumed */
+  for (uint64_t i = 0; i < in_cnt; i++) if (cfg->in_fseq[i]) st_rel(cfg->in_fseq[i], in_seq[i]);
+  if (stats_out) *stats_out = st;
+  return 0;
+}
+
+}  // extern "C"
+
+/* ------------------------------------------------------------ vmux tile */
+
+namespace {
+
+struct VItem {
+  uint64_t seq;
+  uint32_t chunk;       /* where [payload][pad][fd_txn_t][u16 sz] lies in the out dcache */
+  uint32_t sz;          /* that frag's size */
+  uint32_t sig_off;     /* signature 0, from the frag start */
+  uint32_t tsorig;
+};
+
+struct VBatch {
+  uint64_t first_chunk = 0;          /* the arena is out_base + first_chunk * 64 ... + end_off */
+  uint64_t end_off = 0;
+  std::vector<fdgpu_txn_t> txns;
+  std::vector<VItem> items;
+  std::vector<int8_t> codes;
+  uint64_t sig_cnt = 0;
+  int64_t ticket = -1;
+  bool closed = false;               /* takes no more frags (full, or the cursor wrapped) */
+  bool done = false;
+  size_t next = 0;                   /* next item to resolve */
+  uint64_t t_first = 0;
+
+  void reset() {
+    first_chunk = end_off = sig_cnt = 0;
+    txns.clear(); items.clear();
+    ticket = -1; closed = done = false; next = 0; t_first = 0;
+  }
+};
+
+constexpr uint64_t FRAG_CHUNKS = (FDT_TPU_DCACHE_MTU + FDT_CHUNK_SZ - 1) / FDT_CHUNK_SZ;   /* a maximal out frag */
+
+}  // namespace
+
+struct fdgpu_vmux {
+  fdgpu_vmux_cfg_t cfg{};
+  fdgpu_verifier_t ver{};
+  std::vector<uint64_t> tcache_mem;
+  void *tcache = nullptr;
+  uint64_t out_chunk = 0;                 /* write cursor */
+  uint64_t cur_sz = 0;                    /* the frag between during_frag and after_frag */
+  bool cur_ok = false;
+  std::vector<VBatch> storage;
+  std::vector<VBatch *> pool;
+  std::deque<VBatch *> inflight;
+  VBatch *open = nullptr;
+  std::vector<uint32_t> pub_chunk;        /* chunk of each recently published out seq */
+  uint64_t pub_mask = 0, published_total = 0;
+  int error = 0;
+  uint32_t calls = 0;                     /* after_credit calls (rate-limits verifier polls) */
+  fdgpu_vtile_stats_t st{};
+  std::vector<uint64_t> lat;
+  uint64_t log_max = 0;
+  std::vector<uint64_t> log_seq;
+  std::vector<int8_t> log_code;
+
+  std::atomic<uint64_t> final_cnt{0};    /* frags whose outcome is final (readable from other threads) */
+
+  void log(uint64_t seq, int code) {
+    if (log_seq.size() < log_max) { log_seq.push_back(seq); log_code.push_back((int8_t)code); }
+    final_cnt.fetch_add(1, std::memory_order_release);
+  }
+
+  uint8_t *out_laddr(uint64_t chunk) const { return cfg.out_base + (chunk << FDT_CHUNK_LG_SZ); }
+
+  /* chunk of the oldest frag that may still be read: published and possibly
+     unconsumed (the mux's exposed count), else reserved by an unresolved
+     batch item; false when nothing is live */
+  bool live_tail(const fdt_mux_context_t *mux, uint64_t &tail) const {
+    uint64_t exposed = cfg.cr_max - std::min(cfg.cr_max, *mux->cr_avail);
+    exposed = std::min(exposed, published_total);
+    if (exposed) { tail = pub_chunk[(*mux->seq - exposed) & pub_mask]; return true; }
+    for (const VBatch *b : inflight)
+      if (b->next < b->items.size()) { tail = b->items[b->next].chunk; return true; }
+    if (open && !open->items.empty()) { tail = open->items.front().chunk; return true; }
+    return false;
+  }
+
+  /* room for one maximal frag at the cursor (the live region is [tail, cursor)
+     in ring order) */
+  bool room(const fdt_mux_context_t *mux) const {
+    uint64_t tail;
+    if (!live_tail(mux, tail)) return true;
+    const uint64_t w = out_chunk;
+    if (w > tail) return true;
+    if (w == tail) return false;
+    return w + FRAG_CHUNKS <= tail;
+  }
+
+  /* tag, tcache, publish -- strictly in ingest order (fd_verify.h:45-89,
+     fd_verify.c:138-147) */
+  void resolve(fdt_mux_context_t *mux, int *poll_in) {
+    while (!inflight.empty()) {
+      VBatch *b = inflight.front();
+      if (!b->done) {
+        const int rc = ver.poll(ver.ctx, b->ticket, b->codes.data(), 0);
+        if (rc == FDGPU_PENDING) return;
+        if (rc != FDGPU_OK) { error = rc; *poll_in = 0; return; }
+        b->done = true;
+      }
+      while (b->next < b->items.size()) {
+        const VItem &it = b->items[b->next];
+        const uint64_t tag = fdt_hash(cfg.hashmap_seed, out_laddr(it.chunk) + it.sig_off, 64);
+        int outcome;
+        if (fdt_tcache_query(tcache, tag)) outcome = FD_TXN_VERIFY_DEDUP;
+        else if (b->codes[b->next] != FD_ED25519_SUCCESS) outcome = FD_TXN_VERIFY_FAILED;
+        else outcome = FD_TXN_VERIFY_SUCCESS;
+        if (outcome == FD_TXN_VERIFY_SUCCESS) {
+          if (mux->cr_decrement_amount && !*mux->cr_avail) {
+            *poll_in = 0;                         /* out of credits: the mux refreshes them, then this item */
+            st.backpressure++;                    /* is resolved again from the top (nothing inserted yet) */
+            return;
+          }
+          (void)fdt_tcache_insert(tcache, tag);   /* not present: the query above missed */
+          pub_chunk[*mux->seq & pub_mask] = it.chunk;
+          fdt_mux_publish(mux, tag, it.chunk, it.sz, 0, it.tsorig, (uint32_t)now_ns());
+          published_total++;
+          st.published++;
+        } else if (outcome == FD_TXN_VERIFY_DEDUP) {
+          st.dedup++;
+        } else {
+          st.verify_failed++;
+        }
+        log(it.seq, outcome);
+        b->next++;
+      }
+      if (lat.size() < (1u << 22) && !b->items.empty()) lat.push_back(now_ns() - b->t_first);
+      inflight.pop_front();
+      b->reset();
+      pool.push_back(b);
+    }
+  }
+
+  /* the verifier refused the batch as malformed: its txns fail (logged),
+     nothing is published, the tile goes on (device errors stay fatal) */
+  void reject_open() {
+    for (const VItem &it : open->items) { st.verify_errors++; log(it.seq, FD_TXN_VERIFY_FAILED); }
+    open->reset();
+    pool.push_back(open);
+    open = nullptr;
+  }
+
+  void submit() {
+    if (!open || open->items.empty()) return;
+    if (!open->closed && now_ns() - open->t_first < cfg.batch_wait_ns) return;
+    if (inflight.size() >= cfg.inflight_max) return;
+    const int64_t t = ver.submit(ver.ctx, out_laddr(open->first_chunk), open->end_off, open->txns.data(),
+                                 open->txns.size());
+    if (t == FDGPU_ERR_FULL) return;
+    if (t == FDGPU_ERR_INVAL) { reject_open(); return; }
+    if (t < 0) { error = (int)t; return; }
+    open->ticket = t;
+    inflight.push_back(open);
+    open = nullptr;
+    st.batches++;
+  }
+
+  bool can_take() {
+    if (open && open->closed) return false;
+    if (!open) {
+      if (pool.empty()) return false;
+      open = pool.back();
+      pool.pop_back();
+    }
+    return true;
+  }
+};
+
+namespace {
+
+void vm_before_frag(void *ctx, uint64_t in_idx, uint64_t seq, uint64_t sig, int *opt_filter) {
+  (void)in_idx; (void)sig;
+  auto *t = (fdgpu_vmux *)ctx;
+  t->st.in_frags++;
+  if (t->cfg.round_robin_cnt > 1 && seq % t->cfg.round_robin_cnt != t->cfg.round_robin_idx) {
+    *opt_filter = 1;
+    t->st.filtered_rr++;
+    t->log(seq, FDGPU_VTILE_LOG_FILTERED);
+  }
+}
+
+void vm_during_frag(void *ctx, uint64_t in_idx, uint64_t seq, uint64_t sig, uint64_t chunk, uint64_t sz,
+                    int *opt_filter) {
+  (void)sig;
+  auto *t = (fdgpu_vmux *)ctx;
+  const fdgpu_vmux_cfg_t &c = t->cfg;
+  t->cur_ok = false;
+  if (chunk < c.in_chunk0[in_idx] || chunk > c.in_wmark[in_idx] || sz > FDT_TPU_MTU) {
+    /* the reference aborts the tile here (FD_LOG_ERR, fd_verify.c:67-68) */
+    t->st.corrupt++;
+    t->log(seq, FDGPU_VTILE_LOG_LOST);
+    *opt_filter = 1;
+    return;
+  }
+  std::memcpy(t->out_laddr(t->out_chunk), c.in_base[in_idx] + (chunk << FDT_CHUNK_LG_SZ), sz);
+  t->cur_sz = sz;
+  t->cur_ok = true;
+}
+
+void vm_after_frag(void *ctx, uint64_t in_idx, uint64_t seq, uint64_t *opt_sig, uint64_t *opt_chunk,
+                   uint64_t *opt_sz, uint64_t *opt_tsorig, int *opt_filter, fdt_mux_context_t *mux) {
+  (void)in_idx; (void)opt_sig; (void)opt_chunk; (void)mux;
+  auto *t = (fdgpu_vmux *)ctx;
+  if (!t->cur_ok) { *opt_filter = 1; return; }
+  const uint64_t payload_sz = *opt_sz;
+  uint8_t *txn = t->out_laddr(t->out_chunk);
+  const uint64_t toff = align2(payload_sz);
+  uint8_t *txn_t = txn + toff;
+  if (toff != payload_sz) txn[payload_sz] = 0;
+  const uint64_t tsz = fdt_txn_parse(txn, payload_sz, txn_t, nullptr);
+  if (!tsz) {                                           /* fd_verify.c:117-121 */
+    t->st.parse_fail++;
+    t->log(seq, FDGPU_VTILE_LOG_PARSE_FAIL);
+    *opt_filter = 1;
+    return;
+  }
+  const uint16_t psz = (uint16_t)payload_sz;
+  std::memcpy(txn_t + tsz, &psz, 2);
+  const uint64_t new_sz = toff + tsz + 2;
+  const fdt_txn_t *tt = (const fdt_txn_t *)txn_t;
+  VBatch &b = *t->open;                                 /* after_credit made sure one is open */
+  if (b.items.empty()) { b.first_chunk = t->out_chunk; b.t_first = now_ns(); }
+  const uint64_t off = (t->out_chunk - b.first_chunk) << FDT_CHUNK_LG_SZ;
+  fdgpu_txn_t d;
+  d.msg_off = (uint32_t)(off + tt->message_off);
+  d.msg_sz = (uint32_t)(payload_sz - tt->message_off);
+  d.sig_off = (uint32_t)(off + tt->signature_off);
+  d.pub_off = (uint32_t)(off + tt->acct_addr_off);
+  d.sig_cnt = tt->signature_cnt;
+  b.txns.push_back(d);
+  b.items.push_back(VItem{seq, (uint32_t)t->out_chunk, (uint32_t)new_sz, tt->signature_off, (uint32_t)*opt_tsorig});
+  b.end_off = off + new_sz;
+  if (tt->signature_cnt <= 16) { b.sig_cnt += tt->signature_cnt; t->st.sigs += tt->signature_cnt; }
+  t->out_chunk = fdt_dcache_compact_next(t->out_chunk, new_sz, t->cfg.out_chunk0, t->cfg.out_wmark);
+  /* the arena must stay one contiguous run of chunks: a wrapped cursor closes it */
+  if (t->out_chunk <= b.first_chunk || b.items.size() >= t->cfg.batch_txn_max ||
+      b.sig_cnt + 16 > t->cfg.batch_sig_max || b.end_off + FRAG_CHUNKS * FDT_CHUNK_SZ > t->cfg.batch_bytes_max)
+    b.closed = true;
+  /* accepted: published later, in order, by after_credit (MANUAL_PUBLISH) */
+}
+
+/* after_credit runs once per mux loop iteration, i.e. about once per frag:
+   the verifier is polled (an event query) and the partial-batch timer read
+   only every 32nd call, or at once when the tile cannot take the next frag
+   or is mid-way through publishing a completed batch. */
+void vm_after_credit(void *ctx, fdt_mux_context_t *mux, int *opt_poll_in) {
+  auto *t = (fdgpu_vmux *)ctx;
+  if (t->error) { *opt_poll_in = 0; return; }
+  const bool due = (++t->calls & 31u) == 0;
+  const bool stuck = t->open ? t->open->closed : t->pool.empty();
+  if (due || stuck || (!t->inflight.empty() && t->inflight.front()->done)) t->resolve(mux, opt_poll_in);
+  if (due || stuck) t->submit();
+  if (!*opt_poll_in || t->error || !t->can_take()) { *opt_poll_in = 0; return; }
+  if (!t->room(mux)) { *opt_poll_in = 0; t->st.backpressure++; }
+}
+
+}  // namespace
+
+extern "C" {
+
+uint64_t fdgpu_vmux_dcache_data_sz(uint64_t cr_max, uint32_t batch_txn_max, uint32_t inflight_max) {
+  if (!inflight_max) inflight_max = 2;
+  return (cr_max + (uint64_t)(inflight_max + 1) * batch_txn_max + 2) * FRAG_CHUNKS * FDT_CHUNK_SZ;
+}
+
+fdgpu_vmux_t *fdgpu_vmux_new(const fdgpu_vmux_cfg_t *cfg, fdgpu_verifier_t ver) {
+  if (!cfg || !ver.submit || !ver.poll || !cfg->out_base || !cfg->batch_txn_max || !cfg->cr_max ||
+      cfg->in_cnt > FDT_MUX_IN_MAX || cfg->out_wmark < cfg->out_chunk0)
+    return nullptr;
+  for (uint64_t i = 0; i < cfg->in_cnt; i++) if (!cfg->in_base[i]) return nullptr;
+  auto *t = new (std::nothrow) fdgpu_vmux;
+  if (!t) return nullptr;
+  t->cfg = *cfg;
+  fdgpu_vmux_cfg_t &c = t->cfg;
+  if (!c.round_robin_cnt) c.round_robin_cnt = 1;
+  if (!c.inflight_max) c.inflight_max = 2;
+  if (!c.tcache_depth) c.tcache_depth = FDT_VERIFY_TCACHE_DEPTH;
+  if (!cfg->tcache_depth && !c.tcache_map_cnt) c.tcache_map_cnt = FDT_VERIFY_TCACHE_MAP_CNT;
+  if (!c.batch_sig_max) c.batch_sig_max = std::max<uint64_t>(16, (uint64_t)c.batch_txn_max * 12);
+  if (!c.batch_bytes_max) c.batch_bytes_max = (uint64_t)c.batch_txn_max * FRAG_CHUNKS * FDT_CHUNK_SZ;
+  /* the ring must hold two maximal frags; a batch one */
+  if (c.batch_sig_max < 16 || c.batch_bytes_max < FRAG_CHUNKS * FDT_CHUNK_SZ ||
+      c.out_wmark - c.out_chunk0 < 2 * FRAG_CHUNKS) {
+    delete t;
+    return nullptr;
+  }
+  const uint64_t fp = fdt_tcache_footprint(c.tcache_depth, c.tcache_map_cnt);
+  if (!fp) { delete t; return nullptr; }
+  t->tcache_mem.assign(fp / 8, 0);
+  t->tcache = fdt_tcache_new(t->tcache_mem.data(), c.tcache_depth, c.tcache_map_cnt);
+  t->ver = ver;
+  t->out_chunk = c.out_chunk0;
+  uint64_t n = 1;
+  while (n < c.cr_max) n <<= 1;
+  t->pub_chunk.assign(n, 0);
+  t->pub_mask = n - 1;
+  t->storage.resize(c.inflight_max + 1);
+  for (auto &b : t->storage) {
+    b.codes.resize(c.batch_txn_max);
+    b.txns.reserve(c.batch_txn_max);
+    b.items.reserve(c.batch_txn_max);
+    t->pool.push_back(&b);
+  }
+  return t;
+}
+
+void fdgpu_vmux_delete(fdgpu_vmux_t *t) {
+  if (!t) return;
+  for (VBatch *b : t->inflight)                 /* the verifier may still write codes / read the arena */
+    if (!b->done) t->ver.poll(t->ver.ctx, b->ticket, b->codes.data(), 1);
+  delete t;
+}
+
+fdt_mux_callbacks_t fdgpu_vmux_callbacks(void) {
+  fdt_mux_callbacks_t cb{};
+  cb.before_frag = vm_before_frag;
+  cb.during_frag = vm_during_frag;
+  cb.after_frag = vm_after_frag;
+  cb.after_credit = vm_after_credit;
+  return cb;
+}
+
+void fdgpu_vmux_stats(const fdgpu_vmux_t *t, fdgpu_vtile_stats_t *out) {
+  *out = t->st;
+  out->lat_cnt = t->lat.size();
+}
+
+int fdgpu_vmux_idle(const fdgpu_vmux_t *t) {
+  return t->inflight.empty() && (!t->open || t->open->items.empty());
+}
+
+int fdgpu_vmux_error(const fdgpu_vmux_t *t) { return t->error; }
+
+uint64_t fdgpu_vmux_final_cnt(const fdgpu_vmux_t *t) { return t->final_cnt.load(std::memory_order_acquire); }
+
+uint64_t fdgpu_vmux_latencies(const fdgpu_vmux_t *t, uint64_t *out, uint64_t max) {
+  const uint64_t n = std::min<uint64_t>(max, t->lat.size());
+  std::memcpy(out, t->lat.data(), n * 8);
+  return n;
+}
+
+void fdgpu_vmux_log_enable(fdgpu_vmux_t *t, uint64_t log_max) {
+  t->log_max = log_max;
+  t->log_seq.reserve(log_max);
+  t->log_code.reserve(log_max);
+}
+
+uint64_t fdgpu_vmux_log(const fdgpu_vmux_t *t, uint64_t *seqs, int8_t *codes, uint64_t max) {
+  const uint64_t n = std::min<uint64_t>(max, t->log_seq.size());
+  std::memcpy(seqs, t->log_seq.data(), n * 8);
+  std::memcpy(codes, t->log_code.data(), n);
+  return n;
+}
+
+}  // extern "C"

@@ -96,11 +96,26 @@ class VerifyEngine:
                  (FLAG_FULL_PATH if full_path else 0))
         cfg = _lib.FdgpuCfg(max_txn, self.max_sig, max_arena or 1232 * max_txn, ring_depth, flags)
         self._cfg = cfg
+        self.max_arena = cfg.max_arena
         self._h = L.fdgpu_engine_open(int(device), ctypes.byref(cfg))
         if not self._h:
             raise RuntimeError(f"fdgpu_engine_open({device}) failed: {_lib.last_error()}")
         self.device = device
         self._pending = {}
+
+    def host_register(self, buf):
+        """Registers a long-lived host buffer (numpy array) for direct DMA:
+        batches whose arena lies inside it upload with no staging copy
+        (fdgpu_host_register)."""
+        arr = np.asarray(buf)
+        r = _lib.lib().fdgpu_host_register(self._h, arr.ctypes.data, arr.nbytes)
+        if r:
+            raise RuntimeError(f"fdgpu_host_register failed: {r} ({_lib.last_error()})")
+
+    def host_unregister(self, buf):
+        r = _lib.lib().fdgpu_host_unregister(self._h, np.asarray(buf).ctypes.data)
+        if r:
+            raise RuntimeError(f"fdgpu_host_unregister failed: {r} ({_lib.last_error()})")
 
     def close(self):
         if self._h:

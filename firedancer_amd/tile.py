@@ -121,6 +121,43 @@ class DTileStats(c.Structure):
         return {n: getattr(self, n) for n, _ in self._fields_}
 
 
+MUX_FLAG_DEFAULT, MUX_FLAG_MANUAL_PUBLISH, MUX_FLAG_COPY = 0, 1, 2
+MUX_IN_MAX = 16
+
+
+class MuxCfg(c.Structure):
+    """fdt_mux_cfg_t (the reference mux run loop's configuration)."""
+    _fields_ = [("in_cnt", c.c_uint64), ("in_mcache", vp * MUX_IN_MAX), ("in_depth", c.c_uint64 * MUX_IN_MAX),
+                ("in_seq0", c.c_uint64 * MUX_IN_MAX), ("in_fseq", vp * MUX_IN_MAX),
+                ("out_mcache", vp), ("out_depth", c.c_uint64), ("out_seq0", c.c_uint64), ("out_cnt", c.c_uint64),
+                ("out_fseq", vp * MUX_IN_MAX), ("flags", c.c_uint64), ("burst", c.c_uint64),
+                ("cr_max", c.c_uint64), ("lazy_iters", c.c_uint64)]
+
+
+class MuxCallbacks(c.Structure):
+    """fdt_mux_callbacks_t (fd_mux_callbacks_t, fd_mux.h:288-299)."""
+    _fields_ = [(n, vp) for n in ("during_housekeeping", "before_credit", "after_credit", "before_frag",
+                                  "during_frag", "after_frag", "metrics_write")]
+
+
+class MuxStats(c.Structure):
+    _fields_ = [(n, c.c_uint64) for n in ("in_frags", "filtered_before", "filtered_after", "overrun_polling",
+                                          "overrun_reading", "backpressure", "published", "loops")]
+
+    def as_dict(self):
+        return {n: getattr(self, n) for n, _ in self._fields_}
+
+
+class VMuxCfg(c.Structure):
+    """fdgpu_vmux_cfg_t (the verify tile as mux callbacks)."""
+    _fields_ = [("in_cnt", c.c_uint64), ("in_base", vp * MUX_IN_MAX), ("in_chunk0", c.c_uint64 * MUX_IN_MAX),
+                ("in_wmark", c.c_uint64 * MUX_IN_MAX), ("out_base", vp), ("out_chunk0", c.c_uint64),
+                ("out_wmark", c.c_uint64), ("cr_max", c.c_uint64), ("round_robin_idx", c.c_uint64),
+                ("round_robin_cnt", c.c_uint64), ("hashmap_seed", c.c_uint64), ("tcache_depth", c.c_uint64),
+                ("tcache_map_cnt", c.c_uint64), ("batch_txn_max", c.c_uint32), ("inflight_max", c.c_uint32),
+                ("batch_wait_ns", c.c_uint64), ("batch_sig_max", c.c_uint64), ("batch_bytes_max", c.c_uint64)]
+
+
 class LinkT(c.Structure):
     _fields_ = [("mcache", vp), ("depth", c.c_uint64), ("seq0", c.c_uint64), ("mtu", c.c_uint64),
                 ("base", vp), ("chunk0", c.c_uint64), ("wmark", c.c_uint64), ("fseq", vp)]
@@ -192,6 +229,20 @@ def lib():
         "fdt_sandbox_enter": (c.c_int, [c.c_int]),
         "fdgpu_dtile_run_sandboxed": (None, [vp, u64, u64, c.POINTER(DTileStats), c.c_int]),
         "fdgpu_producer_join": (u64, [vp, c.POINTER(c.c_double)]),
+        "fdt_mux_publish": (None, [vp, u64, u64, u64, u64, u64, u64]),
+        "fdt_mux_run": (c.c_int, [c.POINTER(MuxCfg), c.POINTER(MuxCallbacks), vp, c.POINTER(u64),
+                                  c.POINTER(MuxStats)]),
+        "fdgpu_vmux_new": (vp, [c.POINTER(VMuxCfg), Verifier]),
+        "fdgpu_vmux_delete": (None, [vp]),
+        "fdgpu_vmux_callbacks": (MuxCallbacks, []),
+        "fdgpu_vmux_dcache_data_sz": (u64, [u64, c.c_uint32, c.c_uint32]),
+        "fdgpu_vmux_stats": (None, [vp, c.POINTER(VTileStats)]),
+        "fdgpu_vmux_idle": (c.c_int, [vp]),
+        "fdgpu_vmux_error": (c.c_int, [vp]),
+        "fdgpu_vmux_final_cnt": (u64, [vp]),
+        "fdgpu_vmux_latencies": (u64, [vp, vp, u64]),
+        "fdgpu_vmux_log_enable": (None, [vp, u64]),
+        "fdgpu_vmux_log": (u64, [vp, vp, vp, u64]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -305,13 +356,14 @@ class Link:
     """One tango link: an mcache of `depth` frag metas and a compact dcache
     sized for `depth` frags of up to `mtu` bytes (chunk 0 = dcache start)."""
 
-    def __init__(self, depth, mtu, seq0=0):
+    def __init__(self, depth, mtu, seq0=0, data_sz=None):
         L = lib()
         if depth & (depth - 1):
             raise ValueError("depth must be a power of 2")
         self.depth, self.mtu, self.seq0 = depth, mtu, seq0
         self.mcache = _aligned(depth * 32, 128).view(FRAG_META_DTYPE)
-        data_sz = L.fdt_dcache_data_sz(mtu, depth)
+        data_sz = data_sz or L.fdt_dcache_data_sz(mtu, depth)   # explicit: a dcache sized by its producer
+        data_sz = (data_sz + CHUNK_SZ - 1) // CHUNK_SZ * CHUNK_SZ
         self.dcache = _aligned(data_sz, 4096)
         self.chunk0 = 0
         self.chunk1 = data_sz // CHUNK_SZ
@@ -536,6 +588,7 @@ class EngineVerifier:
         L = lib()
         self.engines = list(engines)
         self.sig_max = min(e.max_sig for e in self.engines)     # signatures per batch every engine accepts
+        self.arena_max = min(e.max_arena for e in self.engines)
         arr = (vp * len(self.engines))(*[e._h for e in self.engines])
         self._d = L.fdgpu_dispatch_new(arr, len(self.engines))
         if not self._d:
@@ -662,6 +715,140 @@ class VerifyTile:
             self.close()
         except Exception:
             pass
+
+
+class VerifyMuxTile:
+    """The verify tile as the reference's mux callbacks (fdgpu_vmux, run by
+    fdt_mux_run with FD_MUX_FLAG_COPY | FD_MUX_FLAG_MANUAL_PUBLISH, burst 1;
+    fd_verify.c:232-246) on its own thread.  Frags are copied into the out
+    link's dcache (registered with every engine of an EngineVerifier, so the
+    GPU reads the batch from there with no staging copy) and published from
+    there in order.  `flow_control`: the out link's fseq is the mux's one
+    reliable consumer (otherwise published frags count as consumed)."""
+
+    def __init__(self, in_links, out_link, verifier, hashmap_seed=0x5EEDF00D, batch_txn_max=4096, inflight_max=2,
+                 batch_wait_us=200, round_robin_idx=0, round_robin_cnt=1, cr_max=0, log_max=0, batch_sig_max=0,
+                 batch_bytes_max=0, lazy_iters=16, flow_control=False, register=True):
+        import threading
+        L = lib()
+        in_links = list(in_links) if isinstance(in_links, (list, tuple)) else [in_links]
+        self.verifier, self.in_links, self.out_link = verifier, in_links, out_link
+        self.cr_max = cr_max or out_link.depth
+        vc = VMuxCfg()
+        vc.in_cnt = len(in_links)
+        for i, ln in enumerate(in_links):
+            vc.in_base[i], vc.in_chunk0[i], vc.in_wmark[i] = ln.base_ptr, ln.chunk0, ln.wmark
+        vc.out_base, vc.out_chunk0, vc.out_wmark = out_link.base_ptr, out_link.chunk0, out_link.wmark
+        vc.cr_max, vc.round_robin_idx, vc.round_robin_cnt = self.cr_max, round_robin_idx, round_robin_cnt
+        vc.hashmap_seed, vc.batch_txn_max, vc.inflight_max = hashmap_seed, batch_txn_max, inflight_max
+        vc.batch_wait_ns = int(batch_wait_us * 1000)
+        vc.batch_sig_max = batch_sig_max or getattr(verifier, "sig_max", 0)
+        vc.batch_bytes_max = batch_bytes_max or getattr(verifier, "arena_max", 0)
+        self.vcfg = vc
+        self._t = L.fdgpu_vmux_new(c.byref(vc), verifier.struct)
+        if not self._t:
+            raise RuntimeError("fdgpu_vmux_new: bad configuration")
+        if log_max:
+            L.fdgpu_vmux_log_enable(self._t, log_max)
+        mc = MuxCfg()
+        mc.in_cnt = len(in_links)
+        for i, ln in enumerate(in_links):
+            mc.in_mcache[i], mc.in_depth[i], mc.in_seq0[i] = ln.mcache_ptr, ln.depth, ln.seq0
+        mc.out_mcache, mc.out_depth, mc.out_seq0 = out_link.mcache_ptr, out_link.depth, out_link.seq0
+        if flow_control:
+            mc.out_cnt, mc.out_fseq[0] = 1, out_link.fseq.ctypes.data
+        mc.flags, mc.burst, mc.cr_max, mc.lazy_iters = MUX_FLAG_COPY | MUX_FLAG_MANUAL_PUBLISH, 1, self.cr_max, lazy_iters
+        self.mcfg = mc
+        self.cb = L.fdgpu_vmux_callbacks()
+        self._halt = c.c_uint64(0)
+        self._mstats = MuxStats()
+        self._rc = None
+        self._registered = []
+        if register:
+            for e in getattr(verifier, "engines", []):
+                e.host_register(out_link.dcache)
+                self._registered.append(e)
+        self._threading = threading
+        self._th = None
+
+    def start(self):
+        def body():
+            self._rc = lib().fdt_mux_run(c.byref(self.mcfg), c.byref(self.cb), self._t, c.byref(self._halt),
+                                         c.byref(self._mstats))
+        self._halt.value = 0
+        self._th = self._threading.Thread(target=body, daemon=True)
+        self._th.start()
+
+    def stop(self):
+        if self._th is not None:
+            self._halt.value = 1
+            self._th.join()
+            self._th = None
+            if self._rc:
+                raise RuntimeError("fdt_mux_run: bad configuration")
+
+    def final_cnt(self):
+        return lib().fdgpu_vmux_final_cnt(self._t)
+
+    def run(self, n_frags, timeout_s=60.0):
+        """Runs the mux thread until the outcome of n_frags frags (all of this
+        tile's in-link frags, its round-robin share included) is final."""
+        import time
+        self.start()
+        t0 = time.time()
+        try:
+            while self.final_cnt() < n_frags:
+                if lib().fdgpu_vmux_error(self._t):
+                    raise RuntimeError(f"verify mux tile: verifier error {lib().fdgpu_vmux_error(self._t)}")
+                if time.time() - t0 > timeout_s:
+                    raise TimeoutError(f"verify mux tile: {self.final_cnt()}/{n_frags} frags final")
+                time.sleep(0.0005)
+        finally:
+            self.stop()
+
+    def stats(self):
+        s = VTileStats()
+        lib().fdgpu_vmux_stats(self._t, c.byref(s))
+        return s.as_dict()
+
+    def mux_stats(self):
+        return self._mstats.as_dict()
+
+    def latencies_ns(self):
+        n = self.stats()["lat_cnt"]
+        out = np.zeros(max(n, 1), dtype=np.uint64)
+        n = lib().fdgpu_vmux_latencies(self._t, out.ctypes.data, n)
+        return out[:n]
+
+    def idle(self):
+        return bool(lib().fdgpu_vmux_idle(self._t))
+
+    def log(self, max_entries=1 << 24):
+        seqs = np.zeros(max_entries, dtype=np.uint64)
+        codes = np.zeros(max_entries, dtype=np.int8)
+        n = lib().fdgpu_vmux_log(self._t, seqs.ctypes.data, codes.ctypes.data, max_entries)
+        order = np.argsort(seqs[:n], kind="stable")
+        return seqs[:n][order], codes[:n][order]
+
+    def close(self):
+        self.stop()
+        if self._t:
+            lib().fdgpu_vmux_delete(self._t)
+            self._t = None
+        for e in self._registered:
+            e.host_unregister(self.out_link.dcache)
+        self._registered = []
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def vmux_dcache_data_sz(cr_max, batch_txn_max, inflight_max=2):
+    """Out dcache bytes the verify mux tile wants (fdgpu_vmux_dcache_data_sz)."""
+    return lib().fdgpu_vmux_dcache_data_sz(cr_max, batch_txn_max, inflight_max)
 
 
 class DedupTile:

@@ -144,6 +144,21 @@ int       fdgpu_release( fdgpu_engine_t * e, int64_t ticket );
 /* Returns a staged (acquired, not submitted) slot to the ring. */
 int       fdgpu_stage_cancel( fdgpu_engine_t * e );
 
+/* Registered host memory (the mux-callback verify tile's path): the caller
+   registers a long-lived region once -- e.g. the workspace holding the
+   verify -> dedup dcache, into which the tile copies each frag exactly as the
+   reference's during_frag does (fd_verify.c:53-74) -- and fdgpu_submit of an
+   arena lying inside a registered region uploads it by DMA straight from
+   there, with no staging copy.  The arena's bytes must stay unchanged until
+   the batch is polled.  Regions are page-rounded and shared (reference
+   counted) across the engines that register them; fdgpu_engine_close drops
+   this engine's registrations.  FDGPU_OK or < 0.
+
+   The ring API (submit, stage_*, poll*, release, host_register) is
+   thread-safe per engine: several tile threads may share one engine. */
+int       fdgpu_host_register  ( fdgpu_engine_t * e, void * p, uint64_t sz );
+int       fdgpu_host_unregister( fdgpu_engine_t * e, void * p );
+
 /* Device-resident path: inputs already in HBM (device pointers), codes
    written to device memory, work enqueued on `hip_stream` (a hipStream_t,
    NULL = the engine's compute stream).  d_sig_desc: per-signature

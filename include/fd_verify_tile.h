@@ -275,6 +275,168 @@ void *          fdgpu_vtile_tcache( fdgpu_vtile_t * t );
 void            fdgpu_vtile_log_enable( fdgpu_vtile_t * t, uint64_t log_max );
 uint64_t        fdgpu_vtile_log( fdgpu_vtile_t const * t, uint64_t * seqs, int8_t * codes, uint64_t max );
 
+/* ------------------------------------------ mux (src/disco/mux/fd_mux.h) */
+
+/* The reference's tiles are written as callbacks of its mux run loop
+   (fd_mux.h:114-299, fd_mux.c:387-699); the verify tile is the vtable of
+   fd_verify.c:232-246 with FD_MUX_FLAG_COPY | FD_MUX_FLAG_MANUAL_PUBLISH.
+   Restated here with the same names, argument meanings and call order so a
+   tile written for the reference mux runs on fdt_mux_run, and the batched
+   GPU verify tile below plugs into the reference's mux unchanged. */
+#define FDT_MUX_FLAG_DEFAULT        (0UL)                 /* fd_mux.h:71-73 */
+#define FDT_MUX_FLAG_MANUAL_PUBLISH (1UL)
+#define FDT_MUX_FLAG_COPY           (2UL)
+
+typedef struct {                                          /* fd_mux_context_t, fd_mux.h:106-112 */
+  fdt_frag_meta_t * mcache;
+  uint64_t          depth;
+  uint64_t *        cr_avail;
+  uint64_t *        seq;
+  uint64_t          cr_decrement_amount;
+} fdt_mux_context_t;
+
+typedef void (fdt_mux_during_housekeeping_fn)( void * ctx );                                   /* fd_mux.h:125 */
+typedef void (fdt_mux_before_credit_fn)( void * ctx, fdt_mux_context_t * mux );                 /* :141-142 */
+typedef void (fdt_mux_after_credit_fn)( void * ctx, fdt_mux_context_t * mux, int * opt_poll_in );  /* :167-169 */
+typedef void (fdt_mux_before_frag_fn)( void * ctx, uint64_t in_idx, uint64_t seq, uint64_t sig,
+                                       int * opt_filter );                                      /* :188-192 */
+typedef void (fdt_mux_during_frag_fn)( void * ctx, uint64_t in_idx, uint64_t seq, uint64_t sig,
+                                       uint64_t chunk, uint64_t sz, int * opt_filter );         /* :222-228 */
+typedef void (fdt_mux_after_frag_fn)( void * ctx, uint64_t in_idx, uint64_t seq, uint64_t * opt_sig,
+                                      uint64_t * opt_chunk, uint64_t * opt_sz, uint64_t * opt_tsorig,
+                                      int * opt_filter, fdt_mux_context_t * mux );              /* :260-268 */
+typedef void (fdt_mux_metrics_write_fn)( void * ctx );                                          /* :281 */
+
+typedef struct {                                          /* fd_mux_callbacks_t, fd_mux.h:288-299 */
+  fdt_mux_during_housekeeping_fn * during_housekeeping;
+  fdt_mux_before_credit_fn *       before_credit;
+  fdt_mux_after_credit_fn *        after_credit;
+  fdt_mux_before_frag_fn *         before_frag;
+  fdt_mux_during_frag_fn *         during_frag;
+  fdt_mux_after_frag_fn *          after_frag;
+  fdt_mux_metrics_write_fn *       metrics_write;
+} fdt_mux_callbacks_t;
+
+/* fd_mux_publish (fd_mux.h:484-496): publish to the mux's out mcache at
+   *ctx->seq, take one credit, advance seq. */
+void fdt_mux_publish( fdt_mux_context_t * ctx, uint64_t sig, uint64_t chunk, uint64_t sz, uint64_t ctl,
+                      uint64_t tsorig, uint64_t tspub );
+
+#define FDT_MUX_IN_MAX  (16UL)
+#define FDT_MUX_OUT_MAX (16UL)
+
+typedef struct {
+  uint64_t                in_cnt;
+  fdt_frag_meta_t const * in_mcache[ FDT_MUX_IN_MAX ];
+  uint64_t                in_depth [ FDT_MUX_IN_MAX ];
+  uint64_t                in_seq0  [ FDT_MUX_IN_MAX ];
+  uint64_t *              in_fseq  [ FDT_MUX_IN_MAX ];   /* the mux's position, for the in's producer (may be NULL) */
+  fdt_frag_meta_t *       out_mcache;                    /* NULL: no out stream */
+  uint64_t                out_depth;
+  uint64_t                out_seq0;
+  uint64_t                out_cnt;                       /* reliable consumers of the out stream */
+  uint64_t const *        out_fseq [ FDT_MUX_OUT_MAX ];
+  uint64_t                flags;                         /* FDT_MUX_FLAG_* */
+  uint64_t                burst;                         /* frags published per in frag (>= 1) */
+  uint64_t                cr_max;                        /* 0: the reference default (fd_mux.c:326-327) */
+  uint64_t                lazy_iters;                    /* loop iterations between housekeeping events (0: 16) */
+} fdt_mux_cfg_t;
+
+typedef struct {
+  uint64_t in_frags;            /* frags read (before_frag called) */
+  uint64_t filtered_before;     /* before_frag filtered */
+  uint64_t filtered_after;      /* during/after_frag filtered */
+  uint64_t overrun_polling;     /* frags skipped: the in producer lapped the mux */
+  uint64_t overrun_reading;     /* frags abandoned: overwritten while being read */
+  uint64_t backpressure;        /* loop iterations without credits */
+  uint64_t published;           /* automatic publishes (not MANUAL_PUBLISH) */
+  uint64_t loops;
+} fdt_mux_stats_t;
+
+/* The mux run loop (fd_mux.c:387-699) with the cnc replaced by a halt word:
+   housekeeping every lazy_iters iterations (out credits from the out fseqs,
+   in fseqs updated, during_housekeeping / metrics_write, halt checked);
+   then before_credit; backpressure while cr_avail < cr_filt + burst;
+   after_credit (poll_in 0 restarts the loop); one in polled round robin:
+   overrun -> resume from the producer; before_frag; metadata read;
+   during_frag; overrun while reading -> abandon (re-checked after
+   during_frag as well); after_frag; automatic publish unless filtered or
+   MANUAL_PUBLISH.  Runs until *halt != 0.  Returns 0, or -1 on a bad cfg. */
+int  fdt_mux_run( fdt_mux_cfg_t const * cfg, fdt_mux_callbacks_t const * callbacks, void * ctx,
+                  uint64_t const volatile * halt, fdt_mux_stats_t * stats_out );
+
+/* ------------------------------- the verify tile as mux callbacks (vmux) */
+
+/* fd_tile_verify (fd_verify.c:232-246) restated for batched GPU
+   verification, run by fdt_mux_run (or the reference's fd_mux_tile) with
+   FDT_MUX_FLAG_COPY | FDT_MUX_FLAG_MANUAL_PUBLISH and burst 1:
+     before_frag   round-robin share (fd_verify.c:36-47);
+     during_frag   copy the payload into the OUT dcache at the tile's write
+                   cursor (fd_verify.c:53-74);
+     after_frag    fd_txn_parse in place, append the trailer (fd_verify.c:
+                   76-136), then append {msg, sigs, pubkeys, sig_cnt} to the
+                   open batch -- the batch's arena IS the contiguous run of
+                   out-dcache chunks its frags occupy, so with that dcache
+                   registered (fdgpu_host_register) the engine DMAs it with
+                   no staging copy -- and advance the cursor;
+     after_credit  poll in-flight batches and resolve completed ones strictly
+                   in ingest order (tcache query -> verify code -> insert ->
+                   fdt_mux_publish of the frag where it already lies), while
+                   credits last (opt_poll_in = 0 when they run out); submit
+                   the open batch when full / after batch_wait_ns; stop
+                   polling the ins (opt_poll_in = 0) while the out dcache has
+                   no room for one more frag.
+   Out-dcache accounting: the region from the oldest frag that may still be
+   read -- published within the last cr_max - cr_avail (the mux's exposed
+   count) or reserved by a batch not yet resolved -- to the write cursor is
+   live; a frag is copied in only if a maximal one fits before that region.
+   Size the dcache for cr_max + (inflight_max + 1) * batch_txn_max frags of
+   FDT_TPU_DCACHE_MTU (fdgpu_vmux_dcache_data_sz) or the tile stalls early. */
+typedef struct {
+  uint64_t        in_cnt;
+  uint8_t const * in_base  [ FDT_MUX_IN_MAX ];   /* chunk 0 address of each in link */
+  uint64_t        in_chunk0[ FDT_MUX_IN_MAX ];   /* valid chunk range [chunk0, wmark] */
+  uint64_t        in_wmark [ FDT_MUX_IN_MAX ];
+  uint8_t *       out_base;                      /* chunk 0 address of the out dcache */
+  uint64_t        out_chunk0;
+  uint64_t        out_wmark;
+  uint64_t        cr_max;                        /* the mux's cr_max (frags the consumers may lag) */
+  uint64_t        round_robin_idx;
+  uint64_t        round_robin_cnt;
+  uint64_t        hashmap_seed;
+  uint64_t        tcache_depth;                  /* 0: FDT_VERIFY_TCACHE_DEPTH */
+  uint64_t        tcache_map_cnt;                /* 0: FDT_VERIFY_TCACHE_MAP_CNT */
+  uint32_t        batch_txn_max;
+  uint32_t        inflight_max;                  /* 0: 2 */
+  uint64_t        batch_wait_ns;
+  uint64_t        batch_sig_max;                 /* 0: 12 x batch_txn_max */
+  uint64_t        batch_bytes_max;               /* arena bytes per batch (<= the engines' max_arena);
+                                                    0: batch_txn_max x FDT_TPU_DCACHE_MTU rounded to chunks */
+} fdgpu_vmux_cfg_t;
+
+typedef struct fdgpu_vmux fdgpu_vmux_t;
+
+fdgpu_vmux_t *      fdgpu_vmux_new      ( fdgpu_vmux_cfg_t const * cfg, fdgpu_verifier_t verifier );
+void                fdgpu_vmux_delete   ( fdgpu_vmux_t * t );
+/* The tile's vtable (ctx = the fdgpu_vmux_t *). */
+fdt_mux_callbacks_t fdgpu_vmux_callbacks( void );
+/* Out dcache bytes the tile wants (see above). */
+uint64_t            fdgpu_vmux_dcache_data_sz( uint64_t cr_max, uint32_t batch_txn_max, uint32_t inflight_max );
+void                fdgpu_vmux_stats    ( fdgpu_vmux_t const * t, fdgpu_vtile_stats_t * out );
+/* 1 when no frag is held in an open or in-flight batch. */
+int                 fdgpu_vmux_idle     ( fdgpu_vmux_t const * t );
+/* 0, or the verifier's fatal error (the tile then stops taking frags). */
+int                 fdgpu_vmux_error    ( fdgpu_vmux_t const * t );
+/* Frags whose outcome is final (published, failed, dedup, filtered, parse
+   failure, corrupt); safe to read from another thread while the mux runs. */
+uint64_t            fdgpu_vmux_final_cnt( fdgpu_vmux_t const * t );
+/* Batch latencies (first frag ingested -> its batch resolved), ns; returns count. */
+uint64_t            fdgpu_vmux_latencies( fdgpu_vmux_t const * t, uint64_t * out, uint64_t max );
+/* Per-frag outcome log, as fdgpu_vtile_log (codes FD_TXN_VERIFY_* and
+   FDGPU_VTILE_LOG_*). */
+void                fdgpu_vmux_log_enable( fdgpu_vmux_t * t, uint64_t log_max );
+uint64_t            fdgpu_vmux_log      ( fdgpu_vmux_t const * t, uint64_t * seqs, int8_t * codes, uint64_t max );
+
 /* ---------------------------------------------------------- dedup tile */
 
 /* src/app/fdctl/run/tiles/fd_dedup.c:89-205: consumes verify outputs (the

@@ -1,0 +1,277 @@
+"""The reference's mux callback API restated (fdt_mux_run / fdt_mux_publish,
+src/disco/mux/fd_mux.h:106-299, fd_mux.c:387-699) and the verify tile written
+against it (fdgpu_vmux: fd_verify.c:232-246 with FD_MUX_FLAG_COPY |
+FD_MUX_FLAG_MANUAL_PUBLISH), on CPU.  The tile's verifier here is a
+PyVerifier over the CPU oracle; tests/test_tile_gpu.py runs the same tile
+over the MI355X engines."""
+import ctypes as c
+import random
+import threading
+import time
+
+import numpy as np
+import pytest
+
+from firedancer_amd import tile, workload
+import tile_model
+from test_tile import _mixed_stream, oracle_fn
+
+u64 = c.c_uint64
+BEFORE_CREDIT = c.CFUNCTYPE(None, c.c_void_p, c.c_void_p)
+AFTER_CREDIT = c.CFUNCTYPE(None, c.c_void_p, c.c_void_p, c.POINTER(c.c_int))
+BEFORE_FRAG = c.CFUNCTYPE(None, c.c_void_p, u64, u64, u64, c.POINTER(c.c_int))
+DURING_FRAG = c.CFUNCTYPE(None, c.c_void_p, u64, u64, u64, u64, u64, c.POINTER(c.c_int))
+AFTER_FRAG = c.CFUNCTYPE(None, c.c_void_p, u64, u64, c.POINTER(u64), c.POINTER(u64), c.POINTER(u64),
+                         c.POINTER(u64), c.POINTER(c.c_int), c.c_void_p)
+HOUSEKEEPING = c.CFUNCTYPE(None, c.c_void_p)
+
+
+def _mux_cfg(in_links, out_link=None, flags=tile.MUX_FLAG_DEFAULT, out_fseq=None, cr_max=0):
+    mc = tile.MuxCfg()
+    mc.in_cnt = len(in_links)
+    for i, ln in enumerate(in_links):
+        mc.in_mcache[i], mc.in_depth[i], mc.in_seq0[i] = ln.mcache_ptr, ln.depth, ln.seq0
+    if out_link is not None:
+        mc.out_mcache, mc.out_depth, mc.out_seq0 = out_link.mcache_ptr, out_link.depth, out_link.seq0
+    if out_fseq is not None:
+        mc.out_cnt, mc.out_fseq[0] = 1, out_fseq.ctypes.data
+    mc.flags, mc.burst, mc.cr_max, mc.lazy_iters = flags, 1, cr_max, 4
+    return mc
+
+
+class MuxThread:
+    def __init__(self, cfg, cb, ctx=None):
+        self.cfg, self.cb, self.ctx = cfg, cb, ctx
+        self.halt, self.stats, self.rc = u64(0), tile.MuxStats(), None
+        self.th = threading.Thread(target=self._body, daemon=True)
+        self.th.start()
+
+    def _body(self):
+        self.rc = tile.lib().fdt_mux_run(c.byref(self.cfg), c.byref(self.cb), self.ctx, c.byref(self.halt),
+                                         c.byref(self.stats))
+
+    def stop(self):
+        self.halt.value = 1
+        self.th.join(30)
+        assert not self.th.is_alive()
+        return self.rc
+
+
+def _wait(cond, timeout=30.0):
+    t0 = time.time()
+    while not cond():
+        assert time.time() - t0 < timeout, "timed out"
+        time.sleep(0.001)
+
+
+def test_mux_relays_frags_without_callbacks():
+    """No callbacks, default flags: every in frag is republished on the out
+    mcache with its sig / chunk / sz / ctl / tsorig (the zero-copy mux), and
+    two ins are serviced round robin, each in order."""
+    a, b = tile.Link(64, 1232), tile.Link(64, 1232)
+    out = tile.Link(256, 1232)
+    for i in range(40):
+        a.publish(bytes([i]) * (10 + i), sig=1000 + i)
+        b.publish(bytes([i]) * 5, sig=2000 + i)
+    m = MuxThread(_mux_cfg([a, b], out), tile.MuxCallbacks())
+    _wait(lambda: out.poll(out.seq0 + 79)[0] == 1)
+    assert m.stop() == 0
+    got = out.drain()
+    assert len(got) == 80 and m.stats.published == 80
+    sa = [mt["sig"] for mt, _ in got if mt["sig"] < 2000]
+    sb = [mt["sig"] for mt, _ in got if mt["sig"] >= 2000]
+    assert sa == list(range(1000, 1040)) and sb == list(range(2000, 2040))
+    for mt, _ in got:                                      # chunk / sz point at the in link's payload
+        src = a if mt["sig"] < 2000 else b
+        i = mt["sig"] % 1000
+        assert bytes(src.dcache[mt["chunk"] * 64: mt["chunk"] * 64 + mt["sz"]]) == \
+            (bytes([i]) * (10 + i) if src is a else bytes([i]) * 5)
+
+
+def test_mux_callback_order_and_filters():
+    """before_frag sees (seq, sig) and can drop a frag unread; during_frag
+    sees chunk/sz and can filter; after_frag runs only for unfiltered frags
+    and can rewrite sig/sz before the mux publishes; after_credit runs every
+    loop with poll_in defaulting to 1 (fd_mux.c:559-660)."""
+    inl = tile.Link(128, 1232)
+    out = tile.Link(128, 1232)
+    for i in range(60):
+        inl.publish(bytes([i & 255]) * 20, sig=i * 7)
+    ev = {"before": [], "during": [], "after": [], "credit": 0}
+
+    def before(ctx, idx, seq, sig, filt):
+        ev["before"].append((seq, sig))
+        if seq % 2:
+            filt[0] = 1
+
+    def during(ctx, idx, seq, sig, chunk, sz, filt):
+        ev["during"].append(seq)
+        assert sz == 20
+        if seq % 3 == 0:
+            filt[0] = 1
+
+    def after(ctx, idx, seq, opt_sig, opt_chunk, opt_sz, opt_tsorig, filt, mux):
+        ev["after"].append(seq)
+        opt_sig[0] = 100000 + seq
+        opt_sz[0] = 8
+
+    def credit(ctx, mux, poll_in):
+        ev["credit"] += 1
+        assert poll_in[0] == 1
+
+    fns = [BEFORE_FRAG(before), DURING_FRAG(during), AFTER_FRAG(after), AFTER_CREDIT(credit)]
+    cb = tile.MuxCallbacks()
+    cb.before_frag, cb.during_frag, cb.after_frag, cb.after_credit = [c.cast(f, c.c_void_p) for f in fns]
+    m = MuxThread(_mux_cfg([inl], out), cb)
+    exp = [s for s in range(60) if s % 2 == 0 and s % 3]
+    _wait(lambda: len(ev["before"]) >= 60)
+    assert m.stop() == 0
+    assert [s for s, _ in ev["before"]][:60] == list(range(60))
+    assert all(sig == 7 * s for s, sig in ev["before"])
+    assert ev["during"] == [s for s in range(60) if s % 2 == 0]
+    assert ev["after"] == exp
+    got = out.drain()
+    assert [mt["sig"] for mt, _ in got] == [100000 + s for s in exp] and all(mt["sz"] == 8 for mt, _ in got)
+    assert ev["credit"] >= 60
+    st = m.stats.as_dict()
+    assert st["filtered_before"] == 30 and st["filtered_after"] == 10 and st["published"] == len(exp)
+
+
+def test_mux_credits_backpressure():
+    """With one reliable consumer whose fseq does not move, the mux exposes at
+    most cr_max frags, then spins backpressured (after_credit not called)
+    until the consumer's fseq advances (fd_mux.c:467-487,548-556)."""
+    inl = tile.Link(64, 1232)
+    out = tile.Link(64, 1232)
+    for i in range(20):
+        inl.publish(b"x" * 10, sig=i)
+    fseq = np.zeros(1, dtype=np.uint64)
+    m = MuxThread(_mux_cfg([inl], out, out_fseq=fseq, cr_max=4), tile.MuxCallbacks())
+    _wait(lambda: out.poll(3)[0] == 1)
+    time.sleep(0.05)
+    assert out.poll(4)[0] == 0                             # 4 exposed, no credit for a 5th
+    fseq[0] = 3                                            # consumer read 3 frags
+    _wait(lambda: out.poll(6)[0] == 1)
+    time.sleep(0.05)
+    assert out.poll(7)[0] == 0
+    fseq[0] = 20
+    _wait(lambda: out.poll(19)[0] == 1)
+    assert m.stop() == 0
+    assert m.stats.backpressure > 0 and m.stats.published == 20
+
+
+def test_mux_overrun_polling():
+    """An in producer that laps the mux: the mux resumes from the sequence
+    number it found in the line it polled (fd_mux.c:595-603: here line 0
+    holds seq 32) and counts the frags it skipped."""
+    inl = tile.Link(16, 1232)
+    out = tile.Link(64, 1232)
+    for i in range(40):                                    # 24 frags overwritten before the mux starts
+        inl.publish(b"y" * 10, sig=i)
+    m = MuxThread(_mux_cfg([inl], out), tile.MuxCallbacks())
+    _wait(lambda: out.poll(7)[0] == 1)
+    assert m.stop() == 0
+    got = out.drain()
+    assert [mt["sig"] for mt, _ in got] == list(range(32, 40))
+    assert m.stats.overrun_polling == 32
+
+
+# ------------------------------------------------- verify tile as callbacks
+
+def _run_vmux(payloads, verifier, seed=0xABCD, batch=4, inflight=2, rr=(0, 1), depth=1 << 12, out_data=None,
+              flow=False, consumer=None, cr_max=0):
+    inl = tile.Link(depth, 1232)
+    outl = tile.Link(depth, tile.TPU_DCACHE_MTU,
+                     data_sz=out_data or (len(payloads) + 8) * (tile.TPU_DCACHE_MTU + 64))
+    vm = tile.VerifyMuxTile(inl, outl, verifier, hashmap_seed=seed, batch_txn_max=batch, inflight_max=inflight,
+                            round_robin_idx=rr[0], round_robin_cnt=rr[1], log_max=1 << 16, flow_control=flow,
+                            batch_wait_us=100, cr_max=cr_max)
+    for p in payloads:
+        inl.publish(p)
+    th = None
+    if consumer is not None:
+        th = threading.Thread(target=consumer, args=(outl,), daemon=True)
+        th.start()
+    vm.run(len(payloads), timeout_s=60)
+    if th is not None:
+        th.join(30)
+    return vm, inl, outl
+
+
+@pytest.mark.parametrize("batch,inflight,lag,rr", [(1, 1, 0, (0, 1)), (7, 2, 2, (0, 1)), (64, 3, 1, (1, 3)),
+                                                    (1000, 2, 0, (0, 1))])
+def test_vmux_vs_sequential_model(oracle, batch, inflight, lag, rr):
+    """The verify tile as mux callbacks produces the reference loop's outcome
+    for every frag and the same published stream (sig = tag, payload,
+    fd_txn_t trailer), for any batch size / batches in flight / verifier
+    latency / round-robin share."""
+    ps = _mixed_stream(800, seed=batch * 17 + lag)
+    seed = 0x99 + batch
+    ver = tile.PyVerifier(oracle_fn(oracle), slots=inflight, lag=lag)
+    vm, _, outl = _run_vmux(ps, ver, seed=seed, batch=batch, inflight=inflight, rr=rr)
+    exp_out, exp_pub = tile_model.verify_tile_model(ps, seed, oracle_fn(oracle), rr_idx=rr[0], rr_cnt=rr[1])
+    seqs, codes = vm.log()
+    assert seqs.tolist() == list(range(len(ps)))
+    assert codes.tolist() == exp_out
+    outs = outl.drain()
+    assert [(m["sig"], tile.split_verify_output(f)[0]) for m, f in outs] == [(t, p) for p, _, t in exp_pub]
+    assert [tile.split_verify_output(f)[1] for _, f in outs] == [raw for _, raw, _ in exp_pub]
+    assert all(m["ctl"] == 0 for m, _ in outs)
+    st = vm.stats()
+    assert st["published"] == exp_out.count(0) and st["dedup"] == exp_out.count(-2)
+    assert st["verify_failed"] == exp_out.count(-1) and st["parse_fail"] == exp_out.count(1)
+    assert st["filtered_rr"] == exp_out.count(2)
+    assert vm.idle()
+    vm.close()
+
+
+def test_vmux_small_dcache_wraps_under_flow_control(oracle):
+    """An out dcache with room for ~8 maximal frags, 12 credits, and a slow
+    consumer that reads each published frag (then advances the fseq) while
+    the tile runs: the tile wraps the ring many times, stops taking frags
+    while the region it would write still holds a frag the consumer may
+    read, stops publishing without credits, and every frag the consumer sees
+    is intact and in model order."""
+    ps = _mixed_stream(600, seed=5)
+    seed = 0x5151
+    exp_out, exp_pub = tile_model.verify_tile_model(ps, seed, oracle_fn(oracle))
+    seen = []
+
+    def consumer(outl):
+        seq = outl.seq0
+        t0 = time.time()
+        while len(seen) < len(exp_pub) and time.time() - t0 < 60:
+            rc, meta, _ = outl.poll(seq)
+            if rc != 1:
+                time.sleep(0.0002)
+                continue
+            seen.append((meta["sig"], outl.payload(meta)))
+            seq += 1
+            if random.random() < 0.3:
+                time.sleep(0.002)                          # a slow consumer
+            outl.fseq[0] = seq
+
+    ver = tile.PyVerifier(oracle_fn(oracle), slots=2, lag=1)
+    vm, _, outl = _run_vmux(ps, ver, seed=seed, batch=16, inflight=2, depth=1 << 10,
+                            out_data=8 * (tile.TPU_DCACHE_MTU + 64), flow=True, consumer=consumer, cr_max=12)
+    assert len(seen) == len(exp_pub)
+    for (sig, frag), (p, raw, tag) in zip(seen, exp_pub):
+        assert sig == tag
+        pay, traw = tile.split_verify_output(frag)
+        assert pay == p and traw == raw
+    seqs, codes = vm.log()
+    assert codes.tolist() == exp_out
+    assert vm.stats()["backpressure"] > 0 and vm.mux_stats()["backpressure"] > 0
+    vm.close()
+
+
+def test_vmux_cfg_checks():
+    inl = tile.Link(64, 1232)
+    outl = tile.Link(64, tile.TPU_DCACHE_MTU)
+    ver = tile.PyVerifier(lambda a, t: np.zeros(len(t), dtype=np.int8))
+    with pytest.raises(RuntimeError):
+        tile.VerifyMuxTile(inl, outl, ver, batch_txn_max=0)
+    tiny = tile.Link(4, 64)                               # ring smaller than two maximal frags
+    with pytest.raises(RuntimeError):
+        tile.VerifyMuxTile(inl, tiny, ver, batch_txn_max=4)
+    assert tile.vmux_dcache_data_sz(64, 16, 2) >= (64 + 3 * 16) * tile.TPU_DCACHE_MTU

@@ -119,3 +119,91 @@ def test_twelve_signature_txns_default_config():
         vt.close()
     finally:
         eng.close()
+
+
+# ------------------------------------ the verify tile as mux callbacks (vmux)
+
+def test_vmux_mixed_stream_vs_model_gpu(engines, oracle):
+    """fdgpu_vmux on fdt_mux_run over the MI355X engines: frags copied into
+    the out dcache (registered with both engines, so each batch is DMA'd from
+    there with no staging copy), verified, and published in place -- every
+    outcome and the published stream equal the sequential model's."""
+    from test_tile import _mixed_stream
+    ps = _mixed_stream(3000, seed=7)
+    seed = 0xC0DE
+    inl = tile.Link(1 << 13, 1232)
+    outl = tile.Link(1 << 13, tile.TPU_DCACHE_MTU, data_sz=tile.vmux_dcache_data_sz(1 << 13, 101, 3))
+    ver = tile.EngineVerifier(engines)
+    vm = tile.VerifyMuxTile(inl, outl, ver, hashmap_seed=seed, batch_txn_max=101, inflight_max=3, log_max=1 << 14)
+    for p in ps:
+        inl.publish(p)
+    vm.run(len(ps), timeout_s=60)
+    exp, pub = tile_model.verify_tile_model(ps, seed, lambda a, t: oracle.verify_txns(a, t))
+    seqs, codes = vm.log()
+    assert seqs.tolist() == list(range(len(ps))) and codes.tolist() == exp
+    outs = outl.drain()
+    assert [(m["sig"], tile.split_verify_output(f)) for m, f in outs] == [(t, (p, raw)) for p, raw, t in pub]
+    st = vm.stats()
+    assert st["batches"] >= (len(ps) - st["parse_fail"]) // 101 and vm.idle()
+    vm.close()
+    ver.close()
+
+
+def test_vmux_two_tiles_share_engines_gpu(engines, oracle):
+    """Two verify mux tiles on their own threads take the round-robin shares
+    of one in link (fd_verify.c:46) and share the node's engines (the ring
+    API is thread-safe per engine); each tile's outcomes and published
+    stream equal the model of its share, with the out dcache wrapping
+    several times under flow control from a consumer thread."""
+    import threading
+    import time
+    from test_tile import _mixed_stream
+    ps = _mixed_stream(4000, seed=11)
+    seed = 0xBEEF
+    inl = tile.Link(1 << 13, 1232)
+    tiles, outs, vers = [], [], []
+    for k in range(2):
+        outl = tile.Link(1 << 12, tile.TPU_DCACHE_MTU, data_sz=tile.vmux_dcache_data_sz(64, 64, 2))
+        ver = tile.EngineVerifier(engines)
+        vm = tile.VerifyMuxTile(inl, outl, ver, hashmap_seed=seed, batch_txn_max=64, inflight_max=2,
+                                round_robin_idx=k, round_robin_cnt=2, log_max=1 << 14, cr_max=64,
+                                flow_control=True)
+        tiles.append(vm); outs.append(outl); vers.append(ver)
+    seen = [[], []]
+    stop = threading.Event()
+
+    def consume(k):
+        outl, seq = outs[k], outs[k].seq0
+        while not stop.is_set():
+            rc, meta, _ = outl.poll(seq)
+            if rc != 1:
+                time.sleep(0.0001)
+                continue
+            seen[k].append((meta["sig"], outl.payload(meta)))
+            seq += 1
+            outl.fseq[0] = seq
+
+    cons = [threading.Thread(target=consume, args=(k,), daemon=True) for k in range(2)]
+    for t in cons:
+        t.start()
+    for p in ps:
+        inl.publish(p)
+    for vm in tiles:
+        vm.start()
+    t0 = time.time()
+    while any(vm.final_cnt() < len(ps) for vm in tiles):
+        assert time.time() - t0 < 60
+        time.sleep(0.001)
+    for vm in tiles:
+        vm.stop()
+    time.sleep(0.05)
+    stop.set()
+    for t in cons:
+        t.join(10)
+    for k, vm in enumerate(tiles):
+        exp, pub = tile_model.verify_tile_model(ps, seed, lambda a, t: oracle.verify_txns(a, t), rr_idx=k,
+                                                rr_cnt=2)
+        assert vm.log()[1].tolist() == exp
+        assert [(s, tile.split_verify_output(f)) for s, f in seen[k]] == [(t, (p, raw)) for p, raw, t in pub]
+        vm.close()
+        vers[k].close()

@@ -36,6 +36,9 @@ def main():
     ap.add_argument("--wait-us", type=float, default=200.0)
     ap.add_argument("--depth-lg", type=int, default=19, help="log2 of the quic->verify mcache depth")
     ap.add_argument("--multi", type=int, default=1, help="1: cfg3 multi-sig txns, 0: cfg1 single-sig")
+    ap.add_argument("--mux", type=int, default=0,
+                    help="1: the verify tile as mux callbacks (fdgpu_vmux on fdt_mux_run; frags copied once into "
+                         "the registered out dcache and DMA'd from there), 0: the step-loop tile (fdgpu_vtile)")
     ap.add_argument("--out", default="")
     ap.add_argument("--sweep", default="", help="';'-separated runs of 'tiles,batch,inflight,rate' over the same txns")
     args = ap.parse_args()
@@ -66,7 +69,9 @@ def main():
 
 
 def run_once(args, ps, arena, offs, sizes, n_sig, modes, tiles_n, batch, inflight, rate):
-    # one engine per tile thread (an engine is single-threaded), tiles spread over the GPUs
+    if args.mux:
+        return run_once_mux(args, ps, arena, offs, sizes, n_sig, modes, tiles_n, batch, inflight, rate)
+    # one engine per tile thread, tiles spread over the GPUs
     engines = [fa.VerifyEngine(k % args.gpus, max_txn=batch, max_sig=batch * 12,
                                max_arena=batch * 1232, ring_depth=inflight) for k in range(tiles_n)]
     inl = tile.Link(1 << args.depth_lg, 1232)
@@ -117,6 +122,63 @@ def run_once(args, ps, arena, offs, sizes, n_sig, modes, tiles_n, batch, infligh
     }
     for vt in vts:
         vt.close()
+    for ver, _ in vers:
+        ver.close()
+    for e in engines:
+        e.close()
+    return res
+
+
+def run_once_mux(args, ps, arena, offs, sizes, n_sig, modes, tiles_n, batch, inflight, rate):
+    """T verify mux tiles (fdt_mux_run threads) over one engine each; the
+    out links have no reliable consumer here (published frags count as
+    consumed), so this measures ingest + verify + publish."""
+    frag_bytes = (tile.TPU_DCACHE_MTU + 63) // 64 * 64
+    engines = [fa.VerifyEngine(k % args.gpus, max_txn=batch, max_sig=batch * 12,
+                               max_arena=batch * frag_bytes, ring_depth=inflight) for k in range(tiles_n)]
+    inl = tile.Link(1 << args.depth_lg, 1232)
+    vms, vers = [], []
+    for k in range(tiles_n):
+        ver = tile.EngineVerifier([engines[k]])
+        outl = tile.Link(1 << 14, tile.TPU_DCACHE_MTU, data_sz=tile.vmux_dcache_data_sz(1 << 14, batch, inflight))
+        vms.append(tile.VerifyMuxTile(inl, outl, ver, batch_txn_max=batch, inflight_max=inflight,
+                                      batch_wait_us=args.wait_us, round_robin_idx=k, round_robin_cnt=tiles_n))
+        vers.append((ver, outl))
+    start = time.perf_counter()
+    prod = tile.Producer(inl, arena, offs, sizes, rate_tps=rate)
+    for vm in vms:
+        vm.start()
+    while any(vm.final_cnt() < len(ps) for vm in vms):
+        if time.perf_counter() - start > 300:
+            raise SystemExit("verify mux tiles timed out")
+        time.sleep(0.0002)
+    wall = time.perf_counter() - start
+    for vm in vms:
+        vm.stop()
+    n_pub, prod_s = prod.join()
+    stats = [vm.stats() for vm in vms]
+    mstats = [vm.mux_stats() for vm in vms]
+    lat = np.concatenate([vm.latencies_ns() for vm in vms]) / 1e6
+    agg = {k: int(sum(s[k] for s in stats)) for k in stats[0]}
+    agg["overrun"] = int(sum(m["overrun_polling"] + m["overrun_reading"] for m in mstats))
+    res = {
+        "metric": "verify mux tile end-to-end transactions/s (tango in -> GPU verify -> tango out)",
+        "tile": "fdgpu_vmux on fdt_mux_run (mux callbacks; registered out dcache, no staging copy)",
+        "txns_per_s": round(len(ps) / wall, 1),
+        "sigs_per_s": round(agg["sigs"] / wall, 1),
+        "wall_s": round(wall, 4), "producer_s": round(prod_s, 4), "producer_published": int(n_pub),
+        "gpus": args.gpus, "tiles": tiles_n, "batch_txn_max": batch, "inflight": inflight,
+        "rate_target": rate, "workload": "cfg3 (1-12 sigs/txn, payload <= 1232 B, 10% corrupted)"
+        if args.multi else "cfg1 (1 sig, msg U[180,220] B, 10% corrupted)",
+        "txns": len(ps), "sigs": n_sig,
+        "batch_latency_ms": {"p50": round(float(np.percentile(lat, 50)), 3) if len(lat) else None,
+                             "p99": round(float(np.percentile(lat, 99)), 3) if len(lat) else None,
+                             "n": int(len(lat))},
+        "counters": agg, "mux": {k: int(sum(m[k] for m in mstats)) for k in mstats[0]},
+        "expected_published": int((modes == 0).sum()),
+    }
+    for vm in vms:
+        vm.close()
     for ver, _ in vers:
         ver.close()
     for e in engines:
