@@ -113,7 +113,7 @@ def aggregate(dist, n_sig, steps, dt):
     return total / dt_max, dt_max
 
 
-RING_DEPTH = 4        # ring slots (one stream + workspace each) of the latency/PCIe engine
+RING_DEPTH = 8        # ring slots (one stream + workspace each) of the latency/PCIe engine (8: tools/pcie_probe.py)
 
 
 def latency_and_pcie(eng, arena, txns, batch, nbatches):

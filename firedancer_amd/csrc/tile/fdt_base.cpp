@@ -67,7 +67,7 @@ int fdt_mcache_poll(const fdt_frag_meta_t *mcache, uint64_t depth, uint64_t seq,
   if (s0 != s1 || diff < 0) return 0;    /* being written, or not yet published */
   if (diff > 0) return -1;               /* overrun */
   copy.seq = s0;
-  *meta = copy;
+  std::memcpy((void *)meta, &copy, sizeof copy);   /* caller storage need not be 32-B aligned */
   return 1;
 }
 

@@ -283,6 +283,29 @@ def test_txn_parse_rejects_malformed():
     assert tile.txn_parse(b"")[0] == 0 and tile.txn_parse(b"\0" * 1233)[0] == 0
 
 
+def test_txn_parse_random_bytes(fixtures):
+    """fd_txn_parse on untrusted bytes: random payloads of every size class,
+    random splices of the fixtures and every truncation of one fixture never
+    read or write out of bounds (run under ASan/UBSan by test_sanitize.py) and
+    accept only what round-trips through the restated decoder."""
+    rnd = random.Random(0xF022)
+    base = list(fixtures.values())
+    cases = [bytes(rnd.getrandbits(8) for _ in range(rnd.choice((0, 1, 3, 64, 65, 200, 1231, 1232, 1233, 2000))))
+             for _ in range(1500)]
+    for _ in range(1500):
+        a, b = rnd.choice(base), rnd.choice(base)
+        i, j = rnd.randrange(len(a) + 1), rnd.randrange(len(b) + 1)
+        cases.append(a[:i] + b[j:])
+    p = base[0]
+    cases += [p[:n] for n in range(len(p) + 1)]
+    for cse in cases:
+        sz, raw = tile.txn_parse(cse)
+        if sz:
+            d = tile.txn_decode(raw)
+            assert d["signature_off"] + 64 * d["signature_cnt"] <= len(cse)
+            assert d["message_off"] < len(cse) or len(cse) == 0
+
+
 # ----------------------------------------------------------- verify tile
 
 def _run_tile(payloads, verifier, seed=0xABCD, batch=4, inflight=2, rr=(0, 1), depth=1 << 12, tcache=None):

@@ -51,6 +51,20 @@ def run(eng, vs, depth, rounds=2):
     return sigs / wall, t_sub / (len(vs) * rounds) * 1e3
 
 
+def upload_only(eng, buf, nbytes, depth, reps=40):
+    """GB/s of batches with no transactions: only the arena's H2D copy runs"""
+    t = np.zeros(0, dtype=fa.ed25519.TXN_DTYPE)
+    inflight = []
+    t0 = time.perf_counter()
+    for i in range(reps):
+        if len(inflight) == depth:
+            eng.poll(inflight.pop(0), blocking=True)
+        inflight.append(eng.submit(buf[:nbytes], t))
+    for tk in inflight:
+        eng.poll(tk, blocking=True)
+    return nbytes * reps / (time.perf_counter() - t0) / 1e9
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--txns", type=int, default=1_000_000)
@@ -58,7 +72,16 @@ def main():
     args = ap.parse_args()
     arena, txns, _ = workload.cfg1(args.txns, seed=0x9C1E)
     lines = []
-    for batch, depth in ((65536, 4), (131072, 4), (262144, 3), (65536, 8)):
+    eng = fa.VerifyEngine(0, max_txn=65536, ring_depth=4)
+    nb = 22 << 20
+    d = {"upload_only_staged_GBps": round(upload_only(eng, arena, nb, 4), 2)}
+    eng.host_register(arena)
+    d["upload_only_registered_GBps"] = round(upload_only(eng, arena, nb, 4), 2)
+    eng.host_unregister(arena)
+    eng.close()
+    print(json.dumps(d), flush=True)
+    lines.append(json.dumps(d))
+    for batch, depth in ((65536, 4), (65536, 6), (65536, 8), (32768, 8), (131072, 6)):
         eng = fa.VerifyEngine(0, max_txn=batch, ring_depth=depth)
         staged = views_of(arena, txns, batch, True)
         r_st = run(eng, staged, depth)
