@@ -54,6 +54,11 @@ struct Slot {
   bool staged = false;      /* reserved by fdgpu_stage_acquire, not yet submitted */
   bool held = false;        /* polled with fdgpu_poll_keep, awaiting fdgpu_release */
   uint64_t txn_cnt = 0;
+  /* completion word in pinned host memory: the slot's stream writes
+     flag_seq into it after the code read-back (hipStreamWriteValue32), so a
+     non-blocking poll is one host load instead of a runtime event query */
+  uint32_t *h_flag = nullptr, *d_flag = nullptr;
+  uint32_t flag_seq = 0;
 };
 
 }  // namespace
@@ -75,6 +80,7 @@ struct fdgpu_engine {
   /* the ring API (submit / stage / poll / release) may be called from several
      host threads (verify tiles sharing the node's engines) */
   std::mutex ring_mu;
+  bool flag_poll = false;            /* slots signal completion through h_flag (probed at open) */
   std::vector<std::pair<uintptr_t, uint64_t>> regions;   /* fdgpu_host_register'ed [p, p + sz) */
 };
 
@@ -97,6 +103,7 @@ void slot_free(Slot &s) {
   if (s.d_txn_codes) (void)hipFree(s.d_txn_codes);
   if (s.d_sig_codes) (void)hipFree(s.d_sig_codes);
   if (s.d_ws) (void)hipFree(s.d_ws);
+  if (s.h_flag) (void)hipHostFree(s.h_flag);
   s = Slot{};
 }
 
@@ -118,6 +125,9 @@ bool slot_alloc(Slot &s, const fdgpu_cfg_t &c) {
   HIPCHK(hipMalloc((void **)&s.d_txn_codes, c.max_txn + 16), false);
   HIPCHK(hipMalloc((void **)&s.d_sig_codes, c.max_sig + 16), false);
   HIPCHK(hipMalloc((void **)&s.d_ws, fdgpu_ws_bytes(c.max_sig ? c.max_sig : 1)), false);
+  HIPCHK(hipHostMalloc((void **)&s.h_flag, 64, hipHostMallocDefault), false);   /* own cache line */
+  *s.h_flag = 0;
+  HIPCHK(hipHostGetDevicePointer((void **)&s.d_flag, s.h_flag, 0), false);
   return true;
 }
 
@@ -199,6 +209,31 @@ int ensure_ws(fdgpu_engine *e, uint64_t n_sig) {
    device), reference-counted across the engines that registered them. */
 namespace {
 std::mutex g_reg_mu;
+
+/* The fixed-base comb table is a device constant (67 MB): one copy per
+   device, shared by every engine opened on it (refcounted), so engines of
+   several verify tiles on one GPU read the same lines from the Infinity
+   Cache instead of each streaming its own copy. */
+std::mutex g_btab_mu;
+std::map<int, std::pair<uint32_t *, int>> g_btab;
+
+uint32_t *btab_acquire(int device, hipStream_t st) {
+  std::lock_guard<std::mutex> lk(g_btab_mu);
+  auto it = g_btab.find(device);
+  if (it != g_btab.end()) { it->second.second++; return it->second.first; }
+  uint32_t *p = nullptr;
+  if (hipMalloc((void **)&p, fdgpu_btab_bytes()) != hipSuccess) { set_err("btab alloc"); return nullptr; }
+  if (fdgpu_btab_build(p, st) != hipSuccess) { (void)hipFree(p); set_err("fixed-base table build failed"); return nullptr; }
+  g_btab[device] = {p, 1};
+  return p;
+}
+
+void btab_release(int device, uint32_t *p) {
+  std::lock_guard<std::mutex> lk(g_btab_mu);
+  auto it = g_btab.find(device);
+  if (it == g_btab.end() || it->second.first != p) return;
+  if (--it->second.second == 0) { (void)hipFree(p); g_btab.erase(it); }
+}
 std::map<uintptr_t, std::pair<uint64_t, int>> g_regions;   /* page-aligned base -> (bytes, engines) */
 
 bool region_covers(const fdgpu_engine *e, const uint8_t *p, uint64_t sz) {
@@ -253,8 +288,7 @@ fdgpu_engine_t *fdgpu_engine_open(int device, fdgpu_cfg_t const *cfg_in) {
   e->cfg = cfg;
   auto fail = [&]() -> fdgpu_engine_t * { fdgpu_engine_close(e); return nullptr; };
   if (hipStreamCreateWithFlags(&e->compute, hipStreamNonBlocking) != hipSuccess) { set_err("stream"); return fail(); }
-  if (hipMalloc((void **)&e->d_btab, fdgpu_btab_bytes()) != hipSuccess) { set_err("btab alloc"); return fail(); }
-  if (fdgpu_btab_build(e->d_btab, e->compute) != hipSuccess) { set_err("fixed-base table build failed"); return fail(); }
+  if (!(e->d_btab = btab_acquire(device, e->compute))) return fail();
   int bpcu = 0;
   hipDeviceProp_t prop;
   if (fdgpu_verify_occupancy(&bpcu) != hipSuccess || bpcu < 1) bpcu = 1;
@@ -264,6 +298,17 @@ fdgpu_engine_t *fdgpu_engine_open(int device, fdgpu_cfg_t const *cfg_in) {
   e->slots.resize(cfg.ring_depth);
   for (auto &s : e->slots) if (!slot_alloc(s, cfg)) return fail();
   if (hipStreamSynchronize(e->compute) != hipSuccess) { set_err("btab init failed"); return fail(); }
+  /* completion words: probe that a stream write reaches pinned host memory
+     (FDGPU_POLL_EVENT=1 keeps hipEventQuery polling) */
+  {
+    const char *pe = getenv("FDGPU_POLL_EVENT");
+    Slot &s0 = e->slots[0];
+    if (!(pe && pe[0] == '1') && hipStreamWriteValue32(s0.stream, s0.d_flag, 0x5a5a5a5au, 0) == hipSuccess &&
+        hipStreamSynchronize(s0.stream) == hipSuccess)
+      e->flag_poll = __atomic_load_n(s0.h_flag, __ATOMIC_ACQUIRE) == 0x5a5a5a5au;
+    (void)hipGetLastError();
+    *s0.h_flag = 0;
+  }
   return e;
 }
 
@@ -274,7 +319,7 @@ void fdgpu_engine_close(fdgpu_engine_t *e) {
   for (auto &s : e->slots) { if (s.stream) (void)hipStreamSynchronize(s.stream); slot_free(s); }
   for (auto &r : e->regions) unregister_one(e, r.first);
   for (auto st : e->batch_streams) (void)hipStreamSynchronize(st);   /* btab is read there */
-  if (e->d_btab) (void)hipFree(e->d_btab);
+  if (e->d_btab) btab_release(e->device, e->d_btab);
   if (e->d_ws) (void)hipFree(e->d_ws);
   if (e->d_scratch_codes) (void)hipFree(e->d_scratch_codes);
   if (e->compute) (void)hipStreamDestroy(e->compute);
@@ -339,6 +384,7 @@ static int64_t submit_slot(fdgpu_engine_t *e, Slot *s, uint64_t arena_sz, fdgpu_
                           s->d_sig_codes, s->d_txn_codes, s->stream, s->d_ws);
   if (rc) return rc;
   if (txn_cnt) HIPCHK(hipMemcpyAsync(s->h_codes, s->d_txn_codes, txn_cnt, hipMemcpyDeviceToHost, s->stream), FDGPU_ERR_DEVICE);
+  if (e->flag_poll) HIPCHK(hipStreamWriteValue32(s->stream, s->d_flag, ++s->flag_seq, 0), FDGPU_ERR_DEVICE);
   HIPCHK(hipEventRecord(s->done, s->stream), FDGPU_ERR_DEVICE);
   s->staged = false;
   s->held = false;
@@ -431,12 +477,16 @@ static int poll_slot(fdgpu_engine_t *e, int64_t ticket, int8_t *txn_codes, int b
   Slot *s = nullptr;
   for (auto &c : e->slots) if (c.ticket == ticket && ticket >= 0 && !c.held) { s = &c; break; }
   if (!s) { set_err("unknown ticket %lld", (long long)ticket); return FDGPU_ERR_TICKET; }
-  HIPCHK(hipSetDevice(e->device), FDGPU_ERR_DEVICE);
   if (blocking) {
+    HIPCHK(hipSetDevice(e->device), FDGPU_ERR_DEVICE);
     lk.unlock();                               /* the slot is this caller's until it is polled */
     HIPCHK(hipEventSynchronize(s->done), FDGPU_ERR_DEVICE);
     lk.lock();
+  } else if (e->flag_poll) {
+    /* the stream wrote flag_seq after the codes' read-back completed */
+    if (__atomic_load_n(s->h_flag, __ATOMIC_ACQUIRE) != s->flag_seq) return FDGPU_PENDING;
   } else {
+    HIPCHK(hipSetDevice(e->device), FDGPU_ERR_DEVICE);
     hipError_t q = hipEventQuery(s->done);
     if (q == hipErrorNotReady) return FDGPU_PENDING;
     HIPCHK(q, FDGPU_ERR_DEVICE);

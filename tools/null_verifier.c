@@ -1,0 +1,35 @@
+/* A verifier (include/fd_verify_tile.h fdgpu_verifier_t) that accepts every
+   transaction at once, with no GPU and no signature check: a host-path cost
+   probe for the verify tile (tools/tile_host_probe.py), so ingest, parse,
+   tcache and publish are timed without the engine.  Bench infrastructure
+   only -- it verifies nothing.
+   Build: gcc -O2 -shared -fPIC -I include tools/null_verifier.c -o tools/libnullver.so */
+#include <stdlib.h>
+#include <string.h>
+
+#include "fd_verify_tile.h"
+
+#define NV_RING 256
+
+typedef struct { int64_t next; uint64_t cnt[NV_RING]; } nv_t;
+
+static int64_t nv_submit(void *ctx, uint8_t const *arena, uint64_t arena_sz, fdgpu_txn_t const *txns, uint64_t n) {
+  (void)arena; (void)arena_sz; (void)txns;
+  nv_t *v = (nv_t *)ctx;
+  v->cnt[v->next % NV_RING] = n;
+  return v->next++;
+}
+
+static int nv_poll(void *ctx, int64_t ticket, int8_t *codes, int blocking) {
+  (void)blocking;
+  nv_t *v = (nv_t *)ctx;
+  if (codes) memset(codes, 0, v->cnt[ticket % NV_RING]);
+  return FDGPU_OK;
+}
+
+void null_verifier_make(fdgpu_verifier_t *out) {
+  memset(out, 0, sizeof(*out));
+  out->ctx = calloc(1, sizeof(nv_t));
+  out->submit = nv_submit;
+  out->poll = nv_poll;
+}

@@ -1,0 +1,75 @@
+"""Host-path scaling of the verify tile with no GPU: T step-loop tiles
+(fdgpu_vtile, round-robin shares of one quic->verify link, as
+fd_verify.c:46) over a verifier that accepts everything at once
+(tools/null_verifier.c), fed by the line-rate producer thread.  Measures
+what ingest + parse + tcache + publish cost per frag, and how it scales with
+tile threads, apart from the engine.
+
+    gcc -O2 -shared -fPIC -I include tools/null_verifier.c -o tools/libnullver.so
+    python tools/tile_host_probe.py --tiles 1,2,4 --txns 1000000
+"""
+import argparse
+import ctypes as c
+import json
+import os
+import sys
+import threading
+import time
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+
+from firedancer_amd import tile, workload  # noqa: E402
+
+
+class NullVerifier:
+    sig_max = 1 << 30
+
+    def __init__(self):
+        lib = c.CDLL(os.path.join(REPO, "tools", "libnullver.so"))
+        self.struct = tile.Verifier()
+        lib.null_verifier_make(c.byref(self.struct))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--tiles", default="1,2,4")
+    ap.add_argument("--txns", type=int, default=1_000_000)
+    ap.add_argument("--batch", type=int, default=16384)
+    ap.add_argument("--depth-lg", type=int, default=21)
+    ap.add_argument("--prefill", type=int, default=0, help="1: publish everything before the tiles start")
+    args = ap.parse_args()
+    a, t, modes = workload.cfg1(args.txns, seed=0x5EED0005)
+    ps = workload.payloads(a, t)
+    arena, offs, sizes = workload.pack_payloads(ps)
+    for T in [int(x) for x in args.tiles.split(",")]:
+        inl = tile.Link(1 << args.depth_lg, 1232)
+        vts = []
+        for k in range(T):
+            outl = tile.Link(1 << 12, tile.TPU_DCACHE_MTU)
+            vts.append((tile.VerifyTile(inl, outl, NullVerifier(), batch_txn_max=args.batch, inflight_max=4,
+                                        round_robin_idx=k, round_robin_cnt=T), outl))
+        prod = None
+        if args.prefill:
+            prod = tile.Producer(inl, arena, offs, sizes, rate_tps=0)
+            prod.join()
+        ths = [threading.Thread(target=lambda vt=vt: vt.run(len(ps), timeout_s=120)) for vt, _ in vts]
+        t0 = time.perf_counter()
+        if not args.prefill:
+            prod = tile.Producer(inl, arena, offs, sizes, rate_tps=0)
+        for th in ths:
+            th.start()
+        for th in ths:
+            th.join()
+        wall = time.perf_counter() - t0
+        _, prod_s = prod.join() if not args.prefill else (None, 0.0)
+        pub = sum(vt.stats()["published"] for vt, _ in vts)
+        print(json.dumps({"tiles": T, "txns": len(ps), "prefill": bool(args.prefill), "txns_per_s": round(len(ps) / wall, 1),
+                          "wall_s": round(wall, 4), "producer_s": round(prod_s, 4), "published": pub,
+                          "ns_per_frag_per_tile": round(wall * 1e9 / len(ps), 1)}), flush=True)
+        for vt, _ in vts:
+            vt.close()
+
+
+if __name__ == "__main__":
+    main()
