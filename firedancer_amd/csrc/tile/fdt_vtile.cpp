@@ -248,8 +248,10 @@ struct fdgpu_vtile {
     while (!inflight.empty()) {
       Batch *b = inflight.front();
       if (!b->done) {
+        const uint64_t t0 = now_ns();
         const int rc = b->staged ? ver.poll_keep(ver.ctx, b->ticket, b->codes.data(), 0)
                                  : ver.poll(ver.ctx, b->ticket, b->codes.data(), 0);
+        st.poll_ns += now_ns() - t0;
         if (rc == FDGPU_PENDING) break;
         if (rc != FDGPU_OK) return rc;
         b->done = true;
@@ -281,13 +283,19 @@ struct fdgpu_vtile {
 
   /* ingest available frags into the open batch (stops when it is full) */
   void ingest() {
+    const uint64_t t_in = now_ns();
+    struct Acc { uint64_t &ns; uint64_t t; ~Acc() { ns += now_ns() - t; } } acc{st.ingest_ns, t_in};
     if (!open) {
-      if (pool.empty()) return;
+      if (pool.empty()) { st.no_slot_steps++; return; }
       Batch *nb = pool.back();
       if (ver.stage) {                                  /* zero-copy: frags go straight to pinned memory */
         uint64_t cap = 0;
+        const uint64_t t0 = now_ns();
         uint8_t *p = ver.stage(ver.ctx, &cap);
-        if (!p) return;                                 /* every slot busy: resolve first */
+        const uint64_t dt = now_ns() - t0;
+        st.submit_ns += dt;
+        acc.t += dt;                                    /* counted as submit time, not ingest */
+        if (!p) { st.no_slot_steps++; return; }         /* every slot busy: resolve first */
         nb->ap = p; nb->cap = cap; nb->staged = true;
       } else {
         nb->ap = nb->arena.data(); nb->cap = nb->arena.size();
@@ -363,9 +371,11 @@ struct fdgpu_vtile {
                       open->sig_cnt + 16 > cfg.batch_sig_max;
     if (!full && !force && now_ns() - open->t_first < cfg.batch_wait_ns) return 0;
     if (inflight.size() >= cfg.inflight_max) return 0;
+    const uint64_t t0 = now_ns();
     const int64_t t = open->staged
         ? ver.submit_staged(ver.ctx, open->arena_used, open->txns.data(), open->txns.size())
         : ver.submit(ver.ctx, open->ap, open->arena_used, open->txns.data(), open->txns.size());
+    st.submit_ns += now_ns() - t0;
     if (t == FDGPU_ERR_FULL) return 0;
     if (t == FDGPU_ERR_INVAL) { reject_open(); return 0; }
     if (t < 0) return (int)t;

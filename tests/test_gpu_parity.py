@@ -497,3 +497,44 @@ def test_full_length_fallback_path(vectors, oracle):
         assert (got == oracle.verify_txns(arena, txns, nthreads=8)).all()
     finally:
         eng.close()
+
+
+def test_engines_share_device_table(oracle):
+    """Engines opened on one device share its fixed-base comb table
+    (refcounted): closing the engine that built it leaves the others
+    verifying correctly, a later open reuses the table, and concurrent
+    batches of two engines give the oracle's codes."""
+    arena, txns, _ = workload.cfg1(5000, seed=0x0B01)
+    exp = oracle.verify_txns(arena, txns, nthreads=8)
+    e1 = fa.VerifyEngine(0, max_txn=8192, ring_depth=2)
+    e2 = fa.VerifyEngine(0, max_txn=8192, ring_depth=2)
+    try:
+        t1, t2 = e1.submit(arena, txns), e2.submit(arena, txns)
+        assert (e1.poll(t1, blocking=True) == exp).all()
+        assert (e2.poll(t2, blocking=True) == exp).all()
+        e1.close()                                       # the table's builder goes first
+        assert (e2.verify_txns(arena, txns) == exp).all()
+        e3 = fa.VerifyEngine(0, max_txn=8192, ring_depth=2)
+        try:
+            assert (e3.verify_txns(arena, txns) == exp).all()
+        finally:
+            e3.close()
+        assert (e2.verify_txns(arena, txns) == exp).all()
+    finally:
+        e1.close()
+        e2.close()
+
+
+def test_nonblocking_poll_sees_completion(engine, oracle):
+    """The ring slots' completion words: a non-blocking poll returns pending
+    until the batch's codes are on the host, then exactly the codes."""
+    arena, txns, _ = workload.cfg1(20000, seed=0x0B02)
+    exp = oracle.verify_txns(arena, txns, nthreads=8)
+    for _ in range(3):
+        tk = engine.submit(arena, txns)
+        got = None
+        for _ in range(10_000_000):
+            got = engine.poll(tk, blocking=False)
+            if got is not None:
+                break
+        assert got is not None and (got == exp).all()

@@ -39,6 +39,8 @@ def main():
     ap.add_argument("--mux", type=int, default=0,
                     help="1: the verify tile as mux callbacks (fdgpu_vmux on fdt_mux_run; frags copied once into "
                          "the registered out dcache and DMA'd from there), 0: the step-loop tile (fdgpu_vtile)")
+    ap.add_argument("--pin", type=int, default=1,
+                    help="1: producer and each tile thread pinned to its own physical core (workload.physical_cpus)")
     ap.add_argument("--out", default="")
     ap.add_argument("--sweep", default="", help="';'-separated runs of 'tiles,batch,inflight,rate' over the same txns")
     args = ap.parse_args()
@@ -66,6 +68,19 @@ def main():
         with open(args.out, "w") as f:
             f.write("\n".join(lines) + "\n")
     return 0 if ok else 1
+
+
+def start_producer(args, inl, arena, offs, sizes, rate, cpus):
+    """The producer's C thread inherits the creating thread's CPU mask: pin
+    this thread to cpus[0] around its start."""
+    if not args.pin:
+        return tile.Producer(inl, arena, offs, sizes, rate_tps=rate)
+    keep = os.sched_getaffinity(0)
+    os.sched_setaffinity(0, {cpus[0]})
+    try:
+        return tile.Producer(inl, arena, offs, sizes, rate_tps=rate)
+    finally:
+        os.sched_setaffinity(0, keep)
 
 
 def warm(engines, inflight):
@@ -97,15 +112,19 @@ def run_once(args, ps, arena, offs, sizes, n_sig, modes, tiles_n, batch, infligh
 
     errs = []
 
-    def run(vt):
+    cpus = workload.physical_cpus()
+
+    def run(vt, k):
         try:
+            if args.pin:
+                os.sched_setaffinity(0, {cpus[(1 + k) % len(cpus)]})   # this thread only
             vt.run(len(ps), timeout_s=300)
         except Exception as e:  # noqa: BLE001
             errs.append(repr(e))
 
-    ths = [threading.Thread(target=run, args=(vt,)) for vt in vts]
+    ths = [threading.Thread(target=run, args=(vt, k)) for k, vt in enumerate(vts)]
     start = time.perf_counter()
-    prod = tile.Producer(inl, arena, offs, sizes, rate_tps=rate)
+    prod = start_producer(args, inl, arena, offs, sizes, rate, cpus)
     for th in ths:
         th.start()
     for th in ths:
@@ -158,7 +177,7 @@ def run_once_mux(args, ps, arena, offs, sizes, n_sig, modes, tiles_n, batch, inf
                                       batch_wait_us=args.wait_us, round_robin_idx=k, round_robin_cnt=tiles_n))
         vers.append((ver, outl))
     start = time.perf_counter()
-    prod = tile.Producer(inl, arena, offs, sizes, rate_tps=rate)
+    prod = start_producer(args, inl, arena, offs, sizes, rate, workload.physical_cpus())
     for vm in vms:
         vm.start()
     while any(vm.final_cnt() < len(ps) for vm in vms):

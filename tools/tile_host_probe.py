@@ -53,7 +53,12 @@ def main():
         if args.prefill:
             prod = tile.Producer(inl, arena, offs, sizes, rate_tps=0)
             prod.join()
-        ths = [threading.Thread(target=lambda vt=vt: vt.run(len(ps), timeout_s=120)) for vt, _ in vts]
+        cpus = workload.physical_cpus()
+
+        def body(vt, k):
+            os.sched_setaffinity(0, {cpus[(1 + k) % len(cpus)]})
+            vt.run(len(ps), timeout_s=120)
+        ths = [threading.Thread(target=body, args=(vt, k)) for k, (vt, _) in enumerate(vts)]
         t0 = time.perf_counter()
         if not args.prefill:
             prod = tile.Producer(inl, arena, offs, sizes, rate_tps=0)
@@ -63,10 +68,13 @@ def main():
             th.join()
         wall = time.perf_counter() - t0
         _, prod_s = prod.join() if not args.prefill else (None, 0.0)
-        pub = sum(vt.stats()["published"] for vt, _ in vts)
+        sts = [vt.stats() for vt, _ in vts]
+        pub = sum(x["published"] for x in sts)
         print(json.dumps({"tiles": T, "txns": len(ps), "prefill": bool(args.prefill), "txns_per_s": round(len(ps) / wall, 1),
                           "wall_s": round(wall, 4), "producer_s": round(prod_s, 4), "published": pub,
-                          "ns_per_frag_per_tile": round(wall * 1e9 / len(ps), 1)}), flush=True)
+                          "ns_per_frag_per_tile": round(wall * 1e9 / len(ps), 1),
+                          "ingest_ms_per_tile": [round(x["ingest_ns"] / 1e6, 1) for x in sts],
+                          "submit_ms_per_tile": [round(x["submit_ns"] / 1e6, 1) for x in sts]}), flush=True)
         for vt, _ in vts:
             vt.close()
 
