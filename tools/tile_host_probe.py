@@ -38,7 +38,17 @@ def main():
     ap.add_argument("--batch", type=int, default=16384)
     ap.add_argument("--depth-lg", type=int, default=21)
     ap.add_argument("--prefill", type=int, default=0, help="1: publish everything before the tiles start")
+    ap.add_argument("--cpus", default="", help="comma-separated CPUs for tile k (default: physical cores 1, 2, ...)"
+                                               "; 'none' leaves the threads unpinned")
     args = ap.parse_args()
+    topo = {}
+    for cpu in sorted(os.sched_getaffinity(0)):
+        b = f"/sys/devices/system/cpu/cpu{cpu}/topology/"
+        try:
+            topo[cpu] = tuple(open(b + f).read().strip() for f in ("physical_package_id", "die_id", "core_id"))
+        except OSError:
+            pass
+    print(json.dumps({"affinity_topology(package,die,core)": topo}), flush=True)
     a, t, modes = workload.cfg1(args.txns, seed=0x5EED0005)
     ps = workload.payloads(a, t)
     arena, offs, sizes = workload.pack_payloads(ps)
@@ -53,10 +63,12 @@ def main():
         if args.prefill:
             prod = tile.Producer(inl, arena, offs, sizes, rate_tps=0)
             prod.join()
-        cpus = workload.physical_cpus()
+        cpus = [int(x) for x in args.cpus.split(",")] if args.cpus not in ("", "none") else \
+            workload.physical_cpus()[1:] or [0]
 
         def body(vt, k):
-            os.sched_setaffinity(0, {cpus[(1 + k) % len(cpus)]})
+            if args.cpus != "none":
+                os.sched_setaffinity(0, {cpus[k % len(cpus)]})
             vt.run(len(ps), timeout_s=120)
         ths = [threading.Thread(target=body, args=(vt, k)) for k, (vt, _) in enumerate(vts)]
         t0 = time.perf_counter()
