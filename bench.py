@@ -56,6 +56,7 @@ def parse():
                     help="device batches verified round-robin, each on its own HIP stream (1: one stream)")
     ap.add_argument("--cfg3-txns", type=int, default=150_000,
                     help="multi-signature (cfg3) txns for the secondary device-resident line (0: skip)")
+    ap.add_argument("--tile", type=int, default=1, help="1: add the cfg5 verify-tile lines (tango in -> GPU -> tango out)")
     ap.add_argument("--adv-txns", type=int, default=1_000_000,
                     help="txns of each adversarial batch (all equation failures / all corrupted R; 0: skip)")
     return ap.parse_args()
@@ -168,6 +169,59 @@ def latency_and_pcie(eng, arena, txns, batch, nbatches):
     eng.host_unregister(arena)
     lat = np.array(lat)
     return float(np.percentile(lat, 50)), float(np.percentile(lat, 99)), pcie, pcie_reg
+
+
+def tile_lines(eng, arena, txns, modes):
+    """BASELINE configs[4] (cfg5) on this rank's GPU: the verify tile
+    (fdgpu_vtile: tango in -> parse -> batched GPU verify -> tcache -> tango
+    out) over this rank's cfg1 txns as raw frags, one tile thread and a
+    producer thread pinned to their own cores, 16K-txn batches, 4 in flight.
+    'backlog': the producer publishes as fast as it can into a 2^21-deep
+    link; 'paced': 8M txn/s into a 2^17-deep link (line rate: the tile must
+    keep up with no overrun).  Every run checks that exactly the verified
+    txns were published."""
+    import threading
+    from firedancer_amd import tile, workload
+    offs = txns["sig_off"].astype(np.uint64) - 1                 # payload = [sig_cnt][sigs][message]
+    sizes = (txns["msg_off"].astype(np.uint64) + txns["msg_sz"] - offs).astype(np.uint32)
+    expected = int((modes == 0).sum())
+    cpus = workload.physical_cpus()
+    out = {}
+    for name, depth_lg, rate in (("backlog", 21, 0.0), ("paced_8M", 17, 8e6)):
+        inl = tile.Link(1 << depth_lg, 1232)
+        outl = tile.Link(1 << 12, tile.TPU_DCACHE_MTU)
+        ver = tile.EngineVerifier([eng])
+        vt = tile.VerifyTile(inl, outl, ver, batch_txn_max=16384, inflight_max=4, batch_wait_us=200)
+        err = []
+
+        def body():
+            try:
+                os.sched_setaffinity(0, {cpus[1 % len(cpus)]})
+                vt.run(len(txns), timeout_s=120)
+            except Exception as e:  # noqa: BLE001
+                err.append(repr(e))
+        th = threading.Thread(target=body)
+        keep = os.sched_getaffinity(0)
+        os.sched_setaffinity(0, {cpus[0]})               # the producer's C thread inherits this mask
+        t0 = time.perf_counter()
+        prod = tile.Producer(inl, arena, offs, sizes, rate_tps=rate)
+        os.sched_setaffinity(0, keep)
+        th.start()
+        th.join()
+        wall = time.perf_counter() - t0
+        prod.join()
+        st = vt.stats()
+        lat = vt.latencies_ns() / 1e6
+        vt.close()
+        ver.close()
+        out[f"tile_{name}_txns_per_s"] = round(len(txns) / wall, 1)
+        out[f"tile_{name}_batch_latency_ms_p50_p99"] = [round(float(np.percentile(lat, 50)), 3),
+                                                       round(float(np.percentile(lat, 99)), 3)] if len(lat) else None
+        out[f"tile_{name}_overruns"] = int(st["overrun"])
+        out[f"tile_{name}_published_ok"] = (not err) and int(st["published"]) == expected
+    out["tile_config"] = ("1 verify tile thread + 1 producer thread, cfg1 frags, batch 16384 txns, 4 in flight; "
+                          "backlog: 2^21-deep link at producer speed; paced_8M: 8M txn/s offered, 2^17-deep link")
+    return out
 
 
 def cpu_model():
@@ -318,6 +372,12 @@ def main():
                   "latency_batch_txns": args.latency_batch,
                   "pcie_inclusive_sigs_per_s_per_gpu": round(pcie, 1),
                   "pcie_inclusive_registered_sigs_per_s_per_gpu": round(pcie_reg, 1)}
+        if args.tile:
+            tl = tile_lines(eng, arena, txns, modes)
+            tl["tile_backlog_txns_per_s_node"] = round(dist.sum(tl["tile_backlog_txns_per_s"]), 1)
+            tl["tile_paced_8M_published_ok_all_ranks"] = dist.sum(1 if tl["tile_paced_8M_published_ok"] else 0) \
+                == dist.world
+            extras.update(tl)
         if args.cfg3_txns:
             eng_nb = VerifyEngine(dist.local_rank, max_txn=1024, ring_depth=1, bucket=False)
             extras.update(cfg3_rate(eng, eng_nb, args.cfg3_txns, workload.CFG3_SEED + dist.rank))
