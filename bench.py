@@ -100,6 +100,30 @@ class Dist:
         if self.dist:
             self.dist.destroy_process_group()
 
+    def cpus(self):
+        """This rank's host cores: one logical CPU per physical core of its
+        affinity, at most the box's 16-CPU share.  When ranks on the node
+        see overlapping affinities (one process per GPU, unpinned), the union
+        of physical cores is split into disjoint per-rank ranges, so the tile
+        threads and the oracle of 8 ranks never share a core."""
+        from firedancer_amd.workload import physical_cpus, BOX_CPU_SHARE
+        mine = physical_cpus(limit=1 << 20)
+        if not self.dist:
+            return mine[:BOX_CPU_SHARE]
+        every = [None] * self.world
+        self.dist.all_gather_object(every, mine)
+        seen = set()
+        overlap = False
+        for c in every:
+            overlap |= bool(seen & set(c))
+            seen |= set(c)
+        if not overlap:
+            return mine[:BOX_CPU_SHARE]
+        union = sorted(seen)
+        k = max(1, len(union) // self.world)
+        part = union[self.rank * k:(self.rank + 1) * k] or union[-k:]
+        return part[:BOX_CPU_SHARE]
+
 
 def rank_seed(rank):
     """Each rank verifies its own independent cfg1 shard (weak scaling)."""
@@ -171,7 +195,7 @@ def latency_and_pcie(eng, arena, txns, batch, nbatches):
     return float(np.percentile(lat, 50)), float(np.percentile(lat, 99)), pcie, pcie_reg
 
 
-def tile_lines(eng, arena, txns, modes):
+def tile_lines(eng, arena, txns, modes, cpus):
     """BASELINE configs[4] (cfg5) on this rank's GPU: the verify tile
     (fdgpu_vtile: tango in -> parse -> batched GPU verify -> tcache -> tango
     out) over this rank's cfg1 txns as raw frags, one tile thread and a
@@ -185,7 +209,6 @@ def tile_lines(eng, arena, txns, modes):
     offs = txns["sig_off"].astype(np.uint64) - 1                 # payload = [sig_cnt][sigs][message]
     sizes = (txns["msg_off"].astype(np.uint64) + txns["msg_sz"] - offs).astype(np.uint32)
     expected = int((modes == 0).sum())
-    cpus = workload.physical_cpus()
     out = {}
     for name, depth_lg, rate in (("backlog", 21, 0.0), ("paced_8M", 17, 8e6)):
         inl = tile.Link(1 << depth_lg, 1232)
@@ -234,13 +257,11 @@ def cpu_model():
     return "unknown"
 
 
-def cpu_baseline(arena, txns, sample):
+def cpu_baseline(arena, txns, sample, cpus):
     """The oracle (C restatement) on one pinned thread per physical core of
     this host (at most the GPU box's 16-CPU share), inputs statically
     partitioned.  Returns (baseline record, the CPU codes of the sample)."""
     from oracle import oracle as orc
-    from firedancer_amd.workload import physical_cpus
-    cpus = physical_cpus()
     sub = txns[:sample]
     t0 = time.perf_counter()
     codes = orc.verify_txns(arena, sub, cpus=cpus)
@@ -255,7 +276,7 @@ def cpu_baseline(arena, txns, sample):
     return rec, codes
 
 
-def adversarial(eng, n_txn, seed, ref_ms_per_sig):
+def adversarial(eng, n_txn, seed, ref_ms_per_sig, cpus):
     """SURVEY §8(d) / test_ed25519.c:920-951 bad-sig/msg modes at batch
     scale: 1M single-signature txns where EVERY signature fails the
     equation (one message bit flipped -> ERR_MSG), and where every R is
@@ -271,7 +292,7 @@ def adversarial(eng, n_txn, seed, ref_ms_per_sig):
         b.verify()
         got = b.codes()
         _, kv, kc = b.time(5)
-        exp = orc.verify_txns(arena, txns, cpus=workload.physical_cpus())
+        exp = orc.verify_txns(arena, txns, cpus=cpus)
         sigs_per_s = b.n_sig / ((kv + kc) * 1e-3)
         out[f"adv_{name}_sigs_per_s"] = round(sigs_per_s, 1)
         out[f"adv_{name}_vs_cfg2_isolated"] = round(ref_ms_per_sig / ((kv + kc) / b.n_sig), 4)   # throughput ratio
@@ -327,6 +348,7 @@ def cfg3_rate(eng, eng_nobucket, n_txn, seed):
 def main():
     args = parse()
     dist = Dist()
+    cpus = dist.cpus()
     from firedancer_amd import VerifyEngine, _lib, workload
 
     t_gen = time.perf_counter()
@@ -373,7 +395,7 @@ def main():
                   "pcie_inclusive_sigs_per_s_per_gpu": round(pcie, 1),
                   "pcie_inclusive_registered_sigs_per_s_per_gpu": round(pcie_reg, 1)}
         if args.tile:
-            tl = tile_lines(eng, arena, txns, modes)
+            tl = tile_lines(eng, arena, txns, modes, cpus)
             tl["tile_backlog_txns_per_s_node"] = round(dist.sum(tl["tile_backlog_txns_per_s"]), 1)
             tl["tile_paced_8M_published_ok_all_ranks"] = dist.sum(1 if tl["tile_paced_8M_published_ok"] else 0) \
                 == dist.world
@@ -384,7 +406,7 @@ def main():
             eng_nb.close()
         if args.adv_txns:
             extras.update(adversarial(eng, args.adv_txns, workload.CFG1_SEED + 0x400 + dist.rank,
-                                      (kv_ms + kc_ms) / n_sig))
+                                      (kv_ms + kc_ms) / n_sig, cpus))
     cpu = None
     parity = {}
     if not args.no_extras:
@@ -393,10 +415,10 @@ def main():
         gpu_codes = batch.codes()
         n_chk = min(args.cpu_sample, len(txns))
         if dist.rank == 0 and dist.world == 1:
-            cpu, cpu_codes = cpu_baseline(arena, txns, n_chk)
+            cpu, cpu_codes = cpu_baseline(arena, txns, n_chk, cpus)
         else:
             from oracle import oracle as orc
-            cpu_codes = orc.verify_txns(arena, txns[:n_chk], cpus=workload.physical_cpus())
+            cpu_codes = orc.verify_txns(arena, txns[:n_chk], cpus=cpus)
         mism = int((gpu_codes[:n_chk] != cpu_codes).sum())
         parity = {"parity_checked_txns": int(dist.sum(n_chk)), "parity_mismatches": int(dist.sum(mism)),
                   "parity_codes": {int(c): int(k) for c, k in zip(*np.unique(cpu_codes, return_counts=True))}}

@@ -18,6 +18,7 @@ from oracle import oracle as orc  # noqa: E402
 def main():
     dist = bench.Dist()
     assert dist.world == 2
+    cpus = dist.cpus()                       # this rank's cores (disjoint from the other rank's)
     n = 64
     arena, txns, modes = workload.cfg1(n, seed=bench.rank_seed(dist.rank), nthreads=1)
     dist.barrier()
@@ -32,7 +33,7 @@ def main():
     first = int.from_bytes(arena[1:9].tobytes(), "little")
     firsts = dist.sum(first % 1000003)
     out = {"rank": dist.rank, "value": value, "dt_max": dt_max, "ok": ok, "firsts_sum": firsts,
-           "first": first % 1000003}
+           "first": first % 1000003, "cpus": cpus}
     path = os.environ["MULTIRANK_OUT"] + f".{dist.rank}"
     json.dump(out, open(path, "w"))
     dist.close()

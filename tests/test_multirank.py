@@ -23,3 +23,6 @@ def test_two_rank_gloo(tmp_path):
     assert abs(res[0]["dt_max"] - res[1]["dt_max"]) < 1e-9     # both ranks agree on the max
     assert abs(res[0]["value"] - res[1]["value"]) < 1e-6
     assert res[0]["value"] > 0
+    # ranks sharing one host affinity get disjoint physical cores (tile threads, oracle)
+    assert res[0]["cpus"] and res[1]["cpus"]
+    assert not set(res[0]["cpus"]) & set(res[1]["cpus"])
