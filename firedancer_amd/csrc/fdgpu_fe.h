@@ -134,6 +134,24 @@ FDG_DEV void fe_carry(fe &h) {
   t = h.v[0] >> 26; h.v[0] &= M26; h.v[1] += t;
 }
 
+/* One parallel carry pass (every limb's excess moves up once, limb 9's
+   wraps into limb 0 times 19): inputs up to 2^31 come out with limbs <=
+   mask + 2^6 (limb 0: 2^26 + 19 * 2^6), inside R.  The ten steps are
+   independent, 3 instructions each (fe_carry's sequential 12-step chain
+   is 36 and serial). */
+FDG_DEV void fe_carry_par(fe &h) {
+  uint32_t c[10];
+#pragma unroll
+  for (int i = 0; i < 10; i++) {
+    const int w = (i & 1) ? 25 : 26;
+    c[i] = h.v[i] >> w;
+    h.v[i] &= (1u << w) - 1;
+  }
+  h.v[0] += 19u * c[9];
+#pragma unroll
+  for (int i = 1; i < 10; i++) h.v[i] += c[i - 1];
+}
+
 /* Column-sum schemes (tools/ubench_carry.hip, profiles/r01_ubench_carry.json):
    FDGPU_FE_FF=1 (default) sums the columns in order 0..9 and starts each
    column's v_mad_u64_u32 chain from the previous column's carry, so the
@@ -239,6 +257,28 @@ template <> struct madc<10> {
   }
 };
 
+/* madc0<N>::run(s, a, b): s = a[0] b[0] + ... + a[N-1] b[N-1] -- a column
+   chain that starts from zero (column 0 of a product): the first mad takes
+   the inline constant 0 as its addend, so no zeroed register pair is
+   materialised per product. */
+template <int N> struct madc0;
+template <> struct madc0<6> {
+  static FDG_DEV void run(uint64_t &s, const uint32_t *a, const uint32_t *b) {
+    uint64_t cc;
+    asm("v_mad_u64_u32 %0, %1, %2, %3, 0\n" "v_mad_u64_u32 %0, %1, %4, %5, %0\n" "v_mad_u64_u32 %0, %1, %6, %7, %0\n" "v_mad_u64_u32 %0, %1, %8, %9, %0\n" "v_mad_u64_u32 %0, %1, %10, %11, %0\n" "v_mad_u64_u32 %0, %1, %12, %13, %0\n"
+        : "=&v"(s), "=&s"(cc) : "v"(a[0]), "v"(b[0]), "v"(a[1]), "v"(b[1]), "v"(a[2]), "v"(b[2]), "v"(a[3]), "v"(b[3]), "v"(a[4]), "v"(b[4]), "v"(a[5]), "v"(b[5]));
+    (void)cc;
+  }
+};
+template <> struct madc0<10> {
+  static FDG_DEV void run(uint64_t &s, const uint32_t *a, const uint32_t *b) {
+    uint64_t cc;
+    asm("v_mad_u64_u32 %0, %1, %2, %3, 0\n" "v_mad_u64_u32 %0, %1, %4, %5, %0\n" "v_mad_u64_u32 %0, %1, %6, %7, %0\n" "v_mad_u64_u32 %0, %1, %8, %9, %0\n" "v_mad_u64_u32 %0, %1, %10, %11, %0\n" "v_mad_u64_u32 %0, %1, %12, %13, %0\n" "v_mad_u64_u32 %0, %1, %14, %15, %0\n" "v_mad_u64_u32 %0, %1, %16, %17, %0\n" "v_mad_u64_u32 %0, %1, %18, %19, %0\n" "v_mad_u64_u32 %0, %1, %20, %21, %0\n"
+        : "=&v"(s), "=&s"(cc) : "v"(a[0]), "v"(b[0]), "v"(a[1]), "v"(b[1]), "v"(a[2]), "v"(b[2]), "v"(a[3]), "v"(b[3]), "v"(a[4]), "v"(b[4]), "v"(a[5]), "v"(b[5]), "v"(a[6]), "v"(b[6]), "v"(a[7]), "v"(b[7]), "v"(a[8]), "v"(b[8]), "v"(a[9]), "v"(b[9]));
+    (void)cc;
+  }
+};
+
 /* s += a * b as one v_mad_u64_u32 (carry-out SGPR pair unused) */
 FDG_DEV void mad_acc(uint64_t &s, uint32_t a, uint32_t b) {
   uint64_t cc;
@@ -282,7 +322,8 @@ FDG_DEV void fe_mul(fe &h, const fe &f, const fe &g) {
       ca[i] = dbl ? f2[i] : f.v[i];
       cb[i] = wrap ? g19[j] : g.v[j];
     }
-    madc<10>::run(s, ca, cb);
+    if (k == 0) madc0<10>::run(s, ca, cb);
+    else madc<10>::run(s, ca, cb);
 #else
 #pragma unroll
     for (int i = 0; i < 10; i++) {
@@ -354,6 +395,7 @@ FDG_DEV void fe_sq_sh(fe &h, const fe &f) {
       }
     }
     if (k & 1) madc<5>::run(s, ca, cb);             /* odd columns: 5 symmetric terms, even: 6 */
+    else if (k == 0) madc0<6>::run(s, ca, cb);
     else madc<6>::run(s, ca, cb);
 #else
 #pragma unroll

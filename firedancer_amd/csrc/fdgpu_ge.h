@@ -27,16 +27,21 @@ FDG_DEV void ge_p2_0(ge_p2 &h) { fe_0(h.X); fe_1(h.Y); fe_1(h.Z); }
 FDG_DEV void ge_p3_0(ge_p3 &h) { fe_0(h.X); fe_1(h.Y); fe_1(h.Z); fe_0(h.T); }
 FDG_DEV void ge_cached_0(ge_cached &h) { fe_1(h.YpX); fe_1(h.YmX); fe_0(h.Z2); h.Z2.v[0] = 2; fe_0(h.T2d); }
 
-/* p1p1 -> p2: 3M.  X' (S4|S) first operand, T' (R|S) second; Y' (A) x Z' (S|A). */
+/* p1p1 -> p2: 3M.  X' (S4|S) first operand, T' (R|S) second; Z' (S|A|2^27.6)
+   first x Y' (A) second.  Operand roles are fixed per coordinate (X', Z'
+   always first, T', Y' always second) so the pre-scaled operands fe_mul
+   derives (2f on odd limbs of the first, 19g of the second) are computed
+   once per coordinate and shared by the products that reuse it (and by the
+   T = X'Y' product the chain adds for a p3). */
 FDG_DEV void ge_p1p1_to_p2(ge_p2 &r, const ge_p1p1 &p) {
   fe_mul(r.X, p.X, p.T);
-  fe_mul(r.Y, p.Y, p.Z);
+  fe_mul(r.Y, p.Z, p.Y);
   fe_mul(r.Z, p.Z, p.T);
 }
-/* p1p1 -> p3: 4M. */
+/* p1p1 -> p3: 4M (roles as in ge_p1p1_to_p2). */
 FDG_DEV void ge_p1p1_to_p3(ge_p3 &r, const ge_p1p1 &p) {
   fe_mul(r.X, p.X, p.T);
-  fe_mul(r.Y, p.Y, p.Z);
+  fe_mul(r.Y, p.Z, p.Y);
   fe_mul(r.Z, p.Z, p.T);
   fe_mul(r.T, p.X, p.Y);
 }
@@ -65,7 +70,7 @@ FDG_DEV void ge_dbl(ge_p1p1 &r, const ge_p2 &p) {
   fe_add(r.T, r.T, r.T);           /* B = 2 Z^2 */
 #endif
   fe_sub4(r.T, r.T, r.Z);          /* T' = B - Z' */
-  fe_carry(r.T);
+  fe_carry_par(r.T);
 }
 
 FDG_DEV void fe_cswap(fe &a, fe &b, bool c) {
@@ -170,7 +175,7 @@ FDG_DEV void ge_add_niels_ld(ge_p1p1 &r, const ge_p3 &p, const LD &ld, bool neg)
   fe_mul(r.Y, t, q);               /* B */
   fe_add(t, r.T, r.Z);
   fe_sub(r.T, r.T, r.Z);
-  fe_carry(r.T);
+  fe_carry_par(r.T);
   r.Z = t;
   fe_add(t, r.X, r.Y);
   fe_sub(r.X, r.X, r.Y);
@@ -253,7 +258,7 @@ FDG_DEV void ge_add_niels_regs(ge_p1p1 &r, const ge_p3 &p, const uint32_t (&q)[3
   fe_mul(r.Y, t, c);               /* B */
   fe_add(t, r.T, r.Z);
   fe_sub(r.T, r.T, r.Z);
-  fe_carry(r.T);
+  fe_carry_par(r.T);
   r.Z = t;
   fe_add(t, r.X, r.Y);
   fe_sub(r.X, r.X, r.Y);

@@ -702,6 +702,9 @@ FDG_DEV void hs_wscalar(uint32_t (&w)[8], const uint32_t (&v)[5], bool v_neg, co
 #ifndef HS_STAGE
 #define HS_STAGE 2
 #endif
+#ifndef HS_DBL_UNROLL
+#define HS_DBL_UNROLL 1
+#endif
 typedef __attribute__((address_space(3))) void lds_void_t;
 
 FDG_DEV void stage_entry(uint32_t *lds_wave, const uint32_t *tab, int e) {
@@ -757,7 +760,7 @@ FDG_DEV void hs_chain(ge_p1p1 &t, uint32_t (&ud)[5], uint32_t (&vd)[5], bool u_n
     atab_load(q, ta, du);
 #endif
     stage_entry(st_r, tr, dv);
-#pragma unroll 1
+#pragma unroll HS_DBL_UNROLL
     for (int r = 0; r < 4; r++) {
       ge_dbl(t, acc2);
       ge_p1p1_to_p2(acc2, t);

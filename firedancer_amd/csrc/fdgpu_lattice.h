@@ -361,12 +361,35 @@ FDG_HD void hs_split_euclid(hs_split_t &o, const uint32_t (&k)[8]) {
 #define HS_MAX_OUTER 200u     /* matrix applications + full steps (random k: ~6-10) */
 #define HS_MAX_INNER 48u      /* simulated steps per application (cofactors < 2^31) */
 
-/* floor(x / y) for integers 0 <= x < 2^53, 0 < y < 2^53 held in doubles:
-   the rounded quotient is never below the true floor (integers are
-   representable, rounding is monotonic), and the remainder is exact */
+/* 1/y to ~2^-52 relative: the hardware reciprocal (v_rcp_f64) and one
+   Newton step on the device, a division on the host */
+FDG_HD double hs_rcp(double y) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  const double r = __builtin_amdgcn_rcp(y);
+  return fma(r, fma(-y, r, 1.0), r);
+#else
+  return 1.0 / y;
+#endif
+}
+
+/* floor(x / y) for integers 0 <= x < 2^53, 0 < y < 2^53 held in doubles.
+   The estimate floor(x * (1/y)) is within one of the floor while the
+   quotient is below ~2^50 (every quotient the Lehmer simulation can take
+   is below 2^31: a larger one breaks it on the cofactor bound), and the
+   remainder x - q y is exact (an integer of magnitude < 2y < 2^54 computed
+   by one fma; its sign and its comparison with y are exact even when it
+   rounds), so one correction step gives the floor. */
 FDG_HD double hs_fdivf(double x, double y) {
-  const double q = floor(x / y);
-  return fma(-q, y, x) < 0.0 ? q - 1.0 : q;
+  const double q = floor(x * hs_rcp(y));
+  const double r = fma(-q, y, x);
+  return r < 0.0 ? q - 1.0 : (r >= y ? q + 1.0 : q);
+}
+
+/* q == floor(x / y) for integers 0 <= x < 2^53, 0 < y < 2^53: the remainder
+   x - q y lies in [0, y) (one fma, exact as above) */
+FDG_HD bool hs_isquot(double q, double x, double y) {
+  const double r = fma(-q, y, x);
+  return r >= 0.0 && r < y;
 }
 
 /* (x >> s) for an 8-limb x < 2^(s + 64), s < 256 (selects, no dynamic
@@ -455,7 +478,7 @@ FDG_HD void hs_split(hs_split_t &o, const uint32_t (&k)[8]) {
         for (uint32_t j = 0; j < HS_MAX_INNER; j++) {
           if (V + C <= 0.0 || V + D <= 0.0) break;
           const double q = hs_fdivf(U + A, V + C);
-          if (q != hs_fdivf(U + B, V + D)) break;
+          if (!hs_isquot(q, U + B, V + D)) break;     /* both brackets agree on q */
           const double Vn = fma(-q, V, U), Cn = fma(-q, C, A), Dn = fma(-q, D, B);
           if (fmax(fabs(Cn), fabs(Dn)) >= 2147483648.0) break;
           /* the true remainder / 2^s lies in (Vn + min(Cn, Dn), Vn + max(Cn, Dn)) */

@@ -39,7 +39,32 @@ __constant__ static const uint64_t SHA512_K[80] = {
   0x4cc5d4becb3e42b6ULL, 0x597f299cfc657e2aULL, 0x5fcb6fab3ad6faecULL, 0x6c44198c4a475817ULL,
 };
 
-FDG_DEV uint64_t rotr64(uint64_t x, int r) { return (x >> r) | (x << (64 - r)); }
+/* 64-bit rotate / shift as two v_alignbit_b32 (funnel shifts of the two
+   halves; r is a compile-time constant in every use); the generic lowering
+   is four 64-bit shifts and ors */
+FDG_DEV uint64_t rotr64(uint64_t x, int r) {
+  const uint32_t lo = (uint32_t)x, hi = (uint32_t)(x >> 32);
+  const uint32_t a = r < 32 ? hi : lo, b = r < 32 ? lo : hi, n = (uint32_t)(r & 31);
+  return ((uint64_t)__builtin_amdgcn_alignbit(b, a, n) << 32) | __builtin_amdgcn_alignbit(a, b, n);
+}
+/* majority of three bits, one v_bitop3_b32 per half (truth table 0xE8,
+   symmetric in its inputs) */
+FDG_DEV uint64_t maj64(uint64_t a, uint64_t b, uint64_t c) {
+  const uint32_t lo = __builtin_amdgcn_bitop3_b32((uint32_t)a, (uint32_t)b, (uint32_t)c, 0xE8);
+  const uint32_t hi = __builtin_amdgcn_bitop3_b32((uint32_t)(a >> 32), (uint32_t)(b >> 32), (uint32_t)(c >> 32), 0xE8);
+  return ((uint64_t)hi << 32) | lo;
+}
+FDG_DEV uint64_t shr64(uint64_t x, int r) {           /* r < 32 */
+  const uint32_t lo = (uint32_t)x, hi = (uint32_t)(x >> 32);
+  return ((uint64_t)(hi >> r) << 32) | __builtin_amdgcn_alignbit(hi, lo, (uint32_t)r);
+}
+/* a ^ b ^ c as one gfx950 v_bitop3_b32 per half (truth table 0x96: the
+   parity of the three inputs); the compiler emits two v_xor_b32 otherwise */
+FDG_DEV uint64_t xor3_64(uint64_t a, uint64_t b, uint64_t c) {
+  const uint32_t lo = __builtin_amdgcn_bitop3_b32((uint32_t)a, (uint32_t)b, (uint32_t)c, 0x96);
+  const uint32_t hi = __builtin_amdgcn_bitop3_b32((uint32_t)(a >> 32), (uint32_t)(b >> 32), (uint32_t)(c >> 32), 0x96);
+  return ((uint64_t)hi << 32) | lo;
+}
 FDG_DEV uint32_t bswap32(uint32_t x) { return __builtin_bswap32(x); }
 
 FDG_DEV void sha512_compress(uint64_t (&h)[8], uint64_t (&w)[16]) {
@@ -49,15 +74,15 @@ FDG_DEV void sha512_compress(uint64_t (&h)[8], uint64_t (&w)[16]) {
     for (int t = 0; t < 16; t++) {
       if (r) {
         const uint64_t w15 = w[(t + 1) & 15], w2 = w[(t + 14) & 15];
-        const uint64_t s0 = rotr64(w15, 1) ^ rotr64(w15, 8) ^ (w15 >> 7);
-        const uint64_t s1 = rotr64(w2, 19) ^ rotr64(w2, 61) ^ (w2 >> 6);
+        const uint64_t s0 = xor3_64(rotr64(w15, 1), rotr64(w15, 8), shr64(w15, 7));
+        const uint64_t s1 = xor3_64(rotr64(w2, 19), rotr64(w2, 61), shr64(w2, 6));
         w[t] += s0 + w[(t + 9) & 15] + s1;
       }
-      const uint64_t S1 = rotr64(e, 14) ^ rotr64(e, 18) ^ rotr64(e, 41);
+      const uint64_t S1 = xor3_64(rotr64(e, 14), rotr64(e, 18), rotr64(e, 41));
       const uint64_t ch = (e & f) ^ (~e & g);
       const uint64_t t1 = hh + S1 + ch + SHA512_K[r + t] + w[t];
-      const uint64_t S0 = rotr64(a, 28) ^ rotr64(a, 34) ^ rotr64(a, 39);
-      const uint64_t maj = (a & b) ^ (c & (a ^ b));
+      const uint64_t S0 = xor3_64(rotr64(a, 28), rotr64(a, 34), rotr64(a, 39));
+      const uint64_t maj = maj64(a, b, c);
       hh = g; g = f; f = e; e = d + t1; d = c; c = b; b = a; a = t1 + S0 + maj;
     }
   }
