@@ -81,6 +81,7 @@ def lib():
     L.fdgpu_debug_sha512.argtypes = [vp, vp, c.c_uint64, vp, c.c_uint64, vp]
     L.fdgpu_debug_hram.argtypes = [vp, vp, c.c_uint64, vp, c.c_uint64, vp]
     L.fdgpu_debug_sc_reduce.argtypes = [vp, vp, c.c_uint64, vp]
+    L.fdgpu_debug_hs_split.argtypes = [vp, vp, c.c_uint64, vp]
     L.fdgpu_debug_sig_codes.argtypes = [vp, vp, c.c_uint64, vp, c.c_uint64, vp]
     L.fdgpu_dev_batch_upload.argtypes = [vp, vp, c.c_uint64, vp, c.c_uint64]
     L.fdgpu_dev_batch_upload.restype = vp
@@ -102,7 +103,7 @@ def lib():
     L.fdgpu_sync.argtypes = [vp]
     L.fdgpu_sync.restype = c.c_int
     for fn in ("fdgpu_debug_fe_ops", "fdgpu_debug_decode", "fdgpu_debug_sha512", "fdgpu_debug_hram",
-               "fdgpu_debug_sc_reduce", "fdgpu_debug_sig_codes"):
+               "fdgpu_debug_sc_reduce", "fdgpu_debug_hs_split", "fdgpu_debug_sig_codes"):
         getattr(L, fn).restype = c.c_int
     _LIB = L
     return L

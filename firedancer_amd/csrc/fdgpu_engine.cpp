@@ -915,6 +915,20 @@ int fdgpu_debug_sc_reduce(fdgpu_engine_t *e, uint8_t const *in, uint64_t n, uint
   return FDGPU_OK;
 }
 
+int fdgpu_debug_hs_split(fdgpu_engine_t *e, uint8_t const *k, uint64_t n, uint8_t *out) {
+  if (!e || !n) return FDGPU_ERR_INVAL;
+  HIPCHK(hipSetDevice(e->device), FDGPU_ERR_DEVICE);
+  DevBuf din, dout;
+  DALLOC(din, uint32_t, n * 8);
+  DALLOC(dout, uint32_t, n * 16);
+  HIPCHK(hipMemcpy(din.p, k, n * 32, hipMemcpyHostToDevice), FDGPU_ERR_DEVICE);
+  HIPCHK(fdgpu_launch_test_hs_split((uint32_t *)din.p, (uint32_t *)dout.p, (uint32_t)n, e->compute),
+         FDGPU_ERR_DEVICE);
+  HIPCHK(hipStreamSynchronize(e->compute), FDGPU_ERR_DEVICE);
+  HIPCHK(hipMemcpy(out, dout.p, n * 64, hipMemcpyDeviceToHost), FDGPU_ERR_DEVICE);
+  return FDGPU_OK;
+}
+
 int fdgpu_debug_sig_codes(fdgpu_engine_t *e, uint8_t const *arena, uint64_t arena_sz, fdgpu_txn_t const *txns,
                           uint64_t txn_cnt, int8_t *sig_codes) {
   if (!e) return FDGPU_ERR_INVAL;

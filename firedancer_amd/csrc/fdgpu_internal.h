@@ -92,6 +92,7 @@ hipError_t fdgpu_launch_test_sha512(const uint8_t *d_arena, const fdgpu_sig_desc
 hipError_t fdgpu_launch_test_hram(const uint8_t *d_arena, const fdgpu_sig_desc_t *d_sigs, uint32_t n,
                                   uint32_t *d_out, hipStream_t stream);
 hipError_t fdgpu_launch_test_sc_reduce(const uint32_t *d_in, uint32_t *d_out, uint32_t n, hipStream_t stream);
+hipError_t fdgpu_launch_test_hs_split(const uint32_t *d_in, uint32_t *d_out, uint32_t n, hipStream_t stream);
 
 #ifdef __cplusplus
 }

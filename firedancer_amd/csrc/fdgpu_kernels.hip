@@ -1065,6 +1065,21 @@ __global__ void __launch_bounds__(64) fdgpu_test_sc_reduce_kernel(const uint32_t
   for (int j = 0; j < 8; j++) out[8 * i + j] = r[j];
 }
 
+/* hs_split on the device (v_rcp_f64 quotients) for the parity tests: n
+   scalars k < L (8 words each) -> 16 words each: |u| (5), |v| (5), ok,
+   u_neg, v_neg, bits, 0, 0 */
+__global__ void __launch_bounds__(64) fdgpu_test_hs_split_kernel(const uint32_t *in, uint32_t *out, uint32_t n) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  uint32_t k[8];
+  for (int j = 0; j < 8; j++) k[j] = i < n ? in[8 * i + j] : 0u;
+  hs_split_t o;
+  hs_split(o, k);                               /* every lane runs it: the loops are wave-uniform */
+  if (i >= n) return;
+  uint32_t *w = out + 16 * (size_t)i;
+  for (int j = 0; j < 5; j++) { w[j] = o.u[j]; w[5 + j] = o.v[j]; }
+  w[10] = o.ok; w[11] = o.u_neg; w[12] = o.v_neg; w[13] = o.bits; w[14] = 0u; w[15] = 0u;
+}
+
 }  // namespace
 
 extern "C" {
@@ -1192,6 +1207,10 @@ hipError_t fdgpu_launch_test_hram(const uint8_t *d_arena, const fdgpu_sig_desc_t
 }
 hipError_t fdgpu_launch_test_sc_reduce(const uint32_t *d_in, uint32_t *d_out, uint32_t n, hipStream_t stream) {
   hipLaunchKernelGGL(fdgpu_test_sc_reduce_kernel, dim3((n + 63) / 64), dim3(64), 0, stream, d_in, d_out, n);
+  return hipGetLastError();
+}
+hipError_t fdgpu_launch_test_hs_split(const uint32_t *d_in, uint32_t *d_out, uint32_t n, hipStream_t stream) {
+  hipLaunchKernelGGL(fdgpu_test_hs_split_kernel, dim3((n + 63) / 64), dim3(64), 0, stream, d_in, d_out, n);
   return hipGetLastError();
 }
 

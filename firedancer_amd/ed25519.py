@@ -220,6 +220,13 @@ class VerifyEngine:
         self._chk(_lib.lib().fdgpu_debug_sc_reduce(self._h, x.ctypes.data, len(x), out.ctypes.data), "debug_sc_reduce")
         return out
 
+    def debug_hs_split(self, k):
+        """k: uint8[n, 32] scalars < L -> uint32[n, 16] (|u|, |v|, ok, u_neg, v_neg, bits)"""
+        k = np.ascontiguousarray(k, dtype=np.uint8).reshape(-1, 32)
+        out = np.zeros((len(k), 16), dtype=np.uint32)
+        self._chk(_lib.lib().fdgpu_debug_hs_split(self._h, k.ctypes.data, len(k), out.ctypes.data), "debug_hs_split")
+        return out
+
     def debug_sig_codes(self, arena, txns):
         arena = np.ascontiguousarray(arena, dtype=np.uint8)
         txns = np.ascontiguousarray(txns, dtype=TXN_DTYPE)

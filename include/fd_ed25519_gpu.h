@@ -240,6 +240,10 @@ int fdgpu_debug_hram( fdgpu_engine_t * e, uint8_t const * arena, uint64_t arena_
                       fdgpu_txn_t const * txns, uint64_t n, uint8_t * out );
 /* n 64-B little-endian integers -> n x 32 B (x mod L) */
 int fdgpu_debug_sc_reduce( fdgpu_engine_t * e, uint8_t const * in, uint64_t n, uint8_t * out );
+/* the half-size scalar split of n scalars k < L (32-B little-endian each)
+   on the device -> n x 64 B: |u| (20 B), |v| (20 B), then u32 ok, u_neg,
+   v_neg, bits and 8 zero bytes (fdgpu_lattice.h hs_split) */
+int fdgpu_debug_hs_split( fdgpu_engine_t * e, uint8_t const * k, uint64_t n, uint8_t * out );
 /* per-signature codes of a batch (single-signature verify code of each
    signature, in txn order) -> sig_codes[sum sig_cnt] */
 int fdgpu_debug_sig_codes( fdgpu_engine_t * e, uint8_t const * arena, uint64_t arena_sz,
