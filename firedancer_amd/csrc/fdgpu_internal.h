@@ -33,7 +33,9 @@ typedef struct {
    entry), so [S]B costs NDIG mixed additions and no doublings.  Tables live
    in HBM (W=16: 16 x 32769 x 128 B = 67 MB, resident in the 256 MB Infinity
    Cache). */
-#define FDGPU_BCOMB_BITS    16u
+#ifndef FDGPU_BCOMB_BITS
+#define FDGPU_BCOMB_BITS    16u           /* comb radix: NDIG tables of 2^(W-1)+1 entries */
+#endif
 #define FDGPU_BCOMB_NDIG    ((254u + FDGPU_BCOMB_BITS - 1u) / FDGPU_BCOMB_BITS)   /* covers S < 2^253 + carry */
 #define FDGPU_BCOMB_ENTRIES ((1u << (FDGPU_BCOMB_BITS - 1u)) + 1u)
 #define FDGPU_BCOMB_STRIDE  32u           /* u32 per entry (30 used): one 128-B line */

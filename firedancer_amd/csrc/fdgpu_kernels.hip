@@ -91,7 +91,7 @@ __global__ void __launch_bounds__(64) fdgpu_bcomb_fill_kernel(const uint32_t *ba
   ge_cached bc; ge_p3_to_cached(bc, base);
   ge_p3 P; ge_p3_0(P);
   ge_p1p1 t;
-  for (int bit = 15; bit >= 0; bit--) {
+  for (int bit = (int)BC_W - 1; bit >= 0; bit--) {                   /* j0 < 2^(W-1) + 1 */
     ge_p2 a; ge_p3_to_p2(a, P); ge_dbl(t, a); ge_p1p1_to_p3(P, t);
     if ((j0 >> bit) & 1u) { ge_add_cached(t, P, bc, false); ge_p1p1_to_p3(P, t); }
   }
@@ -212,14 +212,14 @@ FDG_DEV void dsm_k(ge_p2 &acc2, uint32_t (&kd)[KD_WORDS], const uint32_t *wsl, u
    128-B line, random across the 67-MB table) is loaded one digit ahead of
    its use so the load latency hides behind the previous addition. */
 FDG_DEV void comb_sb(ge_p3 &acc, const uint32_t (&S)[8], const uint32_t *__restrict__ btab) {
-  constexpr int NW = (BC_NDIG + 1) / 2;
+  constexpr int NW = COMB_WORDS(BC_W, BC_NDIG), SLOT = COMB_SLOT(BC_W);
   uint32_t dg[NW];
   sc_recode_comb<(int)BC_W, (int)BC_NDIG>(dg, S);
   auto next_digit = [&dg]() {
-    const int d = (int)(int16_t)(dg[0] & 0xffffu);
+    const int d = SLOT == 16 ? (int)(int16_t)(dg[0] & 0xffffu) : (int)dg[0];
 #pragma unroll
-    for (int i = 0; i < NW - 1; i++) dg[i] = (dg[i] >> 16) | (dg[i + 1] << 16);
-    dg[NW - 1] >>= 16;
+    for (int i = 0; i < NW - 1; i++) dg[i] = SLOT == 16 ? (dg[i] >> 16) | (dg[i + 1] << 16) : dg[i + 1];
+    dg[NW - 1] = SLOT == 16 ? dg[NW - 1] >> 16 : 0u;
     return d;
   };
   auto load_entry = [btab](uint32_t (&q)[32], uint32_t ti, int d) {

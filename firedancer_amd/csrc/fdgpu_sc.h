@@ -112,14 +112,19 @@ FDG_DEV void sc_recode16(uint32_t (&out)[8], const uint32_t (&k)[8]) {
 }
 
 /* Signed radix-2^W digits of S for the fixed-base comb (W = FDGPU_BCOMB_BITS):
-   NDIG digits d_i in [-2^(W-1), 2^(W-1)], S = sum d_i 2^(W i), packed as
-   int16 slots (two per word, digit 0 in the low half of word 0).  Needs
+   NDIG digits d_i in [-2^(W-1), 2^(W-1)), S = sum d_i 2^(W i), packed in
+   COMB_SLOT(W)-bit two's complement slots (two int16 per word for W <= 16,
+   one per word above; digit 0 in the low slot of word 0).  Needs
    S < 2^(W NDIG - 1) (callers pass S < L or 0). */
+#define COMB_SLOT(W) ((W) <= 16 ? 16 : 32)
+#define COMB_WORDS(W, NDIG) (((NDIG) * COMB_SLOT(W) + 31) / 32)
 template <int W, int NDIG>
-FDG_DEV void sc_recode_comb(uint32_t (&out)[(NDIG + 1) / 2], const uint32_t (&s)[8]) {
+FDG_DEV void sc_recode_comb(uint32_t (&out)[COMB_WORDS(W, NDIG)], const uint32_t (&s)[8]) {
+  constexpr int SLOT = COMB_SLOT(W), PER = 32 / SLOT;
+  constexpr uint64_t SMASK = SLOT == 32 ? 0xffffffffull : 0xffffull;
   uint32_t carry = 0;
 #pragma unroll
-  for (int i = 0; i < (NDIG + 1) / 2; i++) out[i] = 0;
+  for (int i = 0; i < COMB_WORDS(W, NDIG); i++) out[i] = 0;
 #pragma unroll
   for (int i = 0; i < NDIG; i++) {
     const int bit = W * i, wd = bit >> 5, sh = bit & 31;
@@ -127,8 +132,8 @@ FDG_DEV void sc_recode_comb(uint32_t (&out)[(NDIG + 1) / 2], const uint32_t (&s)
     if (wd + 1 < 8) x |= (uint64_t)s[wd + 1] << 32;
     const uint32_t e = (uint32_t)((x >> sh) & ((1ull << W) - 1)) + carry;
     carry = e >= (1u << (W - 1)) ? 1u : 0u;
-    const uint32_t d = (e - (carry << W)) & 0xffffu;   /* int16 two's complement */
-    out[i >> 1] |= d << (16 * (i & 1));
+    const uint32_t d = (uint32_t)(((uint64_t)e - ((uint64_t)carry << W)) & SMASK);   /* two's complement slot */
+    out[i / PER] |= d << (SLOT * (i % PER));
   }
 }
 
