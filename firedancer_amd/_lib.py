@@ -91,6 +91,12 @@ def lib():
     L.fdgpu_dev_batch_own_queue.restype = c.c_int
     L.fdgpu_dev_batch_codes.argtypes = [vp, vp, vp, vp]
     L.fdgpu_dev_batch_codes.restype = c.c_int
+    L.fdgpu_dev_batch_upload_frags.argtypes = [vp, vp, c.c_uint64, vp, c.c_uint64]
+    L.fdgpu_dev_batch_upload_frags.restype = vp
+    L.fdgpu_dev_batch_txns.argtypes = [vp, vp, vp, vp]
+    L.fdgpu_dev_batch_txns.restype = c.c_int
+    L.fdgpu_dev_batch_time2.argtypes = [vp, vp, c.c_int] + [c.POINTER(c.c_double)] * 4
+    L.fdgpu_dev_batch_time2.restype = c.c_int
     L.fdgpu_dev_batch_free.argtypes = [vp, vp]
     L.fdgpu_dev_batch_free.restype = None
     L.fdgpu_dev_batch_sig_cnt.argtypes = [vp]

@@ -591,6 +591,17 @@ struct fdgpu_dev_batch {
      the previous one's last, partial round leaves idle) */
   hipStream_t stream = nullptr;
   uint32_t *d_ws = nullptr;
+  /* frag batches (GPU-side ingest): raw payloads in d_arena; the descriptors
+     above are produced on the device by each verify, n_sig is the bound the
+     buffers and the grid are sized for until a codes() call reads the count */
+  bool frags = false;
+  int device = 0;
+  fdgpu_frag_t *d_frags = nullptr;
+  uint8_t *d_txn_out = nullptr;
+  uint16_t *d_txn_sz = nullptr;
+  fdgpu_txn_t *d_txd = nullptr;
+  uint32_t *d_cnt = nullptr, *d_sig0 = nullptr, *d_blocktot = nullptr, *d_n_sig = nullptr;
+  uint64_t n_sig_bound = 0;
 };
 
 namespace {
@@ -600,7 +611,15 @@ uint32_t *batch_ws(fdgpu_engine_t *e, fdgpu_dev_batch_t *b) { return b->d_ws ? b
 
 extern "C" {
 
-uint64_t fdgpu_dev_batch_sig_cnt(fdgpu_dev_batch_t const *b) { return b ? b->n_sig : 0; }
+uint64_t fdgpu_dev_batch_sig_cnt(fdgpu_dev_batch_t const *b) {
+  if (!b) return 0;
+  if (!b->frags) return b->n_sig;
+  uint32_t n = 0;                             /* the count the last verify produced on the device */
+  if (hipSetDevice(b->device) != hipSuccess) return 0;
+  if (b->stream && hipStreamSynchronize(b->stream) != hipSuccess) return 0;
+  if (hipMemcpy(&n, b->d_n_sig, sizeof(n), hipMemcpyDeviceToHost) != hipSuccess) return 0;
+  return n;
+}
 
 int fdgpu_dev_batch_device_ptrs(fdgpu_dev_batch_t const *b, void **d_arena, void **d_sig_desc, void **d_perm,
                                 void **d_txn_desc, int8_t **d_sig_codes, int8_t **d_txn_codes) {
@@ -618,7 +637,8 @@ int fdgpu_dev_batch_own_queue(fdgpu_engine_t *e, fdgpu_dev_batch_t *b) {
   if (!e || !b) return FDGPU_ERR_INVAL;
   if (b->stream) return FDGPU_OK;
   HIPCHK(hipSetDevice(e->device), FDGPU_ERR_DEVICE);
-  if (hipMalloc((void **)&b->d_ws, fdgpu_ws_bytes(b->n_sig ? b->n_sig : 1)) != hipSuccess) {
+  const uint64_t nsig = b->frags ? b->n_sig_bound : b->n_sig;
+  if (hipMalloc((void **)&b->d_ws, fdgpu_ws_bytes(nsig ? nsig : 1)) != hipSuccess) {
     b->d_ws = nullptr; set_err("batch workspace alloc"); return FDGPU_ERR_DEVICE;
   }
   if (hipStreamCreateWithFlags(&b->stream, hipStreamNonBlocking) != hipSuccess) {
@@ -646,6 +666,9 @@ void fdgpu_dev_batch_free(fdgpu_engine_t *e, fdgpu_dev_batch_t *b) {
   if (b->d_txns) (void)hipFree(b->d_txns);
   if (b->d_sig_codes) (void)hipFree(b->d_sig_codes);
   if (b->d_txn_codes) (void)hipFree(b->d_txn_codes);
+  for (void *p : {(void *)b->d_frags, (void *)b->d_txn_out, (void *)b->d_txn_sz, (void *)b->d_txd, (void *)b->d_cnt,
+                  (void *)b->d_sig0, (void *)b->d_blocktot, (void *)b->d_n_sig})
+    if (p) (void)hipFree(p);
   delete b;
 }
 
@@ -684,61 +707,159 @@ fdgpu_dev_batch_t *fdgpu_dev_batch_upload(fdgpu_engine_t *e, uint8_t const *aren
   return b;
 }
 
+fdgpu_dev_batch_t *fdgpu_dev_batch_upload_frags(fdgpu_engine_t *e, uint8_t const *arena, uint64_t arena_sz,
+                                                fdgpu_frag_t const *frags, uint64_t frag_cnt) {
+  if (!e || (!arena && arena_sz) || (!frags && frag_cnt)) { set_err("null argument"); return nullptr; }
+  if (!FDGPU_HALFSIZE) { set_err("frag batches need the half-size build"); return nullptr; }
+  if (arena_sz > 0xFFFFFFF0ull || frag_cnt > 0x0FFFFFFFull) { set_err("batch exceeds 32-bit offsets"); return nullptr; }
+  uint64_t bound = 0;
+  for (uint64_t t = 0; t < frag_cnt; t++) {
+    if ((uint64_t)frags[t].off + frags[t].sz > arena_sz) {
+      set_err("frag %llu out of arena bounds", (unsigned long long)t);
+      return nullptr;
+    }
+    bound += fdgpu_frag_sig_bound(frags[t].sz);
+  }
+  HIPCHK(hipSetDevice(e->device), nullptr);
+  fdgpu_dev_batch *b = new fdgpu_dev_batch();
+  b->frags = true;
+  b->device = e->device;
+  b->n_txn = frag_cnt;
+  b->n_sig = bound;
+  b->n_sig_bound = bound;
+  auto fail = [&](const char *what) -> fdgpu_dev_batch_t * { set_err("%s", what); fdgpu_dev_batch_free(e, b); return nullptr; };
+  const uint64_t nt = frag_cnt + 1, nb = (frag_cnt + 1023) / 1024 + 1;
+  if (hipMalloc((void **)&b->d_arena, arena_sz + FDGPU_ARENA_SLACK) != hipSuccess) return fail("arena alloc");
+  if (hipMalloc((void **)&b->d_frags, nt * sizeof(fdgpu_frag_t)) != hipSuccess) return fail("frag alloc");
+  if (hipMalloc((void **)&b->d_txn_out, nt * 852u) != hipSuccess) return fail("txn alloc");
+  if (hipMalloc((void **)&b->d_txn_sz, nt * sizeof(uint16_t)) != hipSuccess) return fail("txn alloc");
+  if (hipMalloc((void **)&b->d_txd, nt * sizeof(fdgpu_txn_t)) != hipSuccess) return fail("txn alloc");
+  if (hipMalloc((void **)&b->d_cnt, nt * sizeof(uint32_t)) != hipSuccess) return fail("scan alloc");
+  if (hipMalloc((void **)&b->d_sig0, nt * sizeof(uint32_t)) != hipSuccess) return fail("scan alloc");
+  if (hipMalloc((void **)&b->d_blocktot, nb * sizeof(uint32_t)) != hipSuccess) return fail("scan alloc");
+  if (hipMalloc((void **)&b->d_n_sig, sizeof(uint32_t)) != hipSuccess) return fail("scan alloc");
+  if (hipMalloc((void **)&b->d_sigs, (bound + 1) * sizeof(fdgpu_sig_desc_t)) != hipSuccess) return fail("sig alloc");
+  if (hipMalloc((void **)&b->d_txns, nt * sizeof(fdgpu_txn_desc_t)) != hipSuccess) return fail("txn alloc");
+  if (hipMalloc((void **)&b->d_sig_codes, bound + 16) != hipSuccess) return fail("code alloc");
+  if (hipMalloc((void **)&b->d_txn_codes, frag_cnt + 16) != hipSuccess) return fail("code alloc");
+  if (hipMemset(b->d_arena, 0, arena_sz + FDGPU_ARENA_SLACK) != hipSuccess) return fail("memset");
+  if (hipMemset(b->d_n_sig, 0, sizeof(uint32_t)) != hipSuccess) return fail("memset");
+  if (arena_sz && hipMemcpy(b->d_arena, arena, arena_sz, hipMemcpyHostToDevice) != hipSuccess) return fail("h2d");
+  if (frag_cnt && hipMemcpy(b->d_frags, frags, frag_cnt * sizeof(fdgpu_frag_t), hipMemcpyHostToDevice) != hipSuccess)
+    return fail("h2d");
+  if (bound > e->ws_sig) {
+    if (hipStreamSynchronize(e->compute) != hipSuccess) return fail("sync");
+    if (ensure_ws(e, bound) != FDGPU_OK) { fdgpu_dev_batch_free(e, b); return nullptr; }
+  }
+  return b;
+}
+
+/* the ingest kernels of a frag batch (parse -> scan -> expand) on st */
+static int enqueue_ingest(fdgpu_dev_batch_t *b, hipStream_t st) {
+  HIPCHK(fdgpu_launch_frag_ingest(b->d_arena, b->d_frags, (uint32_t)b->n_txn, b->d_txn_out, b->d_txn_sz, b->d_txd,
+                                  b->d_cnt, b->d_sig0, b->d_blocktot, b->d_n_sig, b->d_sigs, b->d_txns, st),
+         FDGPU_ERR_DEVICE);
+  return FDGPU_OK;
+}
+
 int fdgpu_dev_batch_verify(fdgpu_engine_t *e, fdgpu_dev_batch_t *b) {
   if (!e || !b) return FDGPU_ERR_INVAL;
   HIPCHK(hipSetDevice(e->device), FDGPU_ERR_DEVICE);
-  return enqueue_verify(e, b->d_arena, b->d_sigs, b->d_perm, b->n_sig, b->d_txns, b->n_txn, b->d_sig_codes,
-                        b->d_txn_codes, batch_stream(e, b), b->d_ws);
+  if (!b->frags)
+    return enqueue_verify(e, b->d_arena, b->d_sigs, b->d_perm, b->n_sig, b->d_txns, b->n_txn, b->d_sig_codes,
+                          b->d_txn_codes, batch_stream(e, b), b->d_ws);
+  const hipStream_t st = batch_stream(e, b);
+  int rc = enqueue_ingest(b, st);
+  if (rc) return rc;
+  HIPCHK(fdgpu_launch_verify_sigs(b->d_arena, b->d_sigs, (uint32_t)b->n_sig_bound, nullptr, e->d_btab, batch_ws(e, b),
+                                  b->d_sig_codes, kflags(e), st, b->d_n_sig),
+         FDGPU_ERR_DEVICE);
+  HIPCHK(fdgpu_launch_combine(b->d_txns, (uint32_t)b->n_txn, b->d_sig_codes, b->d_txn_codes, nullptr, st),
+         FDGPU_ERR_DEVICE);
+  HIPCHK(fdgpu_launch_frag_codes(b->d_txn_sz, (uint32_t)b->n_txn, b->d_txn_codes, st), FDGPU_ERR_DEVICE);
+  return FDGPU_OK;
+}
+
+int fdgpu_dev_batch_txns(fdgpu_engine_t *e, fdgpu_dev_batch_t *b, void *txn_out, uint16_t *txn_sz) {
+  if (!e || !b || !b->frags) return FDGPU_ERR_INVAL;
+  HIPCHK(hipSetDevice(e->device), FDGPU_ERR_DEVICE);
+  HIPCHK(hipStreamSynchronize(batch_stream(e, b)), FDGPU_ERR_DEVICE);
+  if (txn_out && b->n_txn) HIPCHK(hipMemcpy(txn_out, b->d_txn_out, b->n_txn * 852u, hipMemcpyDeviceToHost), FDGPU_ERR_DEVICE);
+  if (txn_sz && b->n_txn)
+    HIPCHK(hipMemcpy(txn_sz, b->d_txn_sz, b->n_txn * sizeof(uint16_t), hipMemcpyDeviceToHost), FDGPU_ERR_DEVICE);
+  return FDGPU_OK;
 }
 
 int fdgpu_dev_batch_codes(fdgpu_engine_t *e, fdgpu_dev_batch_t *b, int8_t *txn_codes, int8_t *sig_codes) {
   if (!e || !b) return FDGPU_ERR_INVAL;
   HIPCHK(hipSetDevice(e->device), FDGPU_ERR_DEVICE);
   HIPCHK(hipStreamSynchronize(batch_stream(e, b)), FDGPU_ERR_DEVICE);
+  if (b->frags) {                             /* the signature count the verify produced on the device */
+    uint32_t n = 0;
+    HIPCHK(hipMemcpy(&n, b->d_n_sig, sizeof(n), hipMemcpyDeviceToHost), FDGPU_ERR_DEVICE);
+    b->n_sig = n;
+  }
   if (txn_codes && b->n_txn) HIPCHK(hipMemcpy(txn_codes, b->d_txn_codes, b->n_txn, hipMemcpyDeviceToHost), FDGPU_ERR_DEVICE);
   if (sig_codes && b->n_sig) HIPCHK(hipMemcpy(sig_codes, b->d_sig_codes, b->n_sig, hipMemcpyDeviceToHost), FDGPU_ERR_DEVICE);
   return FDGPU_OK;
 }
 
-int fdgpu_dev_batch_time(fdgpu_engine_t *e, fdgpu_dev_batch_t *b, int iters, double *wall_ms, double *verify_kernel_ms,
-                         double *combine_kernel_ms) {
+int fdgpu_dev_batch_time2(fdgpu_engine_t *e, fdgpu_dev_batch_t *b, int iters, double *wall_ms, double *ingest_ms,
+                          double *verify_kernel_ms, double *combine_kernel_ms) {
   if (!e || !b || iters < 1) return FDGPU_ERR_INVAL;
   HIPCHK(hipSetDevice(e->device), FDGPU_ERR_DEVICE);
   const uint32_t flags = kflags(e);
   const hipStream_t st = batch_stream(e, b);
-  if (!b->d_ws && b->n_sig > e->ws_sig) {
+  const uint64_t nsig = b->frags ? b->n_sig_bound : b->n_sig;
+  if (!b->d_ws && nsig > e->ws_sig) {
     HIPCHK(hipStreamSynchronize(e->compute), FDGPU_ERR_DEVICE);
-    const int wrc = ensure_ws(e, b->n_sig);
+    const int wrc = ensure_ws(e, nsig);
     if (wrc) return wrc;
   }
-  std::vector<hipEvent_t> ev(3 * (size_t)iters + 1);
+  std::vector<hipEvent_t> ev(4 * (size_t)iters + 1);
   for (auto &x : ev) HIPCHK(hipEventCreate(&x), FDGPU_ERR_DEVICE);
   int rc = FDGPU_OK;
   for (int i = 0; i < iters && rc == FDGPU_OK; i++) {
-    if (hipEventRecord(ev[3 * i], st) != hipSuccess) rc = FDGPU_ERR_DEVICE;
-    if (fdgpu_launch_verify_sigs(b->d_arena, b->d_sigs, (uint32_t)b->n_sig, b->d_perm, e->d_btab, batch_ws(e, b),
-                                 b->d_sig_codes, flags, st) != hipSuccess) rc = FDGPU_ERR_DEVICE;
-    if (hipEventRecord(ev[3 * i + 1], st) != hipSuccess) rc = FDGPU_ERR_DEVICE;
+    if (hipEventRecord(ev[4 * i], st) != hipSuccess) rc = FDGPU_ERR_DEVICE;
+    if (b->frags && rc == FDGPU_OK) rc = enqueue_ingest(b, st);
+    if (hipEventRecord(ev[4 * i + 1], st) != hipSuccess) rc = FDGPU_ERR_DEVICE;
+    if (fdgpu_launch_verify_sigs(b->d_arena, b->d_sigs, (uint32_t)nsig, b->d_perm, e->d_btab, batch_ws(e, b),
+                                 b->d_sig_codes, flags, st, b->frags ? b->d_n_sig : nullptr) != hipSuccess)
+      rc = FDGPU_ERR_DEVICE;
+    if (hipEventRecord(ev[4 * i + 2], st) != hipSuccess) rc = FDGPU_ERR_DEVICE;
     if (fdgpu_launch_combine(b->d_txns, (uint32_t)b->n_txn, b->d_sig_codes, b->d_txn_codes, nullptr, st) != hipSuccess)
       rc = FDGPU_ERR_DEVICE;
-    if (hipEventRecord(ev[3 * i + 2], st) != hipSuccess) rc = FDGPU_ERR_DEVICE;
+    if (b->frags && fdgpu_launch_frag_codes(b->d_txn_sz, (uint32_t)b->n_txn, b->d_txn_codes, st) != hipSuccess)
+      rc = FDGPU_ERR_DEVICE;
+    if (hipEventRecord(ev[4 * i + 3], st) != hipSuccess) rc = FDGPU_ERR_DEVICE;
   }
-  if (rc == FDGPU_OK && hipEventSynchronize(ev[3 * (iters - 1) + 2]) != hipSuccess) rc = FDGPU_ERR_DEVICE;
-  double sv = 0, sc = 0;
+  if (rc == FDGPU_OK && hipEventSynchronize(ev[4 * (iters - 1) + 3]) != hipSuccess) rc = FDGPU_ERR_DEVICE;
+  double si = 0, sv = 0, sc = 0;
   float ms = 0;
   for (int i = 0; rc == FDGPU_OK && i < iters; i++) {
-    (void)hipEventElapsedTime(&ms, ev[3 * i], ev[3 * i + 1]); sv += ms;
-    (void)hipEventElapsedTime(&ms, ev[3 * i + 1], ev[3 * i + 2]); sc += ms;
+    (void)hipEventElapsedTime(&ms, ev[4 * i], ev[4 * i + 1]); si += ms;
+    (void)hipEventElapsedTime(&ms, ev[4 * i + 1], ev[4 * i + 2]); sv += ms;
+    (void)hipEventElapsedTime(&ms, ev[4 * i + 2], ev[4 * i + 3]); sc += ms;
   }
   if (rc == FDGPU_OK) {
-    (void)hipEventElapsedTime(&ms, ev[0], ev[3 * (iters - 1) + 2]);
+    (void)hipEventElapsedTime(&ms, ev[0], ev[4 * (iters - 1) + 3]);
     if (wall_ms) *wall_ms = ms;
+    if (ingest_ms) *ingest_ms = b->frags ? si / iters : 0.0;
     if (verify_kernel_ms) *verify_kernel_ms = sv / iters;
     if (combine_kernel_ms) *combine_kernel_ms = sc / iters;
   } else {
     set_err("timing launch failed");
   }
   for (auto &x : ev) (void)hipEventDestroy(x);
+  return rc;
+}
+
+/* for a frag batch the ingest kernels count in *verify_kernel_ms */
+int fdgpu_dev_batch_time(fdgpu_engine_t *e, fdgpu_dev_batch_t *b, int iters, double *wall_ms, double *verify_kernel_ms,
+                         double *combine_kernel_ms) {
+  double ig = 0, v = 0;
+  const int rc = fdgpu_dev_batch_time2(e, b, iters, wall_ms, &ig, &v, combine_kernel_ms);
+  if (rc == FDGPU_OK && verify_kernel_ms) *verify_kernel_ms = v + ig;
   return rc;
 }
 

@@ -6,6 +6,8 @@
 #include <stddef.h>
 #include <stdint.h>
 
+#include "../../include/fd_ed25519_gpu.h"
+
 /* Per-signature work item (16 B, one dwordx4 per lane).  Offsets index the
    batch arena; the arena carries FDGPU_ARENA_SLACK readable bytes after
    the last payload byte. */
@@ -77,9 +79,13 @@ hipError_t fdgpu_btab_build(uint32_t *d_btab, hipStream_t stream);
 /* d_perm (NULL = identity): d_sig_codes[d_perm[i]] receives the code of
    descriptor i (descriptors grouped by SHA-512 block count, codes in the
    caller's order) */
+/* d_n_sig != NULL: the signature count is read on the device (it is produced
+   there by the GPU-side ingest); n_sig is then an upper bound that sizes the
+   grid (and the workspace).  Half-size path only. */
 hipError_t fdgpu_launch_verify_sigs(const uint8_t *d_arena, const fdgpu_sig_desc_t *d_sigs, uint32_t n_sig,
                                     const uint32_t *d_perm, const uint32_t *d_btab, uint32_t *d_ws,
-                                    int8_t *d_sig_codes, uint32_t flags, hipStream_t stream);
+                                    int8_t *d_sig_codes, uint32_t flags, hipStream_t stream,
+                                    const uint32_t *d_n_sig = nullptr);
 /* d_accept (NULL: not written): ceil(n_txn / 64) words, bit t = txn t verified */
 hipError_t fdgpu_launch_combine(const fdgpu_txn_desc_t *d_txns, uint32_t n_txn, const int8_t *d_sig_codes,
                                 int8_t *d_txn_codes, uint64_t *d_accept, hipStream_t stream);
@@ -94,6 +100,17 @@ hipError_t fdgpu_launch_test_sha512(const uint8_t *d_arena, const fdgpu_sig_desc
 hipError_t fdgpu_launch_test_hram(const uint8_t *d_arena, const fdgpu_sig_desc_t *d_sigs, uint32_t n,
                                   uint32_t *d_out, hipStream_t stream);
 hipError_t fdgpu_launch_test_sc_reduce(const uint32_t *d_in, uint32_t *d_out, uint32_t n, hipStream_t stream);
+/* GPU-side ingest: parse n raw payloads (frags index d_arena), scan the
+   signature counts, expand the descriptors; the batch's signature count is
+   left in *d_n_sig.  Buffers: d_txn_out n x FDT_TXN_MAX_SZ, d_txn_sz /
+   d_txd / d_cnt / d_sig0 / d_tds n entries, d_blocktot ceil(n / 1024),
+   d_sigs the sum of fdgpu_frag_sig_bound over the frags. */
+uint64_t   fdgpu_frag_sig_bound(uint32_t sz);
+hipError_t fdgpu_launch_frag_ingest(const uint8_t *d_arena, const fdgpu_frag_t *d_frags, uint32_t n,
+                                    uint8_t *d_txn_out, uint16_t *d_txn_sz, fdgpu_txn_t *d_txd, uint32_t *d_cnt,
+                                    uint32_t *d_sig0, uint32_t *d_blocktot, uint32_t *d_n_sig,
+                                    fdgpu_sig_desc_t *d_sigs, fdgpu_txn_desc_t *d_tds, hipStream_t stream);
+hipError_t fdgpu_launch_frag_codes(const uint16_t *d_txn_sz, uint32_t n, int8_t *d_codes, hipStream_t stream);
 hipError_t fdgpu_launch_test_hs_split(const uint32_t *d_in, uint32_t *d_out, uint32_t n, hipStream_t stream);
 
 #ifdef __cplusplus

@@ -26,6 +26,7 @@
 #include "fdgpu_sha512.h"
 #include "fdgpu_lattice.h"
 #include "fdgpu_stamps.h"
+#include "fdt_parse.h"
 
 using namespace fdgpu;
 
@@ -780,10 +781,14 @@ FDG_DEV void hs_chain(ge_p1p1 &t, uint32_t (&ud)[5], uint32_t (&vd)[5], bool u_n
 /* The verify kernel of the half-size path; codes of lanes it settles are
    written here, lanes whose split failed are queued for fdgpu_full_kernel. */
 __global__ void __launch_bounds__(FDGPU_BLOCK, FDGPU_VERIFY_WAVES)
-fdgpu_verify_hs_kernel(const uint8_t *__restrict__ arena, const fdgpu_sig_desc_t *__restrict__ sigs, uint32_t n_sig,
-                       const uint32_t *__restrict__ btab, uint32_t *__restrict__ ws, const uint32_t *__restrict__ perm,
-                       int8_t *__restrict__ codes, uint32_t *__restrict__ queue, uint32_t *__restrict__ queue_cnt,
-                       uint32_t flags) {
+fdgpu_verify_hs_kernel(const uint8_t *__restrict__ arena, const fdgpu_sig_desc_t *__restrict__ sigs, uint32_t n_sig_arg,
+                       const uint32_t *__restrict__ n_sig_dev, const uint32_t *__restrict__ btab,
+                       uint32_t *__restrict__ ws, const uint32_t *__restrict__ perm, int8_t *__restrict__ codes,
+                       uint32_t *__restrict__ queue, uint32_t *__restrict__ queue_cnt, uint32_t flags) {
+  /* n_sig_dev: the count is produced on the device (GPU-side ingest) and the
+     grid covers an upper bound; blocks past it leave at once */
+  const uint32_t n_sig = n_sig_dev ? *n_sig_dev : n_sig_arg;
+  if (blockIdx.x * blockDim.x >= n_sig) return;
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   const bool active = i < n_sig;
   const bool ref_map = (flags & FDGPU_FLAG_REF_MAP) != 0;
@@ -1065,6 +1070,141 @@ __global__ void __launch_bounds__(64) fdgpu_test_sc_reduce_kernel(const uint32_t
   for (int j = 0; j < 8; j++) out[8 * i + j] = r[j];
 }
 
+/* ---------------- GPU-side ingest ----------------
+   Raw transaction payloads -> the verify's descriptors, on the device:
+     parse   one payload per lane through fdt_parse_core (fdt_parse.h, the
+             host parser's own source): the fd_txn_t (which the verify tile
+             writes into its output trailer), its footprint (0: not a
+             transaction), and the signature layout -- signatures at
+             signature_off, the signer keys are the first sig_cnt account
+             addresses, the message runs from message_off to the end;
+     scan    exclusive prefix sum of the per-txn signature counts (a count
+             outside [1,16] contributes none: batch_single_msg rejects the
+             txn unverified, fd_ed25519_user.c:238-241) -> each txn's first
+             signature and the batch's signature count, left on the device;
+     expand  the per-signature descriptors, in transaction order.
+   A valid txn with s signatures is at least 96 s + 38 bytes (s signatures,
+   s signer keys, blockhash, the counts), which bounds the signature count
+   of a batch from its frag sizes alone (fdgpu_frag_sig_bound). */
+#define FDGPU_SCAN_BLOCK 1024u      /* txns per scan block: 256 threads x 4 */
+
+FDG_DEV uint32_t frag_sig_bound(uint32_t sz) { return sz >= 134u ? min(16u, (sz - 38u) / 96u) : 0u; }
+
+__global__ void __launch_bounds__(64) fdgpu_frag_parse_kernel(
+    const uint8_t *__restrict__ arena, const fdgpu_frag_t *__restrict__ frags, uint32_t n,
+    uint8_t *__restrict__ txn_out, uint16_t *__restrict__ txn_sz, fdgpu_txn_t *__restrict__ txd,
+    uint32_t *__restrict__ cnt) {
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= n) return;
+  const fdgpu_frag_t f = frags[t];
+  fdt_txn_t *x = (fdt_txn_t *)(txn_out + (size_t)t * FDT_TXN_MAX_SZ);
+  uint64_t why = 0;
+  uint64_t fp = fdt_parse_core(arena + f.off, f.sz, x, &why);
+  const uint32_t sc = fp ? x->signature_cnt : 0u;
+  uint32_t c = (sc >= 1u && sc <= 16u) ? sc : 0u;
+  if (c > frag_sig_bound(f.sz)) { c = 0u; fp = 0u; }       /* cannot happen for a parsed txn (see above) */
+  fdgpu_txn_t d;
+  d.msg_off = fp ? f.off + x->message_off : f.off;
+  d.msg_sz = fp ? f.sz - x->message_off : 0u;
+  d.sig_off = fp ? f.off + x->signature_off : f.off;
+  d.pub_off = fp ? f.off + x->acct_addr_off : f.off;
+  d.sig_cnt = fp ? sc : 0u;
+  txd[t] = d;
+  cnt[t] = c;
+  txn_sz[t] = (uint16_t)fp;
+}
+
+/* Inclusive scan of v over the 64 lanes of a wave */
+FDG_DEV uint32_t wave_incl_scan(uint32_t v) {
+  const int lane = (int)(threadIdx.x & 63u);
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const uint32_t u = (uint32_t)__shfl_up((int)v, off, 64);
+    v += lane >= off ? u : 0u;
+  }
+  return v;
+}
+
+/* Block-local exclusive scan of cnt over FDGPU_SCAN_BLOCK txns -> sig0
+   (local), the block's total -> blocktot */
+__global__ void __launch_bounds__(256) fdgpu_scan_local_kernel(const uint32_t *__restrict__ cnt, uint32_t n,
+                                                               uint32_t *__restrict__ sig0,
+                                                               uint32_t *__restrict__ blocktot) {
+  __shared__ uint32_t s_wave[4];
+  const uint32_t base = blockIdx.x * FDGPU_SCAN_BLOCK + threadIdx.x * 4u;
+  uint32_t v[4], sum = 0;
+#pragma unroll
+  for (int k = 0; k < 4; k++) { v[k] = base + k < n ? cnt[base + k] : 0u; sum += v[k]; }
+  const uint32_t incl = wave_incl_scan(sum);
+  const uint32_t wv = threadIdx.x >> 6;
+  if ((threadIdx.x & 63u) == 63u) s_wave[wv] = incl;
+  __syncthreads();
+  uint32_t off = incl - sum;
+  for (uint32_t w = 0; w < wv; w++) off += s_wave[w];
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    if (base + k < n) sig0[base + k] = off;
+    off += v[k];
+  }
+  if (threadIdx.x == 255u) blocktot[blockIdx.x] = off;
+}
+
+/* One block: exclusive scan of the nb block totals (in place) and the
+   grand total -> *n_sig */
+__global__ void __launch_bounds__(1024) fdgpu_scan_blocks_kernel(uint32_t *__restrict__ blocktot, uint32_t nb,
+                                                                 uint32_t *__restrict__ n_sig) {
+  __shared__ uint32_t s_wave[16];
+  __shared__ uint32_t s_carry;
+  if (threadIdx.x == 0) s_carry = 0;
+  __syncthreads();
+  for (uint32_t b0 = 0; b0 < nb; b0 += 1024u) {
+    const uint32_t i = b0 + threadIdx.x;
+    const uint32_t v = i < nb ? blocktot[i] : 0u;
+    const uint32_t incl = wave_incl_scan(v);
+    const uint32_t wv = threadIdx.x >> 6;
+    if ((threadIdx.x & 63u) == 63u) s_wave[wv] = incl;
+    __syncthreads();
+    uint32_t off = s_carry + incl - v;
+    for (uint32_t w = 0; w < wv; w++) off += s_wave[w];
+    __syncthreads();
+    if (i < nb) blocktot[i] = off;
+    if (threadIdx.x == 1023u) s_carry = off + v;
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) *n_sig = s_carry;
+}
+
+/* One thread per txn: its combine item and its signatures' descriptors */
+__global__ void __launch_bounds__(256) fdgpu_frag_expand_kernel(
+    const fdgpu_txn_t *__restrict__ txd, const uint32_t *__restrict__ cnt, const uint32_t *__restrict__ sig0,
+    const uint32_t *__restrict__ blockoff, uint32_t n, fdgpu_sig_desc_t *__restrict__ sigs,
+    fdgpu_txn_desc_t *__restrict__ tds) {
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= n) return;
+  const uint32_t c = cnt[t], s0 = sig0[t] + blockoff[t / FDGPU_SCAN_BLOCK];
+  fdgpu_txn_desc_t td;
+  td.sig0 = s0;
+  td.sig_cnt = c;
+  tds[t] = td;
+  if (!c) return;
+  const fdgpu_txn_t d = txd[t];
+  for (uint32_t j = 0; j < c; j++) {
+    fdgpu_sig_desc_t sd;
+    sd.msg_off = d.msg_off;
+    sd.msg_sz = d.msg_sz;
+    sd.sig_off = d.sig_off + 64u * j;
+    sd.pub_off = d.pub_off + 32u * j;
+    sigs[s0 + j] = sd;
+  }
+}
+
+/* After the combine: a payload that did not parse gets FDGPU_CODE_PARSE_FAIL */
+__global__ void __launch_bounds__(256) fdgpu_frag_codes_kernel(const uint16_t *__restrict__ txn_sz, uint32_t n,
+                                                               int8_t *__restrict__ codes) {
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t < n && !txn_sz[t]) codes[t] = (int8_t)FDGPU_CODE_PARSE_FAIL;
+}
+
 /* hs_split on the device (v_rcp_f64 quotients) for the parity tests: n
    scalars k < L (8 words each) -> 16 words each: |u| (5), |v| (5), ok,
    u_neg, v_neg, bits, 0, 0 */
@@ -1130,7 +1270,7 @@ size_t fdgpu_ws_bytes(uint64_t n_sig) {
 
 hipError_t fdgpu_launch_verify_sigs(const uint8_t *d_arena, const fdgpu_sig_desc_t *d_sigs, uint32_t n_sig,
                                     const uint32_t *d_perm, const uint32_t *d_btab, uint32_t *d_ws,
-                                    int8_t *d_sig_codes, uint32_t flags, hipStream_t stream) {
+                                    int8_t *d_sig_codes, uint32_t flags, hipStream_t stream, const uint32_t *d_n_sig) {
   if (!n_sig) return hipSuccess;
   const uint32_t grid = (n_sig + FDGPU_BLOCK - 1) / FDGPU_BLOCK;
   const size_t lanes = (size_t)grid * FDGPU_BLOCK;
@@ -1153,12 +1293,13 @@ hipError_t fdgpu_launch_verify_sigs(const uint8_t *d_arena, const fdgpu_sig_desc
   const uint32_t slow_blocks = grid < (uint32_t)resident ? grid : (uint32_t)resident;
 #if FDGPU_HALFSIZE
   (void)wg_tot; (void)wg_inv;
-  hipLaunchKernelGGL(fdgpu_verify_hs_kernel, dim3(grid), dim3(FDGPU_BLOCK), 0, stream, d_arena, d_sigs, n_sig, d_btab,
-                     d_ws, d_perm, d_sig_codes, queue, cnt, flags);
+  hipLaunchKernelGGL(fdgpu_verify_hs_kernel, dim3(grid), dim3(FDGPU_BLOCK), 0, stream, d_arena, d_sigs, n_sig, d_n_sig,
+                     d_btab, d_ws, d_perm, d_sig_codes, queue, cnt, flags);
   hipLaunchKernelGGL(fdgpu_full_kernel, dim3(slow_blocks), dim3(FDGPU_BLOCK), 0, stream, d_ws, d_perm, d_sig_codes,
                      queue, cnt, slow_blocks * FDGPU_BLOCK);
   return hipGetLastError();
 #endif
+  if (d_n_sig) return hipErrorInvalidValue;                  /* device-side counts: half-size path only */
   hipLaunchKernelGGL(fdgpu_verify_ra_kernel, dim3(grid), dim3(FDGPU_BLOCK), 0, stream, d_arena, d_sigs, n_sig, d_btab,
                      d_ws, wg_tot, queue, cnt, flags);
   const uint32_t inv_blocks = (grid + FDGPU_BLOCK - 1) / FDGPU_BLOCK;
@@ -1209,6 +1350,29 @@ hipError_t fdgpu_launch_test_sc_reduce(const uint32_t *d_in, uint32_t *d_out, ui
   hipLaunchKernelGGL(fdgpu_test_sc_reduce_kernel, dim3((n + 63) / 64), dim3(64), 0, stream, d_in, d_out, n);
   return hipGetLastError();
 }
+uint64_t fdgpu_frag_sig_bound(uint32_t sz) { return sz >= 134u ? (sz - 38u) / 96u < 16u ? (sz - 38u) / 96u : 16u : 0u; }
+
+hipError_t fdgpu_launch_frag_ingest(const uint8_t *d_arena, const fdgpu_frag_t *d_frags, uint32_t n,
+                                    uint8_t *d_txn_out, uint16_t *d_txn_sz, fdgpu_txn_t *d_txd, uint32_t *d_cnt,
+                                    uint32_t *d_sig0, uint32_t *d_blocktot, uint32_t *d_n_sig,
+                                    fdgpu_sig_desc_t *d_sigs, fdgpu_txn_desc_t *d_tds, hipStream_t stream) {
+  if (!n) return hipMemsetAsync(d_n_sig, 0, sizeof(uint32_t), stream);
+  const uint32_t nb = (n + FDGPU_SCAN_BLOCK - 1) / FDGPU_SCAN_BLOCK;
+  hipLaunchKernelGGL(fdgpu_frag_parse_kernel, dim3((n + 63) / 64), dim3(64), 0, stream, d_arena, d_frags, n, d_txn_out,
+                     d_txn_sz, d_txd, d_cnt);
+  hipLaunchKernelGGL(fdgpu_scan_local_kernel, dim3(nb), dim3(256), 0, stream, d_cnt, n, d_sig0, d_blocktot);
+  hipLaunchKernelGGL(fdgpu_scan_blocks_kernel, dim3(1), dim3(1024), 0, stream, d_blocktot, nb, d_n_sig);
+  hipLaunchKernelGGL(fdgpu_frag_expand_kernel, dim3((n + 255) / 256), dim3(256), 0, stream, d_txd, d_cnt, d_sig0,
+                     d_blocktot, n, d_sigs, d_tds);
+  return hipGetLastError();
+}
+
+hipError_t fdgpu_launch_frag_codes(const uint16_t *d_txn_sz, uint32_t n, int8_t *d_codes, hipStream_t stream) {
+  if (!n) return hipSuccess;
+  hipLaunchKernelGGL(fdgpu_frag_codes_kernel, dim3((n + 255) / 256), dim3(256), 0, stream, d_txn_sz, n, d_codes);
+  return hipGetLastError();
+}
+
 hipError_t fdgpu_launch_test_hs_split(const uint32_t *d_in, uint32_t *d_out, uint32_t n, hipStream_t stream) {
   hipLaunchKernelGGL(fdgpu_test_hs_split_kernel, dim3((n + 63) / 64), dim3(64), 0, stream, d_in, d_out, n);
   return hipGetLastError();

@@ -6,6 +6,7 @@
 #include <cstring>
 
 #include "../../../include/fd_verify_tile.h"
+#include "../fdt_parse.h"
 
 namespace {
 
@@ -253,179 +254,16 @@ static_assert(sizeof(fdt_txn_t) == 20, "fd_txn_t header is 20 B");
 static_assert(sizeof(fdt_txn_instr_t) == 10, "fd_txn_instr_t is 10 B");
 static_assert(sizeof(fdt_txn_acct_addr_lut_t) == 8, "fd_txn_acct_addr_lut_t is 8 B");
 
-namespace {
-
-/* Failure reasons recorded in the counters' ring (the reference records
-   the source line of the failed check; any non-zero token serves). */
-enum ParseFail : uint64_t {
-  PF_MTU = 1, PF_SHORT, PF_SIG_CNT, PF_VERSION, PF_HDR_SIG_CNT, PF_RO_SIGNED, PF_CU16, PF_ACCT_CNT,
-  PF_ACCT_SIGNERS, PF_INSTR_CNT, PF_NO_PROGRAM_ACCT, PF_PROGRAM_ID, PF_LUT_CNT, PF_LUT_WRITABLE, PF_LUT_READONLY,
-  PF_LUT_EMPTY, PF_TRAILING, PF_TOTAL_ACCTS, PF_ACCT_IDX
-};
-
-/* Bounds-checked reader over an untrusted payload (fd_txn_parse.c:12-75:
-   check that n bytes remain before every read; compact-u16 must be
-   minimally encoded and fit 16 bits). */
-struct Reader {
-  const uint8_t *p;
-  uint64_t sz, i = 0;
-  uint64_t fail = 0;
-  bool need(uint64_t n, uint64_t why = PF_SHORT) {
-    if (fail) return false;
-    if (n > sz - i) { fail = why; return false; }
-    return true;
-  }
-  bool u8(uint8_t &v) { if (!need(1)) return false; v = p[i++]; return true; }
-  bool skip(uint64_t n) { if (!need(n)) return false; i += n; return true; }
-  /* fd_compact_u16.h:60-75 */
-  bool cu16(uint16_t &v) {
-    if (fail) return false;
-    const uint64_t avail = sz - i;
-    const uint8_t *b = p + i;
-    if (avail >= 1 && !(b[0] & 0x80)) { v = b[0]; i += 1; return true; }
-    if (avail >= 2 && !(b[1] & 0x80)) {
-      if (!b[1]) { fail = PF_CU16; return false; }
-      v = (uint16_t)((b[0] & 0x7f) | (b[1] << 7)); i += 2; return true;
-    }
-    if (avail >= 3 && !(b[2] & 0xfc)) {
-      if (!b[2]) { fail = PF_CU16; return false; }
-      v = (uint16_t)((b[0] & 0x7f) | ((b[1] & 0x7f) << 7) | (b[2] << 14)); i += 3; return true;
-    }
-    fail = PF_CU16;
-    return false;
-  }
-  bool check(bool ok, uint64_t why) { if (!fail && !ok) fail = why; return !fail; }
-};
-
-}  // namespace
-
+/* fd_txn_parse (fd_txn_parse.c:7-243): the parser lives in
+   ../fdt_parse.h, shared with the GPU ingest kernel; this wrapper keeps the
+   reference's counters (a success count and a ring of failure reasons). */
 extern "C" uint64_t fdt_txn_parse(const uint8_t *payload, uint64_t payload_sz, void *out_buf,
                                   fdt_txn_parse_counters_t *counters) {
-  Reader r{payload, payload_sz};
-  fdt_txn_t *t = (fdt_txn_t *)out_buf;
-  auto bail = [&]() -> uint64_t {
-    if (counters) counters->failure_ring[counters->failure_cnt++ % 32] = r.fail ? r.fail : PF_SHORT;
-    return 0;
-  };
-  if (!r.check(payload_sz <= FDT_TXN_MTU, PF_MTU)) return bail();
-
-  /* signatures: count (u8 == compact-u16 below 128), at least one signer */
-  uint8_t sig_cnt;
-  if (!r.u8(sig_cnt) || !r.check(sig_cnt >= 1 && sig_cnt <= FDT_TXN_SIG_MAX, PF_SIG_CNT)) return bail();
-  const uint64_t sig_off = r.i;
-  if (!r.skip(64ULL * sig_cnt)) return bail();
-
-  /* message header: optional version prefix, then the signer count again */
-  const uint64_t msg_off = r.i;
-  uint8_t b0;
-  if (!r.u8(b0)) return bail();
-  uint8_t version;
-  if (b0 & 0x80) {
-    version = b0 & 0x7f;
-    uint8_t n;
-    if (!r.check(version == FDT_TXN_V0, PF_VERSION) || !r.u8(n) || !r.check(n == sig_cnt, PF_HDR_SIG_CNT))
-      return bail();
-  } else {
-    version = FDT_TXN_VLEGACY;
-    if (!r.check(b0 == sig_cnt, PF_HDR_SIG_CNT)) return bail();
+  uint64_t why = 0;
+  const uint64_t fp = fdt_parse_core(payload, payload_sz, (fdt_txn_t *)out_buf, &why);
+  if (counters) {
+    if (fp) counters->success_cnt++;
+    else counters->failure_ring[counters->failure_cnt++ % 32] = why;
   }
-  uint8_t ro_signed, ro_unsigned;
-  if (!r.u8(ro_signed) || !r.check(ro_signed < sig_cnt, PF_RO_SIGNED) || !r.u8(ro_unsigned)) return bail();
-
-  /* account addresses and the recent blockhash */
-  uint16_t acct_cnt;
-  if (!r.cu16(acct_cnt)) return bail();
-  if (!r.check(sig_cnt <= acct_cnt && acct_cnt <= FDT_TXN_ACCT_ADDR_MAX, PF_ACCT_CNT) ||
-      !r.check((uint64_t)sig_cnt + ro_unsigned <= acct_cnt, PF_ACCT_SIGNERS))
-    return bail();
-  const uint64_t acct_off = r.i;
-  if (!r.skip(32ULL * acct_cnt)) return bail();
-  const uint64_t blockhash_off = r.i;
-  if (!r.skip(32)) return bail();
-
-  /* instructions: each at least 3 bytes (program id, two empty lists) */
-  uint16_t instr_cnt;
-  if (!r.cu16(instr_cnt) || !r.check(instr_cnt <= FDT_TXN_INSTR_MAX, PF_INSTR_CNT) || !r.need(3ULL * instr_cnt) ||
-      !r.check(acct_cnt > (instr_cnt ? 1 : 0), PF_NO_PROGRAM_ACCT))
-    return bail();
-  if (t) {
-    t->transaction_version = version;
-    t->signature_cnt = sig_cnt;
-    t->signature_off = (uint16_t)sig_off;
-    t->message_off = (uint16_t)msg_off;
-    t->readonly_signed_cnt = ro_signed;
-    t->readonly_unsigned_cnt = ro_unsigned;
-    t->acct_addr_cnt = acct_cnt;
-    t->acct_addr_off = (uint16_t)acct_off;
-    t->recent_blockhash_off = (uint16_t)blockhash_off;
-    t->instr_cnt = instr_cnt;
-  }
-  uint8_t max_acct = 0;
-  for (uint16_t j = 0; j < instr_cnt; j++) {
-    uint8_t program_id;
-    uint16_t n_acct, data_sz;
-    if (!r.need(3) || !r.u8(program_id) || !r.cu16(n_acct) || !r.need(n_acct)) return bail();
-    const uint64_t a_off = r.i;
-    for (uint16_t k = 0; k < n_acct; k++) max_acct = payload[a_off + k] > max_acct ? payload[a_off + k] : max_acct;
-    r.i += n_acct;
-    if (!r.cu16(data_sz) || !r.need(data_sz)) return bail();
-    const uint64_t d_off = r.i;
-    r.i += data_sz;
-    /* the program is neither the fee payer nor outside the static keys */
-    if (!r.check(program_id > 0 && program_id < acct_cnt, PF_PROGRAM_ID)) return bail();
-    if (t) {
-      fdt_txn_instr_t &ins = t->instr[j];
-      ins.program_id = program_id;
-      ins._padding_reserved_1 = 0;
-      ins.acct_cnt = n_acct;
-      ins.data_sz = data_sz;
-      ins.acct_off = (uint16_t)a_off;
-      ins.data_off = (uint16_t)d_off;
-    }
-  }
-
-  /* v0 address lookup tables: each >= 34 bytes (key + two lists) */
-  uint16_t lut_cnt = 0;
-  uint64_t adtl_w = 0, adtl = 0;
-  fdt_txn_acct_addr_lut_t *luts = t ? (fdt_txn_acct_addr_lut_t *)(t->instr + instr_cnt) : nullptr;
-  if (version == FDT_TXN_V0) {
-    if (!r.cu16(lut_cnt) || !r.check(lut_cnt <= FDT_TXN_ADDR_TABLE_LOOKUP_MAX, PF_LUT_CNT) ||
-        !r.need(34ULL * lut_cnt))
-      return bail();
-    for (uint16_t j = 0; j < lut_cnt; j++) {
-      uint16_t nw, nr;
-      const uint64_t addr_off = r.i;
-      if (!r.skip(32) || !r.cu16(nw) || !r.need(nw)) return bail();
-      const uint64_t w_off = r.i;
-      r.i += nw;
-      if (!r.cu16(nr) || !r.need(nr)) return bail();
-      const uint64_t ro_off = r.i;
-      r.i += nr;
-      if (!r.check(nw <= FDT_TXN_ACCT_ADDR_MAX - acct_cnt, PF_LUT_WRITABLE) ||
-          !r.check(nr <= FDT_TXN_ACCT_ADDR_MAX - acct_cnt, PF_LUT_READONLY) ||
-          !r.check(nw + nr >= 1, PF_LUT_EMPTY))
-        return bail();
-      if (luts) {
-        luts[j].addr_off = (uint16_t)addr_off;
-        luts[j].writable_cnt = (uint8_t)nw;
-        luts[j].readonly_cnt = (uint8_t)nr;
-        luts[j].writable_off = (uint16_t)w_off;
-        luts[j].readonly_off = (uint16_t)ro_off;
-      }
-      adtl_w += nw;
-      adtl += (uint64_t)nw + nr;
-    }
-  }
-  if (!r.check(r.i == payload_sz, PF_TRAILING) ||
-      !r.check(acct_cnt + adtl <= FDT_TXN_ACCT_ADDR_MAX, PF_TOTAL_ACCTS) ||
-      !r.check(max_acct < acct_cnt + adtl, PF_ACCT_IDX))
-    return bail();
-  if (t) {
-    t->addr_table_lookup_cnt = (uint8_t)lut_cnt;
-    t->addr_table_adtl_writable_cnt = (uint8_t)adtl_w;
-    t->addr_table_adtl_cnt = (uint8_t)adtl;
-    t->_padding_reserved_1 = 0;
-  }
-  if (counters) counters->success_cnt++;
-  return fdt_txn_footprint(instr_cnt, lut_cnt);
+  return fp;
 }

@@ -175,6 +175,11 @@ class VerifyEngine:
         """Stage a batch in HBM once (DeviceBatch); verify it any number of times."""
         return DeviceBatch(self, arena, txns)
 
+    def upload_frags(self, arena, frags):
+        """Raw transaction payloads in HBM (FragBatch): each verify parses
+        them on the GPU (fdgpu_dev_batch_upload_frags)."""
+        return FragBatch(self, arena, frags)
+
     def sync(self):
         self._chk(_lib.lib().fdgpu_sync(self._h), "fdgpu_sync")
 
@@ -296,3 +301,53 @@ class DeviceBatch:
             self.free()
         except Exception:
             pass
+
+
+FRAG_DTYPE = np.dtype([("off", "<u4"), ("sz", "<u4")])
+CODE_PARSE_FAIL = -64          # FDGPU_CODE_PARSE_FAIL
+TXN_MAX_SZ = 852               # FD_TXN_MAX_SZ: stride of the parsed fd_txn_t records
+
+
+class FragBatch(DeviceBatch):
+    """Raw payloads resident in HBM (fdgpu_dev_batch_upload_frags): verify()
+    runs fd_txn_parse, the signature-count scan and the descriptor expansion
+    on the GPU before the verify kernels."""
+
+    def __init__(self, engine, arena, frags):
+        arena = np.ascontiguousarray(arena, dtype=np.uint8)
+        frags = np.ascontiguousarray(frags, dtype=FRAG_DTYPE)
+        self._e = engine
+        self.n_txn = len(frags)
+        self._b = _lib.lib().fdgpu_dev_batch_upload_frags(engine._h, arena.ctypes.data, arena.size,
+                                                          frags.ctypes.data, len(frags))
+        if not self._b:
+            raise RuntimeError(f"fdgpu_dev_batch_upload_frags failed: {_lib.last_error()}")
+        self.sig_bound = int(sum(min(16, (int(z) - 38) // 96) if z >= 134 else 0 for z in frags["sz"]))
+        self.n_sig = self.sig_bound
+
+    def codes(self, sig_codes=False):
+        out = super().codes(sig_codes)
+        self.n_sig = int(_lib.lib().fdgpu_dev_batch_sig_cnt(self._b))
+        if sig_codes:
+            return out[0], out[1][:self.n_sig]
+        return out
+
+    def txns(self):
+        """(parsed fd_txn_t records uint8[n, 852], footprints uint16[n]; 0 = not a txn)"""
+        out = np.zeros((max(self.n_txn, 1), TXN_MAX_SZ), dtype=np.uint8)
+        sz = np.zeros(max(self.n_txn, 1), dtype=np.uint16)
+        rc = _lib.lib().fdgpu_dev_batch_txns(self._e._h, self._b, out.ctypes.data, sz.ctypes.data)
+        if rc != 0:
+            raise RuntimeError(f"fdgpu_dev_batch_txns failed ({rc}): {_lib.last_error()}")
+        return out[:self.n_txn], sz[:self.n_txn]
+
+    def time2(self, iters):
+        """HIP-event timing: (wall_ms, mean ingest ms (parse + scan + expand),
+        mean verify-kernel ms, mean combine ms)."""
+        import ctypes as c
+        w, g, v, k = c.c_double(), c.c_double(), c.c_double(), c.c_double()
+        rc = _lib.lib().fdgpu_dev_batch_time2(self._e._h, self._b, int(iters), c.byref(w), c.byref(g), c.byref(v),
+                                              c.byref(k))
+        if rc != 0:
+            raise RuntimeError(f"fdgpu_dev_batch_time2 failed ({rc}): {_lib.last_error()}")
+        return w.value, g.value, v.value, k.value

@@ -211,6 +211,32 @@ uint64_t fdgpu_dev_batch_sig_cnt( fdgpu_dev_batch_t const * b );
    *combine_kernel_ms = mean duration of the per-txn combine kernel. */
 int  fdgpu_dev_batch_time( fdgpu_engine_t * e, fdgpu_dev_batch_t * b, int iters, double * wall_ms,
                            double * verify_kernel_ms, double * combine_kernel_ms );
+
+/* GPU-side ingest (fd_txn_parse on the device).  A
+   frag batch holds raw transaction payloads -- frag i is arena bytes
+   [off, off + sz), as the verify tile receives them from the quic tile --
+   and each fdgpu_dev_batch_verify runs, on the batch's queue:
+   fd_txn_parse of every payload (the host parser's own source, fdt_parse.h),
+   an exclusive scan of the signature counts, the per-signature expansion,
+   the verify kernels and the batch_single_msg combine.  Nothing is parsed
+   or expanded on the host.  A payload that is not a transaction gets
+   FDGPU_CODE_PARSE_FAIL instead of a verify code.  Half-size build only. */
+typedef struct {
+  uint32_t off;
+  uint32_t sz;          /* <= FD_TXN_MTU (1232) to parse */
+} fdgpu_frag_t;
+#define FDGPU_CODE_PARSE_FAIL (-64)
+fdgpu_dev_batch_t * fdgpu_dev_batch_upload_frags( fdgpu_engine_t * e, uint8_t const * arena, uint64_t arena_sz,
+                                                  fdgpu_frag_t const * frags, uint64_t frag_cnt );
+/* After a verify of a frag batch: frag i's parsed fd_txn_t (byte-identical to
+   fd_txn_parse's output) at txn_out + i * 852 (FD_TXN_MAX_SZ; NULL: skip),
+   its footprint (0: not a transaction) in txn_sz[i] (NULL: skip). */
+int  fdgpu_dev_batch_txns( fdgpu_engine_t * e, fdgpu_dev_batch_t * b, void * txn_out, uint16_t * txn_sz );
+/* fdgpu_dev_batch_time with the ingest kernels (parse + scan + expand of a
+   frag batch; 0 for a descriptor batch) timed apart: *ingest_ms. */
+int  fdgpu_dev_batch_time2( fdgpu_engine_t * e, fdgpu_dev_batch_t * b, int iters, double * wall_ms,
+                            double * ingest_ms, double * verify_kernel_ms, double * combine_kernel_ms );
+
 /* Blocks until all work enqueued on the engine's streams has finished. */
 int  fdgpu_sync( fdgpu_engine_t * e );
 

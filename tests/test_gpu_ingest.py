@@ -1,0 +1,152 @@
+"""GPU-side ingest: raw transaction payloads parsed on
+the MI355X (fdt_parse.h compiled by hipcc), the signature counts scanned and
+the descriptors expanded on the device, then verified.
+
+* the device parser's output equals the host fdt_txn_parse's (itself pinned
+  by test_txn_parse.c's expectations in tests/test_tile.py) byte for byte:
+  footprint and fd_txn_t, on the QUIC corpus, the txn fixtures, generated
+  cfg1/cfg3 txns, every single-byte mutation of two fixtures, every
+  truncation, and random splices/bytes;
+* the codes of a frag batch equal the oracle's on the parsed descriptors,
+  payloads that do not parse get FDGPU_CODE_PARSE_FAIL, and the signature
+  count produced on the device equals the host's;
+* a frag batch and a descriptor batch of the same txns give the same codes.
+"""
+import random
+
+import numpy as np
+import pytest
+
+from firedancer_amd import tile, workload
+from firedancer_amd.ed25519 import CODE_PARSE_FAIL, FRAG_DTYPE, TXN_MAX_SZ
+
+pytestmark = pytest.mark.gpu
+
+
+def _pack(payloads):
+    """payload list -> (arena with slack, frags)"""
+    offs, o = [], 0
+    for p in payloads:
+        offs.append(o)
+        o += (len(p) + 15) // 16 * 16
+    arena = np.zeros(o + 256, dtype=np.uint8)
+    for p, off in zip(payloads, offs):
+        arena[off:off + len(p)] = np.frombuffer(p, dtype=np.uint8)
+    frags = np.zeros(len(payloads), dtype=FRAG_DTYPE)
+    frags["off"] = offs
+    frags["sz"] = [len(p) for p in payloads]
+    return arena, frags
+
+
+def _payload_cases(txn_fixtures, quic_corpus):
+    fx = {t["name"]: bytes.fromhex(t["payload"]) for t in txn_fixtures}
+    arena, txns, _ = quic_corpus
+    cases = workload.payloads(arena, txns)
+    cases += list(fx.values())
+    for cfgf in (workload.cfg1, workload.cfg3):
+        a, tx, _ = cfgf(300, seed=5)
+        cases += workload.payloads(a, tx)
+    rnd = random.Random(0x1E57)
+    for name in ("transaction1", "transaction2"):          # every single-byte mutation (test_txn_parse.c:141-221)
+        p = fx[name]
+        for i in range(len(p)):
+            for off in (1, 0x7f, 0x80, 0xff) + tuple(rnd.randrange(1, 256) for _ in range(4)):
+                q = bytearray(p)
+                q[i] = (q[i] + off) & 255
+                cases.append(bytes(q))
+        cases += [p[:n] for n in range(len(p))]             # every truncation fails
+    base = list(fx.values())
+    for _ in range(2000):                                  # splices and random bytes
+        a, b = rnd.choice(base), rnd.choice(base)
+        i, j = rnd.randrange(len(a) + 1), rnd.randrange(len(b) + 1)
+        cases.append(a[:i] + b[j:])
+    cases += [bytes(rnd.getrandbits(8) for _ in range(rnd.choice((0, 1, 64, 200, 1232, 1233)))) for _ in range(500)]
+    return cases
+
+
+def test_device_parse_equals_host(engine, txn_fixtures, quic_corpus):
+    cases = _payload_cases(txn_fixtures, quic_corpus)
+    arena, frags = _pack(cases)
+    b = engine.upload_frags(arena, frags)
+    b.verify()
+    b.codes()
+    out, sz = b.txns()
+    n_ok = 0
+    for k, p in enumerate(cases):
+        hsz, raw = tile.txn_parse(p)
+        assert int(sz[k]) == hsz, (k, len(p))
+        if hsz:
+            n_ok += 1
+            assert bytes(out[k, :hsz]) == raw, k
+    assert n_ok > 3000 and n_ok < len(cases)
+    b.free()
+
+
+def test_frag_batch_codes_vs_oracle(engine, oracle, quic_corpus):
+    qa, qt, qcodes = quic_corpus
+    payloads = workload.payloads(qa, qt)
+    ca, ct, _ = workload.cfg1(6000, seed=0xF7A6)
+    payloads += workload.payloads(ca, ct)
+    ma, mt, _ = workload.cfg3(1500, seed=0xF7A7)
+    payloads += workload.payloads(ma, mt)
+    rnd = random.Random(3)
+    garbage = [bytes(rnd.getrandbits(8) for _ in range(rnd.randrange(0, 400))) for _ in range(300)]
+    payloads += garbage
+    rnd.shuffle(payloads)
+    arena, frags = _pack(payloads)
+    b = engine.upload_frags(arena, frags)
+    b.verify()
+    codes, sig_codes = b.codes(sig_codes=True)
+    # the host's view of the same payloads: parse, descriptors, oracle codes
+    parsed = [tile.txn_parse(p) for p in payloads]
+    td = np.zeros(len(payloads), dtype=workload.TXN_DTYPE)
+    n_sig = 0
+    for k, ((fp, raw), f) in enumerate(zip(parsed, frags)):
+        if not fp:
+            continue
+        d = tile.txn_decode(raw)
+        base = int(f["off"])
+        td[k] = (base + d["message_off"], int(f["sz"]) - d["message_off"], base + d["signature_off"],
+                 base + d["acct_addr_off"], d["signature_cnt"])
+        n_sig += d["signature_cnt"] if 1 <= d["signature_cnt"] <= 16 else 0
+    ok = np.array([fp != 0 for fp, _ in parsed])
+    exp = oracle.verify_txns(arena, td)
+    assert (codes[~ok] == CODE_PARSE_FAIL).all()
+    assert (codes[ok] == exp[ok]).all(), int((codes[ok] != exp[ok]).sum())
+    assert b.n_sig == n_sig and len(sig_codes) == n_sig
+    assert (codes == 0).sum() > 5000
+    # the same txns as a descriptor batch (host expansion) give the same codes
+    db = engine.upload(arena, td[ok])
+    db.verify()
+    assert (db.codes() == codes[ok]).all()
+    db.free()
+    b.free()
+
+
+def test_frag_batch_time_and_reverify(engine):
+    a, t, modes = workload.cfg1(20000, seed=0xF7A8)
+    arena, frags = _pack(workload.payloads(a, t))
+    b = engine.upload_frags(arena, frags)
+    b.verify()
+    first = b.codes().copy()
+    assert ((first == 0) == (modes == 0)).all()
+    wall, ingest, ver, comb = b.time2(3)
+    assert ingest > 0 and ver > 0 and wall >= 0.9 * (ingest + ver)
+    assert (b.codes() == first).all()
+    b.free()
+
+
+def test_frag_batch_edges(engine):
+    # a batch of only garbage (an empty payload included), and one payload
+    arena, frags = _pack([b"\x00" * 10, b""])
+    b = engine.upload_frags(arena, frags)
+    b.verify()
+    assert (b.codes() == CODE_PARSE_FAIL).all() and b.n_sig == 0
+    b.free()
+    a, t, _ = workload.cfg1(1, seed=9)
+    arena, frags = _pack(workload.payloads(a, t))
+    b = engine.upload_frags(arena, frags)
+    b.verify()
+    out, sz = b.txns()
+    assert sz[0] and b.codes()[0] in (0, -1, -2, -3) and out.shape == (1, TXN_MAX_SZ)
+    b.free()
