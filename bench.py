@@ -247,6 +247,42 @@ def tile_lines(eng, arena, txns, modes, cpus):
     return out
 
 
+def gpu_ingest(eng, arena, txns, ref_codes):
+    """SURVEY 8(f) row 3 on the device: the same cfg2 txns as raw payloads
+    ([sig_cnt][sigs][message], as the quic tile hands them over), parsed,
+    scanned and expanded on the GPU (fdgpu_dev_batch_upload_frags) before the
+    verify; HIP-event times of the ingest kernels and the verify, and the
+    codes against the descriptor path's (already checked against the oracle)."""
+    from firedancer_amd.ed25519 import FRAG_DTYPE
+    frags = np.zeros(len(txns), dtype=FRAG_DTYPE)
+    frags["off"] = txns["sig_off"] - 1
+    frags["sz"] = txns["msg_off"] + txns["msg_sz"] - frags["off"]
+    from firedancer_amd import tile
+    from firedancer_amd.ed25519 import CODE_PARSE_FAIL
+    fb = eng.upload_frags(arena, frags)
+    fb.verify()
+    got = fb.codes()
+    _, ing, ver, comb = fb.time2(5)
+    n_sig = fb.n_sig
+    fb.free()
+    # a corrupted message byte can leave a payload that is not a transaction:
+    # the verify tile drops it at parse (FDGPU_CODE_PARSE_FAIL here) where the
+    # descriptor path verifies it; every such frag must fail the host parser
+    # too, and every other code must equal the descriptor path's
+    pf = np.flatnonzero(got == CODE_PARSE_FAIL)
+    offs, sizes = frags["off"].astype(np.int64), frags["sz"].astype(np.int64)
+    host_pf_ok = all(tile.txn_parse(arena[offs[i]:offs[i] + sizes[i]].tobytes())[0] == 0 for i in pf)
+    rnd = np.random.default_rng(7).choice(len(txns), size=min(2000, len(txns)), replace=False)
+    host_ok = all(tile.txn_parse(arena[offs[i]:offs[i] + sizes[i]].tobytes())[0] != 0 for i in rnd if got[i] != CODE_PARSE_FAIL)
+    mism = int(((got != ref_codes) & (got != CODE_PARSE_FAIL)).sum()) + (0 if host_pf_ok and host_ok else 1)
+    return {"gpu_ingest_sigs_per_s": round(n_sig / ((ing + ver + comb) * 1e-3), 1),
+            "gpu_ingest_ms": round(ing, 4), "gpu_ingest_verify_ms": round(ver, 4),
+            "gpu_ingest_parse_failures": int(len(pf)), "gpu_ingest_parse_failures_match_host": bool(host_pf_ok),
+            "gpu_ingest_parity_mismatches": mism,
+            "gpu_ingest_note": "raw payloads -> fd_txn_parse + signature-count scan + descriptor expansion on the "
+                               "GPU, then verify + combine; isolated launches, HIP events"}
+
+
 def cpu_model():
     try:
         for line in open("/proc/cpuinfo"):
@@ -422,6 +458,8 @@ def main():
         mism = int((gpu_codes[:n_chk] != cpu_codes).sum())
         parity = {"parity_checked_txns": int(dist.sum(n_chk)), "parity_mismatches": int(dist.sum(mism)),
                   "parity_codes": {int(c): int(k) for c, k in zip(*np.unique(cpu_codes, return_counts=True))}}
+    if not args.no_extras:
+        extras.update(gpu_ingest(eng, arena, txns, batch.codes()))
     for b in batches:
         b.free()
     eng.close()
