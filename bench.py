@@ -264,7 +264,13 @@ def gpu_ingest(eng, arena, txns, ref_codes):
     got = fb.codes()
     _, ing, ver, comb = fb.time2(5)
     n_sig = fb.n_sig
+    _, tsz = fb.txns()
     fb.free()
+    # algorithmic HBM bytes of the ingest kernels: payloads read, fd_txn_t
+    # records written, per-txn records (frag 8 + txn record 20 + count 4 +
+    # first-signature 4 (x2: scan and expand) + combine item 8 + footprint 2)
+    # and 16-B signature descriptors written
+    ing_bytes = int(frags["sz"].sum()) + int(tsz.sum()) + len(frags) * 50 + n_sig * 16
     # a corrupted message byte can leave a payload that is not a transaction:
     # the verify tile drops it at parse (FDGPU_CODE_PARSE_FAIL here) where the
     # descriptor path verifies it; every such frag must fail the host parser
@@ -277,6 +283,7 @@ def gpu_ingest(eng, arena, txns, ref_codes):
     mism = int(((got != ref_codes) & (got != CODE_PARSE_FAIL)).sum()) + (0 if host_pf_ok and host_ok else 1)
     return {"gpu_ingest_sigs_per_s": round(n_sig / ((ing + ver + comb) * 1e-3), 1),
             "gpu_ingest_ms": round(ing, 4), "gpu_ingest_verify_ms": round(ver, 4),
+            "gpu_ingest_hbm_gbps": round(ing_bytes / (ing * 1e-3) / 1e9, 1), "gpu_ingest_bytes": ing_bytes,
             "gpu_ingest_parse_failures": int(len(pf)), "gpu_ingest_parse_failures_match_host": bool(host_pf_ok),
             "gpu_ingest_parity_mismatches": mism,
             "gpu_ingest_note": "raw payloads -> fd_txn_parse + signature-count scan + descriptor expansion on the "
