@@ -73,7 +73,16 @@ class Dist:
         if self.world > 1:
             import torch.distributed as dist
             os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-            dist.init_process_group("gloo", rank=self.rank, world_size=self.world)
+            # gloo reports its connections on fd 1; keep stdout for the one JSON line
+            sys.stdout.flush()
+            saved = os.dup(1)
+            os.dup2(2, 1)
+            try:
+                dist.init_process_group("gloo", rank=self.rank, world_size=self.world)
+            finally:
+                sys.stdout.flush()
+                os.dup2(saved, 1)
+                os.close(saved)
             self.dist = dist
 
     def barrier(self):
@@ -397,7 +406,14 @@ def main():
     t_gen = time.perf_counter()
     arena, txns, modes = workload.cfg1(args.txns, seed=rank_seed(dist.rank))
     t_gen = time.perf_counter() - t_gen
-    eng = VerifyEngine(dist.local_rank, max_txn=args.latency_batch, max_sig=2 * args.latency_batch,
+    # one process per GPU; more ranks than visible GPUs (a rehearsal of the
+    # multi-rank path on a one-GPU box) share devices round robin
+    device = dist.local_rank
+    if dist.world > 1:
+        import torch
+        ndev = torch.cuda.device_count()
+        device = dist.local_rank % ndev if ndev > 0 else dist.local_rank
+    eng = VerifyEngine(device, max_txn=args.latency_batch, max_sig=2 * args.latency_batch,
                        max_arena=args.latency_batch * 1232, ring_depth=RING_DEPTH)
     # `queues` device-resident copies of the batch, each on its own HIP stream
     # + workspace: step i verifies copy i % queues, so consecutive 1M-signature
@@ -444,7 +460,7 @@ def main():
                 == dist.world
             extras.update(tl)
         if args.cfg3_txns:
-            eng_nb = VerifyEngine(dist.local_rank, max_txn=1024, ring_depth=1, bucket=False)
+            eng_nb = VerifyEngine(device, max_txn=1024, ring_depth=1, bucket=False)
             extras.update(cfg3_rate(eng, eng_nb, args.cfg3_txns, workload.CFG3_SEED + dist.rank))
             eng_nb.close()
         if args.adv_txns:
