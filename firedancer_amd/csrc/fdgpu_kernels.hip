@@ -2,20 +2,25 @@
    verify engine.  One signature per lane, 256-thread workgroups; integer /
    bignum work only (no MFMA).  Per batch, on one stream:
 
-   fdgpu_verify_ra_kernel  everything but the last inversion: S < L,
-       k = SHA-512(R||A||M) mod L, [S]B by a fixed-base comb, decode A and its
-       small-order test, the per-lane table {O, -A, .., -8A}, [k](-A) + [S]B
-       by signed radix-16 windows (the reference's wNAF double-scalar
-       multiplication, fd_curve25519.c:109-153, made divergence-free), then
-       R' is compared with R's encoding (y, sign) without decompressing R,
-       using one batched inversion per workgroup.
-   fdgpu_tail_kernel       the workgroup inversions, and the signatures whose
-       y did not match (or whose A is small order) with the reference's
-       full R decode and projective compare.
-   fdgpu_finish_kernel     per signature: x = U / (Z product) -> code.
+   fdgpu_verify_hs_kernel  (default, FDGPU_HALFSIZE=1) everything: S < L,
+       k = SHA-512(R||A||M) mod L, decode A and R (decode2's rules and code
+       order) with their small-order tests and the per-lane tables
+       {O, -A, .., -8A}, {O, -R, .., -8R}; the lattice split of k into two
+       ~128-bit scalars u = v k (mod 8L) (fdgpu_lattice.h); [w]B (w = v S
+       mod L) by the fixed-base comb; [u](+-A) + [v](+-R) on one shared,
+       divergence-free signed radix-16 chain with the table entries staged
+       through LDS by LDS-DMA; the projective check against -[w]B.
+   fdgpu_full_kernel       the rare lanes whose split failed: the full-length
+       [S]B + [k](-A) chain, compared with the decoded R.
+   fdgpu_verify_ra_kernel, fdgpu_tail_kernel, fdgpu_finish_kernel
+                           (FDGPU_HALFSIZE=0) the round-1 R-avoiding path:
+       full-length k, R' compared with R's encoding through one batched
+       inversion per workgroup, the reference's full R decode for the rest.
    fdgpu_combine_kernel    per transaction, batch_single_msg first-error
        semantics (fd_ed25519_user.c:232-310), plus a ballot-compacted
        accept bitmap.
+   fdgpu_frag_* / fdgpu_scan_*  GPU-side ingest of raw payloads: fd_txn_parse
+       (fdt_parse.h), the signature-count scan, the descriptor expansion.
    fdgpu_bcomb_*           build the comb tables at engine open.
    fdgpu_test_*            per-stage diagnostics for the parity tests. */
 #include <hip/hip_runtime.h>
