@@ -51,30 +51,55 @@ FDT_HD uint64_t fdt_parse_footprint(uint64_t instr_cnt, uint64_t lut_cnt) {
   return sizeof(fdt_txn_t) + instr_cnt * sizeof(fdt_txn_instr_t) + lut_cnt * sizeof(fdt_txn_acct_addr_lut_t);
 }
 
-/* Bounds-checked reader over an untrusted payload (fd_txn_parse.c:12-75). */
+/* Bounds-checked reader over an untrusted payload (fd_txn_parse.c:12-75).
+   at(k) reads payload byte k (k < sz, checked by the callers).  On the host
+   it is a plain load.  On the GPU each lane parses its own payload, so
+   byte loads from 64 payloads hundreds of bytes apart would each touch a
+   different line, and with every lane of the chip in flight the lines are
+   evicted from L2 before the lane comes back for the next byte; there the
+   reader keeps the aligned 16 B around the cursor in registers and reloads
+   them only when the cursor leaves them (one dwordx4 per 16 bytes read;
+   the batch arena has FDGPU_ARENA_SLACK readable bytes past its end). */
 struct fdt_reader {
   const uint8_t *p;
   uint64_t sz, i, fail;
+#if defined(__HIP_DEVICE_COMPILE__)
+  const uint8_t *wb = nullptr;           /* 16-B aligned address of the window */
+  uint32_t w0 = 0, w1 = 0, w2 = 0, w3 = 0;
+  __device__ __forceinline__ uint8_t at(uint64_t k) {
+    const uint8_t *a = p + k;
+    const uint32_t o = (uint32_t)((uintptr_t)a & 15u);
+    const uint8_t *b = a - o;
+    if (b != wb) {
+      const uint4 v = *(const uint4 *)b;
+      w0 = v.x; w1 = v.y; w2 = v.z; w3 = v.w; wb = b;
+    }
+    const uint32_t d = o < 8u ? (o < 4u ? w0 : w1) : (o < 12u ? w2 : w3);
+    return (uint8_t)(d >> ((o & 3u) * 8u));
+  }
+#else
+  FDT_HDM uint8_t at(uint64_t k) { return p[k]; }
+#endif
   FDT_HDM bool need(uint64_t n, uint64_t why = FDT_PF_SHORT) {
     if (fail) return false;
     if (n > sz - i) { fail = why; return false; }
     return true;
   }
-  FDT_HDM bool u8(uint8_t &v) { if (!need(1)) return false; v = p[i++]; return true; }
+  FDT_HDM bool u8(uint8_t &v) { if (!need(1)) return false; v = at(i++); return true; }
   FDT_HDM bool skip(uint64_t n) { if (!need(n)) return false; i += n; return true; }
   /* fd_compact_u16.h:60-75 */
   FDT_HDM bool cu16(uint16_t &v) {
     if (fail) return false;
     const uint64_t avail = sz - i;
-    const uint8_t *b = p + i;
-    if (avail >= 1 && !(b[0] & 0x80)) { v = b[0]; i += 1; return true; }
-    if (avail >= 2 && !(b[1] & 0x80)) {
-      if (!b[1]) { fail = FDT_PF_CU16; return false; }
-      v = (uint16_t)((b[0] & 0x7f) | (b[1] << 7)); i += 2; return true;
+    const uint8_t b0 = avail >= 1 ? at(i) : 0, b1 = avail >= 2 ? at(i + 1) : 0, b2 = avail >= 3 ? at(i + 2) : 0;
+    if (avail >= 1 && !(b0 & 0x80)) { v = b0; i += 1; return true; }
+    if (avail >= 2 && !(b1 & 0x80)) {
+      if (!b1) { fail = FDT_PF_CU16; return false; }
+      v = (uint16_t)((b0 & 0x7f) | (b1 << 7)); i += 2; return true;
     }
-    if (avail >= 3 && !(b[2] & 0xfc)) {
-      if (!b[2]) { fail = FDT_PF_CU16; return false; }
-      v = (uint16_t)((b[0] & 0x7f) | ((b[1] & 0x7f) << 7) | (b[2] << 14)); i += 3; return true;
+    if (avail >= 3 && !(b2 & 0xfc)) {
+      if (!b2) { fail = FDT_PF_CU16; return false; }
+      v = (uint16_t)((b0 & 0x7f) | ((b1 & 0x7f) << 7) | (b2 << 14)); i += 3; return true;
     }
     fail = FDT_PF_CU16;
     return false;
@@ -83,7 +108,8 @@ struct fdt_reader {
 };
 
 FDT_HD uint64_t fdt_parse_core(const uint8_t *payload, uint64_t payload_sz, fdt_txn_t *t, uint64_t *fail) {
-  fdt_reader r{payload, payload_sz, 0, 0};
+  fdt_reader r;
+  r.p = payload; r.sz = payload_sz; r.i = 0; r.fail = 0;
   uint64_t fp = 0;
   do {
     if (!r.check(payload_sz <= FDT_TXN_MTU, FDT_PF_MTU)) break;
@@ -146,7 +172,10 @@ FDT_HD uint64_t fdt_parse_core(const uint8_t *payload, uint64_t payload_sz, fdt_
       uint16_t n_acct, data_sz;
       if (!r.need(3) || !r.u8(program_id) || !r.cu16(n_acct) || !r.need(n_acct)) { ok = false; break; }
       const uint64_t a_off = r.i;
-      for (uint16_t k = 0; k < n_acct; k++) max_acct = payload[a_off + k] > max_acct ? payload[a_off + k] : max_acct;
+      for (uint16_t k = 0; k < n_acct; k++) {
+        const uint8_t x = r.at(a_off + k);
+        max_acct = x > max_acct ? x : max_acct;
+      }
       r.i += n_acct;
       if (!r.cu16(data_sz) || !r.need(data_sz)) { ok = false; break; }
       const uint64_t d_off = r.i;
