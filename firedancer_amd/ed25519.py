@@ -322,7 +322,8 @@ class FragBatch(DeviceBatch):
                                                           frags.ctypes.data, len(frags))
         if not self._b:
             raise RuntimeError(f"fdgpu_dev_batch_upload_frags failed: {_lib.last_error()}")
-        self.sig_bound = int(sum(min(16, (int(z) - 38) // 96) if z >= 134 else 0 for z in frags["sz"]))
+        sz = frags["sz"].astype(np.int64)
+        self.sig_bound = int(np.where(sz >= 134, np.minimum(16, (sz - 38) // 96), 0).sum())   # fdgpu_frag_sig_bound
         self.n_sig = self.sig_bound
 
     def codes(self, sig_codes=False):
