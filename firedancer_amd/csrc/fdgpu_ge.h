@@ -210,6 +210,33 @@ FDG_DEV void ge_add_cached_regs(ge_p1p1 &r, const ge_p3 &p, const uint32_t (&q)[
   r.Y = t;
 }
 
+/* ge_add_cached_regs with the Y+X / Y-X swap for neg already applied by the
+   caller (q[0..9] multiplies Y1+X1, q[10..19] Y1-X1); neg still negates 2dT. */
+FDG_DEV void ge_add_cached_regs_swapped(ge_p1p1 &r, const ge_p3 &p, const uint32_t (&q)[40], bool neg) {
+  fe t, c;
+#pragma unroll
+  for (int i = 0; i < 10; i++) c.v[i] = q[30 + i];
+  fe_cneg(c, neg);
+  fe_mul(r.Z, p.T, c);             /* C = T1 2dT2 */
+#pragma unroll
+  for (int i = 0; i < 10; i++) c.v[i] = q[20 + i];
+  fe_mul(r.T, p.Z, c);             /* D = Z1 2Z2 */
+#pragma unroll
+  for (int i = 0; i < 10; i++) c.v[i] = q[i];
+  fe_add(t, p.Y, p.X);
+  fe_mul(r.X, t, c);               /* A */
+#pragma unroll
+  for (int i = 0; i < 10; i++) c.v[i] = q[10 + i];
+  fe_sub(t, p.Y, p.X);
+  fe_mul(r.Y, t, c);               /* B */
+  fe_add(t, r.T, r.Z);
+  fe_sub(r.T, r.T, r.Z);
+  r.Z = t;
+  fe_add(t, r.X, r.Y);
+  fe_sub(r.X, r.X, r.Y);
+  r.Y = t;
+}
+
 /* A cached entry in registers (Y+X, Y-X, 2Z, 2dT) as a p2 point:
    (Y+X) - (Y-X) = 2X and (Y+X) + (Y-X) = 2Y over 2Z are the same projective
    point.  neg gives -P (Y+X and Y-X swapped).  X, Y carried to R; Z = the

@@ -146,13 +146,29 @@ __global__ void __launch_bounds__(64) fdgpu_bcomb_fill_kernel(const uint32_t *ba
    uses every byte it fetches.  Entries 0..8 are the table; entry 9 parks
    (x_R, y_R), the digit strings and the pass-1 code across the kernels. */
 
+/* Stored word order of a cached entry (FDGPU_ATAB_PAIRS=1): Y+X and Y-X
+   interleaved by pairs in the first five 16-B chunks -- chunk k = (Y+X
+   limbs 2k, 2k+1, Y-X limbs 2k, 2k+1) -- then 2Z and 2dT as they are.  A
+   chain addition of -P reads Y+X and Y-X swapped: with pairs the swap is a
+   per-lane 8-B offset of two ds_read_b64 (unstage_entry_signed) instead of
+   20 per-word selects.  atab_store / atab_load convert, so every other
+   reader sees the canonical order (Y+X, Y-X, 2Z, 2dT). */
+#ifndef FDGPU_ATAB_PAIRS
+#define FDGPU_ATAB_PAIRS 1
+#endif
+FDG_DEV constexpr int atab_pos(int w) {
+  return !FDGPU_ATAB_PAIRS || w >= 20 ? w : w < 10 ? 4 * (w / 2) + (w % 2) : 4 * ((w - 10) / 2) + 2 + (w % 2);
+}
+
 FDG_DEV void atab_store(uint32_t *wsl, uint32_t entry, const ge_cached &c) {
   uint4 *p = (uint4 *)(wsl + entry * FDGPU_ATAB_WORDS);
-  uint32_t w[40];
+  uint32_t w[40], o[40];
 #pragma unroll
   for (int i = 0; i < 10; i++) { w[i] = c.YpX.v[i]; w[10 + i] = c.YmX.v[i]; w[20 + i] = c.Z2.v[i]; w[30 + i] = c.T2d.v[i]; }
 #pragma unroll
-  for (int q = 0; q < 10; q++) p[q] = make_uint4(w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]);
+  for (int i = 0; i < 40; i++) o[atab_pos(i)] = w[i];
+#pragma unroll
+  for (int q = 0; q < 10; q++) p[q] = make_uint4(o[4 * q], o[4 * q + 1], o[4 * q + 2], o[4 * q + 3]);
 }
 FDG_DEV int sext4(uint32_t x) { return ((int)(x << 28)) >> 28; }
 
@@ -160,11 +176,14 @@ FDG_DEV int sext4(uint32_t x) { return ((int)(x << 28)) >> 28; }
 
 FDG_DEV void atab_load(uint32_t (&q)[40], const uint32_t *wsl, int e) {
   const uint4 *ent = (const uint4 *)(wsl + (uint32_t)(e < 0 ? -e : e) * FDGPU_ATAB_WORDS);
+  uint32_t o[40];
 #pragma unroll
   for (int i = 0; i < 10; i++) {
     const uint4 v = ent[i];
-    q[4 * i] = v.x; q[4 * i + 1] = v.y; q[4 * i + 2] = v.z; q[4 * i + 3] = v.w;
+    o[4 * i] = v.x; o[4 * i + 1] = v.y; o[4 * i + 2] = v.z; o[4 * i + 3] = v.w;
   }
+#pragma unroll
+  for (int i = 0; i < 40; i++) q[i] = o[atab_pos(i)];
 }
 
 /* shift a 256-bit little-endian word vector left by 4 bits */
@@ -273,7 +292,7 @@ FDG_DEV void atab_build(uint32_t *wsl, const ge_p3 &An) {
   ge_p3_to_p2(a2, An); ge_dbl(t, a2); ge_p1p1_to_p3(P, t);          /* 2(-A) */
   ge_p3_to_cached(c, P); atab_store(wsl, 2, c);
   const uint32_t *ent1 = wsl + 1u * FDGPU_ATAB_WORDS;
-  auto ld1 = [ent1](int cc, int w) { return ent1[10 * cc + w]; };
+  auto ld1 = [ent1](int cc, int w) { return ent1[atab_pos(10 * cc + w)]; };
 #pragma unroll 1
   for (uint32_t e = 3; e < FDGPU_ATAB_ENTRIES; e++) {
     if (e & 1u) {
@@ -722,11 +741,39 @@ FDG_DEV void stage_entry(uint32_t *lds_wave, const uint32_t *tab, int e) {
 
 FDG_DEV void unstage_entry(uint32_t (&q)[40], const uint32_t *lds_wave) {
   const uint32_t lane = threadIdx.x & 63u;
+  uint32_t o[40];
 #pragma unroll
   for (int c = 0; c < 10; c++) {
     const uint4 v = *(const uint4 *)(lds_wave + 256 * c + 4 * lane);
+    o[4 * c] = v.x; o[4 * c + 1] = v.y; o[4 * c + 2] = v.z; o[4 * c + 3] = v.w;
+  }
+#pragma unroll
+  for (int i = 0; i < 40; i++) q[i] = o[atab_pos(i)];
+}
+
+/* The staged entry of a signed digit: q[0..9] = Y+X of the digit's point
+   (Y-X of the table's -kP when neg), q[10..19] the other, 2Z, 2dT as stored
+   (2dT still to be negated when neg).  With FDGPU_ATAB_PAIRS the swap is the
+   8-B offset of two ds_read_b64 per pair chunk. */
+FDG_DEV void unstage_entry_signed(uint32_t (&q)[40], const uint32_t *lds_wave, bool neg) {
+  const uint32_t lane = threadIdx.x & 63u;
+#if FDGPU_ATAB_PAIRS
+  const uint32_t *a = lds_wave + 4 * lane + (neg ? 2u : 0u), *b = lds_wave + 4 * lane + (neg ? 0u : 2u);
+#pragma unroll
+  for (int c = 0; c < 5; c++) {
+    const uint2 x = *(const uint2 *)(a + 256 * c), y = *(const uint2 *)(b + 256 * c);
+    q[2 * c] = x.x; q[2 * c + 1] = x.y; q[10 + 2 * c] = y.x; q[10 + 2 * c + 1] = y.y;
+  }
+#pragma unroll
+  for (int c = 5; c < 10; c++) {
+    const uint4 v = *(const uint4 *)(lds_wave + 256 * c + 4 * lane);
     q[4 * c] = v.x; q[4 * c + 1] = v.y; q[4 * c + 2] = v.z; q[4 * c + 3] = v.w;
   }
+#else
+  unstage_entry(q, lds_wave);
+#pragma unroll
+  for (int i = 0; i < 10; i++) { const uint32_t x = q[i], y = q[10 + i]; q[i] = neg ? y : x; q[10 + i] = neg ? x : y; }
+#endif
 }
 
 /* [|u|](T_A) + [|v|](T_R), digit strings pre-shifted so that digit nwin-1
@@ -774,12 +821,14 @@ FDG_DEV void hs_chain(ge_p1p1 &t, uint32_t (&ud)[5], uint32_t (&vd)[5], bool u_n
     acc3.X = acc2.X; acc3.Y = acc2.Y; acc3.Z = acc2.Z; fe_mul(acc3.T, t.X, t.Y);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   /* the window's LDS-DMA has landed */
 #if HS_STAGE == 2
-    unstage_entry(q, st_a);
-#endif
+    unstage_entry_signed(q, st_a, (du < 0) != u_neg);
+    ge_add_cached_regs_swapped(t, acc3, q, (du < 0) != u_neg);
+#else
     ge_add_cached_regs(t, acc3, q, (du < 0) != u_neg);
+#endif
     ge_p1p1_to_p3(acc3, t);
-    unstage_entry(q, st_r);
-    ge_add_cached_regs(t, acc3, q, (dv < 0) != v_neg);
+    unstage_entry_signed(q, st_r, (dv < 0) != v_neg);
+    ge_add_cached_regs_swapped(t, acc3, q, (dv < 0) != v_neg);
   }
 }
 
