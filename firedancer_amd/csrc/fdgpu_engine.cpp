@@ -596,6 +596,7 @@ struct fdgpu_dev_batch {
      buffers and the grid are sized for until a codes() call reads the count */
   bool frags = false;
   int device = 0;
+  hipStream_t compute = nullptr;            /* the engine's stream (the batch's queue until own_queue) */
   fdgpu_frag_t *d_frags = nullptr;
   uint8_t *d_txn_out = nullptr;
   uint16_t *d_txn_sz = nullptr;
@@ -616,7 +617,7 @@ uint64_t fdgpu_dev_batch_sig_cnt(fdgpu_dev_batch_t const *b) {
   if (!b->frags) return b->n_sig;
   uint32_t n = 0;                             /* the count the last verify produced on the device */
   if (hipSetDevice(b->device) != hipSuccess) return 0;
-  if (b->stream && hipStreamSynchronize(b->stream) != hipSuccess) return 0;
+  if (hipStreamSynchronize(b->stream ? b->stream : b->compute) != hipSuccess) return 0;
   if (hipMemcpy(&n, b->d_n_sig, sizeof(n), hipMemcpyDeviceToHost) != hipSuccess) return 0;
   return n;
 }
@@ -724,6 +725,7 @@ fdgpu_dev_batch_t *fdgpu_dev_batch_upload_frags(fdgpu_engine_t *e, uint8_t const
   fdgpu_dev_batch *b = new fdgpu_dev_batch();
   b->frags = true;
   b->device = e->device;
+  b->compute = e->compute;
   b->n_txn = frag_cnt;
   b->n_sig = bound;
   b->n_sig_bound = bound;
