@@ -204,6 +204,8 @@ void fdgpu_dev_batch_free( fdgpu_engine_t * e, fdgpu_dev_batch_t * b );
 int  fdgpu_dev_batch_device_ptrs( fdgpu_dev_batch_t const * b, void ** d_arena, void ** d_sig_desc,
                                   void ** d_perm, void ** d_txn_desc, int8_t ** d_sig_codes,
                                   int8_t ** d_txn_codes );
+/* signatures of the batch; for a frag batch (below) the count its last
+   verify produced on the device (waits for that verify; 0 before one) */
 uint64_t fdgpu_dev_batch_sig_cnt( fdgpu_dev_batch_t const * b );
 /* Times `iters` back-to-back verifies of the batch on the compute stream
    with HIP events: *wall_ms = first-to-last event span (all launches),
