@@ -273,7 +273,7 @@ def gpu_ingest(eng, arena, txns, ref_codes):
     got = fb.codes()
     _, ing, ver, comb = fb.time2(5)
     n_sig = fb.n_sig
-    _, tsz = fb.txns()
+    _, tsz = fb.txns(records=False)
     fb.free()
     # algorithmic HBM bytes of the ingest kernels: payloads read, fd_txn_t
     # records written, per-txn records (frag 8 + txn record 20 + count 4 +

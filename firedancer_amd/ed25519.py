@@ -333,14 +333,15 @@ class FragBatch(DeviceBatch):
             return out[0], out[1][:self.n_sig]
         return out
 
-    def txns(self):
-        """(parsed fd_txn_t records uint8[n, 852], footprints uint16[n]; 0 = not a txn)"""
-        out = np.zeros((max(self.n_txn, 1), TXN_MAX_SZ), dtype=np.uint8)
+    def txns(self, records=True):
+        """(parsed fd_txn_t records uint8[n, 852] or None, footprints uint16[n]; 0 = not a txn)"""
+        out = np.zeros((max(self.n_txn, 1), TXN_MAX_SZ), dtype=np.uint8) if records else None
         sz = np.zeros(max(self.n_txn, 1), dtype=np.uint16)
-        rc = _lib.lib().fdgpu_dev_batch_txns(self._e._h, self._b, out.ctypes.data, sz.ctypes.data)
+        rc = _lib.lib().fdgpu_dev_batch_txns(self._e._h, self._b, out.ctypes.data if records else None,
+                                             sz.ctypes.data)
         if rc != 0:
             raise RuntimeError(f"fdgpu_dev_batch_txns failed ({rc}): {_lib.last_error()}")
-        return out[:self.n_txn], sz[:self.n_txn]
+        return (out[:self.n_txn] if records else None), sz[:self.n_txn]
 
     def time2(self, iters):
         """HIP-event timing: (wall_ms, mean ingest ms (parse + scan + expand),

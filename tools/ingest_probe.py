@@ -33,7 +33,7 @@ def main():
     for _ in range(args.iters):
         fb.verify()
     codes = fb.codes()
-    _, tsz = fb.txns()
+    _, tsz = fb.txns(records=False)
     wall, ing, ver, comb = fb.time2(args.iters)
     n_sig = fb.n_sig
     ing_bytes = int(frags["sz"].sum()) + int(tsz.sum()) + len(frags) * 50 + n_sig * 16
