@@ -59,6 +59,9 @@ def parse():
     ap.add_argument("--tile", type=int, default=1, help="1: add the cfg5 verify-tile lines (tango in -> GPU -> tango out)")
     ap.add_argument("--adv-txns", type=int, default=1_000_000,
                     help="txns of each adversarial batch (all equation failures / all corrupted R; 0: skip)")
+    ap.add_argument("--keypool-txns", type=int, default=1_000_000,
+                    help="txns of the signer-reuse batch (key pool of 4096) timed with and without the key "
+                         "cache (0: skip)")
     return ap.parse_args()
 
 
@@ -407,6 +410,29 @@ def cfg3_rate(eng, eng_nobucket, n_txn, seed):
     return out
 
 
+def key_cache_rate(eng, device, n_txn, seed, pool=4096):
+    """Signer reuse (a secondary line, not `value`): cfg1-shaped txns whose
+    signers come from a pool of `pool` keys (10% corrupted, so ~1/30 of the
+    keys are one-off corrupted ones), device-resident, timed without and with
+    FDGPU_FLAG_KEY_CACHE (one A decode + table per distinct key); the two
+    must give the same codes."""
+    from firedancer_amd import VerifyEngine, workload
+    arena, txns, modes = workload.make_txns(n_txn, seed, key_pool=pool)
+    kc = VerifyEngine(device, max_txn=1024, ring_depth=1, key_cache=True)
+    out, codes = {"keypool_txns": n_txn, "keypool_keys": pool}, {}
+    for tag, e in (("", eng), ("_key_cache", kc)):
+        b = e.upload(arena, txns)
+        b.verify()
+        codes[tag] = b.codes()
+        _, kv, kcomb = b.time(5)
+        out[f"keypool{tag}_sigs_per_s"] = round(b.n_sig / ((kv + kcomb) * 1e-3), 1)
+        b.free()
+    kc.close()
+    out["keypool_key_cache_codes_equal"] = bool((codes[""] == codes["_key_cache"]).all())
+    out["keypool_self_check"] = bool(((codes[""] == 0) == (modes == 0)).all())
+    return out
+
+
 def main():
     args = parse()
     dist = Dist()
@@ -476,6 +502,8 @@ def main():
             eng_nb = VerifyEngine(device, max_txn=1024, ring_depth=1, bucket=False)
             extras.update(cfg3_rate(eng, eng_nb, args.cfg3_txns, workload.CFG3_SEED + dist.rank))
             eng_nb.close()
+        if args.keypool_txns:
+            extras.update(key_cache_rate(eng, device, args.keypool_txns, workload.CFG1_SEED + 0x700 + dist.rank))
         if args.adv_txns:
             extras.update(adversarial(eng, args.adv_txns, workload.CFG1_SEED + 0x400 + dist.rank,
                                       (kv_ms + kc_ms) / n_sig, cpus))

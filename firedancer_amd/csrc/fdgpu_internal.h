@@ -63,6 +63,7 @@ typedef struct {
 #define FDGPU_BLOCK         256u
 #define FDGPU_FLAG_REF_MAP  1u            /* portable-backend error mapping */
 #define FDGPU_FLAG_KFULL    2u            /* half-size path: every lane takes the full-length fallback */
+#define FDGPU_FLAG_KCACHE   4u            /* half-size path: one -A decode + table per distinct key */
 /* SHA-512 block-count groups of the host-side bucketing (expand): messages of
    more blocks than this share the last group */
 #define FDGPU_NBLK_GROUPS   32u

@@ -24,6 +24,7 @@
    fdgpu_bcomb_*           build the comb tables at engine open.
    fdgpu_test_*            per-stage diagnostics for the parity tests. */
 #include <hip/hip_runtime.h>
+#include <random>
 
 #include "fdgpu_ge.h"
 #include "fdgpu_internal.h"
@@ -197,7 +198,9 @@ FDG_DEV void shl4(uint32_t (&w)[8]) {
    comb in pass 1 and parked (cached form) in workspace entry 10.  The chain
    only serves k: 64 windows of 4 doublings + one A-table addition; the last
    window's sum is converted to p3 and the parked [S]B added. */
-FDG_DEV void dsm_k(ge_p2 &acc2, uint32_t (&kd)[KD_WORDS], const uint32_t *wsl, uint32_t sb_entry = FDGPU_WS_SB) {
+FDG_DEV void dsm_k(ge_p2 &acc2, uint32_t (&kd)[KD_WORDS], const uint32_t *wsl, uint32_t sb_entry = FDGPU_WS_SB,
+                   const uint32_t *ta = nullptr) {
+  if (!ta) ta = wsl;                      /* the -A table: own workspace, or the key cache's */
   ge_p3 acc3;
   ge_p1p1 t;
   uint32_t q[40];
@@ -206,14 +209,14 @@ FDG_DEV void dsm_k(ge_p2 &acc2, uint32_t (&kd)[KD_WORDS], const uint32_t *wsl, u
   {
     const int e = sext4(kd[7] >> 28);
     shl4(kd);
-    atab_load(q, wsl, e);
+    atab_load(q, ta, e);
     ge_cached_regs_to_p2(acc2, q, e < 0);
   }
 #pragma unroll 1
   for (int j = 62; j >= 0; j--) {
     const int e = sext4(kd[7] >> 28);
     shl4(kd);
-    atab_load(q, wsl, e);
+    atab_load(q, ta, e);
 #pragma unroll 1
     for (int r = 0; r < 4; r++) {
       ge_dbl(t, acc2);
@@ -780,8 +783,8 @@ FDG_DEV void unstage_entry_signed(uint32_t (&q)[40], const uint32_t *lds_wave, b
    sits in the top nibble; u_neg / v_neg flip every digit's sign (the tables
    hold -A, -R).  Leaves the completed sum of the last addition in t. */
 FDG_DEV void hs_chain(ge_p1p1 &t, uint32_t (&ud)[5], uint32_t (&vd)[5], bool u_neg, bool v_neg, uint32_t nwin,
-                      const uint32_t *wsl) {
-  const uint32_t *ta = wsl, *tr = wsl + FDGPU_WS_RTAB * FDGPU_ATAB_WORDS;
+                      const uint32_t *wsl, const uint32_t *ta) {
+  const uint32_t *tr = wsl + FDGPU_WS_RTAB * FDGPU_ATAB_WORDS;
   __shared__ uint32_t s_stage[FDGPU_BLOCK / 64][HS_STAGE][10 * 256];
   uint32_t *st_r = &s_stage[threadIdx.x >> 6][0][0];
 #if HS_STAGE == 2
@@ -834,11 +837,13 @@ FDG_DEV void hs_chain(ge_p1p1 &t, uint32_t (&ud)[5], uint32_t (&vd)[5], bool u_n
 
 /* The verify kernel of the half-size path; codes of lanes it settles are
    written here, lanes whose split failed are queued for fdgpu_full_kernel. */
+template <bool KC>
 __global__ void __launch_bounds__(FDGPU_BLOCK, FDGPU_VERIFY_WAVES)
 fdgpu_verify_hs_kernel(const uint8_t *__restrict__ arena, const fdgpu_sig_desc_t *__restrict__ sigs, uint32_t n_sig_arg,
                        const uint32_t *__restrict__ n_sig_dev, const uint32_t *__restrict__ btab,
                        uint32_t *__restrict__ ws, const uint32_t *__restrict__ perm, int8_t *__restrict__ codes,
-                       uint32_t *__restrict__ queue, uint32_t *__restrict__ queue_cnt, uint32_t flags) {
+                       uint32_t *__restrict__ queue, uint32_t *__restrict__ queue_cnt, uint32_t flags,
+                       const uint32_t *__restrict__ key_of, const uint32_t *__restrict__ kverd) {
   /* n_sig_dev: the count is produced on the device (GPU-side ingest) and the
      grid covers an upper bound; blocks past it leave at once */
   const uint32_t n_sig = n_sig_dev ? *n_sig_dev : n_sig_arg;
@@ -852,6 +857,7 @@ fdgpu_verify_hs_kernel(const uint8_t *__restrict__ arena, const fdgpu_sig_desc_t
   for (int off = 32; off > 0; off >>= 1) nb = max(nb, (uint32_t)__shfl_xor((int)nb, off));
   uint32_t *wsl = lane_ws(ws, i);
   uint32_t *park = wsl + FDGPU_WS_PARK * FDGPU_ATAB_WORDS;
+  const uint32_t *ta = wsl;                    /* this lane's -A table */
   FDGPU_STAMP(0);
   uint32_t Renc[8], Aenc[8];
   load32(Renc, arena + d.sig_off);
@@ -878,10 +884,21 @@ fdgpu_verify_hs_kernel(const uint8_t *__restrict__ arena, const fdgpu_sig_desc_t
      tables of -A and -R */
   {
     ge_p3 P, Pn;
-    const bool a_ok = ge_decode(P, Aenc, ref_map);
-    const bool a_small = ge_is_small_order_affine(P);
-    ge_p3_neg(Pn, P);
-    atab_build(wsl, Pn);
+    bool a_ok, a_small;
+    if (KC) {
+      /* key cache: the -A table was built once per distinct key by
+         fdgpu_key_table_kernel in its representative lane's workspace, and
+         the chain reads it there */
+      const uint32_t r = key_of[active ? i : n_sig - 1u], vd = kverd[r];
+      a_ok = (vd & 1u) != 0;
+      a_small = (vd & 2u) != 0;
+      ta = lane_ws(ws, r);
+    } else {
+      a_ok = ge_decode(P, Aenc, ref_map);
+      a_small = ge_is_small_order_affine(P);
+      ge_p3_neg(Pn, P);
+      atab_build(wsl, Pn);
+    }
     FDGPU_STAMP(3);
     const bool r_ok = ge_decode(P, Renc, ref_map);
     const bool r_small = ge_is_small_order_affine(P);
@@ -939,7 +956,7 @@ fdgpu_verify_hs_kernel(const uint8_t *__restrict__ arena, const fdgpu_sig_desc_t
 #pragma unroll 1
     for (uint32_t s = nwin; s < 40; s++) { shl4_5(ud); shl4_5(vd); }
     ge_p1p1 t;
-    hs_chain(t, ud, vd, hs.u_neg, hs.v_neg, nwin, wsl);
+    hs_chain(t, ud, vd, hs.u_neg, hs.v_neg, nwin, wsl, ta);
     /* chain == -[w]B:  x = X/Z = -(YpX - YmX)/Z2,  y = Y/T = (YpX + YmX)/Z2 */
     uint32_t q[40];
     atab_load(q, wsl, (int)FDGPU_WS_SB);
@@ -972,11 +989,103 @@ fdgpu_verify_hs_kernel(const uint8_t *__restrict__ arena, const fdgpu_sig_desc_t
   }
 }
 
+/* ---------------- key cache (FDGPU_FLAG_KCACHE) ----------------
+   Signers repeat within a batch (a vote account signs every slot).  Each
+   distinct public key is decoded and its -A table built once, in the
+   workspace of one representative lane; the verify kernel's other lanes with
+   that key copy the table (1440 B) instead of decompressing A (a 2^252-3
+   exponentiation) and building it.  Results are unchanged: the decode is a
+   function of the 32 key bytes only.
+
+   fdgpu_key_dedup_kernel: an open-addressing table of signature indices,
+   keyed by a seeded hash of all 32 key bytes.  A lane claims an empty slot
+   with atomicCAS (after a plain load saw it empty), or compares its key with
+   the bytes of the index a slot already holds (the arena is immutable, so
+   nothing waits on another lane);
+   after KC_PROBES probes it stays its own representative, which bounds the
+   work whatever keys a batch carries.  key_of[i] = representative of i;
+   the representatives are appended to reps (compact, so the table kernel
+   runs dense waves however they are scattered over the batch). */
+#define KC_PROBES 32u
+#define KC_EMPTY 0xffffffffu
+
+FDG_DEV uint32_t kc_hash(const uint32_t (&a)[8], uint64_t seed) {
+  uint64_t h = seed;
+#pragma unroll
+  for (int j = 0; j < 4; j++) {
+    h ^= ((uint64_t)a[2 * j + 1] << 32) | a[2 * j];
+    h *= 0x9e3779b97f4a7c15ull;
+    h ^= h >> 29;
+  }
+  h *= 0xbf58476d1ce4e5b9ull;
+  return (uint32_t)(h >> 32) ^ (uint32_t)h;
+}
+
+__global__ void __launch_bounds__(256) fdgpu_key_dedup_kernel(const uint8_t *__restrict__ arena,
+                                                              const fdgpu_sig_desc_t *__restrict__ sigs,
+                                                              uint32_t n_sig_arg, const uint32_t *__restrict__ n_sig_dev,
+                                                              uint32_t *__restrict__ ht, uint32_t ht_mask,
+                                                              uint32_t *__restrict__ key_of, uint32_t *__restrict__ reps,
+                                                              uint32_t *__restrict__ rep_cnt, uint64_t seed) {
+  const uint32_t n_sig = n_sig_dev ? *n_sig_dev : n_sig_arg;
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n_sig) return;
+  uint32_t a[8];
+  load32(a, arena + sigs[i].pub_off);
+  uint32_t slot = kc_hash(a, seed) & ht_mask, rep = i;
+  for (uint32_t p = 0; p < KC_PROBES; p++, slot = (slot + 1u) & ht_mask) {
+    /* a plain load first: a signer's slot is taken by its first signature,
+       and the many later ones then compare without an atomic on a hot line */
+    uint32_t v = ht[slot];                          /* stale only as EMPTY: the CAS then reads it */
+    if (v == KC_EMPTY) {
+      v = atomicCAS(&ht[slot], KC_EMPTY, i);
+      if (v == KC_EMPTY) break;                     /* claimed: i represents its key */
+    }
+    uint32_t b[8];
+    load32(b, arena + sigs[v].pub_off);
+    uint32_t diff = 0;
+#pragma unroll
+    for (int j = 0; j < 8; j++) diff |= a[j] ^ b[j];
+    if (!diff) { rep = v; break; }
+  }
+  key_of[i] = rep;
+  const uint64_t m = __ballot(rep == i);
+  if (m) {
+    const int lane = (int)(threadIdx.x & 63u), leader = __ffsll((long long)m) - 1;
+    uint32_t base = 0;
+    if (lane == leader) base = atomicAdd(rep_cnt, (uint32_t)__popcll(m));
+    base = (uint32_t)__shfl((int)base, leader, 64);
+    if (rep == i) reps[base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull))] = i;
+  }
+}
+
+/* One lane per representative: decode A, small-order test, -A table into the
+   representative's own workspace, verdict (bit 0 decoded, bit 1 small
+   order) into kverd.  The grid covers every signature; blocks past the
+   representative count leave at once. */
+__global__ void __launch_bounds__(FDGPU_BLOCK, FDGPU_VERIFY_WAVES)
+fdgpu_key_table_kernel(const uint8_t *__restrict__ arena, const fdgpu_sig_desc_t *__restrict__ sigs,
+                       uint32_t *__restrict__ ws, const uint32_t *__restrict__ reps,
+                       const uint32_t *__restrict__ rep_cnt, uint32_t *__restrict__ kverd, uint32_t flags) {
+  const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
+  if (q >= *rep_cnt) return;
+  const uint32_t i = reps[q];
+  uint32_t Aenc[8];
+  load32(Aenc, arena + sigs[i].pub_off);
+  ge_p3 P, Pn;
+  const bool a_ok = ge_decode(P, Aenc, (flags & FDGPU_FLAG_REF_MAP) != 0);
+  const bool a_small = ge_is_small_order_affine(P);
+  ge_p3_neg(Pn, P);
+  atab_build(lane_ws(ws, i), Pn);
+  kverd[i] = (a_ok ? 1u : 0u) | (a_small ? 2u : 0u);
+}
+
 /* The queued lanes of fdgpu_verify_hs_kernel: [S]B + [k](-A) with k's 64
    windows (dsm_k), compared with the decoded R (affine, parked). */
 __global__ void __launch_bounds__(FDGPU_BLOCK, FDGPU_VERIFY_WAVES)
 fdgpu_full_kernel(uint32_t *__restrict__ ws, const uint32_t *__restrict__ perm, int8_t *__restrict__ codes,
-                  const uint32_t *__restrict__ queue, const uint32_t *__restrict__ queue_cnt, uint32_t slots) {
+                  const uint32_t *__restrict__ queue, const uint32_t *__restrict__ queue_cnt, uint32_t slots,
+                  const uint32_t *__restrict__ key_of) {
   const uint32_t cnt = *queue_cnt;
   if (blockIdx.x * blockDim.x >= cnt) return;
   for (uint32_t q = blockIdx.x * blockDim.x + threadIdx.x; q < cnt; q += slots) {
@@ -987,7 +1096,7 @@ fdgpu_full_kernel(uint32_t *__restrict__ ws, const uint32_t *__restrict__ perm, 
 #pragma unroll
     for (int j = 0; j < KD_WORDS; j++) kd[j] = park[HPARK_KD + j];
     ge_p2 Rc;
-    dsm_k(Rc, kd, wsl, FDGPU_WS_SB);
+    dsm_k(Rc, kd, wsl, FDGPU_WS_SB, key_of ? lane_ws(ws, key_of[i]) : wsl);
     fe x, y, l;
 #pragma unroll
     for (int j = 0; j < 10; j++) { x.v[j] = park[HPARK_XR + j]; y.v[j] = park[HPARK_YR + j]; }
@@ -1309,17 +1418,27 @@ hipError_t fdgpu_btab_build(uint32_t *d_btab, hipStream_t stream) {
 
 hipError_t fdgpu_verify_occupancy(int *blocks_per_cu) {
 #if FDGPU_HALFSIZE
-  return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, fdgpu_verify_hs_kernel, FDGPU_BLOCK, 0);
+  return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, fdgpu_verify_hs_kernel<false>, FDGPU_BLOCK, 0);
 #else
   return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, fdgpu_verify_ra_kernel, FDGPU_BLOCK, 0);
 #endif
 }
 
 /* workspace: per-lane words, then per-workgroup Z products and their
-   inverses, the slow-path queue and its counter */
+   inverses, the slow-path queue and its counter (+ the key cache's
+   representative count), then the key cache's hash table, key_of, verdicts
+   and representative list */
+static uint64_t kc_ht_slots(uint64_t lanes) {       /* power of two >= 2 lanes */
+  uint64_t h = 64;
+  while (h < 2 * lanes) h <<= 1;
+  return h;
+}
+
 size_t fdgpu_ws_bytes(uint64_t n_sig) {
   const uint64_t grid = (n_sig + FDGPU_BLOCK - 1) / FDGPU_BLOCK, lanes = grid * FDGPU_BLOCK;
-  return (size_t)(lanes * FDGPU_WS_LANE_WORDS + 20 * grid + lanes + 16) * sizeof(uint32_t);
+  /* + the key cache's hash table, key_of and verdicts (FDGPU_FLAG_KCACHE) */
+  return (size_t)(lanes * FDGPU_WS_LANE_WORDS + 20 * grid + lanes + 16 + kc_ht_slots(lanes) + 3 * lanes) *
+         sizeof(uint32_t);
 }
 
 hipError_t fdgpu_launch_verify_sigs(const uint8_t *d_arena, const fdgpu_sig_desc_t *d_sigs, uint32_t n_sig,
@@ -1347,10 +1466,28 @@ hipError_t fdgpu_launch_verify_sigs(const uint8_t *d_arena, const fdgpu_sig_desc
   const uint32_t slow_blocks = grid < (uint32_t)resident ? grid : (uint32_t)resident;
 #if FDGPU_HALFSIZE
   (void)wg_tot; (void)wg_inv;
-  hipLaunchKernelGGL(fdgpu_verify_hs_kernel, dim3(grid), dim3(FDGPU_BLOCK), 0, stream, d_arena, d_sigs, n_sig, d_n_sig,
-                     d_btab, d_ws, d_perm, d_sig_codes, queue, cnt, flags);
+  if (flags & FDGPU_FLAG_KCACHE) {
+    const uint64_t hts = kc_ht_slots(lanes);
+    uint32_t *ht = cnt + 16, *key_of = ht + hts, *kverd = key_of + lanes, *reps = kverd + lanes, *rep_cnt = cnt + 1;
+    static uint64_t seed = 0;
+    if (!seed) seed = ((uint64_t)std::random_device{}() << 32 | std::random_device{}()) | 1u;
+    e = hipMemsetAsync(ht, 0xff, hts * sizeof(uint32_t), stream);
+    if (e == hipSuccess) e = hipMemsetAsync(rep_cnt, 0, sizeof(uint32_t), stream);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(fdgpu_key_dedup_kernel, dim3((n_sig + 255) / 256), dim3(256), 0, stream, d_arena, d_sigs, n_sig,
+                       d_n_sig, ht, (uint32_t)(hts - 1), key_of, reps, rep_cnt, seed);
+    hipLaunchKernelGGL(fdgpu_key_table_kernel, dim3(grid), dim3(FDGPU_BLOCK), 0, stream, d_arena, d_sigs, d_ws, reps,
+                       rep_cnt, kverd, flags);
+    hipLaunchKernelGGL(fdgpu_verify_hs_kernel<true>, dim3(grid), dim3(FDGPU_BLOCK), 0, stream, d_arena, d_sigs, n_sig,
+                       d_n_sig, d_btab, d_ws, d_perm, d_sig_codes, queue, cnt, flags, key_of, kverd);
+    hipLaunchKernelGGL(fdgpu_full_kernel, dim3(slow_blocks), dim3(FDGPU_BLOCK), 0, stream, d_ws, d_perm, d_sig_codes,
+                       queue, cnt, slow_blocks * FDGPU_BLOCK, key_of);
+    return hipGetLastError();
+  }
+  hipLaunchKernelGGL(fdgpu_verify_hs_kernel<false>, dim3(grid), dim3(FDGPU_BLOCK), 0, stream, d_arena, d_sigs, n_sig,
+                     d_n_sig, d_btab, d_ws, d_perm, d_sig_codes, queue, cnt, flags, nullptr, nullptr);
   hipLaunchKernelGGL(fdgpu_full_kernel, dim3(slow_blocks), dim3(FDGPU_BLOCK), 0, stream, d_ws, d_perm, d_sig_codes,
-                     queue, cnt, slow_blocks * FDGPU_BLOCK);
+                     queue, cnt, slow_blocks * FDGPU_BLOCK, nullptr);
   return hipGetLastError();
 #endif
   if (d_n_sig) return hipErrorInvalidValue;                  /* device-side counts: half-size path only */

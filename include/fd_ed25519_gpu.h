@@ -96,6 +96,10 @@ typedef struct {
                                       SHA-512 block count, codes still returned in order) */
 #define FDGPU_FLAG_FULL_PATH  4u  /* diagnostics: every signature takes the full-length fallback chain
                                       (fdgpu_full_kernel), so the parity tests cover that path */
+#define FDGPU_FLAG_KEY_CACHE  8u  /* decode each distinct public key of a batch once (signer reuse, e.g.
+                                      vote traffic): a hash dedup + one -A table per key, copied by the
+                                      other signatures of that key; same codes, faster when keys repeat,
+                                      ~2% slower when every key is distinct */
 
 /* Status codes of the engine API (distinct from verify codes). */
 #define FDGPU_OK            ( 0)
