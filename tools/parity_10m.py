@@ -13,6 +13,9 @@ fd_ed25519_verify codes of every (R||S, A, msg) it contains):
   quic       the reference's 1000-txn QUIC corpus (src/waltz/quic/tests/txn/tx)
   cfg1       single-signature txns, 10% one-bit corrupted
   cfg3       1-12 signature txns sharing one message, msg <= 1232 B
+--key-cache runs the engine with FDGPU_FLAG_KEY_CACHE and --key-pool K draws
+the cfg1/cfg3 signers from K keys (signer reuse), so the key cache is held
+to the same bar.
 Exit status 1 on any mismatch.
 """
 import argparse
@@ -63,9 +66,11 @@ def main():
     ap.add_argument("--cfg3", type=int, default=600_000, help="multi-signature txns")
     ap.add_argument("--threads", type=int, default=workload.default_threads())
     ap.add_argument("--out", default=os.path.join(REPO, "gpurun_out", "parity10m.json"))
+    ap.add_argument("--key-cache", action="store_true", help="engine with FDGPU_FLAG_KEY_CACHE")
+    ap.add_argument("--key-pool", type=int, default=0, help="cfg1/cfg3 signers from this many keys (0: fresh)")
     args = ap.parse_args()
 
-    eng = fa.VerifyEngine(0, max_txn=1 << 17, max_sig=1 << 21, max_arena=1 << 28)
+    eng = fa.VerifyEngine(0, max_txn=1 << 17, max_sig=1 << 21, max_arena=1 << 28, key_cache=args.key_cache)
     parts = []
 
     def check(name, arena, txns, per_sig):
@@ -105,14 +110,14 @@ def main():
 
     n1 = args.cfg1
     t = time.time()
-    a, tx, modes = workload.make_txns(n1, workload.CFG1_SEED + 0x100, multi=False)
+    a, tx, modes = workload.make_txns(n1, workload.CFG1_SEED + 0x100, multi=False, key_pool=args.key_pool)
     log(f"generated cfg1 {n1} txns in {time.time() - t:.1f}s")
     check("cfg1", a, tx, False)
     del a, tx, modes
 
     n3 = args.cfg3
     t = time.time()
-    a, tx, modes = workload.make_txns(n3, workload.CFG3_SEED + 0x100, multi=True)
+    a, tx, modes = workload.make_txns(n3, workload.CFG3_SEED + 0x100, multi=True, key_pool=args.key_pool)
     log(f"generated cfg3 {n3} txns ({int(tx['sig_cnt'].sum())} sigs) in {time.time() - t:.1f}s")
     check("cfg3", a, tx, True)
     del a, tx, modes
@@ -122,6 +127,7 @@ def main():
     total_checks = sum(p["sigs"] if "per_sig_checked" not in p else p["per_sig_checked"] for p in parts)
     bad = sum(p["txn_mismatches"] + p.get("sig_mismatches", 0) for p in parts)
     summary = {"what": "cfg4 full-scale parity: GPU engine vs CPU oracle, code for code",
+               "key_cache": bool(args.key_cache), "key_pool": args.key_pool,
                "signatures": total_sigs, "per_signature_codes_compared": total_checks,
                "transactions": sum(p["txns"] for p in parts), "mismatches": bad, "parts": parts,
                "wall_s": round(time.time() - T0, 1)}
