@@ -64,6 +64,9 @@ typedef struct {
 #define FDGPU_FLAG_REF_MAP  1u            /* portable-backend error mapping */
 #define FDGPU_FLAG_KFULL    2u            /* half-size path: every lane takes the full-length fallback */
 #define FDGPU_FLAG_KCACHE   4u            /* half-size path: one -A decode + table per distinct key */
+#ifndef FDGPU_SPLIT_A
+#define FDGPU_SPLIT_A       0             /* A/B: A decode + table in a kernel of its own (no dedup) */
+#endif
 /* SHA-512 block-count groups of the host-side bucketing (expand): messages of
    more blocks than this share the last group */
 #define FDGPU_NBLK_GROUPS   32u

@@ -889,7 +889,7 @@ fdgpu_verify_hs_kernel(const uint8_t *__restrict__ arena, const fdgpu_sig_desc_t
       /* key cache: the -A table was built once per distinct key by
          fdgpu_key_table_kernel in its representative lane's workspace, and
          the chain reads it there */
-      const uint32_t r = key_of[active ? i : n_sig - 1u], vd = kverd[r];
+      const uint32_t di = active ? i : n_sig - 1u, r = key_of ? key_of[di] : di, vd = kverd[r];
       a_ok = (vd & 1u) != 0;
       a_small = (vd & 2u) != 0;
       ta = lane_ws(ws, r);
@@ -1066,10 +1066,13 @@ __global__ void __launch_bounds__(256) fdgpu_key_dedup_kernel(const uint8_t *__r
 __global__ void __launch_bounds__(FDGPU_BLOCK, FDGPU_VERIFY_WAVES)
 fdgpu_key_table_kernel(const uint8_t *__restrict__ arena, const fdgpu_sig_desc_t *__restrict__ sigs,
                        uint32_t *__restrict__ ws, const uint32_t *__restrict__ reps,
-                       const uint32_t *__restrict__ rep_cnt, uint32_t *__restrict__ kverd, uint32_t flags) {
+                       const uint32_t *__restrict__ rep_cnt, uint32_t n_arg, uint32_t *__restrict__ kverd,
+                       uint32_t flags) {
+  /* reps == nullptr (FDGPU_SPLIT_A): every signature is its own
+     representative, counted by *rep_cnt (device-side count) or n_arg */
   const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
-  if (q >= *rep_cnt) return;
-  const uint32_t i = reps[q];
+  if (q >= (rep_cnt ? *rep_cnt : n_arg)) return;
+  const uint32_t i = reps ? reps[q] : q;
   uint32_t Aenc[8];
   load32(Aenc, arena + sigs[i].pub_off);
   ge_p3 P, Pn;
@@ -1466,6 +1469,19 @@ hipError_t fdgpu_launch_verify_sigs(const uint8_t *d_arena, const fdgpu_sig_desc
   const uint32_t slow_blocks = grid < (uint32_t)resident ? grid : (uint32_t)resident;
 #if FDGPU_HALFSIZE
   (void)wg_tot; (void)wg_inv;
+#if FDGPU_SPLIT_A
+  /* A/B variant: every lane's A decode + table in a kernel of its own */
+  if (!(flags & FDGPU_FLAG_KCACHE)) {
+    uint32_t *kverd = cnt + 16 + kc_ht_slots(lanes) + lanes;
+    hipLaunchKernelGGL(fdgpu_key_table_kernel, dim3(grid), dim3(FDGPU_BLOCK), 0, stream, d_arena, d_sigs, d_ws,
+                       (const uint32_t *)nullptr, d_n_sig, n_sig, kverd, flags);
+    hipLaunchKernelGGL(fdgpu_verify_hs_kernel<true>, dim3(grid), dim3(FDGPU_BLOCK), 0, stream, d_arena, d_sigs, n_sig,
+                       d_n_sig, d_btab, d_ws, d_perm, d_sig_codes, queue, cnt, flags, (const uint32_t *)nullptr, kverd);
+    hipLaunchKernelGGL(fdgpu_full_kernel, dim3(slow_blocks), dim3(FDGPU_BLOCK), 0, stream, d_ws, d_perm, d_sig_codes,
+                       queue, cnt, slow_blocks * FDGPU_BLOCK, (const uint32_t *)nullptr);
+    return hipGetLastError();
+  }
+#endif
   if (flags & FDGPU_FLAG_KCACHE) {
     const uint64_t hts = kc_ht_slots(lanes);
     uint32_t *ht = cnt + 16, *key_of = ht + hts, *kverd = key_of + lanes, *reps = kverd + lanes, *rep_cnt = cnt + 1;
@@ -1477,7 +1493,7 @@ hipError_t fdgpu_launch_verify_sigs(const uint8_t *d_arena, const fdgpu_sig_desc
     hipLaunchKernelGGL(fdgpu_key_dedup_kernel, dim3((n_sig + 255) / 256), dim3(256), 0, stream, d_arena, d_sigs, n_sig,
                        d_n_sig, ht, (uint32_t)(hts - 1), key_of, reps, rep_cnt, seed);
     hipLaunchKernelGGL(fdgpu_key_table_kernel, dim3(grid), dim3(FDGPU_BLOCK), 0, stream, d_arena, d_sigs, d_ws, reps,
-                       rep_cnt, kverd, flags);
+                       rep_cnt, 0u, kverd, flags);
     hipLaunchKernelGGL(fdgpu_verify_hs_kernel<true>, dim3(grid), dim3(FDGPU_BLOCK), 0, stream, d_arena, d_sigs, n_sig,
                        d_n_sig, d_btab, d_ws, d_perm, d_sig_codes, queue, cnt, flags, key_of, kverd);
     hipLaunchKernelGGL(fdgpu_full_kernel, dim3(slow_blocks), dim3(FDGPU_BLOCK), 0, stream, d_ws, d_perm, d_sig_codes,
