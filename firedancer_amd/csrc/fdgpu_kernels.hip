@@ -1028,35 +1028,45 @@ __global__ void __launch_bounds__(256) fdgpu_key_dedup_kernel(const uint8_t *__r
                                                               uint32_t *__restrict__ key_of, uint32_t *__restrict__ reps,
                                                               uint32_t *__restrict__ rep_cnt, uint64_t seed) {
   const uint32_t n_sig = n_sig_dev ? *n_sig_dev : n_sig_arg;
+  if (blockIdx.x * blockDim.x >= n_sig) return;     /* whole block: the barriers below need every thread */
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n_sig) return;
-  uint32_t a[8];
-  load32(a, arena + sigs[i].pub_off);
-  uint32_t slot = kc_hash(a, seed) & ht_mask, rep = i;
-  for (uint32_t p = 0; p < KC_PROBES; p++, slot = (slot + 1u) & ht_mask) {
-    /* a plain load first: a signer's slot is taken by its first signature,
-       and the many later ones then compare without an atomic on a hot line */
-    uint32_t v = ht[slot];                          /* stale only as EMPTY: the CAS then reads it */
-    if (v == KC_EMPTY) {
-      v = atomicCAS(&ht[slot], KC_EMPTY, i);
-      if (v == KC_EMPTY) break;                     /* claimed: i represents its key */
-    }
-    uint32_t b[8];
-    load32(b, arena + sigs[v].pub_off);
-    uint32_t diff = 0;
+  bool is_rep = false;
+  if (i < n_sig) {
+    uint32_t a[8];
+    load32(a, arena + sigs[i].pub_off);
+    uint32_t slot = kc_hash(a, seed) & ht_mask, rep = i;
+    for (uint32_t p = 0; p < KC_PROBES; p++, slot = (slot + 1u) & ht_mask) {
+      /* a plain load first: a signer's slot is taken by its first signature,
+         and the many later ones then compare without an atomic on a hot line */
+      uint32_t v = ht[slot];                        /* stale only as EMPTY: the CAS then reads it */
+      if (v == KC_EMPTY) {
+        v = atomicCAS(&ht[slot], KC_EMPTY, i);
+        if (v == KC_EMPTY) break;                   /* claimed: i represents its key */
+      }
+      uint32_t b[8];
+      load32(b, arena + sigs[v].pub_off);
+      uint32_t diff = 0;
 #pragma unroll
-    for (int j = 0; j < 8; j++) diff |= a[j] ^ b[j];
-    if (!diff) { rep = v; break; }
+      for (int j = 0; j < 8; j++) diff |= a[j] ^ b[j];
+      if (!diff) { rep = v; break; }
+    }
+    key_of[i] = rep;
+    is_rep = rep == i;
   }
-  key_of[i] = rep;
-  const uint64_t m = __ballot(rep == i);
-  if (m) {
-    const int lane = (int)(threadIdx.x & 63u), leader = __ffsll((long long)m) - 1;
-    uint32_t base = 0;
-    if (lane == leader) base = atomicAdd(rep_cnt, (uint32_t)__popcll(m));
-    base = (uint32_t)__shfl((int)base, leader, 64);
-    if (rep == i) reps[base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull))] = i;
-  }
+  /* append the representatives: wave offsets in LDS, one global atomic per
+     workgroup (a single counter takes every one of them) */
+  __shared__ uint32_t s_cnt, s_base;
+  if (threadIdx.x == 0) s_cnt = 0;
+  __syncthreads();
+  const uint64_t m = __ballot(is_rep);
+  const int lane = (int)(threadIdx.x & 63u);
+  uint32_t wbase = 0;
+  if (m && lane == __ffsll((long long)m) - 1) wbase = atomicAdd(&s_cnt, (uint32_t)__popcll(m));
+  if (m) wbase = (uint32_t)__shfl((int)wbase, __ffsll((long long)m) - 1, 64);
+  __syncthreads();
+  if (threadIdx.x == 0) s_base = s_cnt ? atomicAdd(rep_cnt, s_cnt) : 0u;
+  __syncthreads();
+  if (is_rep) reps[s_base + wbase + (uint32_t)__popcll(m & ((1ull << lane) - 1ull))] = i;
 }
 
 /* One lane per representative: decode A, small-order test, -A table into the
