@@ -992,18 +992,17 @@ fdgpu_verify_hs_kernel(const uint8_t *__restrict__ arena, const fdgpu_sig_desc_t
 /* ---------------- key cache (FDGPU_FLAG_KCACHE) ----------------
    Signers repeat within a batch (a vote account signs every slot).  Each
    distinct public key is decoded and its -A table built once, in the
-   workspace of one representative lane; the verify kernel's other lanes with
-   that key copy the table (1440 B) instead of decompressing A (a 2^252-3
-   exponentiation) and building it.  Results are unchanged: the decode is a
-   function of the 32 key bytes only.
+   workspace of one representative lane; the verify and fallback kernels'
+   other lanes with that key read that table in place instead of
+   decompressing A (a 2^252-3 exponentiation) and building their own.
+   Results are unchanged: the decode is a function of the 32 key bytes only.
 
    fdgpu_key_dedup_kernel: an open-addressing table of signature indices,
    keyed by a seeded hash of all 32 key bytes.  A lane claims an empty slot
    with atomicCAS (after a plain load saw it empty), or compares its key with
    the bytes of the index a slot already holds (the arena is immutable, so
-   nothing waits on another lane);
-   after KC_PROBES probes it stays its own representative, which bounds the
-   work whatever keys a batch carries.  key_of[i] = representative of i;
+   nothing waits on another lane).  After KC_PROBES probes it stays its own
+   representative, which bounds the work whatever keys a batch carries.  key_of[i] = representative of i;
    the representatives are appended to reps (compact, so the table kernel
    runs dense waves however they are scattered over the batch). */
 #define KC_PROBES 32u
