@@ -12,6 +12,9 @@
        through LDS by LDS-DMA; the projective check against -[w]B.
    fdgpu_full_kernel       the rare lanes whose split failed: the full-length
        [S]B + [k](-A) chain, compared with the decoded R.
+   fdgpu_key_dedup_kernel, fdgpu_key_table_kernel  (FDGPU_FLAG_KCACHE) one A
+       decode + table per distinct public key, read in place by
+       fdgpu_verify_hs_kernel<true> and the fallback kernel.
    fdgpu_verify_ra_kernel, fdgpu_tail_kernel, fdgpu_finish_kernel
                            (FDGPU_HALFSIZE=0) the round-1 R-avoiding path:
        full-length k, R' compared with R's encoding through one batched
