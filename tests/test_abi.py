@@ -85,3 +85,13 @@ def test_product_does_not_reference_oracle():
                     assert bad not in text, (f, bad)
     out = subprocess.run(["ldd", _lib.LIB_PATH], capture_output=True, text=True).stdout
     assert "oracle" not in out
+
+
+def test_engine_flags_match_header():
+    """The Python engine flags are the header's FDGPU_FLAG_* values."""
+    from firedancer_amd import ed25519 as ed
+    text = open(_lib.HEADER_PATH).read()
+    hdr = {m.group(1): int(m.group(2)) for m in re.finditer(r"#define\s+FDGPU_FLAG_(\w+)\s+(\d+)u", text)}
+    py = {"REF_MAPPING": ed.FLAG_REF_MAPPING, "NO_BUCKET": ed.FLAG_NO_BUCKET, "FULL_PATH": ed.FLAG_FULL_PATH,
+          "KEY_CACHE": ed.FLAG_KEY_CACHE}
+    assert hdr == py, (hdr, py)
