@@ -217,6 +217,53 @@ def latency_and_pcie(eng, arena, txns, batch, nbatches):
             float(np.percentile(lat_reg, 50)), float(np.percentile(lat_reg, 99)))
 
 
+def sync_latency(arena, txns, calls=1000, threads=64):
+    """The synchronous drop-in API (fd_ed25519_verify through the C ABI,
+    fd_ed25519.h:96-101): p50/p99 of `calls` sequential calls on one thread
+    (one GPU round trip each), then `threads` threads calling concurrently
+    (the engine coalesces concurrent calls into one batch per round trip)."""
+    import threading
+    from firedancer_amd import _lib, ed25519
+    L = _lib.lib()
+    recs = []
+    for t in txns[:max(calls, threads * 16)]:
+        m = arena[int(t["msg_off"]):int(t["msg_off"]) + int(t["msg_sz"])].tobytes()
+        recs.append((m, arena[int(t["sig_off"]):int(t["sig_off"]) + 64].tobytes(),
+                     arena[int(t["pub_off"]):int(t["pub_off"]) + 32].tobytes()))
+    for m, sg, pb in recs[:50]:                                        # warm-up (engine open)
+        L.fd_ed25519_verify(m, len(m), sg, pb, None)
+    lat = []
+    for m, sg, pb in recs[:calls]:
+        t0 = time.perf_counter()
+        L.fd_ed25519_verify(m, len(m), sg, pb, None)
+        lat.append((time.perf_counter() - t0) * 1e6)
+    per = len(recs) // threads
+    before = ed25519.sync_stats()
+
+    def worker(k):
+        for m, sg, pb in recs[k * per:(k + 1) * per]:
+            L.fd_ed25519_verify(m, len(m), sg, pb, None)
+    ths = [threading.Thread(target=worker, args=(k,)) for k in range(threads)]
+    t0 = time.perf_counter()
+    for th in ths:
+        th.start()
+    for th in ths:
+        th.join()
+    dt = time.perf_counter() - t0
+    after = ed25519.sync_stats()
+    lat = np.array(lat)
+    n_conc = after["calls"] - before["calls"]
+    return {"sync_call_latency_us_p50": round(float(np.percentile(lat, 50)), 1),
+            "sync_call_latency_us_p99": round(float(np.percentile(lat, 99)), 1),
+            "sync_calls": calls,
+            "sync_concurrent_threads": threads,
+            "sync_concurrent_calls_per_s": round(n_conc / dt, 1),
+            "sync_concurrent_calls_per_batch": round(n_conc / max(1, after["batches"] - before["batches"]), 2),
+            "sync_errors": after["errors"],
+            "sync_note": "fd_ed25519_verify via ctypes, cfg1 single-signature txns; sequential: one GPU round "
+                         "trip per call; concurrent: calls coalesced into shared batches (group commit)"}
+
+
 def tile_lines(eng, arena, txns, modes, cpus):
     """BASELINE configs[4] (cfg5) on this rank's GPU: the verify tile
     (fdgpu_vtile: tango in -> parse -> batched GPU verify -> tcache -> tango
@@ -324,9 +371,11 @@ def cpu_model():
 
 def cpu_baseline(arena, txns, sample, cpus):
     """The oracle (C restatement) on one pinned thread per physical core of
-    this host (at most the GPU box's 16-CPU share), inputs statically
+    this host (at most the GPU box's CPU share,
+    workload.cpu_share_evidence), inputs statically
     partitioned.  Returns (baseline record, the CPU codes of the sample)."""
     from oracle import oracle as orc
+    from firedancer_amd import workload
     sub = txns[:sample]
     t0 = time.perf_counter()
     codes = orc.verify_txns(arena, sub, cpus=cpus)
@@ -337,7 +386,8 @@ def cpu_baseline(arena, txns, sample, cpus):
            "sample": f"first {len(sub)} txns of the rank-0 cfg1 batch, oracle/fd_ed25519_oracle.c "
                      f"(C restatement, radix-2^51, wNAF), one pinned thread per physical core on "
                      f"{len(cpus)} cores (the box's CPU share), {dt:.2f} s wall",
-           "published_ref_per_core": "20-40K sigs/s/core (Icelake, book/guide/tuning.md:75) -- published, not measured"}
+           "published_ref_per_core": "20-40K sigs/s/core (Icelake, book/guide/tuning.md:75) -- published, not measured",
+           "cpu_share": workload.cpu_share_evidence()}
     return rec, codes
 
 
@@ -492,6 +542,8 @@ def main():
                   "latency_batch_txns": args.latency_batch,
                   "pcie_inclusive_sigs_per_s_per_gpu": round(pcie, 1),
                   "pcie_inclusive_registered_sigs_per_s_per_gpu": round(pcie_reg, 1)}
+        if dist.rank == 0:
+            extras.update(sync_latency(arena, txns))
         if args.tile:
             tl = tile_lines(eng, arena, txns, modes, cpus)
             tl["tile_backlog_txns_per_s_node"] = round(dist.sum(tl["tile_backlog_txns_per_s"]), 1)

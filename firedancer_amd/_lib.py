@@ -108,6 +108,14 @@ def lib():
     L.fdgpu_dev_batch_time.restype = c.c_int
     L.fdgpu_sync.argtypes = [vp]
     L.fdgpu_sync.restype = c.c_int
+    L.fdgpu_ed25519_verify.argtypes = [u8p, c.c_uint64, u8p, u8p]
+    L.fdgpu_ed25519_verify.restype = c.c_int
+    L.fdgpu_ed25519_verify_batch_single_msg.argtypes = [u8p, c.c_uint64, u8p, u8p, c.c_uint8]
+    L.fdgpu_ed25519_verify_batch_single_msg.restype = c.c_int
+    L.fdgpu_sync_stats.argtypes = [c.POINTER(c.c_uint64)] * 3
+    L.fdgpu_sync_stats.restype = None
+    L.fdgpu_sync_errors.argtypes = []
+    L.fdgpu_sync_errors.restype = c.c_uint64
     for fn in ("fdgpu_debug_fe_ops", "fdgpu_debug_decode", "fdgpu_debug_sha512", "fdgpu_debug_hram",
                "fdgpu_debug_sc_reduce", "fdgpu_debug_hs_split", "fdgpu_debug_sig_codes"):
         getattr(L, fn).restype = c.c_int

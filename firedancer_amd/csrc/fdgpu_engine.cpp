@@ -15,12 +15,15 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
+#include <condition_variable>
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <map>
 #include <mutex>
+#include <random>
 #include <string>
 #include <thread>
 #include <vector>
@@ -49,7 +52,8 @@ struct Slot {
   uint32_t *h_perm = nullptr, *d_perm = nullptr;   /* block-count grouping: descriptor i -> signature perm[i] */
   fdgpu_txn_desc_t *h_txns = nullptr, *d_txns = nullptr;
   int8_t *h_codes = nullptr, *d_txn_codes = nullptr, *d_sig_codes = nullptr;
-  uint32_t *d_ws = nullptr;   /* this slot's workspace: slots run concurrently on their own streams */
+  uint32_t *d_ws = nullptr;   /* this slot's workspace: slots run concurrently on their own streams; */
+  uint64_t ws_sig = 0;        /* sized on demand to the largest batch the slot has carried */
   int64_t ticket = -1;      /* -1: free */
   bool staged = false;      /* reserved by fdgpu_stage_acquire, not yet submitted */
   bool held = false;        /* polled with fdgpu_poll_keep, awaiting fdgpu_release */
@@ -59,6 +63,7 @@ struct Slot {
      non-blocking poll is one host load instead of a runtime event query */
   uint32_t *h_flag = nullptr, *d_flag = nullptr;
   uint32_t flag_seq = 0;
+  uint32_t polls = 0;         /* non-blocking polls of the current batch (stream error checks) */
 };
 
 }  // namespace
@@ -71,7 +76,8 @@ struct fdgpu_engine {
   uint32_t *d_ws = nullptr;          /* per-lane A-table workspace, fdgpu_ws_bytes(ws_sig) */
   size_t ws_bytes = 0;
   uint64_t ws_sig = 0;
-  uint32_t resident_blocks = 0;     /* occupancy x CUs, for reporting */
+  uint32_t resident_blocks = 0;     /* verify-kernel occupancy x CUs (fallback grid cap, reporting) */
+  uint64_t kc_seed = 0;             /* key cache hash seed, drawn at open */
   std::vector<Slot> slots;
   int64_t next_ticket = 0;
   int8_t *d_scratch_codes = nullptr;   /* for fdgpu_verify_device with d_sig_codes == NULL */
@@ -81,7 +87,13 @@ struct fdgpu_engine {
      host threads (verify tiles sharing the node's engines) */
   std::mutex ring_mu;
   bool flag_poll = false;            /* slots signal completion through h_flag (probed at open) */
-  std::vector<std::pair<uintptr_t, uint64_t>> regions;   /* fdgpu_host_register'ed [p, p + sz) */
+  /* fdgpu_host_register calls of this engine, one entry each (a range
+     registered twice holds two references): the page-aligned start the
+     caller named, and the pinned region [base, end) that covers it */
+  struct Reg { uintptr_t user, base, end; };
+  std::vector<Reg> regions;
+  bool drop_flag = false;            /* test hook (FDGPU_DEBUG_DROP_FLAG=1): the stream never writes the
+                                        completion word, so polls must finish through the event */
 };
 
 namespace {
@@ -124,10 +136,31 @@ bool slot_alloc(Slot &s, const fdgpu_cfg_t &c) {
   HIPCHK(hipMalloc((void **)&s.d_txns, c.max_txn * sizeof(fdgpu_txn_desc_t) + 16), false);
   HIPCHK(hipMalloc((void **)&s.d_txn_codes, c.max_txn + 16), false);
   HIPCHK(hipMalloc((void **)&s.d_sig_codes, c.max_sig + 16), false);
-  HIPCHK(hipMalloc((void **)&s.d_ws, fdgpu_ws_bytes(c.max_sig ? c.max_sig : 1)), false);
   HIPCHK(hipHostMalloc((void **)&s.h_flag, 64, hipHostMallocDefault), false);   /* own cache line */
   *s.h_flag = 0;
   HIPCHK(hipHostGetDevicePointer((void **)&s.d_flag, s.h_flag, 0), false);
+  return true;
+}
+
+/* Grow the slot's workspace to cover n_sig signatures (the slot is free, so
+   nothing of its stream still reads the old one).  Grown by half again each
+   time, so a default engine (65,536 txns, up to 12 signatures each) holds
+   what its batches actually carry, not 12 x 3.2 KB per txn up front. */
+bool slot_ws(Slot &s, uint64_t n_sig) {
+  if (s.d_ws && n_sig <= s.ws_sig) return true;
+  const uint64_t want = std::max<uint64_t>(n_sig, s.ws_sig + s.ws_sig / 2);
+  if (s.d_ws) { HIPCHK(hipStreamSynchronize(s.stream), false); (void)hipFree(s.d_ws); s.d_ws = nullptr; s.ws_sig = 0; }
+  if (hipMalloc((void **)&s.d_ws, fdgpu_ws_bytes(want ? want : 1)) != hipSuccess) {
+    if (want == n_sig || hipMalloc((void **)&s.d_ws, fdgpu_ws_bytes(n_sig ? n_sig : 1)) != hipSuccess) {
+      (void)hipGetLastError();
+      s.d_ws = nullptr;
+      set_err("slot workspace alloc (%llu signatures)", (unsigned long long)n_sig);
+      return false;
+    }
+    s.ws_sig = n_sig ? n_sig : 1;
+    return true;
+  }
+  s.ws_sig = want ? want : 1;
   return true;
 }
 
@@ -234,22 +267,25 @@ void btab_release(int device, uint32_t *p) {
   if (it == g_btab.end() || it->second.first != p) return;
   if (--it->second.second == 0) { (void)hipFree(p); g_btab.erase(it); }
 }
-std::map<uintptr_t, std::pair<uint64_t, int>> g_regions;   /* page-aligned base -> (bytes, engines) */
+/* pinned host regions: page-aligned base -> (end, references over every
+   engine's registrations) */
+std::map<uintptr_t, std::pair<uintptr_t, int>> g_regions;
 
 bool region_covers(const fdgpu_engine *e, const uint8_t *p, uint64_t sz) {
   const uintptr_t a = (uintptr_t)p;
   for (const auto &r : e->regions)
-    if (a >= r.first && a + sz <= r.first + r.second) return true;
+    if (a >= r.base && a + sz <= r.end) return true;
   return false;
 }
 
-void unregister_one(fdgpu_engine *e, uintptr_t a) {
+/* drop one reference to the pinned region at base */
+void region_release(int device, uintptr_t base) {
   std::lock_guard<std::mutex> rk(g_reg_mu);
-  auto it = g_regions.find(a);
+  auto it = g_regions.find(base);
   if (it == g_regions.end()) return;
   if (--it->second.second == 0) {
-    (void)hipSetDevice(e->device);
-    (void)hipHostUnregister((void *)a);
+    (void)hipSetDevice(device);
+    (void)hipHostUnregister((void *)base);
     g_regions.erase(it);
   }
 }
@@ -295,14 +331,18 @@ fdgpu_engine_t *fdgpu_engine_open(int device, fdgpu_cfg_t const *cfg_in) {
   if (fdgpu_verify_occupancy(&bpcu) != hipSuccess || bpcu < 1) bpcu = 1;
   if (hipGetDeviceProperties(&prop, device) != hipSuccess) { set_err("props"); return fail(); }
   e->resident_blocks = (uint32_t)(bpcu * prop.multiProcessorCount);
-  if (ensure_ws(e, cfg.max_sig) != FDGPU_OK) return fail();
+  {
+    std::random_device rd;                     /* per-engine key-cache seed: crafted keys cannot target it */
+    e->kc_seed = (((uint64_t)rd() << 32) | rd()) | 1u;
+  }
   e->slots.resize(cfg.ring_depth);
   for (auto &s : e->slots) if (!slot_alloc(s, cfg)) return fail();
   if (hipStreamSynchronize(e->compute) != hipSuccess) { set_err("btab init failed"); return fail(); }
   /* completion words: probe that a stream write reaches pinned host memory
      (FDGPU_POLL_EVENT=1 keeps hipEventQuery polling) */
   {
-    const char *pe = getenv("FDGPU_POLL_EVENT");
+    const char *pe = getenv("FDGPU_POLL_EVENT"), *df = getenv("FDGPU_DEBUG_DROP_FLAG");
+    e->drop_flag = df && df[0] == '1';
     Slot &s0 = e->slots[0];
     if (!(pe && pe[0] == '1') && hipStreamWriteValue32(s0.stream, s0.d_flag, 0x5a5a5a5au, 0) == hipSuccess &&
         hipStreamSynchronize(s0.stream) == hipSuccess)
@@ -318,7 +358,7 @@ void fdgpu_engine_close(fdgpu_engine_t *e) {
   (void)hipSetDevice(e->device);
   if (e->compute) (void)hipStreamSynchronize(e->compute);
   for (auto &s : e->slots) { if (s.stream) (void)hipStreamSynchronize(s.stream); slot_free(s); }
-  for (auto &r : e->regions) unregister_one(e, r.first);
+  for (auto &r : e->regions) region_release(e->device, r.base);
   for (auto st : e->batch_streams) (void)hipStreamSynchronize(st);   /* btab is read there */
   if (e->d_btab) btab_release(e->device, e->d_btab);
   if (e->d_ws) (void)hipFree(e->d_ws);
@@ -348,7 +388,7 @@ static int enqueue_verify(fdgpu_engine_t *e, const uint8_t *d_arena, const fdgpu
     if (rc) return rc;
   }
   HIPCHK(fdgpu_launch_verify_sigs(d_arena, d_sigs, (uint32_t)n_sig, d_perm, e->d_btab, ws ? ws : e->d_ws, d_sig_codes,
-                                  flags, st),
+                                  flags, st, nullptr, e->resident_blocks, e->kc_seed),
          FDGPU_ERR_DEVICE);
   HIPCHK(fdgpu_launch_combine(d_txns, (uint32_t)n_txn, d_sig_codes, d_txn_codes, nullptr, st), FDGPU_ERR_DEVICE);
   return FDGPU_OK;
@@ -365,6 +405,7 @@ static int64_t submit_slot(fdgpu_engine_t *e, Slot *s, uint64_t arena_sz, fdgpu_
   uint32_t *perm = bucket(e) ? s->h_perm : nullptr;
   const int64_t ns = expand(arena_sz, txns, txn_cnt, e->cfg.max_sig, s->h_sigs, s->h_txns, perm);
   if (ns < 0) return FDGPU_ERR_INVAL;
+  if (!slot_ws(*s, (uint64_t)ns)) return FDGPU_ERR_DEVICE;
   if (src) {
     if (arena_sz) HIPCHK(hipMemcpyAsync(s->d_arena, src, arena_sz, hipMemcpyHostToDevice, s->stream), FDGPU_ERR_DEVICE);
     HIPCHK(hipMemsetAsync(s->d_arena + arena_sz, 0, FDGPU_ARENA_SLACK, s->stream), FDGPU_ERR_DEVICE);
@@ -385,10 +426,12 @@ static int64_t submit_slot(fdgpu_engine_t *e, Slot *s, uint64_t arena_sz, fdgpu_
                           s->d_sig_codes, s->d_txn_codes, s->stream, s->d_ws);
   if (rc) return rc;
   if (txn_cnt) HIPCHK(hipMemcpyAsync(s->h_codes, s->d_txn_codes, txn_cnt, hipMemcpyDeviceToHost, s->stream), FDGPU_ERR_DEVICE);
-  if (e->flag_poll) HIPCHK(hipStreamWriteValue32(s->stream, s->d_flag, ++s->flag_seq, 0), FDGPU_ERR_DEVICE);
+  ++s->flag_seq;
+  if (e->flag_poll && !e->drop_flag) HIPCHK(hipStreamWriteValue32(s->stream, s->d_flag, s->flag_seq, 0), FDGPU_ERR_DEVICE);
   HIPCHK(hipEventRecord(s->done, s->stream), FDGPU_ERR_DEVICE);
   s->staged = false;
   s->held = false;
+  s->polls = 0;
   s->ticket = e->next_ticket++;
   s->txn_cnt = txn_cnt;
   return s->ticket;
@@ -484,8 +527,17 @@ static int poll_slot(fdgpu_engine_t *e, int64_t ticket, int8_t *txn_codes, int b
     HIPCHK(hipEventSynchronize(s->done), FDGPU_ERR_DEVICE);
     lk.lock();
   } else if (e->flag_poll) {
-    /* the stream wrote flag_seq after the codes' read-back completed */
-    if (__atomic_load_n(s->h_flag, __ATOMIC_ACQUIRE) != s->flag_seq) return FDGPU_PENDING;
+    /* the stream wrote flag_seq after the codes' read-back completed.  A
+       stream that failed never writes it, so every 64th unanswered poll asks
+       the runtime: an error ends the wait (the tile stops instead of polling
+       forever), a completed event means the batch is done. */
+    if (__atomic_load_n(s->h_flag, __ATOMIC_ACQUIRE) != s->flag_seq) {
+      if ((++s->polls & 63u) != 0) return FDGPU_PENDING;
+      HIPCHK(hipSetDevice(e->device), FDGPU_ERR_DEVICE);
+      const hipError_t q = hipEventQuery(s->done);
+      if (q == hipErrorNotReady) return FDGPU_PENDING;
+      HIPCHK(q, FDGPU_ERR_DEVICE);
+    }
   } else {
     HIPCHK(hipSetDevice(e->device), FDGPU_ERR_DEVICE);
     hipError_t q = hipEventQuery(s->done);
@@ -526,19 +578,24 @@ int fdgpu_host_register(fdgpu_engine_t *e, void *p, uint64_t sz) {
   if (!e || !p || !sz) { set_err("null argument"); return FDGPU_ERR_INVAL; }
   const uintptr_t a = (uintptr_t)p & ~(uintptr_t)4095, b = ((uintptr_t)p + sz + 4095) & ~(uintptr_t)4095;
   std::lock_guard<std::mutex> lk(e->ring_mu);
-  if (region_covers(e, (const uint8_t *)p, sz)) return FDGPU_OK;
   std::lock_guard<std::mutex> rk(g_reg_mu);
-  auto it = g_regions.find(a);
-  if (it != g_regions.end() && it->second.first >= b - a) {
-    it->second.second++;
-  } else {
-    if (it != g_regions.end()) { set_err("region overlaps a smaller registered one"); return FDGPU_ERR_INVAL; }
+  /* a range inside a region already pinned (by any engine) shares it;
+     a range that only partly overlaps one cannot be pinned */
+  auto it = g_regions.upper_bound(a);
+  uintptr_t base = 0, end = 0;
+  if (it != g_regions.begin()) {
+    auto pv = std::prev(it);
+    if (pv->first <= a && pv->second.first >= b) { base = pv->first; end = pv->second.first; pv->second.second++; }
+    else if (pv->second.first > a) { set_err("range partly overlaps a registered region"); return FDGPU_ERR_INVAL; }
+  }
+  if (!base) {
+    if (it != g_regions.end() && it->first < b) { set_err("range partly overlaps a registered region"); return FDGPU_ERR_INVAL; }
     HIPCHK(hipSetDevice(e->device), FDGPU_ERR_DEVICE);
     HIPCHK(hipHostRegister((void *)a, b - a, hipHostRegisterPortable), FDGPU_ERR_DEVICE);
-    g_regions[a] = {b - a, 1};
-    it = g_regions.find(a);
+    g_regions[a] = {b, 1};
+    base = a; end = b;
   }
-  e->regions.push_back({a, it->second.first});
+  e->regions.push_back({a, base, end});
   return FDGPU_OK;
 }
 
@@ -546,10 +603,10 @@ int fdgpu_host_unregister(fdgpu_engine_t *e, void *p) {
   if (!e || !p) return FDGPU_ERR_INVAL;
   const uintptr_t a = (uintptr_t)p & ~(uintptr_t)4095;
   std::lock_guard<std::mutex> lk(e->ring_mu);
-  for (size_t i = 0; i < e->regions.size(); i++) {
-    if (e->regions[i].first != a) continue;
+  for (size_t i = e->regions.size(); i-- > 0;) {            /* the latest registration of this range */
+    if (e->regions[i].user != a) continue;
     for (auto &sl : e->slots) if (sl.stream) (void)hipStreamSynchronize(sl.stream);   /* no DMA still reads it */
-    unregister_one(e, a);
+    region_release(e->device, e->regions[i].base);
     e->regions.erase(e->regions.begin() + (long)i);
     return FDGPU_OK;
   }
@@ -712,7 +769,6 @@ fdgpu_dev_batch_t *fdgpu_dev_batch_upload(fdgpu_engine_t *e, uint8_t const *aren
 fdgpu_dev_batch_t *fdgpu_dev_batch_upload_frags(fdgpu_engine_t *e, uint8_t const *arena, uint64_t arena_sz,
                                                 fdgpu_frag_t const *frags, uint64_t frag_cnt) {
   if (!e || (!arena && arena_sz) || (!frags && frag_cnt)) { set_err("null argument"); return nullptr; }
-  if (!FDGPU_HALFSIZE) { set_err("frag batches need the half-size build"); return nullptr; }
   if (arena_sz > 0xFFFFFFF0ull || frag_cnt > 0x0FFFFFFFull) { set_err("batch exceeds 32-bit offsets"); return nullptr; }
   uint64_t bound = 0;
   for (uint64_t t = 0; t < frag_cnt; t++) {
@@ -775,7 +831,7 @@ int fdgpu_dev_batch_verify(fdgpu_engine_t *e, fdgpu_dev_batch_t *b) {
   int rc = enqueue_ingest(b, st);
   if (rc) return rc;
   HIPCHK(fdgpu_launch_verify_sigs(b->d_arena, b->d_sigs, (uint32_t)b->n_sig_bound, nullptr, e->d_btab, batch_ws(e, b),
-                                  b->d_sig_codes, kflags(e), st, b->d_n_sig),
+                                  b->d_sig_codes, kflags(e), st, b->d_n_sig, e->resident_blocks, e->kc_seed),
          FDGPU_ERR_DEVICE);
   HIPCHK(fdgpu_launch_combine(b->d_txns, (uint32_t)b->n_txn, b->d_sig_codes, b->d_txn_codes, nullptr, st),
          FDGPU_ERR_DEVICE);
@@ -827,7 +883,8 @@ int fdgpu_dev_batch_time2(fdgpu_engine_t *e, fdgpu_dev_batch_t *b, int iters, do
     if (b->frags && rc == FDGPU_OK) rc = enqueue_ingest(b, st);
     if (hipEventRecord(ev[4 * i + 1], st) != hipSuccess) rc = FDGPU_ERR_DEVICE;
     if (fdgpu_launch_verify_sigs(b->d_arena, b->d_sigs, (uint32_t)nsig, b->d_perm, e->d_btab, batch_ws(e, b),
-                                 b->d_sig_codes, flags, st, b->frags ? b->d_n_sig : nullptr) != hipSuccess)
+                                 b->d_sig_codes, flags, st, b->frags ? b->d_n_sig : nullptr, e->resident_blocks,
+                                 e->kc_seed) != hipSuccess)
       rc = FDGPU_ERR_DEVICE;
     if (hipEventRecord(ev[4 * i + 2], st) != hipSuccess) rc = FDGPU_ERR_DEVICE;
     if (fdgpu_launch_combine(b->d_txns, (uint32_t)b->n_txn, b->d_sig_codes, b->d_txn_codes, nullptr, st) != hipSuccess)
@@ -877,54 +934,135 @@ int fdgpu_sync(fdgpu_engine_t *e) {
 
 /* ------------------------------------------------------------ sync API */
 
-/* Compatibility shim for the reference's synchronous per-call API: one
-   process-wide engine on device 0, one GPU round trip per call, serialised
-   on a lock.  The batch API is the throughput path; hot callers (the verify
-   tile, replay, FEC roots) use it.  The caller's current HIP device is saved
-   and restored.  The reference API has no error channel besides the verify
-   codes, so an engine failure (no device, a HIP error) aborts the process
-   (documented in fd_ed25519_gpu.h): answering ERR_SIG for a signature that
-   was never checked would silently drop valid traffic. */
-static std::mutex g_sync_mu;
-static fdgpu_engine_t *g_sync_engine = nullptr;
+/* The reference's synchronous per-call API (fd_ed25519.h:96-101,124-130) on
+   one process-wide engine on device 0.  A call is one GPU round trip: about
+   a millisecond, the lifetime of the verify kernel's single wave, not the
+   CPU's ~30 us (bench.py `sync_*` lines).
 
-[[noreturn]] static void sync_fatal(const char *what) {
-  fprintf(stderr, "fd_ed25519_gpu: %s: %s\n", what, fdgpu_last_error());
-  abort();   /* no silent CPU fallback, no unchecked verdict */
+   Calls from concurrent threads are coalesced (group commit): a caller that
+   finds no batch in flight becomes the leader, takes every call queued so
+   far as one batch (one txn per call) and verifies it; calls arriving
+   meanwhile queue for the next leader.  A lone caller pays one round trip,
+   N concurrent callers share theirs, so throughput grows with the number of
+   callers instead of serialising on a lock.  The caller's current HIP device
+   is saved and restored.
+
+   The reference API has no error channel besides the verify codes.  On an
+   engine failure (no device, a HIP error) every call of the failed batch
+   returns FD_ED25519_ERR_SIG -- fail closed: nothing unchecked is accepted --
+   and fdgpu_sync_errors() counts the event (fdgpu_last_error() of the
+   failing thread says why).  FDGPU_SYNC_ABORT=1 in the environment aborts
+   the process instead. */
+}  // extern "C"
+
+namespace {
+
+struct SyncReq {
+  const uint8_t *msg, *sigs, *pubs;
+  uint64_t msg_sz;
+  uint32_t n;
+  int code = 0;
+  bool done = false;
+};
+
+struct SyncState {
+  std::mutex mu;
+  std::condition_variable cv;
+  std::vector<SyncReq *> pending;
+  bool leader = false;
+  fdgpu_engine_t *eng = nullptr;
+  std::vector<uint8_t> arena;
+  std::vector<fdgpu_txn_t> txns;
+  std::vector<int8_t> codes;
+  std::atomic<uint64_t> errors{0}, calls{0}, batches{0};
+};
+
+SyncState &sync_state() {
+  /* leaked on purpose: no destructor runs at exit, after the HIP runtime may
+     already be gone, or while a caller thread still waits */
+  static SyncState *st = new SyncState;
+  return *st;
 }
 
-static fdgpu_engine_t *sync_engine(uint64_t need) {
-  if (g_sync_engine && need <= g_sync_engine->cfg.max_arena) return g_sync_engine;
-  /* first use, or a message longer than the engine's arena: (re)open */
-  if (g_sync_engine) fdgpu_engine_close(g_sync_engine);
-  fdgpu_cfg_t cfg{};
-  cfg.max_txn = 1; cfg.max_sig = 16; cfg.ring_depth = 1;
-  cfg.max_arena = std::max<uint64_t>(64 * 16 + 32 * 16 + 65536, need * 2);
-  g_sync_engine = fdgpu_engine_open(0, &cfg);
-  if (!g_sync_engine) sync_fatal("cannot open the GPU engine");
-  return g_sync_engine;
+constexpr uint64_t SYNC_BATCH_MAX = 4096;    /* calls per coalesced batch */
+
+void sync_failed(SyncState &st, const char *what) {
+  st.errors.fetch_add(1, std::memory_order_relaxed);
+  const char *ab = getenv("FDGPU_SYNC_ABORT");
+  if (ab && ab[0] == '1') {
+    fprintf(stderr, "fd_ed25519_gpu: %s: %s\n", what, fdgpu_last_error());
+    abort();
+  }
 }
 
-static int sync_verify(const uint8_t *msg, uint64_t msg_sz, const uint8_t *sigs, const uint8_t *pubs, uint32_t n) {
-  if (n == 0 || n > 16) return FD_ED25519_ERR_SIG;
-  std::lock_guard<std::mutex> lk(g_sync_mu);
-  int prev_dev = -1;
-  if (hipGetDevice(&prev_dev) != hipSuccess) prev_dev = -1;
-  const uint64_t need = 64ull * n + 32ull * n + msg_sz;
-  fdgpu_engine_t *e = sync_engine(need);
-  std::vector<uint8_t> arena(need);
-  memcpy(arena.data(), sigs, 64ull * n);
-  memcpy(arena.data() + 64ull * n, pubs, 32ull * n);
-  if (msg_sz) memcpy(arena.data() + 96ull * n, msg, msg_sz);
-  fdgpu_txn_t t;
-  t.sig_off = 0; t.pub_off = 64u * n; t.msg_off = 96u * n; t.msg_sz = (uint32_t)msg_sz; t.sig_cnt = n;
-  const int64_t tk = fdgpu_submit(e, arena.data(), need, &t, 1);
-  if (tk < 0) sync_fatal("submit failed");
-  int8_t code = 0;
-  if (fdgpu_poll(e, tk, &code, 1) != FDGPU_OK) sync_fatal("poll failed");
-  if (prev_dev >= 0) (void)hipSetDevice(prev_dev);
-  return code;
+/* the leader's batch: returns false on an engine failure */
+bool sync_run(SyncState &st, const std::vector<SyncReq *> &batch) {
+  uint64_t need = 0;
+  for (const SyncReq *r : batch) need += 96ull * r->n + r->msg_sz;
+  if (!st.eng || need > st.eng->cfg.max_arena) {
+    if (st.eng) fdgpu_engine_close(st.eng);
+    fdgpu_cfg_t cfg{};
+    cfg.max_txn = SYNC_BATCH_MAX; cfg.max_sig = SYNC_BATCH_MAX * 16; cfg.ring_depth = 1;
+    cfg.max_arena = std::max<uint64_t>(SYNC_BATCH_MAX * (96 * 16 + 1232), need * 2);
+    st.eng = fdgpu_engine_open(0, &cfg);
+    if (!st.eng) return false;
+  }
+  st.arena.resize(need);
+  st.txns.resize(batch.size());
+  st.codes.resize(batch.size());
+  uint64_t o = 0;
+  for (size_t k = 0; k < batch.size(); k++) {
+    const SyncReq &r = *batch[k];
+    fdgpu_txn_t &t = st.txns[k];
+    t.sig_off = (uint32_t)o; memcpy(st.arena.data() + o, r.sigs, 64ull * r.n); o += 64ull * r.n;
+    t.pub_off = (uint32_t)o; memcpy(st.arena.data() + o, r.pubs, 32ull * r.n); o += 32ull * r.n;
+    t.msg_off = (uint32_t)o; if (r.msg_sz) memcpy(st.arena.data() + o, r.msg, r.msg_sz); o += r.msg_sz;
+    t.msg_sz = (uint32_t)r.msg_sz; t.sig_cnt = r.n;
+  }
+  const int64_t tk = fdgpu_submit(st.eng, st.arena.data(), need, st.txns.data(), batch.size());
+  if (tk < 0) return false;
+  if (fdgpu_poll(st.eng, tk, st.codes.data(), 1) != FDGPU_OK) return false;
+  for (size_t k = 0; k < batch.size(); k++) batch[k]->code = st.codes[k];
+  return true;
 }
+
+int sync_verify(const uint8_t *msg, uint64_t msg_sz, const uint8_t *sigs, const uint8_t *pubs, uint32_t n) {
+  if (n == 0 || n > 16) return FD_ED25519_ERR_SIG;            /* fd_ed25519_user.c:238-241 */
+  if (msg_sz > 0xFFFF0000ull) return FD_ED25519_ERR_SIG;      /* beyond the engine's 32-bit offsets */
+  SyncState &st = sync_state();
+  st.calls.fetch_add(1, std::memory_order_relaxed);
+  SyncReq req{msg, sigs, pubs, msg_sz, n};
+  std::unique_lock<std::mutex> lk(st.mu);
+  st.pending.push_back(&req);
+  while (!req.done) {
+    if (st.leader) { st.cv.wait(lk); continue; }
+    st.leader = true;                          /* this thread verifies everything queued so far */
+    std::vector<SyncReq *> batch;
+    const size_t take = std::min<size_t>(st.pending.size(), SYNC_BATCH_MAX);
+    batch.assign(st.pending.begin(), st.pending.begin() + (long)take);
+    st.pending.erase(st.pending.begin(), st.pending.begin() + (long)take);
+    lk.unlock();
+    int prev_dev = -1;
+    if (hipGetDevice(&prev_dev) != hipSuccess) prev_dev = -1;
+    const bool ok = sync_run(st, batch);
+    if (prev_dev >= 0) (void)hipSetDevice(prev_dev);
+    if (!ok) {
+      sync_failed(st, "verify batch failed");
+      for (SyncReq *r : batch) r->code = FD_ED25519_ERR_SIG;   /* fail closed */
+      if (st.eng) { fdgpu_engine_close(st.eng); st.eng = nullptr; }   /* reopened by the next batch */
+    }
+    st.batches.fetch_add(1, std::memory_order_relaxed);
+    lk.lock();
+    for (SyncReq *r : batch) r->done = true;
+    st.leader = false;
+    st.cv.notify_all();
+  }
+  return req.code;
+}
+
+}  // namespace
+
+extern "C" {
 
 int fd_ed25519_verify(uint8_t const msg[], uint64_t msg_sz, uint8_t const sig[64], uint8_t const public_key[32],
                       fd_sha512_t *sha) {
@@ -937,6 +1075,24 @@ int fd_ed25519_verify_batch_single_msg(uint8_t const msg[], uint64_t const msg_s
   (void)shas;
   return sync_verify(msg, msg_sz, signatures, pubkeys, batch_sz);
 }
+
+int fdgpu_ed25519_verify(uint8_t const msg[], uint64_t msg_sz, uint8_t const sig[64], uint8_t const public_key[32]) {
+  return sync_verify(msg, msg_sz, sig, public_key, 1);
+}
+
+int fdgpu_ed25519_verify_batch_single_msg(uint8_t const msg[], uint64_t msg_sz, uint8_t const signatures[64],
+                                          uint8_t const pubkeys[32], uint8_t batch_sz) {
+  return sync_verify(msg, msg_sz, signatures, pubkeys, batch_sz);
+}
+
+void fdgpu_sync_stats(uint64_t *calls, uint64_t *batches, uint64_t *errors) {
+  SyncState &st = sync_state();
+  if (calls) *calls = st.calls.load(std::memory_order_relaxed);
+  if (batches) *batches = st.batches.load(std::memory_order_relaxed);
+  if (errors) *errors = st.errors.load(std::memory_order_relaxed);
+}
+
+uint64_t fdgpu_sync_errors(void) { return sync_state().errors.load(std::memory_order_relaxed); }
 
 char const *fd_ed25519_strerror(int err) {
   switch (err) {
@@ -1079,7 +1235,7 @@ int fdgpu_debug_sig_codes(fdgpu_engine_t *e, uint8_t const *arena, uint64_t aren
   if ((uint64_t)ns > e->ws_sig) { int rc = ensure_ws(e, (uint64_t)ns); if (rc) return rc; }
   HIPCHK(fdgpu_launch_verify_sigs((uint8_t *)da.p, (fdgpu_sig_desc_t *)dd.p, (uint32_t)ns,
                                   perm ? (uint32_t *)dp.p : nullptr, e->d_btab, e->d_ws, (int8_t *)dc.p, flags,
-                                  e->compute),
+                                  e->compute, nullptr, e->resident_blocks, e->kc_seed),
          FDGPU_ERR_DEVICE);
   HIPCHK(hipStreamSynchronize(e->compute), FDGPU_ERR_DEVICE);
   HIPCHK(hipMemcpy(sig_codes, dc.p, ns, hipMemcpyDeviceToHost), FDGPU_ERR_DEVICE);

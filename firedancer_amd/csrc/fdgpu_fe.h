@@ -39,11 +39,7 @@
    interleaving consecutive independent field products (which it otherwise
    does up to the full VGPR budget, forcing spills in the point formulas).
    Each product alone has 10 independent column chains of ILP. */
-#ifndef FDG_NO_SCHED_FENCE
 #define FDG_SCHED_FENCE() __builtin_amdgcn_sched_barrier(0)
-#else
-#define FDG_SCHED_FENCE() do {} while (0)
-#endif
 
 namespace fdgpu {
 
@@ -94,28 +90,6 @@ FDG_DEV void fe_cmov(fe &h, const fe &a, const fe &b, bool c) {
   for (int i = 0; i < 10; i++) h.v[i] = c ? a.v[i] : b.v[i];
 }
 
-/* Carry-propagate 64-bit column sums into an R-bound element.  Order as
-   two interleaved chains (0->1->2->3->4->5, 4->5->...->9->0->1) so the two
-   halves run in parallel: 12 carry steps. */
-FDG_DEV void fe_carry64(fe &h, uint64_t (&c)[10]) {
-  constexpr uint64_t M26 = (1ull << 26) - 1, M25 = (1ull << 25) - 1;
-  uint64_t t;
-  t = c[0] >> 26; c[0] &= M26; c[1] += t;
-  t = c[4] >> 26; c[4] &= M26; c[5] += t;
-  t = c[1] >> 25; c[1] &= M25; c[2] += t;
-  t = c[5] >> 25; c[5] &= M25; c[6] += t;
-  t = c[2] >> 26; c[2] &= M26; c[3] += t;
-  t = c[6] >> 26; c[6] &= M26; c[7] += t;
-  t = c[3] >> 25; c[3] &= M25; c[4] += t;
-  t = c[7] >> 25; c[7] &= M25; c[8] += t;
-  t = c[4] >> 26; c[4] &= M26; c[5] += t;
-  t = c[8] >> 26; c[8] &= M26; c[9] += t;
-  t = c[9] >> 25; c[9] &= M25; c[0] += t * 19u;
-  t = c[0] >> 26; c[0] &= M26; c[1] += t;
-#pragma unroll
-  for (int i = 0; i < 10; i++) h.v[i] = (uint32_t)c[i];
-}
-
 /* Weak reduction of 32-bit limbs (inputs up to ~2^31) to R. */
 FDG_DEV void fe_carry(fe &h) {
   constexpr uint32_t M26 = (1u << 26) - 1, M25 = (1u << 25) - 1;
@@ -152,26 +126,18 @@ FDG_DEV void fe_carry_par(fe &h) {
   for (int i = 1; i < 10; i++) h.v[i] += c[i - 1];
 }
 
-/* Column-sum schemes (tools/ubench_carry.hip, profiles/r01_ubench_carry.json):
-   FDGPU_FE_FF=1 (default) sums the columns in order 0..9 and starts each
-   column's v_mad_u64_u32 chain from the previous column's carry, so the
-   carry add rides in a mad addend instead of a separate 64-bit add (the
-   chain is kept in inline asm: the compiler would otherwise re-associate it
-   into independent partial sums plus an add).  8% faster per product on
-   gfx950 than FDGPU_FE_FF=0: ten independent column sums and a 12-step
-   two-chain carry.  Outputs are R-bound either way (FF: slack on limb 1
-   only), and both write h last, so h may alias f or g. */
-#ifndef FDGPU_FE_FF
-#define FDGPU_FE_FF 1
-#endif
+/* Column sums (tools/ubench_carry.hip, profiles/r01_ubench_carry.json): the
+   columns are summed in order 0..9 and each column's v_mad_u64_u32 chain
+   starts from the previous column's carry, so the carry add rides in a mad
+   addend instead of a separate 64-bit add (the chain is kept in inline asm:
+   the compiler would otherwise re-associate it into independent partial sums
+   plus an add).  8% faster per product on gfx950 than ten independent column
+   sums and a 12-step two-chain carry.  Outputs are R-bound (slack on limb 1
+   only) and h is written last, so h may alias f or g.
 
-#ifndef FDGPU_FE_ASMCOL
-#define FDGPU_FE_ASMCOL 1
-#endif
-
-/* FDGPU_FE_ASMCOL=1: each column's v_mad_u64_u32 chain is ONE inline-asm
-   block.  With one block per mad the compiler's hazard recognizer cannot see
-   inside the asm and pads every block with an s_nop; compiler-generated
+   Each column's v_mad_u64_u32 chain is ONE inline-asm block.  With one
+   block per mad the compiler's hazard recognizer cannot see inside the asm
+   and pads every block with an s_nop; compiler-generated
    back-to-back mads writing the same carry SGPR need none, so a block of N
    dependent mads is as safe as N separate ones.  madc<N>::run(s, a, b):
    s += a[0] b[0] + ... + a[N-1] b[N-1], in that order. */
@@ -279,13 +245,6 @@ template <> struct madc0<10> {
   }
 };
 
-/* s += a * b as one v_mad_u64_u32 (carry-out SGPR pair unused) */
-FDG_DEV void mad_acc(uint64_t &s, uint32_t a, uint32_t b) {
-  uint64_t cc;
-  asm("v_mad_u64_u32 %0, %1, %2, %3, %0" : "+v"(s), "=s"(cc) : "v"(a), "v"(b));
-  (void)cc;
-}
-
 /* Close a feed-forward product: the carry out of column 9 (weight 2^255)
    re-enters limb 0 times 19, and limb 0's excess moves to limb 1
    (carry < 2^39, so limb 1 grows by < 2^17.3). */
@@ -305,13 +264,11 @@ FDG_DEV void fe_mul(fe &h, const fe &f, const fe &g) {
   uint32_t g19[10], f2[10];
 #pragma unroll
   for (int i = 0; i < 10; i++) { g19[i] = 19u * g.v[i]; f2[i] = f.v[i] << 1; }
-#if FDGPU_FE_FF
   uint32_t r[10];
   uint64_t carry = 0;
 #pragma unroll
   for (int k = 0; k < 10; k++) {
     uint64_t s = carry;
-#if FDGPU_FE_ASMCOL
     uint32_t ca[10], cb[10];
 #pragma unroll
     for (int i = 0; i < 10; i++) {
@@ -324,40 +281,11 @@ FDG_DEV void fe_mul(fe &h, const fe &f, const fe &g) {
     }
     if (k == 0) madc0<10>::run(s, ca, cb);
     else madc<10>::run(s, ca, cb);
-#else
-#pragma unroll
-    for (int i = 0; i < 10; i++) {
-      int j = k - i;
-      const bool wrap = j < 0;
-      if (wrap) j += 10;
-      const bool dbl = (i & 1) && (j & 1);
-      mad_acc(s, dbl ? f2[i] : f.v[i], wrap ? g19[j] : g.v[j]);
-    }
-#endif
     const int bits = (k & 1) ? 25 : 26;
     r[k] = (uint32_t)s & ((1u << bits) - 1);
     carry = s >> bits;
   }
   fe_ff_close(h, r, carry);
-#else
-  uint64_t c[10];
-#pragma unroll
-  for (int k = 0; k < 10; k++) {
-    uint64_t s = 0;
-#pragma unroll
-    for (int i = 0; i < 10; i++) {
-      int j = k - i;
-      const bool wrap = j < 0;
-      if (wrap) j += 10;
-      const bool dbl = (i & 1) && (j & 1);
-      const uint32_t a = dbl ? f2[i] : f.v[i];
-      const uint32_t b = wrap ? g19[j] : g.v[j];
-      s += (uint64_t)a * b;
-    }
-    c[k] = s;
-  }
-  fe_carry64(h, c);
-#endif
   FDG_SCHED_FENCE();
 }
 
@@ -374,13 +302,11 @@ FDG_DEV void fe_sq_sh(fe &h, const fe &f) {
     f2[i] = f.v[i] << 1; f4[i] = f.v[i] << 2; f8[i] = f.v[i] << 3; f19[i] = 19u * f.v[i];
   }
   auto pick = [&](int m, int i) { return m == 0 ? f.v[i] : m == 1 ? f2[i] : m == 2 ? f4[i] : f8[i]; };
-#if FDGPU_FE_FF
   uint32_t r[10];
   uint64_t carry = 0;
 #pragma unroll
   for (int k = 0; k < 10; k++) {
     uint64_t s = carry;
-#if FDGPU_FE_ASMCOL
     uint32_t ca[6], cb[6];
     int n = 0;
 #pragma unroll
@@ -397,38 +323,11 @@ FDG_DEV void fe_sq_sh(fe &h, const fe &f) {
     if (k & 1) madc<5>::run(s, ca, cb);             /* odd columns: 5 symmetric terms, even: 6 */
     else if (k == 0) madc0<6>::run(s, ca, cb);
     else madc<6>::run(s, ca, cb);
-#else
-#pragma unroll
-    for (int i = 0; i < 10; i++) {
-#pragma unroll
-      for (int j = i; j < 10; j++) {
-        if ((i + j) % 10 != k) continue;
-        const int mul2 = (i != j ? 1 : 0) + (((i & 1) && (j & 1)) ? 1 : 0) + SH;
-        mad_acc(s, pick(mul2, i), (i + j) >= 10 ? f19[j] : f.v[j]);
-      }
-    }
-#endif
     const int bits = (k & 1) ? 25 : 26;
     r[k] = (uint32_t)s & ((1u << bits) - 1);
     carry = s >> bits;
   }
   fe_ff_close(h, r, carry);
-#else
-  uint64_t c[10];
-#pragma unroll
-  for (int k = 0; k < 10; k++) c[k] = 0;
-#pragma unroll
-  for (int i = 0; i < 10; i++) {
-#pragma unroll
-    for (int j = i; j < 10; j++) {
-      const int k = (i + j) % 10;
-      const bool wrap = (i + j) >= 10;
-      const int mul2 = (i != j ? 1 : 0) + (((i & 1) && (j & 1)) ? 1 : 0) + SH;
-      c[k] += (uint64_t)pick(mul2, i) * (wrap ? f19[j] : f.v[j]);
-    }
-  }
-  fe_carry64(h, c);
-#endif
   FDG_SCHED_FENCE();
 }
 

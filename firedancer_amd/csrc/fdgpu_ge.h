@@ -60,15 +60,7 @@ FDG_DEV void ge_dbl(ge_p1p1 &r, const ge_p2 &p) {
   fe_add(s, p.X, p.Y);
   fe_sq(r.X, s);                   /* AA */
   fe_sub4(r.X, r.X, r.Y);          /* X' = AA - Y' */
-#ifndef FDGPU_DBL_SQ2
-#define FDGPU_DBL_SQ2 1
-#endif
-#if FDGPU_DBL_SQ2
   fe_sq2(r.T, p.Z);                /* B = 2 Z^2 (R) */
-#else
-  fe_sq(r.T, p.Z);
-  fe_add(r.T, r.T, r.T);           /* B = 2 Z^2 */
-#endif
   fe_sub4(r.T, r.T, r.Z);          /* T' = B - Z' */
   fe_carry_par(r.T);
 }

@@ -35,38 +35,24 @@ typedef struct {
    entry), so [S]B costs NDIG mixed additions and no doublings.  Tables live
    in HBM (W=16: 16 x 32769 x 128 B = 67 MB, resident in the 256 MB Infinity
    Cache). */
-#ifndef FDGPU_BCOMB_BITS
 #define FDGPU_BCOMB_BITS    16u           /* comb radix: NDIG tables of 2^(W-1)+1 entries */
-#endif
 #define FDGPU_BCOMB_NDIG    ((254u + FDGPU_BCOMB_BITS - 1u) / FDGPU_BCOMB_BITS)   /* covers S < 2^253 + carry */
 #define FDGPU_BCOMB_ENTRIES ((1u << (FDGPU_BCOMB_BITS - 1u)) + 1u)
 #define FDGPU_BCOMB_STRIDE  32u           /* u32 per entry (30 used): one 128-B line */
 #define FDGPU_BCOMB_CHUNK   64u           /* entries per lane in the table build (one batch inversion) */
-/* FDGPU_HALFSIZE=1 (default): the verify equation with half-size scalars
-   (fdgpu_lattice.h); 0: the full-length chain with R compared on its
-   encoding (R-avoiding path). */
-#ifndef FDGPU_HALFSIZE
-#define FDGPU_HALFSIZE 1
-#endif
+/* The verify equation with half-size scalars (fdgpu_lattice.h).  Per-lane
+   workspace entries (cached form, 40 words each): */
 #define HS_MAX_WIN          40u           /* radix-16 windows of |u|, |v| (< 2^159) */
-#if FDGPU_HALFSIZE
+                                          /* entries 0..8: the -A table */
 #define FDGPU_WS_RTAB       FDGPU_ATAB_ENTRIES          /* entries 9..17: the -R table */
 #define FDGPU_WS_PARK       (2u * FDGPU_ATAB_ENTRIES)   /* entry: k digits, decoded R, code (full path) */
 #define FDGPU_WS_SB         (FDGPU_WS_PARK + 1u)        /* entry: [w]B (or [S]B) in cached form */
 #define FDGPU_WS_ENTRIES    (FDGPU_WS_SB + 1u)          /* 20 entries: 3200 B per signature */
-#else
-#define FDGPU_WS_PARK       FDGPU_ATAB_ENTRIES          /* entry: digits, code, R' (slow path) */
-#define FDGPU_WS_SB         (FDGPU_ATAB_ENTRIES + 1u)   /* entry: [S]B in cached form, then U + flags */
-#define FDGPU_WS_ENTRIES    (FDGPU_ATAB_ENTRIES + 2u)   /* per-lane workspace: A table, park, [S]B: 1760 B */
-#endif
 #define FDGPU_WS_LANE_WORDS (FDGPU_WS_ENTRIES * FDGPU_ATAB_WORDS)
 #define FDGPU_BLOCK         256u
 #define FDGPU_FLAG_REF_MAP  1u            /* portable-backend error mapping */
 #define FDGPU_FLAG_KFULL    2u            /* half-size path: every lane takes the full-length fallback */
 #define FDGPU_FLAG_KCACHE   4u            /* half-size path: one -A decode + table per distinct key */
-#ifndef FDGPU_SPLIT_A
-#define FDGPU_SPLIT_A       0             /* A/B: A decode + table in a kernel of its own (no dedup) */
-#endif
 /* SHA-512 block-count groups of the host-side bucketing (expand): messages of
    more blocks than this share the last group */
 #define FDGPU_NBLK_GROUPS   32u
@@ -85,11 +71,13 @@ hipError_t fdgpu_btab_build(uint32_t *d_btab, hipStream_t stream);
    caller's order) */
 /* d_n_sig != NULL: the signature count is read on the device (it is produced
    there by the GPU-side ingest); n_sig is then an upper bound that sizes the
-   grid (and the workspace).  Half-size path only. */
+   grid (and the workspace).  resident_blocks: verify-kernel blocks the
+   device keeps resident (occupancy x CUs, the fallback kernel's grid cap);
+   kc_seed: the key cache's hash seed (FDGPU_FLAG_KCACHE). */
 hipError_t fdgpu_launch_verify_sigs(const uint8_t *d_arena, const fdgpu_sig_desc_t *d_sigs, uint32_t n_sig,
                                     const uint32_t *d_perm, const uint32_t *d_btab, uint32_t *d_ws,
                                     int8_t *d_sig_codes, uint32_t flags, hipStream_t stream,
-                                    const uint32_t *d_n_sig = nullptr);
+                                    const uint32_t *d_n_sig, uint32_t resident_blocks, uint64_t kc_seed);
 /* d_accept (NULL: not written): ceil(n_txn / 64) words, bit t = txn t verified */
 hipError_t fdgpu_launch_combine(const fdgpu_txn_desc_t *d_txns, uint32_t n_txn, const int8_t *d_sig_codes,
                                 int8_t *d_txn_codes, uint64_t *d_accept, hipStream_t stream);

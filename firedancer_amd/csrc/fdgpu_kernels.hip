@@ -2,7 +2,7 @@
    verify engine.  One signature per lane, 256-thread workgroups; integer /
    bignum work only (no MFMA).  Per batch, on one stream:
 
-   fdgpu_verify_hs_kernel  (default, FDGPU_HALFSIZE=1) everything: S < L,
+   fdgpu_verify_hs_kernel  everything: S < L,
        k = SHA-512(R||A||M) mod L, decode A and R (decode2's rules and code
        order) with their small-order tests and the per-lane tables
        {O, -A, .., -8A}, {O, -R, .., -8R}; the lattice split of k into two
@@ -15,10 +15,6 @@
    fdgpu_key_dedup_kernel, fdgpu_key_table_kernel  (FDGPU_FLAG_KCACHE) one A
        decode + table per distinct public key, read in place by
        fdgpu_verify_hs_kernel<true> and the fallback kernel.
-   fdgpu_verify_ra_kernel, fdgpu_tail_kernel, fdgpu_finish_kernel
-                           (FDGPU_HALFSIZE=0) the round-1 R-avoiding path:
-       full-length k, R' compared with R's encoding through one batched
-       inversion per workgroup, the reference's full R decode for the rest.
    fdgpu_combine_kernel    per transaction, batch_single_msg first-error
        semantics (fd_ed25519_user.c:232-310), plus a ballot-compacted
        accept bitmap.
@@ -27,7 +23,6 @@
    fdgpu_bcomb_*           build the comb tables at engine open.
    fdgpu_test_*            per-stage diagnostics for the parity tests. */
 #include <hip/hip_runtime.h>
-#include <random>
 
 #include "fdgpu_ge.h"
 #include "fdgpu_internal.h"
@@ -143,25 +138,22 @@ __global__ void __launch_bounds__(64) fdgpu_bcomb_fill_kernel(const uint32_t *ba
   }
 }
 
-/* ---- per-lane A table in the global workspace ----
-   layout: lane-contiguous, ws[i * 400 + entry * 40 + word] for signature i:
-   a lane's entry is 160 contiguous bytes (32-B aligned), read whole with ten
-   16-B loads, so a wave's table read touches ~2 cache lines per lane and
-   uses every byte it fetches.  Entries 0..8 are the table; entry 9 parks
-   (x_R, y_R), the digit strings and the pass-1 code across the kernels. */
+/* ---- per-lane tables in the global workspace ----
+   layout: lane-contiguous, ws[i * FDGPU_WS_LANE_WORDS + entry * 40 + word]
+   for signature i: a lane's entry is 160 contiguous bytes (32-B aligned),
+   read whole with ten 16-B loads, so a wave's table read touches ~2 cache
+   lines per lane and uses every byte it fetches (fdgpu_internal.h lists the
+   entries). */
 
-/* Stored word order of a cached entry (FDGPU_ATAB_PAIRS=1): Y+X and Y-X
+/* Stored word order of a cached entry: Y+X and Y-X
    interleaved by pairs in the first five 16-B chunks -- chunk k = (Y+X
    limbs 2k, 2k+1, Y-X limbs 2k, 2k+1) -- then 2Z and 2dT as they are.  A
    chain addition of -P reads Y+X and Y-X swapped: with pairs the swap is a
    per-lane 8-B offset of two ds_read_b64 (unstage_entry_signed) instead of
    20 per-word selects.  atab_store / atab_load convert, so every other
    reader sees the canonical order (Y+X, Y-X, 2Z, 2dT). */
-#ifndef FDGPU_ATAB_PAIRS
-#define FDGPU_ATAB_PAIRS 1
-#endif
 FDG_DEV constexpr int atab_pos(int w) {
-  return !FDGPU_ATAB_PAIRS || w >= 20 ? w : w < 10 ? 4 * (w / 2) + (w % 2) : 4 * ((w - 10) / 2) + 2 + (w % 2);
+  return w >= 20 ? w : w < 10 ? 4 * (w / 2) + (w % 2) : 4 * ((w - 10) / 2) + 2 + (w % 2);
 }
 
 FDG_DEV void atab_store(uint32_t *wsl, uint32_t entry, const ge_cached &c) {
@@ -314,235 +306,8 @@ FDG_DEV void atab_build(uint32_t *wsl, const ge_p3 &An) {
   }
 }
 
-/* Per-lane workspace words beyond the A table (entries 0..8):
-   entry FDGPU_WS_PARK ("park"):
-     words 20-27  radix-16 digits of k (pass 1 -> dsm_k; dead once dsm_k
-                  has read them)
-     word  36     pass-1 code (low byte) | RA_ASMALL
-     words  0-29  X, Y, Z of R' (slow-path lanes only, after dsm_k)
-   entry FDGPU_WS_SB ("post" once dsm_k has consumed [S]B):
-     words  0-39  [S]B in cached form (pass 1 -> the last addition of dsm_k)
-     words  0-9   U = X * (product of the workgroup's other Z)  } written after
-     word  10     pass-1 code | RA_* flags                       } dsm_k */
-#define PARK_KD 20
-#define PARK_CODE 36
-#define POST_U 0
-#define POST_FLAGS 10
-static_assert(PARK_KD + KD_WORDS <= PARK_CODE, "digit string overlaps the pass-1 code");
-static_assert(PARK_CODE < (int)FDGPU_ATAB_WORDS && POST_FLAGS + 2 <= (int)FDGPU_ATAB_WORDS, "park layout");
-static_assert(POST_U == 0 && POST_FLAGS == 10, "U and flags are written as three dwordx4 at the entry start");
-/* flag bits above the int8 pass-1 code */
-#define RA_ASMALL (1u << 8)
-#define RA_YMATCH (1u << 9)
-
-FDG_DEV uint32_t *park_ptr(uint32_t *wsl) { return wsl + FDGPU_WS_PARK * FDGPU_ATAB_WORDS; }
-FDG_DEV uint32_t *post_ptr(uint32_t *wsl) { return wsl + FDGPU_WS_SB * FDGPU_ATAB_WORDS; }
-
-/* Pass 1 of one signature without R (fd_ed25519_user.c:158-207; SURVEY
-   Appendix A steps 1-5): S < L, k = SHA-512(R||A||M) mod L, [S]B by the
-   comb, decode A and its small-order test, the table {O, -A, .., -8A}.  R is
-   resolved after the scalar multiplication (fdgpu_finish_kernel / the slow
-   path).  Returns the S / A verdict; parks k's digits and the flags. */
-FDG_DEV int verify_pass1(const uint8_t *arena, const fdgpu_sig_desc_t &sd_in, uint32_t nblk_wave, uint32_t *wsl,
-                         const uint32_t *__restrict__ btab, bool ref_map) {
-  uint32_t R[8], A[8];
-  load32(R, arena + sd_in.sig_off);
-  load32(A, arena + sd_in.pub_off);
-  uint32_t *park = park_ptr(wsl);
-
-  /* k = SHA-512(R || A || M) mod L, recoded to signed radix 16 */
-  {
-    uint64_t h[8];
-    sha512_hram(h, R, A, arena + sd_in.msg_off, sd_in.msg_sz, nblk_wave);
-    FDGPU_STAMP(1);
-    uint32_t kx[16], k[8], kd[KD_WORDS];
-#pragma unroll
-    for (int i = 0; i < 8; i++) { kx[2 * i] = bswap32((uint32_t)(h[i] >> 32)); kx[2 * i + 1] = bswap32((uint32_t)h[i]); }
-    sc_reduce512(k, kx);
-    sc_recode16(kd, k);
-#pragma unroll
-    for (int i = 0; i < KD_WORDS; i++) park[PARK_KD + i] = kd[i];
-  }
-  /* step 1: S < L (fd_ed25519_user.c:159-161); [S]B by the comb, parked in
-     cached form for dsm_k (rejected S -> 0) */
-  int code;
-  {
-    uint32_t S[8];
-    load32(S, arena + sd_in.sig_off + 32);
-    code = sc_lt_L(S) ? 0 : -1;
-#pragma unroll
-    for (int i = 0; i < 8; i++) S[i] = code ? 0u : S[i];
-    ge_p3 SB;
-    FDGPU_STAMP(2);
-    comb_sb(SB, S, btab);
-    ge_cached c; ge_p3_to_cached(c, SB);
-    atab_store(wsl, FDGPU_WS_SB, c);
-  }
-  FDGPU_STAMP(3);
-  /* step 2 (A): decode, small order, table of -A */
-  bool a_ok, a_small;
-  {
-    ge_p3 Ap;
-    a_ok = ge_decode(Ap, A, ref_map);
-    a_small = ge_is_small_order_affine(Ap);
-    FDGPU_STAMP(4);
-    ge_p3 An; ge_p3_neg(An, Ap);
-    atab_build(wsl, An);
-  }
-  if (code == 0 && !a_ok) code = ref_map ? -2 : -1;    /* decode2 reports A before R */
-  park[PARK_CODE] = ((uint32_t)code & 0xffu) | (a_small ? RA_ASMALL : 0u);
-  return code;
-}
-
 FDG_DEV uint32_t *lane_ws(uint32_t *ws, uint32_t i) {
   return ws + (size_t)i * FDGPU_WS_LANE_WORDS;
-}
-
-/* ---------------- R-avoiding verify ----------------
-   The reference decompresses R (a 2^252-3 exponentiation) only to compare it
-   with R' = [S]B - [k]A (fd_ed25519_user.c:164-229).  Here R' is compared on
-   its encoding instead: y_R (the encoded y, reduced mod p) must equal Y/Z,
-   and the parity of the canonical x = X/Z must equal R's sign bit.  The
-   one inversion of Z this needs is batched (Montgomery's trick): a
-   workgroup-wide product scan of Z in the verify kernel, one inversion per
-   workgroup in fdgpu_wginv_kernel, and 3 products per signature in
-   fdgpu_finish_kernel.  Equal y determines the decoded R up to the sign of
-   x, so every code of fd_ed25519_user.c follows without decompressing R:
-     y match, parity match      -> R = R' (x = 0 included):  small(R) ? ERR_SIG : SUCCESS
-     y match, parity mismatch   -> x = 0: decode fails (AVX) / R small (ref): ERR_SIG
-                                   else R = -R':             small(R) ? ERR_SIG : ERR_MSG
-   Signatures whose y differs, or whose A is small order (the R decode verdict
-   then outranks ERR_PUBKEY), are queued and finished by fdgpu_slow_kernel
-   with the full R decode, as the reference does. */
-
-FDG_DEV void fe_shfl_up(fe &o, const fe &a, int off) {
-#pragma unroll
-  for (int i = 0; i < 10; i++) o.v[i] = (uint32_t)__shfl_up((int)a.v[i], off, 64);
-}
-FDG_DEV void fe_shfl_down(fe &o, const fe &a, int off) {
-#pragma unroll
-  for (int i = 0; i < 10; i++) o.v[i] = (uint32_t)__shfl_down((int)a.v[i], off, 64);
-}
-
-/* Exclusive prefix and suffix products of z over the workgroup (256 lanes =
-   4 waves): within a wave by log-step shuffles, across waves through LDS.
-   Thread 0 writes the workgroup's total product. */
-FDG_DEV void wg_scan(const fe &z, fe &pex, fe &sex, uint32_t *tot_out) {
-  __shared__ uint32_t s_tot[FDGPU_BLOCK / 64][10];
-  const int lane = (int)(threadIdx.x & 63u), wv = (int)(threadIdx.x >> 6);
-  fe p = z, q = z, t, m;
-#pragma unroll
-  for (int off = 1; off < 64; off <<= 1) {
-    fe_shfl_up(t, p, off);
-    fe_mul(m, p, t);
-    fe_cmov(p, m, p, lane >= off);
-    fe_shfl_down(t, q, off);
-    fe_mul(m, q, t);
-    fe_cmov(q, m, q, lane + off < 64);
-  }
-  fe one; fe_1(one);
-  fe_shfl_up(t, p, 1);   fe_cmov(pex, one, t, lane == 0);
-  fe_shfl_down(t, q, 1); fe_cmov(sex, one, t, lane == 63);
-  if (lane == 63) {
-#pragma unroll
-    for (int i = 0; i < 10; i++) s_tot[wv][i] = p.v[i];
-  }
-  __syncthreads();
-  fe pre, suf, w;
-  fe_1(pre); fe_1(suf);
-#pragma unroll
-  for (int v = 0; v < (int)(FDGPU_BLOCK / 64); v++) {
-#pragma unroll
-    for (int i = 0; i < 10; i++) w.v[i] = s_tot[v][i];
-    if (v < wv) fe_mul(pre, pre, w);          /* wave-uniform branches */
-    if (v > wv) fe_mul(suf, suf, w);
-  }
-  fe_mul(pex, pex, pre);
-  fe_mul(sex, sex, suf);
-  if (threadIdx.x == 63) {                    /* wave 0's inclusive total x waves 1..3 */
-    fe all; fe_mul(all, p, suf);
-#pragma unroll
-    for (int i = 0; i < 10; i++) tot_out[i] = all.v[i];
-  }
-}
-
-/* Kernel A: pass 1 without R, [S]B - [k]A, y check, Z scan.  Parks R'
-   (slow-path lanes, park words 0-29) and U + flags (post entry). */
-__global__ void __launch_bounds__(FDGPU_BLOCK, FDGPU_VERIFY_WAVES)
-fdgpu_verify_ra_kernel(const uint8_t *__restrict__ arena, const fdgpu_sig_desc_t *__restrict__ sigs, uint32_t n_sig,
-                       const uint32_t *__restrict__ btab, uint32_t *__restrict__ ws, uint32_t *__restrict__ wg_tot,
-                       uint32_t *__restrict__ queue, uint32_t *__restrict__ queue_cnt, uint32_t flags) {
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  const bool active = i < n_sig;
-  const fdgpu_sig_desc_t d = sigs[active ? i : n_sig - 1];
-  uint32_t nb = sha512_hram_blocks(d.msg_sz);
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) nb = max(nb, (uint32_t)__shfl_xor((int)nb, off));
-  uint32_t *wsl = lane_ws(ws, i);
-  uint32_t *park = park_ptr(wsl);
-  FDGPU_STAMP(0);
-  const int code1 = verify_pass1(arena, d, nb, wsl, btab, (flags & FDGPU_FLAG_REF_MAP) != 0);
-  FDGPU_STAMP(5);
-  const bool need = active && code1 == 0;
-  ge_p2 Rc;
-  if (__any(need)) {
-    uint32_t kd[KD_WORDS];
-#pragma unroll
-    for (int k = 0; k < KD_WORDS; k++) kd[k] = park[PARK_KD + k];
-    dsm_k(Rc, kd, wsl);
-  } else {
-    ge_p2_0(Rc);
-  }
-  FDGPU_STAMP(6);
-  uint32_t Renc[8];
-  load32(Renc, arena + d.sig_off);
-  fe yR, t;
-  fe_frombytes(yR, Renc);
-  fe_mul(t, yR, Rc.Z);
-  const bool ymatch = fe_eq(Rc.Y, t);
-  fe z, one; fe_1(one);
-  fe_cmov(z, Rc.Z, one, need && !fe_iszero(Rc.Z));
-  const uint32_t fl = park[PARK_CODE] | (ymatch ? RA_YMATCH : 0u);
-  const bool slow = need && ((fl & RA_ASMALL) || !ymatch);
-  if (slow) {                                  /* only the slow path needs R' itself */
-#pragma unroll
-    for (int k = 0; k < 10; k++) { park[k] = Rc.X.v[k]; park[10 + k] = Rc.Y.v[k]; park[20 + k] = Rc.Z.v[k]; }
-  }
-  /* queue the slow signatures (one atomic per wave; waves finish spread over
-     the kernel's lifetime, so the counter is not contended) */
-  {
-    const uint64_t m = __ballot(slow);
-    if (m) {
-      const int lane = (int)(threadIdx.x & 63u);
-      const int leader = __ffsll((long long)m) - 1;
-      uint32_t base = 0;
-      if (lane == leader) base = atomicAdd(queue_cnt, (uint32_t)__popcll(m));
-      base = (uint32_t)__shfl((int)base, leader, 64);
-      if (slow) queue[base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull))] = i;
-    }
-  }
-  fe pex, sex;
-  wg_scan(z, pex, sex, wg_tot + (size_t)blockIdx.x * 10);
-  /* U = X * (product of every other Z in the workgroup): x = U / (all Z) */
-  fe U;
-  fe_mul(U, Rc.X, pex);
-  fe_mul(U, U, sex);
-  uint4 *o = (uint4 *)(post_ptr(wsl) + POST_U);   /* [S]B is dead here: dsm_k added it */
-  o[0] = make_uint4(U.v[0], U.v[1], U.v[2], U.v[3]);
-  o[1] = make_uint4(U.v[4], U.v[5], U.v[6], U.v[7]);
-  o[2] = make_uint4(U.v[8], U.v[9], fl, 0u);
-  FDGPU_STAMP(7);
-}
-
-/* Inverse of one workgroup's Z product (run by the extra blocks of
-   fdgpu_tail_kernel). */
-FDG_DEV void wg_invert(const uint32_t *__restrict__ wg_tot, uint32_t *__restrict__ wg_inv, uint32_t g) {
-  fe a, r;
-#pragma unroll
-  for (int k = 0; k < 10; k++) a.v[k] = wg_tot[10 * g + k];
-  fe_invert(r, a);
-#pragma unroll
-  for (int k = 0; k < 10; k++) wg_inv[10 * g + k] = r.v[k];
 }
 
 /* Output slot of lane i: signatures may be verified in an order grouped by
@@ -550,96 +315,7 @@ FDG_DEV void wg_invert(const uint32_t *__restrict__ wg_tot, uint32_t *__restrict
    order); codes are always written in the caller's order. */
 FDG_DEV uint32_t out_idx(const uint32_t *__restrict__ perm, uint32_t i) { return perm ? perm[i] : i; }
 
-/* Kernel C: finish each signature from its y check and the parity of
-   x = X / Z (Z^-1 = workgroup inverse x prefix x suffix); slow-path lanes
-   are left to fdgpu_tail_kernel. */
-__global__ void __launch_bounds__(FDGPU_BLOCK) fdgpu_finish_kernel(
-    const uint8_t *__restrict__ arena, const fdgpu_sig_desc_t *__restrict__ sigs, uint32_t n_sig,
-    const uint32_t *__restrict__ ws, const uint32_t *__restrict__ wg_inv, const uint32_t *__restrict__ perm,
-    int8_t *__restrict__ codes) {
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  const bool active = i < n_sig;
-  const uint32_t *post = ws + (size_t)(active ? i : 0) * FDGPU_WS_LANE_WORDS + FDGPU_WS_SB * FDGPU_ATAB_WORDS;
-  const uint4 *pv = (const uint4 *)(post + POST_U);
-  const uint4 u0 = pv[0], u1 = pv[1], u2 = pv[2];
-  const uint32_t fl = u2.z;
-  const int code1 = (int)(int8_t)(fl & 0xffu);
-  const bool slow = active && code1 == 0 && ((fl & RA_ASMALL) || !(fl & RA_YMATCH));
-  int code = code1;
-  if (__any(active && code1 == 0 && !slow)) {
-    fe U, inv, x;
-    U.v[0] = u0.x; U.v[1] = u0.y; U.v[2] = u0.z; U.v[3] = u0.w; U.v[4] = u1.x; U.v[5] = u1.y; U.v[6] = u1.z;
-    U.v[7] = u1.w; U.v[8] = u2.x; U.v[9] = u2.y;
-#pragma unroll
-    for (int k = 0; k < 10; k++) inv.v[k] = wg_inv[10 * blockIdx.x + k];
-    fe_mul(x, U, inv);
-    fe_canon(x);
-    uint32_t xnz = 0;
-#pragma unroll
-    for (int k = 0; k < 10; k++) xnz |= x.v[k];
-    uint32_t Renc[8];
-    load32(Renc, arena + sigs[active ? i : 0].sig_off);
-    ge_p3 Rp;                                  /* affine (x, y) with y = y_R: only x==0 and y feed the test */
-    Rp.X = x; fe_frombytes(Rp.Y, Renc);
-    const bool small = ge_is_small_order_affine(Rp);
-    const uint32_t sign = Renc[7] >> 31;
-    int c;
-    if ((x.v[0] & 1u) == sign) c = small ? -1 : 0;
-    else if (xnz == 0) c = -1;
-    else c = small ? -1 : -3;
-    if (active && code1 == 0 && !slow) code = c;
-  }
-  if (active && !slow) codes[out_idx(perm, i)] = (int8_t)code;
-}
-
-/* Kernel B+D (one launch, both latency-bound): blocks [0, slow_blocks) run
-   the queued signatures grid-stride with the reference's full R decode
-   (fd_ed25519_user.c:164-229 order: R decode failure, A small, R small,
-   equation); the remaining blocks invert the workgroup Z products, one per
-   thread.  slow_blocks covers every resident wave slot the batch's grid
-   has, so a batch where every signature fails the equation (all queued)
-   spreads the decodes over the whole GPU. */
-__global__ void __launch_bounds__(FDGPU_BLOCK, FDGPU_VERIFY_WAVES) fdgpu_tail_kernel(
-    const uint8_t *__restrict__ arena, const fdgpu_sig_desc_t *__restrict__ sigs, const uint32_t *__restrict__ ws,
-    const uint32_t *__restrict__ perm, int8_t *__restrict__ codes, const uint32_t *__restrict__ queue,
-    const uint32_t *__restrict__ queue_cnt, const uint32_t *__restrict__ wg_tot, uint32_t *__restrict__ wg_inv,
-    uint32_t n_wg, uint32_t slow_blocks, uint32_t flags) {
-  if (blockIdx.x >= slow_blocks) {
-    const uint32_t g = (blockIdx.x - slow_blocks) * blockDim.x + threadIdx.x;
-    if (g < n_wg) wg_invert(wg_tot, wg_inv, g);
-    return;
-  }
-  const uint32_t cnt = *queue_cnt;
-  if (blockIdx.x * blockDim.x >= cnt) return;            /* nothing queued for this block */
-  for (uint32_t q = blockIdx.x * blockDim.x + threadIdx.x; q < cnt; q += slow_blocks * blockDim.x) {
-    const uint32_t i = queue[q];
-    const uint32_t *wsl = ws + (size_t)i * FDGPU_WS_LANE_WORDS;
-    const uint32_t *park = wsl + FDGPU_WS_PARK * FDGPU_ATAB_WORDS;
-    const uint32_t fl = wsl[FDGPU_WS_SB * FDGPU_ATAB_WORDS + POST_FLAGS];
-    uint32_t Renc[8];
-    load32(Renc, arena + sigs[i].sig_off);
-    ge_p3 Rp;
-    const bool r_ok = ge_decode(Rp, Renc, (flags & FDGPU_FLAG_REF_MAP) != 0);
-    int code;
-    if (!r_ok) code = -1;
-    else if (fl & RA_ASMALL) code = -2;
-    else if (ge_is_small_order_affine(Rp)) code = -1;
-    else {
-      fe X, Y, Z, l;
-#pragma unroll
-      for (int k = 0; k < 10; k++) { X.v[k] = park[k]; Y.v[k] = park[10 + k]; Z.v[k] = park[20 + k]; }
-      fe_mul(l, Rp.X, Z);
-      bool eq = fe_eq(X, l);
-      fe_mul(l, Rp.Y, Z);
-      eq = eq && fe_eq(Y, l);
-      code = eq ? 0 : -3;
-    }
-    codes[out_idx(perm, i)] = (int8_t)code;
-  }
-}
-
-#if FDGPU_HALFSIZE
-/* ---------------- half-size verify (FDGPU_HALFSIZE) ----------------
+/* ---------------- half-size verify ----------------
    fdgpu_lattice.h: with u = v k (mod 8L), v odd and |u|, |v| < 2^159,
    [S]B - [k]A == R  <=>  [w]B - [u]A - [v]R == O  (w = v S mod L), decided
    with ~132 doublings instead of ~252.  Per lane:
@@ -728,14 +404,7 @@ FDG_DEV void hs_wscalar(uint32_t (&w)[8], const uint32_t (&v)[5], bool v_neg, co
    window and read back after its doublings, so no 40-word entry stays live
    in VGPRs across the doublings.  One wave-instruction moves 16 B for each
    of the 64 lanes into 1 KiB of LDS (wave-uniform base + 16 B x lane).
-   HS_STAGE 1: the R entry through LDS, the A entry in VGPRs (prefetched);
-   2: both through LDS (20 KiB per wave). */
-#ifndef HS_STAGE
-#define HS_STAGE 2
-#endif
-#ifndef HS_DBL_UNROLL
-#define HS_DBL_UNROLL 1
-#endif
+   Both entries of a window go through LDS (2 x 10 KiB per wave). */
 typedef __attribute__((address_space(3))) void lds_void_t;
 
 FDG_DEV void stage_entry(uint32_t *lds_wave, const uint32_t *tab, int e) {
@@ -745,25 +414,12 @@ FDG_DEV void stage_entry(uint32_t *lds_wave, const uint32_t *tab, int e) {
     __builtin_amdgcn_global_load_lds((const void *)(src + 4 * c), (lds_void_t *)(lds_wave + 256 * c), 16, 0, 0);
 }
 
-FDG_DEV void unstage_entry(uint32_t (&q)[40], const uint32_t *lds_wave) {
-  const uint32_t lane = threadIdx.x & 63u;
-  uint32_t o[40];
-#pragma unroll
-  for (int c = 0; c < 10; c++) {
-    const uint4 v = *(const uint4 *)(lds_wave + 256 * c + 4 * lane);
-    o[4 * c] = v.x; o[4 * c + 1] = v.y; o[4 * c + 2] = v.z; o[4 * c + 3] = v.w;
-  }
-#pragma unroll
-  for (int i = 0; i < 40; i++) q[i] = o[atab_pos(i)];
-}
-
 /* The staged entry of a signed digit: q[0..9] = Y+X of the digit's point
    (Y-X of the table's -kP when neg), q[10..19] the other, 2Z, 2dT as stored
-   (2dT still to be negated when neg).  With FDGPU_ATAB_PAIRS the swap is the
-   8-B offset of two ds_read_b64 per pair chunk. */
+   (2dT still to be negated when neg).  With the pair-interleaved entries the
+   swap is the 8-B offset of two ds_read_b64 per pair chunk. */
 FDG_DEV void unstage_entry_signed(uint32_t (&q)[40], const uint32_t *lds_wave, bool neg) {
   const uint32_t lane = threadIdx.x & 63u;
-#if FDGPU_ATAB_PAIRS
   const uint32_t *a = lds_wave + 4 * lane + (neg ? 2u : 0u), *b = lds_wave + 4 * lane + (neg ? 0u : 2u);
 #pragma unroll
   for (int c = 0; c < 5; c++) {
@@ -775,11 +431,6 @@ FDG_DEV void unstage_entry_signed(uint32_t (&q)[40], const uint32_t *lds_wave, b
     const uint4 v = *(const uint4 *)(lds_wave + 256 * c + 4 * lane);
     q[4 * c] = v.x; q[4 * c + 1] = v.y; q[4 * c + 2] = v.z; q[4 * c + 3] = v.w;
   }
-#else
-  unstage_entry(q, lds_wave);
-#pragma unroll
-  for (int i = 0; i < 10; i++) { const uint32_t x = q[i], y = q[10 + i]; q[i] = neg ? y : x; q[10 + i] = neg ? x : y; }
-#endif
 }
 
 /* [|u|](T_A) + [|v|](T_R), digit strings pre-shifted so that digit nwin-1
@@ -788,11 +439,9 @@ FDG_DEV void unstage_entry_signed(uint32_t (&q)[40], const uint32_t *lds_wave, b
 FDG_DEV void hs_chain(ge_p1p1 &t, uint32_t (&ud)[5], uint32_t (&vd)[5], bool u_neg, bool v_neg, uint32_t nwin,
                       const uint32_t *wsl, const uint32_t *ta) {
   const uint32_t *tr = wsl + FDGPU_WS_RTAB * FDGPU_ATAB_WORDS;
-  __shared__ uint32_t s_stage[FDGPU_BLOCK / 64][HS_STAGE][10 * 256];
+  __shared__ uint32_t s_stage[FDGPU_BLOCK / 64][2][10 * 256];
   uint32_t *st_r = &s_stage[threadIdx.x >> 6][0][0];
-#if HS_STAGE == 2
   uint32_t *st_a = &s_stage[threadIdx.x >> 6][1][0];
-#endif
   ge_p2 acc2;
   ge_p3 acc3;
   uint32_t q[40];
@@ -813,25 +462,17 @@ FDG_DEV void hs_chain(ge_p1p1 &t, uint32_t (&ud)[5], uint32_t (&vd)[5], bool u_n
     ge_p1p1_to_p2(acc2, t);
     const int du = sext4(ud[4] >> 28), dv = sext4(vd[4] >> 28);
     shl4_5(ud); shl4_5(vd);
-#if HS_STAGE == 2
     stage_entry(st_a, ta, du);
-#else
-    atab_load(q, ta, du);
-#endif
     stage_entry(st_r, tr, dv);
-#pragma unroll HS_DBL_UNROLL
+#pragma unroll 1
     for (int r = 0; r < 4; r++) {
       ge_dbl(t, acc2);
       ge_p1p1_to_p2(acc2, t);
     }
     acc3.X = acc2.X; acc3.Y = acc2.Y; acc3.Z = acc2.Z; fe_mul(acc3.T, t.X, t.Y);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   /* the window's LDS-DMA has landed */
-#if HS_STAGE == 2
     unstage_entry_signed(q, st_a, (du < 0) != u_neg);
     ge_add_cached_regs_swapped(t, acc3, q, (du < 0) != u_neg);
-#else
-    ge_add_cached_regs(t, acc3, q, (du < 0) != u_neg);
-#endif
     ge_p1p1_to_p3(acc3, t);
     unstage_entry_signed(q, st_r, (dv < 0) != v_neg);
     ge_add_cached_regs_swapped(t, acc3, q, (dv < 0) != v_neg);
@@ -892,7 +533,7 @@ fdgpu_verify_hs_kernel(const uint8_t *__restrict__ arena, const fdgpu_sig_desc_t
       /* key cache: the -A table was built once per distinct key by
          fdgpu_key_table_kernel in its representative lane's workspace, and
          the chain reads it there */
-      const uint32_t di = active ? i : n_sig - 1u, r = key_of ? key_of[di] : di, vd = kverd[r];
+      const uint32_t di = active ? i : n_sig - 1u, r = key_of[di], vd = kverd[r];
       a_ok = (vd & 1u) != 0;
       a_small = (vd & 2u) != 0;
       ta = lane_ws(ws, r);
@@ -1078,13 +719,10 @@ __global__ void __launch_bounds__(256) fdgpu_key_dedup_kernel(const uint8_t *__r
 __global__ void __launch_bounds__(FDGPU_BLOCK, FDGPU_VERIFY_WAVES)
 fdgpu_key_table_kernel(const uint8_t *__restrict__ arena, const fdgpu_sig_desc_t *__restrict__ sigs,
                        uint32_t *__restrict__ ws, const uint32_t *__restrict__ reps,
-                       const uint32_t *__restrict__ rep_cnt, uint32_t n_arg, uint32_t *__restrict__ kverd,
-                       uint32_t flags) {
-  /* reps == nullptr (FDGPU_SPLIT_A): every signature is its own
-     representative, counted by *rep_cnt (device-side count) or n_arg */
+                       const uint32_t *__restrict__ rep_cnt, uint32_t *__restrict__ kverd, uint32_t flags) {
   const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
-  if (q >= (rep_cnt ? *rep_cnt : n_arg)) return;
-  const uint32_t i = reps ? reps[q] : q;
+  if (q >= *rep_cnt) return;
+  const uint32_t i = reps[q];
   uint32_t Aenc[8];
   load32(Aenc, arena + sigs[i].pub_off);
   ge_p3 P, Pn;
@@ -1122,8 +760,6 @@ fdgpu_full_kernel(uint32_t *__restrict__ ws, const uint32_t *__restrict__ perm, 
     codes[out_idx(perm, i)] = (int8_t)(eq ? 0 : -3);
   }
 }
-
-#endif  /* FDGPU_HALFSIZE */
 
 /* Per transaction: fd_ed25519_verify_batch_single_msg's first-error order
    (fd_ed25519_user.c:232-310) over its signatures' codes, plus the batch's
@@ -1402,13 +1038,7 @@ __global__ void __launch_bounds__(64) fdgpu_test_hs_split_kernel(const uint32_t 
 
 extern "C" {
 
-char const *fdgpu_kernel_path(void) {
-#if FDGPU_HALFSIZE
-  return "halfsize: fdgpu_verify_hs_kernel + fdgpu_full_kernel";
-#else
-  return "r-avoiding: fdgpu_verify_ra_kernel + fdgpu_tail_kernel + fdgpu_finish_kernel";
-#endif
-}
+char const *fdgpu_kernel_path(void) { return "halfsize: fdgpu_verify_hs_kernel + fdgpu_full_kernel"; }
 
 size_t fdgpu_btab_bytes(void) { return (size_t)BC_NDIG * BC_ENT * FDGPU_BCOMB_STRIDE * sizeof(uint32_t); }
 
@@ -1432,17 +1062,12 @@ hipError_t fdgpu_btab_build(uint32_t *d_btab, hipStream_t stream) {
 }
 
 hipError_t fdgpu_verify_occupancy(int *blocks_per_cu) {
-#if FDGPU_HALFSIZE
   return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, fdgpu_verify_hs_kernel<false>, FDGPU_BLOCK, 0);
-#else
-  return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, fdgpu_verify_ra_kernel, FDGPU_BLOCK, 0);
-#endif
 }
 
-/* workspace: per-lane words, then per-workgroup Z products and their
-   inverses, the slow-path queue and its counter (+ the key cache's
-   representative count), then the key cache's hash table, key_of, verdicts
-   and representative list */
+/* workspace: per-lane words, the fallback queue, its counter and the key
+   cache's representative count (16 words), then the key cache's hash table,
+   key_of, verdicts and representative list */
 static uint64_t kc_ht_slots(uint64_t lanes) {       /* power of two >= 2 lanes */
   uint64_t h = 64;
   while (h < 2 * lanes) h <<= 1;
@@ -1451,81 +1076,45 @@ static uint64_t kc_ht_slots(uint64_t lanes) {       /* power of two >= 2 lanes *
 
 size_t fdgpu_ws_bytes(uint64_t n_sig) {
   const uint64_t grid = (n_sig + FDGPU_BLOCK - 1) / FDGPU_BLOCK, lanes = grid * FDGPU_BLOCK;
-  /* + the key cache's hash table, key_of and verdicts (FDGPU_FLAG_KCACHE) */
-  return (size_t)(lanes * FDGPU_WS_LANE_WORDS + 20 * grid + lanes + 16 + kc_ht_slots(lanes) + 3 * lanes) *
-         sizeof(uint32_t);
+  return (size_t)(lanes * FDGPU_WS_LANE_WORDS + lanes + 16 + kc_ht_slots(lanes) + 3 * lanes) * sizeof(uint32_t);
 }
 
 hipError_t fdgpu_launch_verify_sigs(const uint8_t *d_arena, const fdgpu_sig_desc_t *d_sigs, uint32_t n_sig,
                                     const uint32_t *d_perm, const uint32_t *d_btab, uint32_t *d_ws,
-                                    int8_t *d_sig_codes, uint32_t flags, hipStream_t stream, const uint32_t *d_n_sig) {
+                                    int8_t *d_sig_codes, uint32_t flags, hipStream_t stream, const uint32_t *d_n_sig,
+                                    uint32_t resident_blocks, uint64_t kc_seed) {
   if (!n_sig) return hipSuccess;
   const uint32_t grid = (n_sig + FDGPU_BLOCK - 1) / FDGPU_BLOCK;
   const size_t lanes = (size_t)grid * FDGPU_BLOCK;
-  uint32_t *wg_tot = d_ws + lanes * FDGPU_WS_LANE_WORDS, *wg_inv = wg_tot + 10 * (size_t)grid;
-  uint32_t *queue = wg_inv + 10 * (size_t)grid, *cnt = queue + lanes;
+  uint32_t *queue = d_ws + lanes * FDGPU_WS_LANE_WORDS, *cnt = queue + lanes;
   hipError_t e = hipMemsetAsync(cnt, 0, sizeof(uint32_t), stream);
   if (e != hipSuccess) return e;
-  /* the queued (slow / full-length) lanes get as many blocks as the batch's
-     grid could keep resident (all of them, up to every wave slot of the
-     GPU), each exiting at once when the queue holds nothing for it */
-  static int resident = 0;
-  if (!resident) {
-    int bpcu = 0, dev = 0, cus = 0;
-    if (fdgpu_verify_occupancy(&bpcu) != hipSuccess || bpcu < 1) bpcu = 1;
-    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) !=
-                                                hipSuccess || cus < 1)
-      cus = 256;
-    resident = bpcu * cus;
-  }
-  const uint32_t slow_blocks = grid < (uint32_t)resident ? grid : (uint32_t)resident;
-#if FDGPU_HALFSIZE
-  (void)wg_tot; (void)wg_inv;
-#if FDGPU_SPLIT_A
-  /* A/B variant: every lane's A decode + table in a kernel of its own */
-  if (!(flags & FDGPU_FLAG_KCACHE)) {
-    uint32_t *kverd = cnt + 16 + kc_ht_slots(lanes) + lanes;
-    hipLaunchKernelGGL(fdgpu_key_table_kernel, dim3(grid), dim3(FDGPU_BLOCK), 0, stream, d_arena, d_sigs, d_ws,
-                       (const uint32_t *)nullptr, d_n_sig, n_sig, kverd, flags);
-    hipLaunchKernelGGL(fdgpu_verify_hs_kernel<true>, dim3(grid), dim3(FDGPU_BLOCK), 0, stream, d_arena, d_sigs, n_sig,
-                       d_n_sig, d_btab, d_ws, d_perm, d_sig_codes, queue, cnt, flags, (const uint32_t *)nullptr, kverd);
-    hipLaunchKernelGGL(fdgpu_full_kernel, dim3(slow_blocks), dim3(FDGPU_BLOCK), 0, stream, d_ws, d_perm, d_sig_codes,
-                       queue, cnt, slow_blocks * FDGPU_BLOCK, (const uint32_t *)nullptr);
-    return hipGetLastError();
-  }
-#endif
+  /* the queued full-length lanes get as many blocks as the batch's grid could
+     keep resident (all of them, up to every wave slot of the GPU: the
+     engine's occupancy x CUs), each exiting at once when the queue holds
+     nothing for it */
+  if (!resident_blocks) resident_blocks = 1;
+  const uint32_t slow_blocks = grid < resident_blocks ? grid : resident_blocks;
+  const uint32_t *key_of = nullptr;
   if (flags & FDGPU_FLAG_KCACHE) {
     const uint64_t hts = kc_ht_slots(lanes);
-    uint32_t *ht = cnt + 16, *key_of = ht + hts, *kverd = key_of + lanes, *reps = kverd + lanes, *rep_cnt = cnt + 1;
-    static uint64_t seed = 0;
-    if (!seed) seed = ((uint64_t)std::random_device{}() << 32 | std::random_device{}()) | 1u;
+    uint32_t *ht = cnt + 16, *kof = ht + hts, *kverd = kof + lanes, *reps = kverd + lanes, *rep_cnt = cnt + 1;
     e = hipMemsetAsync(ht, 0xff, hts * sizeof(uint32_t), stream);
     if (e == hipSuccess) e = hipMemsetAsync(rep_cnt, 0, sizeof(uint32_t), stream);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(fdgpu_key_dedup_kernel, dim3((n_sig + 255) / 256), dim3(256), 0, stream, d_arena, d_sigs, n_sig,
-                       d_n_sig, ht, (uint32_t)(hts - 1), key_of, reps, rep_cnt, seed);
+                       d_n_sig, ht, (uint32_t)(hts - 1), kof, reps, rep_cnt, kc_seed);
     hipLaunchKernelGGL(fdgpu_key_table_kernel, dim3(grid), dim3(FDGPU_BLOCK), 0, stream, d_arena, d_sigs, d_ws, reps,
-                       rep_cnt, 0u, kverd, flags);
+                       rep_cnt, kverd, flags);
     hipLaunchKernelGGL(fdgpu_verify_hs_kernel<true>, dim3(grid), dim3(FDGPU_BLOCK), 0, stream, d_arena, d_sigs, n_sig,
-                       d_n_sig, d_btab, d_ws, d_perm, d_sig_codes, queue, cnt, flags, key_of, kverd);
-    hipLaunchKernelGGL(fdgpu_full_kernel, dim3(slow_blocks), dim3(FDGPU_BLOCK), 0, stream, d_ws, d_perm, d_sig_codes,
-                       queue, cnt, slow_blocks * FDGPU_BLOCK, key_of);
-    return hipGetLastError();
+                       d_n_sig, d_btab, d_ws, d_perm, d_sig_codes, queue, cnt, flags, kof, kverd);
+    key_of = kof;
+  } else {
+    hipLaunchKernelGGL(fdgpu_verify_hs_kernel<false>, dim3(grid), dim3(FDGPU_BLOCK), 0, stream, d_arena, d_sigs, n_sig,
+                       d_n_sig, d_btab, d_ws, d_perm, d_sig_codes, queue, cnt, flags, nullptr, nullptr);
   }
-  hipLaunchKernelGGL(fdgpu_verify_hs_kernel<false>, dim3(grid), dim3(FDGPU_BLOCK), 0, stream, d_arena, d_sigs, n_sig,
-                     d_n_sig, d_btab, d_ws, d_perm, d_sig_codes, queue, cnt, flags, nullptr, nullptr);
   hipLaunchKernelGGL(fdgpu_full_kernel, dim3(slow_blocks), dim3(FDGPU_BLOCK), 0, stream, d_ws, d_perm, d_sig_codes,
-                     queue, cnt, slow_blocks * FDGPU_BLOCK, nullptr);
-  return hipGetLastError();
-#endif
-  if (d_n_sig) return hipErrorInvalidValue;                  /* device-side counts: half-size path only */
-  hipLaunchKernelGGL(fdgpu_verify_ra_kernel, dim3(grid), dim3(FDGPU_BLOCK), 0, stream, d_arena, d_sigs, n_sig, d_btab,
-                     d_ws, wg_tot, queue, cnt, flags);
-  const uint32_t inv_blocks = (grid + FDGPU_BLOCK - 1) / FDGPU_BLOCK;
-  hipLaunchKernelGGL(fdgpu_tail_kernel, dim3(slow_blocks + inv_blocks), dim3(FDGPU_BLOCK), 0, stream, d_arena,
-                     d_sigs, d_ws, d_perm, d_sig_codes, queue, cnt, wg_tot, wg_inv, grid, slow_blocks, flags);
-  hipLaunchKernelGGL(fdgpu_finish_kernel, dim3(grid), dim3(FDGPU_BLOCK), 0, stream, d_arena, d_sigs, n_sig, d_ws,
-                     wg_inv, d_perm, d_sig_codes);
+                     queue, cnt, slow_blocks * FDGPU_BLOCK, key_of);
   return hipGetLastError();
 }
 

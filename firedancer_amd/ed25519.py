@@ -54,6 +54,16 @@ def verify_batch_single_msg(msg, signatures, pubkeys, shas, batch_sz):
     return _lib.lib().fd_ed25519_verify_batch_single_msg(msg, len(msg), signatures, pubkeys, None, n)
 
 
+def sync_stats():
+    """Counters of the synchronous API (fdgpu_sync_stats): calls, the GPU
+    batches concurrent calls were coalesced into, engine failures answered
+    with ERR_SIG."""
+    import ctypes as c
+    v = [c.c_uint64() for _ in range(3)]
+    _lib.lib().fdgpu_sync_stats(*[c.byref(x) for x in v])
+    return {"calls": v[0].value, "batches": v[1].value, "errors": v[2].value}
+
+
 def strerror(err):
     """fd_ed25519_strerror."""
     return _lib.lib().fd_ed25519_strerror(int(err)).decode()

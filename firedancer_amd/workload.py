@@ -39,9 +39,42 @@ def gen():
     return _GEN
 
 
-# A GPU box gives one GPU's share of the host, 16 CPUs (os.cpu_count() and
-# the affinity mask show the whole machine there): worker pools stay within it.
-BOX_CPU_SHARE = 16
+def cpu_share_evidence():
+    """What bounds this process's CPU use, as read on the host: the cgroup v2
+    quota (/sys/fs/cgroup/cpu.max, quota/period CPUs), the affinity mask, and
+    the thread limit the environment sets (a GPU box sets OMP_NUM_THREADS to
+    its one-GPU share, 16, while os.cpu_count() and the affinity mask show the
+    whole machine).  share = the quota when one is set, else
+    OMP_NUM_THREADS, else 16; never more than the affinity mask."""
+    ev = {}
+    try:
+        q = open("/sys/fs/cgroup/cpu.max").read().split()
+        ev["cgroup_cpu_max"] = " ".join(q)
+        if q and q[0] != "max":
+            ev["cgroup_quota_cpus"] = int(q[0]) / int(q[1])
+    except (OSError, ValueError, IndexError):
+        ev["cgroup_cpu_max"] = None
+    try:
+        ev["affinity_cpus"] = len(os.sched_getaffinity(0))
+    except AttributeError:
+        ev["affinity_cpus"] = os.cpu_count() or 1
+    ev["os_cpu_count"] = os.cpu_count()
+    omp = os.environ.get("OMP_NUM_THREADS", "")
+    ev["OMP_NUM_THREADS"] = omp or None
+    if ev.get("cgroup_quota_cpus"):
+        share, src = int(ev["cgroup_quota_cpus"]), "cgroup cpu.max quota"
+    elif omp.isdigit() and int(omp) > 0:
+        share, src = int(omp), "OMP_NUM_THREADS"
+    else:
+        share, src = 16, "default one-GPU share (16)"
+    ev["share"] = max(1, min(share, ev["affinity_cpus"]))
+    ev["share_source"] = src
+    return ev
+
+
+# A GPU box gives one GPU's share of the host (cpu_share_evidence): worker
+# pools stay within it.
+BOX_CPU_SHARE = cpu_share_evidence()["share"]
 
 
 def default_threads():

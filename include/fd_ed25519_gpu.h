@@ -10,14 +10,21 @@
                                             (impl fd_ed25519_user.c:232-310)
          fd_ed25519_strerror                replaces src/ballet/ed25519/fd_ed25519.h:132-136
                                             (impl fd_ed25519_user.c:312-322)
-       A compatibility shim served by the GPU engine (device 0, opened on
-       first use); results are bit-identical to the reference's AVX-512
-       build.  Each call is one serialised GPU round trip (tens of
-       microseconds): correct, but hot callers belong on the batch API below.
+       Served by the GPU engine (device 0, opened on first use); results
+       are bit-identical to the reference's AVX-512 build.
+       LATENCY: each call is one GPU round trip, about 1 ms (the lifetime of
+       the verify kernel's one wave; bench.py `sync_call_latency_*`), against
+       ~33 us for the reference's CPU verify.  Concurrent callers are
+       coalesced into one batch per round trip (group commit), so throughput
+       grows with the number of calling threads.  Latency-bound callers
+       (TLS handshakes, gossip, repair, the precompile) should keep the
+       reference's CPU fd_ed25519_verify; INTEGRATION.md 1 shows how both
+       link into one process (the fdgpu_ed25519_* names below).
        The caller thread's current HIP device is preserved.  The reference
-       API returns verify codes only, so an engine failure (no GPU, a HIP
-       error) ABORTS the process rather than return a verdict nothing
-       computed.
+       API returns verify codes only: on an engine failure (no GPU, a HIP
+       error) every call of the failed batch returns FD_ED25519_ERR_SIG
+       (fail closed) and fdgpu_sync_errors() counts it; FDGPU_SYNC_ABORT=1 in
+       the environment makes such a failure abort the process instead.
 
    (ii) Asynchronous batch API for the verify stage (the north-star shim;
        SURVEY.md §8(b)(ii)).  One engine per GPU; each engine owns pinned,
@@ -27,8 +34,9 @@
        verify tile's fd_txn_verify call, src/app/fdctl/run/tiles/fd_verify.h:75).
        Result per transaction: exactly the code the reference would return.
 
-   Threading: an engine is not thread-safe; use one host thread per engine
-   (one engine per GPU).  The synchronous API serialises on an internal lock. */
+   Threading: the ring API (submit / stage / poll / release / register) is
+   thread-safe per engine; the synchronous API is thread-safe and coalesces
+   concurrent calls. */
 #ifndef FD_ED25519_GPU_H
 #define FD_ED25519_GPU_H
 
@@ -66,6 +74,19 @@ int fd_ed25519_verify_batch_single_msg( uint8_t const   msg[],
                                         uint8_t const   batch_sz );
 
 char const * fd_ed25519_strerror( int err );
+
+/* The same two calls under engine-prefixed names, so a process can link the
+   reference's CPU fd_ed25519_user.c for its latency-bound callers and call
+   the GPU from its batch callers (no symbol clash). */
+int fdgpu_ed25519_verify( uint8_t const msg[], uint64_t msg_sz, uint8_t const sig[ 64 ],
+                          uint8_t const public_key[ 32 ] );
+int fdgpu_ed25519_verify_batch_single_msg( uint8_t const msg[], uint64_t msg_sz, uint8_t const signatures[ 64 ],
+                                           uint8_t const pubkeys[ 32 ], uint8_t batch_sz );
+/* Counters of the synchronous API: calls, GPU batches they were coalesced
+   into, and engine failures answered with FD_ED25519_ERR_SIG (any out
+   pointer may be NULL). */
+void     fdgpu_sync_stats( uint64_t * calls, uint64_t * batches, uint64_t * errors );
+uint64_t fdgpu_sync_errors( void );
 
 /* ----------------------------------------------------------------- (ii) */
 
@@ -226,7 +247,7 @@ int  fdgpu_dev_batch_time( fdgpu_engine_t * e, fdgpu_dev_batch_t * b, int iters,
    an exclusive scan of the signature counts, the per-signature expansion,
    the verify kernels and the batch_single_msg combine.  Nothing is parsed
    or expanded on the host.  A payload that is not a transaction gets
-   FDGPU_CODE_PARSE_FAIL instead of a verify code.  Half-size build only. */
+   FDGPU_CODE_PARSE_FAIL instead of a verify code. */
 typedef struct {
   uint32_t off;
   uint32_t sz;          /* <= FD_TXN_MTU (1232) to parse */

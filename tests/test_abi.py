@@ -21,7 +21,7 @@ def test_exports_every_header_function():
     names = _lib.header_functions()
     for fn in REF_API:
         assert fn in names
-    assert len(names) == 37, names
+    assert len(names) == 41, names
     L = _lib.lib()
     for n in names:
         assert hasattr(L, n), n
@@ -95,3 +95,14 @@ def test_engine_flags_match_header():
     py = {"REF_MAPPING": ed.FLAG_REF_MAPPING, "NO_BUCKET": ed.FLAG_NO_BUCKET, "FULL_PATH": ed.FLAG_FULL_PATH,
           "KEY_CACHE": ed.FLAG_KEY_CACHE}
     assert hdr == py, (hdr, py)
+
+
+def test_stamps_variant_builds():
+    """The one kernel variant kept (per-phase stamps for tools/phase_stamps.py)
+    still compiles for gfx950 and exports its stamp reader."""
+    csrc = os.path.join(os.path.dirname(_lib.HEADER_PATH), "..", "firedancer_amd", "csrc")
+    r = subprocess.run(["make", "-C", csrc, "stamps"], capture_output=True, text=True)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    so = os.path.join(os.path.dirname(_lib.HEADER_PATH), "..", "build", "stamps", "libfd_ed25519_gpu.so")
+    out = subprocess.run(["nm", "-D", "--defined-only", so], capture_output=True, text=True, check=True).stdout
+    assert "fdgpu_debug_stamps" in out and "fdgpu_submit" in out

@@ -1,6 +1,6 @@
-"""Per-phase cycle breakdown of fdgpu_verify_ra_kernel (diagnostic build).
+"""Per-phase cycle breakdown of fdgpu_verify_hs_kernel (diagnostic build).
 
-    bash tools/build_variant.sh stamps -DFDGPU_PHASE_STAMPS=1
+    make -C firedancer_amd/csrc stamps
     FDGPU_LIB=build/stamps/libfd_ed25519_gpu.so python tools/phase_stamps.py [--txns N] [--out f.json]
 
 Lane 0 of every wave stamps the shader clock at the phase boundaries of
@@ -20,9 +20,7 @@ import numpy as np
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, REPO)
 
-PHASES = {"ra": ["sha512 + loads", "mod L + recode + S check", "comb [S]B", "decode A + small order",
-                  "A table", "dsm_k ([k](-A) + [S]B)", "y check + Z scan + park"],
-          "hs": ["sha512 + loads", "mod L + S check", "decode A + A table", "decode R + R table",
+PHASES = {"hs": ["sha512 + loads", "mod L + S check", "decode A + A table", "decode R + R table",
                  "lattice split + recode", "w = vS mod L + comb [w]B", "chain + check"]}
 
 
@@ -30,7 +28,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--txns", type=int, default=1_000_000)
     ap.add_argument("--out", default=None)
-    ap.add_argument("--path", choices=("ra", "hs"), default="hs", help="kernel path of the stamped build")
+    ap.add_argument("--path", choices=("hs",), default="hs", help="kernel path of the stamped build")
     args = ap.parse_args()
     import firedancer_amd as fa
     from firedancer_amd import _lib, workload
