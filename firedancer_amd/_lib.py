@@ -108,6 +108,10 @@ def lib():
     L.fdgpu_dev_batch_time.restype = c.c_int
     L.fdgpu_sync.argtypes = [vp]
     L.fdgpu_sync.restype = c.c_int
+    L.fdgpu_submit_frags.argtypes = [vp, vp, c.c_uint64, vp, c.c_uint64, c.c_uint64]
+    L.fdgpu_submit_frags.restype = c.c_int64
+    L.fdgpu_poll_frags.argtypes = [vp, c.c_int64, vp, vp, c.c_int]
+    L.fdgpu_poll_frags.restype = c.c_int
     L.fdgpu_ed25519_verify.argtypes = [u8p, c.c_uint64, u8p, u8p]
     L.fdgpu_ed25519_verify.restype = c.c_int
     L.fdgpu_ed25519_verify_batch_single_msg.argtypes = [u8p, c.c_uint64, u8p, u8p, c.c_uint8]

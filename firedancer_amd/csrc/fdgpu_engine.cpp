@@ -31,6 +31,8 @@
 #include "../../include/fd_ed25519_gpu.h"
 #include "fdgpu_internal.h"
 
+#define FDT_TXN_MAX_SZ_BYTES 852u   /* FD_TXN_MAX_SZ (fd_txn.h:98): one parsed fd_txn_t record */
+
 namespace {
 
 thread_local std::string g_err;
@@ -64,6 +66,16 @@ struct Slot {
   uint32_t *h_flag = nullptr, *d_flag = nullptr;
   uint32_t flag_seq = 0;
   uint32_t polls = 0;         /* non-blocking polls of the current batch (stream error checks) */
+  /* frag batches (fdgpu_submit_frags): GPU-side parse buffers, allocated on
+     the slot's first frag batch; the trailer buffers grow to the batches */
+  bool frag = false;          /* the batch in flight is a frag batch */
+  fdgpu_frag_ex_t *h_fx = nullptr, *d_fx = nullptr;
+  uint8_t *d_txn_out = nullptr;
+  uint16_t *d_txn_sz = nullptr;
+  fdgpu_txn_t *d_txd = nullptr;
+  uint32_t *d_cnt = nullptr, *d_sig0 = nullptr, *d_blocktot = nullptr, *d_n_sig = nullptr;
+  uint8_t *d_tr = nullptr, *h_tr = nullptr;
+  uint64_t tr_cap = 0, tr_sz = 0;
 };
 
 }  // namespace
@@ -116,6 +128,11 @@ void slot_free(Slot &s) {
   if (s.d_sig_codes) (void)hipFree(s.d_sig_codes);
   if (s.d_ws) (void)hipFree(s.d_ws);
   if (s.h_flag) (void)hipHostFree(s.h_flag);
+  if (s.h_fx) (void)hipHostFree(s.h_fx);
+  if (s.h_tr) (void)hipHostFree(s.h_tr);
+  for (void *p : {(void *)s.d_fx, (void *)s.d_txn_out, (void *)s.d_txn_sz, (void *)s.d_txd, (void *)s.d_cnt,
+                  (void *)s.d_sig0, (void *)s.d_blocktot, (void *)s.d_n_sig, (void *)s.d_tr})
+    if (p) (void)hipFree(p);
   s = Slot{};
 }
 
@@ -161,6 +178,34 @@ bool slot_ws(Slot &s, uint64_t n_sig) {
     return true;
   }
   s.ws_sig = want ? want : 1;
+  return true;
+}
+
+/* The slot's GPU-side parse buffers (first frag batch) and a trailer
+   buffer of at least tr bytes (the slot is free: nothing reads them). */
+bool slot_frag_bufs(Slot &s, const fdgpu_cfg_t &c, uint64_t tr) {
+  if (!s.d_fx) {
+    const uint64_t n = c.max_txn + 1, nb = (c.max_txn + 1023) / 1024 + 2;
+    HIPCHK(hipHostMalloc((void **)&s.h_fx, n * sizeof(fdgpu_frag_ex_t), hipHostMallocDefault), false);
+    HIPCHK(hipMalloc((void **)&s.d_fx, n * sizeof(fdgpu_frag_ex_t)), false);
+    HIPCHK(hipMalloc((void **)&s.d_txn_out, n * FDT_TXN_MAX_SZ_BYTES), false);
+    HIPCHK(hipMalloc((void **)&s.d_txn_sz, n * sizeof(uint16_t)), false);
+    HIPCHK(hipMalloc((void **)&s.d_txd, n * sizeof(fdgpu_txn_t)), false);
+    HIPCHK(hipMalloc((void **)&s.d_cnt, n * sizeof(uint32_t)), false);
+    HIPCHK(hipMalloc((void **)&s.d_sig0, n * sizeof(uint32_t)), false);
+    HIPCHK(hipMalloc((void **)&s.d_blocktot, nb * sizeof(uint32_t)), false);
+    HIPCHK(hipMalloc((void **)&s.d_n_sig, sizeof(uint32_t)), false);
+  }
+  if (tr > s.tr_cap) {
+    HIPCHK(hipStreamSynchronize(s.stream), false);
+    if (s.d_tr) { (void)hipFree(s.d_tr); s.d_tr = nullptr; }
+    if (s.h_tr) { (void)hipHostFree(s.h_tr); s.h_tr = nullptr; }
+    s.tr_cap = 0;
+    const uint64_t want = std::max<uint64_t>(tr, 64 * 1024);
+    HIPCHK(hipMalloc((void **)&s.d_tr, want), false);
+    HIPCHK(hipHostMalloc((void **)&s.h_tr, want, hipHostMallocDefault), false);
+    s.tr_cap = want;
+  }
   return true;
 }
 
@@ -432,6 +477,7 @@ static int64_t submit_slot(fdgpu_engine_t *e, Slot *s, uint64_t arena_sz, fdgpu_
   s->staged = false;
   s->held = false;
   s->polls = 0;
+  s->frag = false;
   s->ticket = e->next_ticket++;
   s->txn_cnt = txn_cnt;
   return s->ticket;
@@ -515,7 +561,8 @@ int64_t fdgpu_stage_submit(fdgpu_engine_t *e, uint64_t arena_sz, fdgpu_txn_t con
   return submit_slot(e, s, arena_sz, txns, txn_cnt);
 }
 
-static int poll_slot(fdgpu_engine_t *e, int64_t ticket, int8_t *txn_codes, int blocking, bool keep) {
+static int poll_slot(fdgpu_engine_t *e, int64_t ticket, int8_t *txn_codes, int blocking, bool keep,
+                     uint8_t *trailers = nullptr) {
   if (!e) return FDGPU_ERR_INVAL;
   std::unique_lock<std::mutex> lk(e->ring_mu);
   Slot *s = nullptr;
@@ -545,6 +592,7 @@ static int poll_slot(fdgpu_engine_t *e, int64_t ticket, int8_t *txn_codes, int b
     HIPCHK(q, FDGPU_ERR_DEVICE);
   }
   if (txn_codes && s->txn_cnt) memcpy(txn_codes, s->h_codes, s->txn_cnt);
+  if (trailers && s->frag && s->tr_sz) memcpy(trailers, s->h_tr, s->tr_sz);
   if (keep) s->held = true;
   else s->ticket = -1;
   return FDGPU_OK;
@@ -556,6 +604,74 @@ int fdgpu_poll(fdgpu_engine_t *e, int64_t ticket, int8_t *txn_codes, int blockin
 
 int fdgpu_poll_keep(fdgpu_engine_t *e, int64_t ticket, int8_t *txn_codes, int blocking) {
   return poll_slot(e, ticket, txn_codes, blocking, true);
+}
+
+int fdgpu_poll_frags(fdgpu_engine_t *e, int64_t ticket, int8_t *codes, uint8_t *trailers, int blocking) {
+  return poll_slot(e, ticket, codes, blocking, false, trailers);
+}
+
+/* fdgpu_submit with the parse on the device: upload (DMA from a registered
+   region, or staged), then on the slot's stream parse -> scan -> expand ->
+   verify -> combine -> parse-failure codes -> trailer pack, and the codes and
+   trailers back to pinned memory. */
+int64_t fdgpu_submit_frags(fdgpu_engine_t *e, uint8_t const *arena, uint64_t arena_sz, fdgpu_frag_ex_t const *fx,
+                           uint64_t n, uint64_t trailer_sz) {
+  if (!e || (!arena && arena_sz) || (!fx && n)) { set_err("null argument"); return FDGPU_ERR_INVAL; }
+  if (arena_sz > e->cfg.max_arena || n > e->cfg.max_txn) { set_err("batch exceeds engine limits"); return FDGPU_ERR_INVAL; }
+  if (trailer_sz > (uint64_t)n * FDT_TXN_MAX_SZ_BYTES + 4) { set_err("trailer buffer larger than the frags' maximum"); return FDGPU_ERR_INVAL; }
+  uint64_t bound = 0;
+  for (uint64_t t = 0; t < n; t++) {
+    const fdgpu_frag_ex_t &f = fx[t];
+    if ((uint64_t)f.off + f.sz > arena_sz || (f.tr_off & 3u) || (uint64_t)f.tr_off + f.tr_cap > trailer_sz ||
+        f.tr_cap > FDT_TXN_MAX_SZ_BYTES) {
+      set_err("frag %llu: out of arena or trailer bounds", (unsigned long long)t);
+      return FDGPU_ERR_INVAL;
+    }
+    bound += fdgpu_frag_sig_bound(f.sz);
+  }
+  if (bound > e->cfg.max_sig) { set_err("batch may exceed max_sig (%llu)", (unsigned long long)e->cfg.max_sig); return FDGPU_ERR_INVAL; }
+  std::lock_guard<std::mutex> lk(e->ring_mu);
+  HIPCHK(hipSetDevice(e->device), FDGPU_ERR_DEVICE);
+  Slot *s = free_slot(e);
+  if (!s) { set_err("all ring slots hold unpolled batches"); return FDGPU_ERR_FULL; }
+  if (!slot_frag_bufs(*s, e->cfg, trailer_sz) || !slot_ws(*s, bound)) return FDGPU_ERR_DEVICE;
+  if (region_covers(e, arena, arena_sz)) {
+    if (arena_sz) HIPCHK(hipMemcpyAsync(s->d_arena, arena, arena_sz, hipMemcpyHostToDevice, s->stream), FDGPU_ERR_DEVICE);
+    HIPCHK(hipMemsetAsync(s->d_arena + arena_sz, 0, FDGPU_ARENA_SLACK, s->stream), FDGPU_ERR_DEVICE);
+  } else {
+    const uint64_t up = stage_arena(e, s, arena, arena_sz);
+    if (up == UINT64_MAX) return FDGPU_ERR_DEVICE;
+    memset(s->h_arena + arena_sz, 0, FDGPU_ARENA_SLACK);
+    HIPCHK(hipMemcpyAsync(s->d_arena + up, s->h_arena + up, arena_sz + FDGPU_ARENA_SLACK - up, hipMemcpyHostToDevice,
+                          s->stream), FDGPU_ERR_DEVICE);
+  }
+  if (n) {
+    memcpy(s->h_fx, fx, n * sizeof(fdgpu_frag_ex_t));
+    HIPCHK(hipMemcpyAsync(s->d_fx, s->h_fx, n * sizeof(fdgpu_frag_ex_t), hipMemcpyHostToDevice, s->stream), FDGPU_ERR_DEVICE);
+    HIPCHK(fdgpu_launch_frag_ingest(s->d_arena, s->d_fx, 4u, (uint32_t)n, s->d_txn_out, s->d_txn_sz, s->d_txd, s->d_cnt,
+                                    s->d_sig0, s->d_blocktot, s->d_n_sig, s->d_sigs, s->d_txns, s->stream),
+           FDGPU_ERR_DEVICE);
+    HIPCHK(fdgpu_launch_verify_sigs(s->d_arena, s->d_sigs, (uint32_t)bound, nullptr, e->d_btab, s->d_ws, s->d_sig_codes,
+                                    kflags(e), s->stream, s->d_n_sig, e->resident_blocks, e->kc_seed),
+           FDGPU_ERR_DEVICE);
+    HIPCHK(fdgpu_launch_combine(s->d_txns, (uint32_t)n, s->d_sig_codes, s->d_txn_codes, nullptr, s->stream), FDGPU_ERR_DEVICE);
+    HIPCHK(fdgpu_launch_frag_codes(s->d_txn_sz, (uint32_t)n, s->d_txn_codes, s->stream), FDGPU_ERR_DEVICE);
+    HIPCHK(fdgpu_launch_trailer_pack(s->d_fx, (uint32_t)n, s->d_txn_out, s->d_txn_sz, s->d_tr, s->d_txn_codes, s->stream),
+           FDGPU_ERR_DEVICE);
+    HIPCHK(hipMemcpyAsync(s->h_codes, s->d_txn_codes, n, hipMemcpyDeviceToHost, s->stream), FDGPU_ERR_DEVICE);
+    if (trailer_sz) HIPCHK(hipMemcpyAsync(s->h_tr, s->d_tr, trailer_sz, hipMemcpyDeviceToHost, s->stream), FDGPU_ERR_DEVICE);
+  }
+  ++s->flag_seq;
+  if (e->flag_poll && !e->drop_flag) HIPCHK(hipStreamWriteValue32(s->stream, s->d_flag, s->flag_seq, 0), FDGPU_ERR_DEVICE);
+  HIPCHK(hipEventRecord(s->done, s->stream), FDGPU_ERR_DEVICE);
+  s->staged = false;
+  s->held = false;
+  s->polls = 0;
+  s->frag = true;
+  s->tr_sz = trailer_sz;
+  s->ticket = e->next_ticket++;
+  s->txn_cnt = n;
+  return s->ticket;
 }
 
 int fdgpu_stage_cancel(fdgpu_engine_t *e) {
@@ -815,7 +931,7 @@ fdgpu_dev_batch_t *fdgpu_dev_batch_upload_frags(fdgpu_engine_t *e, uint8_t const
 
 /* the ingest kernels of a frag batch (parse -> scan -> expand) on st */
 static int enqueue_ingest(fdgpu_dev_batch_t *b, hipStream_t st) {
-  HIPCHK(fdgpu_launch_frag_ingest(b->d_arena, b->d_frags, (uint32_t)b->n_txn, b->d_txn_out, b->d_txn_sz, b->d_txd,
+  HIPCHK(fdgpu_launch_frag_ingest(b->d_arena, b->d_frags, 2u, (uint32_t)b->n_txn, b->d_txn_out, b->d_txn_sz, b->d_txd,
                                   b->d_cnt, b->d_sig0, b->d_blocktot, b->d_n_sig, b->d_sigs, b->d_txns, st),
          FDGPU_ERR_DEVICE);
   return FDGPU_OK;

@@ -98,11 +98,18 @@ hipError_t fdgpu_launch_test_sc_reduce(const uint32_t *d_in, uint32_t *d_out, ui
    d_txd / d_cnt / d_sig0 / d_tds n entries, d_blocktot ceil(n / 1024),
    d_sigs the sum of fdgpu_frag_sig_bound over the frags. */
 uint64_t   fdgpu_frag_sig_bound(uint32_t sz);
-hipError_t fdgpu_launch_frag_ingest(const uint8_t *d_arena, const fdgpu_frag_t *d_frags, uint32_t n,
+/* d_frags: n records of frag_stride u32 words whose first two are {off, sz}
+   (fdgpu_frag_t: 2, fdgpu_frag_ex_t: 4) */
+hipError_t fdgpu_launch_frag_ingest(const uint8_t *d_arena, const void *d_frags, uint32_t frag_stride, uint32_t n,
                                     uint8_t *d_txn_out, uint16_t *d_txn_sz, fdgpu_txn_t *d_txd, uint32_t *d_cnt,
                                     uint32_t *d_sig0, uint32_t *d_blocktot, uint32_t *d_n_sig,
                                     fdgpu_sig_desc_t *d_sigs, fdgpu_txn_desc_t *d_tds, hipStream_t stream);
 hipError_t fdgpu_launch_frag_codes(const uint16_t *d_txn_sz, uint32_t n, int8_t *d_codes, hipStream_t stream);
+/* fdgpu_submit_frags: parsed fd_txn_t records (stride FDT_TXN_MAX_SZ in
+   d_txn_out) to their reserved places in d_trailers; a footprint other than
+   the reservation -> FDGPU_CODE_TRAILER_CAP in d_codes */
+hipError_t fdgpu_launch_trailer_pack(const fdgpu_frag_ex_t *d_fx, uint32_t n, const uint8_t *d_txn_out,
+                                     const uint16_t *d_txn_sz, uint8_t *d_trailers, int8_t *d_codes, hipStream_t stream);
 hipError_t fdgpu_launch_test_hs_split(const uint32_t *d_in, uint32_t *d_out, uint32_t n, hipStream_t stream);
 
 #ifdef __cplusplus

@@ -902,21 +902,22 @@ __global__ void __launch_bounds__(64) fdgpu_test_sc_reduce_kernel(const uint32_t
    of a batch from its frag sizes alone (fdgpu_frag_sig_bound). */
 #define FDGPU_SCAN_BLOCK 1024u      /* txns per scan block: 256 threads x 4 */
 
-FDG_DEV uint32_t frag_sig_bound(uint32_t sz) { return sz >= 134u ? min(16u, (sz - 38u) / 96u) : 0u; }
 
+/* frag t's {off, sz} are the first two words of a record of `stride` words
+   (fdgpu_frag_t: 2, fdgpu_frag_ex_t: 4) */
 __global__ void __launch_bounds__(64) fdgpu_frag_parse_kernel(
-    const uint8_t *__restrict__ arena, const fdgpu_frag_t *__restrict__ frags, uint32_t n,
+    const uint8_t *__restrict__ arena, const uint32_t *__restrict__ frags, uint32_t stride, uint32_t n,
     uint8_t *__restrict__ txn_out, uint16_t *__restrict__ txn_sz, fdgpu_txn_t *__restrict__ txd,
     uint32_t *__restrict__ cnt) {
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= n) return;
-  const fdgpu_frag_t f = frags[t];
+  const fdgpu_frag_t f = *(const fdgpu_frag_t *)(frags + (size_t)t * stride);
   fdt_txn_t *x = (fdt_txn_t *)(txn_out + (size_t)t * FDT_TXN_MAX_SZ);
   uint64_t why = 0;
   uint64_t fp = fdt_parse_core(arena + f.off, f.sz, x, &why);
   const uint32_t sc = fp ? x->signature_cnt : 0u;
   uint32_t c = (sc >= 1u && sc <= 16u) ? sc : 0u;
-  if (c > frag_sig_bound(f.sz)) { c = 0u; fp = 0u; }       /* cannot happen for a parsed txn (see above) */
+  if (c > fdt_frag_sig_bound(f.sz)) { c = 0u; fp = 0u; }       /* cannot happen for a parsed txn (see above) */
   fdgpu_txn_t d;
   d.msg_off = fp ? f.off + x->message_off : f.off;
   d.msg_sz = fp ? f.sz - x->message_off : 0u;
@@ -1010,6 +1011,28 @@ __global__ void __launch_bounds__(256) fdgpu_frag_expand_kernel(
     sd.pub_off = d.pub_off + 32u * j;
     sigs[s0 + j] = sd;
   }
+}
+
+/* Ring-slot frag batches (fdgpu_submit_frags): each parsed fd_txn_t goes to
+   the caller's trailer buffer at its reserved place, whose size the caller
+   derived from the payload's counts (fdt_txn_peek); a footprint other than
+   the reservation (only a caller bug can cause one) gets
+   FDGPU_CODE_TRAILER_CAP instead of a verify code.  Lane per frag; tr_off is
+   4-byte aligned, the txn record starts a 852-B (4-aligned) stride. */
+__global__ void __launch_bounds__(256) fdgpu_trailer_pack_kernel(const fdgpu_frag_ex_t *__restrict__ fx, uint32_t n,
+                                                                 const uint8_t *__restrict__ txn_out,
+                                                                 const uint16_t *__restrict__ txn_sz,
+                                                                 uint8_t *__restrict__ trailers,
+                                                                 int8_t *__restrict__ codes) {
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= n) return;
+  const uint32_t fp = txn_sz[t];
+  if (!fp) return;                                        /* not a transaction: PARSE_FAIL already */
+  const fdgpu_frag_ex_t f = fx[t];
+  if (fp != f.tr_cap) { codes[t] = (int8_t)FDGPU_CODE_TRAILER_CAP; return; }
+  const uint32_t *src = (const uint32_t *)(txn_out + (size_t)t * FDT_TXN_MAX_SZ);
+  uint32_t *dst = (uint32_t *)(trailers + f.tr_off);
+  for (uint32_t w = 0; w < (fp + 3u) / 4u; w++) dst[w] = src[w];
 }
 
 /* After the combine: a payload that did not parse gets FDGPU_CODE_PARSE_FAIL */
@@ -1158,15 +1181,16 @@ hipError_t fdgpu_launch_test_sc_reduce(const uint32_t *d_in, uint32_t *d_out, ui
   hipLaunchKernelGGL(fdgpu_test_sc_reduce_kernel, dim3((n + 63) / 64), dim3(64), 0, stream, d_in, d_out, n);
   return hipGetLastError();
 }
-uint64_t fdgpu_frag_sig_bound(uint32_t sz) { return sz >= 134u ? (sz - 38u) / 96u < 16u ? (sz - 38u) / 96u : 16u : 0u; }
+uint64_t fdgpu_frag_sig_bound(uint32_t sz) { return fdt_frag_sig_bound(sz); }
 
-hipError_t fdgpu_launch_frag_ingest(const uint8_t *d_arena, const fdgpu_frag_t *d_frags, uint32_t n,
+hipError_t fdgpu_launch_frag_ingest(const uint8_t *d_arena, const void *d_frags, uint32_t frag_stride, uint32_t n,
                                     uint8_t *d_txn_out, uint16_t *d_txn_sz, fdgpu_txn_t *d_txd, uint32_t *d_cnt,
                                     uint32_t *d_sig0, uint32_t *d_blocktot, uint32_t *d_n_sig,
                                     fdgpu_sig_desc_t *d_sigs, fdgpu_txn_desc_t *d_tds, hipStream_t stream) {
   if (!n) return hipMemsetAsync(d_n_sig, 0, sizeof(uint32_t), stream);
   const uint32_t nb = (n + FDGPU_SCAN_BLOCK - 1) / FDGPU_SCAN_BLOCK;
-  hipLaunchKernelGGL(fdgpu_frag_parse_kernel, dim3((n + 63) / 64), dim3(64), 0, stream, d_arena, d_frags, n, d_txn_out,
+  hipLaunchKernelGGL(fdgpu_frag_parse_kernel, dim3((n + 63) / 64), dim3(64), 0, stream, d_arena,
+                     (const uint32_t *)d_frags, frag_stride, n, d_txn_out,
                      d_txn_sz, d_txd, d_cnt);
   hipLaunchKernelGGL(fdgpu_scan_local_kernel, dim3(nb), dim3(256), 0, stream, d_cnt, n, d_sig0, d_blocktot);
   hipLaunchKernelGGL(fdgpu_scan_blocks_kernel, dim3(1), dim3(1024), 0, stream, d_blocktot, nb, d_n_sig);
@@ -1178,6 +1202,14 @@ hipError_t fdgpu_launch_frag_ingest(const uint8_t *d_arena, const fdgpu_frag_t *
 hipError_t fdgpu_launch_frag_codes(const uint16_t *d_txn_sz, uint32_t n, int8_t *d_codes, hipStream_t stream) {
   if (!n) return hipSuccess;
   hipLaunchKernelGGL(fdgpu_frag_codes_kernel, dim3((n + 255) / 256), dim3(256), 0, stream, d_txn_sz, n, d_codes);
+  return hipGetLastError();
+}
+
+hipError_t fdgpu_launch_trailer_pack(const fdgpu_frag_ex_t *d_fx, uint32_t n, const uint8_t *d_txn_out,
+                                     const uint16_t *d_txn_sz, uint8_t *d_trailers, int8_t *d_codes, hipStream_t stream) {
+  if (!n) return hipSuccess;
+  hipLaunchKernelGGL(fdgpu_trailer_pack_kernel, dim3((n + 255) / 256), dim3(256), 0, stream, d_fx, n, d_txn_out,
+                     d_txn_sz, d_trailers, d_codes);
   return hipGetLastError();
 }
 

@@ -47,6 +47,13 @@
 #define FDT_PF_TOTAL_ACCTS    18u
 #define FDT_PF_ACCT_IDX       19u
 
+/* A valid txn with s signatures is at least 96 s + 38 bytes (s signatures,
+   s signer keys, the blockhash, the counts): an upper bound on the
+   signatures a frag of sz bytes can send to the verifier. */
+FDT_HD uint32_t fdt_frag_sig_bound(uint64_t sz) {
+  return sz >= 134u ? (uint32_t)((sz - 38u) / 96u < 16u ? (sz - 38u) / 96u : 16u) : 0u;
+}
+
 FDT_HD uint64_t fdt_parse_footprint(uint64_t instr_cnt, uint64_t lut_cnt) {
   return sizeof(fdt_txn_t) + instr_cnt * sizeof(fdt_txn_instr_t) + lut_cnt * sizeof(fdt_txn_acct_addr_lut_t);
 }
@@ -242,5 +249,41 @@ FDT_HD uint64_t fdt_parse_core(const uint8_t *payload, uint64_t payload_sz, fdt_
     fp = fdt_parse_footprint(instr_cnt, lut_cnt);
   } while (0);
   if (fail) *fail = fp ? 0u : (r.fail ? r.fail : FDT_PF_SHORT);
+  return fp;
+}
+
+/* The footprint fdt_parse_core would return for this payload if it parses,
+   read from the counts alone (signature, account, instruction and lookup
+   table counts; for v0 the instruction list is walked to reach the table
+   count) with none of the structural checks: the same reads of the same
+   bytes as the parser, so whenever the payload is a valid transaction the
+   two agree.  0 when the walk runs past the payload (the parser then fails
+   too).  *sig_cnt gets the leading signature count.  The verify tile uses it
+   to reserve a frag's trailer before the GPU has parsed the frag. */
+FDT_HD uint64_t fdt_peek_core(const uint8_t *payload, uint64_t payload_sz, uint64_t *sig_cnt_out) {
+  fdt_reader r;
+  r.p = payload; r.sz = payload_sz; r.i = 0; r.fail = 0;
+  uint8_t sig_cnt = 0, b0, x;
+  uint16_t acct_cnt, instr_cnt, lut_cnt = 0;
+  uint64_t fp = 0;
+  do {
+    if (payload_sz > FDT_TXN_MTU || !r.u8(sig_cnt) || sig_cnt < 1 || sig_cnt > FDT_TXN_SIG_MAX) break;
+    if (!r.skip(64ULL * sig_cnt) || !r.u8(b0)) break;
+    const bool v0 = (b0 & 0x80) != 0;
+    if (v0 && ((b0 & 0x7f) != FDT_TXN_V0 || !r.u8(x))) break;
+    if (!r.skip(2) || !r.cu16(acct_cnt) || !r.skip(32ULL * acct_cnt + 32) || !r.cu16(instr_cnt) ||
+        instr_cnt > FDT_TXN_INSTR_MAX)
+      break;
+    if (v0) {
+      bool ok = true;
+      for (uint16_t j = 0; j < instr_cnt && ok; j++) {
+        uint16_t n_acct, data_sz;
+        ok = r.u8(x) && r.cu16(n_acct) && r.skip(n_acct) && r.cu16(data_sz) && r.skip(data_sz);
+      }
+      if (!ok || !r.cu16(lut_cnt) || lut_cnt > FDT_TXN_ADDR_TABLE_LOOKUP_MAX) break;
+    }
+    fp = fdt_parse_footprint(instr_cnt, lut_cnt);
+  } while (0);
+  if (sig_cnt_out) *sig_cnt_out = sig_cnt;
   return fp;
 }

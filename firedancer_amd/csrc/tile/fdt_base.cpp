@@ -267,3 +267,9 @@ extern "C" uint64_t fdt_txn_parse(const uint8_t *payload, uint64_t payload_sz, v
   }
   return fp;
 }
+
+/* fdt_peek_core (../fdt_parse.h): the footprint a successful parse would
+   have, from the payload's counts */
+extern "C" uint64_t fdt_txn_peek(const uint8_t *payload, uint64_t payload_sz, uint64_t *sig_cnt) {
+  return fdt_peek_core(payload, payload_sz, sig_cnt);
+}

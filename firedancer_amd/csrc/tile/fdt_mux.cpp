@@ -13,6 +13,7 @@
 #include <vector>
 
 #include "../../../include/fd_verify_tile.h"
+#include "../fdt_parse.h"
 
 namespace {
 
@@ -68,9 +69,10 @@ int fdt_mux_run(const fdt_mux_cfg_t *cfg, const fdt_mux_callbacks_t *cb, void *c
   for (uint64_t j = 0; j < out_cnt; j++) out_seq[j] = ld_acq(cfg->out_fseq[j]);
   uint64_t seq = cfg->out_seq0, cr_avail = 0, cr_filt = 0, in_rr = 0;
   fdt_mux_stats_t st{};
-  for (uint64_t it = 0;; it++) {
+  for (uint64_t hk = 0;; hk--) {
     st.loops++;
-    if (it % lazy == 0) {
+    if (!hk) {
+      hk = lazy;
       /* housekeeping (fd_mux.c:391-491): receive credits from the outs, send
          our position to the ins, user callbacks, halt (the cnc signal) */
       for (uint64_t j = 0; j < out_cnt; j++) out_seq[j] = ld_acq(cfg->out_fseq[j]);
@@ -160,18 +162,23 @@ namespace {
 struct VItem {
   uint64_t seq;
   uint32_t chunk;       /* where [payload][pad][fd_txn_t][u16 sz] lies in the out dcache */
-  uint32_t sz;          /* that frag's size */
+  uint32_t sz;          /* that frag's size (gpu_parse: the payload's; the trailer is added at publish) */
   uint32_t sig_off;     /* signature 0, from the frag start */
   uint32_t tsorig;
+  uint32_t tr_off;      /* gpu_parse: the parsed fd_txn_t's place in the batch's trailer buffer */
+  uint32_t tr_cap;      /*            and its footprint (fdt_txn_peek) */
 };
 
 struct VBatch {
   uint64_t first_chunk = 0;          /* the arena is out_base + first_chunk * 64 ... + end_off */
   uint64_t end_off = 0;
   std::vector<fdgpu_txn_t> txns;
+  std::vector<fdgpu_frag_ex_t> frags;  /* gpu_parse: the verifier's view of the items */
+  std::vector<uint8_t> trailers;      /* gpu_parse: parsed fd_txn_t records, filled by poll_frags */
+  uint64_t tr_used = 0;
   std::vector<VItem> items;
   std::vector<int8_t> codes;
-  uint64_t sig_cnt = 0;
+  uint64_t sig_cnt = 0;               /* signatures sent (gpu_parse: the frags' upper bound) */
   int64_t ticket = -1;
   bool closed = false;               /* takes no more frags (full, or the cursor wrapped) */
   bool done = false;
@@ -179,8 +186,8 @@ struct VBatch {
   uint64_t t_first = 0;
 
   void reset() {
-    first_chunk = end_off = sig_cnt = 0;
-    txns.clear(); items.clear();
+    first_chunk = end_off = sig_cnt = tr_used = 0;
+    txns.clear(); items.clear(); frags.clear();
     ticket = -1; closed = done = false; next = 0; t_first = 0;
   }
 };
@@ -211,11 +218,13 @@ struct fdgpu_vmux {
   std::vector<uint64_t> log_seq;
   std::vector<int8_t> log_code;
 
-  std::atomic<uint64_t> final_cnt{0};    /* frags whose outcome is final (readable from other threads) */
+  bool gpu_parse = false;                /* fd_txn_parse on the GPU (verifier submit_frags / poll_frags) */
+  uint64_t final_n = 0;                   /* frags whose outcome is final ... */
+  std::atomic<uint64_t> final_cnt{0};    /* ... published for other threads (one writer: a store, no RMW) */
 
   void log(uint64_t seq, int code) {
-    if (log_seq.size() < log_max) { log_seq.push_back(seq); log_code.push_back((int8_t)code); }
-    final_cnt.fetch_add(1, std::memory_order_release);
+    if (log_max && log_seq.size() < log_max) { log_seq.push_back(seq); log_code.push_back((int8_t)code); }
+    final_cnt.store(++final_n, std::memory_order_release);
   }
 
   uint8_t *out_laddr(uint64_t chunk) const { return cfg.out_base + (chunk << FDT_CHUNK_LG_SZ); }
@@ -250,17 +259,33 @@ struct fdgpu_vmux {
     while (!inflight.empty()) {
       VBatch *b = inflight.front();
       if (!b->done) {
-        const int rc = ver.poll(ver.ctx, b->ticket, b->codes.data(), 0);
+        const int rc = gpu_parse ? ver.poll_frags(ver.ctx, b->ticket, b->codes.data(), b->trailers.data(), 0)
+                                 : ver.poll(ver.ctx, b->ticket, b->codes.data(), 0);
         if (rc == FDGPU_PENDING) return;
         if (rc != FDGPU_OK) { error = rc; *poll_in = 0; return; }
         b->done = true;
       }
-      while (b->next < b->items.size()) {
-        const VItem &it = b->items[b->next];
-        const uint64_t tag = fdt_hash(cfg.hashmap_seed, out_laddr(it.chunk) + it.sig_off, 64);
+      const uint32_t tspub = (uint32_t)now_ns();
+      const size_t n = b->items.size();
+      while (b->next < n) {
+        const size_t k = b->next;
+        if (k + 8 < n) __builtin_prefetch(out_laddr(b->items[k + 8].chunk));   /* its signature, hashed soon */
+        const VItem &it = b->items[k];
+        const int code = b->codes[k];
+        if (gpu_parse && (code == FDGPU_CODE_PARSE_FAIL || code == FDGPU_CODE_TRAILER_CAP)) {
+          /* not a transaction: filtered before the dedup check (fd_verify.c:
+             117-121); a footprint other than the one reserved: a peek / parse
+             disagreement, failed without a verdict */
+          if (code == FDGPU_CODE_PARSE_FAIL) { st.parse_fail++; log(it.seq, FDGPU_VTILE_LOG_PARSE_FAIL); }
+          else { st.verify_errors++; log(it.seq, FD_TXN_VERIFY_FAILED); }
+          b->next++;
+          continue;
+        }
+        uint8_t *frag = out_laddr(it.chunk);
+        const uint64_t tag = fdt_hash(cfg.hashmap_seed, frag + it.sig_off, 64);
         int outcome;
         if (fdt_tcache_query(tcache, tag)) outcome = FD_TXN_VERIFY_DEDUP;
-        else if (b->codes[b->next] != FD_ED25519_SUCCESS) outcome = FD_TXN_VERIFY_FAILED;
+        else if (code != FD_ED25519_SUCCESS) outcome = FD_TXN_VERIFY_FAILED;
         else outcome = FD_TXN_VERIFY_SUCCESS;
         if (outcome == FD_TXN_VERIFY_SUCCESS) {
           if (mux->cr_decrement_amount && !*mux->cr_avail) {
@@ -269,8 +294,17 @@ struct fdgpu_vmux {
             return;
           }
           (void)fdt_tcache_insert(tcache, tag);   /* not present: the query above missed */
+          uint64_t sz = it.sz;
+          if (gpu_parse) {                        /* [payload][pad][fd_txn_t][u16 payload_sz] (fd_verify.c:93-136) */
+            const uint64_t toff = align2(it.sz);
+            if (toff != it.sz) frag[it.sz] = 0;
+            std::memcpy(frag + toff, b->trailers.data() + it.tr_off, it.tr_cap);
+            const uint16_t psz = (uint16_t)it.sz;
+            std::memcpy(frag + toff + it.tr_cap, &psz, 2);
+            sz = toff + it.tr_cap + 2;
+          }
           pub_chunk[*mux->seq & pub_mask] = it.chunk;
-          fdt_mux_publish(mux, tag, it.chunk, it.sz, 0, it.tsorig, (uint32_t)now_ns());
+          fdt_mux_publish(mux, tag, it.chunk, sz, 0, it.tsorig, tspub);
           published_total++;
           st.published++;
         } else if (outcome == FD_TXN_VERIFY_DEDUP) {
@@ -301,8 +335,14 @@ struct fdgpu_vmux {
     if (!open || open->items.empty()) return;
     if (!open->closed && now_ns() - open->t_first < cfg.batch_wait_ns) return;
     if (inflight.size() >= cfg.inflight_max) return;
-    const int64_t t = ver.submit(ver.ctx, out_laddr(open->first_chunk), open->end_off, open->txns.data(),
-                                 open->txns.size());
+    int64_t t;
+    if (gpu_parse) {
+      if (open->trailers.size() < open->tr_used) open->trailers.resize(open->tr_used);
+      t = ver.submit_frags(ver.ctx, out_laddr(open->first_chunk), open->end_off, open->frags.data(),
+                           open->frags.size(), open->tr_used);
+    } else {
+      t = ver.submit(ver.ctx, out_laddr(open->first_chunk), open->end_off, open->txns.data(), open->txns.size());
+    }
     if (t == FDGPU_ERR_FULL) return;
     if (t == FDGPU_ERR_INVAL) { reject_open(); return; }
     if (t < 0) { error = (int)t; return; }
@@ -362,6 +402,27 @@ void vm_after_frag(void *ctx, uint64_t in_idx, uint64_t seq, uint64_t *opt_sig, 
   const uint64_t payload_sz = *opt_sz;
   uint8_t *txn = t->out_laddr(t->out_chunk);
   const uint64_t toff = align2(payload_sz);
+  if (t->gpu_parse) {
+    /* the GPU parses: reserve the trailer the parse will produce (the
+       payload's counts, fdt_txn_peek) and hand the payload over as a frag */
+    uint64_t sc = 0;
+    const uint64_t fp = fdt_txn_peek(txn, payload_sz, &sc);
+    VBatch &b = *t->open;
+    if (b.items.empty()) { b.first_chunk = t->out_chunk; b.t_first = now_ns(); }
+    const uint64_t off = (t->out_chunk - b.first_chunk) << FDT_CHUNK_LG_SZ;
+    b.frags.push_back(fdgpu_frag_ex_t{(uint32_t)off, (uint32_t)payload_sz, (uint32_t)b.tr_used, (uint32_t)fp});
+    b.items.push_back(VItem{seq, (uint32_t)t->out_chunk, (uint32_t)payload_sz, 1u, (uint32_t)*opt_tsorig,
+                            (uint32_t)b.tr_used, (uint32_t)fp});
+    b.tr_used += (fp + 3) & ~3ull;
+    b.end_off = off + payload_sz;
+    b.sig_cnt += fdt_frag_sig_bound(payload_sz);
+    if (sc >= 1 && sc <= 16) t->st.sigs += sc;
+    t->out_chunk = fdt_dcache_compact_next(t->out_chunk, toff + fp + 2, t->cfg.out_chunk0, t->cfg.out_wmark);
+    if (t->out_chunk <= b.first_chunk || b.items.size() >= t->cfg.batch_txn_max ||
+        b.sig_cnt + 16 > t->cfg.batch_sig_max || b.end_off + FRAG_CHUNKS * FDT_CHUNK_SZ > t->cfg.batch_bytes_max)
+      b.closed = true;
+    return;
+  }
   uint8_t *txn_t = txn + toff;
   if (toff != payload_sz) txn[payload_sz] = 0;
   const uint64_t tsz = fdt_txn_parse(txn, payload_sz, txn_t, nullptr);
@@ -385,7 +446,7 @@ void vm_after_frag(void *ctx, uint64_t in_idx, uint64_t seq, uint64_t *opt_sig, 
   d.pub_off = (uint32_t)(off + tt->acct_addr_off);
   d.sig_cnt = tt->signature_cnt;
   b.txns.push_back(d);
-  b.items.push_back(VItem{seq, (uint32_t)t->out_chunk, (uint32_t)new_sz, tt->signature_off, (uint32_t)*opt_tsorig});
+  b.items.push_back(VItem{seq, (uint32_t)t->out_chunk, (uint32_t)new_sz, tt->signature_off, (uint32_t)*opt_tsorig, 0u, 0u});
   b.end_off = off + new_sz;
   if (tt->signature_cnt <= 16) { b.sig_cnt += tt->signature_cnt; t->st.sigs += tt->signature_cnt; }
   t->out_chunk = fdt_dcache_compact_next(t->out_chunk, new_sz, t->cfg.out_chunk0, t->cfg.out_wmark);
@@ -429,6 +490,8 @@ fdgpu_vmux_t *fdgpu_vmux_new(const fdgpu_vmux_cfg_t *cfg, fdgpu_verifier_t ver) 
   if (!t) return nullptr;
   t->cfg = *cfg;
   fdgpu_vmux_cfg_t &c = t->cfg;
+  t->gpu_parse = cfg->gpu_parse != 0;
+  if (t->gpu_parse && (!ver.submit_frags || !ver.poll_frags)) { delete t; return nullptr; }
   if (!c.round_robin_cnt) c.round_robin_cnt = 1;
   if (!c.inflight_max) c.inflight_max = 2;
   if (!c.tcache_depth) c.tcache_depth = FDT_VERIFY_TCACHE_DEPTH;
@@ -455,6 +518,7 @@ fdgpu_vmux_t *fdgpu_vmux_new(const fdgpu_vmux_cfg_t *cfg, fdgpu_verifier_t ver) 
   for (auto &b : t->storage) {
     b.codes.resize(c.batch_txn_max);
     b.txns.reserve(c.batch_txn_max);
+    if (t->gpu_parse) b.frags.reserve(c.batch_txn_max);
     b.items.reserve(c.batch_txn_max);
     t->pool.push_back(&b);
   }
@@ -464,7 +528,10 @@ fdgpu_vmux_t *fdgpu_vmux_new(const fdgpu_vmux_cfg_t *cfg, fdgpu_verifier_t ver) 
 void fdgpu_vmux_delete(fdgpu_vmux_t *t) {
   if (!t) return;
   for (VBatch *b : t->inflight)                 /* the verifier may still write codes / read the arena */
-    if (!b->done) t->ver.poll(t->ver.ctx, b->ticket, b->codes.data(), 1);
+    if (!b->done) {
+      if (t->gpu_parse) t->ver.poll_frags(t->ver.ctx, b->ticket, b->codes.data(), b->trailers.data(), 1);
+      else t->ver.poll(t->ver.ctx, b->ticket, b->codes.data(), 1);
+    }
   delete t;
 }
 

@@ -121,6 +121,28 @@ int dispatch_release(void *ctx, int64_t ticket) {
   return fdgpu_release(d->eng[ticket % n], ticket / n);
 }
 
+int64_t dispatch_submit_frags(void *ctx, const uint8_t *arena, uint64_t arena_sz, const fdgpu_frag_ex_t *fx,
+                              uint64_t n, uint64_t trailer_sz) {
+  auto *d = (fdgpu_dispatch *)ctx;
+  const uint32_t ne = (uint32_t)d->eng.size();
+  for (uint32_t k = 0; k < ne; k++) {
+    const uint32_t idx = (d->next + k) % ne;
+    const int64_t t = fdgpu_submit_frags(d->eng[idx], arena, arena_sz, fx, n, trailer_sz);
+    if (t == FDGPU_ERR_FULL) continue;
+    if (t < 0) return t;
+    d->next = (idx + 1) % ne;
+    return t * ne + idx;
+  }
+  return FDGPU_ERR_FULL;
+}
+
+int dispatch_poll_frags(void *ctx, int64_t ticket, int8_t *codes, uint8_t *trailers, int blocking) {
+  auto *d = (fdgpu_dispatch *)ctx;
+  const int64_t n = (int64_t)d->eng.size();
+  if (ticket < 0) return FDGPU_ERR_TICKET;
+  return fdgpu_poll_frags(d->eng[ticket % n], ticket / n, codes, trailers, blocking);
+}
+
 int dispatch_stage_cancel(void *ctx) {
   auto *d = (fdgpu_dispatch *)ctx;
   if (d->staged < 0) return FDGPU_ERR_INVAL;
@@ -154,6 +176,8 @@ fdgpu_verifier_t fdgpu_dispatch_verifier(fdgpu_dispatch_t *d) {
   v.poll_keep = dispatch_poll_keep;
   v.release = dispatch_release;
   v.stage_cancel = dispatch_stage_cancel;
+  v.submit_frags = dispatch_submit_frags;
+  v.poll_frags = dispatch_poll_frags;
   return v;
 }
 

@@ -175,6 +175,31 @@ class VerifyEngine:
     def verify_txns(self, arena, txns):
         return self.poll(self.submit(arena, txns), blocking=True)
 
+    def submit_frags(self, arena, frags, trailer_sz):
+        """fdgpu_submit_frags: raw payloads parsed on the GPU; frags is a
+        FRAG_EX_DTYPE array ({off, sz, tr_off, tr_cap})."""
+        arena = np.ascontiguousarray(arena, dtype=np.uint8)
+        frags = np.ascontiguousarray(frags, dtype=FRAG_EX_DTYPE)
+        tk = _lib.lib().fdgpu_submit_frags(self._h, arena.ctypes.data, arena.size, frags.ctypes.data, len(frags),
+                                           int(trailer_sz))
+        if tk < 0:
+            raise RuntimeError(f"fdgpu_submit_frags failed ({tk}): {_lib.last_error()}")
+        self._pending[tk] = (len(frags), int(trailer_sz))
+        return tk
+
+    def poll_frags(self, ticket, blocking=True):
+        """-> (codes int8[n], trailers uint8[trailer_sz]) or None while pending."""
+        n, tsz = self._pending[ticket]
+        codes = np.zeros(max(n, 1), dtype=np.int8)
+        tr = np.zeros(max(tsz, 1), dtype=np.uint8)
+        rc = _lib.lib().fdgpu_poll_frags(self._h, ticket, codes.ctypes.data, tr.ctypes.data, 1 if blocking else 0)
+        if rc == 1:
+            return None
+        if rc != 0:
+            raise RuntimeError(f"fdgpu_poll_frags failed ({rc}): {_lib.last_error()}")
+        del self._pending[ticket]
+        return codes[:n], tr[:tsz]
+
     def verify_device(self, d_arena, d_sig_desc, n_sig, d_txn_desc, n_txn, d_sig_codes, d_txn_codes, stream=0):
         """Device-resident path; all pointers are device addresses (ints)."""
         rc = _lib.lib().fdgpu_verify_device(self._h, d_arena, d_sig_desc, n_sig, d_txn_desc, n_txn,
@@ -315,6 +340,8 @@ class DeviceBatch:
 
 
 FRAG_DTYPE = np.dtype([("off", "<u4"), ("sz", "<u4")])
+FRAG_EX_DTYPE = np.dtype([("off", "<u4"), ("sz", "<u4"), ("tr_off", "<u4"), ("tr_cap", "<u4")])
+CODE_TRAILER_CAP = -65        # FDGPU_CODE_TRAILER_CAP
 CODE_PARSE_FAIL = -64          # FDGPU_CODE_PARSE_FAIL
 TXN_MAX_SZ = 852               # FD_TXN_MAX_SZ: stride of the parsed fd_txn_t records
 

@@ -77,13 +77,19 @@ class ParseCounters(c.Structure):
 
 SUBMIT_FN = c.CFUNCTYPE(c.c_int64, vp, vp, c.c_uint64, vp, c.c_uint64)
 POLL_FN = c.CFUNCTYPE(c.c_int, vp, c.c_int64, vp, c.c_int)
+SUBMIT_FRAGS_FN = c.CFUNCTYPE(c.c_int64, vp, vp, c.c_uint64, vp, c.c_uint64, c.c_uint64)
+POLL_FRAGS_FN = c.CFUNCTYPE(c.c_int, vp, c.c_int64, vp, vp, c.c_int)
+# fdgpu_frag_ex_t: a payload and the place its parsed fd_txn_t goes (fdgpu_submit_frags)
+FRAG_EX_DTYPE = np.dtype([("off", "<u4"), ("sz", "<u4"), ("tr_off", "<u4"), ("tr_cap", "<u4")])
+CODE_PARSE_FAIL, CODE_TRAILER_CAP = -64, -65
 
 
 class Verifier(c.Structure):
     """fdgpu_verifier_t: submit/poll, plus the optional zero-copy staging
     hooks (left NULL by PyVerifier; set by the GPU dispatcher)."""
     _fields_ = [("ctx", vp), ("submit", SUBMIT_FN), ("poll", POLL_FN), ("stage", vp), ("submit_staged", vp),
-                ("poll_keep", vp), ("release", vp), ("stage_cancel", vp)]
+                ("poll_keep", vp), ("release", vp), ("stage_cancel", vp), ("submit_frags", SUBMIT_FRAGS_FN),
+                ("poll_frags", POLL_FRAGS_FN)]
 
 
 class VTileCfg(c.Structure):
@@ -156,7 +162,8 @@ class VMuxCfg(c.Structure):
                 ("out_wmark", c.c_uint64), ("cr_max", c.c_uint64), ("round_robin_idx", c.c_uint64),
                 ("round_robin_cnt", c.c_uint64), ("hashmap_seed", c.c_uint64), ("tcache_depth", c.c_uint64),
                 ("tcache_map_cnt", c.c_uint64), ("batch_txn_max", c.c_uint32), ("inflight_max", c.c_uint32),
-                ("batch_wait_ns", c.c_uint64), ("batch_sig_max", c.c_uint64), ("batch_bytes_max", c.c_uint64)]
+                ("batch_wait_ns", c.c_uint64), ("batch_sig_max", c.c_uint64), ("batch_bytes_max", c.c_uint64),
+                ("gpu_parse", c.c_uint32), ("_pad", c.c_uint32)]
 
 
 class LinkT(c.Structure):
@@ -194,6 +201,7 @@ def lib():
         "fdt_hash": (u64, [u64, vp, u64]),
         "fdt_txn_footprint": (u64, [u64, u64]),
         "fdt_txn_parse": (u64, [vp, u64, vp, c.POINTER(ParseCounters)]),
+        "fdt_txn_peek": (u64, [vp, u64, c.POINTER(u64)]),
         "fdgpu_dispatch_new": (vp, [c.POINTER(vp), c.c_uint32]),
         "fdgpu_dispatch_delete": (None, [vp]),
         "fdgpu_dispatch_verifier": (Verifier, [vp]),
@@ -331,6 +339,15 @@ def txn_parse(payload, counters=None):
     out = c.create_string_buffer(TXN_MAX_SZ + 16)
     sz = lib().fdt_txn_parse(payload, len(payload), out, c.byref(counters) if counters is not None else None)
     return (sz, out.raw[:sz]) if sz else (0, None)
+
+
+def txn_peek(payload):
+    """fdt_txn_peek: (the footprint a successful parse would have, the
+    leading signature count), read from the payload's counts."""
+    payload = bytes(payload)
+    sc = c.c_uint64()
+    fp = lib().fdt_txn_peek(payload, len(payload), c.byref(sc))
+    return int(fp), int(sc.value)
 
 
 def txn_decode(raw):
@@ -578,8 +595,57 @@ class PyVerifier:
                 c.memmove(codes, r.ctypes.data, len(r))
             return 0
 
+        def submit_frags(ctx, arena, arena_sz, frags, n, trailer_sz):
+            # the GPU engine's fdgpu_submit_frags on the host: fd_txn_parse of
+            # every payload, codes from fn over the parsed txns, trailers
+            # packed at the caller's reserved places
+            if len(self.results) >= self.slots:
+                return -12
+            a = np.ctypeslib.as_array((c.c_uint8 * max(arena_sz, 1)).from_address(arena))[:arena_sz].copy()
+            fx = np.frombuffer((c.c_uint8 * (16 * n)).from_address(frags), dtype=FRAG_EX_DTYPE).copy() if n else \
+                np.zeros(0, dtype=FRAG_EX_DTYPE)
+            codes = np.zeros(max(n, 1), dtype=np.int8)
+            tr = bytearray(trailer_sz)
+            txns, idx = [], []
+            for i, f in enumerate(fx):
+                off, sz = int(f["off"]), int(f["sz"])
+                fp, raw = txn_parse(a[off:off + sz].tobytes())
+                if not fp:
+                    codes[i] = CODE_PARSE_FAIL
+                    continue
+                if fp != int(f["tr_cap"]):
+                    codes[i] = CODE_TRAILER_CAP
+                    continue
+                tr[int(f["tr_off"]):int(f["tr_off"]) + fp] = raw
+                h = txn_decode(raw)
+                txns.append((off + h["message_off"], sz - h["message_off"], off + h["signature_off"],
+                             off + h["acct_addr_off"], h["signature_cnt"]))
+                idx.append(i)
+            if txns:
+                codes[idx] = np.asarray(self.fn(a, np.array(txns, dtype=TXN_DTYPE)), dtype=np.int8)
+            self.batches.append(n)
+            k = self.next
+            self.next += 1
+            self.results[k] = codes[:n]
+            self.trailers[k] = bytes(tr)
+            self.polls[k] = 0
+            return k
+
+        def poll_frags(ctx, ticket, codes, trailers, blocking):
+            if ticket not in self.trailers:
+                return -13
+            rc = poll(ctx, ticket, codes, blocking)
+            if rc == 0:
+                t = self.trailers.pop(ticket)
+                if t:
+                    c.memmove(trailers, t, len(t))
+            return rc
+
+        self.trailers = {}
         self._submit, self._poll = SUBMIT_FN(submit), POLL_FN(poll)
+        self._submit_frags, self._poll_frags = SUBMIT_FRAGS_FN(submit_frags), POLL_FRAGS_FN(poll_frags)
         self.struct = Verifier(None, self._submit, self._poll)
+        self.struct.submit_frags, self.struct.poll_frags = self._submit_frags, self._poll_frags
 
 
 class EngineVerifier:
@@ -729,7 +795,7 @@ class VerifyMuxTile:
 
     def __init__(self, in_links, out_link, verifier, hashmap_seed=0x5EEDF00D, batch_txn_max=4096, inflight_max=2,
                  batch_wait_us=200, round_robin_idx=0, round_robin_cnt=1, cr_max=0, log_max=0, batch_sig_max=0,
-                 batch_bytes_max=0, lazy_iters=16, flow_control=False, register=True):
+                 batch_bytes_max=0, lazy_iters=16, flow_control=False, register=True, gpu_parse=False):
         import threading
         L = lib()
         in_links = list(in_links) if isinstance(in_links, (list, tuple)) else [in_links]
@@ -745,6 +811,7 @@ class VerifyMuxTile:
         vc.batch_wait_ns = int(batch_wait_us * 1000)
         vc.batch_sig_max = batch_sig_max or getattr(verifier, "sig_max", 0)
         vc.batch_bytes_max = batch_bytes_max or getattr(verifier, "arena_max", 0)
+        vc.gpu_parse = 1 if gpu_parse else 0
         self.vcfg = vc
         self._t = L.fdgpu_vmux_new(c.byref(vc), verifier.struct)
         if not self._t:

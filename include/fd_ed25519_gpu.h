@@ -255,6 +255,29 @@ typedef struct {
 #define FDGPU_CODE_PARSE_FAIL (-64)
 fdgpu_dev_batch_t * fdgpu_dev_batch_upload_frags( fdgpu_engine_t * e, uint8_t const * arena, uint64_t arena_sz,
                                                   fdgpu_frag_t const * frags, uint64_t frag_cnt );
+/* Ring-slot frag batches: the verify tile's path with fd_txn_parse on the
+   GPU.  Like fdgpu_submit, but the arena holds raw payloads (frag i is
+   arena[off, off + sz), e.g. frags copied into a registered out dcache) and
+   every txn is parsed, expanded and verified on the device.  Each frag names
+   where its parsed fd_txn_t goes in a caller-sized trailer buffer:
+   [tr_off, tr_off + tr_cap), tr_off 4-byte aligned, tr_cap the footprint the
+   caller reserved (fdt_txn_peek in libfd_verify_tile.so reads it from the
+   payload's counts without validating).  fdgpu_poll_frags returns, per frag,
+   the batch_single_msg code, FDGPU_CODE_PARSE_FAIL (not a transaction), or
+   FDGPU_CODE_TRAILER_CAP (parsed, but to a footprint other than tr_cap: a
+   caller bug, no verdict), and copies the trailer buffer out (trailer_sz
+   bytes; bytes of frags that did not parse are unspecified). */
+typedef struct {
+  uint32_t off;
+  uint32_t sz;          /* <= FD_TXN_MTU (1232) to parse */
+  uint32_t tr_off;      /* its fd_txn_t at trailers[tr_off, tr_off + tr_cap) */
+  uint32_t tr_cap;
+} fdgpu_frag_ex_t;
+#define FDGPU_CODE_TRAILER_CAP (-65)
+int64_t fdgpu_submit_frags( fdgpu_engine_t * e, uint8_t const * arena, uint64_t arena_sz,
+                            fdgpu_frag_ex_t const * frags, uint64_t frag_cnt, uint64_t trailer_sz );
+int     fdgpu_poll_frags  ( fdgpu_engine_t * e, int64_t ticket, int8_t * codes, uint8_t * trailers, int blocking );
+
 /* After a verify of a frag batch: frag i's parsed fd_txn_t (byte-identical to
    fd_txn_parse's output) at txn_out + i * 852 (FD_TXN_MAX_SZ; NULL: skip),
    its footprint (0: not a transaction) in txn_sz[i] (NULL: skip). */

@@ -171,6 +171,13 @@ uint64_t fdt_txn_footprint( uint64_t instr_cnt, uint64_t addr_table_lookup_cnt )
 uint64_t fdt_txn_parse( uint8_t const * payload, uint64_t payload_sz, void * out_buf,
                         fdt_txn_parse_counters_t * counters_opt );
 
+/* The footprint fdt_txn_parse would return for the payload if it parses,
+   read from its counts without the structural checks (equal to the parse's
+   whenever the payload is a valid transaction; 0 if the counts run past the
+   payload); *sig_cnt_opt gets the leading signature count.  The verify tile
+   reserves each frag's trailer with it when the GPU parses the batch. */
+uint64_t fdt_txn_peek( uint8_t const * payload, uint64_t payload_sz, uint64_t * sig_cnt_opt );
+
 /* ----------------------------------------------------------- verifiers */
 
 /* A verifier runs fd_ed25519_verify_batch_single_msg over whole batches,
@@ -190,6 +197,12 @@ typedef struct {
   int       (*poll_keep)    ( void * ctx, int64_t ticket, int8_t * txn_codes, int blocking );
   int       (*release)      ( void * ctx, int64_t ticket );
   int       (*stage_cancel) ( void * ctx );
+  /* Optional GPU-side parse (NULL when unsupported): batches of raw
+     payloads with their trailers reserved by the caller, fdgpu_submit_frags /
+     fdgpu_poll_frags semantics (include/fd_ed25519_gpu.h). */
+  int64_t   (*submit_frags) ( void * ctx, uint8_t const * arena, uint64_t arena_sz, fdgpu_frag_ex_t const * frags,
+                              uint64_t frag_cnt, uint64_t trailer_sz );
+  int       (*poll_frags)   ( void * ctx, int64_t ticket, int8_t * codes, uint8_t * trailers, int blocking );
 } fdgpu_verifier_t;
 
 /* Multi-GPU dispatcher: batches go round-robin over `engine_cnt` engines
@@ -383,7 +396,11 @@ int  fdt_mux_run( fdt_mux_cfg_t const * cfg, fdt_mux_callbacks_t const * callbac
                    open batch -- the batch's arena IS the contiguous run of
                    out-dcache chunks its frags occupy, so with that dcache
                    registered (fdgpu_host_register) the engine DMAs it with
-                   no staging copy -- and advance the cursor;
+                   no staging copy -- and advance the cursor.  With
+                   gpu_parse the tile only reads the payload's counts
+                   (fdt_txn_peek) to reserve the trailer, and the frag goes
+                   to the batch as {payload, trailer place}: the GPU parses,
+                   and the trailer is copied in at publish;
      after_credit  poll in-flight batches and resolve completed ones strictly
                    in ingest order (tcache query -> verify code -> insert ->
                    fdt_mux_publish of the frag where it already lies), while
@@ -417,6 +434,9 @@ typedef struct {
   uint64_t        batch_sig_max;                 /* 0: 12 x batch_txn_max */
   uint64_t        batch_bytes_max;               /* arena bytes per batch (<= the engines' max_arena);
                                                     0: batch_txn_max x FDT_TPU_DCACHE_MTU rounded to chunks */
+  uint32_t        gpu_parse;                     /* 1: fd_txn_parse runs on the GPU (the verifier's
+                                                    submit_frags / poll_frags; required then) */
+  uint32_t        _pad;
 } fdgpu_vmux_cfg_t;
 
 typedef struct fdgpu_vmux fdgpu_vmux_t;

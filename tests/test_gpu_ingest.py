@@ -150,3 +150,57 @@ def test_frag_batch_edges(engine):
     out, sz = b.txns()
     assert sz[0] and b.codes()[0] in (0, -1, -2, -3) and out.shape == (1, TXN_MAX_SZ)
     b.free()
+
+
+def test_ring_frag_batches_vs_oracle_and_trailers(engine, oracle, txn_fixtures, quic_corpus):
+    """fdgpu_submit_frags / fdgpu_poll_frags (the verify tile's GPU-parse
+    path through the ring slots): per frag the oracle's code on the parsed
+    txn, or PARSE_FAIL; each trailer equals the host fd_txn_parse's bytes at
+    the place reserved from fdt_txn_peek; a reservation other than the
+    footprint gets TRAILER_CAP; several batches in flight at once."""
+    from firedancer_amd.ed25519 import CODE_TRAILER_CAP, FRAG_EX_DTYPE
+    cases = _payload_cases(txn_fixtures, quic_corpus)
+    rnd = random.Random(0x7A11)
+    rnd.shuffle(cases)
+    chunks = [cases[i:i + 2500] for i in range(0, 7500, 2500)]
+    def submit(ci, ps):
+        arena, fr = _pack(ps)
+        fx = np.zeros(len(ps), dtype=FRAG_EX_DTYPE)
+        fx["off"], fx["sz"] = fr["off"], fr["sz"]
+        tr = 0
+        caps = []
+        for k, p in enumerate(ps):
+            fp, _ = tile.txn_peek(p)
+            if ci == 2 and k % 97 == 5 and fp:
+                fp += 10                                      # a wrong reservation
+            fx[k]["tr_off"], fx[k]["tr_cap"] = tr, fp
+            caps.append(fp)
+            tr += (fp + 3) & ~3
+        return engine.submit_frags(arena, fx, tr), arena, fx, ps
+
+    inflight = [submit(0, chunks[0]), submit(1, chunks[1])]     # both ring slots busy
+    for ci in range(len(chunks)):
+        tk, arena, fx, ps = inflight.pop(0)
+        codes, trailers = engine.poll_frags(tk)
+        if ci + 2 < len(chunks):
+            inflight.append(submit(ci + 2, chunks[ci + 2]))
+        td = np.zeros(len(ps), dtype=workload.TXN_DTYPE)
+        parsed = [tile.txn_parse(p) for p in ps]
+        for k, ((fp, raw), f) in enumerate(zip(parsed, fx)):
+            if fp:
+                d = tile.txn_decode(raw)
+                base = int(f["off"])
+                td[k] = (base + d["message_off"], int(f["sz"]) - d["message_off"], base + d["signature_off"],
+                         base + d["acct_addr_off"], d["signature_cnt"])
+        exp = oracle.verify_txns(arena, td)
+        for k, ((fp, raw), f) in enumerate(zip(parsed, fx)):
+            if not fp:
+                assert codes[k] == CODE_PARSE_FAIL, k
+            elif int(f["tr_cap"]) != fp:
+                assert codes[k] == CODE_TRAILER_CAP, k
+            else:
+                assert codes[k] == exp[k], k
+                o = int(f["tr_off"])
+                assert bytes(trailers[o:o + fp]) == raw, k
+        if ci == 2:
+            assert (codes == CODE_TRAILER_CAP).sum() > 5

@@ -179,13 +179,13 @@ def test_mux_overrun_polling():
 # ------------------------------------------------- verify tile as callbacks
 
 def _run_vmux(payloads, verifier, seed=0xABCD, batch=4, inflight=2, rr=(0, 1), depth=1 << 12, out_data=None,
-              flow=False, consumer=None, cr_max=0):
+              flow=False, consumer=None, cr_max=0, gpu_parse=False):
     inl = tile.Link(depth, 1232)
     outl = tile.Link(depth, tile.TPU_DCACHE_MTU,
                      data_sz=out_data or (len(payloads) + 8) * (tile.TPU_DCACHE_MTU + 64))
     vm = tile.VerifyMuxTile(inl, outl, verifier, hashmap_seed=seed, batch_txn_max=batch, inflight_max=inflight,
                             round_robin_idx=rr[0], round_robin_cnt=rr[1], log_max=1 << 16, flow_control=flow,
-                            batch_wait_us=100, cr_max=cr_max)
+                            batch_wait_us=100, cr_max=cr_max, gpu_parse=gpu_parse)
     for p in payloads:
         inl.publish(p)
     th = None
@@ -198,17 +198,21 @@ def _run_vmux(payloads, verifier, seed=0xABCD, batch=4, inflight=2, rr=(0, 1), d
     return vm, inl, outl
 
 
+@pytest.mark.parametrize("gpu_parse", [False, True])
 @pytest.mark.parametrize("batch,inflight,lag,rr", [(1, 1, 0, (0, 1)), (7, 2, 2, (0, 1)), (64, 3, 1, (1, 3)),
                                                     (1000, 2, 0, (0, 1))])
-def test_vmux_vs_sequential_model(oracle, batch, inflight, lag, rr):
+def test_vmux_vs_sequential_model(oracle, batch, inflight, lag, rr, gpu_parse):
     """The verify tile as mux callbacks produces the reference loop's outcome
     for every frag and the same published stream (sig = tag, payload,
     fd_txn_t trailer), for any batch size / batches in flight / verifier
-    latency / round-robin share."""
+    latency / round-robin share -- with fd_txn_parse on the tile's core, and
+    with the parse handed to the verifier (gpu_parse: the tile reserves each
+    trailer from the payload's counts; here a host stand-in of
+    fdgpu_submit_frags parses)."""
     ps = _mixed_stream(800, seed=batch * 17 + lag)
     seed = 0x99 + batch
     ver = tile.PyVerifier(oracle_fn(oracle), slots=inflight, lag=lag)
-    vm, _, outl = _run_vmux(ps, ver, seed=seed, batch=batch, inflight=inflight, rr=rr)
+    vm, _, outl = _run_vmux(ps, ver, seed=seed, batch=batch, inflight=inflight, rr=rr, gpu_parse=gpu_parse)
     exp_out, exp_pub = tile_model.verify_tile_model(ps, seed, oracle_fn(oracle), rr_idx=rr[0], rr_cnt=rr[1])
     seqs, codes = vm.log()
     assert seqs.tolist() == list(range(len(ps)))
@@ -225,7 +229,8 @@ def test_vmux_vs_sequential_model(oracle, batch, inflight, lag, rr):
     vm.close()
 
 
-def test_vmux_small_dcache_wraps_under_flow_control(oracle):
+@pytest.mark.parametrize("gpu_parse", [False, True])
+def test_vmux_small_dcache_wraps_under_flow_control(oracle, gpu_parse):
     """An out dcache with room for ~8 maximal frags, 12 credits, and a slow
     consumer that reads each published frag (then advances the fseq) while
     the tile runs: the tile wraps the ring many times, stops taking frags
@@ -253,7 +258,8 @@ def test_vmux_small_dcache_wraps_under_flow_control(oracle):
 
     ver = tile.PyVerifier(oracle_fn(oracle), slots=2, lag=1)
     vm, _, outl = _run_vmux(ps, ver, seed=seed, batch=16, inflight=2, depth=1 << 10,
-                            out_data=8 * (tile.TPU_DCACHE_MTU + 64), flow=True, consumer=consumer, cr_max=12)
+                            out_data=8 * (tile.TPU_DCACHE_MTU + 64), flow=True, consumer=consumer, cr_max=12,
+                            gpu_parse=gpu_parse)
     assert len(seen) == len(exp_pub)
     for (sig, frag), (p, raw, tag) in zip(seen, exp_pub):
         assert sig == tag

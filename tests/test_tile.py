@@ -598,3 +598,38 @@ def test_tile_header_exports():
     assert len(names) > 30
     for n in names:
         assert hasattr(L, n), n
+
+
+def test_txn_peek_agrees_with_parse(quic_corpus, fixtures):
+    """fdt_txn_peek (the trailer reservation of the GPU-parse verify tile)
+    returns fd_txn_parse's footprint and the signature count for every
+    payload that parses -- the QUIC corpus, the fixtures (legacy and v0 with
+    lookup tables), generated txns, single-byte mutations and truncations of
+    the fixtures, random splices -- and never reads past the payload (run
+    under ASan/UBSan by test_sanitize.py)."""
+    rnd = random.Random(0x9EE)
+    arena, txns, _ = quic_corpus
+    cases = [bytes(arena[int(t["sig_off"]) - 1: int(t["msg_off"]) + int(t["msg_sz"])]) for t in txns[:1000]]
+    base = list(fixtures.values())
+    cases += base
+    for cfgf in (workload.cfg1, workload.cfg3):
+        a, tx, _ = cfgf(300, seed=12)
+        cases += workload.payloads(a, tx)
+    for p in base:
+        cases += [p[:n] for n in range(len(p) + 1)]
+        for _ in range(400):
+            q = bytearray(p)
+            q[rnd.randrange(len(q))] = rnd.getrandbits(8)
+            cases.append(bytes(q))
+    for _ in range(1000):
+        a, b = rnd.choice(base), rnd.choice(base)
+        cases.append(a[:rnd.randrange(len(a) + 1)] + b[rnd.randrange(len(b) + 1):])
+    parsed = 0
+    for p in cases:
+        fp, raw = tile.txn_parse(p)
+        pk, sc = tile.txn_peek(p)
+        if fp:
+            parsed += 1
+            d = tile.txn_decode(raw)
+            assert pk == fp and sc == d["signature_cnt"] and d["signature_off"] == 1, p.hex()[:80]
+    assert parsed > 2000

@@ -123,18 +123,22 @@ def test_twelve_signature_txns_default_config():
 
 # ------------------------------------ the verify tile as mux callbacks (vmux)
 
-def test_vmux_mixed_stream_vs_model_gpu(engines, oracle):
+@pytest.mark.parametrize("gpu_parse", [False, True])
+def test_vmux_mixed_stream_vs_model_gpu(engines, oracle, gpu_parse):
     """fdgpu_vmux on fdt_mux_run over the MI355X engines: frags copied into
     the out dcache (registered with both engines, so each batch is DMA'd from
     there with no staging copy), verified, and published in place -- every
-    outcome and the published stream equal the sequential model's."""
+    outcome and the published stream equal the sequential model's.  With
+    gpu_parse the batches are frag batches (fdgpu_submit_frags): fd_txn_parse
+    runs on the GPU and the trailers come back from it."""
     from test_tile import _mixed_stream
     ps = _mixed_stream(3000, seed=7)
     seed = 0xC0DE
     inl = tile.Link(1 << 13, 1232)
     outl = tile.Link(1 << 13, tile.TPU_DCACHE_MTU, data_sz=tile.vmux_dcache_data_sz(1 << 13, 101, 3))
     ver = tile.EngineVerifier(engines)
-    vm = tile.VerifyMuxTile(inl, outl, ver, hashmap_seed=seed, batch_txn_max=101, inflight_max=3, log_max=1 << 14)
+    vm = tile.VerifyMuxTile(inl, outl, ver, hashmap_seed=seed, batch_txn_max=101, inflight_max=3, log_max=1 << 14,
+                            gpu_parse=gpu_parse)
     for p in ps:
         inl.publish(p)
     vm.run(len(ps), timeout_s=60)
@@ -145,6 +149,7 @@ def test_vmux_mixed_stream_vs_model_gpu(engines, oracle):
     assert [(m["sig"], tile.split_verify_output(f)) for m, f in outs] == [(t, (p, raw)) for p, raw, t in pub]
     st = vm.stats()
     assert st["batches"] >= (len(ps) - st["parse_fail"]) // 101 and vm.idle()
+    assert st["verify_errors"] == 0
     vm.close()
     ver.close()
 

@@ -38,6 +38,8 @@ def main():
     ap.add_argument("--batch", type=int, default=16384)
     ap.add_argument("--depth-lg", type=int, default=21)
     ap.add_argument("--prefill", type=int, default=0, help="1: publish everything before the tiles start")
+    ap.add_argument("--mux", type=int, default=0, help="1: the mux-callback tile (fdgpu_vmux on fdt_mux_run)")
+    ap.add_argument("--inflight", type=int, default=4)
     ap.add_argument("--cpus", default="", help="comma-separated CPUs for tile k (default: physical cores 1, 2, ...)"
                                                "; 'none' leaves the threads unpinned")
     args = ap.parse_args()
@@ -56,9 +58,16 @@ def main():
         inl = tile.Link(1 << args.depth_lg, 1232)
         vts = []
         for k in range(T):
-            outl = tile.Link(1 << 12, tile.TPU_DCACHE_MTU)
-            vts.append((tile.VerifyTile(inl, outl, NullVerifier(), batch_txn_max=args.batch, inflight_max=4,
-                                        round_robin_idx=k, round_robin_cnt=T), outl))
+            if args.mux:
+                outl = tile.Link(1 << 14, tile.TPU_DCACHE_MTU,
+                                 data_sz=tile.vmux_dcache_data_sz(1 << 14, args.batch, args.inflight))
+                vts.append((tile.VerifyMuxTile(inl, outl, NullVerifier(), batch_txn_max=args.batch,
+                                               inflight_max=args.inflight, round_robin_idx=k, round_robin_cnt=T,
+                                               batch_bytes_max=args.batch * 2176), outl))
+            else:
+                outl = tile.Link(1 << 12, tile.TPU_DCACHE_MTU)
+                vts.append((tile.VerifyTile(inl, outl, NullVerifier(), batch_txn_max=args.batch,
+                                            inflight_max=args.inflight, round_robin_idx=k, round_robin_cnt=T), outl))
         prod = None
         if args.prefill:
             prod = tile.Producer(inl, arena, offs, sizes, rate_tps=0)
@@ -70,6 +79,8 @@ def main():
             if args.cpus != "none":
                 os.sched_setaffinity(0, {cpus[k % len(cpus)]})
             vt.run(len(ps), timeout_s=120)
+            if args.mux:
+                vt.mux_wall = time.perf_counter()
         ths = [threading.Thread(target=body, args=(vt, k)) for k, (vt, _) in enumerate(vts)]
         t0 = time.perf_counter()
         if not args.prefill:
@@ -80,11 +91,14 @@ def main():
             th.join()
         wall = time.perf_counter() - t0
         _, prod_s = prod.join() if not args.prefill else (None, 0.0)
+        if args.mux:
+            wall = max(vt.mux_wall for vt, _ in vts) - t0
         sts = [vt.stats() for vt, _ in vts]
         pub = sum(x["published"] for x in sts)
         print(json.dumps({"tiles": T, "txns": len(ps), "prefill": bool(args.prefill), "txns_per_s": round(len(ps) / wall, 1),
                           "wall_s": round(wall, 4), "producer_s": round(prod_s, 4), "published": pub,
                           "ns_per_frag_per_tile": round(wall * 1e9 / len(ps), 1),
+                          "mux": bool(args.mux),
                           "ingest_ms_per_tile": [round(x["ingest_ns"] / 1e6, 1) for x in sts],
                           "submit_ms_per_tile": [round(x["submit_ns"] / 1e6, 1) for x in sts]}), flush=True)
         for vt, _ in vts:
