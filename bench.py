@@ -264,55 +264,48 @@ def sync_latency(arena, txns, calls=1000, threads=64):
                          "trip per call; concurrent: calls coalesced into shared batches (group commit)"}
 
 
-def tile_lines(eng, arena, txns, modes, cpus):
-    """BASELINE configs[4] (cfg5) on this rank's GPU: the verify tile
-    (fdgpu_vtile: tango in -> parse -> batched GPU verify -> tcache -> tango
-    out) over this rank's cfg1 txns as raw frags, one tile thread and a
-    producer thread pinned to their own cores, 16K-txn batches, 4 in flight.
-    'backlog': the producer publishes as fast as it can into a 2^21-deep
-    link; 'paced': 8M txn/s into a 2^17-deep link (line rate: the tile must
-    keep up with no overrun).  Every run checks that exactly the verified
-    txns were published."""
-    import threading
-    from firedancer_amd import tile, workload
-    offs = txns["sig_off"].astype(np.uint64) - 1                 # payload = [sig_cnt][sigs][message]
-    sizes = (txns["msg_off"].astype(np.uint64) + txns["msg_sz"] - offs).astype(np.uint32)
-    expected = int((modes == 0).sum())
-    out = {}
-    for name, depth_lg, rate in (("backlog", 21, 0.0), ("paced_8M", 17, 8e6)):
-        inl = tile.Link(1 << depth_lg, 1232)
-        outl = tile.Link(1 << 12, tile.TPU_DCACHE_MTU)
-        ver = tile.EngineVerifier([eng])
-        vt = tile.VerifyTile(inl, outl, ver, batch_txn_max=16384, inflight_max=4, batch_wait_us=200)
-        err = []
+TILE_RUNS = (  # name, verify tiles, quic links (producers), offered txn/s (0: backlog at producer speed)
+    ("mux1_backlog", 1, 1, 0.0),
+    ("mux1_paced_12M", 1, 1, 12e6),
+    ("mux2_backlog", 2, 2, 0.0),
+    ("mux2_paced_16M", 2, 2, 16e6),
+)
 
-        def body():
-            try:
-                os.sched_setaffinity(0, {cpus[1 % len(cpus)]})
-                vt.run(len(txns), timeout_s=120)
-            except Exception as e:  # noqa: BLE001
-                err.append(repr(e))
-        th = threading.Thread(target=body)
-        keep = os.sched_getaffinity(0)
-        os.sched_setaffinity(0, {cpus[0]})               # the producer's C thread inherits this mask
-        t0 = time.perf_counter()
-        prod = tile.Producer(inl, arena, offs, sizes, rate_tps=rate)
-        os.sched_setaffinity(0, keep)
-        th.start()
-        th.join()
-        wall = time.perf_counter() - t0
-        prod.join()
-        st = vt.stats()
-        lat = vt.latencies_ns() / 1e6
-        vt.close()
-        ver.close()
-        out[f"tile_{name}_txns_per_s"] = round(len(txns) / wall, 1)
-        out[f"tile_{name}_batch_latency_ms_p50_p99"] = [round(float(np.percentile(lat, 50)), 3),
-                                                       round(float(np.percentile(lat, 99)), 3)] if len(lat) else None
-        out[f"tile_{name}_overruns"] = int(st["overrun"])
-        out[f"tile_{name}_published_ok"] = (not err) and int(st["published"]) == expected
-    out["tile_config"] = ("1 verify tile thread + 1 producer thread, cfg1 frags, batch 16384 txns, 4 in flight; "
-                          "backlog: 2^21-deep link at producer speed; paced_8M: 8M txn/s offered, 2^17-deep link")
+
+def tile_lines(device, arena, txns, modes, cpus, runs=TILE_RUNS):
+    """BASELINE configs[4] (cfg5) on this rank's GPU: the verify tile in the
+    reference's shape -- the fd_verify.c:232-246 callbacks (fdgpu_vmux) on
+    the mux loop (fdt_mux_run, FD_MUX_FLAG_COPY | MANUAL_PUBLISH), frags
+    copied into a registered out dcache, fd_txn_parse on the GPU
+    (fdgpu_submit_frags), tcache and publish in order -- over this rank's
+    cfg1 txns as raw frags.  T tiles read P quic->verify links round robin
+    (every verify tile reads every QUIC tile's link, fd_frankendancer.c:131-
+    133), one engine per tile on this GPU, 16K-txn batches, 4 in flight,
+    producers and tiles pinned to their own cores.  Every run checks that
+    exactly the verified txns were published."""
+    import types
+    sys.path.insert(0, os.path.join(REPO, "tools"))
+    import bench_tile
+    from firedancer_amd import workload
+    ps = workload.payloads(arena, txns)
+    parena, poffs, psizes = workload.pack_payloads(ps)
+    n_sig = int(txns["sig_cnt"].sum())
+    out = {}
+    for name, tiles_n, prods, rate in runs:
+        args = types.SimpleNamespace(gpus=1, gpu_parse=1, producers=prods, depth_lg=21 if not rate else 19,
+                                     wait_us=200.0, pin=1)
+        res = bench_tile.run_once_mux(args, ps, parena, poffs, psizes, n_sig, modes, tiles_n, 16384, 4, rate,
+                                      cpus=cpus, device=device)
+        lat = res["batch_latency_ms"]
+        out[f"tile_{name}_txns_per_s"] = res["txns_per_s"]
+        out[f"tile_{name}_batch_latency_ms_p50_p99"] = [lat["p50"], lat["p99"]]
+        out[f"tile_{name}_overruns"] = res["counters"]["overrun"]
+        out[f"tile_{name}_published_ok"] = res["counters"]["published"] == res["expected_published"]
+    out["tile_config"] = ("fdgpu_vmux on fdt_mux_run (the reference's mux-callback verify tile), fd_txn_parse on "
+                          "the GPU; muxT: T verify tiles reading T quic->verify links (one producer thread each), "
+                          "one engine per tile on this GPU, cfg1 frags, 16384-txn batches, 4 in flight; backlog: "
+                          "producers publish as fast as they can into 2^21-deep links; paced_R: R txn/s offered "
+                          "in total into 2^19-deep links")
     return out
 
 
@@ -545,10 +538,10 @@ def main():
         if dist.rank == 0:
             extras.update(sync_latency(arena, txns))
         if args.tile:
-            tl = tile_lines(eng, arena, txns, modes, cpus)
-            tl["tile_backlog_txns_per_s_node"] = round(dist.sum(tl["tile_backlog_txns_per_s"]), 1)
-            tl["tile_paced_8M_published_ok_all_ranks"] = dist.sum(1 if tl["tile_paced_8M_published_ok"] else 0) \
-                == dist.world
+            tl = tile_lines(device, arena, txns, modes, cpus)
+            tl["tile_mux1_backlog_txns_per_s_node"] = round(dist.sum(tl["tile_mux1_backlog_txns_per_s"]), 1)
+            tl["tile_published_ok_all_ranks"] = dist.sum(
+                1 if all(v for k, v in tl.items() if k.endswith("_published_ok")) else 0) == dist.world
             extras.update(tl)
         if args.cfg3_txns:
             eng_nb = VerifyEngine(device, max_txn=1024, ring_depth=1, bucket=False)

@@ -161,6 +161,7 @@ namespace {
 
 struct VItem {
   uint64_t seq;
+  uint64_t tag;         /* fd_hash(seed, signature 0, 64): the dedup tag, taken while the payload is hot */
   uint32_t chunk;       /* where [payload][pad][fd_txn_t][u16 sz] lies in the out dcache */
   uint32_t sz;          /* that frag's size (gpu_parse: the payload's; the trailer is added at publish) */
   uint32_t sig_off;     /* signature 0, from the frag start */
@@ -204,6 +205,7 @@ struct fdgpu_vmux {
   uint64_t out_chunk = 0;                 /* write cursor */
   uint64_t cur_sz = 0;                    /* the frag between during_frag and after_frag */
   bool cur_ok = false;
+  uint64_t cur_fp = 0, cur_sc = 0, cur_tag = 0;   /* gpu_parse: its peeked footprint, signature count, tag */
   std::vector<VBatch> storage;
   std::vector<VBatch *> pool;
   std::deque<VBatch *> inflight;
@@ -269,7 +271,6 @@ struct fdgpu_vmux {
       const size_t n = b->items.size();
       while (b->next < n) {
         const size_t k = b->next;
-        if (k + 8 < n) __builtin_prefetch(out_laddr(b->items[k + 8].chunk));   /* its signature, hashed soon */
         const VItem &it = b->items[k];
         const int code = b->codes[k];
         if (gpu_parse && (code == FDGPU_CODE_PARSE_FAIL || code == FDGPU_CODE_TRAILER_CAP)) {
@@ -282,7 +283,7 @@ struct fdgpu_vmux {
           continue;
         }
         uint8_t *frag = out_laddr(it.chunk);
-        const uint64_t tag = fdt_hash(cfg.hashmap_seed, frag + it.sig_off, 64);
+        const uint64_t tag = it.tag;
         int outcome;
         if (fdt_tcache_query(tcache, tag)) outcome = FD_TXN_VERIFY_DEDUP;
         else if (code != FD_ED25519_SUCCESS) outcome = FD_TXN_VERIFY_FAILED;
@@ -389,7 +390,15 @@ void vm_during_frag(void *ctx, uint64_t in_idx, uint64_t seq, uint64_t sig, uint
     *opt_filter = 1;
     return;
   }
-  std::memcpy(t->out_laddr(t->out_chunk), c.in_base[in_idx] + (chunk << FDT_CHUNK_LG_SZ), sz);
+  const uint8_t *src = c.in_base[in_idx] + (chunk << FDT_CHUNK_LG_SZ);
+  std::memcpy(t->out_laddr(t->out_chunk), src, sz);
+  if (t->gpu_parse) {
+    /* read the counts and hash signature 0 from the source just copied (in
+       L1): the mux's seq re-check after during_frag discards them with the
+       frag if the producer overwrote it meanwhile */
+    t->cur_fp = fdt_txn_peek(src, sz, &t->cur_sc);
+    t->cur_tag = sz >= 65 ? fdt_hash(c.hashmap_seed, src + 1, 64) : 0;
+  }
   t->cur_sz = sz;
   t->cur_ok = true;
 }
@@ -405,13 +414,13 @@ void vm_after_frag(void *ctx, uint64_t in_idx, uint64_t seq, uint64_t *opt_sig, 
   if (t->gpu_parse) {
     /* the GPU parses: reserve the trailer the parse will produce (the
        payload's counts, fdt_txn_peek) and hand the payload over as a frag */
-    uint64_t sc = 0;
-    const uint64_t fp = fdt_txn_peek(txn, payload_sz, &sc);
+    (void)txn;
+    const uint64_t sc = t->cur_sc, fp = t->cur_fp;
     VBatch &b = *t->open;
     if (b.items.empty()) { b.first_chunk = t->out_chunk; b.t_first = now_ns(); }
     const uint64_t off = (t->out_chunk - b.first_chunk) << FDT_CHUNK_LG_SZ;
     b.frags.push_back(fdgpu_frag_ex_t{(uint32_t)off, (uint32_t)payload_sz, (uint32_t)b.tr_used, (uint32_t)fp});
-    b.items.push_back(VItem{seq, (uint32_t)t->out_chunk, (uint32_t)payload_sz, 1u, (uint32_t)*opt_tsorig,
+    b.items.push_back(VItem{seq, t->cur_tag, (uint32_t)t->out_chunk, (uint32_t)payload_sz, 1u, (uint32_t)*opt_tsorig,
                             (uint32_t)b.tr_used, (uint32_t)fp});
     b.tr_used += (fp + 3) & ~3ull;
     b.end_off = off + payload_sz;
@@ -446,7 +455,8 @@ void vm_after_frag(void *ctx, uint64_t in_idx, uint64_t seq, uint64_t *opt_sig, 
   d.pub_off = (uint32_t)(off + tt->acct_addr_off);
   d.sig_cnt = tt->signature_cnt;
   b.txns.push_back(d);
-  b.items.push_back(VItem{seq, (uint32_t)t->out_chunk, (uint32_t)new_sz, tt->signature_off, (uint32_t)*opt_tsorig, 0u, 0u});
+  b.items.push_back(VItem{seq, fdt_hash(t->cfg.hashmap_seed, txn + tt->signature_off, 64), (uint32_t)t->out_chunk,
+                          (uint32_t)new_sz, tt->signature_off, (uint32_t)*opt_tsorig, 0u, 0u});
   b.end_off = off + new_sz;
   if (tt->signature_cnt <= 16) { b.sig_cnt += tt->signature_cnt; t->st.sigs += tt->signature_cnt; }
   t->out_chunk = fdt_dcache_compact_next(t->out_chunk, new_sz, t->cfg.out_chunk0, t->cfg.out_wmark);

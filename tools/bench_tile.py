@@ -39,6 +39,13 @@ def main():
     ap.add_argument("--mux", type=int, default=0,
                     help="1: the verify tile as mux callbacks (fdgpu_vmux on fdt_mux_run; frags copied once into "
                          "the registered out dcache and DMA'd from there), 0: the step-loop tile (fdgpu_vtile)")
+    ap.add_argument("--gpu-parse", type=int, default=1,
+                    help="(mux tile) 1: fd_txn_parse on the GPU (fdgpu_submit_frags); 0: on the tile's core")
+    ap.add_argument("--producers", type=int, default=1,
+                    help="(mux tile) quic->verify links, one producer thread each; every verify tile reads all of "
+                         "them round robin (fd_frankendancer.c: all verify tiles read all QUIC tiles)")
+    ap.add_argument("--producers-same-as-tiles", type=int, default=0,
+                    help="1: as many quic links (producers) as verify tiles in every run")
     ap.add_argument("--pin", type=int, default=1,
                     help="1: producer and each tile thread pinned to its own physical core (workload.physical_cpus)")
     ap.add_argument("--out", default="")
@@ -59,6 +66,8 @@ def main():
     ok = True
     lines = []
     for tiles_n, batch, inflight, rate in runs:
+        if args.producers_same_as_tiles:
+            args.producers = int(tiles_n)
         res = run_once(args, ps, arena, offs, sizes, n_sig, modes, int(tiles_n), int(batch), int(inflight), rate)
         line = json.dumps(res)
         print(line, flush=True)
@@ -70,13 +79,13 @@ def main():
     return 0 if ok else 1
 
 
-def start_producer(args, inl, arena, offs, sizes, rate, cpus):
+def start_producer(args, inl, arena, offs, sizes, rate, cpus, k=0):
     """The producer's C thread inherits the creating thread's CPU mask: pin
-    this thread to cpus[0] around its start."""
+    this thread to cpus[k] around its start."""
     if not args.pin:
         return tile.Producer(inl, arena, offs, sizes, rate_tps=rate)
     keep = os.sched_getaffinity(0)
-    os.sched_setaffinity(0, {cpus[0]})
+    os.sched_setaffinity(0, {cpus[k % len(cpus)]})
     try:
         return tile.Producer(inl, arena, offs, sizes, rate_tps=rate)
     finally:
@@ -88,10 +97,22 @@ def warm(engines, inflight):
     timed region: a HIP stream's first submission creates its hardware queue
     (milliseconds), which would otherwise land inside the run."""
     a, t, _ = workload.cfg1(64, seed=7)
+    ps = workload.payloads(a, t)
+    pa, po, psz = workload.pack_payloads(ps)
+    fx = np.zeros(len(ps), dtype=tile.FRAG_EX_DTYPE)
+    fx["off"], fx["sz"] = po, psz
+    tr = 0
+    for k, p in enumerate(ps):
+        fp, _ = tile.txn_peek(p)
+        fx[k]["tr_off"], fx[k]["tr_cap"] = tr, fp
+        tr += (fp + 3) & ~3
     for e in engines:
         tks = [e.submit(a, t) for _ in range(inflight)]
         for tk in tks:
             e.poll(tk, blocking=True)
+        tks = [e.submit_frags(pa, fx, tr) for _ in range(inflight)]     # the slots' GPU-parse buffers too
+        for tk in tks:
+            e.poll_frags(tk, blocking=True)
 
 
 def run_once(args, ps, arena, offs, sizes, n_sig, modes, tiles_n, batch, inflight, rate):
@@ -160,26 +181,36 @@ def run_once(args, ps, arena, offs, sizes, n_sig, modes, tiles_n, batch, infligh
     return res
 
 
-def run_once_mux(args, ps, arena, offs, sizes, n_sig, modes, tiles_n, batch, inflight, rate):
-    """T verify mux tiles (fdt_mux_run threads) over one engine each; the
-    out links have no reliable consumer here (published frags count as
-    consumed), so this measures ingest + verify + publish."""
+def run_once_mux(args, ps, arena, offs, sizes, n_sig, modes, tiles_n, batch, inflight, rate, cpus=None, device=None):
+    """T verify mux tiles (fdt_mux_run threads) over one engine each, reading
+    P quic->verify links (one producer thread each, the frags dealt round
+    robin over the links, each paced at rate / P); the out links have no
+    reliable consumer here (published frags count as consumed), so this
+    measures ingest + verify + publish."""
     frag_bytes = (tile.TPU_DCACHE_MTU + 63) // 64 * 64
-    engines = [fa.VerifyEngine(k % args.gpus, max_txn=batch, max_sig=batch * 12,
+    engines = [fa.VerifyEngine(device if device is not None else k % args.gpus, max_txn=batch, max_sig=batch * 12,
                                max_arena=batch * frag_bytes, ring_depth=inflight) for k in range(tiles_n)]
     warm(engines, inflight)
-    inl = tile.Link(1 << args.depth_lg, 1232)
+    P = max(1, args.producers)
+    inls = [tile.Link(1 << args.depth_lg, 1232) for _ in range(P)]
     vms, vers = [], []
     for k in range(tiles_n):
         ver = tile.EngineVerifier([engines[k]])
         outl = tile.Link(1 << 14, tile.TPU_DCACHE_MTU, data_sz=tile.vmux_dcache_data_sz(1 << 14, batch, inflight))
-        vms.append(tile.VerifyMuxTile(inl, outl, ver, batch_txn_max=batch, inflight_max=inflight,
-                                      batch_wait_us=args.wait_us, round_robin_idx=k, round_robin_cnt=tiles_n))
+        vms.append(tile.VerifyMuxTile(inls, outl, ver, batch_txn_max=batch, inflight_max=inflight,
+                                      batch_wait_us=args.wait_us, round_robin_idx=k, round_robin_cnt=tiles_n,
+                                      gpu_parse=bool(args.gpu_parse)))
         vers.append((ver, outl))
+    cpus = cpus or workload.physical_cpus()
+    # tile k's thread is pinned to cpus[P + k] (VerifyMuxTile.start inherits the caller's mask)
     start = time.perf_counter()
-    prod = start_producer(args, inl, arena, offs, sizes, rate, workload.physical_cpus())
-    for vm in vms:
+    prods = [start_producer(args, inls[j], arena, offs[j::P], sizes[j::P], rate / P, cpus, j) for j in range(P)]
+    keep = os.sched_getaffinity(0)
+    for k, vm in enumerate(vms):
+        if args.pin:
+            os.sched_setaffinity(0, {cpus[(P + k) % len(cpus)]})
         vm.start()
+    os.sched_setaffinity(0, keep)
     while any(vm.final_cnt() < len(ps) for vm in vms):
         if time.perf_counter() - start > 300:
             raise SystemExit("verify mux tiles timed out")
@@ -187,7 +218,8 @@ def run_once_mux(args, ps, arena, offs, sizes, n_sig, modes, tiles_n, batch, inf
     wall = time.perf_counter() - start
     for vm in vms:
         vm.stop()
-    n_pub, prod_s = prod.join()
+    joined = [pr.join() for pr in prods]
+    n_pub, prod_s = sum(j[0] for j in joined), max(j[1] for j in joined)
     stats = [vm.stats() for vm in vms]
     mstats = [vm.mux_stats() for vm in vms]
     lat = np.concatenate([vm.latencies_ns() for vm in vms]) / 1e6
@@ -195,7 +227,9 @@ def run_once_mux(args, ps, arena, offs, sizes, n_sig, modes, tiles_n, batch, inf
     agg["overrun"] = int(sum(m["overrun_polling"] + m["overrun_reading"] for m in mstats))
     res = {
         "metric": "verify mux tile end-to-end transactions/s (tango in -> GPU verify -> tango out)",
-        "tile": "fdgpu_vmux on fdt_mux_run (mux callbacks; registered out dcache, no staging copy)",
+        "tile": "fdgpu_vmux on fdt_mux_run (mux callbacks; registered out dcache, no staging copy)"
+                + ("; fd_txn_parse on the GPU" if args.gpu_parse else "; fd_txn_parse on the tile core"),
+        "producers": P,
         "txns_per_s": round(len(ps) / wall, 1),
         "sigs_per_s": round(agg["sigs"] / wall, 1),
         "wall_s": round(wall, 4), "producer_s": round(prod_s, 4), "producer_published": int(n_pub),

@@ -27,9 +27,25 @@ static int nv_poll(void *ctx, int64_t ticket, int8_t *codes, int blocking) {
   return FDGPU_OK;
 }
 
+/* frag batches: every frag "parses" to the footprint the tile reserved */
+static int64_t nv_submit_frags(void *ctx, uint8_t const *arena, uint64_t arena_sz, fdgpu_frag_ex_t const *frags,
+                               uint64_t n, uint64_t trailer_sz) {
+  (void)arena; (void)arena_sz; (void)frags; (void)trailer_sz;
+  nv_t *v = (nv_t *)ctx;
+  v->cnt[v->next % NV_RING] = n;
+  return v->next++;
+}
+
+static int nv_poll_frags(void *ctx, int64_t ticket, int8_t *codes, uint8_t *trailers, int blocking) {
+  (void)trailers;
+  return nv_poll(ctx, ticket, codes, blocking);
+}
+
 void null_verifier_make(fdgpu_verifier_t *out) {
   memset(out, 0, sizeof(*out));
   out->ctx = calloc(1, sizeof(nv_t));
   out->submit = nv_submit;
   out->poll = nv_poll;
+  out->submit_frags = nv_submit_frags;
+  out->poll_frags = nv_poll_frags;
 }

@@ -40,6 +40,7 @@ def main():
     ap.add_argument("--prefill", type=int, default=0, help="1: publish everything before the tiles start")
     ap.add_argument("--mux", type=int, default=0, help="1: the mux-callback tile (fdgpu_vmux on fdt_mux_run)")
     ap.add_argument("--inflight", type=int, default=4)
+    ap.add_argument("--gpu-parse", type=int, default=0, help="1 (with --mux 1): the tile hands the parse to the verifier")
     ap.add_argument("--cpus", default="", help="comma-separated CPUs for tile k (default: physical cores 1, 2, ...)"
                                                "; 'none' leaves the threads unpinned")
     args = ap.parse_args()
@@ -63,7 +64,8 @@ def main():
                                  data_sz=tile.vmux_dcache_data_sz(1 << 14, args.batch, args.inflight))
                 vts.append((tile.VerifyMuxTile(inl, outl, NullVerifier(), batch_txn_max=args.batch,
                                                inflight_max=args.inflight, round_robin_idx=k, round_robin_cnt=T,
-                                               batch_bytes_max=args.batch * 2176), outl))
+                                               batch_bytes_max=args.batch * 2176, gpu_parse=bool(args.gpu_parse)),
+                            outl))
             else:
                 outl = tile.Link(1 << 12, tile.TPU_DCACHE_MTU)
                 vts.append((tile.VerifyTile(inl, outl, NullVerifier(), batch_txn_max=args.batch,
