@@ -257,8 +257,8 @@ FDT_HD uint64_t fdt_parse_core(const uint8_t *payload, uint64_t payload_sz, fdt_
    table counts; for v0 the instruction list is walked to reach the table
    count) with none of the structural checks: the same reads of the same
    bytes as the parser, so whenever the payload is a valid transaction the
-   two agree.  0 when the walk runs past the payload (the parser then fails
-   too).  *sig_cnt gets the leading signature count.  The verify tile uses it
+   two agree.  0 when the walk runs past the payload or the footprint would
+   exceed FDT_TXN_MAX_SZ (the parser then fails too).  *sig_cnt gets the leading signature count.  The verify tile uses it
    to reserve a frag's trailer before the GPU has parsed the frag. */
 FDT_HD uint64_t fdt_peek_core(const uint8_t *payload, uint64_t payload_sz, uint64_t *sig_cnt_out) {
   fdt_reader r;
@@ -272,7 +272,7 @@ FDT_HD uint64_t fdt_peek_core(const uint8_t *payload, uint64_t payload_sz, uint6
     const bool v0 = (b0 & 0x80) != 0;
     if (v0 && ((b0 & 0x7f) != FDT_TXN_V0 || !r.u8(x))) break;
     if (!r.skip(2) || !r.cu16(acct_cnt) || !r.skip(32ULL * acct_cnt + 32) || !r.cu16(instr_cnt) ||
-        instr_cnt > FDT_TXN_INSTR_MAX)
+        instr_cnt > FDT_TXN_INSTR_MAX || !r.need(3ULL * instr_cnt))
       break;
     if (v0) {
       bool ok = true;
@@ -280,9 +280,10 @@ FDT_HD uint64_t fdt_peek_core(const uint8_t *payload, uint64_t payload_sz, uint6
         uint16_t n_acct, data_sz;
         ok = r.u8(x) && r.cu16(n_acct) && r.skip(n_acct) && r.cu16(data_sz) && r.skip(data_sz);
       }
-      if (!ok || !r.cu16(lut_cnt) || lut_cnt > FDT_TXN_ADDR_TABLE_LOOKUP_MAX) break;
+      if (!ok || !r.cu16(lut_cnt) || lut_cnt > FDT_TXN_ADDR_TABLE_LOOKUP_MAX || !r.need(34ULL * lut_cnt)) break;
     }
     fp = fdt_parse_footprint(instr_cnt, lut_cnt);
+    if (fp > FDT_TXN_MAX_SZ) fp = 0;               /* no transaction has one: the parse fails */
   } while (0);
   if (sig_cnt_out) *sig_cnt_out = sig_cnt;
   return fp;

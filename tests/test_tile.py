@@ -379,6 +379,7 @@ def _mixed_stream(n, seed, oracle_ok=True):
     duplicates re-sent at short and long distances (inside and beyond the
     16-deep tcache) and some unparseable frags."""
     rnd = random.Random(seed)
+    junk = random.Random(seed ^ 0x7A7A)
     a1, t1, _ = workload.cfg1(n // 2, seed=seed)
     a3, t3, _ = workload.cfg3(n // 4, seed=seed + 1)
     base = workload.payloads(a1, t1) + workload.payloads(a3, t3)
@@ -393,6 +394,9 @@ def _mixed_stream(n, seed, oracle_ok=True):
             out.append(p[:-3])                                  # truncated: parse failure
         elif r < 0.20:
             q = bytearray(p); q[0] = 0; out.append(bytes(q))     # zero signatures
+        elif r < 0.21:                                           # random bytes behind a plausible count
+            out.append(bytes([junk.randrange(1, 13)]) +
+                       bytes(junk.getrandbits(8) for _ in range(junk.randrange(64, 1232))))
     return out
 
 
@@ -632,4 +636,8 @@ def test_txn_peek_agrees_with_parse(quic_corpus, fixtures):
             parsed += 1
             d = tile.txn_decode(raw)
             assert pk == fp and sc == d["signature_cnt"] and d["signature_off"] == 1, p.hex()[:80]
+        assert pk <= tile.TXN_MAX_SZ
+    for _ in range(20000):                                       # random bytes: reservations stay bounded
+        p = bytes([rnd.randrange(1, 13)]) + bytes(rnd.getrandbits(8) for _ in range(rnd.randrange(0, 1232)))
+        assert tile.txn_peek(p)[0] <= tile.TXN_MAX_SZ
     assert parsed > 2000
