@@ -205,6 +205,25 @@ int fdt_tcache_insert(void *tc, uint64_t tag) {
   return 0;
 }
 
+void fdt_tagring_init(fdt_tagring_t *r, uint64_t depth) {
+  std::memset(r, 0, sizeof *r);
+  r->depth = depth < 1 ? 1 : depth > FDT_TAGRING_MAX ? FDT_TAGRING_MAX : depth;
+}
+
+int fdt_tagring_query(const fdt_tagring_t *r, uint64_t tag) {
+  if (tag == FDT_TCACHE_TAG_NULL) return 1;
+  uint64_t hit = 0;
+  for (uint64_t i = 0; i < r->depth; i++) hit |= (uint64_t)(r->tag[i] == tag);   /* no early exit: vectorised */
+  return hit ? 1 : 0;
+}
+
+int fdt_tagring_insert(fdt_tagring_t *r, uint64_t tag) {
+  if (fdt_tagring_query(r, tag)) return 1;
+  r->tag[r->oldest] = tag;                       /* the evicted (oldest) tag leaves with its slot */
+  r->oldest = r->oldest + 1 >= r->depth ? 0 : r->oldest + 1;
+  return 0;
+}
+
 /* -------------------------------------------------------------- hash */
 
 /* xxhash-r39 over 64-bit lanes (fd_hash.c:12-73). */

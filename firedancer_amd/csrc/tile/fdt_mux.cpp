@@ -201,7 +201,11 @@ struct fdgpu_vmux {
   fdgpu_vmux_cfg_t cfg{};
   fdgpu_verifier_t ver{};
   std::vector<uint64_t> tcache_mem;
-  void *tcache = nullptr;
+  void *tcache = nullptr;                 /* fd_tcache (depth > FDT_TAGRING_MAX) ... */
+  fdt_tagring_t ring{};                   /* ... or the ring scan (the tile's 16-deep default) */
+  bool use_ring = false;
+  bool tc_query(uint64_t tag) const { return use_ring ? fdt_tagring_query(&ring, tag) : fdt_tcache_query(tcache, tag); }
+  void tc_insert(uint64_t tag) { if (use_ring) (void)fdt_tagring_insert(&ring, tag); else (void)fdt_tcache_insert(tcache, tag); }
   uint64_t out_chunk = 0;                 /* write cursor */
   uint64_t cur_sz = 0;                    /* the frag between during_frag and after_frag */
   bool cur_ok = false;
@@ -271,6 +275,10 @@ struct fdgpu_vmux {
       const size_t n = b->items.size();
       while (b->next < n) {
         const size_t k = b->next;
+        if (gpu_parse && k + 8 < n) {            /* the trailer store of a frag soon published: own the line */
+          const VItem &f = b->items[k + 8];
+          __builtin_prefetch(out_laddr(f.chunk) + align2(f.sz), 1);
+        }
         const VItem &it = b->items[k];
         const int code = b->codes[k];
         if (gpu_parse && (code == FDGPU_CODE_PARSE_FAIL || code == FDGPU_CODE_TRAILER_CAP)) {
@@ -285,7 +293,7 @@ struct fdgpu_vmux {
         uint8_t *frag = out_laddr(it.chunk);
         const uint64_t tag = it.tag;
         int outcome;
-        if (fdt_tcache_query(tcache, tag)) outcome = FD_TXN_VERIFY_DEDUP;
+        if (tc_query(tag)) outcome = FD_TXN_VERIFY_DEDUP;
         else if (code != FD_ED25519_SUCCESS) outcome = FD_TXN_VERIFY_FAILED;
         else outcome = FD_TXN_VERIFY_SUCCESS;
         if (outcome == FD_TXN_VERIFY_SUCCESS) {
@@ -294,7 +302,7 @@ struct fdgpu_vmux {
             st.backpressure++;                    /* is resolved again from the top (nothing inserted yet) */
             return;
           }
-          (void)fdt_tcache_insert(tcache, tag);   /* not present: the query above missed */
+          tc_insert(tag);                          /* not present: the query above missed */
           uint64_t sz = it.sz;
           if (gpu_parse) {                        /* [payload][pad][fd_txn_t][u16 payload_sz] (fd_verify.c:93-136) */
             const uint64_t toff = align2(it.sz);
@@ -419,6 +427,8 @@ void vm_after_frag(void *ctx, uint64_t in_idx, uint64_t seq, uint64_t *opt_sig, 
     VBatch &b = *t->open;
     if (b.items.empty()) { b.first_chunk = t->out_chunk; b.t_first = now_ns(); }
     const uint64_t off = (t->out_chunk - b.first_chunk) << FDT_CHUNK_LG_SZ;
+    __builtin_prefetch(b.items.data() + b.items.size() + 6, 1);      /* reserved: stores a few frags ahead */
+    __builtin_prefetch(b.frags.data() + b.frags.size() + 12, 1);
     b.frags.push_back(fdgpu_frag_ex_t{(uint32_t)off, (uint32_t)payload_sz, (uint32_t)b.tr_used, (uint32_t)fp});
     b.items.push_back(VItem{seq, t->cur_tag, (uint32_t)t->out_chunk, (uint32_t)payload_sz, 1u, (uint32_t)*opt_tsorig,
                             (uint32_t)b.tr_used, (uint32_t)fp});
@@ -518,6 +528,8 @@ fdgpu_vmux_t *fdgpu_vmux_new(const fdgpu_vmux_cfg_t *cfg, fdgpu_verifier_t ver) 
   if (!fp) { delete t; return nullptr; }
   t->tcache_mem.assign(fp / 8, 0);
   t->tcache = fdt_tcache_new(t->tcache_mem.data(), c.tcache_depth, c.tcache_map_cnt);
+  t->use_ring = c.tcache_depth <= FDT_TAGRING_MAX;
+  fdt_tagring_init(&t->ring, c.tcache_depth);
   t->ver = ver;
   t->out_chunk = c.out_chunk0;
   uint64_t n = 1;

@@ -202,6 +202,9 @@ def lib():
         "fdt_txn_footprint": (u64, [u64, u64]),
         "fdt_txn_parse": (u64, [vp, u64, vp, c.POINTER(ParseCounters)]),
         "fdt_txn_peek": (u64, [vp, u64, c.POINTER(u64)]),
+        "fdt_tagring_init": (None, [vp, u64]),
+        "fdt_tagring_query": (c.c_int, [vp, u64]),
+        "fdt_tagring_insert": (c.c_int, [vp, u64]),
         "fdgpu_dispatch_new": (vp, [c.POINTER(vp), c.c_uint32]),
         "fdgpu_dispatch_delete": (None, [vp]),
         "fdgpu_dispatch_verifier": (Verifier, [vp]),

@@ -116,6 +116,18 @@ int      fdt_tcache_query    ( void const * tcache, uint64_t tag );
 /* returns dup (1: already present, unchanged; 0: inserted, oldest evicted) */
 int      fdt_tcache_insert   ( void * tcache, uint64_t tag );
 
+/* A small tcache as a ring scan: the verify tile's 16-deep tcache
+   (fd_verify.h:6-7) answers exactly as fdt_tcache_query / fdt_tcache_insert
+   of the same depth (the map of fd_tcache.h indexes exactly the ring's
+   tags; the null tag 0 always counts as present, as the map's empty slots
+   match it), with one vector compare over the ring instead of probing and
+   back-shifting the map.  depth 1..FDT_TAGRING_MAX. */
+#define FDT_TAGRING_MAX 32
+typedef struct { uint64_t tag[ FDT_TAGRING_MAX ]; uint64_t depth, oldest; } fdt_tagring_t;
+void fdt_tagring_init  ( fdt_tagring_t * r, uint64_t depth );
+int  fdt_tagring_query ( fdt_tagring_t const * r, uint64_t tag );   /* 1: present */
+int  fdt_tagring_insert( fdt_tagring_t * r, uint64_t tag );         /* 1: was present (no change) */
+
 /* ---------------------------------------------------------------- hash */
 
 uint64_t fdt_hash( uint64_t seed, void const * buf, uint64_t sz );

@@ -641,3 +641,24 @@ def test_txn_peek_agrees_with_parse(quic_corpus, fixtures):
         p = bytes([rnd.randrange(1, 13)]) + bytes(rnd.getrandbits(8) for _ in range(rnd.randrange(0, 1232)))
         assert tile.txn_peek(p)[0] <= tile.TXN_MAX_SZ
     assert parsed > 2000
+
+
+def test_tagring_equals_tcache():
+    """fdt_tagring (the verify tile's 16-deep tcache as a ring scan) answers
+    every query and insert exactly as fdt_tcache of the same depth (the
+    reference's FD_TCACHE_QUERY / FD_TCACHE_INSERT, fd_tcache.h:281-404), on
+    streams with repeats at every distance and the null tag."""
+    import ctypes
+    L = tile.lib()
+    rnd = random.Random(0x7A6)
+    for depth in (1, 2, 5, 16, 32):
+        tc = tile.TCache(depth, 64 if depth <= 16 else 128)
+        ring = ctypes.create_string_buffer(8 * (32 + 2))
+        L.fdt_tagring_init(ring, depth)
+        pool = [rnd.getrandbits(64) for _ in range(3 * depth + 4)] + [0]
+        for _ in range(30000):
+            tag = rnd.choice(pool) if rnd.random() < 0.8 else rnd.getrandbits(64)
+            if rnd.random() < 0.5:
+                assert L.fdt_tagring_query(ring, tag) == tc.query(tag), (depth, tag)
+            else:
+                assert L.fdt_tagring_insert(ring, tag) == tc.insert(tag), (depth, tag)

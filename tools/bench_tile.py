@@ -48,6 +48,9 @@ def main():
                     help="1: as many quic links (producers) as verify tiles in every run")
     ap.add_argument("--pin", type=int, default=1,
                     help="1: producer and each tile thread pinned to its own physical core (workload.physical_cpus)")
+    ap.add_argument("--cpu-offset", type=int, default=0,
+                    help="skip this many of workload.physical_cpus() before pinning (CPU 0 takes interrupts)")
+    ap.add_argument("--reps", type=int, default=1, help="repeat every run of the sweep")
     ap.add_argument("--out", default="")
     ap.add_argument("--sweep", default="", help="';'-separated runs of 'tiles,batch,inflight,rate' over the same txns")
     args = ap.parse_args()
@@ -63,6 +66,7 @@ def main():
 
     runs = [tuple(float(x) for x in r.split(",")) for r in args.sweep.split(";") if r] or \
         [(args.tiles or args.gpus, args.batch, args.inflight, args.rate)]
+    runs = [r for r in runs for _ in range(max(1, args.reps))]
     ok = True
     lines = []
     for tiles_n, batch, inflight, rate in runs:
@@ -201,7 +205,7 @@ def run_once_mux(args, ps, arena, offs, sizes, n_sig, modes, tiles_n, batch, inf
                                       batch_wait_us=args.wait_us, round_robin_idx=k, round_robin_cnt=tiles_n,
                                       gpu_parse=bool(args.gpu_parse)))
         vers.append((ver, outl))
-    cpus = cpus or workload.physical_cpus()
+    cpus = cpus or workload.physical_cpus()[getattr(args, "cpu_offset", 0):] or workload.physical_cpus()
     # tile k's thread is pinned to cpus[P + k] (VerifyMuxTile.start inherits the caller's mask)
     start = time.perf_counter()
     prods = [start_producer(args, inls[j], arena, offs[j::P], sizes[j::P], rate / P, cpus, j) for j in range(P)]
@@ -236,7 +240,7 @@ def run_once_mux(args, ps, arena, offs, sizes, n_sig, modes, tiles_n, batch, inf
         "gpus": args.gpus, "tiles": tiles_n, "batch_txn_max": batch, "inflight": inflight,
         "rate_target": rate, "workload": "cfg3 (1-12 sigs/txn, payload <= 1232 B, 10% corrupted)"
         if args.multi else "cfg1 (1 sig, msg U[180,220] B, 10% corrupted)",
-        "txns": len(ps), "sigs": n_sig,
+        "txns": len(ps), "sigs": n_sig, "batch_wait_us": args.wait_us, "cpus": cpus[:P + tiles_n],
         "batch_latency_ms": {"p50": round(float(np.percentile(lat, 50)), 3) if len(lat) else None,
                              "p99": round(float(np.percentile(lat, 99)), 3) if len(lat) else None,
                              "n": int(len(lat))},

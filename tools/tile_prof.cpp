@@ -12,6 +12,8 @@
    sizes u32.) */
 #define _GNU_SOURCE 1
 #include <dlfcn.h>
+#include <pthread.h>
+#include <sched.h>
 #include <signal.h>
 #include <sys/syscall.h>
 #include <time.h>
@@ -109,6 +111,10 @@ int main(int argc, char **argv) {
     std::atomic<bool> started{false};
     uint64_t t0 = 0;
     std::thread th([&]() {
+      if (getenv("TILE_PROF_CPU")) {                    /* the tile thread alone on that CPU */
+        cpu_set_t cs; CPU_ZERO(&cs); CPU_SET(atoi(getenv("TILE_PROF_CPU")), &cs);
+        pthread_setaffinity_np(pthread_self(), sizeof cs, &cs);
+      }
       tid = (pid_t)syscall(SYS_gettid);
       started = true;
       t0 = now_ns();
@@ -126,7 +132,7 @@ int main(int argc, char **argv) {
     (void)tm;
     g_on = true;
     timer_settime(tm, 0, &its, nullptr);
-    while (fdgpu_vmux_final_cnt(vm) < n) {}
+    while (fdgpu_vmux_final_cnt(vm) < n) usleep(20);   /* never on the tile's CPU for long */
     const uint64_t t1 = now_ns();
     g_on = false;
     halt = 1;
