@@ -265,8 +265,10 @@ struct fdgpu_vmux {
     while (!inflight.empty()) {
       VBatch *b = inflight.front();
       if (!b->done) {
+        const uint64_t p0 = now_ns();
         const int rc = gpu_parse ? ver.poll_frags(ver.ctx, b->ticket, b->codes.data(), b->trailers.data(), 0)
                                  : ver.poll(ver.ctx, b->ticket, b->codes.data(), 0);
+        st.poll_ns += now_ns() - p0;
         if (rc == FDGPU_PENDING) return;
         if (rc != FDGPU_OK) { error = rc; *poll_in = 0; return; }
         b->done = true;
@@ -345,6 +347,8 @@ struct fdgpu_vmux {
     if (!open->closed && now_ns() - open->t_first < cfg.batch_wait_ns) return;
     if (inflight.size() >= cfg.inflight_max) return;
     int64_t t;
+    const uint64_t s0 = now_ns();
+    struct Acc { uint64_t &ns; uint64_t t0; ~Acc() { ns += now_ns() - t0; } } acc{st.submit_ns, s0};
     if (gpu_parse) {
       if (open->trailers.size() < open->tr_used) open->trailers.resize(open->tr_used);
       t = ver.submit_frags(ver.ctx, out_laddr(open->first_chunk), open->end_off, open->frags.data(),

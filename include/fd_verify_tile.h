@@ -269,9 +269,9 @@ typedef struct {
   uint64_t backpressure;    /* steps that stalled on out-link credits */
   uint64_t lat_cnt;         /* batch latencies recorded (ingest of first frag -> publish) */
   uint64_t verify_errors;   /* txns of batches the verifier rejected as malformed (failed, not published) */
-  /* where the step-loop tile's time goes (fdgpu_vtile only; 0 for vmux) */
+  /* where the tile's time goes (ingest_ns: fdgpu_vtile only) */
   uint64_t ingest_ns;       /* polling the in link, copying and parsing frags */
-  uint64_t submit_ns;       /* inside the verifier's submit / stage calls */
+  uint64_t submit_ns;       /* inside the verifier's submit / stage calls (and the submit-wait checks) */
   uint64_t poll_ns;         /* inside the verifier's non-blocking polls */
   uint64_t no_slot_steps;   /* steps that could not open a batch: every batch or ring slot in flight */
 } fdgpu_vtile_stats_t;

@@ -62,6 +62,7 @@ int main(int argc, char **argv) {
   auto S = rd<uint32_t>(argv[3]);
   const int gpu_parse = argc > 4 ? atoi(argv[4]) : 1;
   const int repeat = argc > 5 ? atoi(argv[5]) : 3;
+  const int tiles = getenv("TILE_PROF_TILES") ? atoi(getenv("TILE_PROF_TILES")) : 1;
   const uint64_t n = O.size(), depth = 1ull << 21;
   /* in link: mcache + dcache, prefilled */
   std::vector<fdt_frag_meta_t> in_mc(depth);
@@ -71,12 +72,11 @@ int main(int argc, char **argv) {
   const uint64_t in_chunk0 = 0, in_wmark = fdt_dcache_wmark(0, in_data / 64, FDT_TPU_MTU);
   /* out link */
   const uint64_t out_depth = 1ull << 14, batch = 16384, inflight = 4;
-  std::vector<fdt_frag_meta_t> out_mc(out_depth);
   const uint64_t out_data = fdgpu_vmux_dcache_data_sz(out_depth, (uint32_t)batch, (uint32_t)inflight);
-  std::vector<uint8_t> out_dc(out_data + 64);
-  uint8_t *out_base = (uint8_t *)(((uintptr_t)out_dc.data() + 63) & ~(uintptr_t)63);
-  fdgpu_verifier_t ver;
-  null_verifier_make(&ver);
+  std::vector<std::vector<fdt_frag_meta_t>> out_mcs(tiles, std::vector<fdt_frag_meta_t>(out_depth));
+  std::vector<std::vector<uint8_t>> out_dcs(tiles, std::vector<uint8_t>(out_data + 64));
+  std::vector<fdgpu_verifier_t> vers(tiles);
+  for (auto &v : vers) null_verifier_make(&v);
   struct sigaction sa{};
   sa.sa_sigaction = on_prof;
   sa.sa_flags = SA_SIGINFO | SA_RESTART;
@@ -85,42 +85,50 @@ int main(int argc, char **argv) {
   double best = 1e30;
   for (int r = 0; r < repeat; r++) {
     fdt_mcache_init(in_mc.data(), depth, 0);
-    fdt_mcache_init(out_mc.data(), out_depth, 0);
     uint64_t chunk = in_chunk0;
     for (uint64_t i = 0; i < n; i++) {
       memcpy(in_base + (chunk << 6), A.data() + O[i], S[i]);
       fdt_mcache_publish(in_mc.data(), depth, i, 0, chunk, S[i], fdt_frag_meta_ctl(0, 1, 1, 0), 0, 0);
       chunk = fdt_dcache_compact_next(chunk, S[i], in_chunk0, in_wmark);
     }
-    fdgpu_vmux_cfg_t vc{};
-    vc.in_cnt = 1; vc.in_base[0] = in_base; vc.in_chunk0[0] = in_chunk0; vc.in_wmark[0] = in_wmark;
-    vc.out_base = out_base; vc.out_chunk0 = 0; vc.out_wmark = fdt_dcache_wmark(0, out_data / 64, FDT_TPU_DCACHE_MTU);
-    vc.cr_max = out_depth; vc.round_robin_cnt = 1; vc.hashmap_seed = 0x5EED;
-    vc.batch_txn_max = (uint32_t)batch; vc.inflight_max = (uint32_t)inflight; vc.batch_wait_ns = 200000;
-    vc.batch_bytes_max = batch * 2176; vc.gpu_parse = (uint32_t)gpu_parse;
-    fdgpu_vmux_t *vm = fdgpu_vmux_new(&vc, ver);
-    if (!vm) { fprintf(stderr, "vmux_new failed\n"); return 1; }
-    fdt_mux_cfg_t mc{};
-    mc.in_cnt = 1; mc.in_mcache[0] = in_mc.data(); mc.in_depth[0] = depth; mc.in_seq0[0] = 0;
-    mc.out_mcache = out_mc.data(); mc.out_depth = out_depth; mc.out_seq0 = 0;
-    mc.flags = FDT_MUX_FLAG_COPY | FDT_MUX_FLAG_MANUAL_PUBLISH; mc.burst = 1; mc.cr_max = out_depth; mc.lazy_iters = 16;
+    std::vector<fdgpu_vmux_t *> vms(tiles);
+    std::vector<fdt_mux_cfg_t> mcs(tiles);
+    std::vector<uint64_t> halts(tiles, 0);        /* read by fdt_mux_run through a volatile pointer */
+    std::vector<fdt_mux_stats_t> mss(tiles);
     fdt_mux_callbacks_t cb = fdgpu_vmux_callbacks();
-    volatile uint64_t halt = 0;
-    fdt_mux_stats_t ms{};
+    for (int k = 0; k < tiles; k++) {
+      fdt_mcache_init(out_mcs[k].data(), out_depth, 0);
+      uint8_t *out_base = (uint8_t *)(((uintptr_t)out_dcs[k].data() + 63) & ~(uintptr_t)63);
+      fdgpu_vmux_cfg_t vc{};
+      vc.in_cnt = 1; vc.in_base[0] = in_base; vc.in_chunk0[0] = in_chunk0; vc.in_wmark[0] = in_wmark;
+      vc.out_base = out_base; vc.out_chunk0 = 0; vc.out_wmark = fdt_dcache_wmark(0, out_data / 64, FDT_TPU_DCACHE_MTU);
+      vc.cr_max = out_depth; vc.round_robin_idx = (uint64_t)k; vc.round_robin_cnt = (uint64_t)tiles; vc.hashmap_seed = 0x5EED;
+      vc.batch_txn_max = (uint32_t)batch; vc.inflight_max = (uint32_t)inflight; vc.batch_wait_ns = 200000;
+      vc.batch_bytes_max = batch * 2176; vc.gpu_parse = (uint32_t)gpu_parse;
+      vms[k] = fdgpu_vmux_new(&vc, vers[k]);
+      if (!vms[k]) { fprintf(stderr, "vmux_new failed\n"); return 1; }
+      fdt_mux_cfg_t &mc = mcs[k];
+      mc = fdt_mux_cfg_t{};
+      mc.in_cnt = 1; mc.in_mcache[0] = in_mc.data(); mc.in_depth[0] = depth; mc.in_seq0[0] = 0;
+      mc.out_mcache = out_mcs[k].data(); mc.out_depth = out_depth; mc.out_seq0 = 0;
+      mc.flags = FDT_MUX_FLAG_COPY | FDT_MUX_FLAG_MANUAL_PUBLISH; mc.burst = 1; mc.cr_max = out_depth; mc.lazy_iters = 16;
+    }
     pid_t tid = 0;
-    std::atomic<bool> started{false};
+    std::atomic<int> started{0};
     uint64_t t0 = 0;
-    std::thread th([&]() {
-      if (getenv("TILE_PROF_CPU")) {                    /* the tile thread alone on that CPU */
-        cpu_set_t cs; CPU_ZERO(&cs); CPU_SET(atoi(getenv("TILE_PROF_CPU")), &cs);
-        pthread_setaffinity_np(pthread_self(), sizeof cs, &cs);
-      }
-      tid = (pid_t)syscall(SYS_gettid);
-      started = true;
-      t0 = now_ns();
-      fdt_mux_run(&mc, &cb, vm, &halt, &ms);
-    });
-    while (!started) {}
+    std::vector<std::thread> ths;
+    for (int k = 0; k < tiles; k++)
+      ths.emplace_back([&, k]() {
+        if (getenv("TILE_PROF_CPU")) {                  /* tile k alone on CPU base + k */
+          cpu_set_t cs; CPU_ZERO(&cs); CPU_SET(atoi(getenv("TILE_PROF_CPU")) + k, &cs);
+          pthread_setaffinity_np(pthread_self(), sizeof cs, &cs);
+        }
+        if (k == 0) { tid = (pid_t)syscall(SYS_gettid); t0 = now_ns(); }
+        started++;
+        while (started.load() < tiles) {}
+        fdt_mux_run(&mcs[k], &cb, vms[k], (volatile uint64_t *)&halts[k], &mss[k]);
+      });
+    while (started.load() < tiles || !tid) {}
     timer_t tm;
     sigevent se{};
     se.sigev_notify = SIGEV_THREAD_ID;
@@ -128,23 +136,27 @@ int main(int argc, char **argv) {
     se.sigev_signo = SIGPROF;
     timer_create(CLOCK_MONOTONIC, &se, &tm);
     itimerspec its{};
-    its.it_interval.tv_nsec = its.it_value.tv_nsec = getenv("TILE_PROF_OFF") ? 0 : 200000;   /* 5 kHz (the tile thread never sleeps) */
-    (void)tm;
+    its.it_interval.tv_nsec = its.it_value.tv_nsec = getenv("TILE_PROF_OFF") ? 0 : 200000;   /* 5 kHz (tile 0) */
     g_on = true;
     timer_settime(tm, 0, &its, nullptr);
-    while (fdgpu_vmux_final_cnt(vm) < n) usleep(20);   /* never on the tile's CPU for long */
+    for (int k = 0; k < tiles; k++)
+      while (fdgpu_vmux_final_cnt(vms[k]) < n) usleep(20);   /* never on a tile's CPU for long */
     const uint64_t t1 = now_ns();
     g_on = false;
-    halt = 1;
-    th.join();
+    for (int k = 0; k < tiles; k++) __atomic_store_n(&halts[k], 1, __ATOMIC_RELEASE);
+    for (auto &th : ths) th.join();
     timer_delete(tm);
-    fdgpu_vtile_stats_t st;
-    fdgpu_vmux_stats(vm, &st);
+    uint64_t pub = 0, pf = 0;
+    for (int k = 0; k < tiles; k++) {
+      fdgpu_vtile_stats_t st;
+      fdgpu_vmux_stats(vms[k], &st);
+      pub += st.published; pf += st.parse_fail;
+    }
     const double ns = (double)(t1 - t0) / n;
     best = std::min(best, ns);
-    printf("run %d: %.1f ns/frag (%.2f M/s)  published %llu parse_fail %llu\n", r, ns, 1e3 / ns,
-           (unsigned long long)st.published, (unsigned long long)st.parse_fail);
-    fdgpu_vmux_delete(vm);
+    printf("run %d (%d tiles): %.1f ns/frag (%.2f M/s)  published %llu parse_fail %llu\n", r, tiles, ns, 1e3 / ns,
+           (unsigned long long)pub, (unsigned long long)pf);
+    for (int k = 0; k < tiles; k++) fdgpu_vmux_delete(vms[k]);
   }
   /* symbolise: object + offset (for addr2line -f -i -e <object>) */
   std::map<std::string, uint64_t> by;
