@@ -74,8 +74,8 @@ struct Slot {
   uint16_t *d_txn_sz = nullptr;
   fdgpu_txn_t *d_txd = nullptr;
   uint32_t *d_cnt = nullptr, *d_sig0 = nullptr, *d_blocktot = nullptr, *d_n_sig = nullptr;
-  uint8_t *d_tr = nullptr, *h_tr = nullptr;
-  uint64_t tr_cap = 0, tr_sz = 0;
+  uint8_t *d_tr = nullptr, *h_tr = nullptr;   /* [codes, padded to 64][trailers]: one read-back */
+  uint64_t tr_cap = 0, tr_sz = 0, tr_base = 0;
 };
 
 }  // namespace
@@ -196,12 +196,13 @@ bool slot_frag_bufs(Slot &s, const fdgpu_cfg_t &c, uint64_t tr) {
     HIPCHK(hipMalloc((void **)&s.d_blocktot, nb * sizeof(uint32_t)), false);
     HIPCHK(hipMalloc((void **)&s.d_n_sig, sizeof(uint32_t)), false);
   }
+  tr += (c.max_txn + 64) & ~63ull;                      /* the codes go in front of the trailers */
   if (tr > s.tr_cap) {
     HIPCHK(hipStreamSynchronize(s.stream), false);
     if (s.d_tr) { (void)hipFree(s.d_tr); s.d_tr = nullptr; }
     if (s.h_tr) { (void)hipHostFree(s.h_tr); s.h_tr = nullptr; }
     s.tr_cap = 0;
-    const uint64_t want = std::max<uint64_t>(tr, 64 * 1024);
+    const uint64_t want = std::max<uint64_t>(tr + tr / 4, 256 * 1024);
     HIPCHK(hipMalloc((void **)&s.d_tr, want), false);
     HIPCHK(hipHostMalloc((void **)&s.h_tr, want, hipHostMallocDefault), false);
     s.tr_cap = want;
@@ -591,8 +592,8 @@ static int poll_slot(fdgpu_engine_t *e, int64_t ticket, int8_t *txn_codes, int b
     if (q == hipErrorNotReady) return FDGPU_PENDING;
     HIPCHK(q, FDGPU_ERR_DEVICE);
   }
-  if (txn_codes && s->txn_cnt) memcpy(txn_codes, s->h_codes, s->txn_cnt);
-  if (trailers && s->frag && s->tr_sz) memcpy(trailers, s->h_tr, s->tr_sz);
+  if (txn_codes && s->txn_cnt) memcpy(txn_codes, s->frag ? (const int8_t *)s->h_tr : s->h_codes, s->txn_cnt);
+  if (trailers && s->frag && s->tr_sz) memcpy(trailers, s->h_tr + s->tr_base, s->tr_sz);
   if (keep) s->held = true;
   else s->ticket = -1;
   return FDGPU_OK;
@@ -635,31 +636,32 @@ int64_t fdgpu_submit_frags(fdgpu_engine_t *e, uint8_t const *arena, uint64_t are
   Slot *s = free_slot(e);
   if (!s) { set_err("all ring slots hold unpolled batches"); return FDGPU_ERR_FULL; }
   if (!slot_frag_bufs(*s, e->cfg, trailer_sz) || !slot_ws(*s, bound)) return FDGPU_ERR_DEVICE;
+  /* the slack past the arena needs no zeroing here: every device reader of
+     a frag batch masks the bytes past its payload (fdt_reader, msg_block),
+     only their presence (FDGPU_ARENA_SLACK allocated) matters */
   if (region_covers(e, arena, arena_sz)) {
     if (arena_sz) HIPCHK(hipMemcpyAsync(s->d_arena, arena, arena_sz, hipMemcpyHostToDevice, s->stream), FDGPU_ERR_DEVICE);
-    HIPCHK(hipMemsetAsync(s->d_arena + arena_sz, 0, FDGPU_ARENA_SLACK, s->stream), FDGPU_ERR_DEVICE);
   } else {
     const uint64_t up = stage_arena(e, s, arena, arena_sz);
     if (up == UINT64_MAX) return FDGPU_ERR_DEVICE;
-    memset(s->h_arena + arena_sz, 0, FDGPU_ARENA_SLACK);
-    HIPCHK(hipMemcpyAsync(s->d_arena + up, s->h_arena + up, arena_sz + FDGPU_ARENA_SLACK - up, hipMemcpyHostToDevice,
-                          s->stream), FDGPU_ERR_DEVICE);
+    if (arena_sz > up)
+      HIPCHK(hipMemcpyAsync(s->d_arena + up, s->h_arena + up, arena_sz - up, hipMemcpyHostToDevice, s->stream),
+             FDGPU_ERR_DEVICE);
   }
+  const uint64_t tr_base = (n + 63) & ~63ull;
   if (n) {
     memcpy(s->h_fx, fx, n * sizeof(fdgpu_frag_ex_t));
     HIPCHK(hipMemcpyAsync(s->d_fx, s->h_fx, n * sizeof(fdgpu_frag_ex_t), hipMemcpyHostToDevice, s->stream), FDGPU_ERR_DEVICE);
-    HIPCHK(fdgpu_launch_frag_ingest(s->d_arena, s->d_fx, 4u, (uint32_t)n, s->d_txn_out, s->d_txn_sz, s->d_txd, s->d_cnt,
-                                    s->d_sig0, s->d_blocktot, s->d_n_sig, s->d_sigs, s->d_txns, s->stream),
+    HIPCHK(fdgpu_launch_frag_ring(s->d_arena, s->d_fx, (uint32_t)n, s->d_txn_out, s->d_txn_sz, s->d_txd, s->d_cnt,
+                                  s->d_sig0, s->d_blocktot, s->d_n_sig, s->d_sigs, s->d_txns, s->stream),
            FDGPU_ERR_DEVICE);
     HIPCHK(fdgpu_launch_verify_sigs(s->d_arena, s->d_sigs, (uint32_t)bound, nullptr, e->d_btab, s->d_ws, s->d_sig_codes,
                                     kflags(e), s->stream, s->d_n_sig, e->resident_blocks, e->kc_seed),
            FDGPU_ERR_DEVICE);
-    HIPCHK(fdgpu_launch_combine(s->d_txns, (uint32_t)n, s->d_sig_codes, s->d_txn_codes, nullptr, s->stream), FDGPU_ERR_DEVICE);
-    HIPCHK(fdgpu_launch_frag_codes(s->d_txn_sz, (uint32_t)n, s->d_txn_codes, s->stream), FDGPU_ERR_DEVICE);
-    HIPCHK(fdgpu_launch_trailer_pack(s->d_fx, (uint32_t)n, s->d_txn_out, s->d_txn_sz, s->d_tr, s->d_txn_codes, s->stream),
+    HIPCHK(fdgpu_launch_frag_finish(s->d_txns, (uint32_t)n, s->d_sig_codes, s->d_txn_sz, s->d_fx, s->d_txn_out,
+                                    (int8_t *)s->d_tr, s->d_tr + tr_base, s->stream),
            FDGPU_ERR_DEVICE);
-    HIPCHK(hipMemcpyAsync(s->h_codes, s->d_txn_codes, n, hipMemcpyDeviceToHost, s->stream), FDGPU_ERR_DEVICE);
-    if (trailer_sz) HIPCHK(hipMemcpyAsync(s->h_tr, s->d_tr, trailer_sz, hipMemcpyDeviceToHost, s->stream), FDGPU_ERR_DEVICE);
+    HIPCHK(hipMemcpyAsync(s->h_tr, s->d_tr, tr_base + trailer_sz, hipMemcpyDeviceToHost, s->stream), FDGPU_ERR_DEVICE);
   }
   ++s->flag_seq;
   if (e->flag_poll && !e->drop_flag) HIPCHK(hipStreamWriteValue32(s->stream, s->d_flag, s->flag_seq, 0), FDGPU_ERR_DEVICE);
@@ -669,6 +671,7 @@ int64_t fdgpu_submit_frags(fdgpu_engine_t *e, uint8_t const *arena, uint64_t are
   s->polls = 0;
   s->frag = true;
   s->tr_sz = trailer_sz;
+  s->tr_base = tr_base;
   s->ticket = e->next_ticket++;
   s->txn_cnt = n;
   return s->ticket;

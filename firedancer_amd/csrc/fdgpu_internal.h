@@ -105,11 +105,19 @@ hipError_t fdgpu_launch_frag_ingest(const uint8_t *d_arena, const void *d_frags,
                                     uint32_t *d_sig0, uint32_t *d_blocktot, uint32_t *d_n_sig,
                                     fdgpu_sig_desc_t *d_sigs, fdgpu_txn_desc_t *d_tds, hipStream_t stream);
 hipError_t fdgpu_launch_frag_codes(const uint16_t *d_txn_sz, uint32_t n, int8_t *d_codes, hipStream_t stream);
-/* fdgpu_submit_frags: parsed fd_txn_t records (stride FDT_TXN_MAX_SZ in
-   d_txn_out) to their reserved places in d_trailers; a footprint other than
-   the reservation -> FDGPU_CODE_TRAILER_CAP in d_codes */
-hipError_t fdgpu_launch_trailer_pack(const fdgpu_frag_ex_t *d_fx, uint32_t n, const uint8_t *d_txn_out,
-                                     const uint16_t *d_txn_sz, uint8_t *d_trailers, int8_t *d_codes, hipStream_t stream);
+/* fdgpu_submit_frags, in two launches for batches up to FDGPU_SMALL_SCAN_MAX
+   txns (parse, then scan + expand in one block; larger batches take
+   fdgpu_launch_frag_ingest's path), and the batch's end in one launch
+   (combine + parse failures + trailer pack; codes at d_codes, trailers at
+   d_trailers). */
+#define FDGPU_SMALL_SCAN_MAX 65536u
+hipError_t fdgpu_launch_frag_ring(const uint8_t *d_arena, const fdgpu_frag_ex_t *d_fx, uint32_t n, uint8_t *d_txn_out,
+                                  uint16_t *d_txn_sz, fdgpu_txn_t *d_txd, uint32_t *d_cnt, uint32_t *d_sig0,
+                                  uint32_t *d_blocktot, uint32_t *d_n_sig, fdgpu_sig_desc_t *d_sigs,
+                                  fdgpu_txn_desc_t *d_tds, hipStream_t stream);
+hipError_t fdgpu_launch_frag_finish(const fdgpu_txn_desc_t *d_tds, uint32_t n, const int8_t *d_sig_codes,
+                                    const uint16_t *d_txn_sz, const fdgpu_frag_ex_t *d_fx, const uint8_t *d_txn_out,
+                                    int8_t *d_codes, uint8_t *d_trailers, hipStream_t stream);
 hipError_t fdgpu_launch_test_hs_split(const uint32_t *d_in, uint32_t *d_out, uint32_t n, hipStream_t stream);
 
 #ifdef __cplusplus

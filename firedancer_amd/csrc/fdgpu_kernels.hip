@@ -1013,26 +1013,87 @@ __global__ void __launch_bounds__(256) fdgpu_frag_expand_kernel(
   }
 }
 
-/* Ring-slot frag batches (fdgpu_submit_frags): each parsed fd_txn_t goes to
-   the caller's trailer buffer at its reserved place, whose size the caller
-   derived from the payload's counts (fdt_txn_peek); a footprint other than
-   the reservation (only a caller bug can cause one) gets
-   FDGPU_CODE_TRAILER_CAP instead of a verify code.  Lane per frag; tr_off is
-   4-byte aligned, the txn record starts a 852-B (4-aligned) stride. */
-__global__ void __launch_bounds__(256) fdgpu_trailer_pack_kernel(const fdgpu_frag_ex_t *__restrict__ fx, uint32_t n,
-                                                                 const uint8_t *__restrict__ txn_out,
-                                                                 const uint16_t *__restrict__ txn_sz,
-                                                                 uint8_t *__restrict__ trailers,
-                                                                 int8_t *__restrict__ codes) {
+/* Ring-slot frag batches of up to FDGPU_SMALL_SCAN_MAX txns: the
+   signature-count scan and the descriptor expansion in ONE block (1024
+   threads, each a run of consecutive txns), instead of the three-kernel
+   multi-block scan: a verify tile's batch costs two launches fewer. */
+__global__ void __launch_bounds__(1024) fdgpu_frag_scan_expand_small_kernel(
+    const fdgpu_txn_t *__restrict__ txd, const uint32_t *__restrict__ cnt, uint32_t n,
+    fdgpu_sig_desc_t *__restrict__ sigs, fdgpu_txn_desc_t *__restrict__ tds, uint32_t *__restrict__ n_sig) {
+  __shared__ uint32_t s_wave[16];
+  const uint32_t per = (n + 1023u) / 1024u, t0 = threadIdx.x * per, t1 = min(n, t0 + per);
+  uint32_t sum = 0;
+  for (uint32_t t = t0; t < t1; t++) sum += cnt[t];
+  const uint32_t incl = wave_incl_scan(sum);
+  const uint32_t wv = threadIdx.x >> 6;
+  if ((threadIdx.x & 63u) == 63u) s_wave[wv] = incl;
+  __syncthreads();
+  uint32_t off = incl - sum;
+  for (uint32_t w = 0; w < wv; w++) off += s_wave[w];
+  if (threadIdx.x == 1023u) *n_sig = off + sum;
+  for (uint32_t t = t0; t < t1; t++) {
+    const uint32_t c = cnt[t];
+    fdgpu_txn_desc_t td;
+    td.sig0 = off;
+    td.sig_cnt = c;
+    tds[t] = td;
+    if (c) {
+      const fdgpu_txn_t d = txd[t];
+      for (uint32_t j = 0; j < c; j++) {
+        fdgpu_sig_desc_t sd;
+        sd.msg_off = d.msg_off;
+        sd.msg_sz = d.msg_sz;
+        sd.sig_off = d.sig_off + 64u * j;
+        sd.pub_off = d.pub_off + 32u * j;
+        sigs[off + j] = sd;
+      }
+    }
+    off += c;
+  }
+}
+
+/* The end of a ring-slot frag batch in one launch, per txn: the
+   batch_single_msg combine of its signatures' codes, FDGPU_CODE_PARSE_FAIL
+   for a payload that is not a transaction, and its parsed fd_txn_t copied
+   to the place the caller reserved (from the payload's counts,
+   fdt_txn_peek) -- a footprint other than the reservation (only a caller
+   bug can cause one) gets FDGPU_CODE_TRAILER_CAP and no verdict.  codes and
+   trailers are one buffer (trailers after the codes), copied back in one
+   transfer.  Lane per txn; tr_off is 4-byte aligned, the txn record starts
+   a 852-B (4-aligned) stride. */
+__global__ void __launch_bounds__(256) fdgpu_frag_finish_kernel(const fdgpu_txn_desc_t *__restrict__ txns, uint32_t n,
+                                                                const int8_t *__restrict__ sig_codes,
+                                                                const uint16_t *__restrict__ txn_sz,
+                                                                const fdgpu_frag_ex_t *__restrict__ fx,
+                                                                const uint8_t *__restrict__ txn_out,
+                                                                int8_t *__restrict__ codes, uint8_t *__restrict__ trailers) {
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= n) return;
   const uint32_t fp = txn_sz[t];
-  if (!fp) return;                                        /* not a transaction: PARSE_FAIL already */
-  const fdgpu_frag_ex_t f = fx[t];
-  if (fp != f.tr_cap) { codes[t] = (int8_t)FDGPU_CODE_TRAILER_CAP; return; }
-  const uint32_t *src = (const uint32_t *)(txn_out + (size_t)t * FDT_TXN_MAX_SZ);
-  uint32_t *dst = (uint32_t *)(trailers + f.tr_off);
-  for (uint32_t w = 0; w < (fp + 3u) / 4u; w++) dst[w] = src[w];
+  int code = -1;
+  if (!fp) {
+    code = FDGPU_CODE_PARSE_FAIL;
+  } else {
+    const fdgpu_frag_ex_t f = fx[t];
+    if (fp != f.tr_cap) {
+      code = FDGPU_CODE_TRAILER_CAP;
+    } else {
+      const fdgpu_txn_desc_t d = txns[t];
+      if (d.sig_cnt >= 1 && d.sig_cnt <= 16) {           /* else ERR_SIG (fd_ed25519_user.c:238-241) */
+        int first_struct = 0, any_msg = 0;
+        for (uint32_t j = 0; j < d.sig_cnt; j++) {
+          const int c = sig_codes[d.sig0 + j];
+          if (c == -3) any_msg = 1;
+          else if (c != 0 && first_struct == 0) first_struct = c;
+        }
+        code = first_struct ? first_struct : (any_msg ? -3 : 0);
+      }
+      const uint32_t *src = (const uint32_t *)(txn_out + (size_t)t * FDT_TXN_MAX_SZ);
+      uint32_t *dst = (uint32_t *)(trailers + f.tr_off);
+      for (uint32_t w = 0; w < (fp + 3u) / 4u; w++) dst[w] = src[w];
+    }
+  }
+  codes[t] = (int8_t)code;
 }
 
 /* After the combine: a payload that did not parse gets FDGPU_CODE_PARSE_FAIL */
@@ -1205,11 +1266,27 @@ hipError_t fdgpu_launch_frag_codes(const uint16_t *d_txn_sz, uint32_t n, int8_t 
   return hipGetLastError();
 }
 
-hipError_t fdgpu_launch_trailer_pack(const fdgpu_frag_ex_t *d_fx, uint32_t n, const uint8_t *d_txn_out,
-                                     const uint16_t *d_txn_sz, uint8_t *d_trailers, int8_t *d_codes, hipStream_t stream) {
+hipError_t fdgpu_launch_frag_ring(const uint8_t *d_arena, const fdgpu_frag_ex_t *d_fx, uint32_t n, uint8_t *d_txn_out,
+                                  uint16_t *d_txn_sz, fdgpu_txn_t *d_txd, uint32_t *d_cnt, uint32_t *d_sig0,
+                                  uint32_t *d_blocktot, uint32_t *d_n_sig, fdgpu_sig_desc_t *d_sigs,
+                                  fdgpu_txn_desc_t *d_tds, hipStream_t stream) {
+  if (!n) return hipMemsetAsync(d_n_sig, 0, sizeof(uint32_t), stream);
+  if (n > FDGPU_SMALL_SCAN_MAX)
+    return fdgpu_launch_frag_ingest(d_arena, d_fx, 4u, n, d_txn_out, d_txn_sz, d_txd, d_cnt, d_sig0, d_blocktot,
+                                    d_n_sig, d_sigs, d_tds, stream);
+  hipLaunchKernelGGL(fdgpu_frag_parse_kernel, dim3((n + 63) / 64), dim3(64), 0, stream, d_arena,
+                     (const uint32_t *)d_fx, 4u, n, d_txn_out, d_txn_sz, d_txd, d_cnt);
+  hipLaunchKernelGGL(fdgpu_frag_scan_expand_small_kernel, dim3(1), dim3(1024), 0, stream, d_txd, d_cnt, n, d_sigs,
+                     d_tds, d_n_sig);
+  return hipGetLastError();
+}
+
+hipError_t fdgpu_launch_frag_finish(const fdgpu_txn_desc_t *d_tds, uint32_t n, const int8_t *d_sig_codes,
+                                    const uint16_t *d_txn_sz, const fdgpu_frag_ex_t *d_fx, const uint8_t *d_txn_out,
+                                    int8_t *d_codes, uint8_t *d_trailers, hipStream_t stream) {
   if (!n) return hipSuccess;
-  hipLaunchKernelGGL(fdgpu_trailer_pack_kernel, dim3((n + 255) / 256), dim3(256), 0, stream, d_fx, n, d_txn_out,
-                     d_txn_sz, d_trailers, d_codes);
+  hipLaunchKernelGGL(fdgpu_frag_finish_kernel, dim3((n + 255) / 256), dim3(256), 0, stream, d_tds, n, d_sig_codes,
+                     d_txn_sz, d_fx, d_txn_out, d_codes, d_trailers);
   return hipGetLastError();
 }
 
