@@ -153,10 +153,24 @@ def aggregate(dist, n_sig, steps, dt):
 RING_DEPTH = 8        # ring slots (one stream + workspace each) of the latency/PCIe engine (8: tools/pcie_probe.py)
 
 
+def timed_batch(eng, a, t):
+    """submit -> codes on the host, ms: the completion is watched with
+    non-blocking polls (the completion word, as the verify tile polls), not a
+    blocking event wait whose wake-up adds its own jitter"""
+    t0 = time.perf_counter()
+    tk = eng.submit(a, t)
+    while eng.poll(tk, blocking=False) is None:
+        pass
+    return (time.perf_counter() - t0) * 1e3
+
+
 def latency_and_pcie(eng, arena, txns, batch, nbatches):
     """p50/p99 submit->codes-on-host latency of `batch`-txn batches (one in
     flight at a time), then pipelined throughput with every ring slot busy
-    (PCIe-inclusive: host staging memcpy, uploads, kernels, code read-back)."""
+    (PCIe-inclusive: host staging memcpy, uploads, kernels, code read-back).
+    The latency loops run with Python's garbage collector off, so its pauses
+    do not land in the tail."""
+    import gc
     n = len(txns)
     starts = list(range(0, n - batch + 1, batch)) or [0]
     views = []
@@ -170,13 +184,9 @@ def latency_and_pcie(eng, arena, txns, batch, nbatches):
     for i in range(100):                                   # warm-up
         a, t = views[i % len(views)]
         eng.verify_txns(a, t)
-    lat = []
-    for i in range(nbatches):
-        a, t = views[i % len(views)]
-        t0 = time.perf_counter()
-        tk = eng.submit(a, t)
-        eng.poll(tk, blocking=True)
-        lat.append((time.perf_counter() - t0) * 1e3)
+    gc.disable()
+    lat = [timed_batch(eng, *views[i % len(views)]) for i in range(nbatches)]
+    gc.enable()
     def pipelined(vs):
         """every ring slot busy: submit -> poll over the batches, sigs/s"""
         sigs = 0
@@ -204,13 +214,9 @@ def latency_and_pcie(eng, arena, txns, batch, nbatches):
     pcie_reg = pipelined(reg_views)
     # the same latency measurement from the registered arena (DMA'd in place,
     # as the verify tile's registered out dcache is)
-    lat_reg = []
-    for i in range(nbatches):
-        a, t = reg_views[i % len(reg_views)]
-        t0 = time.perf_counter()
-        tk = eng.submit(a, t)
-        eng.poll(tk, blocking=True)
-        lat_reg.append((time.perf_counter() - t0) * 1e3)
+    gc.disable()
+    lat_reg = [timed_batch(eng, *reg_views[i % len(reg_views)]) for i in range(nbatches)]
+    gc.enable()
     eng.host_unregister(arena)
     lat, lat_reg = np.array(lat), np.array(lat_reg)
     return (float(np.percentile(lat, 50)), float(np.percentile(lat, 99)), pcie, pcie_reg,

@@ -21,6 +21,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <functional>
 #include <map>
 #include <mutex>
 #include <random>
@@ -500,6 +501,57 @@ static Slot *free_slot(fdgpu_engine_t *e) {
 static constexpr unsigned FDGPU_COPY_THREADS = 4;
 static constexpr uint64_t FDGPU_COPY_SPLIT_MIN = 4ull << 20;
 
+}  // extern "C"
+
+/* The staging helpers: FDGPU_COPY_THREADS - 1 process-wide threads started
+   on first use and kept (a thread created per submit costs tens of
+   microseconds and was a visible share of a batch's latency tail). */
+namespace {
+struct CopyPool {
+  std::mutex mu;
+  std::condition_variable cv, done_cv;
+  std::vector<std::function<void()>> jobs;
+  uint64_t pending = 0;
+  std::vector<std::thread> th;
+  CopyPool() {
+    for (unsigned i = 1; i < FDGPU_COPY_THREADS; i++)
+      th.emplace_back([this]() {
+        for (;;) {
+          std::function<void()> job;
+          {
+            std::unique_lock<std::mutex> lk(mu);
+            cv.wait(lk, [this]() { return !jobs.empty(); });
+            job = std::move(jobs.back());
+            jobs.pop_back();
+          }
+          job();
+          std::lock_guard<std::mutex> lk(mu);
+          if (--pending == 0) done_cv.notify_all();
+        }
+      });
+    for (auto &t : th) t.detach();           /* live for the process */
+  }
+  /* runs fns[1..] on the pool and fns[0] here; returns when all are done */
+  void run(std::vector<std::function<void()>> &fns) {
+    {
+      std::lock_guard<std::mutex> lk(mu);
+      for (size_t i = 1; i < fns.size(); i++) { jobs.push_back(fns[i]); pending++; }
+    }
+    cv.notify_all();
+    fns[0]();
+    std::unique_lock<std::mutex> lk(mu);
+    done_cv.wait(lk, [this]() { return pending == 0; });
+  }
+};
+CopyPool &copy_pool() {
+  static CopyPool *p = new CopyPool;         /* never destroyed: its threads outlive main */
+  return *p;
+}
+std::mutex g_stage_mu;                       /* one staging at a time uses the pool */
+}  // namespace
+
+extern "C" {
+
 static uint64_t stage_arena(fdgpu_engine_t *e, Slot *s, uint8_t const *arena, uint64_t sz) {
   if (sz < FDGPU_COPY_SPLIT_MIN) {
     memcpy(s->h_arena, arena, sz);
@@ -507,19 +559,21 @@ static uint64_t stage_arena(fdgpu_engine_t *e, Slot *s, uint8_t const *arena, ui
   }
   const uint64_t part = ((sz + FDGPU_COPY_THREADS - 1) / FDGPU_COPY_THREADS + 63) & ~63ull;
   int err[FDGPU_COPY_THREADS] = {};
-  auto work = [&](unsigned i) {
-    const uint64_t off = (uint64_t)i * part;
-    if (off >= sz) return;
-    const uint64_t n = sz - off < part ? sz - off : part;
-    memcpy(s->h_arena + off, arena + off, n);
-    if (hipSetDevice(e->device) != hipSuccess ||
-        hipMemcpyAsync(s->d_arena + off, s->h_arena + off, n, hipMemcpyHostToDevice, s->stream) != hipSuccess)
-      err[i] = 1;
-  };
-  std::thread th[FDGPU_COPY_THREADS - 1];
-  for (unsigned i = 1; i < FDGPU_COPY_THREADS; i++) th[i - 1] = std::thread(work, i);
-  work(0);
-  for (auto &t : th) t.join();
+  std::vector<std::function<void()>> fns;
+  for (unsigned i = 0; i < FDGPU_COPY_THREADS; i++)
+    fns.push_back([&, i]() {
+      const uint64_t off = (uint64_t)i * part;
+      if (off >= sz) return;
+      const uint64_t n = sz - off < part ? sz - off : part;
+      memcpy(s->h_arena + off, arena + off, n);
+      if (hipSetDevice(e->device) != hipSuccess ||
+          hipMemcpyAsync(s->d_arena + off, s->h_arena + off, n, hipMemcpyHostToDevice, s->stream) != hipSuccess)
+        err[i] = 1;
+    });
+  {
+    std::lock_guard<std::mutex> lk(g_stage_mu);
+    copy_pool().run(fns);
+  }
   for (unsigned i = 0; i < FDGPU_COPY_THREADS; i++)
     if (err[i]) { set_err("staging upload failed"); return UINT64_MAX; }
   return sz;
