@@ -278,6 +278,14 @@ TILE_RUNS = (  # name, verify tiles, quic links (producers), offered txn/s (0: b
 )
 
 
+def tile_args(prods, rate):
+    """bench_tile.run_once_mux's options for one cfg5 run (tests/test_bench_cli.py
+    checks it carries every option run_once_mux and start_producer read)"""
+    import types
+    return types.SimpleNamespace(gpus=1, gpu_parse=1, producers=prods, depth_lg=21 if not rate else 19,
+                                 wait_us=200.0, pin=1, multi=0, cpu_offset=0)
+
+
 def tile_lines(device, arena, txns, modes, cpus, runs=TILE_RUNS):
     """BASELINE configs[4] (cfg5) on this rank's GPU: the verify tile in the
     reference's shape -- the fd_verify.c:232-246 callbacks (fdgpu_vmux) on
@@ -289,7 +297,6 @@ def tile_lines(device, arena, txns, modes, cpus, runs=TILE_RUNS):
     133), one engine per tile on this GPU, 16K-txn batches, 4 in flight,
     producers and tiles pinned to their own cores.  Every run checks that
     exactly the verified txns were published."""
-    import types
     sys.path.insert(0, os.path.join(REPO, "tools"))
     import bench_tile
     from firedancer_amd import workload
@@ -298,8 +305,7 @@ def tile_lines(device, arena, txns, modes, cpus, runs=TILE_RUNS):
     n_sig = int(txns["sig_cnt"].sum())
     out = {}
     for name, tiles_n, prods, rate in runs:
-        args = types.SimpleNamespace(gpus=1, gpu_parse=1, producers=prods, depth_lg=21 if not rate else 19,
-                                     wait_us=200.0, pin=1)
+        args = tile_args(prods, rate)
         res = bench_tile.run_once_mux(args, ps, parena, poffs, psizes, n_sig, modes, tiles_n, 16384, 4, rate,
                                       cpus=cpus, device=device)
         lat = res["batch_latency_ms"]

@@ -239,7 +239,7 @@ def run_once_mux(args, ps, arena, offs, sizes, n_sig, modes, tiles_n, batch, inf
         "wall_s": round(wall, 4), "producer_s": round(prod_s, 4), "producer_published": int(n_pub),
         "gpus": args.gpus, "tiles": tiles_n, "batch_txn_max": batch, "inflight": inflight,
         "rate_target": rate, "workload": "cfg3 (1-12 sigs/txn, payload <= 1232 B, 10% corrupted)"
-        if args.multi else "cfg1 (1 sig, msg U[180,220] B, 10% corrupted)",
+        if getattr(args, "multi", 0) else "cfg1 (1 sig, msg U[180,220] B, 10% corrupted)",
         "txns": len(ps), "sigs": n_sig, "batch_wait_us": args.wait_us, "cpus": cpus[:P + tiles_n],
         "batch_latency_ms": {"p50": round(float(np.percentile(lat, 50)), 3) if len(lat) else None,
                              "p99": round(float(np.percentile(lat, 99)), 3) if len(lat) else None,
