@@ -282,21 +282,23 @@ def tile_args(prods, rate):
     """bench_tile.run_once_mux's options for one cfg5 run (tests/test_bench_cli.py
     checks it carries every option run_once_mux and start_producer read)"""
     import types
-    return types.SimpleNamespace(gpus=1, gpu_parse=1, producers=prods, depth_lg=21 if not rate else 19,
+    return types.SimpleNamespace(gpus=1, gpu_parse=2, producers=prods, depth_lg=21 if not rate else 19,
                                  wait_us=200.0, pin=1, multi=0, cpu_offset=0)
 
 
 def tile_lines(device, arena, txns, modes, cpus, runs=TILE_RUNS):
     """BASELINE configs[4] (cfg5) on this rank's GPU: the verify tile in the
     reference's shape -- the fd_verify.c:232-246 callbacks (fdgpu_vmux) on
-    the mux loop (fdt_mux_run, FD_MUX_FLAG_COPY | MANUAL_PUBLISH), frags
-    copied into a registered out dcache, fd_txn_parse on the GPU
-    (fdgpu_submit_frags), tcache and publish in order -- over this rank's
-    cfg1 txns as raw frags.  T tiles read P quic->verify links round robin
-    (every verify tile reads every QUIC tile's link, fd_frankendancer.c:131-
-    133), one engine per tile on this GPU, 16K-txn batches, 4 in flight,
-    producers and tiles pinned to their own cores.  Every run checks that
-    exactly the verified txns were published."""
+    the mux loop (fdt_mux_run, FD_MUX_FLAG_COPY | MANUAL_PUBLISH), tcache and
+    publish in order -- with the byte work on the GPU (gpu_parse 2,
+    fdgpu_submit_frags_io): the device reads each payload in the registered
+    in dcache, parses, verifies, tags it and writes the out frag into the
+    registered out dcache; the tile core only moves frag metadata.  Over
+    this rank's cfg1 txns as raw frags.  T tiles read P quic->verify links
+    round robin (every verify tile reads every QUIC tile's link,
+    fd_frankendancer.c:131-133), one engine per tile on this GPU, 16K-txn
+    batches, 4 in flight, producers and tiles pinned to their own cores.
+    Every run checks that exactly the verified txns were published."""
     sys.path.insert(0, os.path.join(REPO, "tools"))
     import bench_tile
     from firedancer_amd import workload
@@ -313,8 +315,8 @@ def tile_lines(device, arena, txns, modes, cpus, runs=TILE_RUNS):
         out[f"tile_{name}_batch_latency_ms_p50_p99"] = [lat["p50"], lat["p99"]]
         out[f"tile_{name}_overruns"] = res["counters"]["overrun"]
         out[f"tile_{name}_published_ok"] = res["counters"]["published"] == res["expected_published"]
-    out["tile_config"] = ("fdgpu_vmux on fdt_mux_run (the reference's mux-callback verify tile), fd_txn_parse on "
-                          "the GPU; muxT: T verify tiles reading T quic->verify links (one producer thread each), "
+    out["tile_config"] = ("fdgpu_vmux on fdt_mux_run (the reference's mux-callback verify tile), payload gather, "
+                          "fd_txn_parse, verify, dedup tag and out-frag assembly on the GPU; muxT: T verify tiles reading T quic->verify links (one producer thread each), "
                           "one engine per tile on this GPU, cfg1 frags, 16384-txn batches, 4 in flight; backlog: "
                           "producers publish as fast as they can into 2^21-deep links; paced_R: R txn/s offered "
                           "in total into 2^19-deep links")

@@ -112,6 +112,12 @@ def lib():
     L.fdgpu_submit_frags.restype = c.c_int64
     L.fdgpu_poll_frags.argtypes = [vp, c.c_int64, vp, vp, c.c_int]
     L.fdgpu_poll_frags.restype = c.c_int
+    L.fdgpu_submit_frags_io.argtypes = [vp, vp, c.c_uint64, vp, c.c_uint64, c.c_uint64]
+    L.fdgpu_submit_frags_io.restype = c.c_int64
+    L.fdgpu_poll_frags_io.argtypes = [vp, c.c_int64, vp, vp, vp, c.c_int]
+    L.fdgpu_poll_frags_io.restype = c.c_int
+    L.fdgpu_frag_out_cap.argtypes = [c.c_uint32]
+    L.fdgpu_frag_out_cap.restype = c.c_uint32
     L.fdgpu_ed25519_verify.argtypes = [u8p, c.c_uint64, u8p, u8p]
     L.fdgpu_ed25519_verify.restype = c.c_int
     L.fdgpu_ed25519_verify_batch_single_msg.argtypes = [u8p, c.c_uint64, u8p, u8p, c.c_uint8]

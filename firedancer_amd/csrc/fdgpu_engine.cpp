@@ -33,6 +33,7 @@
 #include "fdgpu_internal.h"
 
 #define FDT_TXN_MAX_SZ_BYTES 852u   /* FD_TXN_MAX_SZ (fd_txn.h:98): one parsed fd_txn_t record */
+#define FDT_TXN_MTU_BYTES 1232u     /* FD_TXN_MTU (fd_txn.h:103) */
 
 namespace {
 
@@ -77,6 +78,13 @@ struct Slot {
   uint32_t *d_cnt = nullptr, *d_sig0 = nullptr, *d_blocktot = nullptr, *d_n_sig = nullptr;
   uint8_t *d_tr = nullptr, *h_tr = nullptr;   /* [codes, padded to 64][trailers]: one read-back */
   uint64_t tr_cap = 0, tr_sz = 0, tr_base = 0;
+  /* gathered frag batches (fdgpu_submit_frags_io): the payloads' device-side
+     addresses, and the out image the finish kernel assembles (grown on
+     demand); the read-back is [codes][tags][out sizes] in h_tr */
+  bool io = false;
+  uint64_t *h_src = nullptr, *d_src = nullptr;
+  uint8_t *d_out = nullptr;
+  uint64_t out_cap_bytes = 0;
 };
 
 }  // namespace
@@ -103,7 +111,7 @@ struct fdgpu_engine {
   /* fdgpu_host_register calls of this engine, one entry each (a range
      registered twice holds two references): the page-aligned start the
      caller named, and the pinned region [base, end) that covers it */
-  struct Reg { uintptr_t user, base, end; };
+  struct Reg { uintptr_t user, base, end, dbase; };   /* dbase: the region's device-side address */
   std::vector<Reg> regions;
   bool drop_flag = false;            /* test hook (FDGPU_DEBUG_DROP_FLAG=1): the stream never writes the
                                         completion word, so polls must finish through the event */
@@ -131,8 +139,10 @@ void slot_free(Slot &s) {
   if (s.h_flag) (void)hipHostFree(s.h_flag);
   if (s.h_fx) (void)hipHostFree(s.h_fx);
   if (s.h_tr) (void)hipHostFree(s.h_tr);
+  if (s.h_src) (void)hipHostFree(s.h_src);
   for (void *p : {(void *)s.d_fx, (void *)s.d_txn_out, (void *)s.d_txn_sz, (void *)s.d_txd, (void *)s.d_cnt,
-                  (void *)s.d_sig0, (void *)s.d_blocktot, (void *)s.d_n_sig, (void *)s.d_tr})
+                  (void *)s.d_sig0, (void *)s.d_blocktot, (void *)s.d_n_sig, (void *)s.d_tr, (void *)s.d_src,
+                  (void *)s.d_out})
     if (p) (void)hipFree(p);
   s = Slot{};
 }
@@ -314,9 +324,18 @@ void btab_release(int device, uint32_t *p) {
   if (it == g_btab.end() || it->second.first != p) return;
   if (--it->second.second == 0) { (void)hipFree(p); g_btab.erase(it); }
 }
-/* pinned host regions: page-aligned base -> (end, references over every
-   engine's registrations) */
-std::map<uintptr_t, std::pair<uintptr_t, int>> g_regions;
+/* pinned host regions: page-aligned base -> end, references over every
+   engine's registrations, and the device-side address of base (regions are
+   mapped, so kernels read them in place: fdgpu_submit_frags_io) */
+struct GReg { uintptr_t end; int refs; uintptr_t dbase; };
+std::map<uintptr_t, GReg> g_regions;
+
+/* the engine's registration covering [p, p + sz), or null */
+const fdgpu_engine::Reg *region_of(const fdgpu_engine *e, uintptr_t p, uint64_t sz) {
+  for (const auto &r : e->regions)
+    if (p >= r.base && p + sz <= r.end) return &r;
+  return nullptr;
+}
 
 bool region_covers(const fdgpu_engine *e, const uint8_t *p, uint64_t sz) {
   const uintptr_t a = (uintptr_t)p;
@@ -330,7 +349,7 @@ void region_release(int device, uintptr_t base) {
   std::lock_guard<std::mutex> rk(g_reg_mu);
   auto it = g_regions.find(base);
   if (it == g_regions.end()) return;
-  if (--it->second.second == 0) {
+  if (--it->second.refs == 0) {
     (void)hipSetDevice(device);
     (void)hipHostUnregister((void *)base);
     g_regions.erase(it);
@@ -480,6 +499,7 @@ static int64_t submit_slot(fdgpu_engine_t *e, Slot *s, uint64_t arena_sz, fdgpu_
   s->held = false;
   s->polls = 0;
   s->frag = false;
+  s->io = false;
   s->ticket = e->next_ticket++;
   s->txn_cnt = txn_cnt;
   return s->ticket;
@@ -617,7 +637,7 @@ int64_t fdgpu_stage_submit(fdgpu_engine_t *e, uint64_t arena_sz, fdgpu_txn_t con
 }
 
 static int poll_slot(fdgpu_engine_t *e, int64_t ticket, int8_t *txn_codes, int blocking, bool keep,
-                     uint8_t *trailers = nullptr) {
+                     uint8_t *trailers = nullptr, uint64_t *tags = nullptr, uint16_t *out_szs = nullptr) {
   if (!e) return FDGPU_ERR_INVAL;
   std::unique_lock<std::mutex> lk(e->ring_mu);
   Slot *s = nullptr;
@@ -646,8 +666,15 @@ static int poll_slot(fdgpu_engine_t *e, int64_t ticket, int8_t *txn_codes, int b
     if (q == hipErrorNotReady) return FDGPU_PENDING;
     HIPCHK(q, FDGPU_ERR_DEVICE);
   }
-  if (txn_codes && s->txn_cnt) memcpy(txn_codes, s->frag ? (const int8_t *)s->h_tr : s->h_codes, s->txn_cnt);
-  if (trailers && s->frag && s->tr_sz) memcpy(trailers, s->h_tr + s->tr_base, s->tr_sz);
+  if (s->io) {                                 /* [codes][tags][out sizes] */
+    const uint64_t n = s->txn_cnt, cb = (n + 63) & ~63ull;
+    if (txn_codes && n) memcpy(txn_codes, s->h_tr, n);
+    if (tags && n) memcpy(tags, s->h_tr + cb, n * 8);
+    if (out_szs && n) memcpy(out_szs, s->h_tr + cb + n * 8, n * 2);
+  } else {
+    if (txn_codes && s->txn_cnt) memcpy(txn_codes, s->frag ? (const int8_t *)s->h_tr : s->h_codes, s->txn_cnt);
+    if (trailers && s->frag && s->tr_sz) memcpy(trailers, s->h_tr + s->tr_base, s->tr_sz);
+  }
   if (keep) s->held = true;
   else s->ticket = -1;
   return FDGPU_OK;
@@ -724,11 +751,109 @@ int64_t fdgpu_submit_frags(fdgpu_engine_t *e, uint8_t const *arena, uint64_t are
   s->held = false;
   s->polls = 0;
   s->frag = true;
+  s->io = false;
   s->tr_sz = trailer_sz;
   s->tr_base = tr_base;
   s->ticket = e->next_ticket++;
   s->txn_cnt = n;
   return s->ticket;
+}
+
+uint32_t fdgpu_frag_out_cap(uint32_t sz) {
+  return (uint32_t)(((uint64_t)sz + 1u) / 2u * 2u + fdgpu_frag_fp_bound(sz) + 2u);
+}
+
+/* Gathered frag batches (the header's fdgpu_submit_frags_io): the device
+   reads each payload from its registered host region (the in dcache) into
+   the slot arena, then parse -> scan -> expand -> verify -> finish (codes,
+   tags, out frags assembled in the slot's out image) on the slot's stream,
+   and two read-backs: the out image into the registered out region, the
+   [codes][tags][out sizes] into pinned memory. */
+int64_t fdgpu_submit_frags_io(fdgpu_engine_t *e, fdgpu_frag_io_t const *fio, uint64_t n, uint8_t *out,
+                              uint64_t out_sz, uint64_t hash_seed) {
+  if (!e || (!fio && n) || (!out && out_sz)) { set_err("null argument"); return FDGPU_ERR_INVAL; }
+  if (n > e->cfg.max_txn) { set_err("batch exceeds engine limits"); return FDGPU_ERR_INVAL; }
+  std::lock_guard<std::mutex> lk(e->ring_mu);
+  const fdgpu_engine::Reg *ro = out_sz ? region_of(e, (uintptr_t)out, out_sz) : nullptr;
+  if (out_sz && !ro) { set_err("out range not inside a registered region"); return FDGPU_ERR_INVAL; }
+  HIPCHK(hipSetDevice(e->device), FDGPU_ERR_DEVICE);
+  Slot *s = free_slot(e);
+  if (!s) { set_err("all ring slots hold unpolled batches"); return FDGPU_ERR_FULL; }
+  /* results: codes (padded to 64) + 8 B tags + 2 B sizes, in the trailer buffer */
+  const uint64_t cb = (n + 63) & ~63ull, res_sz = cb + n * 10;
+  if (!slot_frag_bufs(*s, e->cfg, res_sz)) return FDGPU_ERR_DEVICE;
+  if (!s->d_src) {
+    const uint64_t m = e->cfg.max_txn + 1;
+    HIPCHK(hipHostMalloc((void **)&s->h_src, m * sizeof(uint64_t), hipHostMallocDefault), FDGPU_ERR_DEVICE);
+    HIPCHK(hipMalloc((void **)&s->d_src, m * sizeof(uint64_t)), FDGPU_ERR_DEVICE);
+  }
+  /* bounds: every payload inside a registered region (16-B aligned: the
+     gather reads 16-B units up to round16(sz), inside the payload's own
+     64-B chunks), every out frag inside out, the packed arena within
+     max_arena, the signature bound within max_sig */
+  uint64_t dev_off = 0, bound = 0;
+  const fdgpu_engine::Reg *rc = nullptr;
+  for (uint64_t t = 0; t < n; t++) {
+    const fdgpu_frag_io_t &f = fio[t];
+    const uint64_t q = ((uint64_t)f.sz + 15u) & ~15ull;
+    if (f.sz > FDT_TXN_MTU_BYTES || (f.src & 15u) || (f.out_off & 1u) || (uint64_t)f.out_off + f.out_cap > out_sz ||
+        f.out_cap > 0xFFFFu) {
+      set_err("frag %llu: size, alignment or out bounds", (unsigned long long)t);
+      return FDGPU_ERR_INVAL;
+    }
+    if (!rc || f.src < rc->base || f.src + q > rc->end) rc = region_of(e, (uintptr_t)f.src, q);
+    if (!rc) { set_err("frag %llu: payload not inside a registered region", (unsigned long long)t); return FDGPU_ERR_INVAL; }
+    s->h_src[t] = rc->dbase + (f.src - rc->base);
+    s->h_fx[t] = fdgpu_frag_ex_t{(uint32_t)dev_off, f.sz, f.out_off, f.out_cap};
+    dev_off += q;
+    if (dev_off > e->cfg.max_arena) { set_err("frags exceed the engine's arena"); return FDGPU_ERR_INVAL; }
+    bound += fdgpu_frag_sig_bound(f.sz);
+  }
+  if (bound > e->cfg.max_sig) { set_err("batch may exceed max_sig (%llu)", (unsigned long long)e->cfg.max_sig); return FDGPU_ERR_INVAL; }
+  if (!slot_ws(*s, bound)) return FDGPU_ERR_DEVICE;
+  if (out_sz > s->out_cap_bytes) {
+    HIPCHK(hipStreamSynchronize(s->stream), FDGPU_ERR_DEVICE);
+    if (s->d_out) { (void)hipFree(s->d_out); s->d_out = nullptr; }
+    s->out_cap_bytes = 0;
+    const uint64_t want = std::max<uint64_t>(out_sz + out_sz / 4, 1u << 20);
+    HIPCHK(hipMalloc((void **)&s->d_out, want), FDGPU_ERR_DEVICE);
+    s->out_cap_bytes = want;
+  }
+  if (n) {
+    HIPCHK(hipMemcpyAsync(s->d_fx, s->h_fx, n * sizeof(fdgpu_frag_ex_t), hipMemcpyHostToDevice, s->stream), FDGPU_ERR_DEVICE);
+    HIPCHK(hipMemcpyAsync(s->d_src, s->h_src, n * sizeof(uint64_t), hipMemcpyHostToDevice, s->stream), FDGPU_ERR_DEVICE);
+    HIPCHK(fdgpu_launch_frag_gather(s->d_src, s->d_fx, (uint32_t)n, s->d_arena, s->stream), FDGPU_ERR_DEVICE);
+    HIPCHK(fdgpu_launch_frag_ring(s->d_arena, s->d_fx, (uint32_t)n, s->d_txn_out, s->d_txn_sz, s->d_txd, s->d_cnt,
+                                  s->d_sig0, s->d_blocktot, s->d_n_sig, s->d_sigs, s->d_txns, s->stream),
+           FDGPU_ERR_DEVICE);
+    HIPCHK(fdgpu_launch_verify_sigs(s->d_arena, s->d_sigs, (uint32_t)bound, nullptr, e->d_btab, s->d_ws, s->d_sig_codes,
+                                    kflags(e), s->stream, s->d_n_sig, e->resident_blocks, e->kc_seed),
+           FDGPU_ERR_DEVICE);
+    HIPCHK(fdgpu_launch_frag_finish_io(s->d_txns, (uint32_t)n, s->d_sig_codes, s->d_txn_sz, s->d_fx, s->d_txn_out,
+                                       s->d_arena, hash_seed, s->d_out, (int8_t *)s->d_tr, (uint64_t *)(s->d_tr + cb),
+                                       (uint16_t *)(s->d_tr + cb + n * 8), s->stream),
+           FDGPU_ERR_DEVICE);
+    if (out_sz) HIPCHK(hipMemcpyAsync(out, s->d_out, out_sz, hipMemcpyDeviceToHost, s->stream), FDGPU_ERR_DEVICE);
+    HIPCHK(hipMemcpyAsync(s->h_tr, s->d_tr, res_sz, hipMemcpyDeviceToHost, s->stream), FDGPU_ERR_DEVICE);
+  }
+  ++s->flag_seq;
+  if (e->flag_poll && !e->drop_flag) HIPCHK(hipStreamWriteValue32(s->stream, s->d_flag, s->flag_seq, 0), FDGPU_ERR_DEVICE);
+  HIPCHK(hipEventRecord(s->done, s->stream), FDGPU_ERR_DEVICE);
+  s->staged = false;
+  s->held = false;
+  s->polls = 0;
+  s->frag = true;
+  s->io = true;
+  s->tr_sz = 0;
+  s->tr_base = 0;
+  s->ticket = e->next_ticket++;
+  s->txn_cnt = n;
+  return s->ticket;
+}
+
+int fdgpu_poll_frags_io(fdgpu_engine_t *e, int64_t ticket, int8_t *codes, uint64_t *tags, uint16_t *out_szs,
+                        int blocking) {
+  return poll_slot(e, ticket, codes, blocking, false, nullptr, tags, out_szs);
 }
 
 int fdgpu_stage_cancel(fdgpu_engine_t *e) {
@@ -755,20 +880,31 @@ int fdgpu_host_register(fdgpu_engine_t *e, void *p, uint64_t sz) {
   /* a range inside a region already pinned (by any engine) shares it;
      a range that only partly overlaps one cannot be pinned */
   auto it = g_regions.upper_bound(a);
-  uintptr_t base = 0, end = 0;
+  uintptr_t base = 0, end = 0, dbase = 0;
   if (it != g_regions.begin()) {
     auto pv = std::prev(it);
-    if (pv->first <= a && pv->second.first >= b) { base = pv->first; end = pv->second.first; pv->second.second++; }
-    else if (pv->second.first > a) { set_err("range partly overlaps a registered region"); return FDGPU_ERR_INVAL; }
+    if (pv->first <= a && pv->second.end >= b) {
+      base = pv->first; end = pv->second.end; dbase = pv->second.dbase; pv->second.refs++;
+    } else if (pv->second.end > a) {
+      set_err("range partly overlaps a registered region");
+      return FDGPU_ERR_INVAL;
+    }
   }
   if (!base) {
     if (it != g_regions.end() && it->first < b) { set_err("range partly overlaps a registered region"); return FDGPU_ERR_INVAL; }
     HIPCHK(hipSetDevice(e->device), FDGPU_ERR_DEVICE);
-    HIPCHK(hipHostRegister((void *)a, b - a, hipHostRegisterPortable), FDGPU_ERR_DEVICE);
-    g_regions[a] = {b, 1};
-    base = a; end = b;
+    HIPCHK(hipHostRegister((void *)a, b - a, hipHostRegisterPortable | hipHostRegisterMapped), FDGPU_ERR_DEVICE);
+    void *dp = nullptr;
+    if (hipHostGetDevicePointer(&dp, (void *)a, 0) != hipSuccess || !dp) {
+      (void)hipGetLastError();
+      (void)hipHostUnregister((void *)a);
+      set_err("registered region has no device address");
+      return FDGPU_ERR_DEVICE;
+    }
+    g_regions[a] = {b, 1, (uintptr_t)dp};
+    base = a; end = b; dbase = (uintptr_t)dp;
   }
-  e->regions.push_back({a, base, end});
+  e->regions.push_back({a, base, end, dbase});
   return FDGPU_OK;
 }
 

@@ -118,6 +118,18 @@ hipError_t fdgpu_launch_frag_ring(const uint8_t *d_arena, const fdgpu_frag_ex_t 
 hipError_t fdgpu_launch_frag_finish(const fdgpu_txn_desc_t *d_tds, uint32_t n, const int8_t *d_sig_codes,
                                     const uint16_t *d_txn_sz, const fdgpu_frag_ex_t *d_fx, const uint8_t *d_txn_out,
                                     int8_t *d_codes, uint8_t *d_trailers, hipStream_t stream);
+/* fdgpu_submit_frags_io: one wave per frag copies its payload (16-B units)
+   from host memory (d_src[i], the registered region's device-side address)
+   to d_arena + d_fx[i].off; the finish kernel writes per frag the code, the
+   dedup tag and the out frag's size, and assembles the out frag at
+   d_out + d_fx[i].tr_off ([payload][pad][fd_txn_t][u16 sz]) */
+uint64_t   fdgpu_frag_fp_bound(uint32_t sz);
+hipError_t fdgpu_launch_frag_gather(const uint64_t *d_src, const fdgpu_frag_ex_t *d_fx, uint32_t n, uint8_t *d_arena,
+                                    hipStream_t stream);
+hipError_t fdgpu_launch_frag_finish_io(const fdgpu_txn_desc_t *d_tds, uint32_t n, const int8_t *d_sig_codes,
+                                       const uint16_t *d_txn_sz, const fdgpu_frag_ex_t *d_fx, const uint8_t *d_txn_out,
+                                       const uint8_t *d_arena, uint64_t hash_seed, uint8_t *d_out, int8_t *d_codes,
+                                       uint64_t *d_tags, uint16_t *d_out_szs, hipStream_t stream);
 hipError_t fdgpu_launch_test_hs_split(const uint32_t *d_in, uint32_t *d_out, uint32_t n, hipStream_t stream);
 
 #ifdef __cplusplus

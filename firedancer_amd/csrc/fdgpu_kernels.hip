@@ -30,6 +30,7 @@
 #include "fdgpu_sha512.h"
 #include "fdgpu_lattice.h"
 #include "fdgpu_stamps.h"
+#include "fdt_hash.h"
 #include "fdt_parse.h"
 
 using namespace fdgpu;
@@ -1096,6 +1097,86 @@ __global__ void __launch_bounds__(256) fdgpu_frag_finish_kernel(const fdgpu_txn_
   codes[t] = (int8_t)code;
 }
 
+/* Gathered frag batches (fdgpu_submit_frags_io).  Gather: one wave per frag
+   copies the payload's 16-B units from host memory (the registered in
+   dcache, read in place over PCIe) to its packed, 16-B aligned place in the
+   batch arena; the units past sz lie in the payload's own 64-B chunks. */
+__global__ void __launch_bounds__(256) fdgpu_frag_gather_kernel(const uint64_t *__restrict__ src,
+                                                                const fdgpu_frag_ex_t *__restrict__ fx, uint32_t n,
+                                                                uint8_t *__restrict__ arena) {
+  const uint32_t f = blockIdx.x * 4u + (threadIdx.x >> 6), lane = threadIdx.x & 63u;
+  if (f >= n) return;
+  const uint4 *s = (const uint4 *)src[f];
+  const fdgpu_frag_ex_t x = fx[f];
+  uint4 *d = (uint4 *)(arena + x.off);
+  const uint32_t nq = (x.sz + 15u) >> 4;
+  for (uint32_t q = lane; q < nq; q += 64u) d[q] = s[q];
+}
+
+/* Finish: one wave per frag.  Lane 0 writes the frag's code (the
+   batch_single_msg combine of its signatures; FDGPU_CODE_PARSE_FAIL;
+   FDGPU_CODE_TRAILER_CAP when the out frag would not fit the caller's
+   reservation), its dedup tag (fd_hash of the first signature,
+   fd_verify.h:66) and its out size; the wave writes the out frag as
+   fd_verify.c:93-136 lays it out in the out dcache -- [payload][pad to 2]
+   [fd_txn_t][u16 payload_sz] -- one 16-bit word per lane (the fd_txn_t
+   starts 2-aligned). */
+__global__ void __launch_bounds__(256) fdgpu_frag_finish_io_kernel(
+    const fdgpu_txn_desc_t *__restrict__ txns, uint32_t n, const int8_t *__restrict__ sig_codes,
+    const uint16_t *__restrict__ txn_sz, const fdgpu_frag_ex_t *__restrict__ fx, const uint8_t *__restrict__ txn_out,
+    const uint8_t *__restrict__ arena, uint64_t seed, uint8_t *__restrict__ out, int8_t *__restrict__ codes,
+    uint64_t *__restrict__ tags, uint16_t *__restrict__ out_szs) {
+  const uint32_t f = blockIdx.x * 4u + (threadIdx.x >> 6), lane = threadIdx.x & 63u;
+  if (f >= n) return;
+  const uint32_t fp = txn_sz[f];
+  const fdgpu_frag_ex_t x = fx[f];                    /* off: arena, sz, tr_off: out offset, tr_cap: its room */
+  const uint32_t toff = (x.sz + 1u) & ~1u, osz = toff + fp + 2u;
+  const bool fits = fp && osz <= x.tr_cap;
+  const fdt_txn_t *t = (const fdt_txn_t *)(txn_out + (size_t)f * FDT_TXN_MAX_SZ);
+  const uint8_t *pl = arena + x.off;
+  if (lane == 0) {
+    int code = FDGPU_CODE_PARSE_FAIL;
+    uint64_t tag = 0;
+    if (fp) {
+      tag = fdt_hash_core(seed, pl + t->signature_off, 64);
+      if (!fits) {
+        code = FDGPU_CODE_TRAILER_CAP;
+      } else {
+        code = -1;
+        const fdgpu_txn_desc_t d = txns[f];
+        if (d.sig_cnt >= 1 && d.sig_cnt <= 16) {           /* else ERR_SIG (fd_ed25519_user.c:238-241) */
+          int first_struct = 0, any_msg = 0;
+          for (uint32_t j = 0; j < d.sig_cnt; j++) {
+            const int c = sig_codes[d.sig0 + j];
+            if (c == -3) any_msg = 1;
+            else if (c != 0 && first_struct == 0) first_struct = c;
+          }
+          code = first_struct ? first_struct : (any_msg ? -3 : 0);
+        }
+      }
+    }
+    codes[f] = (int8_t)code;
+    tags[f] = tag;
+    out_szs[f] = (uint16_t)(fits ? osz : 0u);
+  }
+  if (!fits) return;
+  const uint16_t *tr = (const uint16_t *)t;
+  uint16_t *o = (uint16_t *)(out + x.tr_off);
+  for (uint32_t h = lane; h < osz / 2u; h += 64u) {
+    const uint32_t b = 2u * h;
+    uint16_t v;
+    if (b < toff) {
+      v = *(const uint16_t *)(pl + b);              /* arena offsets are 16-B aligned */
+      if (b + 1u >= x.sz) v &= 0x00ffu;               /* the pad byte */
+    } else if (b < toff + fp) {
+      v = tr[(b - toff) / 2u];
+    } else {
+      v = (uint16_t)x.sz;
+    }
+    o[h] = v;
+  }
+}
+
 /* After the combine: a payload that did not parse gets FDGPU_CODE_PARSE_FAIL */
 __global__ void __launch_bounds__(256) fdgpu_frag_codes_kernel(const uint16_t *__restrict__ txn_sz, uint32_t n,
                                                                int8_t *__restrict__ codes) {
@@ -1287,6 +1368,25 @@ hipError_t fdgpu_launch_frag_finish(const fdgpu_txn_desc_t *d_tds, uint32_t n, c
   if (!n) return hipSuccess;
   hipLaunchKernelGGL(fdgpu_frag_finish_kernel, dim3((n + 255) / 256), dim3(256), 0, stream, d_tds, n, d_sig_codes,
                      d_txn_sz, d_fx, d_txn_out, d_codes, d_trailers);
+  return hipGetLastError();
+}
+
+uint64_t fdgpu_frag_fp_bound(uint32_t sz) { return fdt_frag_fp_bound(sz); }
+
+hipError_t fdgpu_launch_frag_gather(const uint64_t *d_src, const fdgpu_frag_ex_t *d_fx, uint32_t n, uint8_t *d_arena,
+                                    hipStream_t stream) {
+  if (!n) return hipSuccess;
+  hipLaunchKernelGGL(fdgpu_frag_gather_kernel, dim3((n + 3) / 4), dim3(256), 0, stream, d_src, d_fx, n, d_arena);
+  return hipGetLastError();
+}
+
+hipError_t fdgpu_launch_frag_finish_io(const fdgpu_txn_desc_t *d_tds, uint32_t n, const int8_t *d_sig_codes,
+                                       const uint16_t *d_txn_sz, const fdgpu_frag_ex_t *d_fx, const uint8_t *d_txn_out,
+                                       const uint8_t *d_arena, uint64_t hash_seed, uint8_t *d_out, int8_t *d_codes,
+                                       uint64_t *d_tags, uint16_t *d_out_szs, hipStream_t stream) {
+  if (!n) return hipSuccess;
+  hipLaunchKernelGGL(fdgpu_frag_finish_io_kernel, dim3((n + 3) / 4), dim3(256), 0, stream, d_tds, n, d_sig_codes,
+                     d_txn_sz, d_fx, d_txn_out, d_arena, hash_seed, d_out, d_codes, d_tags, d_out_szs);
   return hipGetLastError();
 }
 

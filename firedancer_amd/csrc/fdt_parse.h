@@ -58,6 +58,22 @@ FDT_HD uint64_t fdt_parse_footprint(uint64_t instr_cnt, uint64_t lut_cnt) {
   return sizeof(fdt_txn_t) + instr_cnt * sizeof(fdt_txn_instr_t) + lut_cnt * sizeof(fdt_txn_acct_addr_lut_t);
 }
 
+/* An upper bound on the footprint of any transaction parsed from sz bytes,
+   from the size alone: past the 134 bytes every transaction holds (count,
+   one signature, header, one account, blockhash, instruction count) each
+   instruction takes at least 3 bytes and each lookup table 34, and the
+   parser caps both counts and the footprint (FDT_TXN_MAX_SZ).  The verify
+   tile reserves align2(sz) + this + 2 out-dcache bytes for a frag it never
+   reads (fdgpu_submit_frags_io: the GPU writes the trailer). */
+FDT_HD uint64_t fdt_frag_fp_bound(uint64_t sz) {
+  const uint64_t room = sz > 134u ? sz - 134u : 0u;
+  const uint64_t ni = room / 3u < FDT_TXN_INSTR_MAX ? room / 3u : FDT_TXN_INSTR_MAX;
+  const uint64_t nl0 = (room - 3u * ni) / 34u;
+  const uint64_t nl = nl0 < FDT_TXN_ADDR_TABLE_LOOKUP_MAX ? nl0 : FDT_TXN_ADDR_TABLE_LOOKUP_MAX;
+  const uint64_t fp = fdt_parse_footprint(ni, nl);
+  return fp < FDT_TXN_MAX_SZ ? fp : FDT_TXN_MAX_SZ;
+}
+
 /* Bounds-checked reader over an untrusted payload (fd_txn_parse.c:12-75).
    at(k) reads payload byte k (k < sz, checked by the callers).  On the host
    it is a plain load.  On the GPU each lane parses its own payload, so

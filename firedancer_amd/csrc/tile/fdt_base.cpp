@@ -6,6 +6,7 @@
 #include <cstring>
 
 #include "../../../include/fd_verify_tile.h"
+#include "../fdt_hash.h"
 #include "../fdt_parse.h"
 
 namespace {
@@ -226,38 +227,25 @@ int fdt_tagring_insert(fdt_tagring_t *r, uint64_t tag) {
 
 /* -------------------------------------------------------------- hash */
 
-/* xxhash-r39 over 64-bit lanes (fd_hash.c:12-73). */
-namespace {
-constexpr uint64_t P1 = 11400714785074694791ULL, P2 = 14029467366897019727ULL, P3 = 1609587929392839161ULL,
-                   P4 = 9650029242287828579ULL, P5 = 2870177450012600261ULL;
-inline uint64_t rotl(uint64_t x, int r) { return (x << r) | (x >> (64 - r)); }
-inline uint64_t rd64(const uint8_t *p) { uint64_t v; std::memcpy(&v, p, 8); return v; }
-inline uint32_t rd32(const uint8_t *p) { uint32_t v; std::memcpy(&v, p, 4); return v; }
-inline uint64_t lane_round(uint64_t acc, uint64_t in) { return rotl(acc + in * P2, 31) * P1; }
-inline uint64_t merge(uint64_t h, uint64_t acc) { return (h ^ lane_round(0, acc)) * P1 + P4; }
-}  // namespace
-
+/* xxhash-r39 over 64-bit lanes (fd_hash.c:12-73): ../fdt_hash.h, shared
+   with the GPU's frag finish kernel. */
 uint64_t fdt_hash(uint64_t seed, const void *buf, uint64_t sz) {
-  const uint8_t *p = (const uint8_t *)buf, *end = p + sz;
-  uint64_t h;
-  if (sz >= 32) {
-    uint64_t a = seed + P1 + P2, b = seed + P2, c = seed, d = seed - P1;
-    do {
-      a = lane_round(a, rd64(p)); b = lane_round(b, rd64(p + 8));
-      c = lane_round(c, rd64(p + 16)); d = lane_round(d, rd64(p + 24));
-      p += 32;
-    } while (p + 32 <= end);
-    h = rotl(a, 1) + rotl(b, 7) + rotl(c, 12) + rotl(d, 18);
-    h = merge(h, a); h = merge(h, b); h = merge(h, c); h = merge(h, d);
-  } else {
-    h = seed + P5;
+  const uint8_t *p = (const uint8_t *)buf;
+  if (sz == 64) {                               /* the dedup tag: 8-byte loads, the compiler's own */
+    uint64_t w[8];
+    std::memcpy(w, p, 64);
+    uint64_t a = seed + FDT_HASH_P1 + FDT_HASH_P2, b = seed + FDT_HASH_P2, c = seed, d = seed - FDT_HASH_P1;
+    for (int i = 0; i < 8; i += 4) {
+      a = fdt_hash_round(a, w[i]); b = fdt_hash_round(b, w[i + 1]);
+      c = fdt_hash_round(c, w[i + 2]); d = fdt_hash_round(d, w[i + 3]);
+    }
+    uint64_t h = fdt_hash_rotl(a, 1) + fdt_hash_rotl(b, 7) + fdt_hash_rotl(c, 12) + fdt_hash_rotl(d, 18);
+    h = fdt_hash_merge(h, a); h = fdt_hash_merge(h, b); h = fdt_hash_merge(h, c); h = fdt_hash_merge(h, d);
+    h += 64;
+    h ^= h >> 33; h *= FDT_HASH_P2; h ^= h >> 29; h *= FDT_HASH_P3; h ^= h >> 32;
+    return h;
   }
-  h += sz;
-  for (; p + 8 <= end; p += 8) h = rotl(h ^ lane_round(0, rd64(p)), 27) * P1 + P4;
-  if (p + 4 <= end) { h = rotl(h ^ ((uint64_t)rd32(p) * P1), 23) * P2 + P3; p += 4; }
-  for (; p < end; p++) h = rotl(h ^ ((uint64_t)*p * P5), 11) * P1;
-  h ^= h >> 33; h *= P2; h ^= h >> 29; h *= P3; h ^= h >> 32;
-  return h;
+  return fdt_hash_core(seed, p, sz);
 }
 
 /* --------------------------------------------------------------- txn */

@@ -167,7 +167,8 @@ struct VItem {
   uint32_t sig_off;     /* signature 0, from the frag start */
   uint32_t tsorig;
   uint32_t tr_off;      /* gpu_parse: the parsed fd_txn_t's place in the batch's trailer buffer */
-  uint32_t tr_cap;      /*            and its footprint (fdt_txn_peek) */
+  uint32_t tr_cap;      /*            and its footprint (fdt_txn_peek); gather: the out bytes reserved */
+  uint32_t in_idx;      /* gather: the in link it came from */
 };
 
 struct VBatch {
@@ -176,6 +177,11 @@ struct VBatch {
   std::vector<fdgpu_txn_t> txns;
   std::vector<fdgpu_frag_ex_t> frags;  /* gpu_parse: the verifier's view of the items */
   std::vector<uint8_t> trailers;      /* gpu_parse: parsed fd_txn_t records, filled by poll_frags */
+  std::vector<fdgpu_frag_io_t> fio;   /* gather: the verifier's view of the items ... */
+  std::vector<uint64_t> tags;         /* ... and its results: dedup tags, */
+  std::vector<uint16_t> out_szs;      /*     out frag sizes */
+  uint64_t link_first[FDT_MUX_IN_MAX];   /* gather: the oldest seq taken from each in link (lapped-check) */
+  uint32_t link_mask = 0;
   uint64_t tr_used = 0;
   std::vector<VItem> items;
   std::vector<int8_t> codes;
@@ -188,7 +194,8 @@ struct VBatch {
 
   void reset() {
     first_chunk = end_off = sig_cnt = tr_used = 0;
-    txns.clear(); items.clear(); frags.clear();
+    txns.clear(); items.clear(); frags.clear(); fio.clear();
+    link_mask = 0;
     ticket = -1; closed = done = false; next = 0; t_first = 0;
   }
 };
@@ -204,8 +211,25 @@ struct fdgpu_vmux {
   void *tcache = nullptr;                 /* fd_tcache (depth > FDT_TAGRING_MAX) ... */
   fdt_tagring_t ring{};                   /* ... or the ring scan (the tile's 16-deep default) */
   bool use_ring = false;
-  bool tc_query(uint64_t tag) const { return use_ring ? fdt_tagring_query(&ring, tag) : fdt_tcache_query(tcache, tag); }
-  void tc_insert(uint64_t tag) { if (use_ring) (void)fdt_tagring_insert(&ring, tag); else (void)fdt_tcache_insert(tcache, tag); }
+  /* the ring scan inline, over a fixed 16 or 32 slots (the unused ones hold
+     the null tag, which no query reaches): one pass of vector compares */
+  template <int N> static bool ring_hit(const uint64_t *t, uint64_t tag) {
+    uint64_t h = 0;
+    for (int i = 0; i < N; i++) h |= (uint64_t)(t[i] == tag);
+    return h != 0;
+  }
+  bool tc_query(uint64_t tag) const {
+    if (!use_ring) return fdt_tcache_query(tcache, tag);
+    if (tag == FDT_TCACHE_TAG_NULL) return true;
+    return ring.depth <= 16 ? ring_hit<16>(ring.tag, tag) : ring_hit<FDT_TAGRING_MAX>(ring.tag, tag);
+  }
+  /* insert a tag the query just missed (fdt_tagring_insert without its re-query) */
+  void tc_insert(uint64_t tag) {
+    if (!use_ring) { (void)fdt_tcache_insert(tcache, tag); return; }
+    ring.tag[ring.oldest] = tag;
+    ring.oldest = ring.oldest + 1 >= ring.depth ? 0 : ring.oldest + 1;
+  }
+  std::vector<uint16_t> cap_of;          /* gather: out-frag room by payload size (fdt_frag_fp_bound) */
   uint64_t out_chunk = 0;                 /* write cursor */
   uint64_t cur_sz = 0;                    /* the frag between during_frag and after_frag */
   bool cur_ok = false;
@@ -225,6 +249,8 @@ struct fdgpu_vmux {
   std::vector<int8_t> log_code;
 
   bool gpu_parse = false;                /* fd_txn_parse on the GPU (verifier submit_frags / poll_frags) */
+  bool gather = false;                   /* ... and the payload copy too (submit_io / poll_io) */
+  uint64_t cur_src = 0, cur_in = 0;       /* gather: the frag between during_frag and after_frag */
   uint64_t final_n = 0;                   /* frags whose outcome is final ... */
   std::atomic<uint64_t> final_cnt{0};    /* ... published for other threads (one writer: a store, no RMW) */
 
@@ -266,23 +292,31 @@ struct fdgpu_vmux {
       VBatch *b = inflight.front();
       if (!b->done) {
         const uint64_t p0 = now_ns();
-        const int rc = gpu_parse ? ver.poll_frags(ver.ctx, b->ticket, b->codes.data(), b->trailers.data(), 0)
-                                 : ver.poll(ver.ctx, b->ticket, b->codes.data(), 0);
+        const int rc = gather ? ver.poll_io(ver.ctx, b->ticket, b->codes.data(), b->tags.data(), b->out_szs.data(), 0)
+                       : gpu_parse ? ver.poll_frags(ver.ctx, b->ticket, b->codes.data(), b->trailers.data(), 0)
+                                   : ver.poll(ver.ctx, b->ticket, b->codes.data(), 0);
         st.poll_ns += now_ns() - p0;
         if (rc == FDGPU_PENDING) return;
         if (rc != FDGPU_OK) { error = rc; *poll_in = 0; return; }
         b->done = true;
+        if (gather) lapped_check(*b);
       }
       const uint32_t tspub = (uint32_t)now_ns();
       const size_t n = b->items.size();
       while (b->next < n) {
         const size_t k = b->next;
-        if (gpu_parse && k + 8 < n) {            /* the trailer store of a frag soon published: own the line */
+        if (gpu_parse && !gather && k + 8 < n) { /* the trailer store of a frag soon published: own the line */
           const VItem &f = b->items[k + 8];
           __builtin_prefetch(out_laddr(f.chunk) + align2(f.sz), 1);
         }
         const VItem &it = b->items[k];
         const int code = b->codes[k];
+        if (gather && code == FDGPU_CODE_LAPPED) {   /* the producer overwrote it before the GPU read it */
+          st.overrun++;
+          log(it.seq, FDGPU_VTILE_LOG_LOST);
+          b->next++;
+          continue;
+        }
         if (gpu_parse && (code == FDGPU_CODE_PARSE_FAIL || code == FDGPU_CODE_TRAILER_CAP)) {
           /* not a transaction: filtered before the dedup check (fd_verify.c:
              117-121); a footprint other than the one reserved: a peek / parse
@@ -293,7 +327,7 @@ struct fdgpu_vmux {
           continue;
         }
         uint8_t *frag = out_laddr(it.chunk);
-        const uint64_t tag = it.tag;
+        const uint64_t tag = gather ? b->tags[k] : it.tag;
         int outcome;
         if (tc_query(tag)) outcome = FD_TXN_VERIFY_DEDUP;
         else if (code != FD_ED25519_SUCCESS) outcome = FD_TXN_VERIFY_FAILED;
@@ -306,7 +340,9 @@ struct fdgpu_vmux {
           }
           tc_insert(tag);                          /* not present: the query above missed */
           uint64_t sz = it.sz;
-          if (gpu_parse) {                        /* [payload][pad][fd_txn_t][u16 payload_sz] (fd_verify.c:93-136) */
+          if (gather) {
+            sz = b->out_szs[k];                   /* the GPU wrote the out frag where it was reserved */
+          } else if (gpu_parse) {                 /* [payload][pad][fd_txn_t][u16 payload_sz] (fd_verify.c:93-136) */
             const uint64_t toff = align2(it.sz);
             if (toff != it.sz) frag[it.sz] = 0;
             std::memcpy(frag + toff, b->trailers.data() + it.tr_off, it.tr_cap);
@@ -333,6 +369,28 @@ struct fdgpu_vmux {
     }
   }
 
+  /* gather: the GPU read each payload from the in dcache after submit; a
+     frag whose in-mcache line the producer has lapped since may have been
+     read torn, and is dropped (the mux's seq re-check after its copy,
+     fd_mux.c:641-655, moved to after the device's read).  The oldest frag
+     of each link is lapped first, so one line per link is checked unless it
+     was. */
+  void lapped_check(VBatch &b) {
+    uint32_t lapped = 0;
+    for (uint32_t i = 0; i < cfg.in_cnt; i++) {
+      if (!(b.link_mask >> i & 1u)) continue;
+      const fdt_frag_meta_t *line = cfg.in_mcache[i] + (b.link_first[i] & (cfg.in_depth[i] - 1));
+      if (ld_acq(&line->seq) != b.link_first[i]) lapped |= 1u << i;
+    }
+    if (!lapped) return;
+    for (size_t k = 0; k < b.items.size(); k++) {
+      const VItem &it = b.items[k];
+      if (!(lapped >> it.in_idx & 1u)) continue;
+      const fdt_frag_meta_t *line = cfg.in_mcache[it.in_idx] + (it.seq & (cfg.in_depth[it.in_idx] - 1));
+      if (ld_acq(&line->seq) != it.seq) b.codes[k] = (int8_t)FDGPU_CODE_LAPPED;
+    }
+  }
+
   /* the verifier refused the batch as malformed: its txns fail (logged),
      nothing is published, the tile goes on (device errors stay fatal) */
   void reject_open() {
@@ -349,7 +407,11 @@ struct fdgpu_vmux {
     int64_t t;
     const uint64_t s0 = now_ns();
     struct Acc { uint64_t &ns; uint64_t t0; ~Acc() { ns += now_ns() - t0; } } acc{st.submit_ns, s0};
-    if (gpu_parse) {
+    if (gather) {
+      const size_t n = open->fio.size();
+      if (open->tags.size() < n) { open->tags.resize(cfg.batch_txn_max); open->out_szs.resize(cfg.batch_txn_max); }
+      t = ver.submit_io(ver.ctx, open->fio.data(), n, out_laddr(open->first_chunk), open->end_off, cfg.hashmap_seed);
+    } else if (gpu_parse) {
       if (open->trailers.size() < open->tr_used) open->trailers.resize(open->tr_used);
       t = ver.submit_frags(ver.ctx, out_laddr(open->first_chunk), open->end_off, open->frags.data(),
                            open->frags.size(), open->tr_used);
@@ -403,6 +465,13 @@ void vm_during_frag(void *ctx, uint64_t in_idx, uint64_t seq, uint64_t sig, uint
     return;
   }
   const uint8_t *src = c.in_base[in_idx] + (chunk << FDT_CHUNK_LG_SZ);
+  if (t->gather) {                    /* the GPU reads it there (after_credit re-checks the line after the poll) */
+    t->cur_src = (uint64_t)(uintptr_t)src;
+    t->cur_in = in_idx;
+    t->cur_sz = sz;
+    t->cur_ok = true;
+    return;
+  }
   std::memcpy(t->out_laddr(t->out_chunk), src, sz);
   if (t->gpu_parse) {
     /* read the counts and hash signature 0 from the source just copied (in
@@ -423,6 +492,25 @@ void vm_after_frag(void *ctx, uint64_t in_idx, uint64_t seq, uint64_t *opt_sig, 
   const uint64_t payload_sz = *opt_sz;
   uint8_t *txn = t->out_laddr(t->out_chunk);
   const uint64_t toff = align2(payload_sz);
+  if (t->gather) {
+    /* reserve the out frag's room from the size alone (the tile never reads
+       the payload); the GPU writes [payload][pad][fd_txn_t][u16] there */
+    VBatch &b = *t->open;
+    if (b.items.empty()) { b.first_chunk = t->out_chunk; b.t_first = now_ns(); }
+    const uint64_t off = (t->out_chunk - b.first_chunk) << FDT_CHUNK_LG_SZ;
+    const uint32_t cap = t->cap_of[payload_sz];                  /* payload_sz <= FDT_TPU_MTU: during_frag */
+    const uint32_t li = (uint32_t)t->cur_in;
+    if (!(b.link_mask >> li & 1u)) { b.link_mask |= 1u << li; b.link_first[li] = seq; }
+    b.fio.push_back(fdgpu_frag_io_t{t->cur_src, (uint32_t)payload_sz, (uint32_t)off, cap, 0u});
+    b.items.push_back(VItem{seq, 0, (uint32_t)t->out_chunk, (uint32_t)payload_sz, 0u, (uint32_t)*opt_tsorig, 0u, cap, li});
+    b.end_off = off + cap;
+    b.sig_cnt += fdt_frag_sig_bound(payload_sz);       /* (stats.sigs stays 0: the tile never sees the count) */
+    t->out_chunk = fdt_dcache_compact_next(t->out_chunk, cap, t->cfg.out_chunk0, t->cfg.out_wmark);
+    if (t->out_chunk <= b.first_chunk || b.items.size() >= t->cfg.batch_txn_max ||
+        b.sig_cnt + 16 > t->cfg.batch_sig_max || b.end_off + FRAG_CHUNKS * FDT_CHUNK_SZ > t->cfg.batch_bytes_max)
+      b.closed = true;
+    return;
+  }
   if (t->gpu_parse) {
     /* the GPU parses: reserve the trailer the parse will produce (the
        payload's counts, fdt_txn_peek) and hand the payload over as a frag */
@@ -435,7 +523,7 @@ void vm_after_frag(void *ctx, uint64_t in_idx, uint64_t seq, uint64_t *opt_sig, 
     __builtin_prefetch(b.frags.data() + b.frags.size() + 12, 1);
     b.frags.push_back(fdgpu_frag_ex_t{(uint32_t)off, (uint32_t)payload_sz, (uint32_t)b.tr_used, (uint32_t)fp});
     b.items.push_back(VItem{seq, t->cur_tag, (uint32_t)t->out_chunk, (uint32_t)payload_sz, 1u, (uint32_t)*opt_tsorig,
-                            (uint32_t)b.tr_used, (uint32_t)fp});
+                            (uint32_t)b.tr_used, (uint32_t)fp, 0u});
     b.tr_used += (fp + 3) & ~3ull;
     b.end_off = off + payload_sz;
     b.sig_cnt += fdt_frag_sig_bound(payload_sz);
@@ -470,7 +558,7 @@ void vm_after_frag(void *ctx, uint64_t in_idx, uint64_t seq, uint64_t *opt_sig, 
   d.sig_cnt = tt->signature_cnt;
   b.txns.push_back(d);
   b.items.push_back(VItem{seq, fdt_hash(t->cfg.hashmap_seed, txn + tt->signature_off, 64), (uint32_t)t->out_chunk,
-                          (uint32_t)new_sz, tt->signature_off, (uint32_t)*opt_tsorig, 0u, 0u});
+                          (uint32_t)new_sz, tt->signature_off, (uint32_t)*opt_tsorig, 0u, 0u, 0u});
   b.end_off = off + new_sz;
   if (tt->signature_cnt <= 16) { b.sig_cnt += tt->signature_cnt; t->st.sigs += tt->signature_cnt; }
   t->out_chunk = fdt_dcache_compact_next(t->out_chunk, new_sz, t->cfg.out_chunk0, t->cfg.out_wmark);
@@ -515,7 +603,15 @@ fdgpu_vmux_t *fdgpu_vmux_new(const fdgpu_vmux_cfg_t *cfg, fdgpu_verifier_t ver) 
   t->cfg = *cfg;
   fdgpu_vmux_cfg_t &c = t->cfg;
   t->gpu_parse = cfg->gpu_parse != 0;
-  if (t->gpu_parse && (!ver.submit_frags || !ver.poll_frags)) { delete t; return nullptr; }
+  t->gather = cfg->gpu_parse == 2;
+  if (cfg->gpu_parse > 2 || (t->gpu_parse && !t->gather && (!ver.submit_frags || !ver.poll_frags)) ||
+      (t->gather && (!ver.submit_io || !ver.poll_io))) {
+    delete t;
+    return nullptr;
+  }
+  if (t->gather)
+    for (uint64_t i = 0; i < cfg->in_cnt; i++)
+      if (!cfg->in_mcache[i] || !pow2(cfg->in_depth[i])) { delete t; return nullptr; }
   if (!c.round_robin_cnt) c.round_robin_cnt = 1;
   if (!c.inflight_max) c.inflight_max = 2;
   if (!c.tcache_depth) c.tcache_depth = FDT_VERIFY_TCACHE_DEPTH;
@@ -533,6 +629,10 @@ fdgpu_vmux_t *fdgpu_vmux_new(const fdgpu_vmux_cfg_t *cfg, fdgpu_verifier_t ver) 
   t->tcache_mem.assign(fp / 8, 0);
   t->tcache = fdt_tcache_new(t->tcache_mem.data(), c.tcache_depth, c.tcache_map_cnt);
   t->use_ring = c.tcache_depth <= FDT_TAGRING_MAX;
+  if (t->gather) {
+    t->cap_of.resize(FDT_TPU_MTU + 1);
+    for (uint64_t sz = 0; sz <= FDT_TPU_MTU; sz++) t->cap_of[sz] = (uint16_t)(align2(sz) + fdt_frag_fp_bound(sz) + 2);
+  }
   fdt_tagring_init(&t->ring, c.tcache_depth);
   t->ver = ver;
   t->out_chunk = c.out_chunk0;
@@ -544,7 +644,8 @@ fdgpu_vmux_t *fdgpu_vmux_new(const fdgpu_vmux_cfg_t *cfg, fdgpu_verifier_t ver) 
   for (auto &b : t->storage) {
     b.codes.resize(c.batch_txn_max);
     b.txns.reserve(c.batch_txn_max);
-    if (t->gpu_parse) b.frags.reserve(c.batch_txn_max);
+    if (t->gpu_parse && !t->gather) b.frags.reserve(c.batch_txn_max);
+    if (t->gather) { b.fio.reserve(c.batch_txn_max); b.tags.resize(c.batch_txn_max); b.out_szs.resize(c.batch_txn_max); }
     b.items.reserve(c.batch_txn_max);
     t->pool.push_back(&b);
   }
@@ -555,7 +656,8 @@ void fdgpu_vmux_delete(fdgpu_vmux_t *t) {
   if (!t) return;
   for (VBatch *b : t->inflight)                 /* the verifier may still write codes / read the arena */
     if (!b->done) {
-      if (t->gpu_parse) t->ver.poll_frags(t->ver.ctx, b->ticket, b->codes.data(), b->trailers.data(), 1);
+      if (t->gather) t->ver.poll_io(t->ver.ctx, b->ticket, b->codes.data(), b->tags.data(), b->out_szs.data(), 1);
+      else if (t->gpu_parse) t->ver.poll_frags(t->ver.ctx, b->ticket, b->codes.data(), b->trailers.data(), 1);
       else t->ver.poll(t->ver.ctx, b->ticket, b->codes.data(), 1);
     }
   delete t;

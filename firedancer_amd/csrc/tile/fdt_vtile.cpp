@@ -152,6 +152,28 @@ int dispatch_poll_frags(void *ctx, int64_t ticket, int8_t *codes, uint8_t *trail
   return fdgpu_poll_frags(d->eng[ticket % n], ticket / n, codes, trailers, blocking);
 }
 
+int64_t dispatch_submit_io(void *ctx, const fdgpu_frag_io_t *fio, uint64_t n, uint8_t *out, uint64_t out_sz,
+                           uint64_t seed) {
+  auto *d = (fdgpu_dispatch *)ctx;
+  const uint32_t ne = (uint32_t)d->eng.size();
+  for (uint32_t k = 0; k < ne; k++) {
+    const uint32_t idx = (d->next + k) % ne;
+    const int64_t t = fdgpu_submit_frags_io(d->eng[idx], fio, n, out, out_sz, seed);
+    if (t == FDGPU_ERR_FULL) continue;
+    if (t < 0) return t;
+    d->next = (idx + 1) % ne;
+    return t * ne + idx;
+  }
+  return FDGPU_ERR_FULL;
+}
+
+int dispatch_poll_io(void *ctx, int64_t ticket, int8_t *codes, uint64_t *tags, uint16_t *out_szs, int blocking) {
+  auto *d = (fdgpu_dispatch *)ctx;
+  const int64_t n = (int64_t)d->eng.size();
+  if (ticket < 0) return FDGPU_ERR_TICKET;
+  return fdgpu_poll_frags_io(d->eng[ticket % n], ticket / n, codes, tags, out_szs, blocking);
+}
+
 int dispatch_stage_cancel(void *ctx) {
   auto *d = (fdgpu_dispatch *)ctx;
   if (d->staged < 0) return FDGPU_ERR_INVAL;
@@ -187,6 +209,8 @@ fdgpu_verifier_t fdgpu_dispatch_verifier(fdgpu_dispatch_t *d) {
   v.stage_cancel = dispatch_stage_cancel;
   v.submit_frags = dispatch_submit_frags;
   v.poll_frags = dispatch_poll_frags;
+  v.submit_io = dispatch_submit_io;
+  v.poll_io = dispatch_poll_io;
   return v;
 }
 

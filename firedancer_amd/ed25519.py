@@ -200,6 +200,37 @@ class VerifyEngine:
         del self._pending[ticket]
         return codes[:n], tr[:tsz]
 
+    def submit_frags_io(self, frags, out, out_sz, hash_seed):
+        """fdgpu_submit_frags_io: payloads read by the device where they lie
+        (frags: FRAG_IO_DTYPE {src host address, sz, out_off, out_cap}, every
+        src inside a registered buffer), out frags written to `out` (a
+        registered numpy buffer) [0, out_sz)."""
+        frags = np.ascontiguousarray(frags, dtype=FRAG_IO_DTYPE)
+        out = np.asarray(out)
+        if out_sz > out.nbytes:
+            raise ValueError("out_sz exceeds the out buffer")
+        tk = _lib.lib().fdgpu_submit_frags_io(self._h, frags.ctypes.data, len(frags), out.ctypes.data, int(out_sz),
+                                              int(hash_seed))
+        if tk < 0:
+            raise RuntimeError(f"fdgpu_submit_frags_io failed ({tk}): {_lib.last_error()}")
+        self._pending[tk] = (len(frags), frags)
+        return tk
+
+    def poll_frags_io(self, ticket, blocking=True):
+        """-> (codes int8[n], tags uint64[n], out_szs uint16[n]) or None while pending."""
+        n, _ = self._pending[ticket]
+        codes = np.zeros(max(n, 1), dtype=np.int8)
+        tags = np.zeros(max(n, 1), dtype=np.uint64)
+        osz = np.zeros(max(n, 1), dtype=np.uint16)
+        rc = _lib.lib().fdgpu_poll_frags_io(self._h, ticket, codes.ctypes.data, tags.ctypes.data, osz.ctypes.data,
+                                            1 if blocking else 0)
+        if rc == 1:
+            return None
+        if rc != 0:
+            raise RuntimeError(f"fdgpu_poll_frags_io failed ({rc}): {_lib.last_error()}")
+        del self._pending[ticket]
+        return codes[:n], tags[:n], osz[:n]
+
     def verify_device(self, d_arena, d_sig_desc, n_sig, d_txn_desc, n_txn, d_sig_codes, d_txn_codes, stream=0):
         """Device-resident path; all pointers are device addresses (ints)."""
         rc = _lib.lib().fdgpu_verify_device(self._h, d_arena, d_sig_desc, n_sig, d_txn_desc, n_txn,
@@ -341,6 +372,7 @@ class DeviceBatch:
 
 FRAG_DTYPE = np.dtype([("off", "<u4"), ("sz", "<u4")])
 FRAG_EX_DTYPE = np.dtype([("off", "<u4"), ("sz", "<u4"), ("tr_off", "<u4"), ("tr_cap", "<u4")])
+FRAG_IO_DTYPE = np.dtype([("src", "<u8"), ("sz", "<u4"), ("out_off", "<u4"), ("out_cap", "<u4"), ("_pad", "<u4")])
 CODE_TRAILER_CAP = -65        # FDGPU_CODE_TRAILER_CAP
 CODE_PARSE_FAIL = -64          # FDGPU_CODE_PARSE_FAIL
 TXN_MAX_SZ = 852               # FD_TXN_MAX_SZ: stride of the parsed fd_txn_t records

@@ -79,6 +79,11 @@ SUBMIT_FN = c.CFUNCTYPE(c.c_int64, vp, vp, c.c_uint64, vp, c.c_uint64)
 POLL_FN = c.CFUNCTYPE(c.c_int, vp, c.c_int64, vp, c.c_int)
 SUBMIT_FRAGS_FN = c.CFUNCTYPE(c.c_int64, vp, vp, c.c_uint64, vp, c.c_uint64, c.c_uint64)
 POLL_FRAGS_FN = c.CFUNCTYPE(c.c_int, vp, c.c_int64, vp, vp, c.c_int)
+SUBMIT_IO_FN = c.CFUNCTYPE(c.c_int64, vp, vp, c.c_uint64, vp, c.c_uint64, c.c_uint64)
+POLL_IO_FN = c.CFUNCTYPE(c.c_int, vp, c.c_int64, vp, vp, vp, c.c_int)
+# fdgpu_frag_io_t: a payload where it lies and its out frag's room (fdgpu_submit_frags_io)
+FRAG_IO_DTYPE = np.dtype([("src", "<u8"), ("sz", "<u4"), ("out_off", "<u4"), ("out_cap", "<u4"), ("_pad", "<u4")])
+CODE_LAPPED = -66
 # fdgpu_frag_ex_t: a payload and the place its parsed fd_txn_t goes (fdgpu_submit_frags)
 FRAG_EX_DTYPE = np.dtype([("off", "<u4"), ("sz", "<u4"), ("tr_off", "<u4"), ("tr_cap", "<u4")])
 CODE_PARSE_FAIL, CODE_TRAILER_CAP = -64, -65
@@ -89,7 +94,7 @@ class Verifier(c.Structure):
     hooks (left NULL by PyVerifier; set by the GPU dispatcher)."""
     _fields_ = [("ctx", vp), ("submit", SUBMIT_FN), ("poll", POLL_FN), ("stage", vp), ("submit_staged", vp),
                 ("poll_keep", vp), ("release", vp), ("stage_cancel", vp), ("submit_frags", SUBMIT_FRAGS_FN),
-                ("poll_frags", POLL_FRAGS_FN)]
+                ("poll_frags", POLL_FRAGS_FN), ("submit_io", SUBMIT_IO_FN), ("poll_io", POLL_IO_FN)]
 
 
 class VTileCfg(c.Structure):
@@ -163,7 +168,8 @@ class VMuxCfg(c.Structure):
                 ("round_robin_cnt", c.c_uint64), ("hashmap_seed", c.c_uint64), ("tcache_depth", c.c_uint64),
                 ("tcache_map_cnt", c.c_uint64), ("batch_txn_max", c.c_uint32), ("inflight_max", c.c_uint32),
                 ("batch_wait_ns", c.c_uint64), ("batch_sig_max", c.c_uint64), ("batch_bytes_max", c.c_uint64),
-                ("gpu_parse", c.c_uint32), ("_pad", c.c_uint32)]
+                ("gpu_parse", c.c_uint32), ("_pad", c.c_uint32), ("in_mcache", vp * MUX_IN_MAX),
+                ("in_depth", c.c_uint64 * MUX_IN_MAX)]
 
 
 class LinkT(c.Structure):
@@ -644,11 +650,67 @@ class PyVerifier:
                     c.memmove(trailers, t, len(t))
             return rc
 
-        self.trailers = {}
+        def submit_io(ctx, frags, n, out, out_sz, seed):
+            # fdgpu_submit_frags_io on the host: each payload read where it
+            # lies, parsed, tagged, its out frag written at its reserved place
+            if len(self.results) >= self.slots:
+                return -12
+            fio = np.frombuffer((c.c_uint8 * (24 * n)).from_address(frags), dtype=FRAG_IO_DTYPE).copy() if n else \
+                np.zeros(0, dtype=FRAG_IO_DTYPE)
+            codes = np.zeros(max(n, 1), dtype=np.int8)
+            tags = np.zeros(max(n, 1), dtype=np.uint64)
+            osz = np.zeros(max(n, 1), dtype=np.uint16)
+            arena, txns, idx = bytearray(), [], []
+            for i, f in enumerate(fio):
+                sz = int(f["sz"])
+                p = c.string_at(int(f["src"]), sz)
+                fp, raw = txn_parse(p)
+                if not fp:
+                    codes[i] = CODE_PARSE_FAIL
+                    continue
+                h = txn_decode(raw)
+                tags[i] = fd_hash(seed, p[h["signature_off"]:h["signature_off"] + 64])
+                toff = (sz + 1) & ~1
+                frag = p + b"\0" * (toff - sz) + raw + sz.to_bytes(2, "little")
+                if len(frag) > int(f["out_cap"]):
+                    codes[i] = CODE_TRAILER_CAP
+                    continue
+                c.memmove(out + int(f["out_off"]), frag, len(frag))
+                osz[i] = len(frag)
+                off = len(arena)
+                arena += p
+                txns.append((off + h["message_off"], sz - h["message_off"], off + h["signature_off"],
+                             off + h["acct_addr_off"], h["signature_cnt"]))
+                idx.append(i)
+            if txns:
+                codes[idx] = np.asarray(self.fn(np.frombuffer(bytes(arena), dtype=np.uint8),
+                                                np.array(txns, dtype=TXN_DTYPE)), dtype=np.int8)
+            self.batches.append(n)
+            k = self.next
+            self.next += 1
+            self.results[k] = codes[:n]
+            self.io[k] = (tags[:n], osz[:n])
+            self.polls[k] = 0
+            return k
+
+        def poll_io(ctx, ticket, codes, tags, out_szs, blocking):
+            if ticket not in self.io:
+                return -13
+            rc = poll(ctx, ticket, codes, blocking)
+            if rc == 0:
+                t, o = self.io.pop(ticket)
+                if len(t):
+                    c.memmove(tags, t.ctypes.data, 8 * len(t))
+                    c.memmove(out_szs, o.ctypes.data, 2 * len(o))
+            return rc
+
+        self.trailers, self.io = {}, {}
+        self._submit_io, self._poll_io = SUBMIT_IO_FN(submit_io), POLL_IO_FN(poll_io)
         self._submit, self._poll = SUBMIT_FN(submit), POLL_FN(poll)
         self._submit_frags, self._poll_frags = SUBMIT_FRAGS_FN(submit_frags), POLL_FRAGS_FN(poll_frags)
         self.struct = Verifier(None, self._submit, self._poll)
         self.struct.submit_frags, self.struct.poll_frags = self._submit_frags, self._poll_frags
+        self.struct.submit_io, self.struct.poll_io = self._submit_io, self._poll_io
 
 
 class EngineVerifier:
@@ -814,7 +876,9 @@ class VerifyMuxTile:
         vc.batch_wait_ns = int(batch_wait_us * 1000)
         vc.batch_sig_max = batch_sig_max or getattr(verifier, "sig_max", 0)
         vc.batch_bytes_max = batch_bytes_max or getattr(verifier, "arena_max", 0)
-        vc.gpu_parse = 1 if gpu_parse else 0
+        vc.gpu_parse = int(gpu_parse)            # False/True/0/1/2 (2: the GPU also gathers the payloads)
+        for i, ln in enumerate(in_links):
+            vc.in_mcache[i], vc.in_depth[i] = ln.mcache_ptr, ln.depth
         self.vcfg = vc
         self._t = L.fdgpu_vmux_new(c.byref(vc), verifier.struct)
         if not self._t:
@@ -836,9 +900,11 @@ class VerifyMuxTile:
         self._rc = None
         self._registered = []
         if register:
+            bufs = [out_link.dcache] + ([ln.dcache for ln in in_links] if vc.gpu_parse == 2 else [])
             for e in getattr(verifier, "engines", []):
-                e.host_register(out_link.dcache)
-                self._registered.append(e)
+                for b in bufs:
+                    e.host_register(b)
+                    self._registered.append((e, b))
         self._threading = threading
         self._th = None
 
@@ -906,8 +972,8 @@ class VerifyMuxTile:
         if self._t:
             lib().fdgpu_vmux_delete(self._t)
             self._t = None
-        for e in self._registered:
-            e.host_unregister(self.out_link.dcache)
+        for e, b in self._registered:
+            e.host_unregister(b)
         self._registered = []
 
     def __del__(self):

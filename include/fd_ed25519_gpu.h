@@ -278,6 +278,39 @@ int64_t fdgpu_submit_frags( fdgpu_engine_t * e, uint8_t const * arena, uint64_t 
                             fdgpu_frag_ex_t const * frags, uint64_t frag_cnt, uint64_t trailer_sz );
 int     fdgpu_poll_frags  ( fdgpu_engine_t * e, int64_t ticket, int8_t * codes, uint8_t * trailers, int blocking );
 
+/* Gathered frag batches: the verify tile's path with no payload byte touched
+   on the host.  Frag i's payload lies at host address src (16-byte aligned,
+   inside a region registered with fdgpu_host_register -- the quic -> verify
+   dcache, where the producer wrote it) and its out frag goes to
+   out[out_off, out_off + out_cap) (out inside a registered region -- the
+   verify -> dedup dcache).  On the slot's stream the device reads each
+   payload from host memory, parses it (fd_txn_parse), verifies it
+   (batch_single_msg), tags its first signature (fd_hash(hash_seed, sig, 64),
+   the dedup tag fd_verify.c publishes as the frag's sig) and writes the out
+   frag exactly as the reference's after_frag lays it out in the out dcache
+   (fd_verify.c:93-136): [payload][pad to 2][fd_txn_t][u16 payload_sz];
+   then out[0, out_sz) is copied back in one DMA.  out_cap must hold
+   align2(sz) + footprint + 2; fdgpu_frag_out_cap(sz) always does (a bound
+   from the size alone).  fdgpu_poll_frags_io returns per frag the code (as
+   fdgpu_poll_frags: FDGPU_CODE_PARSE_FAIL, FDGPU_CODE_TRAILER_CAP when the
+   parsed out frag does not fit out_cap), the tag (0 unless parsed) and the
+   out frag's size (0 unless parsed).  The payloads must stay unchanged until
+   the batch is polled -- a producer that may lap the reader is detected by
+   the caller after the poll (the tile re-checks the in mcache, as
+   fd_mux.c:641-655 does after its copy). */
+typedef struct {
+  uint64_t src;         /* host address of the payload */
+  uint32_t sz;          /* <= FD_TXN_MTU (1232) */
+  uint32_t out_off;
+  uint32_t out_cap;
+  uint32_t _pad;
+} fdgpu_frag_io_t;
+uint32_t fdgpu_frag_out_cap   ( uint32_t sz );
+int64_t  fdgpu_submit_frags_io( fdgpu_engine_t * e, fdgpu_frag_io_t const * frags, uint64_t frag_cnt,
+                                uint8_t * out, uint64_t out_sz, uint64_t hash_seed );
+int      fdgpu_poll_frags_io  ( fdgpu_engine_t * e, int64_t ticket, int8_t * codes, uint64_t * tags,
+                                uint16_t * out_szs, int blocking );
+
 /* After a verify of a frag batch: frag i's parsed fd_txn_t (byte-identical to
    fd_txn_parse's output) at txn_out + i * 852 (FD_TXN_MAX_SZ; NULL: skip),
    its footprint (0: not a transaction) in txn_sz[i] (NULL: skip). */

@@ -215,6 +215,13 @@ typedef struct {
   int64_t   (*submit_frags) ( void * ctx, uint8_t const * arena, uint64_t arena_sz, fdgpu_frag_ex_t const * frags,
                               uint64_t frag_cnt, uint64_t trailer_sz );
   int       (*poll_frags)   ( void * ctx, int64_t ticket, int8_t * codes, uint8_t * trailers, int blocking );
+  /* Optional gathered frag batches (NULL when unsupported): payloads read
+     where they lie, out frags written back by the verifier,
+     fdgpu_submit_frags_io / fdgpu_poll_frags_io semantics. */
+  int64_t   (*submit_io)    ( void * ctx, fdgpu_frag_io_t const * frags, uint64_t frag_cnt, uint8_t * out,
+                              uint64_t out_sz, uint64_t hash_seed );
+  int       (*poll_io)      ( void * ctx, int64_t ticket, int8_t * codes, uint64_t * tags, uint16_t * out_szs,
+                              int blocking );
 } fdgpu_verifier_t;
 
 /* Multi-GPU dispatcher: batches go round-robin over `engine_cnt` engines
@@ -447,9 +454,22 @@ typedef struct {
   uint64_t        batch_bytes_max;               /* arena bytes per batch (<= the engines' max_arena);
                                                     0: batch_txn_max x FDT_TPU_DCACHE_MTU rounded to chunks */
   uint32_t        gpu_parse;                     /* 1: fd_txn_parse runs on the GPU (the verifier's
-                                                    submit_frags / poll_frags; required then) */
+                                                    submit_frags / poll_frags; required then);
+                                                    2: the GPU also reads the payloads where they lie
+                                                    and writes the out frags (submit_io / poll_io):
+                                                    the tile touches no payload byte */
   uint32_t        _pad;
+  /* gpu_parse 2: the in links' mcaches, re-checked after a batch is polled
+     (a frag whose line the producer has lapped since is dropped as overrun;
+     the in dcaches must hold depth + 1 frags, as fdt_dcache_data_sz sizes
+     them, so an unlapped line means an intact payload) */
+  fdt_frag_meta_t const * in_mcache[ FDT_MUX_IN_MAX ];
+  uint64_t        in_depth [ FDT_MUX_IN_MAX ];
 } fdgpu_vmux_cfg_t;
+
+/* gpu_parse 2: the code a frag gets when its in-mcache line was lapped
+   before the batch was polled (counted as overrun, logged LOST) */
+#define FDGPU_CODE_LAPPED (-66)
 
 typedef struct fdgpu_vmux fdgpu_vmux_t;
 

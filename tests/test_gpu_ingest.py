@@ -204,3 +204,101 @@ def test_ring_frag_batches_vs_oracle_and_trailers(engine, oracle, txn_fixtures, 
                 assert bytes(trailers[o:o + fp]) == raw, k
         if ci == 2:
             assert (codes == CODE_TRAILER_CAP).sum() > 5
+
+
+def _aligned(n, a=4096):
+    buf = np.zeros(n + a, dtype=np.uint8)
+    o = (-buf.ctypes.data) % a
+    return buf[o:o + n]
+
+
+def test_ring_frag_io_batches(engine, oracle, txn_fixtures, quic_corpus):
+    """fdgpu_submit_frags_io / fdgpu_poll_frags_io (the verify tile's gather
+    path): payloads at 64-B chunk offsets of a registered "in dcache", read
+    there by the device; per frag the oracle's code or PARSE_FAIL, the dedup
+    tag fd_hash(seed, first signature, 64) as the host computes it, and the
+    out frag [payload][pad][fd_txn_t][u16 sz] written at its reserved place
+    in a registered "out dcache", byte-equal to the host layout; a
+    reservation too small for the parsed out frag gets TRAILER_CAP; two
+    batches in flight; a payload outside every registered region is
+    refused."""
+    from firedancer_amd.ed25519 import CODE_TRAILER_CAP, FRAG_IO_DTYPE
+    from firedancer_amd import _lib
+    L = _lib.lib()
+    cases = [p for p in _payload_cases(txn_fixtures, quic_corpus) if len(p) <= 1232]
+    rnd = random.Random(0x10A)
+    rnd.shuffle(cases)
+    chunks = [cases[i:i + 2500] for i in range(0, 7500, 2500)]
+    seed = 0x5EED1234ABCD
+    in_buf = _aligned(sum((len(p) + 63) // 64 * 64 for p in cases[:7500]) + 4096)
+    out_buf = _aligned(7500 * (1232 + 852 + 64) + 4096)
+    engine.host_register(in_buf)
+    engine.host_register(out_buf)
+    try:
+        in_off = [0]
+        out_base = [0]
+
+        def submit(ci, ps):
+            fio = np.zeros(len(ps), dtype=FRAG_IO_DTYPE)
+            o = 0
+            short = set()
+            for k, p in enumerate(ps):
+                a = in_off[0]
+                in_buf[a:a + len(p)] = np.frombuffer(p, dtype=np.uint8)
+                in_off[0] = a + (len(p) + 63) // 64 * 64
+                cap = L.fdgpu_frag_out_cap(len(p))
+                fp, _ = tile.txn_parse(p)
+                if ci == 1 and k % 89 == 3 and fp:
+                    cap = ((len(p) + 1) & ~1) + fp + 1        # one byte short
+                    short.add(k)
+                fio[k] = (in_buf.ctypes.data + a, len(p), o, cap, 0)
+                o += (cap + 63) // 64 * 64
+            base = out_base[0]
+            out_base[0] += o
+            view = out_buf[base:base + o]
+            return engine.submit_frags_io(fio, view, o, seed), fio, view, ps, short
+
+        inflight = [submit(0, chunks[0]), submit(1, chunks[1])]
+        for ci in range(len(chunks)):
+            tk, fio, view, ps, short = inflight.pop(0)
+            codes, tags, osz = engine.poll_frags_io(tk)
+            if ci + 2 < len(chunks):
+                inflight.append(submit(ci + 2, chunks[ci + 2]))
+            arena = np.frombuffer(b"".join(ps) + b"\0" * 16, dtype=np.uint8)
+            offs = np.cumsum([0] + [len(p) for p in ps])
+            td = np.zeros(len(ps), dtype=workload.TXN_DTYPE)
+            parsed = [tile.txn_parse(p) for p in ps]
+            for k, (fp, raw) in enumerate(parsed):
+                if fp:
+                    d = tile.txn_decode(raw)
+                    b0 = int(offs[k])
+                    td[k] = (b0 + d["message_off"], len(ps[k]) - d["message_off"], b0 + d["signature_off"],
+                             b0 + d["acct_addr_off"], d["signature_cnt"])
+            exp = oracle.verify_txns(arena, td)
+            for k, ((fp, raw), f) in enumerate(zip(parsed, fio)):
+                p = ps[k]
+                if not fp:
+                    assert codes[k] == CODE_PARSE_FAIL and osz[k] == 0 and tags[k] == 0, k
+                    continue
+                d = tile.txn_decode(raw)
+                so = d["signature_off"]
+                assert tags[k] == tile.fd_hash(seed, p[so:so + 64]), k
+                if k in short:
+                    assert codes[k] == CODE_TRAILER_CAP and osz[k] == 0, k
+                    continue
+                assert codes[k] == exp[k], k
+                frag = p + b"\0" * (((len(p) + 1) & ~1) - len(p)) + raw + len(p).to_bytes(2, "little")
+                assert osz[k] == len(frag), k
+                o = int(f["out_off"])
+                assert bytes(view[o:o + len(frag)]) == frag, k
+            if ci == 1:
+                assert len(short) > 5
+        # a payload outside every registered region
+        stray = np.zeros(4096, dtype=np.uint8)
+        fio = np.zeros(1, dtype=FRAG_IO_DTYPE)
+        fio[0] = ((stray.ctypes.data + 63) // 64 * 64, 100, 0, L.fdgpu_frag_out_cap(100), 0)
+        with pytest.raises(RuntimeError):
+            engine.submit_frags_io(fio, out_buf, 4096, seed)
+    finally:
+        engine.host_unregister(in_buf)
+        engine.host_unregister(out_buf)

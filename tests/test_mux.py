@@ -198,7 +198,7 @@ def _run_vmux(payloads, verifier, seed=0xABCD, batch=4, inflight=2, rr=(0, 1), d
     return vm, inl, outl
 
 
-@pytest.mark.parametrize("gpu_parse", [False, True])
+@pytest.mark.parametrize("gpu_parse", [False, True, 2])
 @pytest.mark.parametrize("batch,inflight,lag,rr", [(1, 1, 0, (0, 1)), (7, 2, 2, (0, 1)), (64, 3, 1, (1, 3)),
                                                     (1000, 2, 0, (0, 1))])
 def test_vmux_vs_sequential_model(oracle, batch, inflight, lag, rr, gpu_parse):
@@ -208,7 +208,10 @@ def test_vmux_vs_sequential_model(oracle, batch, inflight, lag, rr, gpu_parse):
     latency / round-robin share -- with fd_txn_parse on the tile's core, and
     with the parse handed to the verifier (gpu_parse: the tile reserves each
     trailer from the payload's counts; here a host stand-in of
-    fdgpu_submit_frags parses)."""
+    fdgpu_submit_frags parses), and with the payload copy handed over too
+    (gpu_parse 2: the tile reserves the out frag from the size alone, the
+    verifier -- a host stand-in of fdgpu_submit_frags_io -- reads the
+    payload in the in dcache and writes the out frag)."""
     ps = _mixed_stream(800, seed=batch * 17 + lag)
     seed = 0x99 + batch
     ver = tile.PyVerifier(oracle_fn(oracle), slots=inflight, lag=lag)
@@ -229,7 +232,7 @@ def test_vmux_vs_sequential_model(oracle, batch, inflight, lag, rr, gpu_parse):
     vm.close()
 
 
-@pytest.mark.parametrize("gpu_parse", [False, True])
+@pytest.mark.parametrize("gpu_parse", [False, True, 2])
 def test_vmux_small_dcache_wraps_under_flow_control(oracle, gpu_parse):
     """An out dcache with room for ~8 maximal frags, 12 credits, and a slow
     consumer that reads each published frag (then advances the fseq) while
@@ -269,6 +272,66 @@ def test_vmux_small_dcache_wraps_under_flow_control(oracle, gpu_parse):
     assert codes.tolist() == exp_out
     assert vm.stats()["backpressure"] > 0 and vm.mux_stats()["backpressure"] > 0
     vm.close()
+
+
+def test_vmux_gather_drops_lapped_frags(oracle):
+    """gpu_parse 2: the verifier reads payloads in the in dcache after the
+    tile took them, so the tile re-checks the in mcache once the batch is
+    polled; frags whose line the producer lapped meanwhile are dropped as
+    overrun (logged LOST), the rest of the stream is verified as the model
+    says."""
+    ps = _mixed_stream(64, seed=11)[:24]
+    assert len(ps) == 24
+    inl = tile.Link(16, 1232)
+    outl = tile.Link(64, tile.TPU_DCACHE_MTU, data_sz=64 * (tile.TPU_DCACHE_MTU + 64))
+    ver = tile.PyVerifier(oracle_fn(oracle), slots=1, lag=1 << 60)       # pending until released below
+    vm = tile.VerifyMuxTile(inl, outl, ver, hashmap_seed=0x77, batch_txn_max=8, inflight_max=1, log_max=1 << 10,
+                            batch_wait_us=100, gpu_parse=2)
+    for p in ps[:8]:
+        inl.publish(p)
+    vm.start()
+    _wait(lambda: len(ver.batches) == 1)                   # the first 8 frags are in flight
+    for p in ps[8:]:
+        inl.publish(p)                                     # seqs 16..23 overwrite the lines of seqs 0..7
+    ver.lag = 0
+    _wait(lambda: vm.final_cnt() == len(ps))
+    vm.stop()
+    seqs, codes = vm.log()
+    assert seqs.tolist() == list(range(len(ps)))
+    assert codes.tolist()[:8] == [3] * 8                   # FDGPU_VTILE_LOG_LOST
+    exp_out, _ = tile_model.verify_tile_model(ps, 0x77, oracle_fn(oracle))
+    tail_out, _ = tile_model.verify_tile_model(ps[8:], 0x77, oracle_fn(oracle))
+    assert codes.tolist()[8:] == tail_out
+    assert vm.stats()["overrun"] == 8
+    vm.close()
+
+
+def test_frag_out_cap_bounds_every_parse(quic_corpus):
+    """fdgpu_frag_out_cap(sz) (the gather tile's reservation, from the size
+    alone) holds [payload][pad][fd_txn_t][u16] for every payload that
+    parses: the QUIC corpus, generated cfg1/cfg3 txns and random byte
+    mutations of them."""
+    from firedancer_amd import _lib, workload
+    L = _lib.lib()
+    rng = random.Random(3)
+    pays = list(quic_corpus)
+    for gen in (workload.cfg1, workload.cfg3):
+        a, t, _ = gen(300, seed=9)
+        pays += workload.payloads(a, t)
+    muts = []
+    for p in pays[:600]:
+        for _ in range(6):
+            b = bytearray(p)
+            b[rng.randrange(len(b))] = rng.randrange(256)
+            muts.append(bytes(b))
+    checked = 0
+    for p in pays + muts:
+        fp, _ = tile.txn_parse(p)
+        if fp:
+            assert ((len(p) + 1) & ~1) + fp + 2 <= L.fdgpu_frag_out_cap(len(p)), (len(p), fp)
+            checked += 1
+    assert checked > 1000
+    assert L.fdgpu_frag_out_cap(1232) <= 1232 + 852 + 2
 
 
 def test_vmux_cfg_checks():

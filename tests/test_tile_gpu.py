@@ -123,14 +123,16 @@ def test_twelve_signature_txns_default_config():
 
 # ------------------------------------ the verify tile as mux callbacks (vmux)
 
-@pytest.mark.parametrize("gpu_parse", [False, True])
+@pytest.mark.parametrize("gpu_parse", [False, True, 2])
 def test_vmux_mixed_stream_vs_model_gpu(engines, oracle, gpu_parse):
     """fdgpu_vmux on fdt_mux_run over the MI355X engines: frags copied into
     the out dcache (registered with both engines, so each batch is DMA'd from
     there with no staging copy), verified, and published in place -- every
     outcome and the published stream equal the sequential model's.  With
     gpu_parse the batches are frag batches (fdgpu_submit_frags): fd_txn_parse
-    runs on the GPU and the trailers come back from it."""
+    runs on the GPU and the trailers come back from it.  With gpu_parse 2
+    (fdgpu_submit_frags_io) the GPU reads each payload in the registered in
+    dcache and writes the whole out frag back: the tile copies nothing."""
     from test_tile import _mixed_stream
     ps = _mixed_stream(3000, seed=7)
     seed = 0xC0DE
@@ -154,7 +156,8 @@ def test_vmux_mixed_stream_vs_model_gpu(engines, oracle, gpu_parse):
     ver.close()
 
 
-def test_vmux_two_tiles_share_engines_gpu(engines, oracle):
+@pytest.mark.parametrize("gpu_parse", [0, 2])
+def test_vmux_two_tiles_share_engines_gpu(engines, oracle, gpu_parse):
     """Two verify mux tiles on their own threads take the round-robin shares
     of one in link (fd_verify.c:46) and share the node's engines (the ring
     API is thread-safe per engine); each tile's outcomes and published
@@ -172,7 +175,7 @@ def test_vmux_two_tiles_share_engines_gpu(engines, oracle):
         ver = tile.EngineVerifier(engines)
         vm = tile.VerifyMuxTile(inl, outl, ver, hashmap_seed=seed, batch_txn_max=64, inflight_max=2,
                                 round_robin_idx=k, round_robin_cnt=2, log_max=1 << 14, cr_max=64,
-                                flow_control=True)
+                                flow_control=True, gpu_parse=gpu_parse)
         tiles.append(vm); outs.append(outl); vers.append(ver)
     seen = [[], []]
     stop = threading.Event()

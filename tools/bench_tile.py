@@ -39,8 +39,10 @@ def main():
     ap.add_argument("--mux", type=int, default=0,
                     help="1: the verify tile as mux callbacks (fdgpu_vmux on fdt_mux_run; frags copied once into "
                          "the registered out dcache and DMA'd from there), 0: the step-loop tile (fdgpu_vtile)")
-    ap.add_argument("--gpu-parse", type=int, default=1,
-                    help="(mux tile) 1: fd_txn_parse on the GPU (fdgpu_submit_frags); 0: on the tile's core")
+    ap.add_argument("--gpu-parse", type=int, default=2,
+                    help="(mux tile) 2: the GPU reads the payloads where they lie and writes the out frags "
+                         "(fdgpu_submit_frags_io); 1: fd_txn_parse on the GPU (fdgpu_submit_frags); 0: on the "
+                         "tile's core")
     ap.add_argument("--producers", type=int, default=1,
                     help="(mux tile) quic->verify links, one producer thread each; every verify tile reads all of "
                          "them round robin (fd_frankendancer.c: all verify tiles read all QUIC tiles)")
@@ -96,7 +98,7 @@ def start_producer(args, inl, arena, offs, sizes, rate, cpus, k=0):
         os.sched_setaffinity(0, keep)
 
 
-def warm(engines, inflight):
+def warm(engines, inflight, out_bytes=0):
     """One small batch through every ring slot of every engine before the
     timed region: a HIP stream's first submission creates its hardware queue
     (milliseconds), which would otherwise land inside the run."""
@@ -117,6 +119,35 @@ def warm(engines, inflight):
         tks = [e.submit_frags(pa, fx, tr) for _ in range(inflight)]     # the slots' GPU-parse buffers too
         for tk in tks:
             e.poll_frags(tk, blocking=True)
+    if out_bytes:
+        warm_io(engines, inflight, ps, out_bytes)
+
+
+def warm_io(engines, inflight, ps, out_bytes):
+    """The gather path's slot buffers (payload addresses, the out image sized
+    for a full batch's out bytes) through every ring slot."""
+    from firedancer_amd.ed25519 import FRAG_IO_DTYPE
+    from firedancer_amd import _lib
+    L = _lib.lib()
+    src = np.zeros(len(ps) * 1280 + 8192, dtype=np.uint8)
+    src = src[(-src.ctypes.data) % 4096:][:len(ps) * 1280 + 4096]
+    out = np.zeros(out_bytes + 8192, dtype=np.uint8)
+    out = out[(-out.ctypes.data) % 4096:][:out_bytes + 4096]
+    fio = np.zeros(len(ps), dtype=FRAG_IO_DTYPE)
+    o = 0
+    for k, p in enumerate(ps):
+        src[k * 1280:k * 1280 + len(p)] = np.frombuffer(p, dtype=np.uint8)
+        cap = L.fdgpu_frag_out_cap(len(p))
+        fio[k] = (src.ctypes.data + k * 1280, len(p), o, cap, 0)
+        o += (cap + 63) // 64 * 64
+    for e in engines:
+        e.host_register(src)
+        e.host_register(out)
+        tks = [e.submit_frags_io(fio, out, out_bytes, 1) for _ in range(inflight)]
+        for tk in tks:
+            e.poll_frags_io(tk, blocking=True)
+        e.host_unregister(src)
+        e.host_unregister(out)
 
 
 def run_once(args, ps, arena, offs, sizes, n_sig, modes, tiles_n, batch, inflight, rate):
@@ -194,7 +225,7 @@ def run_once_mux(args, ps, arena, offs, sizes, n_sig, modes, tiles_n, batch, inf
     frag_bytes = (tile.TPU_DCACHE_MTU + 63) // 64 * 64
     engines = [fa.VerifyEngine(device if device is not None else k % args.gpus, max_txn=batch, max_sig=batch * 12,
                                max_arena=batch * frag_bytes, ring_depth=inflight) for k in range(tiles_n)]
-    warm(engines, inflight)
+    warm(engines, inflight, out_bytes=batch * frag_bytes if args.gpu_parse == 2 else 0)
     P = max(1, args.producers)
     inls = [tile.Link(1 << args.depth_lg, 1232) for _ in range(P)]
     vms, vers = [], []
@@ -203,7 +234,7 @@ def run_once_mux(args, ps, arena, offs, sizes, n_sig, modes, tiles_n, batch, inf
         outl = tile.Link(1 << 14, tile.TPU_DCACHE_MTU, data_sz=tile.vmux_dcache_data_sz(1 << 14, batch, inflight))
         vms.append(tile.VerifyMuxTile(inls, outl, ver, batch_txn_max=batch, inflight_max=inflight,
                                       batch_wait_us=args.wait_us, round_robin_idx=k, round_robin_cnt=tiles_n,
-                                      gpu_parse=bool(args.gpu_parse)))
+                                      gpu_parse=int(args.gpu_parse)))
         vers.append((ver, outl))
     cpus = cpus or workload.physical_cpus()[getattr(args, "cpu_offset", 0):] or workload.physical_cpus()
     # tile k's thread is pinned to cpus[P + k] (VerifyMuxTile.start inherits the caller's mask)
@@ -232,10 +263,11 @@ def run_once_mux(args, ps, arena, offs, sizes, n_sig, modes, tiles_n, batch, inf
     res = {
         "metric": "verify mux tile end-to-end transactions/s (tango in -> GPU verify -> tango out)",
         "tile": "fdgpu_vmux on fdt_mux_run (mux callbacks; registered out dcache, no staging copy)"
-                + ("; fd_txn_parse on the GPU" if args.gpu_parse else "; fd_txn_parse on the tile core"),
+                + {2: "; the GPU reads the payloads in the in dcache, parses, verifies and writes the out frags",
+                   1: "; fd_txn_parse on the GPU", 0: "; fd_txn_parse on the tile core"}[int(args.gpu_parse)],
         "producers": P,
         "txns_per_s": round(len(ps) / wall, 1),
-        "sigs_per_s": round(agg["sigs"] / wall, 1),
+        "sigs_per_s": round(n_sig / wall, 1),
         "wall_s": round(wall, 4), "producer_s": round(prod_s, 4), "producer_published": int(n_pub),
         "gpus": args.gpus, "tiles": tiles_n, "batch_txn_max": batch, "inflight": inflight,
         "rate_target": rate, "workload": "cfg3 (1-12 sigs/txn, payload <= 1232 B, 10% corrupted)"

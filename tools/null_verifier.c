@@ -11,7 +11,7 @@
 
 #define NV_RING 256
 
-typedef struct { int64_t next; uint64_t cnt[NV_RING]; } nv_t;
+typedef struct { int64_t next; uint64_t cnt[NV_RING]; fdgpu_frag_io_t const *sz[NV_RING]; } nv_t;
 
 static int64_t nv_submit(void *ctx, uint8_t const *arena, uint64_t arena_sz, fdgpu_txn_t const *txns, uint64_t n) {
   (void)arena; (void)arena_sz; (void)txns;
@@ -41,6 +41,26 @@ static int nv_poll_frags(void *ctx, int64_t ticket, int8_t *codes, uint8_t *trai
   return nv_poll(ctx, ticket, codes, blocking);
 }
 
+/* gathered frag batches: every frag accepted with a distinct tag and an out
+   size within its reservation; nothing is read or written */
+static uint64_t nv_tag = 1;
+static int64_t nv_submit_io(void *ctx, fdgpu_frag_io_t const *frags, uint64_t n, uint8_t *out, uint64_t out_sz,
+                            uint64_t seed) {
+  (void)out; (void)out_sz; (void)seed;
+  nv_t *v = (nv_t *)ctx;
+  v->cnt[v->next % NV_RING] = n;
+  v->sz[v->next % NV_RING] = frags;
+  return v->next++;
+}
+
+static int nv_poll_io(void *ctx, int64_t ticket, int8_t *codes, uint64_t *tags, uint16_t *out_szs, int blocking) {
+  nv_t *v = (nv_t *)ctx;
+  const uint64_t n = v->cnt[ticket % NV_RING];
+  fdgpu_frag_io_t const *f = v->sz[ticket % NV_RING];
+  for (uint64_t i = 0; i < n; i++) { tags[i] = nv_tag++; out_szs[i] = (uint16_t)(f[i].sz + 32u); }
+  return nv_poll(ctx, ticket, codes, blocking);
+}
+
 void null_verifier_make(fdgpu_verifier_t *out) {
   memset(out, 0, sizeof(*out));
   out->ctx = calloc(1, sizeof(nv_t));
@@ -48,4 +68,6 @@ void null_verifier_make(fdgpu_verifier_t *out) {
   out->poll = nv_poll;
   out->submit_frags = nv_submit_frags;
   out->poll_frags = nv_poll_frags;
+  out->submit_io = nv_submit_io;
+  out->poll_io = nv_poll_io;
 }

@@ -6,7 +6,7 @@
 
      g++ -O2 -g -std=c++17 -I include tools/tile_prof.cpp tools/null_verifier.c -o tools/tile_prof \
          -L firedancer_amd -l:libfd_verify_tile.so -Wl,-rpath,$PWD/firedancer_amd -lpthread -ldl
-     tools/tile_prof <payloads.bin> <offs.bin> <sizes.bin> [gpu_parse 0|1] [repeat]
+     tools/tile_prof <payloads.bin> <offs.bin> <sizes.bin> [gpu_parse 0|1|2] [repeat]
 
    (payload files: numpy tofile of workload.pack_payloads' arena / offs u64 /
    sizes u32.) */
@@ -105,6 +105,7 @@ int main(int argc, char **argv) {
       vc.cr_max = out_depth; vc.round_robin_idx = (uint64_t)k; vc.round_robin_cnt = (uint64_t)tiles; vc.hashmap_seed = 0x5EED;
       vc.batch_txn_max = (uint32_t)batch; vc.inflight_max = (uint32_t)inflight; vc.batch_wait_ns = 200000;
       vc.batch_bytes_max = batch * 2176; vc.gpu_parse = (uint32_t)gpu_parse;
+      vc.in_mcache[0] = in_mc.data(); vc.in_depth[0] = depth;
       vms[k] = fdgpu_vmux_new(&vc, vers[k]);
       if (!vms[k]) { fprintf(stderr, "vmux_new failed\n"); return 1; }
       fdt_mux_cfg_t &mc = mcs[k];
