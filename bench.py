@@ -154,14 +154,16 @@ RING_DEPTH = 8        # ring slots (one stream + workspace each) of the latency/
 
 
 def timed_batch(eng, a, t):
-    """submit -> codes on the host, ms: the completion is watched with
-    non-blocking polls (the completion word, as the verify tile polls), not a
-    blocking event wait whose wake-up adds its own jitter"""
+    """submit -> codes on the host, ms, and the part spent inside submit
+    (descriptor expansion, staging copy, enqueue): the completion is watched
+    with non-blocking polls (the completion word, as the verify tile polls),
+    not a blocking event wait whose wake-up adds its own jitter"""
     t0 = time.perf_counter()
     tk = eng.submit(a, t)
+    t1 = time.perf_counter()
     while eng.poll(tk, blocking=False) is None:
         pass
-    return (time.perf_counter() - t0) * 1e3
+    return (time.perf_counter() - t0) * 1e3, (t1 - t0) * 1e3
 
 
 def latency_and_pcie(eng, arena, txns, batch, nbatches):
@@ -185,7 +187,7 @@ def latency_and_pcie(eng, arena, txns, batch, nbatches):
         a, t = views[i % len(views)]
         eng.verify_txns(a, t)
     gc.disable()
-    lat = [timed_batch(eng, *views[i % len(views)]) for i in range(nbatches)]
+    lat = np.array([timed_batch(eng, *views[i % len(views)]) for i in range(nbatches)])
     gc.enable()
     def pipelined(vs):
         """every ring slot busy: submit -> poll over the batches, sigs/s"""
@@ -215,12 +217,24 @@ def latency_and_pcie(eng, arena, txns, batch, nbatches):
     # the same latency measurement from the registered arena (DMA'd in place,
     # as the verify tile's registered out dcache is)
     gc.disable()
-    lat_reg = [timed_batch(eng, *reg_views[i % len(reg_views)]) for i in range(nbatches)]
+    lat_reg = np.array([timed_batch(eng, *reg_views[i % len(reg_views)]) for i in range(nbatches)])
     gc.enable()
     eng.host_unregister(arena)
-    lat, lat_reg = np.array(lat), np.array(lat_reg)
-    return (float(np.percentile(lat, 50)), float(np.percentile(lat, 99)), pcie, pcie_reg,
-            float(np.percentile(lat_reg, 50)), float(np.percentile(lat_reg, 99)))
+
+    def pct(x, q):
+        return round(float(np.percentile(x, q)), 3)
+    return {"p50_batch_latency_ms": pct(lat[:, 0], 50), "p99_batch_latency_ms": pct(lat[:, 0], 99),
+            "p50_batch_latency_registered_ms": pct(lat_reg[:, 0], 50),
+            "p99_batch_latency_registered_ms": pct(lat_reg[:, 0], 99),
+            # where the tail sits: inside submit (host: expansion, staging) or after it (GPU, read-back, poll)
+            "latency_split_ms": {"staged_submit_p50_p99": [pct(lat[:, 1], 50), pct(lat[:, 1], 99)],
+                                 "staged_rest_p50_p99": [pct(lat[:, 0] - lat[:, 1], 50),
+                                                         pct(lat[:, 0] - lat[:, 1], 99)],
+                                 "registered_submit_p50_p99": [pct(lat_reg[:, 1], 50), pct(lat_reg[:, 1], 99)],
+                                 "registered_rest_p50_p99": [pct(lat_reg[:, 0] - lat_reg[:, 1], 50),
+                                                             pct(lat_reg[:, 0] - lat_reg[:, 1], 99)]},
+            "pcie_inclusive_sigs_per_s_per_gpu": round(pcie, 1),
+            "pcie_inclusive_registered_sigs_per_s_per_gpu": round(pcie_reg, 1)}
 
 
 def sync_latency(arena, txns, calls=1000, threads=64):
@@ -541,14 +555,8 @@ def main():
 
     extras = {}
     if not args.no_extras:
-        p50, p99, pcie, pcie_reg, p50r, p99r = latency_and_pcie(eng, arena, txns, args.latency_batch,
-                                                                 args.latency_batches)
-        extras = {"p50_batch_latency_ms": round(p50, 3), "p99_batch_latency_ms": round(p99, 3),
-                  "p50_batch_latency_registered_ms": round(p50r, 3),
-                  "p99_batch_latency_registered_ms": round(p99r, 3),
-                  "latency_batch_txns": args.latency_batch,
-                  "pcie_inclusive_sigs_per_s_per_gpu": round(pcie, 1),
-                  "pcie_inclusive_registered_sigs_per_s_per_gpu": round(pcie_reg, 1)}
+        extras = latency_and_pcie(eng, arena, txns, args.latency_batch, args.latency_batches)
+        extras["latency_batch_txns"] = args.latency_batch
         if dist.rank == 0:
             extras.update(sync_latency(arena, txns))
         if args.tile:

@@ -34,6 +34,9 @@
 
 #define FDT_TXN_MAX_SZ_BYTES 852u   /* FD_TXN_MAX_SZ (fd_txn.h:98): one parsed fd_txn_t record */
 #define FDT_TXN_MTU_BYTES 1232u     /* FD_TXN_MTU (fd_txn.h:103) */
+#ifndef FDGPU_IO_DIRECT
+#define FDGPU_IO_DIRECT 1           /* gathered batches write out frags and results in place (else: D2H copies) */
+#endif
 
 namespace {
 
@@ -47,6 +50,18 @@ void set_err(const char *fmt, ...) {
 
 #define HIPCHK(x, ret) do { hipError_t e_ = (x); if (e_ != hipSuccess) { \
   set_err("%s failed: %s (%s:%d)", #x, hipGetErrorString(e_), __FILE__, __LINE__); return ret; } } while (0)
+
+}  // namespace
+
+/* FDGPU_SUBMIT_PROF=1: where fdgpu_submit_frags_io's time goes (validation
+   loop, enqueue of copies and kernels), printed at engine close */
+namespace {
+std::atomic<uint64_t> g_sp_loop{0}, g_sp_enq{0}, g_sp_calls{0}, g_sp_frags{0};
+inline uint64_t sp_now() { timespec ts; clock_gettime(CLOCK_MONOTONIC, &ts); return ts.tv_sec * 1000000000ull + ts.tv_nsec; }
+const bool g_sp_on = getenv("FDGPU_SUBMIT_PROF") && getenv("FDGPU_SUBMIT_PROF")[0] == '1';
+}
+
+namespace {
 
 struct Slot {
   hipStream_t stream = nullptr;
@@ -85,6 +100,8 @@ struct Slot {
   uint64_t *h_src = nullptr, *d_src = nullptr;
   uint8_t *d_out = nullptr;
   uint64_t out_cap_bytes = 0;
+  uint8_t *h_io = nullptr, *d_io = nullptr;   /* direct: [frag records][payload addresses], one upload */
+  uint8_t *d_trh = nullptr;                   /* h_tr's device-side address (results written in place) */
 };
 
 }  // namespace
@@ -140,6 +157,8 @@ void slot_free(Slot &s) {
   if (s.h_fx) (void)hipHostFree(s.h_fx);
   if (s.h_tr) (void)hipHostFree(s.h_tr);
   if (s.h_src) (void)hipHostFree(s.h_src);
+  if (s.h_io) (void)hipHostFree(s.h_io);
+  if (s.d_io) (void)hipFree(s.d_io);
   for (void *p : {(void *)s.d_fx, (void *)s.d_txn_out, (void *)s.d_txn_sz, (void *)s.d_txd, (void *)s.d_cnt,
                   (void *)s.d_sig0, (void *)s.d_blocktot, (void *)s.d_n_sig, (void *)s.d_tr, (void *)s.d_src,
                   (void *)s.d_out})
@@ -216,6 +235,7 @@ bool slot_frag_bufs(Slot &s, const fdgpu_cfg_t &c, uint64_t tr) {
     const uint64_t want = std::max<uint64_t>(tr + tr / 4, 256 * 1024);
     HIPCHK(hipMalloc((void **)&s.d_tr, want), false);
     HIPCHK(hipHostMalloc((void **)&s.h_tr, want, hipHostMallocDefault), false);
+    HIPCHK(hipHostGetDevicePointer((void **)&s.d_trh, s.h_tr, 0), false);
     s.tr_cap = want;
   }
   return true;
@@ -421,6 +441,10 @@ fdgpu_engine_t *fdgpu_engine_open(int device, fdgpu_cfg_t const *cfg_in) {
 
 void fdgpu_engine_close(fdgpu_engine_t *e) {
   if (!e) return;
+  if (g_sp_on && g_sp_calls)
+    fprintf(stderr, "[fdgpu submit_frags_io] calls %llu frags %llu: loop %.1f us/call, enqueue %.1f us/call\n",
+            (unsigned long long)g_sp_calls.load(), (unsigned long long)g_sp_frags.load(),
+            g_sp_loop.load() / 1e3 / g_sp_calls.load(), g_sp_enq.load() / 1e3 / g_sp_calls.load());
   (void)hipSetDevice(e->device);
   if (e->compute) (void)hipStreamSynchronize(e->compute);
   for (auto &s : e->slots) { if (s.stream) (void)hipStreamSynchronize(s.stream); slot_free(s); }
@@ -771,6 +795,7 @@ uint32_t fdgpu_frag_out_cap(uint32_t sz) {
    [codes][tags][out sizes] into pinned memory. */
 int64_t fdgpu_submit_frags_io(fdgpu_engine_t *e, fdgpu_frag_io_t const *fio, uint64_t n, uint8_t *out,
                               uint64_t out_sz, uint64_t hash_seed) {
+  const uint64_t sp0 = g_sp_on ? sp_now() : 0;
   if (!e || (!fio && n) || (!out && out_sz)) { set_err("null argument"); return FDGPU_ERR_INVAL; }
   if (n > e->cfg.max_txn) { set_err("batch exceeds engine limits"); return FDGPU_ERR_INVAL; }
   std::lock_guard<std::mutex> lk(e->ring_mu);
@@ -782,11 +807,25 @@ int64_t fdgpu_submit_frags_io(fdgpu_engine_t *e, fdgpu_frag_io_t const *fio, uin
   /* results: codes (padded to 64) + 8 B tags + 2 B sizes, in the trailer buffer */
   const uint64_t cb = (n + 63) & ~63ull, res_sz = cb + n * 10;
   if (!slot_frag_bufs(*s, e->cfg, res_sz)) return FDGPU_ERR_DEVICE;
+#if FDGPU_IO_DIRECT
+  /* one upload: the frag records, then (64-B aligned) the payload addresses */
+  const uint64_t src_at = (n * sizeof(fdgpu_frag_ex_t) + 63) & ~63ull;
+  if (!s->h_io) {
+    const uint64_t m = e->cfg.max_txn + 1, bytes = m * (sizeof(fdgpu_frag_ex_t) + sizeof(uint64_t)) + 64;
+    HIPCHK(hipHostMalloc((void **)&s->h_io, bytes, hipHostMallocDefault), FDGPU_ERR_DEVICE);
+    HIPCHK(hipMalloc((void **)&s->d_io, bytes), FDGPU_ERR_DEVICE);
+  }
+  fdgpu_frag_ex_t *h_fx = (fdgpu_frag_ex_t *)s->h_io;
+  uint64_t *h_src = (uint64_t *)(s->h_io + src_at);
+#else
   if (!s->d_src) {
     const uint64_t m = e->cfg.max_txn + 1;
     HIPCHK(hipHostMalloc((void **)&s->h_src, m * sizeof(uint64_t), hipHostMallocDefault), FDGPU_ERR_DEVICE);
     HIPCHK(hipMalloc((void **)&s->d_src, m * sizeof(uint64_t)), FDGPU_ERR_DEVICE);
   }
+  fdgpu_frag_ex_t *h_fx = s->h_fx;
+  uint64_t *h_src = s->h_src;
+#endif
   /* bounds: every payload inside a registered region (16-B aligned: the
      gather reads 16-B units up to round16(sz), inside the payload's own
      64-B chunks), every out frag inside out, the packed arena within
@@ -803,14 +842,37 @@ int64_t fdgpu_submit_frags_io(fdgpu_engine_t *e, fdgpu_frag_io_t const *fio, uin
     }
     if (!rc || f.src < rc->base || f.src + q > rc->end) rc = region_of(e, (uintptr_t)f.src, q);
     if (!rc) { set_err("frag %llu: payload not inside a registered region", (unsigned long long)t); return FDGPU_ERR_INVAL; }
-    s->h_src[t] = rc->dbase + (f.src - rc->base);
-    s->h_fx[t] = fdgpu_frag_ex_t{(uint32_t)dev_off, f.sz, f.out_off, f.out_cap};
+    h_src[t] = rc->dbase + (f.src - rc->base);
+    h_fx[t] = fdgpu_frag_ex_t{(uint32_t)dev_off, f.sz, f.out_off, f.out_cap};
     dev_off += q;
     if (dev_off > e->cfg.max_arena) { set_err("frags exceed the engine's arena"); return FDGPU_ERR_INVAL; }
     bound += fdgpu_frag_sig_bound(f.sz);
   }
   if (bound > e->cfg.max_sig) { set_err("batch may exceed max_sig (%llu)", (unsigned long long)e->cfg.max_sig); return FDGPU_ERR_INVAL; }
+  const uint64_t sp1 = g_sp_on ? sp_now() : 0;
   if (!slot_ws(*s, bound)) return FDGPU_ERR_DEVICE;
+#if FDGPU_IO_DIRECT
+  /* the finish kernel writes the out frags and the results in place, over
+     the bus: no device-side out image, no read-back copies */
+  uint8_t *out_dev = out_sz ? (uint8_t *)(ro->dbase + ((uintptr_t)out - ro->base)) : nullptr;
+  if (n) {
+    HIPCHK(hipMemcpyAsync(s->d_io, s->h_io, src_at + n * sizeof(uint64_t), hipMemcpyHostToDevice, s->stream),
+           FDGPU_ERR_DEVICE);
+    const fdgpu_frag_ex_t *d_fx = (const fdgpu_frag_ex_t *)s->d_io;
+    HIPCHK(fdgpu_launch_frag_gather((const uint64_t *)(s->d_io + src_at), d_fx, (uint32_t)n, s->d_arena, s->stream),
+           FDGPU_ERR_DEVICE);
+    HIPCHK(fdgpu_launch_frag_ring(s->d_arena, d_fx, (uint32_t)n, s->d_txn_out, s->d_txn_sz, s->d_txd, s->d_cnt,
+                                  s->d_sig0, s->d_blocktot, s->d_n_sig, s->d_sigs, s->d_txns, s->stream),
+           FDGPU_ERR_DEVICE);
+    HIPCHK(fdgpu_launch_verify_sigs(s->d_arena, s->d_sigs, (uint32_t)bound, nullptr, e->d_btab, s->d_ws, s->d_sig_codes,
+                                    kflags(e), s->stream, s->d_n_sig, e->resident_blocks, e->kc_seed),
+           FDGPU_ERR_DEVICE);
+    HIPCHK(fdgpu_launch_frag_finish_io(s->d_txns, (uint32_t)n, s->d_sig_codes, s->d_txn_sz, d_fx, s->d_txn_out,
+                                       s->d_arena, hash_seed, out_dev, (int8_t *)s->d_trh, (uint64_t *)(s->d_trh + cb),
+                                       (uint16_t *)(s->d_trh + cb + n * 8), s->stream),
+           FDGPU_ERR_DEVICE);
+  }
+#else
   if (out_sz > s->out_cap_bytes) {
     HIPCHK(hipStreamSynchronize(s->stream), FDGPU_ERR_DEVICE);
     if (s->d_out) { (void)hipFree(s->d_out); s->d_out = nullptr; }
@@ -836,6 +898,7 @@ int64_t fdgpu_submit_frags_io(fdgpu_engine_t *e, fdgpu_frag_io_t const *fio, uin
     if (out_sz) HIPCHK(hipMemcpyAsync(out, s->d_out, out_sz, hipMemcpyDeviceToHost, s->stream), FDGPU_ERR_DEVICE);
     HIPCHK(hipMemcpyAsync(s->h_tr, s->d_tr, res_sz, hipMemcpyDeviceToHost, s->stream), FDGPU_ERR_DEVICE);
   }
+#endif
   ++s->flag_seq;
   if (e->flag_poll && !e->drop_flag) HIPCHK(hipStreamWriteValue32(s->stream, s->d_flag, s->flag_seq, 0), FDGPU_ERR_DEVICE);
   HIPCHK(hipEventRecord(s->done, s->stream), FDGPU_ERR_DEVICE);
@@ -848,6 +911,10 @@ int64_t fdgpu_submit_frags_io(fdgpu_engine_t *e, fdgpu_frag_io_t const *fio, uin
   s->tr_base = 0;
   s->ticket = e->next_ticket++;
   s->txn_cnt = n;
+  if (g_sp_on) {
+    const uint64_t sp2 = sp_now();
+    g_sp_loop += sp1 - sp0; g_sp_enq += sp2 - sp1; g_sp_calls++; g_sp_frags += n;
+  }
   return s->ticket;
 }
 

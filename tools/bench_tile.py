@@ -98,12 +98,16 @@ def start_producer(args, inl, arena, offs, sizes, rate, cpus, k=0):
         os.sched_setaffinity(0, keep)
 
 
-def warm(engines, inflight, out_bytes=0):
-    """One small batch through every ring slot of every engine before the
+def warm(engines, inflight, out_bytes=0, batch=64):
+    """A full-size batch through every ring slot of every engine before the
     timed region: a HIP stream's first submission creates its hardware queue
-    (milliseconds), which would otherwise land inside the run."""
+    (milliseconds), and a slot sizes its workspace (and the gather path its
+    out image) on first use to the batch it carries -- both would otherwise
+    land inside the run."""
     a, t, _ = workload.cfg1(64, seed=7)
     ps = workload.payloads(a, t)
+    ps = [ps[k % len(ps)] for k in range(batch)]
+    a, t, _ = workload.cfg1(batch, seed=7)
     pa, po, psz = workload.pack_payloads(ps)
     fx = np.zeros(len(ps), dtype=tile.FRAG_EX_DTYPE)
     fx["off"], fx["sz"] = po, psz
@@ -225,7 +229,7 @@ def run_once_mux(args, ps, arena, offs, sizes, n_sig, modes, tiles_n, batch, inf
     frag_bytes = (tile.TPU_DCACHE_MTU + 63) // 64 * 64
     engines = [fa.VerifyEngine(device if device is not None else k % args.gpus, max_txn=batch, max_sig=batch * 12,
                                max_arena=batch * frag_bytes, ring_depth=inflight) for k in range(tiles_n)]
-    warm(engines, inflight, out_bytes=batch * frag_bytes if args.gpu_parse == 2 else 0)
+    warm(engines, inflight, out_bytes=batch * frag_bytes if args.gpu_parse == 2 else 0, batch=batch)
     P = max(1, args.producers)
     inls = [tile.Link(1 << args.depth_lg, 1232) for _ in range(P)]
     vms, vers = [], []
