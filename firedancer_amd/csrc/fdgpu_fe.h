@@ -245,53 +245,6 @@ template <> struct madc0<10> {
   }
 };
 
-#if FDGPU_AB_SHASM
-/* A/B: the column's carry shift inside its asm block (madcs<N, SH>: s +=
-   sum a[i] b[i], then c = s >> SH) */
-template <int N, int SH> struct madcs;
-template <int N, int SH> struct madcs0;
-template <int SH> struct madcs<5, SH> {
-  static FDG_DEV void run(uint64_t &s, uint64_t &c, const uint32_t *a, const uint32_t *b) {
-    uint64_t cc;
-    asm("v_mad_u64_u32 %0, %2, %4, %5, %0\n" "v_mad_u64_u32 %0, %2, %6, %7, %0\n" "v_mad_u64_u32 %0, %2, %8, %9, %0\n" "v_mad_u64_u32 %0, %2, %10, %11, %0\n" "v_mad_u64_u32 %0, %2, %12, %13, %0\n" "v_lshrrev_b64 %1, %3, %0\n"
-        : "+v"(s), "=v"(c), "=&s"(cc) : "n"(SH), "v"(a[0]), "v"(b[0]), "v"(a[1]), "v"(b[1]), "v"(a[2]), "v"(b[2]), "v"(a[3]), "v"(b[3]), "v"(a[4]), "v"(b[4]));
-    (void)cc;
-  }
-};
-template <int SH> struct madcs<6, SH> {
-  static FDG_DEV void run(uint64_t &s, uint64_t &c, const uint32_t *a, const uint32_t *b) {
-    uint64_t cc;
-    asm("v_mad_u64_u32 %0, %2, %4, %5, %0\n" "v_mad_u64_u32 %0, %2, %6, %7, %0\n" "v_mad_u64_u32 %0, %2, %8, %9, %0\n" "v_mad_u64_u32 %0, %2, %10, %11, %0\n" "v_mad_u64_u32 %0, %2, %12, %13, %0\n" "v_mad_u64_u32 %0, %2, %14, %15, %0\n" "v_lshrrev_b64 %1, %3, %0\n"
-        : "+v"(s), "=v"(c), "=&s"(cc) : "n"(SH), "v"(a[0]), "v"(b[0]), "v"(a[1]), "v"(b[1]), "v"(a[2]), "v"(b[2]), "v"(a[3]), "v"(b[3]), "v"(a[4]), "v"(b[4]), "v"(a[5]), "v"(b[5]));
-    (void)cc;
-  }
-};
-template <int SH> struct madcs<10, SH> {
-  static FDG_DEV void run(uint64_t &s, uint64_t &c, const uint32_t *a, const uint32_t *b) {
-    uint64_t cc;
-    asm("v_mad_u64_u32 %0, %2, %4, %5, %0\n" "v_mad_u64_u32 %0, %2, %6, %7, %0\n" "v_mad_u64_u32 %0, %2, %8, %9, %0\n" "v_mad_u64_u32 %0, %2, %10, %11, %0\n" "v_mad_u64_u32 %0, %2, %12, %13, %0\n" "v_mad_u64_u32 %0, %2, %14, %15, %0\n" "v_mad_u64_u32 %0, %2, %16, %17, %0\n" "v_mad_u64_u32 %0, %2, %18, %19, %0\n" "v_mad_u64_u32 %0, %2, %20, %21, %0\n" "v_mad_u64_u32 %0, %2, %22, %23, %0\n" "v_lshrrev_b64 %1, %3, %0\n"
-        : "+v"(s), "=v"(c), "=&s"(cc) : "n"(SH), "v"(a[0]), "v"(b[0]), "v"(a[1]), "v"(b[1]), "v"(a[2]), "v"(b[2]), "v"(a[3]), "v"(b[3]), "v"(a[4]), "v"(b[4]), "v"(a[5]), "v"(b[5]), "v"(a[6]), "v"(b[6]), "v"(a[7]), "v"(b[7]), "v"(a[8]), "v"(b[8]), "v"(a[9]), "v"(b[9]));
-    (void)cc;
-  }
-};
-template <int SH> struct madcs0<6, SH> {
-  static FDG_DEV void run(uint64_t &s, uint64_t &c, const uint32_t *a, const uint32_t *b) {
-    uint64_t cc;
-    asm("v_mad_u64_u32 %0, %2, %4, %5, 0\n" "v_mad_u64_u32 %0, %2, %6, %7, %0\n" "v_mad_u64_u32 %0, %2, %8, %9, %0\n" "v_mad_u64_u32 %0, %2, %10, %11, %0\n" "v_mad_u64_u32 %0, %2, %12, %13, %0\n" "v_mad_u64_u32 %0, %2, %14, %15, %0\n" "v_lshrrev_b64 %1, %3, %0\n"
-        : "=&v"(s), "=v"(c), "=&s"(cc) : "n"(SH), "v"(a[0]), "v"(b[0]), "v"(a[1]), "v"(b[1]), "v"(a[2]), "v"(b[2]), "v"(a[3]), "v"(b[3]), "v"(a[4]), "v"(b[4]), "v"(a[5]), "v"(b[5]));
-    (void)cc;
-  }
-};
-template <int SH> struct madcs0<10, SH> {
-  static FDG_DEV void run(uint64_t &s, uint64_t &c, const uint32_t *a, const uint32_t *b) {
-    uint64_t cc;
-    asm("v_mad_u64_u32 %0, %2, %4, %5, 0\n" "v_mad_u64_u32 %0, %2, %6, %7, %0\n" "v_mad_u64_u32 %0, %2, %8, %9, %0\n" "v_mad_u64_u32 %0, %2, %10, %11, %0\n" "v_mad_u64_u32 %0, %2, %12, %13, %0\n" "v_mad_u64_u32 %0, %2, %14, %15, %0\n" "v_mad_u64_u32 %0, %2, %16, %17, %0\n" "v_mad_u64_u32 %0, %2, %18, %19, %0\n" "v_mad_u64_u32 %0, %2, %20, %21, %0\n" "v_mad_u64_u32 %0, %2, %22, %23, %0\n" "v_lshrrev_b64 %1, %3, %0\n"
-        : "=&v"(s), "=v"(c), "=&s"(cc) : "n"(SH), "v"(a[0]), "v"(b[0]), "v"(a[1]), "v"(b[1]), "v"(a[2]), "v"(b[2]), "v"(a[3]), "v"(b[3]), "v"(a[4]), "v"(b[4]), "v"(a[5]), "v"(b[5]), "v"(a[6]), "v"(b[6]), "v"(a[7]), "v"(b[7]), "v"(a[8]), "v"(b[8]), "v"(a[9]), "v"(b[9]));
-    (void)cc;
-  }
-};
-#endif
-
 /* Close a feed-forward product: the carry out of column 9 (weight 2^255)
    re-enters limb 0 times 19, and limb 0's excess moves to limb 1
    (carry < 2^39, so limb 1 grows by < 2^17.3). */
@@ -326,18 +279,11 @@ FDG_DEV void fe_mul(fe &h, const fe &f, const fe &g) {
       ca[i] = dbl ? f2[i] : f.v[i];
       cb[i] = wrap ? g19[j] : g.v[j];
     }
-#if FDGPU_AB_SHASM
-    if (k == 0) madcs0<10, 26>::run(s, carry, ca, cb);
-    else if (k & 1) madcs<10, 25>::run(s, carry, ca, cb);
-    else madcs<10, 26>::run(s, carry, ca, cb);
-    r[k] = (uint32_t)s & ((1u << ((k & 1) ? 25 : 26)) - 1);
-#else
     if (k == 0) madc0<10>::run(s, ca, cb);
     else madc<10>::run(s, ca, cb);
     const int bits = (k & 1) ? 25 : 26;
     r[k] = (uint32_t)s & ((1u << bits) - 1);
     carry = s >> bits;
-#endif
   }
   fe_ff_close(h, r, carry);
   FDG_SCHED_FENCE();
@@ -374,19 +320,12 @@ FDG_DEV void fe_sq_sh(fe &h, const fe &f) {
         n++;
       }
     }
-#if FDGPU_AB_SHASM
-    if (k & 1) madcs<5, 25>::run(s, carry, ca, cb);
-    else if (k == 0) madcs0<6, 26>::run(s, carry, ca, cb);
-    else madcs<6, 26>::run(s, carry, ca, cb);
-    r[k] = (uint32_t)s & ((1u << ((k & 1) ? 25 : 26)) - 1);
-#else
     if (k & 1) madc<5>::run(s, ca, cb);             /* odd columns: 5 symmetric terms, even: 6 */
     else if (k == 0) madc0<6>::run(s, ca, cb);
     else madc<6>::run(s, ca, cb);
     const int bits = (k & 1) ? 25 : 26;
     r[k] = (uint32_t)s & ((1u << bits) - 1);
     carry = s >> bits;
-#endif
   }
   fe_ff_close(h, r, carry);
   FDG_SCHED_FENCE();

@@ -295,13 +295,7 @@ FDG_DEV void atab_build(uint32_t *wsl, const ge_p3 &An) {
 #pragma unroll 1
   for (uint32_t e = 3; e < FDGPU_ATAB_ENTRIES; e++) {
     if (e & 1u) {
-#if FDGPU_AB_TBLD
-      uint32_t q[40];
-      atab_load(q, wsl, 1);                     /* entry 1 in one batch of loads: one memory latency */
-      ge_add_cached_regs(t, P, q, false);
-#else
       ge_add_cached_ld(t, P, ld1, false);
-#endif
     } else {
       uint32_t q[40];
       atab_load(q, wsl, (int)(e >> 1));
@@ -471,11 +465,7 @@ FDG_DEV void hs_chain(ge_p1p1 &t, uint32_t (&ud)[5], uint32_t (&vd)[5], bool u_n
     shl4_5(ud); shl4_5(vd);
     stage_entry(st_a, ta, du);
     stage_entry(st_r, tr, dv);
-#if FDGPU_AB_UNROLL
-#pragma unroll
-#else
 #pragma unroll 1
-#endif
     for (int r = 0; r < 4; r++) {
       ge_dbl(t, acc2);
       ge_p1p1_to_p2(acc2, t);
