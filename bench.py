@@ -284,11 +284,11 @@ def sync_latency(arena, txns, calls=1000, threads=64):
                          "trip per call; concurrent: calls coalesced into shared batches (group commit)"}
 
 
-TILE_RUNS = (  # name, verify tiles, quic links (producers), offered txn/s (0: backlog at producer speed)
-    ("mux1_backlog", 1, 1, 0.0),
-    ("mux1_paced_12M", 1, 1, 12e6),
-    ("mux2_backlog", 2, 2, 0.0),
-    ("mux2_paced_16M", 2, 2, 16e6),
+TILE_RUNS = (  # name, verify tiles, quic links (producers), offered txn/s (-1: prefilled links, the tiles' capacity)
+    ("mux1_capacity", 1, 1, -1.0),
+    ("mux1_paced_16M", 1, 1, 16e6),
+    ("mux2_capacity", 2, 2, -1.0),
+    ("mux2_paced_24M", 2, 2, 24e6),
 )
 
 
@@ -296,7 +296,7 @@ def tile_args(prods, rate):
     """bench_tile.run_once_mux's options for one cfg5 run (tests/test_bench_cli.py
     checks it carries every option run_once_mux and start_producer read)"""
     import types
-    return types.SimpleNamespace(gpus=1, gpu_parse=2, producers=prods, depth_lg=21 if not rate else 19,
+    return types.SimpleNamespace(gpus=1, gpu_parse=2, producers=prods, depth_lg=21 if rate <= 0 else 19,
                                  wait_us=200.0, pin=1, multi=0, cpu_offset=0)
 
 
@@ -329,11 +329,15 @@ def tile_lines(device, arena, txns, modes, cpus, runs=TILE_RUNS):
         out[f"tile_{name}_batch_latency_ms_p50_p99"] = [lat["p50"], lat["p99"]]
         out[f"tile_{name}_overruns"] = res["counters"]["overrun"]
         out[f"tile_{name}_published_ok"] = res["counters"]["published"] == res["expected_published"]
+    out["tile_mux2_vs_mux1_capacity"] = round(out["tile_mux2_capacity_txns_per_s"] /
+                                              out["tile_mux1_capacity_txns_per_s"], 3)
     out["tile_config"] = ("fdgpu_vmux on fdt_mux_run (the reference's mux-callback verify tile), payload gather, "
-                          "fd_txn_parse, verify, dedup tag and out-frag assembly on the GPU; muxT: T verify tiles reading T quic->verify links (one producer thread each), "
-                          "one engine per tile on this GPU, cfg1 frags, 16384-txn batches, 4 in flight; backlog: "
-                          "producers publish as fast as they can into 2^21-deep links; paced_R: R txn/s offered "
-                          "in total into 2^19-deep links")
+                          "fd_txn_parse, verify, dedup tag and out-frag assembly on the GPU; muxT: T verify tiles "
+                          "reading T quic->verify links (one producer thread each), one engine per tile on this GPU, "
+                          "cfg1 frags, 16384-txn batches, 4 in flight; capacity: "
+                          "every frag published into 2^21-deep links before the tiles start, timed from tile start "
+                          "to the last outcome; paced_R: R txn/s offered in total into 2^19-deep links while the "
+                          "tiles run")
     return out
 
 
@@ -561,7 +565,7 @@ def main():
             extras.update(sync_latency(arena, txns))
         if args.tile:
             tl = tile_lines(device, arena, txns, modes, cpus)
-            tl["tile_mux1_backlog_txns_per_s_node"] = round(dist.sum(tl["tile_mux1_backlog_txns_per_s"]), 1)
+            tl["tile_mux1_capacity_txns_per_s_node"] = round(dist.sum(tl["tile_mux1_capacity_txns_per_s"]), 1)
             tl["tile_published_ok_all_ranks"] = dist.sum(
                 1 if all(v for k, v in tl.items() if k.endswith("_published_ok")) else 0) == dist.world
             extras.update(tl)

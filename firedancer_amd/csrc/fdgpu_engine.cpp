@@ -83,6 +83,7 @@ struct Slot {
   uint32_t *h_flag = nullptr, *d_flag = nullptr;
   uint32_t flag_seq = 0;
   uint32_t polls = 0;         /* non-blocking polls of the current batch (stream error checks) */
+  uint64_t last_query = 0;    /* when a poll last asked the runtime (ns) */
   /* frag batches (fdgpu_submit_frags): GPU-side parse buffers, allocated on
      the slot's first frag batch; the trailer buffers grow to the batches */
   bool frag = false;          /* the batch in flight is a frag batch */
@@ -674,11 +675,16 @@ static int poll_slot(fdgpu_engine_t *e, int64_t ticket, int8_t *txn_codes, int b
     lk.lock();
   } else if (e->flag_poll) {
     /* the stream wrote flag_seq after the codes' read-back completed.  A
-       stream that failed never writes it, so every 64th unanswered poll asks
-       the runtime: an error ends the wait (the tile stops instead of polling
-       forever), a completed event means the batch is done. */
+       stream that failed never writes it, so an unanswered poll asks the
+       runtime now and then -- every 256th poll once 1 ms has passed since the
+       last question (runtime queries from several tile threads contend):
+       an error ends the wait (the tile stops instead of polling forever), a
+       completed event means the batch is done. */
     if (__atomic_load_n(s->h_flag, __ATOMIC_ACQUIRE) != s->flag_seq) {
-      if ((++s->polls & 63u) != 0) return FDGPU_PENDING;
+      if ((++s->polls & 255u) != 0) return FDGPU_PENDING;
+      const uint64_t now = sp_now();
+      if (now - s->last_query < 1000000ull) return FDGPU_PENDING;
+      s->last_query = now;
       HIPCHK(hipSetDevice(e->device), FDGPU_ERR_DEVICE);
       const hipError_t q = hipEventQuery(s->done);
       if (q == hipErrorNotReady) return FDGPU_PENDING;

@@ -32,4 +32,5 @@ def test_tile_args_cover_run_once_mux():
 
 def test_tile_runs_shape():
     for name, tiles_n, prods, rate in bench.TILE_RUNS:
-        assert tiles_n >= 1 and prods >= 1 and rate >= 0 and name
+        assert tiles_n >= 1 and prods >= 1 and (rate > 0 or rate == -1.0) and name
+        assert bench.tile_args(prods, rate).depth_lg == (21 if rate < 0 else 19)   # a prefill fits its links

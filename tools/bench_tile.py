@@ -242,8 +242,15 @@ def run_once_mux(args, ps, arena, offs, sizes, n_sig, modes, tiles_n, batch, inf
         vers.append((ver, outl))
     cpus = cpus or workload.physical_cpus()[getattr(args, "cpu_offset", 0):] or workload.physical_cpus()
     # tile k's thread is pinned to cpus[P + k] (VerifyMuxTile.start inherits the caller's mask)
+    # rate < 0: prefill -- every frag is published before the tiles start, so
+    # the run measures the tiles' own drain rate (capacity), not the producers'
+    prefill = rate < 0
     start = time.perf_counter()
-    prods = [start_producer(args, inls[j], arena, offs[j::P], sizes[j::P], rate / P, cpus, j) for j in range(P)]
+    prods = [start_producer(args, inls[j], arena, offs[j::P], sizes[j::P], 0.0 if prefill else rate / P, cpus, j)
+             for j in range(P)]
+    if prefill:
+        joined = [pr.join() for pr in prods]
+        start = time.perf_counter()
     keep = os.sched_getaffinity(0)
     for k, vm in enumerate(vms):
         if args.pin:
@@ -257,7 +264,8 @@ def run_once_mux(args, ps, arena, offs, sizes, n_sig, modes, tiles_n, batch, inf
     wall = time.perf_counter() - start
     for vm in vms:
         vm.stop()
-    joined = [pr.join() for pr in prods]
+    if not prefill:
+        joined = [pr.join() for pr in prods]
     n_pub, prod_s = sum(j[0] for j in joined), max(j[1] for j in joined)
     stats = [vm.stats() for vm in vms]
     mstats = [vm.mux_stats() for vm in vms]
@@ -274,8 +282,8 @@ def run_once_mux(args, ps, arena, offs, sizes, n_sig, modes, tiles_n, batch, inf
         "sigs_per_s": round(n_sig / wall, 1),
         "wall_s": round(wall, 4), "producer_s": round(prod_s, 4), "producer_published": int(n_pub),
         "gpus": args.gpus, "tiles": tiles_n, "batch_txn_max": batch, "inflight": inflight,
-        "rate_target": rate, "workload": "cfg3 (1-12 sigs/txn, payload <= 1232 B, 10% corrupted)"
-        if getattr(args, "multi", 0) else "cfg1 (1 sig, msg U[180,220] B, 10% corrupted)",
+        "rate_target": rate, "prefill": prefill,
+        "workload": "cfg3 (1-12 sigs/txn, payload <= 1232 B, 10% corrupted)" if getattr(args, "multi", 0) else "cfg1 (1 sig, msg U[180,220] B, 10% corrupted)",
         "txns": len(ps), "sigs": n_sig, "batch_wait_us": args.wait_us, "cpus": cpus[:P + tiles_n],
         "batch_latency_ms": {"p50": round(float(np.percentile(lat, 50)), 3) if len(lat) else None,
                              "p99": round(float(np.percentile(lat, 99)), 3) if len(lat) else None,
