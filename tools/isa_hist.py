@@ -72,7 +72,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("asm")
     ap.add_argument("--kernel", required=True)
-    ap.add_argument("--weights", default="", help="LINE:TRIPS,... for the loops starting at LINE")
+    ap.add_argument("--weights", default="",
+                    help="LINE:TRIPS or FIRST-LAST:TRIPS,... for the loops starting at LINE (spanning FIRST-LAST)")
     ap.add_argument("--json", default="")
     args = ap.parse_args()
     body = parse(args.asm, args.kernel)
@@ -86,7 +87,10 @@ def main():
             loops.append((label_pos[tgt], k))
     total = collections.Counter(klass(t.split()[0]) for _, kind, t in body if kind == "insn")
     print(f"kernel {args.kernel}: {sum(total.values())} instructions (static)")
-    weights = {int(a): float(b) for a, b in (w.split(":") for w in args.weights.split(",") if w)}
+    weights = {}
+    for w in (w for w in args.weights.split(",") if w):
+        key, trips = w.split(":")
+        weights[tuple(int(x) for x in key.split("-")) if "-" in key else int(key)] = float(trips)
     weighted = collections.Counter()
     report = {"static_total": dict(total), "loops": []}
     for a, b in loops:
@@ -98,9 +102,10 @@ def main():
               + ", ".join(f"{k} {v}" for k, v in h.most_common(8)))
         report["loops"].append({"first_line": first, "last_line": body[b][0], "insns": len(ins),
                                 "inner_loops": nested, "classes": dict(h)})
-        if first in weights:
+        wt = weights.get((first, body[b][0]), weights.get(first))
+        if wt:
             for k, v in h.items():
-                weighted[k] += v * weights[first]
+                weighted[k] += v * wt
     if weighted:
         tot = sum(weighted.values())
         print(f"trip-weighted total over the named loops: {tot:.0f} instructions per lane")
