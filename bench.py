@@ -26,6 +26,15 @@ import time
 import numpy as np
 
 REPO = os.path.dirname(os.path.abspath(__file__))
+
+# HIP hardware queues of this process, set before the runtime starts: every
+# ring slot, device batch and tile engine owns a stream, and HIP maps streams
+# onto GPU_MAX_HW_QUEUES hardware queues (4 by default); two streams on one
+# queue serialise, so with the cfg5 tile lines' two engines x four slots
+# beside the headline engine the tiles' batches would queue behind each other
+# (profiles/r03/hwq_*.jsonl).  16 is HIP's supported range.
+HW_QUEUES = 16
+os.environ["GPU_MAX_HW_QUEUES"] = str(HW_QUEUES)
 sys.path.insert(0, REPO)
 
 # Algorithmic INT32 multiply-accumulates per signature:

@@ -20,6 +20,15 @@ import numpy as np
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, REPO)
+# HIP hardware queues (see bench.py HW_QUEUES); --hw-queues overrides, 0 keeps the environment's
+for i, a in enumerate(sys.argv):
+    if a.startswith("--hw-queues"):
+        v = a.split("=", 1)[1] if "=" in a else sys.argv[i + 1]
+        if int(v):
+            os.environ["GPU_MAX_HW_QUEUES"] = v
+        break
+else:
+    os.environ["GPU_MAX_HW_QUEUES"] = "16"
 
 import firedancer_amd as fa  # noqa: E402
 from firedancer_amd import tile, workload  # noqa: E402
@@ -53,6 +62,8 @@ def main():
     ap.add_argument("--cpu-offset", type=int, default=0,
                     help="skip this many of workload.physical_cpus() before pinning (CPU 0 takes interrupts)")
     ap.add_argument("--reps", type=int, default=1, help="repeat every run of the sweep")
+    ap.add_argument("--hw-queues", type=int, default=16,
+                    help="GPU_MAX_HW_QUEUES for this process (applied before HIP starts; 0: the environment's)")
     ap.add_argument("--out", default="")
     ap.add_argument("--sweep", default="", help="';'-separated runs of 'tiles,batch,inflight,rate' over the same txns")
     args = ap.parse_args()
