@@ -102,6 +102,9 @@ int fdt_mux_run(const fdt_mux_cfg_t *cfg, const fdt_mux_callbacks_t *cb, void *c
     const uint64_t i = in_rr;
     in_rr = in_rr + 1 == in_cnt ? 0 : in_rr + 1;
     const fdt_frag_meta_t *line = cfg->in_mcache[i] + (in_seq[i] & (cfg->in_depth[i] - 1));
+    /* the line 16 frags ahead: a tile that reads every frag's line (round
+       robin over tiles, fd_verify.c:46) streams the whole mcache */
+    __builtin_prefetch(cfg->in_mcache[i] + ((in_seq[i] + 16) & (cfg->in_depth[i] - 1)));
     const uint64_t seq_found = ld_acq(&line->seq);
     const int64_t diff = (int64_t)(in_seq[i] - seq_found);
     if (diff) {                                     /* caught up, or overrun (fd_mux.c:595-609) */
