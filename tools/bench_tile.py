@@ -256,8 +256,18 @@ def run_once_mux(args, ps, arena, offs, sizes, n_sig, modes, tiles_n, batch, inf
     # rate < 0: prefill -- every frag is published before the tiles start, so
     # the run measures the tiles' own drain rate (capacity), not the producers'
     prefill = rate < 0
+    # a prefilled run gives every link the whole stream (link j starting a
+    # j/P-th of the way in, so a txn's copies are far apart in every tile's
+    # tcache window): P x N frags, long enough that the pipeline's fill and
+    # drain do not dominate the drain time of several tiles
+    if prefill:
+        n = len(offs)
+        feeds = [(np.roll(offs, -(j * n // P)), np.roll(sizes, -(j * n // P))) for j in range(P)]
+    else:
+        feeds = [(offs[j::P], sizes[j::P]) for j in range(P)]
+    n_total = sum(len(f[0]) for f in feeds)
     start = time.perf_counter()
-    prods = [start_producer(args, inls[j], arena, offs[j::P], sizes[j::P], 0.0 if prefill else rate / P, cpus, j)
+    prods = [start_producer(args, inls[j], arena, feeds[j][0], feeds[j][1], 0.0 if prefill else rate / P, cpus, j)
              for j in range(P)]
     if prefill:
         joined = [pr.join() for pr in prods]
@@ -268,7 +278,7 @@ def run_once_mux(args, ps, arena, offs, sizes, n_sig, modes, tiles_n, batch, inf
             os.sched_setaffinity(0, {cpus[(P + k) % len(cpus)]})
         vm.start()
     os.sched_setaffinity(0, keep)
-    while any(vm.final_cnt() < len(ps) for vm in vms):
+    while any(vm.final_cnt() < n_total for vm in vms):
         if time.perf_counter() - start > 300:
             raise SystemExit("verify mux tiles timed out")
         time.sleep(0.0002)
@@ -289,18 +299,18 @@ def run_once_mux(args, ps, arena, offs, sizes, n_sig, modes, tiles_n, batch, inf
                 + {2: "; the GPU reads the payloads in the in dcache, parses, verifies and writes the out frags",
                    1: "; fd_txn_parse on the GPU", 0: "; fd_txn_parse on the tile core"}[int(args.gpu_parse)],
         "producers": P,
-        "txns_per_s": round(len(ps) / wall, 1),
-        "sigs_per_s": round(n_sig / wall, 1),
+        "txns_per_s": round(n_total / wall, 1),
+        "sigs_per_s": round(n_sig * n_total / len(ps) / wall, 1),
         "wall_s": round(wall, 4), "producer_s": round(prod_s, 4), "producer_published": int(n_pub),
         "gpus": args.gpus, "tiles": tiles_n, "batch_txn_max": batch, "inflight": inflight,
         "rate_target": rate, "prefill": prefill,
         "workload": "cfg3 (1-12 sigs/txn, payload <= 1232 B, 10% corrupted)" if getattr(args, "multi", 0) else "cfg1 (1 sig, msg U[180,220] B, 10% corrupted)",
-        "txns": len(ps), "sigs": n_sig, "batch_wait_us": args.wait_us, "cpus": cpus[:P + tiles_n],
+        "txns": n_total, "sigs": n_sig * n_total // len(ps), "batch_wait_us": args.wait_us, "cpus": cpus[:P + tiles_n],
         "batch_latency_ms": {"p50": round(float(np.percentile(lat, 50)), 3) if len(lat) else None,
                              "p99": round(float(np.percentile(lat, 99)), 3) if len(lat) else None,
                              "n": int(len(lat))},
         "counters": agg, "mux": {k: int(sum(m[k] for m in mstats)) for k in mstats[0]},
-        "expected_published": int((modes == 0).sum()),
+        "expected_published": int((modes == 0).sum()) * (n_total // len(ps)),
     }
     for vm in vms:
         vm.close()
