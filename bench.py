@@ -175,6 +175,17 @@ def timed_batch(eng, a, t):
     return (time.perf_counter() - t0) * 1e3, (t1 - t0) * 1e3
 
 
+def submit_parts(k):
+    """p50/p99/max (ms) of the engine's per-call submit parts over its last k
+    fdgpu_submit calls"""
+    from firedancer_amd import _lib
+    out = np.zeros(3 * k, dtype=np.uint64)
+    n = int(_lib.lib().fdgpu_debug_submit_times(out.ctypes.data, k))
+    t = out[:3 * n].reshape(n, 3) / 1e6
+    return {name: [round(float(np.percentile(t[:, j], q)), 3) for q in (50, 99)] + [round(float(t[:, j].max()), 3)]
+            for j, name in enumerate(("stage", "expand", "enqueue"))} if n else {}
+
+
 def latency_and_pcie(eng, arena, txns, batch, nbatches, pin_cpu=None):
     """p50/p99 submit->codes-on-host latency of `batch`-txn batches (one in
     flight at a time), then pipelined throughput with every ring slot busy
@@ -203,6 +214,7 @@ def latency_and_pcie(eng, arena, txns, batch, nbatches, pin_cpu=None):
     gc.disable()
     lat = np.array([timed_batch(eng, *views[i % len(views)]) for i in range(nbatches)])
     gc.enable()
+    parts = submit_parts(nbatches)
     def pipelined(vs):
         """every ring slot busy: submit -> poll over the batches, sigs/s"""
         sigs = 0
@@ -233,6 +245,7 @@ def latency_and_pcie(eng, arena, txns, batch, nbatches, pin_cpu=None):
     gc.disable()
     lat_reg = np.array([timed_batch(eng, *reg_views[i % len(reg_views)]) for i in range(nbatches)])
     gc.enable()
+    parts_reg = submit_parts(nbatches)
     eng.host_unregister(arena)
     os.sched_setaffinity(0, keep)
 
@@ -248,6 +261,9 @@ def latency_and_pcie(eng, arena, txns, batch, nbatches, pin_cpu=None):
                                  "registered_submit_p50_p99": [pct(lat_reg[:, 1], 50), pct(lat_reg[:, 1], 99)],
                                  "registered_rest_p50_p99": [pct(lat_reg[:, 0] - lat_reg[:, 1], 50),
                                                              pct(lat_reg[:, 0] - lat_reg[:, 1], 99)]},
+            # inside submit, from the engine's own clock (fdgpu_debug_submit_times): staging copy,
+            # descriptor expansion, enqueue of copies and launches -- p50 / p99 / max, ms
+            "submit_parts_ms": {"staged": parts, "registered": parts_reg},
             "pcie_inclusive_sigs_per_s_per_gpu": round(pcie, 1),
             "pcie_inclusive_registered_sigs_per_s_per_gpu": round(pcie_reg, 1)}
 

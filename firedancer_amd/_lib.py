@@ -116,6 +116,8 @@ def lib():
     L.fdgpu_submit_frags_io.restype = c.c_int64
     L.fdgpu_poll_frags_io.argtypes = [vp, c.c_int64, vp, vp, vp, c.c_int]
     L.fdgpu_poll_frags_io.restype = c.c_int
+    L.fdgpu_debug_submit_times.argtypes = [vp, c.c_uint64]
+    L.fdgpu_debug_submit_times.restype = c.c_uint64
     L.fdgpu_frag_out_cap.argtypes = [c.c_uint32]
     L.fdgpu_frag_out_cap.restype = c.c_uint32
     L.fdgpu_ed25519_verify.argtypes = [u8p, c.c_uint64, u8p, u8p]

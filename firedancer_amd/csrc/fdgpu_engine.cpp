@@ -59,6 +59,11 @@ namespace {
 std::atomic<uint64_t> g_sp_loop{0}, g_sp_enq{0}, g_sp_calls{0}, g_sp_frags{0};
 inline uint64_t sp_now() { timespec ts; clock_gettime(CLOCK_MONOTONIC, &ts); return ts.tv_sec * 1000000000ull + ts.tv_nsec; }
 const bool g_sp_on = getenv("FDGPU_SUBMIT_PROF") && getenv("FDGPU_SUBMIT_PROF")[0] == '1';
+/* the last FDGPU_ST_RING fdgpu_submit calls of the process: {staging copy,
+   descriptor expansion, enqueue} ns (fdgpu_debug_submit_times) */
+constexpr uint64_t FDGPU_ST_RING = 8192;
+uint64_t g_st[FDGPU_ST_RING][3];
+std::atomic<uint64_t> g_st_n{0};
 }
 
 namespace {
@@ -492,10 +497,19 @@ static int enqueue_verify(fdgpu_engine_t *e, const uint8_t *d_arena, const fdgpu
    straight from there (no staging copy); its bytes must stay unchanged until
    the batch is polled. */
 static int64_t submit_slot(fdgpu_engine_t *e, Slot *s, uint64_t arena_sz, fdgpu_txn_t const *txns, uint64_t txn_cnt,
-                           uint64_t uploaded = 0, const uint8_t *src = nullptr) {
+                           uint64_t uploaded = 0, const uint8_t *src = nullptr, uint64_t t_stage = 0) {
   uint32_t *perm = bucket(e) ? s->h_perm : nullptr;
+  const uint64_t t0 = sp_now();
   const int64_t ns = expand(arena_sz, txns, txn_cnt, e->cfg.max_sig, s->h_sigs, s->h_txns, perm);
   if (ns < 0) return FDGPU_ERR_INVAL;
+  const uint64_t t1 = sp_now();
+  struct Rec {                                  /* the call's times into the ring, on every return */
+    uint64_t st, t0, t1;
+    ~Rec() {
+      const uint64_t k = g_st_n.fetch_add(1, std::memory_order_relaxed) % FDGPU_ST_RING;
+      g_st[k][0] = st; g_st[k][1] = t1 - t0; g_st[k][2] = sp_now() - t1;
+    }
+  } rec{t_stage, t0, t1};
   if (!slot_ws(*s, (uint64_t)ns)) return FDGPU_ERR_DEVICE;
   if (src) {
     if (arena_sz) HIPCHK(hipMemcpyAsync(s->d_arena, src, arena_sz, hipMemcpyHostToDevice, s->stream), FDGPU_ERR_DEVICE);
@@ -634,9 +648,20 @@ int64_t fdgpu_submit(fdgpu_engine_t *e, uint8_t const *arena, uint64_t arena_sz,
   if (!s) { set_err("all ring slots hold unpolled batches"); return FDGPU_ERR_FULL; }
   if (region_covers(e, arena, arena_sz)) return submit_slot(e, s, arena_sz, txns, txn_cnt, 0, arena);
   /* the slot's previous batch was polled, so its copies are complete */
+  const uint64_t ts = sp_now();
   const uint64_t up = stage_arena(e, s, arena, arena_sz);
   if (up == UINT64_MAX) return FDGPU_ERR_DEVICE;
-  return submit_slot(e, s, arena_sz, txns, txn_cnt, up);
+  return submit_slot(e, s, arena_sz, txns, txn_cnt, up, nullptr, sp_now() - ts);
+}
+
+uint64_t fdgpu_debug_submit_times(uint64_t *out, uint64_t max) {
+  const uint64_t n = std::min<uint64_t>(g_st_n.load(), FDGPU_ST_RING), m = std::min(n, max);
+  const uint64_t end = g_st_n.load();
+  for (uint64_t i = 0; i < m; i++) {
+    const uint64_t k = (end - m + i) % FDGPU_ST_RING;
+    out[3 * i] = g_st[k][0]; out[3 * i + 1] = g_st[k][1]; out[3 * i + 2] = g_st[k][2];
+  }
+  return m;
 }
 
 uint8_t *fdgpu_stage_acquire(fdgpu_engine_t *e, uint64_t *cap) {

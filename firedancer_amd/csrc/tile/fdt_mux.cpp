@@ -234,6 +234,9 @@ struct fdgpu_vmux {
   }
   std::vector<uint16_t> cap_of;          /* gather: out-frag room by payload size (fdt_frag_fp_bound) */
   uint64_t out_chunk = 0;                 /* write cursor */
+  bool room_ok = false;                   /* room() held at the cursor (the live region only shrinks
+                                             until the cursor moves, so a yes stays a yes till then) */
+  uint64_t rr_mask = 0;                   /* round_robin_cnt - 1 when a power of two, else 0 */
   uint64_t cur_sz = 0;                    /* the frag between during_frag and after_frag */
   bool cur_ok = false;
   uint64_t cur_fp = 0, cur_sc = 0, cur_tag = 0;   /* gpu_parse: its peeked footprint, signature count, tag */
@@ -447,7 +450,8 @@ void vm_before_frag(void *ctx, uint64_t in_idx, uint64_t seq, uint64_t sig, int 
   (void)in_idx; (void)sig;
   auto *t = (fdgpu_vmux *)ctx;
   t->st.in_frags++;
-  if (t->cfg.round_robin_cnt > 1 && seq % t->cfg.round_robin_cnt != t->cfg.round_robin_idx) {
+  const uint64_t cnt = t->cfg.round_robin_cnt;
+  if (cnt > 1 && (t->rr_mask ? (seq & t->rr_mask) : seq % cnt) != t->cfg.round_robin_idx) {
     *opt_filter = 1;
     t->st.filtered_rr++;
     t->log(seq, FDGPU_VTILE_LOG_FILTERED);
@@ -509,6 +513,7 @@ void vm_after_frag(void *ctx, uint64_t in_idx, uint64_t seq, uint64_t *opt_sig, 
     b.end_off = off + cap;
     b.sig_cnt += fdt_frag_sig_bound(payload_sz);       /* (stats.sigs stays 0: the tile never sees the count) */
     t->out_chunk = fdt_dcache_compact_next(t->out_chunk, cap, t->cfg.out_chunk0, t->cfg.out_wmark);
+    t->room_ok = false;
     if (t->out_chunk <= b.first_chunk || b.items.size() >= t->cfg.batch_txn_max ||
         b.sig_cnt + 16 > t->cfg.batch_sig_max || b.end_off + FRAG_CHUNKS * FDT_CHUNK_SZ > t->cfg.batch_bytes_max)
       b.closed = true;
@@ -532,6 +537,7 @@ void vm_after_frag(void *ctx, uint64_t in_idx, uint64_t seq, uint64_t *opt_sig, 
     b.sig_cnt += fdt_frag_sig_bound(payload_sz);
     if (sc >= 1 && sc <= 16) t->st.sigs += sc;
     t->out_chunk = fdt_dcache_compact_next(t->out_chunk, toff + fp + 2, t->cfg.out_chunk0, t->cfg.out_wmark);
+    t->room_ok = false;
     if (t->out_chunk <= b.first_chunk || b.items.size() >= t->cfg.batch_txn_max ||
         b.sig_cnt + 16 > t->cfg.batch_sig_max || b.end_off + FRAG_CHUNKS * FDT_CHUNK_SZ > t->cfg.batch_bytes_max)
       b.closed = true;
@@ -565,6 +571,7 @@ void vm_after_frag(void *ctx, uint64_t in_idx, uint64_t seq, uint64_t *opt_sig, 
   b.end_off = off + new_sz;
   if (tt->signature_cnt <= 16) { b.sig_cnt += tt->signature_cnt; t->st.sigs += tt->signature_cnt; }
   t->out_chunk = fdt_dcache_compact_next(t->out_chunk, new_sz, t->cfg.out_chunk0, t->cfg.out_wmark);
+  t->room_ok = false;
   /* the arena must stay one contiguous run of chunks: a wrapped cursor closes it */
   if (t->out_chunk <= b.first_chunk || b.items.size() >= t->cfg.batch_txn_max ||
       b.sig_cnt + 16 > t->cfg.batch_sig_max || b.end_off + FRAG_CHUNKS * FDT_CHUNK_SZ > t->cfg.batch_bytes_max)
@@ -584,7 +591,7 @@ void vm_after_credit(void *ctx, fdt_mux_context_t *mux, int *opt_poll_in) {
   if (due || stuck || (!t->inflight.empty() && t->inflight.front()->done)) t->resolve(mux, opt_poll_in);
   if (due || stuck) t->submit();
   if (!*opt_poll_in || t->error || !t->can_take()) { *opt_poll_in = 0; return; }
-  if (!t->room(mux)) { *opt_poll_in = 0; t->st.backpressure++; }
+  if (!t->room_ok && !(t->room_ok = t->room(mux))) { *opt_poll_in = 0; t->st.backpressure++; }
 }
 
 }  // namespace
@@ -639,6 +646,7 @@ fdgpu_vmux_t *fdgpu_vmux_new(const fdgpu_vmux_cfg_t *cfg, fdgpu_verifier_t ver) 
   fdt_tagring_init(&t->ring, c.tcache_depth);
   t->ver = ver;
   t->out_chunk = c.out_chunk0;
+  t->rr_mask = (c.round_robin_cnt & (c.round_robin_cnt - 1)) == 0 ? c.round_robin_cnt - 1 : 0;
   uint64_t n = 1;
   while (n < c.cr_max) n <<= 1;
   t->pub_chunk.assign(n, 0);

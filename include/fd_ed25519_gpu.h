@@ -12,8 +12,9 @@
                                             (impl fd_ed25519_user.c:312-322)
        Served by the GPU engine (device 0, opened on first use); results
        are bit-identical to the reference's AVX-512 build.
-       LATENCY: each call is one GPU round trip, about 1 ms (the lifetime of
-       the verify kernel's one wave; bench.py `sync_call_latency_*`), against
+       LATENCY: each call is one GPU round trip, ~0.7 ms (measured p50/p99
+       690/710 us on MI355X, bench.py `sync_call_latency_*`: the verify
+       kernel's one-wave lifetime plus launches and read-back), against
        ~33 us for the reference's CPU verify.  Concurrent callers are
        coalesced into one batch per round trip (group commit), so throughput
        grows with the number of calling threads.  Latency-bound callers
@@ -332,6 +333,12 @@ int fdgpu_engine_info( fdgpu_engine_t * e, uint32_t * grid_blocks, uint32_t * bl
 char const * fdgpu_kernel_path( void );
 
 /* --------------------------------------------------------- diagnostics */
+
+/* Where the host time of the process's last fdgpu_submit calls went (up to
+   8192, oldest first): per call {staging copy, descriptor expansion, the
+   rest (copies and launches enqueued)} in ns -> out[3 i .. 3 i + 2].
+   Returns the number of calls written. */
+uint64_t fdgpu_debug_submit_times( uint64_t * out, uint64_t max );
 /* Used by the parity tests to check each stage of the path on the GPU in
    isolation.  Host pointers; synchronous.  Return FDGPU_OK or < 0. */
 
