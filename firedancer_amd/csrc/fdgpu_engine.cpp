@@ -34,9 +34,6 @@
 
 #define FDT_TXN_MAX_SZ_BYTES 852u   /* FD_TXN_MAX_SZ (fd_txn.h:98): one parsed fd_txn_t record */
 #define FDT_TXN_MTU_BYTES 1232u     /* FD_TXN_MTU (fd_txn.h:103) */
-#ifndef FDGPU_IO_DIRECT
-#define FDGPU_IO_DIRECT 1           /* gathered batches write out frags and results in place (else: D2H copies) */
-#endif
 
 namespace {
 
@@ -103,10 +100,8 @@ struct Slot {
      addresses, and the out image the finish kernel assembles (grown on
      demand); the read-back is [codes][tags][out sizes] in h_tr */
   bool io = false;
-  uint64_t *h_src = nullptr, *d_src = nullptr;
-  uint8_t *d_out = nullptr;
-  uint64_t out_cap_bytes = 0;
-  uint8_t *h_io = nullptr, *d_io = nullptr;   /* direct: [frag records][payload addresses], one upload */
+  uint8_t *h_io = nullptr, *d_ioh = nullptr;  /* pinned [frag records][payload addresses]; its device view */
+  fdgpu_frag_ex_t *d_fxio = nullptr;          /* the records, kept on the device by the gather */
   uint8_t *d_trh = nullptr;                   /* h_tr's device-side address (results written in place) */
 };
 
@@ -162,12 +157,9 @@ void slot_free(Slot &s) {
   if (s.h_flag) (void)hipHostFree(s.h_flag);
   if (s.h_fx) (void)hipHostFree(s.h_fx);
   if (s.h_tr) (void)hipHostFree(s.h_tr);
-  if (s.h_src) (void)hipHostFree(s.h_src);
   if (s.h_io) (void)hipHostFree(s.h_io);
-  if (s.d_io) (void)hipFree(s.d_io);
   for (void *p : {(void *)s.d_fx, (void *)s.d_txn_out, (void *)s.d_txn_sz, (void *)s.d_txd, (void *)s.d_cnt,
-                  (void *)s.d_sig0, (void *)s.d_blocktot, (void *)s.d_n_sig, (void *)s.d_tr, (void *)s.d_src,
-                  (void *)s.d_out})
+                  (void *)s.d_sig0, (void *)s.d_blocktot, (void *)s.d_n_sig, (void *)s.d_tr, (void *)s.d_fxio})
     if (p) (void)hipFree(p);
   s = Slot{};
 }
@@ -820,10 +812,10 @@ uint32_t fdgpu_frag_out_cap(uint32_t sz) {
 
 /* Gathered frag batches (the header's fdgpu_submit_frags_io): the device
    reads each payload from its registered host region (the in dcache) into
-   the slot arena, then parse -> scan -> expand -> verify -> finish (codes,
-   tags, out frags assembled in the slot's out image) on the slot's stream,
-   and two read-backs: the out image into the registered out region, the
-   [codes][tags][out sizes] into pinned memory. */
+   the slot arena, then parse -> scan -> expand -> verify -> finish on the
+   slot's stream; the finish kernel writes the out frags into the registered
+   out region and [codes][tags][out sizes] into the slot's pinned results,
+   both in place, and stores the completion word.  No copies are queued. */
 int64_t fdgpu_submit_frags_io(fdgpu_engine_t *e, fdgpu_frag_io_t const *fio, uint64_t n, uint8_t *out,
                               uint64_t out_sz, uint64_t hash_seed) {
   const uint64_t sp0 = g_sp_on ? sp_now() : 0;
@@ -838,25 +830,17 @@ int64_t fdgpu_submit_frags_io(fdgpu_engine_t *e, fdgpu_frag_io_t const *fio, uin
   /* results: codes (padded to 64) + 8 B tags + 2 B sizes, in the trailer buffer */
   const uint64_t cb = (n + 63) & ~63ull, res_sz = cb + n * 10;
   if (!slot_frag_bufs(*s, e->cfg, res_sz)) return FDGPU_ERR_DEVICE;
-#if FDGPU_IO_DIRECT
-  /* one upload: the frag records, then (64-B aligned) the payload addresses */
+  /* the frag records, then (64-B aligned) the payload addresses, in pinned
+     memory the gather reads in place */
   const uint64_t src_at = (n * sizeof(fdgpu_frag_ex_t) + 63) & ~63ull;
   if (!s->h_io) {
     const uint64_t m = e->cfg.max_txn + 1, bytes = m * (sizeof(fdgpu_frag_ex_t) + sizeof(uint64_t)) + 64;
     HIPCHK(hipHostMalloc((void **)&s->h_io, bytes, hipHostMallocDefault), FDGPU_ERR_DEVICE);
-    HIPCHK(hipMalloc((void **)&s->d_io, bytes), FDGPU_ERR_DEVICE);
+    HIPCHK(hipHostGetDevicePointer((void **)&s->d_ioh, s->h_io, 0), FDGPU_ERR_DEVICE);
+    HIPCHK(hipMalloc((void **)&s->d_fxio, m * sizeof(fdgpu_frag_ex_t)), FDGPU_ERR_DEVICE);
   }
   fdgpu_frag_ex_t *h_fx = (fdgpu_frag_ex_t *)s->h_io;
   uint64_t *h_src = (uint64_t *)(s->h_io + src_at);
-#else
-  if (!s->d_src) {
-    const uint64_t m = e->cfg.max_txn + 1;
-    HIPCHK(hipHostMalloc((void **)&s->h_src, m * sizeof(uint64_t), hipHostMallocDefault), FDGPU_ERR_DEVICE);
-    HIPCHK(hipMalloc((void **)&s->d_src, m * sizeof(uint64_t)), FDGPU_ERR_DEVICE);
-  }
-  fdgpu_frag_ex_t *h_fx = s->h_fx;
-  uint64_t *h_src = s->h_src;
-#endif
   /* bounds: every payload inside a registered region (16-B aligned: the
      gather reads 16-B units up to round16(sz), inside the payload's own
      64-B chunks), every out frag inside out, the packed arena within
@@ -882,55 +866,31 @@ int64_t fdgpu_submit_frags_io(fdgpu_engine_t *e, fdgpu_frag_io_t const *fio, uin
   if (bound > e->cfg.max_sig) { set_err("batch may exceed max_sig (%llu)", (unsigned long long)e->cfg.max_sig); return FDGPU_ERR_INVAL; }
   const uint64_t sp1 = g_sp_on ? sp_now() : 0;
   if (!slot_ws(*s, bound)) return FDGPU_ERR_DEVICE;
-#if FDGPU_IO_DIRECT
-  /* the finish kernel writes the out frags and the results in place, over
-     the bus: no device-side out image, no read-back copies */
+  /* five launches: gather (which also keeps the records on the device and
+     zeroes the verify queue counter), parse, scan + expand, verify (+ its
+     fallback), finish -- the out frags and the results written in place over
+     the bus -- then the completion word */
   uint8_t *out_dev = out_sz ? (uint8_t *)(ro->dbase + ((uintptr_t)out - ro->base)) : nullptr;
   if (n) {
-    HIPCHK(hipMemcpyAsync(s->d_io, s->h_io, src_at + n * sizeof(uint64_t), hipMemcpyHostToDevice, s->stream),
-           FDGPU_ERR_DEVICE);
-    const fdgpu_frag_ex_t *d_fx = (const fdgpu_frag_ex_t *)s->d_io;
-    HIPCHK(fdgpu_launch_frag_gather((const uint64_t *)(s->d_io + src_at), d_fx, (uint32_t)n, s->d_arena, s->stream),
+    const fdgpu_frag_ex_t *d_fx = s->d_fxio;
+    const bool zero_cnt = !(kflags(e) & FDGPU_FLAG_KCACHE);
+    HIPCHK(fdgpu_launch_frag_gather((const uint64_t *)(s->d_ioh + src_at), (const fdgpu_frag_ex_t *)s->d_ioh, (uint32_t)n,
+                                    s->d_arena, s->d_fxio, zero_cnt ? fdgpu_verify_cnt_word(s->d_ws, (uint32_t)bound) : nullptr,
+                                    s->stream),
            FDGPU_ERR_DEVICE);
     HIPCHK(fdgpu_launch_frag_ring(s->d_arena, d_fx, (uint32_t)n, s->d_txn_out, s->d_txn_sz, s->d_txd, s->d_cnt,
                                   s->d_sig0, s->d_blocktot, s->d_n_sig, s->d_sigs, s->d_txns, s->stream),
            FDGPU_ERR_DEVICE);
     HIPCHK(fdgpu_launch_verify_sigs(s->d_arena, s->d_sigs, (uint32_t)bound, nullptr, e->d_btab, s->d_ws, s->d_sig_codes,
-                                    kflags(e), s->stream, s->d_n_sig, e->resident_blocks, e->kc_seed),
+                                    kflags(e), s->stream, s->d_n_sig, e->resident_blocks, e->kc_seed, zero_cnt),
            FDGPU_ERR_DEVICE);
     HIPCHK(fdgpu_launch_frag_finish_io(s->d_txns, (uint32_t)n, s->d_sig_codes, s->d_txn_sz, d_fx, s->d_txn_out,
                                        s->d_arena, hash_seed, out_dev, (int8_t *)s->d_trh, (uint64_t *)(s->d_trh + cb),
                                        (uint16_t *)(s->d_trh + cb + n * 8), s->stream),
            FDGPU_ERR_DEVICE);
   }
-#else
-  if (out_sz > s->out_cap_bytes) {
-    HIPCHK(hipStreamSynchronize(s->stream), FDGPU_ERR_DEVICE);
-    if (s->d_out) { (void)hipFree(s->d_out); s->d_out = nullptr; }
-    s->out_cap_bytes = 0;
-    const uint64_t want = std::max<uint64_t>(out_sz + out_sz / 4, 1u << 20);
-    HIPCHK(hipMalloc((void **)&s->d_out, want), FDGPU_ERR_DEVICE);
-    s->out_cap_bytes = want;
-  }
-  if (n) {
-    HIPCHK(hipMemcpyAsync(s->d_fx, s->h_fx, n * sizeof(fdgpu_frag_ex_t), hipMemcpyHostToDevice, s->stream), FDGPU_ERR_DEVICE);
-    HIPCHK(hipMemcpyAsync(s->d_src, s->h_src, n * sizeof(uint64_t), hipMemcpyHostToDevice, s->stream), FDGPU_ERR_DEVICE);
-    HIPCHK(fdgpu_launch_frag_gather(s->d_src, s->d_fx, (uint32_t)n, s->d_arena, s->stream), FDGPU_ERR_DEVICE);
-    HIPCHK(fdgpu_launch_frag_ring(s->d_arena, s->d_fx, (uint32_t)n, s->d_txn_out, s->d_txn_sz, s->d_txd, s->d_cnt,
-                                  s->d_sig0, s->d_blocktot, s->d_n_sig, s->d_sigs, s->d_txns, s->stream),
-           FDGPU_ERR_DEVICE);
-    HIPCHK(fdgpu_launch_verify_sigs(s->d_arena, s->d_sigs, (uint32_t)bound, nullptr, e->d_btab, s->d_ws, s->d_sig_codes,
-                                    kflags(e), s->stream, s->d_n_sig, e->resident_blocks, e->kc_seed),
-           FDGPU_ERR_DEVICE);
-    HIPCHK(fdgpu_launch_frag_finish_io(s->d_txns, (uint32_t)n, s->d_sig_codes, s->d_txn_sz, s->d_fx, s->d_txn_out,
-                                       s->d_arena, hash_seed, s->d_out, (int8_t *)s->d_tr, (uint64_t *)(s->d_tr + cb),
-                                       (uint16_t *)(s->d_tr + cb + n * 8), s->stream),
-           FDGPU_ERR_DEVICE);
-    if (out_sz) HIPCHK(hipMemcpyAsync(out, s->d_out, out_sz, hipMemcpyDeviceToHost, s->stream), FDGPU_ERR_DEVICE);
-    HIPCHK(hipMemcpyAsync(s->h_tr, s->d_tr, res_sz, hipMemcpyDeviceToHost, s->stream), FDGPU_ERR_DEVICE);
-  }
-#endif
   ++s->flag_seq;
+  if (e->flag_poll && !e->drop_flag) HIPCHK(hipStreamWriteValue32(s->stream, s->d_flag, s->flag_seq, 0), FDGPU_ERR_DEVICE);
   if (e->flag_poll && !e->drop_flag) HIPCHK(hipStreamWriteValue32(s->stream, s->d_flag, s->flag_seq, 0), FDGPU_ERR_DEVICE);
   HIPCHK(hipEventRecord(s->done, s->stream), FDGPU_ERR_DEVICE);
   s->staged = false;

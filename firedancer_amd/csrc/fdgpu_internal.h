@@ -77,7 +77,11 @@ hipError_t fdgpu_btab_build(uint32_t *d_btab, hipStream_t stream);
 hipError_t fdgpu_launch_verify_sigs(const uint8_t *d_arena, const fdgpu_sig_desc_t *d_sigs, uint32_t n_sig,
                                     const uint32_t *d_perm, const uint32_t *d_btab, uint32_t *d_ws,
                                     int8_t *d_sig_codes, uint32_t flags, hipStream_t stream,
-                                    const uint32_t *d_n_sig, uint32_t resident_blocks, uint64_t kc_seed);
+                                    const uint32_t *d_n_sig, uint32_t resident_blocks, uint64_t kc_seed,
+                                    int cnt_zeroed = 0);
+/* the verify launch's queue counter for an n_sig grid in d_ws: a caller whose
+   earlier kernel on the stream zeroes it passes cnt_zeroed (no memset) */
+uint32_t  *fdgpu_verify_cnt_word(uint32_t *d_ws, uint32_t n_sig);
 /* d_accept (NULL: not written): ceil(n_txn / 64) words, bit t = txn t verified */
 hipError_t fdgpu_launch_combine(const fdgpu_txn_desc_t *d_txns, uint32_t n_txn, const int8_t *d_sig_codes,
                                 int8_t *d_txn_codes, uint64_t *d_accept, hipStream_t stream);
@@ -125,7 +129,7 @@ hipError_t fdgpu_launch_frag_finish(const fdgpu_txn_desc_t *d_tds, uint32_t n, c
    d_out + d_fx[i].tr_off ([payload][pad][fd_txn_t][u16 sz]) */
 uint64_t   fdgpu_frag_fp_bound(uint32_t sz);
 hipError_t fdgpu_launch_frag_gather(const uint64_t *d_src, const fdgpu_frag_ex_t *d_fx, uint32_t n, uint8_t *d_arena,
-                                    hipStream_t stream);
+                                    fdgpu_frag_ex_t *d_fx_dev, uint32_t *d_zero_word, hipStream_t stream);
 hipError_t fdgpu_launch_frag_finish_io(const fdgpu_txn_desc_t *d_tds, uint32_t n, const int8_t *d_sig_codes,
                                        const uint16_t *d_txn_sz, const fdgpu_frag_ex_t *d_fx, const uint8_t *d_txn_out,
                                        const uint8_t *d_arena, uint64_t hash_seed, uint8_t *d_out, int8_t *d_codes,

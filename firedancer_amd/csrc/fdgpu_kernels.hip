@@ -1098,16 +1098,24 @@ __global__ void __launch_bounds__(256) fdgpu_frag_finish_kernel(const fdgpu_txn_
 }
 
 /* Gathered frag batches (fdgpu_submit_frags_io).  Gather: one wave per frag
-   copies the payload's 16-B units from host memory (the registered in
-   dcache, read in place over PCIe) to its packed, 16-B aligned place in the
-   batch arena; the units past sz lie in the payload's own 64-B chunks. */
+   reads its record and payload address from the slot's pinned upload buffer
+   and copies the payload's 16-B units from host memory (the registered in
+   dcache), both read in place over the bus, to its packed, 16-B aligned
+   place in the batch arena; the units past sz lie in the payload's own 64-B
+   chunks.  The record is kept on the device (fx_dev) for the later kernels,
+   and the first thread clears the verify kernel's queue counter (zero_word):
+   the batch needs no upload copy and no memset. */
 __global__ void __launch_bounds__(256) fdgpu_frag_gather_kernel(const uint64_t *__restrict__ src,
                                                                 const fdgpu_frag_ex_t *__restrict__ fx, uint32_t n,
-                                                                uint8_t *__restrict__ arena) {
+                                                                uint8_t *__restrict__ arena,
+                                                                fdgpu_frag_ex_t *__restrict__ fx_dev,
+                                                                uint32_t *__restrict__ zero_word) {
   const uint32_t f = blockIdx.x * 4u + (threadIdx.x >> 6), lane = threadIdx.x & 63u;
+  if (zero_word && blockIdx.x == 0 && threadIdx.x == 0) *zero_word = 0u;
   if (f >= n) return;
   const uint4 *s = (const uint4 *)src[f];
   const fdgpu_frag_ex_t x = fx[f];
+  if (lane == 0) fx_dev[f] = x;
   uint4 *d = (uint4 *)(arena + x.off);
   const uint32_t nq = (x.sz + 15u) >> 4;
   for (uint32_t q = lane; q < nq; q += 64u) d[q] = s[q];
@@ -1120,14 +1128,16 @@ __global__ void __launch_bounds__(256) fdgpu_frag_gather_kernel(const uint64_t *
    fd_verify.h:66) and its out size; the wave writes the out frag as
    fd_verify.c:93-136 lays it out in the out dcache -- [payload][pad to 2]
    [fd_txn_t][u16 payload_sz] -- one 16-bit word per lane (the fd_txn_t
-   starts 2-aligned). */
-__global__ void __launch_bounds__(256) fdgpu_frag_finish_io_kernel(
-    const fdgpu_txn_desc_t *__restrict__ txns, uint32_t n, const int8_t *__restrict__ sig_codes,
-    const uint16_t *__restrict__ txn_sz, const fdgpu_frag_ex_t *__restrict__ fx, const uint8_t *__restrict__ txn_out,
-    const uint8_t *__restrict__ arena, uint64_t seed, uint8_t *__restrict__ out, int8_t *__restrict__ codes,
-    uint64_t *__restrict__ tags, uint16_t *__restrict__ out_szs) {
-  const uint32_t f = blockIdx.x * 4u + (threadIdx.x >> 6), lane = threadIdx.x & 63u;
-  if (f >= n) return;
+   starts 2-aligned).  (A completion word stored by the kernel's last block
+   was tried: the system-scope fence each block then needs writes back the
+   L2 under the concurrent verify kernels and halved the tile's rate; the
+   stream's own write after the kernel stays.) */
+FDG_DEV void frag_finish_io_one(uint32_t f, uint32_t lane, const fdgpu_txn_desc_t *__restrict__ txns,
+                                const int8_t *__restrict__ sig_codes, const uint16_t *__restrict__ txn_sz,
+                                const fdgpu_frag_ex_t *__restrict__ fx, const uint8_t *__restrict__ txn_out,
+                                const uint8_t *__restrict__ arena, uint64_t seed, uint8_t *__restrict__ out,
+                                int8_t *__restrict__ codes, uint64_t *__restrict__ tags,
+                                uint16_t *__restrict__ out_szs) {
   const uint32_t fp = txn_sz[f];
   const fdgpu_frag_ex_t x = fx[f];                    /* off: arena, sz, tr_off: out offset, tr_cap: its room */
   const uint32_t toff = (x.sz + 1u) & ~1u, osz = toff + fp + 2u;
@@ -1175,6 +1185,15 @@ __global__ void __launch_bounds__(256) fdgpu_frag_finish_io_kernel(
     }
     o[h] = v;
   }
+}
+
+__global__ void __launch_bounds__(256) fdgpu_frag_finish_io_kernel(
+    const fdgpu_txn_desc_t *__restrict__ txns, uint32_t n, const int8_t *__restrict__ sig_codes,
+    const uint16_t *__restrict__ txn_sz, const fdgpu_frag_ex_t *__restrict__ fx, const uint8_t *__restrict__ txn_out,
+    const uint8_t *__restrict__ arena, uint64_t seed, uint8_t *__restrict__ out, int8_t *__restrict__ codes,
+    uint64_t *__restrict__ tags, uint16_t *__restrict__ out_szs) {
+  const uint32_t f = blockIdx.x * 4u + (threadIdx.x >> 6), lane = threadIdx.x & 63u;
+  if (f < n) frag_finish_io_one(f, lane, txns, sig_codes, txn_sz, fx, txn_out, arena, seed, out, codes, tags, out_szs);
 }
 
 /* After the combine: a payload that did not parse gets FDGPU_CODE_PARSE_FAIL */
@@ -1247,12 +1266,12 @@ size_t fdgpu_ws_bytes(uint64_t n_sig) {
 hipError_t fdgpu_launch_verify_sigs(const uint8_t *d_arena, const fdgpu_sig_desc_t *d_sigs, uint32_t n_sig,
                                     const uint32_t *d_perm, const uint32_t *d_btab, uint32_t *d_ws,
                                     int8_t *d_sig_codes, uint32_t flags, hipStream_t stream, const uint32_t *d_n_sig,
-                                    uint32_t resident_blocks, uint64_t kc_seed) {
+                                    uint32_t resident_blocks, uint64_t kc_seed, int cnt_zeroed) {
   if (!n_sig) return hipSuccess;
   const uint32_t grid = (n_sig + FDGPU_BLOCK - 1) / FDGPU_BLOCK;
   const size_t lanes = (size_t)grid * FDGPU_BLOCK;
   uint32_t *queue = d_ws + lanes * FDGPU_WS_LANE_WORDS, *cnt = queue + lanes;
-  hipError_t e = hipMemsetAsync(cnt, 0, sizeof(uint32_t), stream);
+  hipError_t e = cnt_zeroed ? hipSuccess : hipMemsetAsync(cnt, 0, sizeof(uint32_t), stream);
   if (e != hipSuccess) return e;
   /* the queued full-length lanes get as many blocks as the batch's grid could
      keep resident (all of them, up to every wave slot of the GPU: the
@@ -1281,6 +1300,11 @@ hipError_t fdgpu_launch_verify_sigs(const uint8_t *d_arena, const fdgpu_sig_desc
   hipLaunchKernelGGL(fdgpu_full_kernel, dim3(slow_blocks), dim3(FDGPU_BLOCK), 0, stream, d_ws, d_perm, d_sig_codes,
                      queue, cnt, slow_blocks * FDGPU_BLOCK, key_of);
   return hipGetLastError();
+}
+
+uint32_t *fdgpu_verify_cnt_word(uint32_t *d_ws, uint32_t n_sig) {
+  const size_t lanes = (size_t)((n_sig + FDGPU_BLOCK - 1) / FDGPU_BLOCK) * FDGPU_BLOCK;
+  return d_ws + lanes * FDGPU_WS_LANE_WORDS + lanes;
 }
 
 hipError_t fdgpu_launch_combine(const fdgpu_txn_desc_t *d_txns, uint32_t n_txn, const int8_t *d_sig_codes,
@@ -1374,9 +1398,10 @@ hipError_t fdgpu_launch_frag_finish(const fdgpu_txn_desc_t *d_tds, uint32_t n, c
 uint64_t fdgpu_frag_fp_bound(uint32_t sz) { return fdt_frag_fp_bound(sz); }
 
 hipError_t fdgpu_launch_frag_gather(const uint64_t *d_src, const fdgpu_frag_ex_t *d_fx, uint32_t n, uint8_t *d_arena,
-                                    hipStream_t stream) {
+                                    fdgpu_frag_ex_t *d_fx_dev, uint32_t *d_zero_word, hipStream_t stream) {
   if (!n) return hipSuccess;
-  hipLaunchKernelGGL(fdgpu_frag_gather_kernel, dim3((n + 3) / 4), dim3(256), 0, stream, d_src, d_fx, n, d_arena);
+  hipLaunchKernelGGL(fdgpu_frag_gather_kernel, dim3((n + 3) / 4), dim3(256), 0, stream, d_src, d_fx, n, d_arena,
+                     d_fx_dev, d_zero_word);
   return hipGetLastError();
 }
 

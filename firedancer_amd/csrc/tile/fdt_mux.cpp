@@ -193,7 +193,7 @@ struct VBatch {
   bool closed = false;               /* takes no more frags (full, or the cursor wrapped) */
   bool done = false;
   size_t next = 0;                   /* next item to resolve */
-  uint64_t t_first = 0;
+  uint64_t t_first = 0, t_submit = 0;
 
   void reset() {
     first_chunk = end_off = sig_cnt = tr_used = 0;
@@ -301,13 +301,19 @@ struct fdgpu_vmux {
         const int rc = gather ? ver.poll_io(ver.ctx, b->ticket, b->codes.data(), b->tags.data(), b->out_szs.data(), 0)
                        : gpu_parse ? ver.poll_frags(ver.ctx, b->ticket, b->codes.data(), b->trailers.data(), 0)
                                    : ver.poll(ver.ctx, b->ticket, b->codes.data(), 0);
-        st.poll_ns += now_ns() - p0;
+        const uint64_t dp = now_ns() - p0;
+        st.poll_ns += dp;
+        st.polls++;
         if (rc == FDGPU_PENDING) return;
+        st.poll_done_ns += dp;
+        st.batch_gpu_ns += now_ns() - b->t_submit;
         if (rc != FDGPU_OK) { error = rc; *poll_in = 0; return; }
         b->done = true;
         if (gather) lapped_check(*b);
       }
-      const uint32_t tspub = (uint32_t)now_ns();
+      const uint64_t t_pub = now_ns();
+      struct Acc { uint64_t &ns; uint64_t t0; ~Acc() { ns += now_ns() - t0; } } acc{st.publish_ns, t_pub};
+      const uint32_t tspub = (uint32_t)t_pub;
       const size_t n = b->items.size();
       while (b->next < n) {
         const size_t k = b->next;
@@ -428,6 +434,8 @@ struct fdgpu_vmux {
     if (t == FDGPU_ERR_INVAL) { reject_open(); return; }
     if (t < 0) { error = (int)t; return; }
     open->ticket = t;
+    open->t_submit = now_ns();
+    st.batch_fill_ns += open->t_submit - open->t_first;
     inflight.push_back(open);
     open = nullptr;
     st.batches++;

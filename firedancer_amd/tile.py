@@ -111,7 +111,8 @@ class VTileStats(c.Structure):
     _fields_ = [(n, c.c_uint64) for n in ("in_frags", "filtered_rr", "corrupt", "overrun", "parse_fail",
                                           "verify_failed", "dedup", "published", "batches", "sigs",
                                           "backpressure", "lat_cnt", "verify_errors", "ingest_ns", "submit_ns",
-                                          "poll_ns", "no_slot_steps")]
+                                          "poll_ns", "no_slot_steps", "polls", "poll_done_ns",
+                                          "publish_ns", "batch_fill_ns", "batch_gpu_ns")]
 
     def as_dict(self):
         return {n: getattr(self, n) for n, _ in self._fields_}

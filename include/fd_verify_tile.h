@@ -281,6 +281,11 @@ typedef struct {
   uint64_t submit_ns;       /* inside the verifier's submit / stage calls (and the submit-wait checks) */
   uint64_t poll_ns;         /* inside the verifier's non-blocking polls */
   uint64_t no_slot_steps;   /* steps that could not open a batch: every batch or ring slot in flight */
+  uint64_t polls;           /* non-blocking polls (fdgpu_vmux) */
+  uint64_t poll_done_ns;    /* the part of poll_ns in polls that completed (the results' read-out) */
+  uint64_t publish_ns;      /* resolving completed batches: tags, tcache, publishing (fdgpu_vmux) */
+  uint64_t batch_fill_ns;   /* summed over batches: first frag taken -> submitted (fdgpu_vmux) */
+  uint64_t batch_gpu_ns;    /* summed over batches: submitted -> a poll saw it complete (fdgpu_vmux) */
 } fdgpu_vtile_stats_t;
 
 typedef struct fdgpu_vtile fdgpu_vtile_t;
