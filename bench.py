@@ -30,10 +30,11 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 # HIP hardware queues of this process, set before the runtime starts: every
 # ring slot, device batch and tile engine owns a stream, and HIP maps streams
 # onto GPU_MAX_HW_QUEUES hardware queues (4 by default); two streams on one
-# queue serialise, so with the cfg5 tile lines' two engines x four slots
+# queue serialise, so with the cfg5 tile lines' two engines x eight slots
 # beside the headline engine the tiles' batches would queue behind each other
-# (profiles/r03/hwq_*.jsonl).  16 is HIP's supported range.
-HW_QUEUES = 16
+# (profiles/r03/hwq_*.jsonl, mux_sweep/r03s_*.jsonl: two tiles 35 M txn/s
+# with 16 queues, 44 M with 32).  32 is the most this pool allows.
+HW_QUEUES = 32
 os.environ["GPU_MAX_HW_QUEUES"] = str(HW_QUEUES)
 sys.path.insert(0, REPO)
 
@@ -319,16 +320,28 @@ TILE_RUNS = (  # name, verify tiles, quic links (producers), offered txn/s (-1: 
     ("mux1_capacity", 1, 1, -1.0),
     ("mux1_paced_16M", 1, 1, 16e6),
     ("mux2_capacity", 2, 2, -1.0),
-    ("mux2_paced_24M", 2, 2, 24e6),
+    ("mux2_paced_32M", 2, 2, 32e6),
 )
+TILE_BATCH, TILE_INFLIGHT = 16384, 8   # txns per GPU batch, batches in flight per tile
 
 
-def tile_args(prods, rate):
-    """bench_tile.run_once_mux's options for one cfg5 run (tests/test_bench_cli.py
-    checks it carries every option run_once_mux and start_producer read)"""
-    import types
-    return types.SimpleNamespace(gpus=1, gpu_parse=2, producers=prods, depth_lg=21 if rate <= 0 else 19,
-                                 wait_us=200.0, pin=1, multi=0, cpu_offset=0)
+TILE_REPS = 3   # a capacity run drains 1M frags in a few tens of ms: the median of three
+
+
+def tile_cmd(device, cpus, npz, out, runs=TILE_RUNS):
+    """tools/bench_tile.py's command line for the cfg5 runs (tests/test_bench_cli.py
+    parses it with bench_tile's own parser).  The tiles run in a child process:
+    its HIP runtime gives the tile engines' slot streams hardware queues of
+    their own, instead of the ones this process's headline, latency and ingest
+    engines already hold (shared queues serialise the tiles' batches)."""
+    sweep = ";".join(f"{tiles_n},{TILE_BATCH},{TILE_INFLIGHT},{rate:g}" for _, tiles_n, _, rate in runs)
+    cmd = [sys.executable, os.path.join(REPO, "tools", "bench_tile.py"), "--mux", "1", "--gpu-parse", "2",
+           "--multi", "0", "--producers-same-as-tiles", "1", "--depth-lg", "21", "--depth-lg-paced", "19",
+           "--wait-us", "200", "--pin", "1", "--hw-queues", str(HW_QUEUES), "--reps", str(TILE_REPS),
+           "--payload-npz", npz, "--device", str(device), "--sweep", sweep, "--out", out]
+    if cpus:
+        cmd += ["--cpu-list", ",".join(str(c) for c in cpus)]
+    return cmd
 
 
 def tile_lines(device, arena, txns, modes, cpus, runs=TILE_RUNS):
@@ -342,37 +355,44 @@ def tile_lines(device, arena, txns, modes, cpus, runs=TILE_RUNS):
     this rank's cfg1 txns as raw frags.  T tiles read P quic->verify links
     round robin (every verify tile reads every QUIC tile's link,
     fd_frankendancer.c:131-133), one engine per tile on this GPU, 16K-txn
-    batches, 4 in flight, producers and tiles pinned to their own cores.
-    Every run checks that exactly the verified txns were published."""
-    sys.path.insert(0, os.path.join(REPO, "tools"))
-    import bench_tile
+    batches, 8 in flight, producers and tiles pinned to their own cores, in
+    a child process (tile_cmd).  Every run checks that exactly the verified
+    txns were published."""
+    import subprocess
+    import tempfile
     from firedancer_amd import workload
     ps = workload.payloads(arena, txns)
     parena, poffs, psizes = workload.pack_payloads(ps)
-    n_sig = int(txns["sig_cnt"].sum())
     out = {}
-    for name, tiles_n, prods, rate in runs:
-        args = tile_args(prods, rate)
-        # a capacity run drains 1M frags in a few tens of ms: the median of three
-        reps = [bench_tile.run_once_mux(args, ps, parena, poffs, psizes, n_sig, modes, tiles_n, 16384, 4, rate,
-                                        cpus=cpus, device=device) for _ in range(3 if rate < 0 else 1)]
-        res = sorted(reps, key=lambda r: r["txns_per_s"])[len(reps) // 2]
-        if len(reps) > 1:
-            out[f"tile_{name}_txns_per_s_runs"] = [r["txns_per_s"] for r in reps]
+    with tempfile.TemporaryDirectory() as td:
+        npz, res_path = os.path.join(td, "frags.npz"), os.path.join(td, "tile.jsonl")
+        np.savez(npz, arena=parena, offs=poffs, sizes=psizes, modes=modes, n_sig=int(txns["sig_cnt"].sum()))
+        r = subprocess.run(tile_cmd(device, cpus, npz, res_path, runs), capture_output=True, text=True, timeout=600)
+        if r.returncode not in (0, 1) or not os.path.exists(res_path):
+            raise RuntimeError(f"tools/bench_tile.py failed ({r.returncode}): {r.stderr[-2000:]}")
+        res_all = [json.loads(x) for x in open(res_path) if x.strip()]
+    if len(res_all) != len(runs) * TILE_REPS:
+        raise RuntimeError(f"tools/bench_tile.py gave {len(res_all)} runs, expected {len(runs) * TILE_REPS}")
+    for i, (name, tiles_n, prods, rate) in enumerate(runs):
+        reps = res_all[i * TILE_REPS:(i + 1) * TILE_REPS]
+        assert all(x["tiles"] == tiles_n and x["producers"] == prods for x in reps)
+        res = sorted(reps, key=lambda x: x["txns_per_s"])[len(reps) // 2]
+        out[f"tile_{name}_txns_per_s_runs"] = [x["txns_per_s"] for x in reps]
         lat = res["batch_latency_ms"]
         out[f"tile_{name}_txns_per_s"] = res["txns_per_s"]
         out[f"tile_{name}_batch_latency_ms_p50_p99"] = [lat["p50"], lat["p99"]]
-        out[f"tile_{name}_overruns"] = res["counters"]["overrun"]
-        out[f"tile_{name}_published_ok"] = res["counters"]["published"] == res["expected_published"]
+        out[f"tile_{name}_overruns"] = max(x["counters"]["overrun"] for x in reps)
+        out[f"tile_{name}_published_ok"] = all(x["counters"]["published"] == x["expected_published"] for x in reps)
     out["tile_mux2_vs_mux1_capacity"] = round(out["tile_mux2_capacity_txns_per_s"] /
                                               out["tile_mux1_capacity_txns_per_s"], 3)
     out["tile_config"] = ("fdgpu_vmux on fdt_mux_run (the reference's mux-callback verify tile), payload gather, "
                           "fd_txn_parse, verify, dedup tag and out-frag assembly on the GPU; muxT: T verify tiles "
                           "reading T quic->verify links (one producer thread each), one engine per tile on this GPU, "
-                          "cfg1 frags, 16384-txn batches, 4 in flight; capacity: "
-                          "every frag published into 2^21-deep links before the tiles start, timed from tile start "
-                          "to the last outcome; paced_R: R txn/s offered in total into 2^19-deep links while the "
-                          "tiles run")
+                          f"cfg1 frags, {TILE_BATCH}-txn batches, {TILE_INFLIGHT} in flight, {HW_QUEUES} HIP hardware "
+                          "queues, in a child process (tools/bench_tile.py); capacity: every frag published into "
+                          "2^21-deep links before the tiles start, timed from tile start to the last outcome; "
+                          f"paced_R: R txn/s offered in total into 2^19-deep links while the tiles run; median of "
+                          f"{TILE_REPS} runs each")
     return out
 
 

@@ -866,20 +866,20 @@ int64_t fdgpu_submit_frags_io(fdgpu_engine_t *e, fdgpu_frag_io_t const *fio, uin
   if (bound > e->cfg.max_sig) { set_err("batch may exceed max_sig (%llu)", (unsigned long long)e->cfg.max_sig); return FDGPU_ERR_INVAL; }
   const uint64_t sp1 = g_sp_on ? sp_now() : 0;
   if (!slot_ws(*s, bound)) return FDGPU_ERR_DEVICE;
-  /* five launches: gather (which also keeps the records on the device and
-     zeroes the verify queue counter), parse, scan + expand, verify (+ its
-     fallback), finish -- the out frags and the results written in place over
-     the bus -- then the completion word */
+  /* five kernels: gather (which also keeps the records on the device and
+     zeroes the verify queue counter and the signature count), parse +
+     expand, verify and its fallback, finish -- the out frags and the results
+     written in place over the bus -- then the completion word */
   uint8_t *out_dev = out_sz ? (uint8_t *)(ro->dbase + ((uintptr_t)out - ro->base)) : nullptr;
   if (n) {
     const fdgpu_frag_ex_t *d_fx = s->d_fxio;
     const bool zero_cnt = !(kflags(e) & FDGPU_FLAG_KCACHE);
     HIPCHK(fdgpu_launch_frag_gather((const uint64_t *)(s->d_ioh + src_at), (const fdgpu_frag_ex_t *)s->d_ioh, (uint32_t)n,
                                     s->d_arena, s->d_fxio, zero_cnt ? fdgpu_verify_cnt_word(s->d_ws, (uint32_t)bound) : nullptr,
-                                    s->stream),
+                                    s->d_n_sig, s->stream),
            FDGPU_ERR_DEVICE);
-    HIPCHK(fdgpu_launch_frag_ring(s->d_arena, d_fx, (uint32_t)n, s->d_txn_out, s->d_txn_sz, s->d_txd, s->d_cnt,
-                                  s->d_sig0, s->d_blocktot, s->d_n_sig, s->d_sigs, s->d_txns, s->stream),
+    HIPCHK(fdgpu_launch_frag_parse_expand(s->d_arena, d_fx, (uint32_t)n, s->d_txn_out, s->d_txn_sz, s->d_sigs, s->d_txns,
+                                          s->d_n_sig, s->stream),
            FDGPU_ERR_DEVICE);
     HIPCHK(fdgpu_launch_verify_sigs(s->d_arena, s->d_sigs, (uint32_t)bound, nullptr, e->d_btab, s->d_ws, s->d_sig_codes,
                                     kflags(e), s->stream, s->d_n_sig, e->resident_blocks, e->kc_seed, zero_cnt),

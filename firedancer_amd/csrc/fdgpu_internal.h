@@ -129,7 +129,14 @@ hipError_t fdgpu_launch_frag_finish(const fdgpu_txn_desc_t *d_tds, uint32_t n, c
    d_out + d_fx[i].tr_off ([payload][pad][fd_txn_t][u16 sz]) */
 uint64_t   fdgpu_frag_fp_bound(uint32_t sz);
 hipError_t fdgpu_launch_frag_gather(const uint64_t *d_src, const fdgpu_frag_ex_t *d_fx, uint32_t n, uint8_t *d_arena,
-                                    fdgpu_frag_ex_t *d_fx_dev, uint32_t *d_zero_word, hipStream_t stream);
+                                    fdgpu_frag_ex_t *d_fx_dev, uint32_t *d_zero_word, uint32_t *d_zero_word2,
+                                    hipStream_t stream);
+/* gathered batches: parse + descriptor expansion in one launch, each wave
+   taking its descriptor slots with one atomic add on *d_n_sig (which must
+   start at zero: the gather kernel clears it) */
+hipError_t fdgpu_launch_frag_parse_expand(const uint8_t *d_arena, const fdgpu_frag_ex_t *d_fx, uint32_t n,
+                                          uint8_t *d_txn_out, uint16_t *d_txn_sz, fdgpu_sig_desc_t *d_sigs,
+                                          fdgpu_txn_desc_t *d_tds, uint32_t *d_n_sig, hipStream_t stream);
 hipError_t fdgpu_launch_frag_finish_io(const fdgpu_txn_desc_t *d_tds, uint32_t n, const int8_t *d_sig_codes,
                                        const uint16_t *d_txn_sz, const fdgpu_frag_ex_t *d_fx, const uint8_t *d_txn_out,
                                        const uint8_t *d_arena, uint64_t hash_seed, uint8_t *d_out, int8_t *d_codes,

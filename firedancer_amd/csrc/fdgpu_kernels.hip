@@ -1053,6 +1053,57 @@ __global__ void __launch_bounds__(1024) fdgpu_frag_scan_expand_small_kernel(
   }
 }
 
+/* Gathered batches: parse and expand in one launch, lane per txn, no scan
+   kernel.  Each wave scans its 64 signature counts and takes its run of
+   descriptor slots with one atomic add on *n_sig (zeroed by the gather
+   kernel), so the descriptors stay dense in [0, n_sig) -- grouped by wave
+   in whatever order the waves ran, which the codes do not depend on: every
+   txn records its own first slot (tds[t].sig0).  The parse itself is
+   fdgpu_frag_parse_kernel's. */
+__global__ void __launch_bounds__(64) fdgpu_frag_parse_expand_kernel(
+    const uint8_t *__restrict__ arena, const fdgpu_frag_ex_t *__restrict__ fx, uint32_t n,
+    uint8_t *__restrict__ txn_out, uint16_t *__restrict__ txn_sz, fdgpu_sig_desc_t *__restrict__ sigs,
+    fdgpu_txn_desc_t *__restrict__ tds, uint32_t *__restrict__ n_sig) {
+  const uint32_t t = blockIdx.x * 64u + threadIdx.x, lane = threadIdx.x;
+  uint32_t c = 0;
+  fdgpu_txn_t d{};
+  if (t < n) {
+    const fdgpu_frag_ex_t f = fx[t];
+    fdt_txn_t *x = (fdt_txn_t *)(txn_out + (size_t)t * FDT_TXN_MAX_SZ);
+    uint64_t why = 0;
+    uint64_t fp = fdt_parse_core(arena + f.off, f.sz, x, &why);
+    const uint32_t sc = fp ? x->signature_cnt : 0u;
+    c = (sc >= 1u && sc <= 16u) ? sc : 0u;
+    if (c > fdt_frag_sig_bound(f.sz)) { c = 0u; fp = 0u; }      /* cannot happen for a parsed txn */
+    if (fp) {
+      d.msg_off = f.off + x->message_off;
+      d.msg_sz = f.sz - x->message_off;
+      d.sig_off = f.off + x->signature_off;
+      d.pub_off = f.off + x->acct_addr_off;
+    }
+    txn_sz[t] = (uint16_t)fp;
+  }
+  const uint32_t incl = wave_incl_scan(c);
+  const uint32_t total = (uint32_t)__shfl((int)incl, 63, 64);
+  uint32_t base = 0;
+  if (lane == 63u && total) base = atomicAdd(n_sig, total);
+  base = (uint32_t)__shfl((int)base, 63, 64);
+  if (t >= n) return;
+  const uint32_t s0 = base + incl - c;
+  fdgpu_txn_desc_t td;
+  td.sig0 = s0;
+  td.sig_cnt = c;
+  tds[t] = td;
+  for (uint32_t j = 0; j < c; j++) {
+    fdgpu_sig_desc_t sd;
+    sd.msg_off = d.msg_off;
+    sd.msg_sz = d.msg_sz;
+    sd.sig_off = d.sig_off + 64u * j;
+    sd.pub_off = d.pub_off + 32u * j;
+    sigs[s0 + j] = sd;
+  }
+}
+
 /* The end of a ring-slot frag batch in one launch, per txn: the
    batch_single_msg combine of its signatures' codes, FDGPU_CODE_PARSE_FAIL
    for a payload that is not a transaction, and its parsed fd_txn_t copied
@@ -1109,9 +1160,13 @@ __global__ void __launch_bounds__(256) fdgpu_frag_gather_kernel(const uint64_t *
                                                                 const fdgpu_frag_ex_t *__restrict__ fx, uint32_t n,
                                                                 uint8_t *__restrict__ arena,
                                                                 fdgpu_frag_ex_t *__restrict__ fx_dev,
-                                                                uint32_t *__restrict__ zero_word) {
+                                                                uint32_t *__restrict__ zero_word,
+                                                                uint32_t *__restrict__ zero_word2) {
   const uint32_t f = blockIdx.x * 4u + (threadIdx.x >> 6), lane = threadIdx.x & 63u;
-  if (zero_word && blockIdx.x == 0 && threadIdx.x == 0) *zero_word = 0u;
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    if (zero_word) *zero_word = 0u;
+    if (zero_word2) *zero_word2 = 0u;
+  }
   if (f >= n) return;
   const uint4 *s = (const uint4 *)src[f];
   const fdgpu_frag_ex_t x = fx[f];
@@ -1398,10 +1453,20 @@ hipError_t fdgpu_launch_frag_finish(const fdgpu_txn_desc_t *d_tds, uint32_t n, c
 uint64_t fdgpu_frag_fp_bound(uint32_t sz) { return fdt_frag_fp_bound(sz); }
 
 hipError_t fdgpu_launch_frag_gather(const uint64_t *d_src, const fdgpu_frag_ex_t *d_fx, uint32_t n, uint8_t *d_arena,
-                                    fdgpu_frag_ex_t *d_fx_dev, uint32_t *d_zero_word, hipStream_t stream) {
+                                    fdgpu_frag_ex_t *d_fx_dev, uint32_t *d_zero_word, uint32_t *d_zero_word2,
+                                    hipStream_t stream) {
   if (!n) return hipSuccess;
   hipLaunchKernelGGL(fdgpu_frag_gather_kernel, dim3((n + 3) / 4), dim3(256), 0, stream, d_src, d_fx, n, d_arena,
-                     d_fx_dev, d_zero_word);
+                     d_fx_dev, d_zero_word, d_zero_word2);
+  return hipGetLastError();
+}
+
+hipError_t fdgpu_launch_frag_parse_expand(const uint8_t *d_arena, const fdgpu_frag_ex_t *d_fx, uint32_t n,
+                                          uint8_t *d_txn_out, uint16_t *d_txn_sz, fdgpu_sig_desc_t *d_sigs,
+                                          fdgpu_txn_desc_t *d_tds, uint32_t *d_n_sig, hipStream_t stream) {
+  if (!n) return hipSuccess;
+  hipLaunchKernelGGL(fdgpu_frag_parse_expand_kernel, dim3((n + 63) / 64), dim3(64), 0, stream, d_arena, d_fx, n,
+                     d_txn_out, d_txn_sz, d_sigs, d_tds, d_n_sig);
   return hipGetLastError();
 }
 

@@ -1,9 +1,8 @@
-"""bench.py's helper plumbing on the CPU: the cfg5 tile lines hand
-bench_tile.run_once_mux an options namespace built by bench.tile_args; every
-option run_once_mux (and the start_producer it calls) reads must be there, or
-the driver's round-end bench dies in its tile leg on the GPU box."""
-import ast
-import inspect
+"""bench.py's helper plumbing on the CPU: the cfg5 tile lines run
+tools/bench_tile.py in a child process with the command bench.tile_cmd
+builds; it must parse with bench_tile's own parser and ask for every run of
+bench.TILE_RUNS, or the driver's round-end bench dies in its tile leg on the
+GPU box."""
 import os
 import sys
 
@@ -15,22 +14,23 @@ import bench  # noqa: E402
 import bench_tile  # noqa: E402
 
 
-def _args_read(fn):
-    """attribute names read as args.X (getattr(args, "X", default) excluded)"""
-    tree = ast.parse(inspect.getsource(fn))
-    return {n.attr for n in ast.walk(tree)
-            if isinstance(n, ast.Attribute) and isinstance(n.value, ast.Name) and n.value.id == "args"}
-
-
-def test_tile_args_cover_run_once_mux():
-    need = _args_read(bench_tile.run_once_mux) | _args_read(bench_tile.start_producer)
-    for prods, rate in ((1, 0.0), (2, 16e6)):
-        ns = bench.tile_args(prods, rate)
-        missing = sorted(a for a in need if not hasattr(ns, a))
-        assert not missing, f"bench.tile_args lacks {missing}"
+def test_tile_cmd_parses():
+    cmd = bench.tile_cmd(0, [3, 4, 5, 6], "/tmp/x.npz", "/tmp/x.jsonl")
+    assert cmd[1].endswith("tools/bench_tile.py")
+    args = bench_tile.make_parser().parse_args(cmd[2:])
+    assert args.mux == 1 and args.gpu_parse == 2 and args.producers_same_as_tiles == 1
+    assert args.payload_npz == "/tmp/x.npz" and args.cpu_list == "3,4,5,6" and args.device == 0
+    assert args.hw_queues == bench.HW_QUEUES and args.reps == bench.TILE_REPS
+    assert args.depth_lg == 21 and args.depth_lg_paced == 19        # a prefill fits its links
+    runs = [tuple(float(x) for x in r.split(",")) for r in args.sweep.split(";")]
+    assert len(runs) == len(bench.TILE_RUNS)
+    for (name, tiles_n, prods, rate), (t, b, k, r) in zip(bench.TILE_RUNS, runs):
+        assert tiles_n == prods and t == tiles_n and r == rate and name
+        assert (b, k) == (bench.TILE_BATCH, bench.TILE_INFLIGHT)
 
 
 def test_tile_runs_shape():
+    names = [r[0] for r in bench.TILE_RUNS]
+    assert "mux1_capacity" in names and "mux2_capacity" in names      # the ratio line needs both
     for name, tiles_n, prods, rate in bench.TILE_RUNS:
         assert tiles_n >= 1 and prods >= 1 and (rate > 0 or rate == -1.0) and name
-        assert bench.tile_args(prods, rate).depth_lg == (21 if rate < 0 else 19)   # a prefill fits its links

@@ -28,13 +28,13 @@ for i, a in enumerate(sys.argv):
             os.environ["GPU_MAX_HW_QUEUES"] = v
         break
 else:
-    os.environ["GPU_MAX_HW_QUEUES"] = "16"
+    os.environ["GPU_MAX_HW_QUEUES"] = "32"
 
 import firedancer_amd as fa  # noqa: E402
 from firedancer_amd import tile, workload  # noqa: E402
 
 
-def main():
+def make_parser():
     ap = argparse.ArgumentParser()
     ap.add_argument("--txns", type=int, default=200_000)
     ap.add_argument("--gpus", type=int, default=1)
@@ -62,20 +62,37 @@ def main():
     ap.add_argument("--cpu-offset", type=int, default=0,
                     help="skip this many of workload.physical_cpus() before pinning (CPU 0 takes interrupts)")
     ap.add_argument("--reps", type=int, default=1, help="repeat every run of the sweep")
-    ap.add_argument("--hw-queues", type=int, default=16,
+    ap.add_argument("--hw-queues", type=int, default=32,
                     help="GPU_MAX_HW_QUEUES for this process (applied before HIP starts; 0: the environment's)")
     ap.add_argument("--out", default="")
     ap.add_argument("--sweep", default="", help="';'-separated runs of 'tiles,batch,inflight,rate' over the same txns")
-    args = ap.parse_args()
+    ap.add_argument("--payload-npz", default="",
+                    help="take the frags from this .npz (arena, offs, sizes, modes, n_sig: bench.py's tile lines) "
+                         "instead of generating --txns")
+    ap.add_argument("--depth-lg-paced", type=int, default=0,
+                    help="log2 of the link depth for paced runs (rate > 0); 0: --depth-lg")
+    ap.add_argument("--cpu-list", default="", help="','-separated CPUs to pin producers and tiles to, in order")
+    ap.add_argument("--device", type=int, default=-1, help="the GPU every tile's engine uses (-1: tile k on k %% gpus)")
+    return ap
 
+
+def main():
+    args = make_parser().parse_args()
     t0 = time.time()
-    gen = workload.cfg3 if args.multi else workload.cfg1
-    a, t, modes = gen(args.txns, seed=0x5EED0005)
-    ps = workload.payloads(a, t)
-    arena, offs, sizes = workload.pack_payloads(ps)
-    n_sig = int(t["sig_cnt"].sum())
-    print(f"[bench_tile] generated {len(ps)} txns / {n_sig} sigs in {time.time() - t0:.1f}s", flush=True)
-    del a, t
+    if args.payload_npz:
+        z = np.load(args.payload_npz)
+        arena, offs, sizes, modes, n_sig = z["arena"], z["offs"], z["sizes"], z["modes"], int(z["n_sig"])
+        ps = [arena[o:o + n].tobytes() for o, n in zip(offs.tolist(), sizes.tolist())]
+    else:
+        gen = workload.cfg3 if args.multi else workload.cfg1
+        a, t, modes = gen(args.txns, seed=0x5EED0005)
+        ps = workload.payloads(a, t)
+        arena, offs, sizes = workload.pack_payloads(ps)
+        n_sig = int(t["sig_cnt"].sum())
+        del a, t
+    print(f"[bench_tile] {len(ps)} txns / {n_sig} sigs ready in {time.time() - t0:.1f}s", flush=True)
+    cpus = [int(x) for x in args.cpu_list.split(",") if x] or None
+    depth_lg = args.depth_lg
 
     runs = [tuple(float(x) for x in r.split(",")) for r in args.sweep.split(";") if r] or \
         [(args.tiles or args.gpus, args.batch, args.inflight, args.rate)]
@@ -85,7 +102,12 @@ def main():
     for tiles_n, batch, inflight, rate in runs:
         if args.producers_same_as_tiles:
             args.producers = int(tiles_n)
-        res = run_once(args, ps, arena, offs, sizes, n_sig, modes, int(tiles_n), int(batch), int(inflight), rate)
+        args.depth_lg = args.depth_lg_paced if rate > 0 and args.depth_lg_paced else depth_lg
+        if args.mux:
+            res = run_once_mux(args, ps, arena, offs, sizes, n_sig, modes, int(tiles_n), int(batch), int(inflight),
+                               rate, cpus=cpus, device=args.device if args.device >= 0 else None)
+        else:
+            res = run_once(args, ps, arena, offs, sizes, n_sig, modes, int(tiles_n), int(batch), int(inflight), rate)
         line = json.dumps(res)
         print(line, flush=True)
         lines.append(line)
