@@ -27,14 +27,16 @@ import numpy as np
 
 REPO = os.path.dirname(os.path.abspath(__file__))
 
-# HIP hardware queues of this process, set before the runtime starts: every
-# ring slot, device batch and tile engine owns a stream, and HIP maps streams
-# onto GPU_MAX_HW_QUEUES hardware queues (4 by default); two streams on one
-# queue serialise, so with the cfg5 tile lines' two engines x eight slots
-# beside the headline engine the tiles' batches would queue behind each other
-# (profiles/r03/hwq_*.jsonl, mux_sweep/r03s_*.jsonl: two tiles 35 M txn/s
-# with 16 queues, 44 M with 32).  32 is the most this pool allows.
-HW_QUEUES = 32
+# HIP hardware queues, set before the runtime starts: every ring slot, device
+# batch and tile engine owns a stream, and HIP maps a process's streams onto
+# GPU_MAX_HW_QUEUES hardware queues (4 by default); two busy streams on one
+# queue serialise.  This process (headline batches, latency ring slots) takes
+# HW_QUEUES; the cfg5 tile lines run in a child process with TILE_HW_QUEUES
+# for their two engines x eight slots (two tiles: 35 M txn/s with 16 queues,
+# 44 M with 32, profiles/r03/mux_sweep/r03s_*.jsonl).  Every queue a process
+# opens stays mapped on the device, so this process keeps to a few.
+HW_QUEUES = 8
+TILE_HW_QUEUES = 32
 os.environ["GPU_MAX_HW_QUEUES"] = str(HW_QUEUES)
 sys.path.insert(0, REPO)
 
@@ -318,14 +320,14 @@ def sync_latency(arena, txns, calls=1000, threads=64):
 
 TILE_RUNS = (  # name, verify tiles, quic links (producers), offered txn/s (-1: prefilled links, the tiles' capacity)
     ("mux1_capacity", 1, 1, -1.0),
-    ("mux1_paced_16M", 1, 1, 16e6),
+    ("mux1_paced_16M", 1, 2, 16e6),
     ("mux2_capacity", 2, 2, -1.0),
-    ("mux2_paced_32M", 2, 2, 32e6),
+    ("mux2_paced_32M", 2, 4, 32e6),
 )
 TILE_BATCH, TILE_INFLIGHT = 16384, 8   # txns per GPU batch, batches in flight per tile
 
 
-TILE_REPS = 3   # a capacity run drains 1M frags in a few tens of ms: the median of three
+TILE_REPS = 5   # a capacity run drains 1M frags in a few tens of ms: the median of five
 
 
 def tile_cmd(device, cpus, npz, out, runs=TILE_RUNS):
@@ -334,10 +336,10 @@ def tile_cmd(device, cpus, npz, out, runs=TILE_RUNS):
     its HIP runtime gives the tile engines' slot streams hardware queues of
     their own, instead of the ones this process's headline, latency and ingest
     engines already hold (shared queues serialise the tiles' batches)."""
-    sweep = ";".join(f"{tiles_n},{TILE_BATCH},{TILE_INFLIGHT},{rate:g}" for _, tiles_n, _, rate in runs)
+    sweep = ";".join(f"{tiles_n},{TILE_BATCH},{TILE_INFLIGHT},{rate:g},{prods}" for _, tiles_n, prods, rate in runs)
     cmd = [sys.executable, os.path.join(REPO, "tools", "bench_tile.py"), "--mux", "1", "--gpu-parse", "2",
            "--multi", "0", "--producers-same-as-tiles", "1", "--depth-lg", "21", "--depth-lg-paced", "19",
-           "--wait-us", "200", "--pin", "1", "--hw-queues", str(HW_QUEUES), "--reps", str(TILE_REPS),
+           "--wait-us", "200", "--pin", "1", "--hw-queues", str(TILE_HW_QUEUES), "--reps", str(TILE_REPS),
            "--payload-npz", npz, "--device", str(device), "--sweep", sweep, "--out", out]
     if cpus:
         cmd += ["--cpu-list", ",".join(str(c) for c in cpus)]
@@ -353,7 +355,8 @@ def tile_lines(device, arena, txns, modes, cpus, runs=TILE_RUNS):
     in dcache, parses, verifies, tags it and writes the out frag into the
     registered out dcache; the tile core only moves frag metadata.  Over
     this rank's cfg1 txns as raw frags.  T tiles read P quic->verify links
-    round robin (every verify tile reads every QUIC tile's link,
+    round robin (P = T for capacity, 2T paced: one producer thread copies
+    ~12 M frags/s; every verify tile reads every QUIC tile's link,
     fd_frankendancer.c:131-133), one engine per tile on this GPU, 16K-txn
     batches, 8 in flight, producers and tiles pinned to their own cores, in
     a child process (tile_cmd).  Every run checks that exactly the verified
@@ -387,8 +390,9 @@ def tile_lines(device, arena, txns, modes, cpus, runs=TILE_RUNS):
                                               out["tile_mux1_capacity_txns_per_s"], 3)
     out["tile_config"] = ("fdgpu_vmux on fdt_mux_run (the reference's mux-callback verify tile), payload gather, "
                           "fd_txn_parse, verify, dedup tag and out-frag assembly on the GPU; muxT: T verify tiles "
-                          "reading T quic->verify links (one producer thread each), one engine per tile on this GPU, "
-                          f"cfg1 frags, {TILE_BATCH}-txn batches, {TILE_INFLIGHT} in flight, {HW_QUEUES} HIP hardware "
+                          "reading P quic->verify links (one producer thread each; P = T for capacity, 2T paced), one engine "
+                          "per tile on this GPU, "
+                          f"cfg1 frags, {TILE_BATCH}-txn batches, {TILE_INFLIGHT} in flight, {TILE_HW_QUEUES} HIP hardware "
                           "queues, in a child process (tools/bench_tile.py); capacity: every frag published into "
                           "2^21-deep links before the tiles start, timed from tile start to the last outcome; "
                           f"paced_R: R txn/s offered in total into 2^19-deep links while the tiles run; median of "

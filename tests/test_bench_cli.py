@@ -20,13 +20,14 @@ def test_tile_cmd_parses():
     args = bench_tile.make_parser().parse_args(cmd[2:])
     assert args.mux == 1 and args.gpu_parse == 2 and args.producers_same_as_tiles == 1
     assert args.payload_npz == "/tmp/x.npz" and args.cpu_list == "3,4,5,6" and args.device == 0
-    assert args.hw_queues == bench.HW_QUEUES and args.reps == bench.TILE_REPS
+    assert args.hw_queues == bench.TILE_HW_QUEUES and args.reps == bench.TILE_REPS
     assert args.depth_lg == 21 and args.depth_lg_paced == 19        # a prefill fits its links
     runs = [tuple(float(x) for x in r.split(",")) for r in args.sweep.split(";")]
     assert len(runs) == len(bench.TILE_RUNS)
-    for (name, tiles_n, prods, rate), (t, b, k, r) in zip(bench.TILE_RUNS, runs):
-        assert tiles_n == prods and t == tiles_n and r == rate and name
+    for (name, tiles_n, prods, rate), (t, b, k, r, p) in zip(bench.TILE_RUNS, runs):
+        assert t == tiles_n and p == prods and r == rate and name
         assert (b, k) == (bench.TILE_BATCH, bench.TILE_INFLIGHT)
+        assert rate > 0 or prods == tiles_n        # a prefilled run gives every link the whole stream
 
 
 def test_tile_runs_shape():

@@ -65,7 +65,8 @@ def make_parser():
     ap.add_argument("--hw-queues", type=int, default=32,
                     help="GPU_MAX_HW_QUEUES for this process (applied before HIP starts; 0: the environment's)")
     ap.add_argument("--out", default="")
-    ap.add_argument("--sweep", default="", help="';'-separated runs of 'tiles,batch,inflight,rate' over the same txns")
+    ap.add_argument("--sweep", default="",
+                    help="';'-separated runs of 'tiles,batch,inflight,rate[,producers]' over the same txns")
     ap.add_argument("--payload-npz", default="",
                     help="take the frags from this .npz (arena, offs, sizes, modes, n_sig: bench.py's tile lines) "
                          "instead of generating --txns")
@@ -99,9 +100,11 @@ def main():
     runs = [r for r in runs for _ in range(max(1, args.reps))]
     ok = True
     lines = []
-    for tiles_n, batch, inflight, rate in runs:
-        if args.producers_same_as_tiles:
-            args.producers = int(tiles_n)
+    prods0 = args.producers
+    for run in runs:
+        tiles_n, batch, inflight, rate = run[:4]
+        # a fifth field sets the run's quic links (producers)
+        args.producers = int(run[4]) if len(run) > 4 else int(tiles_n) if args.producers_same_as_tiles else prods0
         args.depth_lg = args.depth_lg_paced if rate > 0 and args.depth_lg_paced else depth_lg
         if args.mux:
             res = run_once_mux(args, ps, arena, offs, sizes, n_sig, modes, int(tiles_n), int(batch), int(inflight),
