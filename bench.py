@@ -619,7 +619,7 @@ def main():
     extras = {}
     if not args.no_extras:
         extras = latency_and_pcie(eng, arena, txns, args.latency_batch, args.latency_batches,
-                                  pin_cpu=cpus[0] if cpus else None)
+                                  pin_cpu=(cpus[1] if len(cpus) > 1 else cpus[0]) if cpus else None)
         extras["latency_batch_txns"] = args.latency_batch
         if dist.rank == 0:
             extras.update(sync_latency(arena, txns))
