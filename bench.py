@@ -325,12 +325,16 @@ TILE_RUNS = (  # name, verify tiles, quic links (producers), offered txn/s (-1: 
     ("mux2_paced_32M", 2, 4, 32e6),
 )
 TILE_BATCH, TILE_INFLIGHT = 16384, 8   # txns per GPU batch, batches in flight per tile
+TILE_RUNS_CFG3 = (  # the same tile over cfg3 frags (1-12 signatures, payloads up to the 1232-B MTU: SURVEY 8(d) cfg5)
+    ("mux1_capacity_cfg3", 1, 1, -1.0),
+    ("mux2_capacity_cfg3", 2, 2, -1.0),
+)
 
 
 TILE_REPS = 5   # a capacity run drains 1M frags in a few tens of ms: the median of five
 
 
-def tile_cmd(device, cpus, npz, out, runs=TILE_RUNS):
+def tile_cmd(device, cpus, npz, out, runs=TILE_RUNS, multi=0):
     """tools/bench_tile.py's command line for the cfg5 runs (tests/test_bench_cli.py
     parses it with bench_tile's own parser).  The tiles run in a child process:
     its HIP runtime gives the tile engines' slot streams hardware queues of
@@ -338,7 +342,7 @@ def tile_cmd(device, cpus, npz, out, runs=TILE_RUNS):
     engines already hold (shared queues serialise the tiles' batches)."""
     sweep = ";".join(f"{tiles_n},{TILE_BATCH},{TILE_INFLIGHT},{rate:g},{prods}" for _, tiles_n, prods, rate in runs)
     cmd = [sys.executable, os.path.join(REPO, "tools", "bench_tile.py"), "--mux", "1", "--gpu-parse", "2",
-           "--multi", "0", "--producers-same-as-tiles", "1", "--depth-lg", "21", "--depth-lg-paced", "19",
+           "--multi", str(int(multi)), "--producers-same-as-tiles", "1", "--depth-lg", "21", "--depth-lg-paced", "19",
            "--wait-us", "200", "--pin", "1", "--hw-queues", str(TILE_HW_QUEUES), "--reps", str(TILE_REPS),
            "--payload-npz", npz, "--device", str(device), "--sweep", sweep, "--out", out]
     if cpus:
@@ -346,21 +350,9 @@ def tile_cmd(device, cpus, npz, out, runs=TILE_RUNS):
     return cmd
 
 
-def tile_lines(device, arena, txns, modes, cpus, runs=TILE_RUNS):
-    """BASELINE configs[4] (cfg5) on this rank's GPU: the verify tile in the
-    reference's shape -- the fd_verify.c:232-246 callbacks (fdgpu_vmux) on
-    the mux loop (fdt_mux_run, FD_MUX_FLAG_COPY | MANUAL_PUBLISH), tcache and
-    publish in order -- with the byte work on the GPU (gpu_parse 2,
-    fdgpu_submit_frags_io): the device reads each payload in the registered
-    in dcache, parses, verifies, tags it and writes the out frag into the
-    registered out dcache; the tile core only moves frag metadata.  Over
-    this rank's cfg1 txns as raw frags.  T tiles read P quic->verify links
-    round robin (P = T for capacity, 2T paced: one producer thread copies
-    ~12 M frags/s; every verify tile reads every QUIC tile's link,
-    fd_frankendancer.c:131-133), one engine per tile on this GPU, 16K-txn
-    batches, 8 in flight, producers and tiles pinned to their own cores, in
-    a child process (tile_cmd).  Every run checks that exactly the verified
-    txns were published."""
+def _tile_child(device, cpus, arena, txns, modes, runs, tag=""):
+    """tools/bench_tile.py in a child process over these txns as raw frags:
+    {tile_<name>_...} per run (median of TILE_REPS)."""
     import subprocess
     import tempfile
     from firedancer_amd import workload
@@ -370,7 +362,8 @@ def tile_lines(device, arena, txns, modes, cpus, runs=TILE_RUNS):
     with tempfile.TemporaryDirectory() as td:
         npz, res_path = os.path.join(td, "frags.npz"), os.path.join(td, "tile.jsonl")
         np.savez(npz, arena=parena, offs=poffs, sizes=psizes, modes=modes, n_sig=int(txns["sig_cnt"].sum()))
-        r = subprocess.run(tile_cmd(device, cpus, npz, res_path, runs), capture_output=True, text=True, timeout=600)
+        r = subprocess.run(tile_cmd(device, cpus, npz, res_path, runs, multi=tag == "cfg3"), capture_output=True,
+                           text=True, timeout=600)
         if r.returncode not in (0, 1) or not os.path.exists(res_path):
             raise RuntimeError(f"tools/bench_tile.py failed ({r.returncode}): {r.stderr[-2000:]}")
         res_all = [json.loads(x) for x in open(res_path) if x.strip()]
@@ -383,16 +376,41 @@ def tile_lines(device, arena, txns, modes, cpus, runs=TILE_RUNS):
         out[f"tile_{name}_txns_per_s_runs"] = [x["txns_per_s"] for x in reps]
         lat = res["batch_latency_ms"]
         out[f"tile_{name}_txns_per_s"] = res["txns_per_s"]
+        if tag:
+            out[f"tile_{name}_sigs_per_s"] = res["sigs_per_s"]
         out[f"tile_{name}_batch_latency_ms_p50_p99"] = [lat["p50"], lat["p99"]]
         out[f"tile_{name}_overruns"] = max(x["counters"]["overrun"] for x in reps)
         out[f"tile_{name}_published_ok"] = all(x["counters"]["published"] == x["expected_published"] for x in reps)
+    return out
+
+
+def tile_lines(device, arena, txns, modes, cpus, cfg3=None):
+    """BASELINE configs[4] (cfg5) on this rank's GPU: the verify tile in the
+    reference's shape -- the fd_verify.c:232-246 callbacks (fdgpu_vmux) on
+    the mux loop (fdt_mux_run, FD_MUX_FLAG_COPY | MANUAL_PUBLISH), tcache and
+    publish in order -- with the byte work on the GPU (gpu_parse 2,
+    fdgpu_submit_frags_io): the device reads each payload in the registered
+    in dcache, parses, verifies, tags it and writes the out frag into the
+    registered out dcache; the tile core only moves frag metadata.  Over
+    this rank's cfg1 txns as raw frags (TILE_RUNS) and, given `cfg3`, over
+    the cfg3 txns too (TILE_RUNS_CFG3, SURVEY 8(d)'s cfg5 generator).  T
+    tiles read P quic->verify links round robin (P = T for capacity, 2T
+    paced: one producer thread copies ~12 M frags/s; every verify tile reads
+    every QUIC tile's link, fd_frankendancer.c:131-133), one engine per tile
+    on this GPU, 16K-txn batches, 8 in flight, producers and tiles pinned to
+    their own cores, in a child process (tile_cmd).  Every run checks that
+    exactly the verified txns were published."""
+    out = _tile_child(device, cpus, arena, txns, modes, TILE_RUNS)
     out["tile_mux2_vs_mux1_capacity"] = round(out["tile_mux2_capacity_txns_per_s"] /
                                               out["tile_mux1_capacity_txns_per_s"], 3)
+    if cfg3 is not None:
+        out.update(_tile_child(device, cpus, *cfg3, TILE_RUNS_CFG3, tag="cfg3"))
+        out["tile_cfg3_txns"] = len(cfg3[1])
     out["tile_config"] = ("fdgpu_vmux on fdt_mux_run (the reference's mux-callback verify tile), payload gather, "
                           "fd_txn_parse, verify, dedup tag and out-frag assembly on the GPU; muxT: T verify tiles "
                           "reading P quic->verify links (one producer thread each; P = T for capacity, 2T paced), one engine "
                           "per tile on this GPU, "
-                          f"cfg1 frags, {TILE_BATCH}-txn batches, {TILE_INFLIGHT} in flight, {TILE_HW_QUEUES} HIP hardware "
+                          f"cfg1 frags (_cfg3: cfg3 frags), {TILE_BATCH}-txn batches, {TILE_INFLIGHT} in flight, {TILE_HW_QUEUES} HIP hardware "
                           "queues, in a child process (tools/bench_tile.py); capacity: every frag published into "
                           "2^21-deep links before the tiles start, timed from tile start to the last outcome; "
                           f"paced_R: R txn/s offered in total into 2^19-deep links while the tiles run; median of "
@@ -518,14 +536,14 @@ def pmc_traffic():
     return None, None
 
 
-def cfg3_rate(eng, eng_nobucket, n_txn, seed):
+def cfg3_rate(eng, eng_nobucket, cfg3):
     """BASELINE configs[2] (cfg3): 1-12 signatures sharing one message, msg up
     to the 1232-B MTU, 10% with one corrupted signature or message bit;
     device-resident, mean of HIP-event-timed verifies (secondary line, not
     `value`).  Timed with the signatures grouped by SHA-512 block count (the
     engine default) and in transaction order (FDGPU_FLAG_NO_BUCKET)."""
-    from firedancer_amd import workload
-    arena, txns, modes = workload.cfg3(n_txn, seed=seed)
+    arena, txns, modes = cfg3
+    n_txn = len(txns)
     out = {}
     for tag, e in (("", eng), ("_unbucketed", eng_nobucket)):
         b = e.upload(arena, txns)
@@ -623,15 +641,16 @@ def main():
         extras["latency_batch_txns"] = args.latency_batch
         if dist.rank == 0:
             extras.update(sync_latency(arena, txns))
+        cfg3 = workload.cfg3(args.cfg3_txns, seed=workload.CFG3_SEED + dist.rank) if args.cfg3_txns else None
         if args.tile:
-            tl = tile_lines(device, arena, txns, modes, cpus)
+            tl = tile_lines(device, arena, txns, modes, cpus, cfg3=cfg3)
             tl["tile_mux1_capacity_txns_per_s_node"] = round(dist.sum(tl["tile_mux1_capacity_txns_per_s"]), 1)
             tl["tile_published_ok_all_ranks"] = dist.sum(
                 1 if all(v for k, v in tl.items() if k.endswith("_published_ok")) else 0) == dist.world
             extras.update(tl)
         if args.cfg3_txns:
             eng_nb = VerifyEngine(device, max_txn=1024, ring_depth=1, bucket=False)
-            extras.update(cfg3_rate(eng, eng_nb, args.cfg3_txns, workload.CFG3_SEED + dist.rank))
+            extras.update(cfg3_rate(eng, eng_nb, cfg3))
             eng_nb.close()
         if args.keypool_txns:
             extras.update(key_cache_rate(eng, device, args.keypool_txns, workload.CFG1_SEED + 0x700 + dist.rank))

@@ -35,3 +35,11 @@ def test_tile_runs_shape():
     assert "mux1_capacity" in names and "mux2_capacity" in names      # the ratio line needs both
     for name, tiles_n, prods, rate in bench.TILE_RUNS:
         assert tiles_n >= 1 and prods >= 1 and (rate > 0 or rate == -1.0) and name
+
+
+def test_tile_cmd_cfg3():
+    cmd = bench.tile_cmd(1, [], "/tmp/y.npz", "/tmp/y.jsonl", bench.TILE_RUNS_CFG3, multi=1)
+    args = bench_tile.make_parser().parse_args(cmd[2:])
+    assert args.multi == 1 and args.device == 1 and args.cpu_list == ""
+    assert len(args.sweep.split(";")) == len(bench.TILE_RUNS_CFG3)
+    assert all(r[3] == -1.0 for r in bench.TILE_RUNS_CFG3)       # capacity lines
