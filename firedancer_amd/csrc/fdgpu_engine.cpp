@@ -31,6 +31,7 @@
 
 #include "../../include/fd_ed25519_gpu.h"
 #include "fdgpu_internal.h"
+#include "fdt_parse.h"
 
 #define FDT_TXN_MAX_SZ_BYTES 852u   /* FD_TXN_MAX_SZ (fd_txn.h:98): one parsed fd_txn_t record */
 #define FDT_TXN_MTU_BYTES 1232u     /* FD_TXN_MTU (fd_txn.h:103) */
@@ -756,7 +757,7 @@ int64_t fdgpu_submit_frags(fdgpu_engine_t *e, uint8_t const *arena, uint64_t are
       set_err("frag %llu: out of arena or trailer bounds", (unsigned long long)t);
       return FDGPU_ERR_INVAL;
     }
-    bound += fdgpu_frag_sig_bound(f.sz);
+    bound += fdt_frag_sig_bound(f.sz);
   }
   if (bound > e->cfg.max_sig) { set_err("batch may exceed max_sig (%llu)", (unsigned long long)e->cfg.max_sig); return FDGPU_ERR_INVAL; }
   std::lock_guard<std::mutex> lk(e->ring_mu);
@@ -861,7 +862,7 @@ int64_t fdgpu_submit_frags_io(fdgpu_engine_t *e, fdgpu_frag_io_t const *fio, uin
     h_fx[t] = fdgpu_frag_ex_t{(uint32_t)dev_off, f.sz, f.out_off, f.out_cap};
     dev_off += q;
     if (dev_off > e->cfg.max_arena) { set_err("frags exceed the engine's arena"); return FDGPU_ERR_INVAL; }
-    bound += fdgpu_frag_sig_bound(f.sz);
+    bound += fdt_frag_sig_bound(f.sz);
   }
   if (bound > e->cfg.max_sig) { set_err("batch may exceed max_sig (%llu)", (unsigned long long)e->cfg.max_sig); return FDGPU_ERR_INVAL; }
   const uint64_t sp1 = g_sp_on ? sp_now() : 0;
