@@ -37,6 +37,9 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 # opens stays mapped on the device, so this process keeps to a few.
 HW_QUEUES = 8
 TILE_HW_QUEUES = 32
+for _i, _a in enumerate(sys.argv):          # --hw-queues N (this process), read before HIP starts
+    if _a.startswith("--hw-queues"):
+        HW_QUEUES = int(_a.split("=", 1)[1] if "=" in _a else sys.argv[_i + 1])
 os.environ["GPU_MAX_HW_QUEUES"] = str(HW_QUEUES)
 sys.path.insert(0, REPO)
 
@@ -64,6 +67,9 @@ def parse():
     ap.add_argument("--latency-batch", type=int, default=65536)
     ap.add_argument("--cpu-sample", type=int, default=1_000_000, help="txns timed on the CPU oracle (bounded sample)")
     ap.add_argument("--no-extras", action="store_true", help="only the timed device-resident loop (profiling)")
+    ap.add_argument("--hw-queues", type=int, default=HW_QUEUES,
+                    help="GPU_MAX_HW_QUEUES of this process (applied before HIP starts; the tile child uses "
+                         f"{TILE_HW_QUEUES})")
     ap.add_argument("--queues", type=int, default=2,
                     help="device batches verified round-robin, each on its own HIP stream (1: one stream)")
     ap.add_argument("--cfg3-txns", type=int, default=150_000,
