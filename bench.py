@@ -328,7 +328,7 @@ TILE_RUNS = (  # name, verify tiles, quic links (producers), offered txn/s (-1: 
     ("mux1_capacity", 1, 1, -1.0),
     ("mux1_paced_16M", 1, 2, 16e6),
     ("mux2_capacity", 2, 2, -1.0),
-    ("mux2_paced_32M", 2, 4, 32e6),
+    ("mux2_paced_24M", 2, 4, 24e6),
 )
 TILE_BATCH, TILE_INFLIGHT = 16384, 8   # txns per GPU batch, batches in flight per tile
 TILE_RUNS_CFG3 = (  # the same tile over cfg3 frags (1-12 signatures, payloads up to the 1232-B MTU: SURVEY 8(d) cfg5)
