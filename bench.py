@@ -136,10 +136,10 @@ class Dist:
         see overlapping affinities (one process per GPU, unpinned), the union
         of physical cores is split into disjoint per-rank ranges, so the tile
         threads and the oracle of 8 ranks never share a core."""
-        from firedancer_amd.workload import physical_cpus, BOX_CPU_SHARE
+        from firedancer_amd.workload import physical_cpus, idle_first, BOX_CPU_SHARE
         mine = physical_cpus(limit=1 << 20)
         if not self.dist:
-            return mine[:BOX_CPU_SHARE]
+            return idle_first(mine)[:BOX_CPU_SHARE]
         every = [None] * self.world
         self.dist.all_gather_object(every, mine)
         seen = set()
@@ -148,7 +148,7 @@ class Dist:
             overlap |= bool(seen & set(c))
             seen |= set(c)
         if not overlap:
-            return mine[:BOX_CPU_SHARE]
+            return idle_first(mine)[:BOX_CPU_SHARE]
         union = sorted(seen)
         k = max(1, len(union) // self.world)
         part = union[self.rank * k:(self.rank + 1) * k] or union[-k:]

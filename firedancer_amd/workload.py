@@ -85,6 +85,35 @@ def default_threads():
     return max(1, min(n, BOX_CPU_SHARE))
 
 
+def _cpu_busy_ticks():
+    """{cpu: busy jiffies} from /proc/stat (total minus idle and iowait)"""
+    out = {}
+    try:
+        with open("/proc/stat") as f:
+            for line in f:
+                if line.startswith("cpu") and line[3:4].isdigit():
+                    v = line.split()
+                    t = [int(x) for x in v[1:]]
+                    out[int(v[0][3:])] = sum(t) - t[3] - (t[4] if len(t) > 4 else 0)
+    except OSError:
+        pass
+    return out
+
+
+def idle_first(cpus, sample_s=0.2):
+    """`cpus` reordered least busy first over a short sample of /proc/stat
+    (ties keep their order).  On a box whose cores other tenants share, a
+    pinned tile or producer thread on a busy core runs at a fraction of its
+    speed; the benches pin to the quietest cores they may use."""
+    import time
+    a = _cpu_busy_ticks()
+    time.sleep(sample_s)
+    b = _cpu_busy_ticks()
+    if not a or not b:
+        return list(cpus)
+    return sorted(cpus, key=lambda c: (b.get(c, 0) - a.get(c, 0), cpus.index(c)))
+
+
 def physical_cpus(limit=BOX_CPU_SHARE):
     """One logical CPU per physical core among the CPUs this process may run
     on (SMT siblings skipped; /sys topology), at most `limit`: the CPU
