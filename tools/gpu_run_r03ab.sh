@@ -2,7 +2,7 @@
 set -o pipefail
 export TMPDIR=/tmp
 o=gpurun_out/r03ab; mkdir -p $o
-for r in 1 2; do
+for r in 1; do
   echo "[$(date +%T)] run $r"
   timeout -k 10 600 python3 bench.py --adv-txns 0 --keypool-txns 0 > $o/b$r.json 2> $o/b$r.err || { tail $o/b$r.err; exit 1; }
   python3 -c "
