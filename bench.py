@@ -326,10 +326,17 @@ def sync_latency(arena, txns, calls=1000, threads=64):
 
 TILE_RUNS = (  # name, verify tiles, quic links (producers), offered txn/s (-1: prefilled links, the tiles' capacity)
     ("mux1_capacity", 1, 1, -1.0),
+    ("mux1_paced_12M", 1, 2, 12e6),
     ("mux1_paced_16M", 1, 2, 16e6),
     ("mux2_capacity", 2, 2, -1.0),
+    ("mux2_paced_20M", 2, 4, 20e6),
     ("mux2_paced_24M", 2, 4, 24e6),
 )
+# quic -> verify link depth: paced runs at the reference's (config->tiles.verify.receive_buffer_size,
+# default.toml:888-893: 16384, fd_frankendancer.c:59), with the stream published TILE_PACED_REPS times
+# over (>= 30 x the depth per link: the producers can lap the tiles); capacity runs prefill every frag
+# before the tiles start, so their links hold the whole stream
+TILE_DEPTH_LG_PACED, TILE_DEPTH_LG_PREFILL, TILE_PACED_REPS = 14, 21, 2
 TILE_BATCH, TILE_INFLIGHT = 16384, 8   # txns per GPU batch, batches in flight per tile
 TILE_RUNS_CFG3 = (  # the same tile over cfg3 frags (1-12 signatures, payloads up to the 1232-B MTU: SURVEY 8(d) cfg5)
     ("mux1_capacity_cfg3", 1, 1, -1.0),
@@ -348,7 +355,8 @@ def tile_cmd(device, cpus, npz, out, runs=TILE_RUNS, multi=0):
     engines already hold (shared queues serialise the tiles' batches)."""
     sweep = ";".join(f"{tiles_n},{TILE_BATCH},{TILE_INFLIGHT},{rate:g},{prods}" for _, tiles_n, prods, rate in runs)
     cmd = [sys.executable, os.path.join(REPO, "tools", "bench_tile.py"), "--mux", "1", "--gpu-parse", "2",
-           "--multi", str(int(multi)), "--producers-same-as-tiles", "1", "--depth-lg", "21", "--depth-lg-paced", "19",
+           "--multi", str(int(multi)), "--producers-same-as-tiles", "1", "--depth-lg", str(TILE_DEPTH_LG_PREFILL),
+           "--depth-lg-paced", str(TILE_DEPTH_LG_PACED), "--paced-reps", str(TILE_PACED_REPS),
            "--wait-us", "200", "--pin", "1", "--hw-queues", str(TILE_HW_QUEUES), "--reps", str(TILE_REPS),
            "--payload-npz", npz, "--device", str(device), "--sweep", sweep, "--out", out]
     if cpus:
@@ -385,8 +393,16 @@ def _tile_child(device, cpus, arena, txns, modes, runs, tag=""):
         if tag:
             out[f"tile_{name}_sigs_per_s"] = res["sigs_per_s"]
         out[f"tile_{name}_batch_latency_ms_p50_p99"] = [lat["p50"], lat["p99"]]
+        out[f"tile_{name}_link_depth"] = res["link_depth"]
+        if rate > 0:       # what the producers achieved (the line's name is the rate asked of them)
+            out[f"tile_{name}_offered_txns_per_s"] = res["offered_txns_per_s"]
+        # frags lost to the producers, worst of the runs: overruns = lapped (before the device read
+        # them) + skipped while the mux lagged + overwritten while it read their metadata
         out[f"tile_{name}_overruns"] = max(x["counters"]["overrun"] for x in reps)
-        out[f"tile_{name}_published_ok"] = all(x["counters"]["published"] == x["expected_published"] for x in reps)
+        out[f"tile_{name}_lapped"] = max(x["counters"]["lapped"] for x in reps)
+        out[f"tile_{name}_rescued"] = max(x["counters"]["rescued"] for x in reps)
+        out[f"tile_{name}_parse_fail"] = res["counters"]["parse_fail"]
+        out[f"tile_{name}_published_ok"] = all(x["published_ok"] for x in reps)
     return out
 
 
@@ -418,9 +434,12 @@ def tile_lines(device, arena, txns, modes, cpus, cfg3=None):
                           "per tile on this GPU, "
                           f"cfg1 frags (_cfg3: cfg3 frags), {TILE_BATCH}-txn batches, {TILE_INFLIGHT} in flight, {TILE_HW_QUEUES} HIP hardware "
                           "queues, in a child process (tools/bench_tile.py); capacity: every frag published into "
-                          "2^21-deep links before the tiles start, timed from tile start to the last outcome; "
-                          f"paced_R: R txn/s offered in total into 2^19-deep links while the tiles run; median of "
-                          f"{TILE_REPS} runs each")
+                          f"2^{TILE_DEPTH_LG_PREFILL}-deep links before the tiles start, timed from tile start to the "
+                          f"last outcome; paced_R: R txn/s asked of the producers in total (achieved: _offered_txns_per_s) "
+                          f"into {1 << TILE_DEPTH_LG_PACED}-deep links (the reference's receive_buffer_size) while the "
+                          f"tiles run, the stream published {TILE_PACED_REPS}x over; the lap guard on; overruns count "
+                          f"every frag lost to the producers (_lapped: before the GPU read it); median of {TILE_REPS} "
+                          "runs each")
     return out
 
 

@@ -112,7 +112,7 @@ def lib():
     L.fdgpu_submit_frags.restype = c.c_int64
     L.fdgpu_poll_frags.argtypes = [vp, c.c_int64, vp, vp, c.c_int]
     L.fdgpu_poll_frags.restype = c.c_int
-    L.fdgpu_submit_frags_io.argtypes = [vp, vp, c.c_uint64, vp, c.c_uint64, c.c_uint64]
+    L.fdgpu_submit_frags_io.argtypes = [vp, vp, c.c_uint64, vp, c.c_uint64, c.c_uint64, vp, c.c_uint64]
     L.fdgpu_submit_frags_io.restype = c.c_int64
     L.fdgpu_poll_frags_io.argtypes = [vp, c.c_int64, vp, vp, vp, c.c_int]
     L.fdgpu_poll_frags_io.restype = c.c_int

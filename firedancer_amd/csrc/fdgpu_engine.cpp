@@ -58,9 +58,12 @@ std::atomic<uint64_t> g_sp_loop{0}, g_sp_enq{0}, g_sp_calls{0}, g_sp_frags{0};
 inline uint64_t sp_now() { timespec ts; clock_gettime(CLOCK_MONOTONIC, &ts); return ts.tv_sec * 1000000000ull + ts.tv_nsec; }
 const bool g_sp_on = getenv("FDGPU_SUBMIT_PROF") && getenv("FDGPU_SUBMIT_PROF")[0] == '1';
 /* the last FDGPU_ST_RING fdgpu_submit calls of the process: {staging copy,
-   descriptor expansion, enqueue} ns (fdgpu_debug_submit_times) */
+   descriptor expansion, enqueue} ns (fdgpu_debug_submit_times).  Each call
+   writes the entry its fetch_add drew; the words are relaxed atomics, so
+   concurrent submitters and a reader never race (a reader may see a triple
+   that a writer is mid-way through, which is a diagnostic's tolerance) */
 constexpr uint64_t FDGPU_ST_RING = 8192;
-uint64_t g_st[FDGPU_ST_RING][3];
+std::atomic<uint64_t> g_st[FDGPU_ST_RING][3];
 std::atomic<uint64_t> g_st_n{0};
 }
 
@@ -500,7 +503,9 @@ static int64_t submit_slot(fdgpu_engine_t *e, Slot *s, uint64_t arena_sz, fdgpu_
     uint64_t st, t0, t1;
     ~Rec() {
       const uint64_t k = g_st_n.fetch_add(1, std::memory_order_relaxed) % FDGPU_ST_RING;
-      g_st[k][0] = st; g_st[k][1] = t1 - t0; g_st[k][2] = sp_now() - t1;
+      g_st[k][0].store(st, std::memory_order_relaxed);
+      g_st[k][1].store(t1 - t0, std::memory_order_relaxed);
+      g_st[k][2].store(sp_now() - t1, std::memory_order_relaxed);
     }
   } rec{t_stage, t0, t1};
   if (!slot_ws(*s, (uint64_t)ns)) return FDGPU_ERR_DEVICE;
@@ -652,7 +657,7 @@ uint64_t fdgpu_debug_submit_times(uint64_t *out, uint64_t max) {
   const uint64_t end = g_st_n.load();
   for (uint64_t i = 0; i < m; i++) {
     const uint64_t k = (end - m + i) % FDGPU_ST_RING;
-    out[3 * i] = g_st[k][0]; out[3 * i + 1] = g_st[k][1]; out[3 * i + 2] = g_st[k][2];
+    for (int j = 0; j < 3; j++) out[3 * i + j] = g_st[k][j].load(std::memory_order_relaxed);
   }
   return m;
 }
@@ -813,53 +818,80 @@ uint32_t fdgpu_frag_out_cap(uint32_t sz) {
 
 /* Gathered frag batches (the header's fdgpu_submit_frags_io): the device
    reads each payload from its registered host region (the in dcache) into
-   the slot arena, then parse -> scan -> expand -> verify -> finish on the
-   slot's stream; the finish kernel writes the out frags into the registered
-   out region and [codes][tags][out sizes] into the slot's pinned results,
-   both in place, and stores the completion word.  No copies are queued. */
+   the slot arena -- and, for a frag naming an in link, re-reads the frag's
+   mcache line afterwards (the overrun re-check) -- then parse -> expand ->
+   verify -> finish on the slot's stream; the finish kernel writes the out
+   frags into the registered out region and [codes][tags][out sizes] into the
+   slot's pinned results, both in place, and the stream stores the completion
+   word.  No copies are queued. */
 int64_t fdgpu_submit_frags_io(fdgpu_engine_t *e, fdgpu_frag_io_t const *fio, uint64_t n, uint8_t *out,
-                              uint64_t out_sz, uint64_t hash_seed) {
+                              uint64_t out_sz, uint64_t hash_seed, fdgpu_link_t const *links, uint64_t link_cnt) {
   const uint64_t sp0 = g_sp_on ? sp_now() : 0;
-  if (!e || (!fio && n) || (!out && out_sz)) { set_err("null argument"); return FDGPU_ERR_INVAL; }
+  if (!e || (!fio && n) || (!out && out_sz) || (!links && link_cnt)) { set_err("null argument"); return FDGPU_ERR_INVAL; }
   if (n > e->cfg.max_txn) { set_err("batch exceeds engine limits"); return FDGPU_ERR_INVAL; }
+  if (link_cnt > FDGPU_LINK_MAX) { set_err("more than %lu links", (unsigned long)FDGPU_LINK_MAX); return FDGPU_ERR_INVAL; }
   std::lock_guard<std::mutex> lk(e->ring_mu);
   const fdgpu_engine::Reg *ro = out_sz ? region_of(e, (uintptr_t)out, out_sz) : nullptr;
   if (out_sz && !ro) { set_err("out range not inside a registered region"); return FDGPU_ERR_INVAL; }
+  /* each named link's mcache: its device-side address (the lines are read
+     in place over the bus) */
+  uint64_t ldev[FDGPU_LINK_MAX], lmask[FDGPU_LINK_MAX];
+  for (uint64_t l = 0; l < link_cnt; l++) {
+    const uint64_t d = links[l].depth;
+    const fdgpu_engine::Reg *rm = (d && !(d & (d - 1))) ? region_of(e, (uintptr_t)links[l].mcache, d * 32u) : nullptr;
+    if (!rm || (links[l].mcache & 7u)) {
+      set_err("link %llu: mcache not inside a registered region (or a bad depth)", (unsigned long long)l);
+      return FDGPU_ERR_INVAL;
+    }
+    ldev[l] = rm->dbase + (links[l].mcache - rm->base);
+    lmask[l] = d - 1;
+  }
   HIPCHK(hipSetDevice(e->device), FDGPU_ERR_DEVICE);
   Slot *s = free_slot(e);
   if (!s) { set_err("all ring slots hold unpolled batches"); return FDGPU_ERR_FULL; }
   /* results: codes (padded to 64) + 8 B tags + 2 B sizes, in the trailer buffer */
   const uint64_t cb = (n + 63) & ~63ull, res_sz = cb + n * 10;
   if (!slot_frag_bufs(*s, e->cfg, res_sz)) return FDGPU_ERR_DEVICE;
-  /* the frag records, then (64-B aligned) the payload addresses, in pinned
-     memory the gather reads in place */
+  /* the frag records, then (64-B aligned) the payload addresses, then the
+     re-check pairs {line address, seq}, in pinned memory the gather reads in
+     place */
   const uint64_t src_at = (n * sizeof(fdgpu_frag_ex_t) + 63) & ~63ull;
+  const uint64_t chk_at = src_at + ((n * sizeof(uint64_t) + 63) & ~63ull);
   if (!s->h_io) {
-    const uint64_t m = e->cfg.max_txn + 1, bytes = m * (sizeof(fdgpu_frag_ex_t) + sizeof(uint64_t)) + 64;
+    const uint64_t m = e->cfg.max_txn + 1, bytes = m * (sizeof(fdgpu_frag_ex_t) + 3 * sizeof(uint64_t)) + 192;
     HIPCHK(hipHostMalloc((void **)&s->h_io, bytes, hipHostMallocDefault), FDGPU_ERR_DEVICE);
     HIPCHK(hipHostGetDevicePointer((void **)&s->d_ioh, s->h_io, 0), FDGPU_ERR_DEVICE);
     HIPCHK(hipMalloc((void **)&s->d_fxio, m * sizeof(fdgpu_frag_ex_t)), FDGPU_ERR_DEVICE);
   }
   fdgpu_frag_ex_t *h_fx = (fdgpu_frag_ex_t *)s->h_io;
   uint64_t *h_src = (uint64_t *)(s->h_io + src_at);
+  uint64_t *h_chk = (uint64_t *)(s->h_io + chk_at);
   /* bounds: every payload inside a registered region (16-B aligned: the
      gather reads 16-B units up to round16(sz), inside the payload's own
      64-B chunks), every out frag inside out, the packed arena within
-     max_arena, the signature bound within max_sig */
+     max_arena, the signature bound within max_sig, every named link given */
   uint64_t dev_off = 0, bound = 0;
+  bool any_chk = false;
   const fdgpu_engine::Reg *rc = nullptr;
   for (uint64_t t = 0; t < n; t++) {
     const fdgpu_frag_io_t &f = fio[t];
     const uint64_t q = ((uint64_t)f.sz + 15u) & ~15ull;
     if (f.sz > FDT_TXN_MTU_BYTES || (f.src & 15u) || (f.out_off & 1u) || (uint64_t)f.out_off + f.out_cap > out_sz ||
-        f.out_cap > 0xFFFFu) {
-      set_err("frag %llu: size, alignment or out bounds", (unsigned long long)t);
+        f.out_cap > 0xFFFFu || f.link > link_cnt) {
+      set_err("frag %llu: size, alignment, out bounds or link", (unsigned long long)t);
       return FDGPU_ERR_INVAL;
     }
     if (!rc || f.src < rc->base || f.src + q > rc->end) rc = region_of(e, (uintptr_t)f.src, q);
     if (!rc) { set_err("frag %llu: payload not inside a registered region", (unsigned long long)t); return FDGPU_ERR_INVAL; }
     h_src[t] = rc->dbase + (f.src - rc->base);
     h_fx[t] = fdgpu_frag_ex_t{(uint32_t)dev_off, f.sz, f.out_off, f.out_cap};
+    if (f.link) {
+      h_chk[2 * t] = ldev[f.link - 1] + (f.seq & lmask[f.link - 1]) * 32u;    /* fd_frag_meta_t.seq: offset 0 */
+      h_chk[2 * t + 1] = f.seq;
+      any_chk = true;
+    } else {
+      h_chk[2 * t] = 0;
+    }
     dev_off += q;
     if (dev_off > e->cfg.max_arena) { set_err("frags exceed the engine's arena"); return FDGPU_ERR_INVAL; }
     bound += fdt_frag_sig_bound(f.sz);
@@ -867,15 +899,17 @@ int64_t fdgpu_submit_frags_io(fdgpu_engine_t *e, fdgpu_frag_io_t const *fio, uin
   if (bound > e->cfg.max_sig) { set_err("batch may exceed max_sig (%llu)", (unsigned long long)e->cfg.max_sig); return FDGPU_ERR_INVAL; }
   const uint64_t sp1 = g_sp_on ? sp_now() : 0;
   if (!slot_ws(*s, bound)) return FDGPU_ERR_DEVICE;
-  /* five kernels: gather (which also keeps the records on the device and
-     zeroes the verify queue counter and the signature count), parse +
-     expand, verify and its fallback, finish -- the out frags and the results
-     written in place over the bus -- then the completion word */
+  /* five kernels: gather (which also re-checks the in mcache lines, keeps
+     the records on the device and zeroes the verify queue counter and the
+     signature count), parse + expand, verify and its fallback, finish --
+     the out frags and the results written in place over the bus -- then the
+     completion word */
   uint8_t *out_dev = out_sz ? (uint8_t *)(ro->dbase + ((uintptr_t)out - ro->base)) : nullptr;
   if (n) {
     const fdgpu_frag_ex_t *d_fx = s->d_fxio;
     const bool zero_cnt = !(kflags(e) & FDGPU_FLAG_KCACHE);
-    HIPCHK(fdgpu_launch_frag_gather((const uint64_t *)(s->d_ioh + src_at), (const fdgpu_frag_ex_t *)s->d_ioh, (uint32_t)n,
+    HIPCHK(fdgpu_launch_frag_gather((const uint64_t *)(s->d_ioh + src_at), (const fdgpu_frag_ex_t *)s->d_ioh,
+                                    any_chk ? (const uint64_t *)(s->d_ioh + chk_at) : nullptr, (uint32_t)n,
                                     s->d_arena, s->d_fxio, zero_cnt ? fdgpu_verify_cnt_word(s->d_ws, (uint32_t)bound) : nullptr,
                                     s->d_n_sig, s->stream),
            FDGPU_ERR_DEVICE);
@@ -891,7 +925,6 @@ int64_t fdgpu_submit_frags_io(fdgpu_engine_t *e, fdgpu_frag_io_t const *fio, uin
            FDGPU_ERR_DEVICE);
   }
   ++s->flag_seq;
-  if (e->flag_poll && !e->drop_flag) HIPCHK(hipStreamWriteValue32(s->stream, s->d_flag, s->flag_seq, 0), FDGPU_ERR_DEVICE);
   if (e->flag_poll && !e->drop_flag) HIPCHK(hipStreamWriteValue32(s->stream, s->d_flag, s->flag_seq, 0), FDGPU_ERR_DEVICE);
   HIPCHK(hipEventRecord(s->done, s->stream), FDGPU_ERR_DEVICE);
   s->staged = false;
@@ -1315,12 +1348,16 @@ int fdgpu_sync(fdgpu_engine_t *e) {
    callers instead of serialising on a lock.  The caller's current HIP device
    is saved and restored.
 
-   The reference API has no error channel besides the verify codes.  On an
-   engine failure (no device, a HIP error) every call of the failed batch
-   returns FD_ED25519_ERR_SIG -- fail closed: nothing unchecked is accepted --
-   and fdgpu_sync_errors() counts the event (fdgpu_last_error() of the
-   failing thread says why).  FDGPU_SYNC_ABORT=1 in the environment aborts
-   the process instead. */
+   The reference API has no error channel besides the verify codes, and it
+   never answers a good signature with an error.  So an engine failure (no
+   device, a HIP error, a call beyond the engine's 32-bit arena) aborts the
+   process by default, with the reason on stderr: a transient GPU fault must
+   not turn valid transactions or blocks into rejected ones (replay's
+   fd_executor_txn_verify, the shred FEC-root checks).  A caller that prefers
+   to reject instead sets FDGPU_SYNC_FAIL_CLOSED=1: every call of the failed
+   batch then returns FD_ED25519_ERR_SIG and fdgpu_sync_errors() counts the
+   event (fdgpu_last_error() of the failing thread says why).
+   FDGPU_SYNC_DEVICE=<n> puts the engine on device n (default 0). */
 }  // extern "C"
 
 namespace {
@@ -1353,12 +1390,19 @@ SyncState &sync_state() {
 }
 
 constexpr uint64_t SYNC_BATCH_MAX = 4096;    /* calls per coalesced batch */
+/* arena bytes of one coalesced batch: the engine's arena is opened at twice
+   the batch's need (room to grow) and must stay within 32-bit offsets
+   (fdgpu_engine_open), so a batch holds at most half of that; a single call
+   needing more cannot run on the engine at all */
+constexpr uint64_t SYNC_ARENA_MAX = (0xFFFFFFF0ull - FDGPU_ARENA_SLACK) / 2;
+inline uint64_t sync_need(uint64_t msg_sz, uint32_t n) { return 96ull * n + msg_sz; }
 
 void sync_failed(SyncState &st, const char *what) {
   st.errors.fetch_add(1, std::memory_order_relaxed);
-  const char *ab = getenv("FDGPU_SYNC_ABORT");
-  if (ab && ab[0] == '1') {
-    fprintf(stderr, "fd_ed25519_gpu: %s: %s\n", what, fdgpu_last_error());
+  const char *fc = getenv("FDGPU_SYNC_FAIL_CLOSED");
+  if (!(fc && fc[0] == '1')) {
+    fprintf(stderr, "fd_ed25519_gpu: %s: %s (FDGPU_SYNC_FAIL_CLOSED=1 rejects the calls instead)\n", what,
+            fdgpu_last_error());
     abort();
   }
 }
@@ -1366,13 +1410,17 @@ void sync_failed(SyncState &st, const char *what) {
 /* the leader's batch: returns false on an engine failure */
 bool sync_run(SyncState &st, const std::vector<SyncReq *> &batch) {
   uint64_t need = 0;
-  for (const SyncReq *r : batch) need += 96ull * r->n + r->msg_sz;
+  for (const SyncReq *r : batch) need += sync_need(r->msg_sz, r->n);
+  if (need > SYNC_ARENA_MAX) { set_err("a call needs %llu arena bytes (at most %llu)", (unsigned long long)need,
+                                       (unsigned long long)SYNC_ARENA_MAX); return false; }
   if (!st.eng || need > st.eng->cfg.max_arena) {
     if (st.eng) fdgpu_engine_close(st.eng);
     fdgpu_cfg_t cfg{};
     cfg.max_txn = SYNC_BATCH_MAX; cfg.max_sig = SYNC_BATCH_MAX * 16; cfg.ring_depth = 1;
-    cfg.max_arena = std::max<uint64_t>(SYNC_BATCH_MAX * (96 * 16 + 1232), need * 2);
-    st.eng = fdgpu_engine_open(0, &cfg);
+    cfg.max_arena = std::min<uint64_t>(std::max<uint64_t>(SYNC_BATCH_MAX * (96 * 16 + 1232), need * 2),
+                                       2 * SYNC_ARENA_MAX);
+    const char *dv = getenv("FDGPU_SYNC_DEVICE");
+    st.eng = fdgpu_engine_open(dv ? atoi(dv) : 0, &cfg);
     if (!st.eng) return false;
   }
   st.arena.resize(need);
@@ -1396,8 +1444,13 @@ bool sync_run(SyncState &st, const std::vector<SyncReq *> &batch) {
 
 int sync_verify(const uint8_t *msg, uint64_t msg_sz, const uint8_t *sigs, const uint8_t *pubs, uint32_t n) {
   if (n == 0 || n > 16) return FD_ED25519_ERR_SIG;            /* fd_ed25519_user.c:238-241 */
-  if (msg_sz > 0xFFFF0000ull) return FD_ED25519_ERR_SIG;      /* beyond the engine's 32-bit offsets */
   SyncState &st = sync_state();
+  if (sync_need(msg_sz, n) > SYNC_ARENA_MAX) {                /* fits no batch: fails alone, never queued */
+    st.calls.fetch_add(1, std::memory_order_relaxed);
+    set_err("a %llu-byte message exceeds the engine's 32-bit arena", (unsigned long long)msg_sz);
+    sync_failed(st, "call too large for the GPU engine");
+    return FD_ED25519_ERR_SIG;
+  }
   st.calls.fetch_add(1, std::memory_order_relaxed);
   SyncReq req{msg, sigs, pubs, msg_sz, n};
   std::unique_lock<std::mutex> lk(st.mu);
@@ -1406,7 +1459,15 @@ int sync_verify(const uint8_t *msg, uint64_t msg_sz, const uint8_t *sigs, const 
     if (st.leader) { st.cv.wait(lk); continue; }
     st.leader = true;                          /* this thread verifies everything queued so far */
     std::vector<SyncReq *> batch;
-    const size_t take = std::min<size_t>(st.pending.size(), SYNC_BATCH_MAX);
+    /* as many queued calls as fit one batch's arena (each call fits alone) */
+    size_t take = 0;
+    uint64_t need = 0;
+    while (take < st.pending.size() && take < SYNC_BATCH_MAX) {
+      const uint64_t c = sync_need(st.pending[take]->msg_sz, st.pending[take]->n);
+      if (take && need + c > SYNC_ARENA_MAX) break;
+      need += c;
+      take++;
+    }
     batch.assign(st.pending.begin(), st.pending.begin() + (long)take);
     st.pending.erase(st.pending.begin(), st.pending.begin() + (long)take);
     lk.unlock();

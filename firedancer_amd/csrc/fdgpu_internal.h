@@ -124,13 +124,16 @@ hipError_t fdgpu_launch_frag_finish(const fdgpu_txn_desc_t *d_tds, uint32_t n, c
                                     int8_t *d_codes, uint8_t *d_trailers, hipStream_t stream);
 /* fdgpu_submit_frags_io: one wave per frag copies its payload (16-B units)
    from host memory (d_src[i], the registered region's device-side address)
-   to d_arena + d_fx[i].off; the finish kernel writes per frag the code, the
-   dedup tag and the out frag's size, and assembles the out frag at
-   d_out + d_fx[i].tr_off ([payload][pad][fd_txn_t][u16 sz]) */
+   to d_arena + d_fx[i].off; with d_chk (n pairs {mcache line address, seq},
+   line 0: none) the line is re-read after the copy and a republished one
+   marks the kept record FDGPU_FX_LAPPED; the finish kernel writes per frag
+   the code, the dedup tag and the out frag's size, and assembles the out
+   frag at d_out + d_fx[i].tr_off ([payload][pad][fd_txn_t][u16 sz]) */
+#define FDGPU_FX_LAPPED 0x80000000u     /* in fdgpu_frag_ex_t.tr_cap (out_cap <= 0xFFFF) */
 uint64_t   fdgpu_frag_fp_bound(uint32_t sz);
-hipError_t fdgpu_launch_frag_gather(const uint64_t *d_src, const fdgpu_frag_ex_t *d_fx, uint32_t n, uint8_t *d_arena,
-                                    fdgpu_frag_ex_t *d_fx_dev, uint32_t *d_zero_word, uint32_t *d_zero_word2,
-                                    hipStream_t stream);
+hipError_t fdgpu_launch_frag_gather(const uint64_t *d_src, const fdgpu_frag_ex_t *d_fx, const uint64_t *d_chk, uint32_t n,
+                                    uint8_t *d_arena, fdgpu_frag_ex_t *d_fx_dev, uint32_t *d_zero_word,
+                                    uint32_t *d_zero_word2, hipStream_t stream);
 /* gathered batches: parse + descriptor expansion in one launch, each wave
    taking its descriptor slots with one atomic add on *d_n_sig (which must
    start at zero: the gather kernel clears it) */

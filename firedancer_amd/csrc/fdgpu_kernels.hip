@@ -1071,7 +1071,8 @@ __global__ void __launch_bounds__(64) fdgpu_frag_parse_expand_kernel(
     const fdgpu_frag_ex_t f = fx[t];
     fdt_txn_t *x = (fdt_txn_t *)(txn_out + (size_t)t * FDT_TXN_MAX_SZ);
     uint64_t why = 0;
-    uint64_t fp = fdt_parse_core(arena + f.off, f.sz, x, &why);
+    /* a lapped payload (the gather's re-check) may be torn: not parsed */
+    uint64_t fp = (f.tr_cap & FDGPU_FX_LAPPED) ? 0u : fdt_parse_core(arena + f.off, f.sz, x, &why);
     const uint32_t sc = fp ? x->signature_cnt : 0u;
     c = (sc >= 1u && sc <= 16u) ? sc : 0u;
     if (c > fdt_frag_sig_bound(f.sz)) { c = 0u; fp = 0u; }      /* cannot happen for a parsed txn */
@@ -1153,11 +1154,19 @@ __global__ void __launch_bounds__(256) fdgpu_frag_finish_kernel(const fdgpu_txn_
    and copies the payload's 16-B units from host memory (the registered in
    dcache), both read in place over the bus, to its packed, 16-B aligned
    place in the batch arena; the units past sz lie in the payload's own 64-B
-   chunks.  The record is kept on the device (fx_dev) for the later kernels,
-   and the first thread clears the verify kernel's queue counter (zero_word):
-   the batch needs no upload copy and no memset. */
+   chunks.  With chk, a frag whose pair {line, seq} names an in-mcache line
+   is then re-checked as the reference's mux re-checks after its copy
+   (fd_mux.c:641-655): once the wave's payload loads have returned, the line's
+   seq is read again over the bus (a system-scope load: no cache in between);
+   any other value than the frag's seq means the producer republished the
+   line, so its payload may have been rewritten under the read, and the
+   record is kept with FDGPU_FX_LAPPED set (no parse, no verdict).  The
+   record is kept on the device (fx_dev) for the later kernels, and the
+   first thread clears the verify kernel's queue counter (zero_word): the
+   batch needs no upload copy and no memset. */
 __global__ void __launch_bounds__(256) fdgpu_frag_gather_kernel(const uint64_t *__restrict__ src,
-                                                                const fdgpu_frag_ex_t *__restrict__ fx, uint32_t n,
+                                                                const fdgpu_frag_ex_t *__restrict__ fx,
+                                                                const uint64_t *__restrict__ chk, uint32_t n,
                                                                 uint8_t *__restrict__ arena,
                                                                 fdgpu_frag_ex_t *__restrict__ fx_dev,
                                                                 uint32_t *__restrict__ zero_word,
@@ -1169,11 +1178,20 @@ __global__ void __launch_bounds__(256) fdgpu_frag_gather_kernel(const uint64_t *
   }
   if (f >= n) return;
   const uint4 *s = (const uint4 *)src[f];
-  const fdgpu_frag_ex_t x = fx[f];
-  if (lane == 0) fx_dev[f] = x;
+  fdgpu_frag_ex_t x = fx[f];
   uint4 *d = (uint4 *)(arena + x.off);
   const uint32_t nq = (x.sz + 15u) >> 4;
   for (uint32_t q = lane; q < nq; q += 64u) d[q] = s[q];
+  if (chk) {
+    const uint64_t line = chk[2u * f];
+    if (line) {
+      /* every payload load of the wave has returned before the line is read */
+      __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      const uint64_t seq = __hip_atomic_load((const uint64_t *)line, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      if (seq != chk[2u * f + 1u]) x.tr_cap |= FDGPU_FX_LAPPED;
+    }
+  }
+  if (lane == 0) fx_dev[f] = x;
 }
 
 /* Finish: one wave per frag.  Lane 0 writes the frag's code (the
@@ -1195,12 +1213,13 @@ FDG_DEV void frag_finish_io_one(uint32_t f, uint32_t lane, const fdgpu_txn_desc_
                                 uint16_t *__restrict__ out_szs) {
   const uint32_t fp = txn_sz[f];
   const fdgpu_frag_ex_t x = fx[f];                    /* off: arena, sz, tr_off: out offset, tr_cap: its room */
+  const bool lapped = (x.tr_cap & FDGPU_FX_LAPPED) != 0u;   /* fp is 0 then */
   const uint32_t toff = (x.sz + 1u) & ~1u, osz = toff + fp + 2u;
   const bool fits = fp && osz <= x.tr_cap;
   const fdt_txn_t *t = (const fdt_txn_t *)(txn_out + (size_t)f * FDT_TXN_MAX_SZ);
   const uint8_t *pl = arena + x.off;
   if (lane == 0) {
-    int code = FDGPU_CODE_PARSE_FAIL;
+    int code = lapped ? FDGPU_CODE_LAPPED : FDGPU_CODE_PARSE_FAIL;
     uint64_t tag = 0;
     if (fp) {
       tag = fdt_hash_core(seed, pl + t->signature_off, 64);
@@ -1452,11 +1471,11 @@ hipError_t fdgpu_launch_frag_finish(const fdgpu_txn_desc_t *d_tds, uint32_t n, c
 
 uint64_t fdgpu_frag_fp_bound(uint32_t sz) { return fdt_frag_fp_bound(sz); }
 
-hipError_t fdgpu_launch_frag_gather(const uint64_t *d_src, const fdgpu_frag_ex_t *d_fx, uint32_t n, uint8_t *d_arena,
-                                    fdgpu_frag_ex_t *d_fx_dev, uint32_t *d_zero_word, uint32_t *d_zero_word2,
-                                    hipStream_t stream) {
+hipError_t fdgpu_launch_frag_gather(const uint64_t *d_src, const fdgpu_frag_ex_t *d_fx, const uint64_t *d_chk, uint32_t n,
+                                    uint8_t *d_arena, fdgpu_frag_ex_t *d_fx_dev, uint32_t *d_zero_word,
+                                    uint32_t *d_zero_word2, hipStream_t stream) {
   if (!n) return hipSuccess;
-  hipLaunchKernelGGL(fdgpu_frag_gather_kernel, dim3((n + 3) / 4), dim3(256), 0, stream, d_src, d_fx, n, d_arena,
+  hipLaunchKernelGGL(fdgpu_frag_gather_kernel, dim3((n + 3) / 4), dim3(256), 0, stream, d_src, d_fx, d_chk, n, d_arena,
                      d_fx_dev, d_zero_word, d_zero_word2);
   return hipGetLastError();
 }

@@ -172,6 +172,7 @@ struct VItem {
   uint32_t tr_off;      /* gpu_parse: the parsed fd_txn_t's place in the batch's trailer buffer */
   uint32_t tr_cap;      /*            and its footprint (fdt_txn_peek); gather: the out bytes reserved */
   uint32_t in_idx;      /* gather: the in link it came from */
+  uint32_t lost;        /* gather: the lap guard found it lapped when it copied it (dropped at resolution) */
 };
 
 struct VBatch {
@@ -183,8 +184,9 @@ struct VBatch {
   std::vector<fdgpu_frag_io_t> fio;   /* gather: the verifier's view of the items ... */
   std::vector<uint64_t> tags;         /* ... and its results: dedup tags, */
   std::vector<uint16_t> out_szs;      /*     out frag sizes */
-  uint64_t link_first[FDT_MUX_IN_MAX];   /* gather: the oldest seq taken from each in link (lapped-check) */
-  uint32_t link_mask = 0;
+  uint64_t link_first[FDT_MUX_IN_MAX];   /* gather: the oldest seq taken from each in link, */
+  uint32_t guard_cur[FDT_MUX_IN_MAX];    /*   the lap guard's cursor over the items of each, */
+  uint32_t link_mask = 0;                /*   and which links the batch holds frags of */
   uint64_t tr_used = 0;
   std::vector<VItem> items;
   std::vector<int8_t> codes;
@@ -250,6 +252,8 @@ struct fdgpu_vmux {
   uint32_t calls = 0;                     /* after_credit calls (rate-limits verifier polls) */
   fdgpu_vtile_stats_t st{};
   std::vector<uint64_t> lat;
+  fdgpu_link_t links[FDT_MUX_IN_MAX] = {};   /* gather: the in mcaches, re-checked by the device after its read */
+  uint64_t lap_span_max = 0, lap_margin = 0;  /* gather: the lap guard (~0: off) */
   uint64_t log_max = 0;
   std::vector<uint64_t> log_seq;
   std::vector<int8_t> log_code;
@@ -309,7 +313,6 @@ struct fdgpu_vmux {
         st.batch_gpu_ns += now_ns() - b->t_submit;
         if (rc != FDGPU_OK) { error = rc; *poll_in = 0; return; }
         b->done = true;
-        if (gather) lapped_check(*b);
       }
       const uint64_t t_pub = now_ns();
       struct Acc { uint64_t &ns; uint64_t t0; ~Acc() { ns += now_ns() - t0; } } acc{st.publish_ns, t_pub};
@@ -323,8 +326,9 @@ struct fdgpu_vmux {
         }
         const VItem &it = b->items[k];
         const int code = b->codes[k];
-        if (gather && code == FDGPU_CODE_LAPPED) {   /* the producer overwrote it before the GPU read it */
+        if (gather && (code == FDGPU_CODE_LAPPED || it.lost)) {   /* the producer overwrote it before it was read */
           st.overrun++;
+          st.lapped++;
           log(it.seq, FDGPU_VTILE_LOG_LOST);
           b->next++;
           continue;
@@ -381,25 +385,45 @@ struct fdgpu_vmux {
     }
   }
 
-  /* gather: the GPU read each payload from the in dcache after submit; a
-     frag whose in-mcache line the producer has lapped since may have been
-     read torn, and is dropped (the mux's seq re-check after its copy,
-     fd_mux.c:641-655, moved to after the device's read).  The oldest frag
-     of each link is lapped first, so one line per link is checked unless it
-     was. */
-  void lapped_check(VBatch &b) {
-    uint32_t lapped = 0;
+  /* gather: has in link i's producer published seq s yet?  Its line holds
+     s - depth (or older) until then: a signed difference reads the lap. */
+  bool published_by(uint32_t i, uint64_t s) const {
+    const fdt_frag_meta_t *line = cfg.in_mcache[i] + (s & (cfg.in_depth[i] - 1));
+    return (int64_t)(ld_acq(&line->seq) - s) >= 0;
+  }
+
+  /* gather, the lap guard: the device reads a payload only after the batch
+     is submitted (and re-checks its line then, fdgpu_submit_frags_io), and
+     the quic -> verify producer never waits for the tile.  Before a batch
+     goes out -- and while it waits for a free slot -- every frag whose line
+     the producer will reuse within lap_margin more publishes is copied here
+     into its out frag's room, re-checked as the reference re-checks after
+     its copy (fd_mux.c:641-655), and handed to the device from there.  One
+     line read per link tells whether any frag of it is at risk (its oldest
+     frag is the first to be lapped); younger frags of a link are safer, so
+     each link's scan stops at its first frag not at risk. */
+  void lap_guard(VBatch &b) {
     for (uint32_t i = 0; i < cfg.in_cnt; i++) {
       if (!(b.link_mask >> i & 1u)) continue;
-      const fdt_frag_meta_t *line = cfg.in_mcache[i] + (b.link_first[i] & (cfg.in_depth[i] - 1));
-      if (ld_acq(&line->seq) != b.link_first[i]) lapped |= 1u << i;
-    }
-    if (!lapped) return;
-    for (size_t k = 0; k < b.items.size(); k++) {
-      const VItem &it = b.items[k];
-      if (!(lapped >> it.in_idx & 1u)) continue;
-      const fdt_frag_meta_t *line = cfg.in_mcache[it.in_idx] + (it.seq & (cfg.in_depth[it.in_idx] - 1));
-      if (ld_acq(&line->seq) != it.seq) b.codes[k] = (int8_t)FDGPU_CODE_LAPPED;
+      const uint64_t depth = cfg.in_depth[i], m = std::min(lap_margin, depth);
+      const size_t n = b.items.size();
+      size_t k = b.guard_cur[i];
+      while (k < n && b.items[k].in_idx != i) k++;
+      if (k == n || !published_by(i, b.items[k].seq + depth - m)) { b.guard_cur[i] = (uint32_t)k; continue; }
+      for (; k < n; k++) {
+        VItem &it = b.items[k];
+        if (it.in_idx != i) continue;
+        if (!published_by(i, it.seq + depth - m)) break;
+        uint8_t *dst = out_laddr(it.chunk);
+        std::memcpy(dst, (const void *)(uintptr_t)b.fio[k].src, it.sz);
+        std::atomic_thread_fence(std::memory_order_acquire);
+        const fdt_frag_meta_t *line = cfg.in_mcache[i] + (it.seq & (depth - 1));
+        if (ld_acq(&line->seq) != it.seq) it.lost = 1;      /* lapped already: the copy may be torn */
+        else st.rescued++;
+        b.fio[k].src = (uint64_t)(uintptr_t)dst;           /* the device reads this copy: no re-check */
+        b.fio[k].link = 0;
+      }
+      b.guard_cur[i] = (uint32_t)k;
     }
   }
 
@@ -414,15 +438,17 @@ struct fdgpu_vmux {
 
   void submit() {
     if (!open || open->items.empty()) return;
-    if (!open->closed && now_ns() - open->t_first < cfg.batch_wait_ns) return;
-    if (inflight.size() >= cfg.inflight_max) return;
-    int64_t t;
     const uint64_t s0 = now_ns();
     struct Acc { uint64_t &ns; uint64_t t0; ~Acc() { ns += now_ns() - t0; } } acc{st.submit_ns, s0};
+    if (gather && lap_margin != ~0ull) lap_guard(*open);    /* also while the batch fills or waits for a slot */
+    if (!open->closed && s0 - open->t_first < cfg.batch_wait_ns) return;
+    if (inflight.size() >= cfg.inflight_max) return;
+    int64_t t;
     if (gather) {
       const size_t n = open->fio.size();
       if (open->tags.size() < n) { open->tags.resize(cfg.batch_txn_max); open->out_szs.resize(cfg.batch_txn_max); }
-      t = ver.submit_io(ver.ctx, open->fio.data(), n, out_laddr(open->first_chunk), open->end_off, cfg.hashmap_seed);
+      t = ver.submit_io(ver.ctx, open->fio.data(), n, out_laddr(open->first_chunk), open->end_off, cfg.hashmap_seed,
+                        links, cfg.in_cnt);
     } else if (gpu_parse) {
       if (open->trailers.size() < open->tr_used) open->trailers.resize(open->tr_used);
       t = ver.submit_frags(ver.ctx, out_laddr(open->first_chunk), open->end_off, open->frags.data(),
@@ -515,15 +541,23 @@ void vm_after_frag(void *ctx, uint64_t in_idx, uint64_t seq, uint64_t *opt_sig, 
     const uint64_t off = (t->out_chunk - b.first_chunk) << FDT_CHUNK_LG_SZ;
     const uint32_t cap = t->cap_of[payload_sz];                  /* payload_sz <= FDT_TPU_MTU: during_frag */
     const uint32_t li = (uint32_t)t->cur_in;
-    if (!(b.link_mask >> li & 1u)) { b.link_mask |= 1u << li; b.link_first[li] = seq; }
-    b.fio.push_back(fdgpu_frag_io_t{t->cur_src, (uint32_t)payload_sz, (uint32_t)off, cap, 0u});
-    b.items.push_back(VItem{seq, 0, (uint32_t)t->out_chunk, (uint32_t)payload_sz, 0u, (uint32_t)*opt_tsorig, 0u, cap, li});
+    if (!(b.link_mask >> li & 1u)) {
+      b.link_mask |= 1u << li;
+      b.link_first[li] = seq;
+      b.guard_cur[li] = (uint32_t)b.items.size();
+    }
+    /* the device re-reads the frag's in-mcache line after the payload (link li + 1, seq) */
+    b.fio.push_back(fdgpu_frag_io_t{t->cur_src, (uint32_t)payload_sz, (uint32_t)off, cap, li + 1u, seq});
+    b.items.push_back(VItem{seq, 0, (uint32_t)t->out_chunk, (uint32_t)payload_sz, 0u, (uint32_t)*opt_tsorig, 0u, cap, li, 0u});
     b.end_off = off + cap;
     b.sig_cnt += fdt_frag_sig_bound(payload_sz);       /* (stats.sigs stays 0: the tile never sees the count) */
     t->out_chunk = fdt_dcache_compact_next(t->out_chunk, cap, t->cfg.out_chunk0, t->cfg.out_wmark);
     t->room_ok = false;
+    /* the lap guard's span: the batch holds at most lap_span_max seqs of a
+       link (this tile's next frag of the link is round_robin_cnt seqs on) */
     if (t->out_chunk <= b.first_chunk || b.items.size() >= t->cfg.batch_txn_max ||
-        b.sig_cnt + 16 > t->cfg.batch_sig_max || b.end_off + FRAG_CHUNKS * FDT_CHUNK_SZ > t->cfg.batch_bytes_max)
+        b.sig_cnt + 16 > t->cfg.batch_sig_max || b.end_off + FRAG_CHUNKS * FDT_CHUNK_SZ > t->cfg.batch_bytes_max ||
+        seq - b.link_first[li] + t->cfg.round_robin_cnt >= t->lap_span_max)
       b.closed = true;
     return;
   }
@@ -539,7 +573,7 @@ void vm_after_frag(void *ctx, uint64_t in_idx, uint64_t seq, uint64_t *opt_sig, 
     __builtin_prefetch(b.frags.data() + b.frags.size() + 12, 1);
     b.frags.push_back(fdgpu_frag_ex_t{(uint32_t)off, (uint32_t)payload_sz, (uint32_t)b.tr_used, (uint32_t)fp});
     b.items.push_back(VItem{seq, t->cur_tag, (uint32_t)t->out_chunk, (uint32_t)payload_sz, 1u, (uint32_t)*opt_tsorig,
-                            (uint32_t)b.tr_used, (uint32_t)fp, 0u});
+                            (uint32_t)b.tr_used, (uint32_t)fp, 0u, 0u});
     b.tr_used += (fp + 3) & ~3ull;
     b.end_off = off + payload_sz;
     b.sig_cnt += fdt_frag_sig_bound(payload_sz);
@@ -575,7 +609,7 @@ void vm_after_frag(void *ctx, uint64_t in_idx, uint64_t seq, uint64_t *opt_sig, 
   d.sig_cnt = tt->signature_cnt;
   b.txns.push_back(d);
   b.items.push_back(VItem{seq, fdt_hash(t->cfg.hashmap_seed, txn + tt->signature_off, 64), (uint32_t)t->out_chunk,
-                          (uint32_t)new_sz, tt->signature_off, (uint32_t)*opt_tsorig, 0u, 0u, 0u});
+                          (uint32_t)new_sz, tt->signature_off, (uint32_t)*opt_tsorig, 0u, 0u, 0u, 0u});
   b.end_off = off + new_sz;
   if (tt->signature_cnt <= 16) { b.sig_cnt += tt->signature_cnt; t->st.sigs += tt->signature_cnt; }
   t->out_chunk = fdt_dcache_compact_next(t->out_chunk, new_sz, t->cfg.out_chunk0, t->cfg.out_wmark);
@@ -627,9 +661,25 @@ fdgpu_vmux_t *fdgpu_vmux_new(const fdgpu_vmux_cfg_t *cfg, fdgpu_verifier_t ver) 
     delete t;
     return nullptr;
   }
-  if (t->gather)
+  if (t->gather) {
+    /* an unlapped line must mean an intact payload: each in dcache holds
+       depth + 1 maximal frags (fdt_dcache_data_sz), or is a TPU reassembly
+       slot arena of depth + burst slots (the same span from chunk0 to wmark) */
+    const uint64_t mtu_chunks = ((FDT_TPU_MTU + 2 * FDT_CHUNK_SZ - 1) >> (1 + FDT_CHUNK_LG_SZ)) << 1;
     for (uint64_t i = 0; i < cfg->in_cnt; i++)
-      if (!cfg->in_mcache[i] || !pow2(cfg->in_depth[i])) { delete t; return nullptr; }
+      if (!cfg->in_mcache[i] || !pow2(cfg->in_depth[i]) || cfg->in_wmark[i] < cfg->in_chunk0[i] ||
+          cfg->in_wmark[i] - cfg->in_chunk0[i] < cfg->in_depth[i] * mtu_chunks) {
+        delete t;
+        return nullptr;
+      }
+    uint64_t dmin = UINT64_MAX;
+    for (uint64_t i = 0; i < cfg->in_cnt; i++) {
+      t->links[i] = fdgpu_link_t{(uint64_t)(uintptr_t)cfg->in_mcache[i], cfg->in_depth[i]};
+      dmin = std::min(dmin, cfg->in_depth[i]);
+    }
+    t->lap_span_max = cfg->lap_span_max ? cfg->lap_span_max : std::max<uint64_t>(dmin / 2, 1);
+    t->lap_margin = cfg->lap_margin ? cfg->lap_margin : std::max<uint64_t>(dmin / 4, 1);
+  }
   if (!c.round_robin_cnt) c.round_robin_cnt = 1;
   if (!c.inflight_max) c.inflight_max = 2;
   if (!c.tcache_depth) c.tcache_depth = FDT_VERIFY_TCACHE_DEPTH;

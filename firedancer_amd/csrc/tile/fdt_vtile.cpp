@@ -153,12 +153,12 @@ int dispatch_poll_frags(void *ctx, int64_t ticket, int8_t *codes, uint8_t *trail
 }
 
 int64_t dispatch_submit_io(void *ctx, const fdgpu_frag_io_t *fio, uint64_t n, uint8_t *out, uint64_t out_sz,
-                           uint64_t seed) {
+                           uint64_t seed, const fdgpu_link_t *links, uint64_t link_cnt) {
   auto *d = (fdgpu_dispatch *)ctx;
   const uint32_t ne = (uint32_t)d->eng.size();
   for (uint32_t k = 0; k < ne; k++) {
     const uint32_t idx = (d->next + k) % ne;
-    const int64_t t = fdgpu_submit_frags_io(d->eng[idx], fio, n, out, out_sz, seed);
+    const int64_t t = fdgpu_submit_frags_io(d->eng[idx], fio, n, out, out_sz, seed, links, link_cnt);
     if (t == FDGPU_ERR_FULL) continue;
     if (t < 0) return t;
     d->next = (idx + 1) % ne;
@@ -668,6 +668,7 @@ void fdgpu_dtile_stats(const fdgpu_dtile_t *t, fdgpu_dtile_stats_t *out) { *out 
 struct fdgpu_producer {
   std::thread th;
   std::atomic<uint64_t> published{0};
+  std::atomic<int> done{0};
   double elapsed = 0;
 };
 
@@ -690,7 +691,7 @@ fdgpu_producer_t *fdgpu_producer_start(fdt_frag_meta_t *mcache, uint64_t depth, 
       ticks_per_ns = (double)(tick() - c0) / (double)(now_ns() - t0);
     }
     const double ticks_per_frag = rate_tps > 0 ? ticks_per_ns * 1e9 / rate_tps : 0.0;
-    const uint64_t p0 = tick();
+    const uint64_t p0 = tick(), t_pub0 = now_ns();       /* publishing starts (the calibration is not counted) */
     uint64_t chunk = chunk0;
     const uint16_t ctl = (uint16_t)fdt_frag_meta_ctl(0, 1, 1, 0);
     for (uint64_t i = 0; i < cnt; i++) {
@@ -709,10 +710,13 @@ fdgpu_producer_t *fdgpu_producer_start(fdt_frag_meta_t *mcache, uint64_t depth, 
       chunk = fdt_dcache_compact_next(chunk, n, chunk0, wmark);
       if ((i & 255) == 255 || i + 1 == cnt) p->published.store(i + 1, std::memory_order_relaxed);
     }
-    p->elapsed = (double)(now_ns() - t0) * 1e-9;
+    p->elapsed = (double)(now_ns() - t_pub0) * 1e-9;
+    p->done.store(1, std::memory_order_release);
   });
   return p;
 }
+
+int fdgpu_producer_done(const fdgpu_producer_t *p) { return p ? p->done.load(std::memory_order_acquire) : 1; }
 
 uint64_t fdgpu_producer_join(fdgpu_producer_t *p, double *elapsed_s) {
   if (!p) return 0;

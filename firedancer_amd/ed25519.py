@@ -200,17 +200,21 @@ class VerifyEngine:
         del self._pending[ticket]
         return codes[:n], tr[:tsz]
 
-    def submit_frags_io(self, frags, out, out_sz, hash_seed):
+    def submit_frags_io(self, frags, out, out_sz, hash_seed, links=None):
         """fdgpu_submit_frags_io: payloads read by the device where they lie
-        (frags: FRAG_IO_DTYPE {src host address, sz, out_off, out_cap}, every
-        src inside a registered buffer), out frags written to `out` (a
-        registered numpy buffer) [0, out_sz)."""
+        (frags: FRAG_IO_DTYPE {src host address, sz, out_off, out_cap, link,
+        seq}, every src inside a registered buffer), out frags written to
+        `out` (a registered numpy buffer) [0, out_sz).  links: (mcache
+        address, depth) per in link; a frag with link = i + 1 has links[i]'s
+        line of its seq re-read by the device after its payload
+        (FDGPU_CODE_LAPPED when republished)."""
         frags = np.ascontiguousarray(frags, dtype=FRAG_IO_DTYPE)
         out = np.asarray(out)
         if out_sz > out.nbytes:
             raise ValueError("out_sz exceeds the out buffer")
+        lk = np.array(list(links or []), dtype=LINK_DTYPE)
         tk = _lib.lib().fdgpu_submit_frags_io(self._h, frags.ctypes.data, len(frags), out.ctypes.data, int(out_sz),
-                                              int(hash_seed))
+                                              int(hash_seed), lk.ctypes.data if len(lk) else None, len(lk))
         if tk < 0:
             raise RuntimeError(f"fdgpu_submit_frags_io failed ({tk}): {_lib.last_error()}")
         self._pending[tk] = (len(frags), frags)
@@ -372,7 +376,10 @@ class DeviceBatch:
 
 FRAG_DTYPE = np.dtype([("off", "<u4"), ("sz", "<u4")])
 FRAG_EX_DTYPE = np.dtype([("off", "<u4"), ("sz", "<u4"), ("tr_off", "<u4"), ("tr_cap", "<u4")])
-FRAG_IO_DTYPE = np.dtype([("src", "<u8"), ("sz", "<u4"), ("out_off", "<u4"), ("out_cap", "<u4"), ("_pad", "<u4")])
+FRAG_IO_DTYPE = np.dtype([("src", "<u8"), ("sz", "<u4"), ("out_off", "<u4"), ("out_cap", "<u4"), ("link", "<u4"),
+                          ("seq", "<u8")])
+LINK_DTYPE = np.dtype([("mcache", "<u8"), ("depth", "<u8")])   # fdgpu_link_t
+CODE_LAPPED = -66             # FDGPU_CODE_LAPPED
 CODE_TRAILER_CAP = -65        # FDGPU_CODE_TRAILER_CAP
 CODE_PARSE_FAIL = -64          # FDGPU_CODE_PARSE_FAIL
 TXN_MAX_SZ = 852               # FD_TXN_MAX_SZ: stride of the parsed fd_txn_t records

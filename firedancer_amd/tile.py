@@ -79,10 +79,14 @@ SUBMIT_FN = c.CFUNCTYPE(c.c_int64, vp, vp, c.c_uint64, vp, c.c_uint64)
 POLL_FN = c.CFUNCTYPE(c.c_int, vp, c.c_int64, vp, c.c_int)
 SUBMIT_FRAGS_FN = c.CFUNCTYPE(c.c_int64, vp, vp, c.c_uint64, vp, c.c_uint64, c.c_uint64)
 POLL_FRAGS_FN = c.CFUNCTYPE(c.c_int, vp, c.c_int64, vp, vp, c.c_int)
-SUBMIT_IO_FN = c.CFUNCTYPE(c.c_int64, vp, vp, c.c_uint64, vp, c.c_uint64, c.c_uint64)
+SUBMIT_IO_FN = c.CFUNCTYPE(c.c_int64, vp, vp, c.c_uint64, vp, c.c_uint64, c.c_uint64, vp, c.c_uint64)
 POLL_IO_FN = c.CFUNCTYPE(c.c_int, vp, c.c_int64, vp, vp, vp, c.c_int)
 # fdgpu_frag_io_t: a payload where it lies and its out frag's room (fdgpu_submit_frags_io)
-FRAG_IO_DTYPE = np.dtype([("src", "<u8"), ("sz", "<u4"), ("out_off", "<u4"), ("out_cap", "<u4"), ("_pad", "<u4")])
+# (link = i + 1: the in link whose mcache line of seq is re-checked after the payload is read)
+FRAG_IO_DTYPE = np.dtype([("src", "<u8"), ("sz", "<u4"), ("out_off", "<u4"), ("out_cap", "<u4"), ("link", "<u4"),
+                          ("seq", "<u8")])
+assert FRAG_IO_DTYPE.itemsize == 32
+LINK_DTYPE = np.dtype([("mcache", "<u8"), ("depth", "<u8")])   # fdgpu_link_t
 CODE_LAPPED = -66
 # fdgpu_frag_ex_t: a payload and the place its parsed fd_txn_t goes (fdgpu_submit_frags)
 FRAG_EX_DTYPE = np.dtype([("off", "<u4"), ("sz", "<u4"), ("tr_off", "<u4"), ("tr_cap", "<u4")])
@@ -112,7 +116,7 @@ class VTileStats(c.Structure):
                                           "verify_failed", "dedup", "published", "batches", "sigs",
                                           "backpressure", "lat_cnt", "verify_errors", "ingest_ns", "submit_ns",
                                           "poll_ns", "no_slot_steps", "polls", "poll_done_ns",
-                                          "publish_ns", "batch_fill_ns", "batch_gpu_ns")]
+                                          "publish_ns", "batch_fill_ns", "batch_gpu_ns", "lapped", "rescued")]
 
     def as_dict(self):
         return {n: getattr(self, n) for n, _ in self._fields_}
@@ -170,7 +174,7 @@ class VMuxCfg(c.Structure):
                 ("tcache_map_cnt", c.c_uint64), ("batch_txn_max", c.c_uint32), ("inflight_max", c.c_uint32),
                 ("batch_wait_ns", c.c_uint64), ("batch_sig_max", c.c_uint64), ("batch_bytes_max", c.c_uint64),
                 ("gpu_parse", c.c_uint32), ("_pad", c.c_uint32), ("in_mcache", vp * MUX_IN_MAX),
-                ("in_depth", c.c_uint64 * MUX_IN_MAX)]
+                ("in_depth", c.c_uint64 * MUX_IN_MAX), ("lap_span_max", c.c_uint64), ("lap_margin", c.c_uint64)]
 
 
 class LinkT(c.Structure):
@@ -248,6 +252,7 @@ def lib():
         "fdt_sandbox_enter": (c.c_int, [c.c_int]),
         "fdgpu_dtile_run_sandboxed": (None, [vp, u64, u64, c.POINTER(DTileStats), c.c_int]),
         "fdgpu_producer_join": (u64, [vp, c.POINTER(c.c_double)]),
+        "fdgpu_producer_done": (c.c_int, [vp]),
         "fdt_mux_publish": (None, [vp, u64, u64, u64, u64, u64, u64]),
         "fdt_mux_run": (c.c_int, [c.POINTER(MuxCfg), c.POINTER(MuxCallbacks), vp, c.POINTER(u64),
                                   c.POINTER(MuxStats)]),
@@ -290,6 +295,13 @@ def _aligned(nbytes, align):
     buf = np.zeros(nbytes + align, dtype=np.uint8)
     off = (-buf.ctypes.data) % align
     return buf[off:off + nbytes]
+
+
+def _page_buf(nbytes):
+    """nbytes in whole pages of their own: a buffer the GPU engines may
+    register (fdgpu_host_register pins whole pages) without sharing a page
+    with another buffer."""
+    return _aligned((nbytes + 4095) // 4096 * 4096, 4096)[:nbytes]
 
 
 # ---------------------------------------------------------------- basics
@@ -389,10 +401,10 @@ class Link:
         if depth & (depth - 1):
             raise ValueError("depth must be a power of 2")
         self.depth, self.mtu, self.seq0 = depth, mtu, seq0
-        self.mcache = _aligned(depth * 32, 128).view(FRAG_META_DTYPE)
+        self.mcache = _page_buf(depth * 32).view(FRAG_META_DTYPE)
         data_sz = data_sz or L.fdt_dcache_data_sz(mtu, depth)   # explicit: a dcache sized by its producer
         data_sz = (data_sz + CHUNK_SZ - 1) // CHUNK_SZ * CHUNK_SZ
-        self.dcache = _aligned(data_sz, 4096)
+        self.dcache = _page_buf(data_sz)
         self.chunk0 = 0
         self.chunk1 = data_sz // CHUNK_SZ
         self.wmark = L.fdt_dcache_wmark(self.chunk0, self.chunk1, mtu)
@@ -510,11 +522,12 @@ class TpuReasm:
         if not fp:
             raise ValueError("bad reasm parameters")
         self.depth, self.burst, self.seq0, self.mtu = depth, burst, seq0, TPU_REASM_MTU
-        self.region = _aligned(fp, 4096)
+        self.region = _page_buf(fp)
+        self.dcache = self.region                    # the payloads' region (the verify tile registers it)
         self._r = L.fdt_tpu_reasm_new(self.region.ctypes.data, depth, burst, orig)
         if not self._r:
             raise RuntimeError("fdt_tpu_reasm_new failed")
-        self.mcache = _aligned(depth * 32, 128).view(FRAG_META_DTYPE)
+        self.mcache = _page_buf(depth * 32).view(FRAG_META_DTYPE)
         L.fdt_mcache_init(self.mcache.ctypes.data, depth, seq0)
         self.chunk0 = L.fdt_tpu_reasm_chunk0(self._r, self.base_ptr)
         self.wmark = L.fdt_tpu_reasm_wmark(self._r, self.base_ptr)
@@ -651,59 +664,78 @@ class PyVerifier:
                     c.memmove(trailers, t, len(t))
             return rc
 
-        def submit_io(ctx, frags, n, out, out_sz, seed):
+        def submit_io(ctx, frags, n, out, out_sz, seed, links, link_cnt):
             # fdgpu_submit_frags_io on the host: each payload read where it
-            # lies, parsed, tagged, its out frag written at its reserved place
+            # lies -- late, when the batch completes (the first poll that
+            # returns it), as the device reads it some time after submit --
+            # its in-mcache line re-checked after the read, parsed, tagged,
+            # its out frag written at its reserved place
             if len(self.results) >= self.slots:
                 return -12
-            fio = np.frombuffer((c.c_uint8 * (24 * n)).from_address(frags), dtype=FRAG_IO_DTYPE).copy() if n else \
+            fio = np.frombuffer((c.c_uint8 * (32 * n)).from_address(frags), dtype=FRAG_IO_DTYPE).copy() if n else \
                 np.zeros(0, dtype=FRAG_IO_DTYPE)
-            codes = np.zeros(max(n, 1), dtype=np.int8)
-            tags = np.zeros(max(n, 1), dtype=np.uint64)
-            osz = np.zeros(max(n, 1), dtype=np.uint16)
-            arena, txns, idx = bytearray(), [], []
-            for i, f in enumerate(fio):
-                sz = int(f["sz"])
-                p = c.string_at(int(f["src"]), sz)
-                fp, raw = txn_parse(p)
-                if not fp:
-                    codes[i] = CODE_PARSE_FAIL
-                    continue
-                h = txn_decode(raw)
-                tags[i] = fd_hash(seed, p[h["signature_off"]:h["signature_off"] + 64])
-                toff = (sz + 1) & ~1
-                frag = p + b"\0" * (toff - sz) + raw + sz.to_bytes(2, "little")
-                if len(frag) > int(f["out_cap"]):
-                    codes[i] = CODE_TRAILER_CAP
-                    continue
-                c.memmove(out + int(f["out_off"]), frag, len(frag))
-                osz[i] = len(frag)
-                off = len(arena)
-                arena += p
-                txns.append((off + h["message_off"], sz - h["message_off"], off + h["signature_off"],
-                             off + h["acct_addr_off"], h["signature_cnt"]))
-                idx.append(i)
-            if txns:
-                codes[idx] = np.asarray(self.fn(np.frombuffer(bytes(arena), dtype=np.uint8),
-                                                np.array(txns, dtype=TXN_DTYPE)), dtype=np.int8)
+            lk = np.frombuffer((c.c_uint8 * (16 * link_cnt)).from_address(links), dtype=LINK_DTYPE).copy() \
+                if link_cnt else np.zeros(0, dtype=LINK_DTYPE)
+
+            def work():
+                codes = np.zeros(max(n, 1), dtype=np.int8)
+                tags = np.zeros(max(n, 1), dtype=np.uint64)
+                osz = np.zeros(max(n, 1), dtype=np.uint16)
+                arena, txns, idx = bytearray(), [], []
+                for i, f in enumerate(fio):
+                    sz = int(f["sz"])
+                    p = c.string_at(int(f["src"]), sz)
+                    if int(f["link"]):
+                        ln = lk[int(f["link"]) - 1]
+                        line = int(ln["mcache"]) + (int(f["seq"]) & (int(ln["depth"]) - 1)) * 32
+                        if c.c_uint64.from_address(line).value != int(f["seq"]):
+                            codes[i] = CODE_LAPPED
+                            continue
+                    fp, raw = txn_parse(p)
+                    if not fp:
+                        codes[i] = CODE_PARSE_FAIL
+                        continue
+                    h = txn_decode(raw)
+                    tags[i] = fd_hash(seed, p[h["signature_off"]:h["signature_off"] + 64])
+                    toff = (sz + 1) & ~1
+                    frag = p + b"\0" * (toff - sz) + raw + sz.to_bytes(2, "little")
+                    if len(frag) > int(f["out_cap"]):
+                        codes[i] = CODE_TRAILER_CAP
+                        continue
+                    c.memmove(out + int(f["out_off"]), frag, len(frag))
+                    osz[i] = len(frag)
+                    off = len(arena)
+                    arena += p
+                    txns.append((off + h["message_off"], sz - h["message_off"], off + h["signature_off"],
+                                 off + h["acct_addr_off"], h["signature_cnt"]))
+                    idx.append(i)
+                if txns:
+                    codes[idx] = np.asarray(self.fn(np.frombuffer(bytes(arena), dtype=np.uint8),
+                                                    np.array(txns, dtype=TXN_DTYPE)), dtype=np.int8)
+                return codes[:n], tags[:n], osz[:n]
+
             self.batches.append(n)
             k = self.next
             self.next += 1
-            self.results[k] = codes[:n]
-            self.io[k] = (tags[:n], osz[:n])
+            self.results[k] = None
+            self.io[k] = work
             self.polls[k] = 0
             return k
 
         def poll_io(ctx, ticket, codes, tags, out_szs, blocking):
             if ticket not in self.io:
                 return -13
-            rc = poll(ctx, ticket, codes, blocking)
-            if rc == 0:
-                t, o = self.io.pop(ticket)
-                if len(t):
-                    c.memmove(tags, t.ctypes.data, 8 * len(t))
-                    c.memmove(out_szs, o.ctypes.data, 2 * len(o))
-            return rc
+            if not blocking and self.polls[ticket] < self.lag:
+                self.polls[ticket] += 1
+                return 1                                      # FDGPU_PENDING
+            r, t, o = self.io.pop(ticket)()
+            self.results.pop(ticket)
+            self.polls.pop(ticket)
+            if len(r):
+                c.memmove(codes, r.ctypes.data, len(r))
+                c.memmove(tags, t.ctypes.data, 8 * len(t))
+                c.memmove(out_szs, o.ctypes.data, 2 * len(o))
+            return 0
 
         self.trailers, self.io = {}, {}
         self._submit_io, self._poll_io = SUBMIT_IO_FN(submit_io), POLL_IO_FN(poll_io)
@@ -861,7 +893,8 @@ class VerifyMuxTile:
 
     def __init__(self, in_links, out_link, verifier, hashmap_seed=0x5EEDF00D, batch_txn_max=4096, inflight_max=2,
                  batch_wait_us=200, round_robin_idx=0, round_robin_cnt=1, cr_max=0, log_max=0, batch_sig_max=0,
-                 batch_bytes_max=0, lazy_iters=16, flow_control=False, register=True, gpu_parse=False):
+                 batch_bytes_max=0, lazy_iters=16, flow_control=False, register=True, gpu_parse=False,
+                 lap_span_max=0, lap_margin=0):
         import threading
         L = lib()
         in_links = list(in_links) if isinstance(in_links, (list, tuple)) else [in_links]
@@ -880,6 +913,7 @@ class VerifyMuxTile:
         vc.gpu_parse = int(gpu_parse)            # False/True/0/1/2 (2: the GPU also gathers the payloads)
         for i, ln in enumerate(in_links):
             vc.in_mcache[i], vc.in_depth[i] = ln.mcache_ptr, ln.depth
+        vc.lap_span_max, vc.lap_margin = lap_span_max, lap_margin   # 0: depth / 2, depth / 4; LAP_OFF: off
         self.vcfg = vc
         self._t = L.fdgpu_vmux_new(c.byref(vc), verifier.struct)
         if not self._t:
@@ -901,7 +935,13 @@ class VerifyMuxTile:
         self._rc = None
         self._registered = []
         if register:
-            bufs = [out_link.dcache] + ([ln.dcache for ln in in_links] if vc.gpu_parse == 2 else [])
+            # gather: the device reads the payloads in the in dcaches and
+            # re-reads their mcache lines (a shared-memory link: its region)
+            bufs = [out_link.dcache]
+            if vc.gpu_parse == 2:
+                for ln in in_links:
+                    reg = getattr(ln, "_region", None)
+                    bufs += [reg] if reg is not None else [ln.dcache, ln.mcache]
             for e in getattr(verifier, "engines", []):
                 for b in bufs:
                     e.host_register(b)
@@ -982,6 +1022,9 @@ class VerifyMuxTile:
             self.close()
         except Exception:
             pass
+
+
+LAP_OFF = (1 << 64) - 1      # lap_span_max / lap_margin: that part of the lap guard off
 
 
 def vmux_dcache_data_sz(cr_max, batch_txn_max, inflight_max=2):
@@ -1068,6 +1111,9 @@ class Producer:
                                          float(rate_tps))
         if not self._p:
             raise RuntimeError("fdgpu_producer_start failed")
+
+    def running(self):
+        return self._p is not None and not lib().fdgpu_producer_done(self._p)
 
     def join(self):
         el = c.c_double()

@@ -22,10 +22,13 @@
        reference's CPU fd_ed25519_verify; INTEGRATION.md 1 shows how both
        link into one process (the fdgpu_ed25519_* names below).
        The caller thread's current HIP device is preserved.  The reference
-       API returns verify codes only: on an engine failure (no GPU, a HIP
-       error) every call of the failed batch returns FD_ED25519_ERR_SIG
-       (fail closed) and fdgpu_sync_errors() counts it; FDGPU_SYNC_ABORT=1 in
-       the environment makes such a failure abort the process instead.
+       API returns verify codes only and never rejects a good signature, so
+       an engine failure (no GPU, a HIP error, a message beyond the engine's
+       32-bit arena, ~2 GB) aborts the process with the reason on stderr.
+       FDGPU_SYNC_FAIL_CLOSED=1 in the environment makes every call of the
+       failed batch return FD_ED25519_ERR_SIG instead (fdgpu_sync_errors()
+       counts the failures).  FDGPU_SYNC_DEVICE=<n> selects the device
+       (default 0).
 
    (ii) Asynchronous batch API for the verify stage (the north-star shim;
        SURVEY.md §8(b)(ii)).  One engine per GPU; each engine owns pinned,
@@ -289,26 +292,49 @@ int     fdgpu_poll_frags  ( fdgpu_engine_t * e, int64_t ticket, int8_t * codes, 
    (batch_single_msg), tags its first signature (fd_hash(hash_seed, sig, 64),
    the dedup tag fd_verify.c publishes as the frag's sig) and writes the out
    frag exactly as the reference's after_frag lays it out in the out dcache
-   (fd_verify.c:93-136): [payload][pad to 2][fd_txn_t][u16 payload_sz];
-   then out[0, out_sz) is copied back in one DMA.  out_cap must hold
+   (fd_verify.c:93-136): [payload][pad to 2][fd_txn_t][u16 payload_sz].
+   out_cap must hold
    align2(sz) + footprint + 2; fdgpu_frag_out_cap(sz) always does (a bound
    from the size alone).  fdgpu_poll_frags_io returns per frag the code (as
    fdgpu_poll_frags: FDGPU_CODE_PARSE_FAIL, FDGPU_CODE_TRAILER_CAP when the
-   parsed out frag does not fit out_cap), the tag (0 unless parsed) and the
-   out frag's size (0 unless parsed).  The payloads must stay unchanged until
-   the batch is polled -- a producer that may lap the reader is detected by
-   the caller after the poll (the tile re-checks the in mcache, as
-   fd_mux.c:641-655 does after its copy). */
+   parsed out frag does not fit out_cap, FDGPU_CODE_LAPPED below), the tag
+   (0 unless parsed) and the out frag's size (0 unless parsed).  The finish
+   kernel writes the out frags into `out` and the per-frag results into the
+   slot's pinned memory in place, over the bus (no copy is queued); both are
+   visible to the host once fdgpu_poll_frags_io has returned FDGPU_OK for the
+   ticket, and not before.
+
+   Overrun re-check on the device (the reference's seq re-check after its
+   copy, fd_mux.c:641-655): a frag with link = i + 1 names links[i], an in
+   link's mcache, and seq, the frag's sequence number on it.  After the
+   device has read the payload it re-reads that mcache line's seq over the
+   bus; if the producer has republished the line since (any other seq), the
+   payload may be torn and the frag gets FDGPU_CODE_LAPPED (no parse, no
+   verdict, no out frag).  Sound when the producer rewrites a payload only
+   after the line that published it: a compact dcache of depth + 1 frags
+   (fd_dcache_req_data_sz with burst 1), or the TPU reassembly slot arena
+   (fd_tpu.h: a slot is freed when its line is reused).  link = 0: no
+   re-check -- the caller guarantees the bytes stay unchanged until the poll
+   (e.g. it copied them itself).  links / link_cnt may be NULL / 0 when no
+   frag names one; each links[i].mcache must lie in a registered region. */
 typedef struct {
   uint64_t src;         /* host address of the payload */
   uint32_t sz;          /* <= FD_TXN_MTU (1232) */
   uint32_t out_off;
   uint32_t out_cap;
-  uint32_t _pad;
+  uint32_t link;        /* 0: no re-check; i + 1: re-check links[i]'s line of seq after the read */
+  uint64_t seq;         /* the frag's seq on that link */
 } fdgpu_frag_io_t;
+typedef struct {
+  uint64_t mcache;      /* host address of line 0 of an in link's mcache (fd_frag_meta_t, 32 B, seq first) */
+  uint64_t depth;       /* its depth, a power of 2 */
+} fdgpu_link_t;
+#define FDGPU_LINK_MAX    (16UL)
+#define FDGPU_CODE_LAPPED (-66)
 uint32_t fdgpu_frag_out_cap   ( uint32_t sz );
 int64_t  fdgpu_submit_frags_io( fdgpu_engine_t * e, fdgpu_frag_io_t const * frags, uint64_t frag_cnt,
-                                uint8_t * out, uint64_t out_sz, uint64_t hash_seed );
+                                uint8_t * out, uint64_t out_sz, uint64_t hash_seed,
+                                fdgpu_link_t const * links, uint64_t link_cnt );
 int      fdgpu_poll_frags_io  ( fdgpu_engine_t * e, int64_t ticket, int8_t * codes, uint64_t * tags,
                                 uint16_t * out_szs, int blocking );
 

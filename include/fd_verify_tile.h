@@ -219,7 +219,8 @@ typedef struct {
      where they lie, out frags written back by the verifier,
      fdgpu_submit_frags_io / fdgpu_poll_frags_io semantics. */
   int64_t   (*submit_io)    ( void * ctx, fdgpu_frag_io_t const * frags, uint64_t frag_cnt, uint8_t * out,
-                              uint64_t out_sz, uint64_t hash_seed );
+                              uint64_t out_sz, uint64_t hash_seed, fdgpu_link_t const * links,
+                              uint64_t link_cnt );
   int       (*poll_io)      ( void * ctx, int64_t ticket, int8_t * codes, uint64_t * tags, uint16_t * out_szs,
                               int blocking );
 } fdgpu_verifier_t;
@@ -286,6 +287,9 @@ typedef struct {
   uint64_t publish_ns;      /* resolving completed batches: tags, tcache, publishing (fdgpu_vmux) */
   uint64_t batch_fill_ns;   /* summed over batches: first frag taken -> submitted (fdgpu_vmux) */
   uint64_t batch_gpu_ns;    /* summed over batches: submitted -> a poll saw it complete (fdgpu_vmux) */
+  uint64_t lapped;          /* gpu_parse 2: frags the producer lapped before their payload was read
+                               (FDGPU_CODE_LAPPED; also counted in overrun) */
+  uint64_t rescued;         /* gpu_parse 2: payloads the lap guard copied on the tile's core at submit */
 } fdgpu_vtile_stats_t;
 
 typedef struct fdgpu_vtile fdgpu_vtile_t;
@@ -464,17 +468,33 @@ typedef struct {
                                                     and writes the out frags (submit_io / poll_io):
                                                     the tile touches no payload byte */
   uint32_t        _pad;
-  /* gpu_parse 2: the in links' mcaches, re-checked after a batch is polled
-     (a frag whose line the producer has lapped since is dropped as overrun;
-     the in dcaches must hold depth + 1 frags, as fdt_dcache_data_sz sizes
-     them, so an unlapped line means an intact payload) */
+  /* gpu_parse 2: the in links' mcaches.  The device re-reads each frag's
+     line after reading its payload (fdgpu_submit_frags_io's overrun
+     re-check, fd_mux.c:641-655 after the copy): a frag whose line the
+     producer republished before the read is dropped as overrun
+     (FDGPU_CODE_LAPPED, logged LOST).  Each in dcache must hold depth + 1
+     maximal frags (fdt_dcache_data_sz; checked: in_wmark - in_chunk0 >=
+     depth x FDT_TPU_MTU's chunks) or be a TPU reassembly slot arena, so an
+     unlapped line means an intact payload.  The mcaches must be registered
+     with the verifier's engines like the dcaches. */
   fdt_frag_meta_t const * in_mcache[ FDT_MUX_IN_MAX ];
   uint64_t        in_depth [ FDT_MUX_IN_MAX ];
+  /* gpu_parse 2, the lap guard: keeps the device's read of every payload
+     ahead of the producer (the quic -> verify link is unreliable: the
+     producer never waits, fd_frankendancer.c:131-133).
+       lap_span_max  the open batch closes once it spans this many seqs of
+                     any in link (0: depth / 2);
+       lap_margin    at submit, a frag whose line the producer will reuse
+                     within lap_margin more publishes (read in the mcache:
+                     the line lap_margin behind it already holds a seq of
+                     the next lap) is copied by the tile into its out frag's
+                     room right away, re-checked as fd_mux.c:641-655 does,
+                     and handed to the device from there (counted as
+                     `rescued`; one lapped already is dropped) (0: depth / 4).
+     ~0UL disables either. */
+  uint64_t        lap_span_max;
+  uint64_t        lap_margin;
 } fdgpu_vmux_cfg_t;
-
-/* gpu_parse 2: the code a frag gets when its in-mcache line was lapped
-   before the batch was polled (counted as overrun, logged LOST) */
-#define FDGPU_CODE_LAPPED (-66)
 
 typedef struct fdgpu_vmux fdgpu_vmux_t;
 
@@ -634,8 +654,12 @@ fdgpu_producer_t * fdgpu_producer_start( fdt_frag_meta_t * mcache, uint64_t dept
                                          uint8_t * base, uint64_t chunk0, uint64_t wmark,
                                          uint8_t const * arena, uint64_t const * off, uint32_t const * sz,
                                          uint64_t cnt, double rate_tps );
-/* Waits for the producer; returns frags published, *elapsed_s its wall time. */
+/* Waits for the producer; returns frags published, *elapsed_s the time it
+   spent publishing them (first frag to last; a paced producer's counter
+   calibration before the first frag is not counted). */
 uint64_t           fdgpu_producer_join ( fdgpu_producer_t * p, double * elapsed_s );
+/* 1 once the producer has published its last frag (join does not block then). */
+int                fdgpu_producer_done ( fdgpu_producer_t const * p );
 
 #ifdef __cplusplus
 }

@@ -106,3 +106,54 @@ def test_stamps_variant_builds():
     so = os.path.join(os.path.dirname(_lib.HEADER_PATH), "..", "build", "stamps", "libfd_ed25519_gpu.so")
     out = subprocess.run(["nm", "-D", "--defined-only", so], capture_output=True, text=True, check=True).stdout
     assert "fdgpu_debug_stamps" in out and "fdgpu_submit" in out
+
+
+_SYNC_CALL = r"""
+import ctypes, os, sys
+sys.path.insert(0, {repo!r})
+from firedancer_amd import _lib
+L = _lib.lib()
+rc = L.fd_ed25519_verify(b"abc", 3, bytes(64), bytes(32), None)
+print("rc", rc, "errors", L.fdgpu_sync_errors(), flush=True)
+"""
+
+
+def _sync_child(env_extra):
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k != "FDGPU_SYNC_FAIL_CLOSED"}
+    env.update(FDGPU_SYNC_DEVICE="99", **env_extra)
+    return subprocess.run(["python", "-c", _SYNC_CALL.format(repo=repo)], capture_output=True, text=True, env=env,
+                          timeout=120)
+
+
+def test_sync_api_engine_failure_aborts_by_default():
+    """The reference's fd_ed25519_verify never answers a good signature with
+    an error, so an engine failure (here: no device 99, on any machine) aborts
+    the process with the reason on stderr rather than returning a verdict."""
+    r = _sync_child({})
+    assert r.returncode == -6, (r.returncode, r.stdout, r.stderr[-500:])
+    assert "fd_ed25519_gpu:" in r.stderr and "FDGPU_SYNC_FAIL_CLOSED" in r.stderr
+    assert "rc" not in r.stdout
+
+
+def test_sync_api_fail_closed_opt_in():
+    """FDGPU_SYNC_FAIL_CLOSED=1: the failed call returns FD_ED25519_ERR_SIG
+    and fdgpu_sync_errors() counts it."""
+    r = _sync_child({"FDGPU_SYNC_FAIL_CLOSED": "1"})
+    assert r.returncode == 0, r.stderr[-500:]
+    assert r.stdout.split() == ["rc", "-1", "errors", "1"]
+
+
+def test_frag_io_structs_layout():
+    """fdgpu_frag_io_t (32 B: src, sz, out_off, out_cap, link, seq) and
+    fdgpu_link_t (16 B) as C sees them match the Python dtypes."""
+    from firedancer_amd import ed25519 as ed, tile
+    src = (f'#include "{_lib.HEADER_PATH}"\n#include <stddef.h>\n'
+           '_Static_assert(sizeof(fdgpu_frag_io_t) == 32, "io");\n'
+           '_Static_assert(offsetof(fdgpu_frag_io_t, link) == 20 && offsetof(fdgpu_frag_io_t, seq) == 24, "io");\n'
+           '_Static_assert(sizeof(fdgpu_link_t) == 16, "link");\nint main(void){ return 0; }\n')
+    r = subprocess.run(["gcc", "-std=c11", "-Wall", "-Werror", "-x", "c", "-", "-fsyntax-only"], input=src,
+                       capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+    assert ed.FRAG_IO_DTYPE.itemsize == tile.FRAG_IO_DTYPE.itemsize == 32
+    assert ed.FRAG_IO_DTYPE.fields["seq"][1] == 24 and ed.LINK_DTYPE.itemsize == 16

@@ -21,7 +21,11 @@ def test_tile_cmd_parses():
     assert args.mux == 1 and args.gpu_parse == 2 and args.producers_same_as_tiles == 1
     assert args.payload_npz == "/tmp/x.npz" and args.cpu_list == "3,4,5,6" and args.device == 0
     assert args.hw_queues == bench.TILE_HW_QUEUES and args.reps == bench.TILE_REPS
-    assert args.depth_lg == 21 and args.depth_lg_paced == 19        # a prefill fits its links
+    assert args.depth_lg == 21                                       # a prefill fits its links
+    # paced runs: the reference's quic -> verify depth (receive_buffer_size, default.toml:888-893), and a
+    # stream long enough that the producers can lap the tiles (>= 20 x the depth per link)
+    assert args.depth_lg_paced == 14 and args.lap_guard == 1
+    assert 1_000_000 * args.paced_reps // 4 >= 20 * (1 << args.depth_lg_paced)
     runs = [tuple(float(x) for x in r.split(",")) for r in args.sweep.split(";")]
     assert len(runs) == len(bench.TILE_RUNS)
     for (name, tiles_n, prods, rate), (t, b, k, r, p) in zip(bench.TILE_RUNS, runs):

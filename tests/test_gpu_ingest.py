@@ -251,7 +251,7 @@ def test_ring_frag_io_batches(engine, oracle, txn_fixtures, quic_corpus):
                 if ci == 1 and k % 89 == 3 and fp:
                     cap = ((len(p) + 1) & ~1) + fp + 1        # one byte short
                     short.add(k)
-                fio[k] = (in_buf.ctypes.data + a, len(p), o, cap, 0)
+                fio[k] = (in_buf.ctypes.data + a, len(p), o, cap, 0, 0)
                 o += (cap + 63) // 64 * 64
             base = out_base[0]
             out_base[0] += o
@@ -296,9 +296,91 @@ def test_ring_frag_io_batches(engine, oracle, txn_fixtures, quic_corpus):
         # a payload outside every registered region
         stray = np.zeros(4096, dtype=np.uint8)
         fio = np.zeros(1, dtype=FRAG_IO_DTYPE)
-        fio[0] = ((stray.ctypes.data + 63) // 64 * 64, 100, 0, L.fdgpu_frag_out_cap(100), 0)
+        fio[0] = ((stray.ctypes.data + 63) // 64 * 64, 100, 0, L.fdgpu_frag_out_cap(100), 0, 0)
         with pytest.raises(RuntimeError):
             engine.submit_frags_io(fio, out_buf, 4096, seed)
     finally:
         engine.host_unregister(in_buf)
         engine.host_unregister(out_buf)
+
+
+def _pages(n):
+    """n bytes on pages of their own (registrable next to other buffers)"""
+    return _aligned((n + 4095) // 4096 * 4096)[:n]
+
+
+def test_frag_io_device_lap_recheck(engine, oracle):
+    """The gather's overrun re-check on the device (fdgpu_submit_frags_io
+    with links: the reference's seq re-check after its copy,
+    fd_mux.c:641-655): after reading a payload the device re-reads the frag's
+    line in the registered in mcache; a line that holds another seq (the
+    producer republished it) gives FDGPU_CODE_LAPPED, no tag and no out frag;
+    every other frag -- including one naming no link, which is not
+    re-checked -- verifies as the oracle says and gets its out frag.  A link
+    index outside the table, an unregistered mcache or a bad depth is
+    refused."""
+    from firedancer_amd.ed25519 import CODE_LAPPED, FRAG_IO_DTYPE
+    from firedancer_amd import _lib
+    L = _lib.lib()
+    a, t, _ = workload.cfg1(310, seed=0x1A9)
+    ps = [p for p in workload.payloads(a, t) if tile.txn_parse(p)[0]][:300]
+    assert len(ps) == 300
+    depth, seq0 = 256, (1 << 40) + 7
+    mc = _pages(depth * 32).view(tile.FRAG_META_DTYPE)
+    in_buf = _pages(len(ps) * 1280)
+    out_buf = _pages(len(ps) * 2176)
+    for b in (mc, in_buf, out_buf):
+        engine.host_register(b)
+    try:
+        fio = np.zeros(len(ps), dtype=FRAG_IO_DTYPE)
+        o = 0
+        for k, p in enumerate(ps):
+            in_buf[k * 1280:k * 1280 + len(p)] = np.frombuffer(p, dtype=np.uint8)
+            cap = L.fdgpu_frag_out_cap(len(p))
+            fio[k] = (in_buf.ctypes.data + k * 1280, len(p), o, cap, 0 if k % 50 == 7 else 1, seq0 + k)
+            o += (cap + 63) // 64 * 64
+            mc[(seq0 + k) % depth]["seq"] = seq0 + k
+        lapped = set(range(3, len(ps), 11)) - {k for k in range(len(ps)) if k % 50 == 7} - set(range(depth, len(ps)))
+        for k in range(len(ps)):
+            if k >= depth:                                 # lines reused by later frags of the batch: seq0 + k
+                continue
+            if k in lapped:
+                mc[(seq0 + k) % depth]["seq"] = seq0 + k + depth
+        # frags past depth share lines with the first ones: the line holds the later seq, so the earlier
+        # frag of each such pair is lapped and the later one is not
+        lapped |= {k - depth for k in range(depth, len(ps)) if (k - depth) % 50 != 7}
+        for k in range(depth, len(ps)):
+            mc[(seq0 + k) % depth]["seq"] = seq0 + k
+        links = [(mc.ctypes.data, depth)]
+        tk = engine.submit_frags_io(fio, out_buf, o, 0x77, links=links)
+        codes, tags, osz = engine.poll_frags_io(tk)
+        arena = np.frombuffer(b"".join(ps) + b"\0" * 16, dtype=np.uint8)
+        offs = np.cumsum([0] + [len(p) for p in ps])
+        td = np.zeros(len(ps), dtype=workload.TXN_DTYPE)
+        for k, p in enumerate(ps):
+            d = tile.txn_decode(tile.txn_parse(p)[1])
+            td[k] = (int(offs[k]) + d["message_off"], len(p) - d["message_off"], int(offs[k]) + d["signature_off"],
+                     int(offs[k]) + d["acct_addr_off"], d["signature_cnt"])
+        exp = oracle.verify_txns(arena, td)
+        assert len(lapped) > 20
+        for k, p in enumerate(ps):
+            if k in lapped:
+                assert codes[k] == CODE_LAPPED and tags[k] == 0 and osz[k] == 0, k
+            else:
+                assert codes[k] == exp[k] and osz[k] > len(p), k
+                fp, raw = tile.txn_parse(p)
+                frag = p + b"\0" * (((len(p) + 1) & ~1) - len(p)) + raw + len(p).to_bytes(2, "little")
+                off = int(fio[k]["out_off"])
+                assert bytes(out_buf[off:off + len(frag)]) == frag, k
+        bad = fio[:4].copy()
+        bad["link"] = 2                                    # only one link given
+        with pytest.raises(RuntimeError):
+            engine.submit_frags_io(bad, out_buf, o, 0x77, links=links)
+        stray = _pages(depth * 32)
+        with pytest.raises(RuntimeError):
+            engine.submit_frags_io(fio[:4], out_buf, o, 0x77, links=[(stray.ctypes.data, depth)])
+        with pytest.raises(RuntimeError):
+            engine.submit_frags_io(fio[:4], out_buf, o, 0x77, links=[(mc.ctypes.data, depth - 1)])
+    finally:
+        for b in (mc, in_buf, out_buf):
+            engine.host_unregister(b)

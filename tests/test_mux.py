@@ -306,6 +306,84 @@ def test_vmux_gather_drops_lapped_frags(oracle):
     vm.close()
 
 
+def test_vmux_gather_lap_guard_rescues_waiting_frags(oracle):
+    """gpu_parse 2, the lap guard: a closed batch that cannot go out (its one
+    verifier slot busy) while the producer keeps publishing -- the quic ->
+    verify link never waits -- has its frags copied on the tile's core once
+    the producer gets within lap_margin (depth / 4) publishes of their lines,
+    and the verifier then reads those copies: they are verified as the model
+    says.  The in-flight batch's frags whose lines were republished before
+    the (late) read are dropped as lapped, and only those."""
+    ps = _mixed_stream(200, seed=21)[:70]
+    assert len(ps) == 70
+    inl = tile.Link(64, 1232)
+    outl = tile.Link(256, tile.TPU_DCACHE_MTU, data_sz=256 * (tile.TPU_DCACHE_MTU + 64))
+    ver = tile.PyVerifier(oracle_fn(oracle), slots=1, lag=1 << 60)       # pending until released below
+    vm = tile.VerifyMuxTile(inl, outl, ver, hashmap_seed=0x78, batch_txn_max=16, inflight_max=1, log_max=1 << 10,
+                            batch_wait_us=100, gpu_parse=2)
+    for p in ps[:16]:
+        inl.publish(p)
+    vm.start()
+    _wait(lambda: len(ver.batches) == 1)                    # seqs 0..15 in flight, not yet read
+    for p in ps[16:32]:
+        inl.publish(p)                                      # seqs 16..31: the next batch, closed, waiting
+    _wait(lambda: vm.stats()["in_frags"] == 32)
+    assert vm.stats()["rescued"] == 0
+    for p in ps[32:]:
+        inl.publish(p)                                      # up to seq 69: lines 0..5 reused, and the
+    _wait(lambda: vm.stats()["rescued"] == 6)               # producer within 16 of lines 16..21's reuse
+    time.sleep(0.05)
+    assert vm.stats()["rescued"] == 6
+    ver.lag = 0
+    _wait(lambda: vm.final_cnt() == len(ps))
+    vm.stop()
+    seqs, codes = vm.log()
+    assert seqs.tolist() == list(range(len(ps)))
+    assert codes.tolist()[:6] == [3] * 6                    # FDGPU_VTILE_LOG_LOST: lapped before the read
+    tail_out, tail_pub = tile_model.verify_tile_model(ps[6:], 0x78, oracle_fn(oracle), seq0=6)
+    assert codes.tolist()[6:] == tail_out
+    outs = outl.drain()
+    assert [(m["sig"], tile.split_verify_output(f)) for m, f in outs] == [(t, (p, raw)) for p, raw, t in tail_pub]
+    st = vm.stats()
+    assert st["lapped"] == st["overrun"] == 6 and st["rescued"] == 6
+    vm.close()
+
+
+def test_vmux_gather_span_cap_closes_batches(oracle):
+    """gpu_parse 2: a batch closes once it spans lap_span_max seqs of a link
+    (default depth / 2), whatever its txn cap: 4 round-robin tiles' shares of
+    a 64-deep link go out as batches of at most 32 / 4 frags each."""
+    ps = _mixed_stream(400, seed=23)
+    inl = tile.Link(64, 1232)
+    outl = tile.Link(1 << 10, tile.TPU_DCACHE_MTU, data_sz=(len(ps) + 8) * (tile.TPU_DCACHE_MTU + 64))
+    ver = tile.PyVerifier(oracle_fn(oracle), slots=4)
+    vm = tile.VerifyMuxTile(inl, outl, ver, hashmap_seed=0x79, batch_txn_max=1000, inflight_max=4, log_max=1 << 12,
+                            batch_wait_us=1e6, round_robin_idx=1, round_robin_cnt=4, gpu_parse=2)
+    vm.start()
+    for k in range(0, len(ps), 40):                         # in steps the tile keeps up with: nothing lapped
+        for p in ps[k:k + 40]:
+            inl.publish(p)
+        _wait(lambda: vm.stats()["in_frags"] == min(k + 40, len(ps)))
+    _wait(lambda: vm.final_cnt() == len(ps))
+    vm.stop()
+    assert ver.batches and max(ver.batches) <= 8 and sum(ver.batches) == len(range(1, len(ps), 4))
+    exp_out, _ = tile_model.verify_tile_model(ps, 0x79, oracle_fn(oracle), rr_idx=1, rr_cnt=4)
+    assert vm.log()[1].tolist() == exp_out
+    vm.close()
+
+
+def test_vmux_gather_refuses_a_shallow_in_dcache():
+    """gpu_parse 2 needs each in dcache to hold depth + 1 maximal frags (so an
+    unlapped line means an intact payload): a smaller one is refused."""
+    ver = tile.PyVerifier(lambda a, t: np.zeros(len(t), dtype=np.int8))
+    outl = tile.Link(64, tile.TPU_DCACHE_MTU, data_sz=tile.vmux_dcache_data_sz(64, 16, 2))
+    small = tile.Link(64, 1232, data_sz=40 * 1280)
+    with pytest.raises(RuntimeError):
+        tile.VerifyMuxTile(small, outl, ver, batch_txn_max=16, gpu_parse=2)
+    tile.VerifyMuxTile(small, outl, ver, batch_txn_max=16, gpu_parse=1).close()     # copy modes read at once
+    tile.VerifyMuxTile(tile.Link(64, 1232), outl, ver, batch_txn_max=16, gpu_parse=2).close()
+
+
 def test_frag_out_cap_bounds_every_parse(quic_corpus):
     """fdgpu_frag_out_cap(sz) (the gather tile's reservation, from the size
     alone) holds [payload][pad][fd_txn_t][u16] for every payload that

@@ -215,3 +215,147 @@ def test_vmux_two_tiles_share_engines_gpu(engines, oracle, gpu_parse):
         assert [(s, tile.split_verify_output(f)) for s, f in seen[k]] == [(t, (p, raw)) for p, raw, t in pub]
         vm.close()
         vers[k].close()
+
+
+# --------------------- the gather tile against a producer that laps it
+
+def _gather_lap_run(engines, oracle, ps, depth, rate, batch, inflight, wait_us, guard):
+    """A Producer thread publishes ps at `rate` into a `depth`-deep quic ->
+    verify link while the gather-mode mux tile (gpu_parse 2) runs over the
+    MI355X: returns the tile's stats and, for the frags it did not lose, its
+    outcomes and published stream next to the sequential model's over
+    exactly those frags (the lost ones -- lapped before the device read
+    them, or skipped by the mux as overrun -- never reach the tcache)."""
+    import time
+    seed = 0x1AB
+    arena, offs, sizes = workload.pack_payloads(ps)
+    inl = tile.Link(depth, 1232)
+    od = 1 << (len(ps) - 1).bit_length()
+    outl = tile.Link(od, tile.TPU_DCACHE_MTU, data_sz=(len(ps) + 64) * (tile.TPU_DCACHE_MTU + 64))
+    ver = tile.EngineVerifier(engines[:1])
+    kw = {} if guard else dict(lap_span_max=tile.LAP_OFF, lap_margin=tile.LAP_OFF)
+    vm = tile.VerifyMuxTile(inl, outl, ver, hashmap_seed=seed, batch_txn_max=batch, inflight_max=inflight,
+                            batch_wait_us=wait_us, log_max=1 << 17, gpu_parse=2, **kw)
+    try:
+        vm.start()
+        prod = tile.Producer(inl, arena, offs, sizes, rate_tps=rate)
+        n_pub, _ = prod.join()
+        assert n_pub == len(ps)
+        t0, last = time.time(), -1
+        while True:                                   # the tile is done once nothing changes and nothing is held
+            time.sleep(0.2)
+            cur = vm.final_cnt()
+            if cur == last and vm.idle():
+                break
+            last = cur
+            assert time.time() - t0 < 60
+        vm.stop()
+        st, mst = vm.stats(), vm.mux_stats()
+        assert st["corrupt"] == 0 and st["verify_errors"] == 0
+        assert vm.final_cnt() + mst["overrun_polling"] + mst["overrun_reading"] == len(ps)
+        seqs, codes = vm.log()
+        lost = codes == tile.LOG_LOST
+        assert int(lost.sum()) == st["lapped"] == st["overrun"]
+        kept = seqs[~lost].tolist()
+        exp_out, exp_pub = tile_model.verify_tile_model([ps[s] for s in kept], seed,
+                                                        lambda a, t: oracle.verify_txns(a, t), seqs=kept)
+        assert codes[~lost].tolist() == exp_out
+        outs = outl.drain()
+        # no torn frag published: every published frag is the model's, payload and trailer
+        assert [(m["sig"], tile.split_verify_output(f)) for m, f in outs] == [(t, (p, raw)) for p, raw, t in exp_pub]
+        return st, mst, len(kept)
+    finally:
+        vm.close()
+        ver.close()
+
+
+def test_vmux_gather_drops_frags_lapped_on_device_gpu(engines, oracle):
+    """Lap guard off, batches held 3 ms on a 1024-deep link fed at 1 M
+    frags/s: the producer laps the oldest frags of every batch before the
+    device reads them; the device's re-check of each frag's mcache line
+    (fdgpu_submit_frags_io links) drops exactly those as lapped, and every
+    other frag is verified, deduplicated and published as the reference loop
+    would, with no torn payload published."""
+    from test_tile import _mixed_stream
+    ps = _mixed_stream(20000, seed=31)
+    st, mst, kept = _gather_lap_run(engines, oracle, ps, 1024, 1.0e6, 4096, 3, 3000, guard=False)
+    assert st["lapped"] > 1000 and kept > 2000 and st["rescued"] == 0
+
+
+def test_vmux_gather_lap_guard_gpu(engines, oracle):
+    """The same stream with the lap guard on (batches close at depth / 2
+    seqs, frags within depth / 4 of being lapped copied by the tile): the
+    tile's outcomes and published stream equal the model's over every frag
+    it kept, and it keeps nearly all of them."""
+    from test_tile import _mixed_stream
+    ps = _mixed_stream(20000, seed=31)
+    st, mst, kept = _gather_lap_run(engines, oracle, ps, 1024, 1.0e6, 4096, 3, 3000, guard=True)
+    assert kept >= len(ps) * 0.95, (st, mst)
+
+
+def test_vmux_gather_reads_reasm_link_gpu(oracle, engines):
+    """The gather-mode mux tile on the reference's actual quic -> verify link
+    type, the TPU reassembly slot arena (fd_tpu.h:20-45, fd_frankendancer.c:
+    59 is_reasm): fragmented streams reassembled and published while the tile
+    runs on its thread; the device reads each payload in its slot and
+    re-checks the slot's mcache line; outcomes and the published stream equal
+    the model's.  A shallow arena with the lap guard off and batches held
+    20 ms is lapped (a reused slot is rewritten under the pending batch):
+    exactly the lapped frags are dropped, none is published torn."""
+    import random
+    import time
+    from test_tile import _mixed_stream
+    for depth, burst, n, guard, wait_us in ((1 << 12, 32, 4000, True, 100), (64, 4, 3000, False, 20000)):
+        ps = [p for p in _mixed_stream(n, seed=depth + burst) if len(p) <= 1232]
+        rnd = random.Random(depth)
+        r = tile.TpuReasm(depth, burst)
+        outl = tile.Link(1 << 13, tile.TPU_DCACHE_MTU, data_sz=(len(ps) + 64) * (tile.TPU_DCACHE_MTU + 64))
+        ver = tile.EngineVerifier(engines[:1])
+        kw = {} if guard else dict(lap_span_max=tile.LAP_OFF, lap_margin=tile.LAP_OFF)
+        vm = tile.VerifyMuxTile(r, outl, ver, batch_txn_max=256, inflight_max=2, batch_wait_us=wait_us,
+                                log_max=1 << 14, gpu_parse=2, **kw)
+        try:
+            vm.start()
+            i, open_, pub_order = 0, [], []
+            while i < len(ps) or open_:
+                if i < len(ps) and len(open_) < burst and (not open_ or rnd.random() < 0.5):
+                    open_.append([r.prepare(), ps[i], 0])
+                    i += 1
+                    continue
+                k = rnd.randrange(len(open_))
+                slot, p, sent = open_[k]
+                m = rnd.randrange(1, 400)
+                back = rnd.randrange(0, min(sent, 20) + 1)
+                assert r.append(slot, p[sent - back:sent + m], sent - back) == tile.REASM_SUCCESS
+                open_[k][2] = min(len(p), sent + m)
+                if open_[k][2] == len(p):
+                    assert r.publish(slot) == tile.REASM_SUCCESS
+                    pub_order.append(p)
+                    open_.pop(k)
+            t0 = time.time()
+            last = -1
+            while not (vm.idle() and vm.final_cnt() == last):     # (unguarded: the mux may skip lapped seqs)
+                last = vm.final_cnt()
+                assert time.time() - t0 < 60
+                time.sleep(0.1)
+            assert vm.final_cnt() == r.next_seq or not guard
+            vm.stop()
+            st = vm.stats()
+            seqs, codes = vm.log()
+            if guard:
+                assert seqs.tolist() == list(range(r.next_seq))
+            lost = codes == tile.LOG_LOST
+            assert int(lost.sum()) == st["lapped"]
+            kept = seqs[~lost].tolist()
+            exp_out, exp_pub = tile_model.verify_tile_model([pub_order[s] for s in kept], 0x5EEDF00D,
+                                                            lambda a, t: oracle.verify_txns(a, t), seqs=kept)
+            assert codes[~lost].tolist() == exp_out
+            outs = outl.drain()
+            assert [tile.split_verify_output(f)[0] for _, f in outs] == [p for p, _, _ in exp_pub]
+            if guard:
+                assert st["lapped"] == 0 and exp_out.count(0) > 100
+            else:
+                assert st["lapped"] > 0 and len(kept) > 100
+        finally:
+            vm.close()
+            ver.close()

@@ -44,14 +44,15 @@ def txn_descriptor(payload, raw):
             d["signature_cnt"])
 
 
-def verify_tile_model(payloads, seed, verify_fn, rr_idx=0, rr_cnt=1, tcache=None, seq0=0):
-    """payloads: list of bytes (one frag each, seq0+i).  verify_fn(arena, txns)
-    -> codes (the oracle).  Returns (outcomes list, published list of
+def verify_tile_model(payloads, seed, verify_fn, rr_idx=0, rr_cnt=1, tcache=None, seq0=0, seqs=None):
+    """payloads: list of bytes (one frag each, seq0+i; or seqs[i] when given:
+    the frags a tile saw when others were lost to overrun).  verify_fn(arena,
+    txns) -> codes (the oracle).  Returns (outcomes list, published list of
     (payload, raw fd_txn_t, tag))."""
     tc = tcache if tcache is not None else TCacheModel(tile.VERIFY_TCACHE_DEPTH)
     outcomes, published = [], []
     for i, p in enumerate(payloads):
-        seq = seq0 + i
+        seq = seqs[i] if seqs is not None else seq0 + i
         if rr_cnt > 1 and seq % rr_cnt != rr_idx:
             outcomes.append(tile.LOG_FILTERED)
             continue

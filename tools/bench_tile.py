@@ -72,6 +72,10 @@ def make_parser():
                          "instead of generating --txns")
     ap.add_argument("--depth-lg-paced", type=int, default=0,
                     help="log2 of the link depth for paced runs (rate > 0); 0: --depth-lg")
+    ap.add_argument("--paced-reps", type=int, default=1,
+                    help="paced runs publish the frag stream this many times over (a long stream on a shallow "
+                         "link: the producers can lap the tiles)")
+    ap.add_argument("--lap-guard", type=int, default=1, help="gather tile: 1 the lap guard on (default), 0 off")
     ap.add_argument("--cpu-list", default="", help="','-separated CPUs to pin producers and tiles to, in order")
     ap.add_argument("--device", type=int, default=-1, help="the GPU every tile's engine uses (-1: tile k on k %% gpus)")
     return ap
@@ -114,7 +118,7 @@ def main():
         line = json.dumps(res)
         print(line, flush=True)
         lines.append(line)
-        ok &= res["counters"]["published"] == res["expected_published"] and res["counters"]["overrun"] == 0
+        ok &= res["published_ok"] and res["counters"]["overrun"] == 0
     if args.out:
         with open(args.out, "w") as f:
             f.write("\n".join(lines) + "\n")
@@ -178,7 +182,7 @@ def warm_io(engines, inflight, ps, out_bytes):
     for k, p in enumerate(ps):
         src[k * 1280:k * 1280 + len(p)] = np.frombuffer(p, dtype=np.uint8)
         cap = L.fdgpu_frag_out_cap(len(p))
-        fio[k] = (src.ctypes.data + k * 1280, len(p), o, cap, 0)
+        fio[k] = (src.ctypes.data + k * 1280, len(p), o, cap, 0, 0)
         o += (cap + 63) // 64 * 64
     for e in engines:
         e.host_register(src)
@@ -272,9 +276,10 @@ def run_once_mux(args, ps, arena, offs, sizes, n_sig, modes, tiles_n, batch, inf
     for k in range(tiles_n):
         ver = tile.EngineVerifier([engines[k]])
         outl = tile.Link(1 << 14, tile.TPU_DCACHE_MTU, data_sz=tile.vmux_dcache_data_sz(1 << 14, batch, inflight))
+        guard = {} if getattr(args, "lap_guard", 1) else dict(lap_span_max=tile.LAP_OFF, lap_margin=tile.LAP_OFF)
         vms.append(tile.VerifyMuxTile(inls, outl, ver, batch_txn_max=batch, inflight_max=inflight,
                                       batch_wait_us=args.wait_us, round_robin_idx=k, round_robin_cnt=tiles_n,
-                                      gpu_parse=int(args.gpu_parse)))
+                                      gpu_parse=int(args.gpu_parse), **guard))
         vers.append((ver, outl))
     cpus = cpus or workload.physical_cpus()[getattr(args, "cpu_offset", 0):] or workload.physical_cpus()
     # tile k's thread is pinned to cpus[P + k] (VerifyMuxTile.start inherits the caller's mask)
@@ -285,11 +290,15 @@ def run_once_mux(args, ps, arena, offs, sizes, n_sig, modes, tiles_n, batch, inf
     # j/P-th of the way in, so a txn's copies are far apart in every tile's
     # tcache window): P x N frags, long enough that the pipeline's fill and
     # drain do not dominate the drain time of several tiles
+    reps = 1
     if prefill:
         n = len(offs)
         feeds = [(np.roll(offs, -(j * n // P)), np.roll(sizes, -(j * n // P))) for j in range(P)]
     else:
-        feeds = [(offs[j::P], sizes[j::P]) for j in range(P)]
+        # paced: link j carries every P-th frag, the stream published paced_reps times over (a txn's
+        # copies are len(ps) frags apart: far outside the tiles' 16-deep tcache window)
+        reps = max(1, getattr(args, "paced_reps", 1))
+        feeds = [(np.tile(offs[j::P], reps), np.tile(sizes[j::P], reps)) for j in range(P)]
     n_total = sum(len(f[0]) for f in feeds)
     start = time.perf_counter()
     prods = [start_producer(args, inls[j], arena, feeds[j][0], feeds[j][1], 0.0 if prefill else rate / P, cpus, j)
@@ -303,11 +312,23 @@ def run_once_mux(args, ps, arena, offs, sizes, n_sig, modes, tiles_n, batch, inf
             os.sched_setaffinity(0, {cpus[(P + k) % len(cpus)]})
         vm.start()
     os.sched_setaffinity(0, keep)
+    # done: every frag's outcome final -- or, when frags were lost to the
+    # producers (lapped: the tiles log those too; skipped by the mux while it
+    # lagged: never seen), the producers finished and the tiles sit idle with
+    # no outcome added for 20 ms
+    idle_since, last = None, -1
     while any(vm.final_cnt() < n_total for vm in vms):
-        if time.perf_counter() - start > 300:
+        now = time.perf_counter()
+        if now - start > 300:
             raise SystemExit("verify mux tiles timed out")
+        cur = sum(vm.final_cnt() for vm in vms)
+        if cur != last or not all(vm.idle() for vm in vms) or (not prefill and any(pr.running() for pr in prods)):
+            idle_since, last = now, cur
+        elif now - idle_since > 0.02:
+            break
         time.sleep(0.0002)
-    wall = time.perf_counter() - start
+    wall = (idle_since if idle_since is not None and any(vm.final_cnt() < n_total for vm in vms)
+            else time.perf_counter()) - start
     for vm in vms:
         vm.stop()
     if not prefill:
@@ -317,7 +338,13 @@ def run_once_mux(args, ps, arena, offs, sizes, n_sig, modes, tiles_n, batch, inf
     mstats = [vm.mux_stats() for vm in vms]
     lat = np.concatenate([vm.latencies_ns() for vm in vms]) / 1e6
     agg = {k: int(sum(s[k] for s in stats)) for k in stats[0]}
-    agg["overrun"] = int(sum(m["overrun_polling"] + m["overrun_reading"] for m in mstats))
+    # every frag lost to the producers: lapped before the device read it (the
+    # tile's own count, FDGPU_CODE_LAPPED), skipped while the mux lagged, or
+    # overwritten while the mux read its metadata
+    agg["lapped"] = int(sum(s["lapped"] for s in stats))
+    agg["overrun_polling"] = int(sum(m["overrun_polling"] for m in mstats))
+    agg["overrun_reading"] = int(sum(m["overrun_reading"] for m in mstats))
+    agg["overrun"] = agg["lapped"] + agg["overrun_polling"] + agg["overrun_reading"]
     res = {
         "metric": "verify mux tile end-to-end transactions/s (tango in -> GPU verify -> tango out)",
         "tile": "fdgpu_vmux on fdt_mux_run (mux callbacks; registered out dcache, no staging copy)"
@@ -328,7 +355,10 @@ def run_once_mux(args, ps, arena, offs, sizes, n_sig, modes, tiles_n, batch, inf
         "sigs_per_s": round(n_sig * n_total / len(ps) / wall, 1),
         "wall_s": round(wall, 4), "producer_s": round(prod_s, 4), "producer_published": int(n_pub),
         "gpus": args.gpus, "tiles": tiles_n, "batch_txn_max": batch, "inflight": inflight,
-        "rate_target": rate, "prefill": prefill,
+        "rate_target": rate, "prefill": prefill, "link_depth": 1 << args.depth_lg,
+        # what the producers actually offered: frags published / their publishing time
+        "offered_txns_per_s": round(n_pub / prod_s, 1) if prod_s > 0 and not prefill else None,
+        "stream_reps": reps, "lap_guard": int(getattr(args, "lap_guard", 1)),
         "workload": "cfg3 (1-12 sigs/txn, payload <= 1232 B, 10% corrupted)" if getattr(args, "multi", 0) else "cfg1 (1 sig, msg U[180,220] B, 10% corrupted)",
         "txns": n_total, "sigs": n_sig * n_total // len(ps), "batch_wait_us": args.wait_us, "cpus": cpus[:P + tiles_n],
         "batch_latency_ms": {"p50": round(float(np.percentile(lat, 50)), 3) if len(lat) else None,
@@ -337,6 +367,7 @@ def run_once_mux(args, ps, arena, offs, sizes, n_sig, modes, tiles_n, batch, inf
         "counters": agg, "mux": {k: int(sum(m[k] for m in mstats)) for k in mstats[0]},
         "expected_published": int((modes == 0).sum()) * (n_total // len(ps)),
     }
+    res["published_ok"] = res["counters"]["published"] == res["expected_published"]
     for vm in vms:
         vm.close()
     for ver, _ in vers:

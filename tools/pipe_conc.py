@@ -40,7 +40,7 @@ def frag_batch(B, seed=5):
     o = 0
     for k, p in enumerate(ps):
         src[k * 1280:k * 1280 + len(p)] = np.frombuffer(p, dtype=np.uint8)
-        fio[k] = (src.ctypes.data + k * 1280, len(p), o, caps[k], 0)
+        fio[k] = (src.ctypes.data + k * 1280, len(p), o, caps[k], 0, 0)
         o += (caps[k] + 63) // 64 * 64
     return src, out, out_bytes, fio
 
