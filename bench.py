@@ -277,6 +277,86 @@ def latency_and_pcie(eng, arena, txns, batch, nbatches, pin_cpu=None):
             "pcie_inclusive_registered_sigs_per_s_per_gpu": round(pcie_reg, 1)}
 
 
+def latency_frag_io(eng, arena, txns, ref_codes, batch, nbatches, pin_cpu=None, views_n=4):
+    """p50/p99 submit -> results-on-host latency of the verify tile's own
+    path, gathered frag batches (fdgpu_submit_frags_io): `batch` raw payloads
+    at 64-B chunk offsets of a registered "in dcache", read there by the
+    device, parsed, verified, tagged and written back as out frags into a
+    registered "out dcache" -- nothing staged or expanded on the host, so
+    submit is validation + five launches.  One batch in flight, the
+    submitting thread pinned, the garbage collector off; the library is
+    called directly (no Python wrapper inside the timed region)."""
+    import gc
+    from firedancer_amd import _lib, tile, workload
+    L = _lib.lib()
+    n = min(len(txns), batch * views_n)
+    ps = workload.payloads(arena, txns[:n])
+    slots = [(len(p) + 63) // 64 * 64 for p in ps]
+    in_off = np.concatenate([[0], np.cumsum(slots)])
+    in_buf = tile._page_buf(int(in_off[-1]) + 4096)
+    for p, o in zip(ps, in_off[:-1].tolist()):
+        in_buf[o:o + len(p)] = np.frombuffer(p, dtype=np.uint8)
+    caps = np.array([L.fdgpu_frag_out_cap(len(p)) for p in ps], dtype=np.uint64)
+    views = []
+    out_max = 0
+    for b0 in range(0, n - batch + 1, batch):
+        fio = np.zeros(batch, dtype=tile.FRAG_IO_DTYPE)
+        fio["src"] = in_buf.ctypes.data + in_off[b0:b0 + batch]
+        fio["sz"] = [len(p) for p in ps[b0:b0 + batch]]
+        oo = np.concatenate([[0], np.cumsum((caps[b0:b0 + batch] + 63) // 64 * 64)])
+        fio["out_off"], fio["out_cap"] = oo[:-1], caps[b0:b0 + batch]
+        views.append((fio, int(oo[-1]), b0))
+        out_max = max(out_max, int(oo[-1]))
+    out_buf = tile._page_buf(out_max + 4096)
+    codes = np.zeros(batch, dtype=np.int8)
+    tags = np.zeros(batch, dtype=np.uint64)
+    osz = np.zeros(batch, dtype=np.uint16)
+    cp, tp, op, ob = codes.ctypes.data, tags.ctypes.data, osz.ctypes.data, out_buf.ctypes.data
+    eng.host_register(in_buf)
+    eng.host_register(out_buf)
+    keep = os.sched_getaffinity(0)
+    try:
+        def one(v):
+            fio, osz_b, _ = v
+            t0 = time.perf_counter()
+            tk = L.fdgpu_submit_frags_io(eng._h, fio.ctypes.data, batch, ob, osz_b, 0x5EED, None, 0)
+            t1 = time.perf_counter()
+            if tk < 0:
+                raise RuntimeError(f"fdgpu_submit_frags_io: {tk} ({_lib.last_error()})")
+            while True:
+                rc = L.fdgpu_poll_frags_io(eng._h, tk, cp, tp, op, 0)
+                if rc != 1:
+                    break
+            if rc:
+                raise RuntimeError(f"fdgpu_poll_frags_io: {rc}")
+            return (time.perf_counter() - t0) * 1e3, (t1 - t0) * 1e3
+        for i in range(50):                                # warm every slot (buffers sized on first use)
+            one(views[i % len(views)])
+        ok = True
+        for v in views:                                    # the codes, against the device-resident batch's
+            one(v)
+            ref = ref_codes[v[2]:v[2] + batch]
+            parsed = codes != tile.CODE_PARSE_FAIL
+            ok &= bool((codes[parsed] == ref[parsed]).all()) and int((~parsed).sum()) < batch // 100
+        if pin_cpu is not None:
+            os.sched_setaffinity(0, {pin_cpu})
+        gc.disable()
+        lat = np.array([one(views[i % len(views)]) for i in range(nbatches)])
+        gc.enable()
+    finally:
+        os.sched_setaffinity(0, keep)
+        eng.host_unregister(in_buf)
+        eng.host_unregister(out_buf)
+
+    def pct(x, q):
+        return round(float(np.percentile(x, q)), 3)
+    return {"p50_batch_latency_gathered_ms": pct(lat[:, 0], 50), "p99_batch_latency_gathered_ms": pct(lat[:, 0], 99),
+            "latency_split_gathered_ms": {"submit_p50_p99": [pct(lat[:, 1], 50), pct(lat[:, 1], 99)],
+                                          "rest_p50_p99": [pct(lat[:, 0] - lat[:, 1], 50),
+                                                           pct(lat[:, 0] - lat[:, 1], 99)]},
+            "gathered_codes_equal": ok}
+
+
 def sync_latency(arena, txns, calls=1000, threads=64):
     """The synchronous drop-in API (fd_ed25519_verify through the C ABI,
     fd_ed25519.h:96-101): p50/p99 of `calls` sequential calls on one thread
@@ -663,6 +743,8 @@ def main():
     if not args.no_extras:
         extras = latency_and_pcie(eng, arena, txns, args.latency_batch, args.latency_batches,
                                   pin_cpu=(cpus[1] if len(cpus) > 1 else cpus[0]) if cpus else None)
+        extras.update(latency_frag_io(eng, arena, txns, batch.codes(), args.latency_batch, args.latency_batches,
+                                      pin_cpu=(cpus[1] if len(cpus) > 1 else cpus[0]) if cpus else None))
         extras["latency_batch_txns"] = args.latency_batch
         if dist.rank == 0:
             extras.update(sync_latency(arena, txns))

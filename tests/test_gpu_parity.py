@@ -376,10 +376,11 @@ def _chunked(engine, arena, txns, chunk=1 << 17):
 
 
 def test_r_sign_and_equation_edges(engine, oracle):
-    """Edges of the R-avoiding compare (fdgpu_kernels.hip): R's
-    sign bit flipped on valid signatures (decoded R = -R': ERR_MSG), R
-    replaced by A or by B's encoding, S + L (out of range), and every lane of
-    a batch failing (the whole batch takes the slow path)."""
+    """Edges of the final equation check (chain == -[w]B, projective;
+    fdgpu_verify_hs_kernel): R's sign bit flipped on
+    valid signatures (decoded R = -R': ERR_MSG), R replaced by A or by B's
+    encoding, S + L (out of range), and every lane of a batch failing the
+    equation (settled in the one pass like every other lane)."""
     arena, txns, modes = workload.cfg1(2000, seed=0x5157)
     recs = []
     for t in txns[modes == 0][:600]:
@@ -464,8 +465,9 @@ def test_block_count_grouping_keeps_codes(engine, oracle):
 @pytest.mark.parametrize("mode", [workload.MODE_MSG, workload.MODE_R])
 def test_all_failing_batches(engine, oracle, mode):
     """test_ed25519.c:920-951 bad-msg / bad-sig modes at batch scale: every
-    signature of a 65,536-txn batch fails (all queued for the slow path's R
-    decode, spread over the whole grid); codes vs the oracle."""
+    signature of a 65,536-txn batch fails (the equation, or R's decode,
+    across the whole grid -- the half-size kernel settles both in its one
+    pass); codes vs the oracle."""
     arena, txns, modes = workload.make_txns(65536, 0xAD0 + mode, corrupt=1.0, corrupt_mode=mode)
     assert (modes == mode).all()
     got = engine.verify_txns(arena, txns)
