@@ -416,7 +416,7 @@ TILE_RUNS = (  # name, verify tiles, quic links (producers), offered txn/s (-1: 
 # default.toml:888-893: 16384, fd_frankendancer.c:59), with the stream published TILE_PACED_REPS times
 # over (>= 30 x the depth per link: the producers can lap the tiles); capacity runs prefill every frag
 # before the tiles start, so their links hold the whole stream
-TILE_DEPTH_LG_PACED, TILE_DEPTH_LG_PREFILL, TILE_PACED_REPS = 14, 21, 2
+TILE_DEPTH_LG_PACED, TILE_DEPTH_LG_PREFILL, TILE_PACED_REPS = 14, 21, 4
 TILE_BATCH, TILE_INFLIGHT = 16384, 8   # txns per GPU batch, batches in flight per tile
 TILE_RUNS_CFG3 = (  # the same tile over cfg3 frags (1-12 signatures, payloads up to the 1232-B MTU: SURVEY 8(d) cfg5)
     ("mux1_capacity_cfg3", 1, 1, -1.0),

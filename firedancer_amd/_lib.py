@@ -48,6 +48,8 @@ def lib():
     L.fd_ed25519_strerror.restype = c.c_char_p
     L.fdgpu_engine_open.argtypes = [c.c_int, c.POINTER(FdgpuCfg)]
     L.fdgpu_engine_open.restype = vp
+    L.fdgpu_engine_reserve.argtypes = [vp, c.c_uint64]
+    L.fdgpu_engine_reserve.restype = c.c_int
     L.fdgpu_engine_close.argtypes = [vp]
     L.fdgpu_engine_close.restype = None
     L.fdgpu_last_error.argtypes = []

@@ -243,6 +243,18 @@ bool slot_frag_bufs(Slot &s, const fdgpu_cfg_t &c, uint64_t tr) {
   return true;
 }
 
+/* The slot's gathered-batch buffers (fdgpu_submit_frags_io), on first use:
+   pinned [frag records][payload addresses][re-check pairs] the gather reads
+   in place, and the records' device copy. */
+bool slot_io_bufs(Slot &s, const fdgpu_cfg_t &c) {
+  if (s.h_io) return true;
+  const uint64_t m = c.max_txn + 1, bytes = m * (sizeof(fdgpu_frag_ex_t) + 3 * sizeof(uint64_t)) + 192;
+  HIPCHK(hipHostMalloc((void **)&s.h_io, bytes, hipHostMallocDefault), false);
+  HIPCHK(hipHostGetDevicePointer((void **)&s.d_ioh, s.h_io, 0), false);
+  HIPCHK(hipMalloc((void **)&s.d_fxio, m * sizeof(fdgpu_frag_ex_t)), false);
+  return true;
+}
+
 /* SHA-512 blocks of R || A || M (fdgpu_sha512.h sha512_hram_blocks) */
 inline uint32_t hram_blocks(uint32_t msg_sz) { return (64u + msg_sz + 16u) / 128u + 1u; }
 
@@ -457,6 +469,19 @@ void fdgpu_engine_close(fdgpu_engine_t *e) {
   if (e->d_scratch_codes) (void)hipFree(e->d_scratch_codes);
   if (e->compute) (void)hipStreamDestroy(e->compute);
   delete e;
+}
+
+int fdgpu_engine_reserve(fdgpu_engine_t *e, uint64_t n_sig) {
+  if (!e) return FDGPU_ERR_INVAL;
+  if (!n_sig) n_sig = e->cfg.max_sig;
+  if (n_sig > e->cfg.max_sig) { set_err("reserve beyond max_sig"); return FDGPU_ERR_INVAL; }
+  std::lock_guard<std::mutex> lk(e->ring_mu);
+  for (auto &s : e->slots) if (s.ticket >= 0 || s.staged) { set_err("a slot holds a batch"); return FDGPU_ERR_FULL; }
+  HIPCHK(hipSetDevice(e->device), FDGPU_ERR_DEVICE);
+  const uint64_t n = e->cfg.max_txn, res = ((n + 63) & ~63ull) + n * 10;    /* a gathered batch's results */
+  for (auto &s : e->slots)
+    if (!slot_ws(s, n_sig) || !slot_frag_bufs(s, e->cfg, res) || !slot_io_bufs(s, e->cfg)) return FDGPU_ERR_DEVICE;
+  return FDGPU_OK;
 }
 
 int fdgpu_engine_info(fdgpu_engine_t *e, uint32_t *grid_blocks, uint32_t *block_threads, uint64_t *ws_bytes) {
@@ -857,12 +882,7 @@ int64_t fdgpu_submit_frags_io(fdgpu_engine_t *e, fdgpu_frag_io_t const *fio, uin
      place */
   const uint64_t src_at = (n * sizeof(fdgpu_frag_ex_t) + 63) & ~63ull;
   const uint64_t chk_at = src_at + ((n * sizeof(uint64_t) + 63) & ~63ull);
-  if (!s->h_io) {
-    const uint64_t m = e->cfg.max_txn + 1, bytes = m * (sizeof(fdgpu_frag_ex_t) + 3 * sizeof(uint64_t)) + 192;
-    HIPCHK(hipHostMalloc((void **)&s->h_io, bytes, hipHostMallocDefault), FDGPU_ERR_DEVICE);
-    HIPCHK(hipHostGetDevicePointer((void **)&s->d_ioh, s->h_io, 0), FDGPU_ERR_DEVICE);
-    HIPCHK(hipMalloc((void **)&s->d_fxio, m * sizeof(fdgpu_frag_ex_t)), FDGPU_ERR_DEVICE);
-  }
+  if (!slot_io_bufs(*s, e->cfg)) return FDGPU_ERR_DEVICE;
   fdgpu_frag_ex_t *h_fx = (fdgpu_frag_ex_t *)s->h_io;
   uint64_t *h_src = (uint64_t *)(s->h_io + src_at);
   uint64_t *h_chk = (uint64_t *)(s->h_io + chk_at);

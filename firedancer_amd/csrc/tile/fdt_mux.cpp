@@ -162,7 +162,7 @@ int fdt_mux_run(const fdt_mux_cfg_t *cfg, const fdt_mux_callbacks_t *cb, void *c
 
 namespace {
 
-struct VItem {
+struct VItem {                       /* a frag of a batch (host / GPU parse; the gather mode keeps fio + tso) */
   uint64_t seq;
   uint64_t tag;         /* fd_hash(seed, signature 0, 64): the dedup tag, taken while the payload is hot */
   uint32_t chunk;       /* where [payload][pad][fd_txn_t][u16 sz] lies in the out dcache */
@@ -171,8 +171,6 @@ struct VItem {
   uint32_t tsorig;
   uint32_t tr_off;      /* gpu_parse: the parsed fd_txn_t's place in the batch's trailer buffer */
   uint32_t tr_cap;      /*            and its footprint (fdt_txn_peek); gather: the out bytes reserved */
-  uint32_t in_idx;      /* gather: the in link it came from */
-  uint32_t lost;        /* gather: the lap guard found it lapped when it copied it (dropped at resolution) */
 };
 
 struct VBatch {
@@ -181,14 +179,17 @@ struct VBatch {
   std::vector<fdgpu_txn_t> txns;
   std::vector<fdgpu_frag_ex_t> frags;  /* gpu_parse: the verifier's view of the items */
   std::vector<uint8_t> trailers;      /* gpu_parse: parsed fd_txn_t records, filled by poll_frags */
-  std::vector<fdgpu_frag_io_t> fio;   /* gather: the verifier's view of the items ... */
-  std::vector<uint64_t> tags;         /* ... and its results: dedup tags, */
-  std::vector<uint16_t> out_szs;      /*     out frag sizes */
+  std::vector<fdgpu_frag_io_t> fio;   /* gather: the frags themselves (seq, size, out room, in link) ... */
+  std::vector<uint32_t> tso;          /*   their tsorig, */
+  std::vector<uint32_t> lost;         /*   the ones the lap guard found lapped when it copied them, */
+  std::vector<uint64_t> tags;         /*   and the verifier's results: dedup tags, */
+  std::vector<uint16_t> out_szs;      /*   out frag sizes */
   uint64_t link_first[FDT_MUX_IN_MAX];   /* gather: the oldest seq taken from each in link, */
   uint32_t guard_cur[FDT_MUX_IN_MAX];    /*   the lap guard's cursor over the items of each, */
   uint32_t link_mask = 0;                /*   and which links the batch holds frags of */
   uint64_t tr_used = 0;
   std::vector<VItem> items;
+  size_t cnt = 0;                     /* frags in the batch (items, or fio in the gather mode) */
   std::vector<int8_t> codes;
   uint64_t sig_cnt = 0;               /* signatures sent (gpu_parse: the frags' upper bound) */
   int64_t ticket = -1;
@@ -199,7 +200,8 @@ struct VBatch {
 
   void reset() {
     first_chunk = end_off = sig_cnt = tr_used = 0;
-    txns.clear(); items.clear(); frags.clear(); fio.clear();
+    txns.clear(); items.clear(); frags.clear(); fio.clear(); tso.clear(); lost.clear();
+    cnt = 0;
     link_mask = 0;
     ticket = -1; closed = done = false; next = 0; t_first = 0;
   }
@@ -270,6 +272,10 @@ struct fdgpu_vmux {
   }
 
   uint8_t *out_laddr(uint64_t chunk) const { return cfg.out_base + (chunk << FDT_CHUNK_LG_SZ); }
+  /* the out chunk frag k of batch b lies at */
+  uint64_t chunk_of(const VBatch &b, size_t k) const {
+    return gather ? b.first_chunk + (b.fio[k].out_off >> FDT_CHUNK_LG_SZ) : b.items[k].chunk;
+  }
 
   /* chunk of the oldest frag that may still be read: published and possibly
      unconsumed (the mux's exposed count), else reserved by an unresolved
@@ -279,8 +285,8 @@ struct fdgpu_vmux {
     exposed = std::min(exposed, published_total);
     if (exposed) { tail = pub_chunk[(*mux->seq - exposed) & pub_mask]; return true; }
     for (const VBatch *b : inflight)
-      if (b->next < b->items.size()) { tail = b->items[b->next].chunk; return true; }
-    if (open && !open->items.empty()) { tail = open->items.front().chunk; return true; }
+      if (b->next < b->cnt) { tail = chunk_of(*b, b->next); return true; }
+    if (open && open->cnt) { tail = open->first_chunk; return true; }
     return false;
   }
 
@@ -313,76 +319,128 @@ struct fdgpu_vmux {
         st.batch_gpu_ns += now_ns() - b->t_submit;
         if (rc != FDGPU_OK) { error = rc; *poll_in = 0; return; }
         b->done = true;
+        for (uint32_t k : b->lost) b->codes[k] = (int8_t)FDGPU_CODE_LAPPED;
       }
       const uint64_t t_pub = now_ns();
       struct Acc { uint64_t &ns; uint64_t t0; ~Acc() { ns += now_ns() - t0; } } acc{st.publish_ns, t_pub};
       const uint32_t tspub = (uint32_t)t_pub;
-      const size_t n = b->items.size();
-      while (b->next < n) {
-        const size_t k = b->next;
-        if (gpu_parse && !gather && k + 8 < n) { /* the trailer store of a frag soon published: own the line */
-          const VItem &f = b->items[k + 8];
-          __builtin_prefetch(out_laddr(f.chunk) + align2(f.sz), 1);
-        }
-        const VItem &it = b->items[k];
-        const int code = b->codes[k];
-        if (gather && (code == FDGPU_CODE_LAPPED || it.lost)) {   /* the producer overwrote it before it was read */
-          st.overrun++;
-          st.lapped++;
-          log(it.seq, FDGPU_VTILE_LOG_LOST);
-          b->next++;
-          continue;
-        }
-        if (gpu_parse && (code == FDGPU_CODE_PARSE_FAIL || code == FDGPU_CODE_TRAILER_CAP)) {
-          /* not a transaction: filtered before the dedup check (fd_verify.c:
-             117-121); a footprint other than the one reserved: a peek / parse
-             disagreement, failed without a verdict */
-          if (code == FDGPU_CODE_PARSE_FAIL) { st.parse_fail++; log(it.seq, FDGPU_VTILE_LOG_PARSE_FAIL); }
-          else { st.verify_errors++; log(it.seq, FD_TXN_VERIFY_FAILED); }
-          b->next++;
-          continue;
-        }
-        uint8_t *frag = out_laddr(it.chunk);
-        const uint64_t tag = gather ? b->tags[k] : it.tag;
-        int outcome;
-        if (tc_query(tag)) outcome = FD_TXN_VERIFY_DEDUP;
-        else if (code != FD_ED25519_SUCCESS) outcome = FD_TXN_VERIFY_FAILED;
-        else outcome = FD_TXN_VERIFY_SUCCESS;
-        if (outcome == FD_TXN_VERIFY_SUCCESS) {
-          if (mux->cr_decrement_amount && !*mux->cr_avail) {
-            *poll_in = 0;                         /* out of credits: the mux refreshes them, then this item */
-            st.backpressure++;                    /* is resolved again from the top (nothing inserted yet) */
-            return;
-          }
-          tc_insert(tag);                          /* not present: the query above missed */
-          uint64_t sz = it.sz;
-          if (gather) {
-            sz = b->out_szs[k];                   /* the GPU wrote the out frag where it was reserved */
-          } else if (gpu_parse) {                 /* [payload][pad][fd_txn_t][u16 payload_sz] (fd_verify.c:93-136) */
-            const uint64_t toff = align2(it.sz);
-            if (toff != it.sz) frag[it.sz] = 0;
-            std::memcpy(frag + toff, b->trailers.data() + it.tr_off, it.tr_cap);
-            const uint16_t psz = (uint16_t)it.sz;
-            std::memcpy(frag + toff + it.tr_cap, &psz, 2);
-            sz = toff + it.tr_cap + 2;
-          }
-          pub_chunk[*mux->seq & pub_mask] = it.chunk;
-          fdt_mux_publish(mux, tag, it.chunk, sz, 0, it.tsorig, tspub);
-          published_total++;
-          st.published++;
-        } else if (outcome == FD_TXN_VERIFY_DEDUP) {
-          st.dedup++;
-        } else {
-          st.verify_failed++;
-        }
-        log(it.seq, outcome);
-        b->next++;
-      }
-      if (lat.size() < (1u << 22) && !b->items.empty()) lat.push_back(now_ns() - b->t_first);
+      if (!(gather ? resolve_gather(*b, mux, poll_in, tspub) : resolve_items(*b, mux, poll_in, tspub))) return;
+      if (lat.size() < (1u << 22) && b->cnt) lat.push_back(now_ns() - b->t_first);
       inflight.pop_front();
       b->reset();
       pool.push_back(b);
     }
+  }
+
+  /* host / GPU parse: resolve a polled batch item by item; false when
+     credits ran out mid-way (the mux refreshes them, then the rest is
+     resolved from b.next -- nothing of the stalled item was inserted yet) */
+  bool resolve_items(VBatch &b, fdt_mux_context_t *mux, int *poll_in, uint32_t tspub) {
+    const size_t n = b.items.size();
+    while (b.next < n) {
+      const size_t k = b.next;
+      if (gpu_parse && k + 8 < n) {              /* the trailer store of a frag soon published: own the line */
+        const VItem &f = b.items[k + 8];
+        __builtin_prefetch(out_laddr(f.chunk) + align2(f.sz), 1);
+      }
+      const VItem &it = b.items[k];
+      const int code = b.codes[k];
+      if (gpu_parse && (code == FDGPU_CODE_PARSE_FAIL || code == FDGPU_CODE_TRAILER_CAP)) {
+        /* not a transaction: filtered before the dedup check (fd_verify.c:
+           117-121); a footprint other than the one reserved: a peek / parse
+           disagreement, failed without a verdict */
+        if (code == FDGPU_CODE_PARSE_FAIL) { st.parse_fail++; log(it.seq, FDGPU_VTILE_LOG_PARSE_FAIL); }
+        else { st.verify_errors++; log(it.seq, FD_TXN_VERIFY_FAILED); }
+        b.next++;
+        continue;
+      }
+      uint8_t *frag = out_laddr(it.chunk);
+      const uint64_t tag = it.tag;
+      int outcome;
+      if (tc_query(tag)) outcome = FD_TXN_VERIFY_DEDUP;
+      else if (code != FD_ED25519_SUCCESS) outcome = FD_TXN_VERIFY_FAILED;
+      else outcome = FD_TXN_VERIFY_SUCCESS;
+      if (outcome == FD_TXN_VERIFY_SUCCESS) {
+        if (mux->cr_decrement_amount && !*mux->cr_avail) {
+          *poll_in = 0;
+          st.backpressure++;
+          return false;
+        }
+        tc_insert(tag);                          /* not present: the query above missed */
+        uint64_t sz = it.sz;
+        if (gpu_parse) {                         /* [payload][pad][fd_txn_t][u16 payload_sz] (fd_verify.c:93-136) */
+          const uint64_t toff = align2(it.sz);
+          if (toff != it.sz) frag[it.sz] = 0;
+          std::memcpy(frag + toff, b.trailers.data() + it.tr_off, it.tr_cap);
+          const uint16_t psz = (uint16_t)it.sz;
+          std::memcpy(frag + toff + it.tr_cap, &psz, 2);
+          sz = toff + it.tr_cap + 2;
+        }
+        pub_chunk[*mux->seq & pub_mask] = it.chunk;
+        fdt_mux_publish(mux, tag, it.chunk, sz, 0, it.tsorig, tspub);
+        published_total++;
+        st.published++;
+      } else if (outcome == FD_TXN_VERIFY_DEDUP) {
+        st.dedup++;
+      } else {
+        st.verify_failed++;
+      }
+      log(it.seq, outcome);
+      b.next++;
+    }
+    return true;
+  }
+
+  /* gather: resolve a polled batch from its frag records (the GPU's codes,
+     tags and out sizes); false when credits ran out mid-way (the mux
+     refreshes them, then the rest is resolved from b.next) */
+  bool resolve_gather(VBatch &b, fdt_mux_context_t *mux, int *poll_in, uint32_t tspub) {
+    const size_t n = b.cnt;
+    while (b.next < n) {
+      const size_t k = b.next;
+      const fdgpu_frag_io_t &f = b.fio[k];
+      const int code = b.codes[k];
+      if (code == FDGPU_CODE_LAPPED) {                  /* the producer overwrote it before it was read */
+        st.overrun++;
+        st.lapped++;
+        log(f.seq, FDGPU_VTILE_LOG_LOST);
+        b.next++;
+        continue;
+      }
+      if (code == FDGPU_CODE_PARSE_FAIL || code == FDGPU_CODE_TRAILER_CAP) {
+        /* not a transaction: filtered before the dedup check (fd_verify.c:117-121);
+           a parsed out frag larger than its reservation: failed without a verdict */
+        if (code == FDGPU_CODE_PARSE_FAIL) { st.parse_fail++; log(f.seq, FDGPU_VTILE_LOG_PARSE_FAIL); }
+        else { st.verify_errors++; log(f.seq, FD_TXN_VERIFY_FAILED); }
+        b.next++;
+        continue;
+      }
+      const uint64_t tag = b.tags[k];
+      int outcome;
+      if (tc_query(tag)) outcome = FD_TXN_VERIFY_DEDUP;
+      else if (code != FD_ED25519_SUCCESS) outcome = FD_TXN_VERIFY_FAILED;
+      else outcome = FD_TXN_VERIFY_SUCCESS;
+      if (outcome == FD_TXN_VERIFY_SUCCESS) {
+        if (mux->cr_decrement_amount && !*mux->cr_avail) {
+          *poll_in = 0;                                 /* out of credits: resolved again from here */
+          st.backpressure++;
+          return false;
+        }
+        tc_insert(tag);
+        const uint64_t chunk = b.first_chunk + (f.out_off >> FDT_CHUNK_LG_SZ);
+        pub_chunk[*mux->seq & pub_mask] = (uint32_t)chunk;
+        fdt_mux_publish(mux, tag, chunk, b.out_szs[k], 0, b.tso[k], tspub);   /* written there by the GPU */
+        published_total++;
+        st.published++;
+      } else if (outcome == FD_TXN_VERIFY_DEDUP) {
+        st.dedup++;
+      } else {
+        st.verify_failed++;
+      }
+      log(f.seq, outcome);
+      b.next++;
+    }
+    return true;
   }
 
   /* gather: has in link i's producer published seq s yet?  Its line holds
@@ -398,30 +456,31 @@ struct fdgpu_vmux {
      goes out -- and while it waits for a free slot -- every frag whose line
      the producer will reuse within lap_margin more publishes is copied here
      into its out frag's room, re-checked as the reference re-checks after
-     its copy (fd_mux.c:641-655), and handed to the device from there.  One
-     line read per link tells whether any frag of it is at risk (its oldest
-     frag is the first to be lapped); younger frags of a link are safer, so
-     each link's scan stops at its first frag not at risk. */
+     its copy (fd_mux.c:641-655), and handed to the device from there (link
+     0: no device re-check).  One line read per link tells whether any frag
+     of it is at risk (its oldest frag is the first to be lapped); younger
+     frags of a link are safer, so each link's scan stops at its first frag
+     not at risk. */
   void lap_guard(VBatch &b) {
     for (uint32_t i = 0; i < cfg.in_cnt; i++) {
       if (!(b.link_mask >> i & 1u)) continue;
       const uint64_t depth = cfg.in_depth[i], m = std::min(lap_margin, depth);
-      const size_t n = b.items.size();
+      const size_t n = b.cnt;
       size_t k = b.guard_cur[i];
-      while (k < n && b.items[k].in_idx != i) k++;
-      if (k == n || !published_by(i, b.items[k].seq + depth - m)) { b.guard_cur[i] = (uint32_t)k; continue; }
+      while (k < n && b.fio[k].link != i + 1u) k++;
+      if (k == n || !published_by(i, b.fio[k].seq + depth - m)) { b.guard_cur[i] = (uint32_t)k; continue; }
       for (; k < n; k++) {
-        VItem &it = b.items[k];
-        if (it.in_idx != i) continue;
-        if (!published_by(i, it.seq + depth - m)) break;
-        uint8_t *dst = out_laddr(it.chunk);
-        std::memcpy(dst, (const void *)(uintptr_t)b.fio[k].src, it.sz);
+        fdgpu_frag_io_t &f = b.fio[k];
+        if (f.link != i + 1u) continue;
+        if (!published_by(i, f.seq + depth - m)) break;
+        uint8_t *dst = out_laddr(b.first_chunk + (f.out_off >> FDT_CHUNK_LG_SZ));
+        std::memcpy(dst, (const void *)(uintptr_t)f.src, f.sz);
         std::atomic_thread_fence(std::memory_order_acquire);
-        const fdt_frag_meta_t *line = cfg.in_mcache[i] + (it.seq & (depth - 1));
-        if (ld_acq(&line->seq) != it.seq) it.lost = 1;      /* lapped already: the copy may be torn */
+        const fdt_frag_meta_t *line = cfg.in_mcache[i] + (f.seq & (depth - 1));
+        if (ld_acq(&line->seq) != f.seq) b.lost.push_back((uint32_t)k);   /* lapped already: may be torn */
         else st.rescued++;
-        b.fio[k].src = (uint64_t)(uintptr_t)dst;           /* the device reads this copy: no re-check */
-        b.fio[k].link = 0;
+        f.src = (uint64_t)(uintptr_t)dst;                 /* the device reads this copy */
+        f.link = 0;
       }
       b.guard_cur[i] = (uint32_t)k;
     }
@@ -430,14 +489,17 @@ struct fdgpu_vmux {
   /* the verifier refused the batch as malformed: its txns fail (logged),
      nothing is published, the tile goes on (device errors stay fatal) */
   void reject_open() {
-    for (const VItem &it : open->items) { st.verify_errors++; log(it.seq, FD_TXN_VERIFY_FAILED); }
+    for (size_t k = 0; k < open->cnt; k++) {
+      st.verify_errors++;
+      log(gather ? open->fio[k].seq : open->items[k].seq, FD_TXN_VERIFY_FAILED);
+    }
     open->reset();
     pool.push_back(open);
     open = nullptr;
   }
 
   void submit() {
-    if (!open || open->items.empty()) return;
+    if (!open || !open->cnt) return;
     const uint64_t s0 = now_ns();
     struct Acc { uint64_t &ns; uint64_t t0; ~Acc() { ns += now_ns() - t0; } } acc{st.submit_ns, s0};
     if (gather && lap_margin != ~0ull) lap_guard(*open);    /* also while the batch fills or waits for a slot */
@@ -537,25 +599,27 @@ void vm_after_frag(void *ctx, uint64_t in_idx, uint64_t seq, uint64_t *opt_sig, 
     /* reserve the out frag's room from the size alone (the tile never reads
        the payload); the GPU writes [payload][pad][fd_txn_t][u16] there */
     VBatch &b = *t->open;
-    if (b.items.empty()) { b.first_chunk = t->out_chunk; b.t_first = now_ns(); }
+    if (!b.cnt) { b.first_chunk = t->out_chunk; b.t_first = now_ns(); }
     const uint64_t off = (t->out_chunk - b.first_chunk) << FDT_CHUNK_LG_SZ;
     const uint32_t cap = t->cap_of[payload_sz];                  /* payload_sz <= FDT_TPU_MTU: during_frag */
     const uint32_t li = (uint32_t)t->cur_in;
     if (!(b.link_mask >> li & 1u)) {
       b.link_mask |= 1u << li;
       b.link_first[li] = seq;
-      b.guard_cur[li] = (uint32_t)b.items.size();
+      b.guard_cur[li] = (uint32_t)b.cnt;
     }
-    /* the device re-reads the frag's in-mcache line after the payload (link li + 1, seq) */
+    /* the frag's record is what the verifier reads: the device re-reads the
+       frag's in-mcache line after the payload (link li + 1, seq) */
     b.fio.push_back(fdgpu_frag_io_t{t->cur_src, (uint32_t)payload_sz, (uint32_t)off, cap, li + 1u, seq});
-    b.items.push_back(VItem{seq, 0, (uint32_t)t->out_chunk, (uint32_t)payload_sz, 0u, (uint32_t)*opt_tsorig, 0u, cap, li, 0u});
+    b.tso.push_back((uint32_t)*opt_tsorig);
+    b.cnt++;
     b.end_off = off + cap;
     b.sig_cnt += fdt_frag_sig_bound(payload_sz);       /* (stats.sigs stays 0: the tile never sees the count) */
     t->out_chunk = fdt_dcache_compact_next(t->out_chunk, cap, t->cfg.out_chunk0, t->cfg.out_wmark);
     t->room_ok = false;
     /* the lap guard's span: the batch holds at most lap_span_max seqs of a
        link (this tile's next frag of the link is round_robin_cnt seqs on) */
-    if (t->out_chunk <= b.first_chunk || b.items.size() >= t->cfg.batch_txn_max ||
+    if (t->out_chunk <= b.first_chunk || b.cnt >= t->cfg.batch_txn_max ||
         b.sig_cnt + 16 > t->cfg.batch_sig_max || b.end_off + FRAG_CHUNKS * FDT_CHUNK_SZ > t->cfg.batch_bytes_max ||
         seq - b.link_first[li] + t->cfg.round_robin_cnt >= t->lap_span_max)
       b.closed = true;
@@ -567,20 +631,21 @@ void vm_after_frag(void *ctx, uint64_t in_idx, uint64_t seq, uint64_t *opt_sig, 
     (void)txn;
     const uint64_t sc = t->cur_sc, fp = t->cur_fp;
     VBatch &b = *t->open;
-    if (b.items.empty()) { b.first_chunk = t->out_chunk; b.t_first = now_ns(); }
+    if (!b.cnt) { b.first_chunk = t->out_chunk; b.t_first = now_ns(); }
     const uint64_t off = (t->out_chunk - b.first_chunk) << FDT_CHUNK_LG_SZ;
     __builtin_prefetch(b.items.data() + b.items.size() + 6, 1);      /* reserved: stores a few frags ahead */
     __builtin_prefetch(b.frags.data() + b.frags.size() + 12, 1);
     b.frags.push_back(fdgpu_frag_ex_t{(uint32_t)off, (uint32_t)payload_sz, (uint32_t)b.tr_used, (uint32_t)fp});
     b.items.push_back(VItem{seq, t->cur_tag, (uint32_t)t->out_chunk, (uint32_t)payload_sz, 1u, (uint32_t)*opt_tsorig,
-                            (uint32_t)b.tr_used, (uint32_t)fp, 0u, 0u});
+                            (uint32_t)b.tr_used, (uint32_t)fp});
+    b.cnt++;
     b.tr_used += (fp + 3) & ~3ull;
     b.end_off = off + payload_sz;
     b.sig_cnt += fdt_frag_sig_bound(payload_sz);
     if (sc >= 1 && sc <= 16) t->st.sigs += sc;
     t->out_chunk = fdt_dcache_compact_next(t->out_chunk, toff + fp + 2, t->cfg.out_chunk0, t->cfg.out_wmark);
     t->room_ok = false;
-    if (t->out_chunk <= b.first_chunk || b.items.size() >= t->cfg.batch_txn_max ||
+    if (t->out_chunk <= b.first_chunk || b.cnt >= t->cfg.batch_txn_max ||
         b.sig_cnt + 16 > t->cfg.batch_sig_max || b.end_off + FRAG_CHUNKS * FDT_CHUNK_SZ > t->cfg.batch_bytes_max)
       b.closed = true;
     return;
@@ -599,7 +664,7 @@ void vm_after_frag(void *ctx, uint64_t in_idx, uint64_t seq, uint64_t *opt_sig, 
   const uint64_t new_sz = toff + tsz + 2;
   const fdt_txn_t *tt = (const fdt_txn_t *)txn_t;
   VBatch &b = *t->open;                                 /* after_credit made sure one is open */
-  if (b.items.empty()) { b.first_chunk = t->out_chunk; b.t_first = now_ns(); }
+  if (!b.cnt) { b.first_chunk = t->out_chunk; b.t_first = now_ns(); }
   const uint64_t off = (t->out_chunk - b.first_chunk) << FDT_CHUNK_LG_SZ;
   fdgpu_txn_t d;
   d.msg_off = (uint32_t)(off + tt->message_off);
@@ -609,13 +674,14 @@ void vm_after_frag(void *ctx, uint64_t in_idx, uint64_t seq, uint64_t *opt_sig, 
   d.sig_cnt = tt->signature_cnt;
   b.txns.push_back(d);
   b.items.push_back(VItem{seq, fdt_hash(t->cfg.hashmap_seed, txn + tt->signature_off, 64), (uint32_t)t->out_chunk,
-                          (uint32_t)new_sz, tt->signature_off, (uint32_t)*opt_tsorig, 0u, 0u, 0u, 0u});
+                          (uint32_t)new_sz, tt->signature_off, (uint32_t)*opt_tsorig, 0u, 0u});
+  b.cnt++;
   b.end_off = off + new_sz;
   if (tt->signature_cnt <= 16) { b.sig_cnt += tt->signature_cnt; t->st.sigs += tt->signature_cnt; }
   t->out_chunk = fdt_dcache_compact_next(t->out_chunk, new_sz, t->cfg.out_chunk0, t->cfg.out_wmark);
   t->room_ok = false;
   /* the arena must stay one contiguous run of chunks: a wrapped cursor closes it */
-  if (t->out_chunk <= b.first_chunk || b.items.size() >= t->cfg.batch_txn_max ||
+  if (t->out_chunk <= b.first_chunk || b.cnt >= t->cfg.batch_txn_max ||
       b.sig_cnt + 16 > t->cfg.batch_sig_max || b.end_off + FRAG_CHUNKS * FDT_CHUNK_SZ > t->cfg.batch_bytes_max)
     b.closed = true;
   /* accepted: published later, in order, by after_credit (MANUAL_PUBLISH) */
@@ -714,8 +780,12 @@ fdgpu_vmux_t *fdgpu_vmux_new(const fdgpu_vmux_cfg_t *cfg, fdgpu_verifier_t ver) 
     b.codes.resize(c.batch_txn_max);
     b.txns.reserve(c.batch_txn_max);
     if (t->gpu_parse && !t->gather) b.frags.reserve(c.batch_txn_max);
-    if (t->gather) { b.fio.reserve(c.batch_txn_max); b.tags.resize(c.batch_txn_max); b.out_szs.resize(c.batch_txn_max); }
-    b.items.reserve(c.batch_txn_max);
+    if (t->gather) {
+      b.fio.reserve(c.batch_txn_max); b.tso.reserve(c.batch_txn_max);
+      b.tags.resize(c.batch_txn_max); b.out_szs.resize(c.batch_txn_max);
+    } else {
+      b.items.reserve(c.batch_txn_max);
+    }
     t->pool.push_back(&b);
   }
   return t;
@@ -747,7 +817,7 @@ void fdgpu_vmux_stats(const fdgpu_vmux_t *t, fdgpu_vtile_stats_t *out) {
 }
 
 int fdgpu_vmux_idle(const fdgpu_vmux_t *t) {
-  return t->inflight.empty() && (!t->open || t->open->items.empty());
+  return t->inflight.empty() && (!t->open || !t->open->cnt);
 }
 
 int fdgpu_vmux_error(const fdgpu_vmux_t *t) { return t->error; }

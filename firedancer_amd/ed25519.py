@@ -114,6 +114,14 @@ class VerifyEngine:
         self.device = device
         self._pending = {}
 
+    def reserve(self, n_sig=0):
+        """fdgpu_engine_reserve: size every ring slot for batches of up to
+        n_sig signatures (0: max_sig) now, so no batch allocates inside the
+        pipeline (call with nothing in flight)."""
+        r = _lib.lib().fdgpu_engine_reserve(self._h, int(n_sig))
+        if r:
+            raise RuntimeError(f"fdgpu_engine_reserve failed: {r} ({_lib.last_error()})")
+
     def host_register(self, buf):
         """Registers a long-lived host buffer (numpy array) for direct DMA:
         batches whose arena lies inside it upload with no staging copy

@@ -137,6 +137,12 @@ typedef struct {
 /* Opens an engine on HIP device `device`.  Returns NULL on failure (no
    device, allocation failure); fdgpu_last_error() describes it. */
 fdgpu_engine_t * fdgpu_engine_open( int device, fdgpu_cfg_t const * cfg );
+/* Sizes every ring slot now for batches of up to n_sig signatures (0:
+   max_sig) -- the verify workspace (3.2 KB per signature), the frag-batch
+   and gathered-batch buffers -- instead of on the first batches that need
+   them, so no batch allocates device or pinned memory inside the pipeline.
+   Call with no batch in flight (FDGPU_ERR_FULL otherwise).  FDGPU_OK or < 0. */
+int              fdgpu_engine_reserve( fdgpu_engine_t * e, uint64_t n_sig );
 void             fdgpu_engine_close( fdgpu_engine_t * e );
 char const *     fdgpu_last_error( void );
 

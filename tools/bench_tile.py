@@ -269,6 +269,8 @@ def run_once_mux(args, ps, arena, offs, sizes, n_sig, modes, tiles_n, batch, inf
     frag_bytes = (tile.TPU_DCACHE_MTU + 63) // 64 * 64
     engines = [fa.VerifyEngine(device if device is not None else k % args.gpus, max_txn=batch, max_sig=batch * 12,
                                max_arena=batch * frag_bytes, ring_depth=inflight) for k in range(tiles_n)]
+    for e in engines:
+        e.reserve()          # every slot sized for the largest batch now, not inside the run (as a tile's init does)
     warm(engines, inflight, out_bytes=batch * frag_bytes if args.gpu_parse == 2 else 0, batch=batch)
     P = max(1, args.producers)
     inls = [tile.Link(1 << args.depth_lg, 1232) for _ in range(P)]

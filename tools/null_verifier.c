@@ -45,8 +45,8 @@ static int nv_poll_frags(void *ctx, int64_t ticket, int8_t *codes, uint8_t *trai
    size within its reservation; nothing is read or written */
 static uint64_t nv_tag = 1;
 static int64_t nv_submit_io(void *ctx, fdgpu_frag_io_t const *frags, uint64_t n, uint8_t *out, uint64_t out_sz,
-                            uint64_t seed) {
-  (void)out; (void)out_sz; (void)seed;
+                            uint64_t seed, fdgpu_link_t const *links, uint64_t link_cnt) {
+  (void)out; (void)out_sz; (void)seed; (void)links; (void)link_cnt;
   nv_t *v = (nv_t *)ctx;
   v->cnt[v->next % NV_RING] = n;
   v->sz[v->next % NV_RING] = frags;
