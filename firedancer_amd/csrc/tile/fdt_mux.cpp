@@ -3,6 +3,7 @@
    of fd_mux.c:387-699), and the batched GPU verify tile written as mux
    callbacks (fdgpu_vmux_*: fd_verify.c:36-148,232-246).  See
    include/fd_verify_tile.h for the contract. */
+#include <immintrin.h>
 #include <time.h>
 
 #include <algorithm>
@@ -179,7 +180,7 @@ struct VBatch {
   std::vector<fdgpu_txn_t> txns;
   std::vector<fdgpu_frag_ex_t> frags;  /* gpu_parse: the verifier's view of the items */
   std::vector<uint8_t> trailers;      /* gpu_parse: parsed fd_txn_t records, filled by poll_frags */
-  std::vector<fdgpu_frag_io_t> fio;   /* gather: the frags themselves (seq, size, out room, in link) ... */
+  std::vector<fdgpu_frag_io_t> fio;   /* gather: the frags themselves (seq, size, out room, in link), [0, cnt) ... */
   std::vector<uint32_t> tso;          /*   their tsorig, */
   std::vector<uint32_t> lost;         /*   the ones the lap guard found lapped when it copied them, */
   std::vector<uint64_t> tags;         /*   and the verifier's results: dedup tags, */
@@ -200,7 +201,7 @@ struct VBatch {
 
   void reset() {
     first_chunk = end_off = sig_cnt = tr_used = 0;
-    txns.clear(); items.clear(); frags.clear(); fio.clear(); tso.clear(); lost.clear();
+    txns.clear(); items.clear(); frags.clear(); lost.clear();     /* fio, tso: sized once, filled to cnt */
     cnt = 0;
     link_mask = 0;
     ticket = -1; closed = done = false; next = 0; t_first = 0;
@@ -219,11 +220,15 @@ struct fdgpu_vmux {
   fdt_tagring_t ring{};                   /* ... or the ring scan (the tile's 16-deep default) */
   bool use_ring = false;
   /* the ring scan inline, over a fixed 16 or 32 slots (the unused ones hold
-     the null tag, which no query reaches): one pass of vector compares */
+     the null tag, which no query reaches): AVX2 compares of four tags each,
+     OR-ed, one test (the scalar loop the compiler made of it was a serial
+     chain of 16 compare-or steps, a fifth of the tile's time) */
   template <int N> static bool ring_hit(const uint64_t *t, uint64_t tag) {
-    uint64_t h = 0;
-    for (int i = 0; i < N; i++) h |= (uint64_t)(t[i] == tag);
-    return h != 0;
+    const __m256i q = _mm256_set1_epi64x((long long)tag);
+    __m256i h = _mm256_cmpeq_epi64(_mm256_loadu_si256((const __m256i *)t), q);
+#pragma GCC unroll 8
+    for (int i = 4; i < N; i += 4) h = _mm256_or_si256(h, _mm256_cmpeq_epi64(_mm256_loadu_si256((const __m256i *)(t + i)), q));
+    return !_mm256_testz_si256(h, h);
   }
   bool tc_query(uint64_t tag) const {
     if (!use_ring) return fdt_tcache_query(tcache, tag);
@@ -507,7 +512,7 @@ struct fdgpu_vmux {
     if (inflight.size() >= cfg.inflight_max) return;
     int64_t t;
     if (gather) {
-      const size_t n = open->fio.size();
+      const size_t n = open->cnt;
       if (open->tags.size() < n) { open->tags.resize(cfg.batch_txn_max); open->out_szs.resize(cfg.batch_txn_max); }
       t = ver.submit_io(ver.ctx, open->fio.data(), n, out_laddr(open->first_chunk), open->end_off, cfg.hashmap_seed,
                         links, cfg.in_cnt);
@@ -610,8 +615,14 @@ void vm_after_frag(void *ctx, uint64_t in_idx, uint64_t seq, uint64_t *opt_sig, 
     }
     /* the frag's record is what the verifier reads: the device re-reads the
        frag's in-mcache line after the payload (link li + 1, seq) */
-    b.fio.push_back(fdgpu_frag_io_t{t->cur_src, (uint32_t)payload_sz, (uint32_t)off, cap, li + 1u, seq});
-    b.tso.push_back((uint32_t)*opt_tsorig);
+    fdgpu_frag_io_t &f = b.fio[b.cnt];          /* in place: no temporary (a wide reload of narrow stores stalls) */
+    f.src = t->cur_src;
+    f.sz = (uint32_t)payload_sz;
+    f.out_off = (uint32_t)off;
+    f.out_cap = cap;
+    f.link = li + 1u;
+    f.seq = seq;
+    b.tso[b.cnt] = (uint32_t)*opt_tsorig;
     b.cnt++;
     b.end_off = off + cap;
     b.sig_cnt += fdt_frag_sig_bound(payload_sz);       /* (stats.sigs stays 0: the tile never sees the count) */
@@ -781,7 +792,7 @@ fdgpu_vmux_t *fdgpu_vmux_new(const fdgpu_vmux_cfg_t *cfg, fdgpu_verifier_t ver) 
     b.txns.reserve(c.batch_txn_max);
     if (t->gpu_parse && !t->gather) b.frags.reserve(c.batch_txn_max);
     if (t->gather) {
-      b.fio.reserve(c.batch_txn_max); b.tso.reserve(c.batch_txn_max);
+      b.fio.resize(c.batch_txn_max); b.tso.resize(c.batch_txn_max);
       b.tags.resize(c.batch_txn_max); b.out_szs.resize(c.batch_txn_max);
     } else {
       b.items.reserve(c.batch_txn_max);

@@ -1,7 +1,8 @@
-"""Engine services on the GPU: the synchronous API's call coalescing and
-fail-closed contract, the completion-word poll's fallback to the runtime
-event, reference-counted host registration, and slot workspaces that grow
-with the batches.  Codes are checked against the golden vectors / the
+"""Engine services on the GPU: the synchronous API's call coalescing, the
+completion-word poll's fallback to the runtime event, reference-counted host
+registration, slot workspaces that grow with the batches or are reserved up
+front.  (The synchronous API's failure policy is tests/test_abi.py's: it
+needs no GPU.)  Codes are checked against the golden vectors / the
 workload's own labels (bit-exact; no tolerance applies)."""
 import ctypes
 import os
@@ -125,6 +126,28 @@ def test_default_engine_grows_slot_workspace():
         got3 = eng.verify_txns(a3, t3)
         assert ((got3 == 0) == (m3 == 0)).all()
         assert int(t3["sig_cnt"].sum()) > 3 * 3000
+    finally:
+        eng.close()
+
+
+def test_reserve_sizes_every_slot_before_batches():
+    """fdgpu_engine_reserve: every ring slot sized for max_sig up front (the
+    frag-batch buffers too), refused while a batch is in flight; batches of
+    every shape afterwards verify with the workload's labels."""
+    eng = fa.VerifyEngine(0, max_txn=2048, ring_depth=3)
+    try:
+        eng.reserve()
+        a, t, modes = workload.cfg3(2000, seed=0x7E5)
+        tk = eng.submit(a, t)
+        with pytest.raises(RuntimeError):
+            eng.reserve()                                  # a slot holds a batch
+        codes = eng.poll(tk, blocking=True)
+        assert ((codes == 0) == (modes == 0)).all()
+        eng.reserve(1000)                                  # smaller than what is there: no change
+        a1, t1, m1 = workload.cfg1(2048, seed=0x7E6)
+        assert ((eng.verify_txns(a1, t1) == 0) == (m1 == 0)).all()
+        with pytest.raises(RuntimeError):
+            eng.reserve(2048 * 12 + 1)                     # beyond max_sig
     finally:
         eng.close()
 

@@ -76,6 +76,11 @@ def make_parser():
                     help="paced runs publish the frag stream this many times over (a long stream on a shallow "
                          "link: the producers can lap the tiles)")
     ap.add_argument("--lap-guard", type=int, default=1, help="gather tile: 1 the lap guard on (default), 0 off")
+    ap.add_argument("--tiles-per-engine", type=int, default=1,
+                    help="verify tiles sharing one engine (its ring slots): a process's HIP streams are hardware "
+                         "queues, and past ~20 of them the GPU's scheduler time-slices the queues")
+    ap.add_argument("--reserve", type=int, default=1,
+                    help="1: size every engine slot for max_sig before timing (fdgpu_engine_reserve)")
     ap.add_argument("--cpu-list", default="", help="','-separated CPUs to pin producers and tiles to, in order")
     ap.add_argument("--device", type=int, default=-1, help="the GPU every tile's engine uses (-1: tile k on k %% gpus)")
     return ap
@@ -122,6 +127,9 @@ def main():
     if args.out:
         with open(args.out, "w") as f:
             f.write("\n".join(lines) + "\n")
+    for pool in _POOL.values():
+        for e in pool:
+            e.close()
     return 0 if ok else 1
 
 
@@ -266,17 +274,14 @@ def run_once_mux(args, ps, arena, offs, sizes, n_sig, modes, tiles_n, batch, inf
     robin over the links, each paced at rate / P); the out links have no
     reliable consumer here (published frags count as consumed), so this
     measures ingest + verify + publish."""
-    frag_bytes = (tile.TPU_DCACHE_MTU + 63) // 64 * 64
-    engines = [fa.VerifyEngine(device if device is not None else k % args.gpus, max_txn=batch, max_sig=batch * 12,
-                               max_arena=batch * frag_bytes, ring_depth=inflight) for k in range(tiles_n)]
-    for e in engines:
-        e.reserve()          # every slot sized for the largest batch now, not inside the run (as a tile's init does)
-    warm(engines, inflight, out_bytes=batch * frag_bytes if args.gpu_parse == 2 else 0, batch=batch)
+    tpe = max(1, getattr(args, "tiles_per_engine", 1))
+    # tiles sharing an engine share its `inflight` ring slots (each tile may hold up to all of them)
+    engines = engine_pool(args, (tiles_n + tpe - 1) // tpe, batch, inflight, device)
     P = max(1, args.producers)
     inls = [tile.Link(1 << args.depth_lg, 1232) for _ in range(P)]
     vms, vers = [], []
     for k in range(tiles_n):
-        ver = tile.EngineVerifier([engines[k]])
+        ver = tile.EngineVerifier([engines[k // tpe]])
         outl = tile.Link(1 << 14, tile.TPU_DCACHE_MTU, data_sz=tile.vmux_dcache_data_sz(1 << 14, batch, inflight))
         guard = {} if getattr(args, "lap_guard", 1) else dict(lap_span_max=tile.LAP_OFF, lap_margin=tile.LAP_OFF)
         vms.append(tile.VerifyMuxTile(inls, outl, ver, batch_txn_max=batch, inflight_max=inflight,
@@ -357,6 +362,7 @@ def run_once_mux(args, ps, arena, offs, sizes, n_sig, modes, tiles_n, batch, inf
         "sigs_per_s": round(n_sig * n_total / len(ps) / wall, 1),
         "wall_s": round(wall, 4), "producer_s": round(prod_s, 4), "producer_published": int(n_pub),
         "gpus": args.gpus, "tiles": tiles_n, "batch_txn_max": batch, "inflight": inflight,
+        "engines": len(engines), "engine_slots": inflight,
         "rate_target": rate, "prefill": prefill, "link_depth": 1 << args.depth_lg,
         # what the producers actually offered: frags published / their publishing time
         "offered_txns_per_s": round(n_pub / prod_s, 1) if prod_s > 0 and not prefill else None,
@@ -374,9 +380,34 @@ def run_once_mux(args, ps, arena, offs, sizes, n_sig, modes, tiles_n, batch, inf
         vm.close()
     for ver, _ in vers:
         ver.close()
-    for e in engines:
-        e.close()
     return res
+
+
+_POOL = {}
+
+
+def engine_pool(args, n, batch, inflight, device):
+    """n engines (one per tile) for a run, kept across the runs of a sweep:
+    a deployment opens its tiles' engines once, and a process that keeps
+    opening and closing engines keeps creating HIP streams -- after a few
+    dozen, new streams share hardware queues and batches of one tile
+    serialise behind another's (a run after a 3-tile run took 2.5x as long
+    per batch with the same kernel durations, profiles/r04/tile_stream_reuse.md)."""
+    key = (batch, inflight, device)
+    pool = _POOL.setdefault(key, [])
+    frag_bytes = (tile.TPU_DCACHE_MTU + 63) // 64 * 64
+    new = []
+    while len(pool) < n:
+        k = len(pool)
+        e = fa.VerifyEngine(device if device is not None else k % args.gpus, max_txn=batch, max_sig=batch * 12,
+                            max_arena=batch * frag_bytes, ring_depth=inflight)
+        if getattr(args, "reserve", 1):
+            e.reserve()      # every slot sized for the largest batch now, not inside the run (as a tile's init does)
+        pool.append(e)
+        new.append(e)
+    if new:
+        warm(new, inflight, out_bytes=batch * frag_bytes if args.gpu_parse == 2 else 0, batch=batch)
+    return pool[:n]
 
 
 if __name__ == "__main__":
