@@ -76,6 +76,9 @@ def make_parser():
                     help="paced runs publish the frag stream this many times over (a long stream on a shallow "
                          "link: the producers can lap the tiles)")
     ap.add_argument("--lap-guard", type=int, default=1, help="gather tile: 1 the lap guard on (default), 0 off")
+    ap.add_argument("--batch-sig-max", type=int, default=0,
+                    help="(mux tile) signatures per batch, counted by the frag-size bound the tile sees "
+                         "(0: 12 x batch): bounds the GPU work, and the latency, of multi-signature batches")
     ap.add_argument("--tiles-per-engine", type=int, default=1,
                     help="verify tiles sharing one engine (its ring slots): a process's HIP streams are hardware "
                          "queues, and past ~20 of them the GPU's scheduler time-slices the queues")
@@ -286,7 +289,8 @@ def run_once_mux(args, ps, arena, offs, sizes, n_sig, modes, tiles_n, batch, inf
         guard = {} if getattr(args, "lap_guard", 1) else dict(lap_span_max=tile.LAP_OFF, lap_margin=tile.LAP_OFF)
         vms.append(tile.VerifyMuxTile(inls, outl, ver, batch_txn_max=batch, inflight_max=inflight,
                                       batch_wait_us=args.wait_us, round_robin_idx=k, round_robin_cnt=tiles_n,
-                                      gpu_parse=int(args.gpu_parse), **guard))
+                                      gpu_parse=int(args.gpu_parse), batch_sig_max=getattr(args, "batch_sig_max", 0),
+                                      **guard))
         vers.append((ver, outl))
     cpus = cpus or workload.physical_cpus()[getattr(args, "cpu_offset", 0):] or workload.physical_cpus()
     # tile k's thread is pinned to cpus[P + k] (VerifyMuxTile.start inherits the caller's mask)
@@ -363,6 +367,7 @@ def run_once_mux(args, ps, arena, offs, sizes, n_sig, modes, tiles_n, batch, inf
         "wall_s": round(wall, 4), "producer_s": round(prod_s, 4), "producer_published": int(n_pub),
         "gpus": args.gpus, "tiles": tiles_n, "batch_txn_max": batch, "inflight": inflight,
         "engines": len(engines), "engine_slots": inflight,
+        "batch_sig_max": getattr(args, "batch_sig_max", 0) or batch * 12,
         "rate_target": rate, "prefill": prefill, "link_depth": 1 << args.depth_lg,
         # what the producers actually offered: frags published / their publishing time
         "offered_txns_per_s": round(n_pub / prod_s, 1) if prod_s > 0 and not prefill else None,
