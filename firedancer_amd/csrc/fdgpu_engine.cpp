@@ -396,7 +396,8 @@ static bool bucket(const fdgpu_engine_t *e) { return !(e->cfg.flags & FDGPU_FLAG
 static uint32_t kflags(const fdgpu_engine_t *e) {
   return ((e->cfg.flags & FDGPU_FLAG_REF_MAPPING) ? FDGPU_FLAG_REF_MAP : 0u) |
          ((e->cfg.flags & FDGPU_FLAG_FULL_PATH) ? FDGPU_FLAG_KFULL : 0u) |
-         ((e->cfg.flags & FDGPU_FLAG_KEY_CACHE) ? FDGPU_FLAG_KCACHE : 0u);
+         ((e->cfg.flags & FDGPU_FLAG_KEY_CACHE) ? FDGPU_FLAG_KCACHE : 0u) |
+         ((e->cfg.flags & FDGPU_FLAG_PAIR) && !(e->cfg.flags & FDGPU_FLAG_KEY_CACHE) ? FDGPU_FLAG_KPAIR : 0u);
 }
 
 extern "C" {

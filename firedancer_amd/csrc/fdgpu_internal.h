@@ -53,6 +53,7 @@ typedef struct {
 #define FDGPU_FLAG_REF_MAP  1u            /* portable-backend error mapping */
 #define FDGPU_FLAG_KFULL    2u            /* half-size path: every lane takes the full-length fallback */
 #define FDGPU_FLAG_KCACHE   4u            /* half-size path: one -A decode + table per distinct key */
+#define FDGPU_FLAG_KPAIR    8u            /* half-size path, two lanes per signature (fdgpu_verify_pair_kernel) */
 /* SHA-512 block-count groups of the host-side bucketing (expand): messages of
    more blocks than this share the last group */
 #define FDGPU_NBLK_GROUPS   32u

@@ -125,6 +125,11 @@ typedef struct {
                                       vote traffic): a hash dedup + one -A table per key, copied by the
                                       other signatures of that key; same codes, faster when keys repeat,
                                       ~1% slower on 1M-signature batches of distinct keys */
+#define FDGPU_FLAG_PAIR      16u  /* two GPU lanes per signature (A's and R's decode and half-size chain in
+                                      adjacent lanes, the sums exchanged): ~30% shorter verify for batches
+                                      that leave the GPU's wave slots idle (small / latency-bound batches),
+                                      ~1.4x the work per signature, so slower on batches that fill the GPU;
+                                      same codes.  Ignored with FDGPU_FLAG_KEY_CACHE */
 
 /* Status codes of the engine API (distinct from verify codes). */
 #define FDGPU_OK            ( 0)

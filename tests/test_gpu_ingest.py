@@ -384,3 +384,43 @@ def test_frag_io_device_lap_recheck(engine, oracle):
     finally:
         for b in (mc, in_buf, out_buf):
             engine.host_unregister(b)
+
+
+def test_frag_io_pair_kernel(oracle):
+    """Gathered frag batches through an engine with FDGPU_FLAG_PAIR: the
+    signature count comes from the device (parse + expand), the pair kernel
+    sizes its grid from the bound -- codes equal the oracle's on cfg1 and
+    cfg3 payloads."""
+    import firedancer_amd as fa
+    from firedancer_amd import _lib
+    L = _lib.lib()
+    eng = fa.VerifyEngine(0, max_txn=4096, pair=True)
+    try:
+        for gen, seed in ((workload.cfg1, 0xB1), (workload.cfg3, 0xB2)):
+            a, t, _ = gen(1500, seed=seed)
+            ps = [p for p in workload.payloads(a, t) if tile.txn_parse(p)[0]]
+            in_buf, out_buf = _pages(len(ps) * 1280), _pages(len(ps) * 2176)
+            eng.host_register(in_buf)
+            eng.host_register(out_buf)
+            try:
+                fio = np.zeros(len(ps), dtype=tile.FRAG_IO_DTYPE)
+                o = 0
+                for k, p in enumerate(ps):
+                    in_buf[k * 1280:k * 1280 + len(p)] = np.frombuffer(p, dtype=np.uint8)
+                    cap = L.fdgpu_frag_out_cap(len(p))
+                    fio[k] = (in_buf.ctypes.data + k * 1280, len(p), o, cap, 0, 0)
+                    o += (cap + 63) // 64 * 64
+                codes, _, _ = eng.poll_frags_io(eng.submit_frags_io(fio, out_buf, o, 0x33))
+                arena = np.frombuffer(b"".join(ps) + b"\0" * 16, dtype=np.uint8)
+                offs = np.cumsum([0] + [len(p) for p in ps])
+                td = np.zeros(len(ps), dtype=workload.TXN_DTYPE)
+                for k, p in enumerate(ps):
+                    d = tile.txn_decode(tile.txn_parse(p)[1])
+                    td[k] = (int(offs[k]) + d["message_off"], len(p) - d["message_off"],
+                             int(offs[k]) + d["signature_off"], int(offs[k]) + d["acct_addr_off"], d["signature_cnt"])
+                assert (codes == oracle.verify_txns(arena, td, nthreads=8)).all()
+            finally:
+                eng.host_unregister(in_buf)
+                eng.host_unregister(out_buf)
+    finally:
+        eng.close()

@@ -540,3 +540,37 @@ def test_nonblocking_poll_sees_completion(engine, oracle):
             if got is not None:
                 break
         assert got is not None and (got == exp).all()
+
+
+@pytest.mark.parametrize("ref_mapping", [False, True])
+def test_pair_kernel_path(vectors, oracle, ref_mapping):
+    """FDGPU_FLAG_PAIR: two lanes per signature (fdgpu_verify_pair_kernel --
+    A's and R's decode and half-size chain in adjacent lanes, the sums
+    exchanged across the pair).  Held to the same bar as the one-lane
+    kernel: the golden vectors under both error mappings (reference codes),
+    cfg1 / cfg3 sets, the small-order x S-edge cross product, an odd batch
+    (a last pair with no signature) and all-failing batches against the
+    oracle; with FDGPU_FLAG_FULL_PATH as well, every lane queued by its A
+    lane for the full-length kernel."""
+    import firedancer_amd as fa
+    key = "code_refmap" if ref_mapping else "code"
+    for full in (False, True):
+        eng = fa.VerifyEngine(0, max_txn=8192, ref_mapping=ref_mapping, pair=True, full_path=full)
+        try:
+            vs, arena, txns = _vector_batch(vectors)
+            codes = eng.verify_txns(arena, txns)
+            bad = [(v["src"], v["tc_id"], v[key], int(c)) for v, c in zip(vs, codes) if c != v[key]]
+            assert not bad, bad[:20]
+            if ref_mapping:
+                continue
+            sets = [workload.cfg1(2001, seed=0xA1A), workload.cfg3(600, seed=0xA1B),
+                    workload.make_txns(3000, 0xA1C, corrupt=1.0, corrupt_mode=workload.MODE_R)]
+            for arena, txns, _ in sets:
+                got = eng.verify_txns(arena, txns)
+                exp = oracle.verify_txns(arena, txns, nthreads=8)
+                assert (got == exp).all(), np.nonzero(got != exp)[0][:10]
+            arena, txns = workload.pack_single(workload.small_order_cross_product())
+            got = eng.verify_txns(arena, txns)
+            assert (got == oracle.verify_txns(arena, txns, nthreads=8)).all()
+        finally:
+            eng.close()
