@@ -6,8 +6,13 @@
 #include <immintrin.h>
 #include <time.h>
 
+#include <sys/syscall.h>
+#include <unistd.h>
+#include <x86intrin.h>
+
 #include <algorithm>
 #include <atomic>
+#include <cmath>
 #include <cstring>
 #include <deque>
 #include <new>
@@ -28,11 +33,88 @@ inline void st_rel(uint64_t *p, uint64_t v) { __atomic_store_n(p, v, __ATOMIC_RE
 inline bool pow2(uint64_t x) { return x && !(x & (x - 1)); }
 inline uint64_t align2(uint64_t x) { return (x + 1) & ~1ull; }
 
+/* the time stamp counter's rate, measured once per process (the reference's
+   fd_tempo_tick_per_ns) */
+double tick_per_ns() {
+  static double r = [] {
+    const uint64_t c0 = __rdtsc(), t0 = now_ns();
+    while (now_ns() - t0 < 2000000) {}
+    return (double)(__rdtsc() - c0) / (double)(now_ns() - t0);
+  }();
+  return r;
+}
+
+/* the loop's metrics as fd_mux.c keeps them: histograms sampled every
+   iteration, link counters accumulated locally and drained at housekeeping */
+struct MuxMetrics {
+  fdt_mux_metrics_t *out;
+  fdt_mux_metrics_t m;
+  uint64_t now;
+  bool in_backp = false;
+  explicit MuxMetrics(fdt_mux_metrics_t *o) : out(o) {
+    std::memset(&m, 0, sizeof m);
+    if (!out) return;
+    const double tpn = tick_per_ns();
+    const uint64_t t50ns = (uint64_t)(50.0 * tpn), t50us = (uint64_t)(50000.0 * tpn);
+    for (fdt_histf_t *h : {&m.loop_housekeeping_duration_ticks, &m.loop_backpressure_duration_ticks,
+                           &m.loop_caught_up_duration_ticks, &m.loop_overrun_polling_duration_ticks,
+                           &m.loop_overrun_reading_duration_ticks, &m.loop_filter_before_fragment_duration_ticks,
+                           &m.loop_filter_after_fragment_duration_ticks, &m.loop_finish_duration_ticks})
+      fdt_histf_init(h, t50ns, t50us);
+    fdt_histf_init(&m.fragment_filtered_size_bytes, 0, 2094);     /* metrics.xml: min 0, max 2094 */
+    fdt_histf_init(&m.fragment_handled_size_bytes, 0, 2094);
+    m.tick_per_ns = tpn;
+    m.tile_pid = (uint64_t)getpid();
+    m.tile_tid = (uint64_t)syscall(SYS_gettid);
+    now = __rdtsc();
+  }
+  /* one loop iteration ended: its duration into h */
+  void lap(fdt_histf_t &h) {
+    if (!out) return;
+    const uint64_t next = __rdtsc();
+    fdt_histf_sample(&h, next - now);
+    now = next;
+  }
+  void write() {
+    if (!out) return;
+    m.housekeeping_cnt++;
+    std::atomic_thread_fence(std::memory_order_release);
+    std::memcpy((void *)out, &m, sizeof m);
+  }
+};
+
 }  // namespace
 
 /* ------------------------------------------------------------------ mux */
 
 extern "C" {
+
+void fdt_histf_init(fdt_histf_t *h, uint64_t min, uint64_t max) {
+  /* fd_histf_new (fd_histf.h:77-117): min >= 1, at least one value per
+     bucket, edges ~ min * z^i with max ~ min * z^14 */
+  std::memset(h, 0, sizeof *h);
+  min = std::max<uint64_t>(min, 1);
+  max = std::max<uint64_t>(max, min + FDT_HISTF_BUCKET_CNT - 2);
+  h->left_edge[0] = 0;
+  h->left_edge[1] = min;
+  for (uint64_t i = 2; i < FDT_HISTF_BUCKET_CNT - 1; i++) {
+    uint64_t le = (uint64_t)(0.5 + (double)h->left_edge[i - 1] *
+                                       std::pow((double)max / (double)h->left_edge[i - 1],
+                                                1.0 / (double)(FDT_HISTF_BUCKET_CNT - i)));
+    le = std::max(le, h->left_edge[i - 1] + 1);
+    h->left_edge[i] = le;
+  }
+  h->left_edge[FDT_HISTF_BUCKET_CNT - 1] = max;
+  h->left_edge[FDT_HISTF_BUCKET_CNT] = UINT64_MAX;
+}
+
+void fdt_histf_sample(fdt_histf_t *h, uint64_t v) {
+  h->sum += v;
+  uint64_t b = FDT_HISTF_BUCKET_CNT - 1;         /* [max, inf) */
+  for (uint64_t i = 0; i + 1 < FDT_HISTF_BUCKET_CNT; i++)
+    if (v < h->left_edge[i + 1]) { b = i; break; }
+  h->counts[b]++;
+}
 
 void fdt_mux_publish(fdt_mux_context_t *ctx, uint64_t sig, uint64_t chunk, uint64_t sz, uint64_t ctl,
                      uint64_t tsorig, uint64_t tspub) {
@@ -70,15 +152,19 @@ int fdt_mux_run(const fdt_mux_cfg_t *cfg, const fdt_mux_callbacks_t *cb, void *c
   for (uint64_t j = 0; j < out_cnt; j++) out_seq[j] = ld_acq(cfg->out_fseq[j]);
   uint64_t seq = cfg->out_seq0, cr_avail = 0, cr_filt = 0, in_rr = 0;
   fdt_mux_stats_t st{};
+  MuxMetrics mx(cfg->metrics);
+  fdt_mux_metrics_t &M = mx.m;
   for (uint64_t hk = 0;; hk--) {
     st.loops++;
     if (!hk) {
       hk = lazy;
       /* housekeeping (fd_mux.c:391-491): receive credits from the outs, send
-         our position to the ins, user callbacks, halt (the cnc signal) */
+         our position to the ins, metrics, user callbacks, halt (the cnc signal) */
       for (uint64_t j = 0; j < out_cnt; j++) out_seq[j] = ld_acq(cfg->out_fseq[j]);
       const uint64_t exposed = copy ? 0 : cr_max - cr_avail + cr_filt;
       for (uint64_t i = 0; i < in_cnt; i++) if (cfg->in_fseq[i]) st_rel(cfg->in_fseq[i], in_seq[i] - exposed);
+      M.stem_in_backpressure = mx.in_backp;
+      mx.write();
       if (cb->metrics_write) cb->metrics_write(ctx);
       if (halt && *halt) break;
       if (cr_avail < cr_max) {
@@ -91,14 +177,22 @@ int fdt_mux_run(const fdt_mux_cfg_t *cfg, const fdt_mux_callbacks_t *cb, void *c
         if (cr_avail == cr_max) cr_filt = 0;
       }
       if (cb->during_housekeeping) cb->during_housekeeping(ctx);
+      mx.lap(M.loop_housekeeping_duration_ticks);
     }
 
     fdt_mux_context_t mux = {mcache, depth, &cr_avail, &seq, out_cnt ? 1ull : 0ull};
     if (cb->before_credit) cb->before_credit(ctx, &mux);
-    if (cr_avail < cr_filt + burst) { st.backpressure++; continue; }   /* fd_mux.c:548-556 */
+    if (cr_avail < cr_filt + burst) {                                   /* fd_mux.c:548-556 */
+      st.backpressure++;
+      M.stem_backpressure_count += (uint64_t)!mx.in_backp;              /* transitions into backpressure */
+      mx.in_backp = true;
+      mx.lap(M.loop_backpressure_duration_ticks);
+      continue;
+    }
+    mx.in_backp = false;
     int poll_in = 1;
     if (cb->after_credit) cb->after_credit(ctx, &mux, &poll_in);
-    if (!poll_in || !in_cnt) continue;
+    if (!poll_in || !in_cnt) { mx.lap(M.loop_finish_duration_ticks); continue; }
 
     const uint64_t i = in_rr;
     in_rr = in_rr + 1 == in_cnt ? 0 : in_rr + 1;
@@ -109,7 +203,15 @@ int fdt_mux_run(const fdt_mux_cfg_t *cfg, const fdt_mux_callbacks_t *cb, void *c
     const uint64_t seq_found = ld_acq(&line->seq);
     const int64_t diff = (int64_t)(in_seq[i] - seq_found);
     if (diff) {                                     /* caught up, or overrun (fd_mux.c:595-609) */
-      if (diff < 0) { st.overrun_polling += (uint64_t)(-diff); in_seq[i] = seq_found; }
+      if (diff < 0) {
+        st.overrun_polling += (uint64_t)(-diff);
+        M.link_in[i].overrun_polling_count++;
+        M.link_in[i].overrun_polling_frag_count += (uint64_t)(-diff);
+        in_seq[i] = seq_found;
+        mx.lap(M.loop_overrun_polling_duration_ticks);
+      } else {
+        mx.lap(M.loop_caught_up_duration_ticks);
+      }
       continue;
     }
     uint64_t sig = line->sig;
@@ -121,6 +223,7 @@ int fdt_mux_run(const fdt_mux_cfg_t *cfg, const fdt_mux_callbacks_t *cb, void *c
         if (!copy) cr_filt += (uint64_t)(cr_avail < cr_max);
         in_seq[i]++;
         st.filtered_before++;
+        mx.lap(M.loop_filter_before_fragment_duration_ticks);
         continue;
       }
     }
@@ -137,7 +240,9 @@ int fdt_mux_run(const fdt_mux_cfg_t *cfg, const fdt_mux_callbacks_t *cb, void *c
     const uint64_t seq_test2 = ld_acq(&line->seq);
     if (seq_test != seq_found || seq_test2 != seq_found) {
       st.overrun_reading++;
+      M.link_in[i].overrun_reading_count++;
       in_seq[i] = seq_test2;
+      mx.lap(M.loop_overrun_reading_duration_ticks);
       continue;
     }
     uint64_t out_sz = sz, out_tsorig = tsorig;
@@ -150,9 +255,18 @@ int fdt_mux_run(const fdt_mux_cfg_t *cfg, const fdt_mux_callbacks_t *cb, void *c
       st.published++;
     }
     in_seq[i]++;
+    /* fd_mux.c:690-697: PublishedCount/Size or FilteredCount/Size of the in link */
+    fdt_link_in_metrics_t &L = M.link_in[i];
+    if (filter) { L.filtered_count++; L.filtered_size_bytes += sz; }
+    else        { L.published_count++; L.published_size_bytes += sz; }
+    if (mx.out) {
+      mx.lap(filter ? M.loop_filter_after_fragment_duration_ticks : M.loop_finish_duration_ticks);
+      fdt_histf_sample(filter ? &M.fragment_filtered_size_bytes : &M.fragment_handled_size_bytes, sz);
+    }
   }
   /* halting (fd_mux.c:701-714): every exposed frag counts as consumed */
   for (uint64_t i = 0; i < in_cnt; i++) if (cfg->in_fseq[i]) st_rel(cfg->in_fseq[i], in_seq[i]);
+  mx.write();
   if (stats_out) *stats_out = st;
   return 0;
 }

@@ -148,7 +148,47 @@ class MuxCfg(c.Structure):
                 ("in_seq0", c.c_uint64 * MUX_IN_MAX), ("in_fseq", vp * MUX_IN_MAX),
                 ("out_mcache", vp), ("out_depth", c.c_uint64), ("out_seq0", c.c_uint64), ("out_cnt", c.c_uint64),
                 ("out_fseq", vp * MUX_IN_MAX), ("flags", c.c_uint64), ("burst", c.c_uint64),
-                ("cr_max", c.c_uint64), ("lazy_iters", c.c_uint64)]
+                ("cr_max", c.c_uint64), ("lazy_iters", c.c_uint64), ("metrics", vp)]
+
+
+HISTF_BUCKET_CNT = 16
+
+
+class Histf(c.Structure):
+    """fdt_histf_t (the reference's fd_histf: 16 exponential buckets)."""
+    _fields_ = [("counts", c.c_uint64 * HISTF_BUCKET_CNT), ("sum", c.c_uint64),
+                ("left_edge", c.c_uint64 * (HISTF_BUCKET_CNT + 1))]
+
+    def as_dict(self):
+        return {"counts": list(self.counts), "sum": self.sum, "left_edge": list(self.left_edge)}
+
+
+class LinkInMetrics(c.Structure):
+    """fdt_link_in_metrics_t (metrics.xml <group name="Link" linkside="in">)."""
+    _fields_ = [(n, c.c_uint64) for n in ("published_count", "published_size_bytes", "filtered_count",
+                                          "filtered_size_bytes", "overrun_polling_count",
+                                          "overrun_polling_frag_count", "overrun_reading_count")]
+
+
+MUX_HISTS = ("loop_housekeeping_duration_ticks", "loop_backpressure_duration_ticks", "loop_caught_up_duration_ticks",
+             "loop_overrun_polling_duration_ticks", "loop_overrun_reading_duration_ticks",
+             "loop_filter_before_fragment_duration_ticks", "loop_filter_after_fragment_duration_ticks",
+             "loop_finish_duration_ticks", "fragment_filtered_size_bytes", "fragment_handled_size_bytes")
+
+
+class MuxMetrics(c.Structure):
+    """fdt_mux_metrics_t: the reference's Tile, Stem and Link-in metrics of a mux tile."""
+    _fields_ = ([("tile_pid", c.c_uint64), ("tile_tid", c.c_uint64), ("stem_in_backpressure", c.c_uint64),
+                 ("stem_backpressure_count", c.c_uint64)] + [(n, Histf) for n in MUX_HISTS] +
+                [("link_in", LinkInMetrics * MUX_IN_MAX), ("tick_per_ns", c.c_double),
+                 ("housekeeping_cnt", c.c_uint64)])
+
+    def as_dict(self, in_cnt=MUX_IN_MAX):
+        d = {n: getattr(self, n) for n in ("tile_pid", "tile_tid", "stem_in_backpressure", "stem_backpressure_count",
+                                           "tick_per_ns", "housekeeping_cnt")}
+        d.update({n: getattr(self, n).as_dict() for n in MUX_HISTS})
+        d["link_in"] = [{n: getattr(self.link_in[i], n) for n, _ in LinkInMetrics._fields_} for i in range(in_cnt)]
+        return d
 
 
 class MuxCallbacks(c.Structure):
@@ -253,6 +293,8 @@ def lib():
         "fdgpu_dtile_run_sandboxed": (None, [vp, u64, u64, c.POINTER(DTileStats), c.c_int]),
         "fdgpu_producer_join": (u64, [vp, c.POINTER(c.c_double)]),
         "fdgpu_producer_done": (c.c_int, [vp]),
+        "fdt_histf_init": (None, [vp, u64, u64]),
+        "fdt_histf_sample": (None, [vp, u64]),
         "fdt_mux_publish": (None, [vp, u64, u64, u64, u64, u64, u64]),
         "fdt_mux_run": (c.c_int, [c.POINTER(MuxCfg), c.POINTER(MuxCallbacks), vp, c.POINTER(u64),
                                   c.POINTER(MuxStats)]),
@@ -894,7 +936,7 @@ class VerifyMuxTile:
     def __init__(self, in_links, out_link, verifier, hashmap_seed=0x5EEDF00D, batch_txn_max=4096, inflight_max=2,
                  batch_wait_us=200, round_robin_idx=0, round_robin_cnt=1, cr_max=0, log_max=0, batch_sig_max=0,
                  batch_bytes_max=0, lazy_iters=16, flow_control=False, register=True, gpu_parse=False,
-                 lap_span_max=0, lap_margin=0):
+                 lap_span_max=0, lap_margin=0, metrics=False):
         import threading
         L = lib()
         in_links = list(in_links) if isinstance(in_links, (list, tuple)) else [in_links]
@@ -928,6 +970,8 @@ class VerifyMuxTile:
         if flow_control:
             mc.out_cnt, mc.out_fseq[0] = 1, out_link.fseq.ctypes.data
         mc.flags, mc.burst, mc.cr_max, mc.lazy_iters = MUX_FLAG_COPY | MUX_FLAG_MANUAL_PUBLISH, 1, self.cr_max, lazy_iters
+        self._metrics = MuxMetrics() if metrics else None   # the reference's link / stem metrics, written by the loop
+        mc.metrics = c.addressof(self._metrics) if metrics else None
         self.mcfg = mc
         self.cb = L.fdgpu_vmux_callbacks()
         self._halt = c.c_uint64(0)
@@ -991,6 +1035,11 @@ class VerifyMuxTile:
 
     def mux_stats(self):
         return self._mstats.as_dict()
+
+    def metrics(self):
+        """The reference's metrics (Tile, Stem, Link in) as the mux loop last
+        wrote them (metrics=True), or None."""
+        return self._metrics.as_dict(len(self.in_links)) if self._metrics is not None else None
 
     def latencies_ns(self):
         n = self.stats()["lat_cnt"]

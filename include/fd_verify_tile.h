@@ -386,6 +386,7 @@ typedef struct {
   uint64_t                burst;                         /* frags published per in frag (>= 1) */
   uint64_t                cr_max;                        /* 0: the reference default (fd_mux.c:326-327) */
   uint64_t                lazy_iters;                    /* loop iterations between housekeeping events (0: 16) */
+  struct fdt_mux_metrics * metrics;                      /* NULL, or written at every housekeeping event (below) */
 } fdt_mux_cfg_t;
 
 typedef struct {
@@ -398,6 +399,56 @@ typedef struct {
   uint64_t published;           /* automatic publishes (not MANUAL_PUBLISH) */
   uint64_t loops;
 } fdt_mux_stats_t;
+
+/* The reference's metrics of a mux tile (src/disco/metrics/metrics.xml
+   groups Link (in side, per in link), Stem and Tile; accumulated as
+   fd_mux.c:370-379,440-451,525-697 does), written by fdt_mux_run into
+   *cfg->metrics at every housekeeping event and when it halts, for an
+   observer thread or process to read (word-wise; counters only grow).
+   Histograms are the reference's fd_histf: 16 exponential buckets between
+   a min and a max, the first for samples < min, the last for >= max, and
+   the sum of all samples.  Loop durations are sampled in ticks (the time
+   stamp counter, tick_per_ns below) between 50 ns and 50 us; fragment sizes
+   between 0 and 2094 bytes.  Per-iteration timing costs a counter read per
+   loop iteration, so it runs only when metrics is non-NULL. */
+#define FDT_HISTF_BUCKET_CNT (16UL)
+typedef struct {
+  uint64_t counts[ FDT_HISTF_BUCKET_CNT ];
+  uint64_t sum;
+  uint64_t left_edge[ FDT_HISTF_BUCKET_CNT + 1 ];   /* bucket b holds left_edge[b] <= x < left_edge[b+1] */
+} fdt_histf_t;
+/* fd_histf_new's bucket edges for [min, max) (fd_histf.h:77-117) */
+void fdt_histf_init  ( fdt_histf_t * h, uint64_t min, uint64_t max );
+void fdt_histf_sample( fdt_histf_t * h, uint64_t value );
+
+typedef struct {                                 /* metrics.xml <group name="Link" linkside="in"> */
+  uint64_t published_count;                      /* frags consumed and not filtered */
+  uint64_t published_size_bytes;
+  uint64_t filtered_count;
+  uint64_t filtered_size_bytes;
+  uint64_t overrun_polling_count;
+  uint64_t overrun_polling_frag_count;
+  uint64_t overrun_reading_count;
+} fdt_link_in_metrics_t;
+
+typedef struct fdt_mux_metrics {
+  uint64_t tile_pid, tile_tid;                   /* <group name="Tile"> */
+  uint64_t stem_in_backpressure;                 /* <group name="Stem"> gauge */
+  uint64_t stem_backpressure_count;
+  fdt_histf_t loop_housekeeping_duration_ticks;
+  fdt_histf_t loop_backpressure_duration_ticks;
+  fdt_histf_t loop_caught_up_duration_ticks;
+  fdt_histf_t loop_overrun_polling_duration_ticks;
+  fdt_histf_t loop_overrun_reading_duration_ticks;
+  fdt_histf_t loop_filter_before_fragment_duration_ticks;
+  fdt_histf_t loop_filter_after_fragment_duration_ticks;
+  fdt_histf_t loop_finish_duration_ticks;
+  fdt_histf_t fragment_filtered_size_bytes;
+  fdt_histf_t fragment_handled_size_bytes;
+  fdt_link_in_metrics_t link_in[ FDT_MUX_IN_MAX ];
+  double   tick_per_ns;                          /* the "seconds" converter: seconds = ticks / tick_per_ns / 1e9 */
+  uint64_t housekeeping_cnt;                     /* metrics writes so far */
+} fdt_mux_metrics_t;
 
 /* The mux run loop (fd_mux.c:387-699) with the cnc replaced by a halt word:
    housekeeping every lazy_iters iterations (out credits from the out fseqs,

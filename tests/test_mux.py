@@ -422,3 +422,52 @@ def test_vmux_cfg_checks():
     with pytest.raises(RuntimeError):
         tile.VerifyMuxTile(inl, tiny, ver, batch_txn_max=4)
     assert tile.vmux_dcache_data_sz(64, 16, 2) >= (64 + 3 * 16) * tile.TPU_DCACHE_MTU
+
+
+def test_histf_matches_reference_buckets():
+    """fdt_histf_init / fdt_histf_sample restate fd_histf (src/util/hist/
+    fd_histf.h:77-117,131-158): the header's own example -- min 1, max 100 --
+    has exactly these left edges, and a sample lands in [left, right)."""
+    h = tile.Histf()
+    L = tile.lib()
+    L.fdt_histf_init(c.byref(h), 1, 100)
+    assert list(h.left_edge)[:16] == [0, 1, 2, 3, 4, 5, 7, 9, 12, 16, 22, 30, 41, 55, 74, 100]
+    for v in (0, 1, 6, 99, 100, 10 ** 9):
+        L.fdt_histf_sample(c.byref(h), v)
+    assert h.counts[0] == 1 and h.counts[1] == 1 and h.counts[5] == 1 and h.counts[14] == 1 and h.counts[15] == 2
+    assert h.sum == 0 + 1 + 6 + 99 + 100 + 10 ** 9
+
+
+def test_vmux_reference_metrics(oracle):
+    """The mux loop's metrics in the reference's schema (metrics.xml Link in,
+    Stem, Tile; fd_mux.c:597-697): per in link, the consumed frags split into
+    published (after_frag kept it) and filtered (after_frag dropped it: here
+    the host parse's failures) with their byte counts; before_frag's
+    round-robin drops count in no link counter, only in their loop
+    histogram; every handled / filtered frag's size is in the size
+    histograms; no overrun."""
+    ps = _mixed_stream(600, seed=41)
+    ver = tile.PyVerifier(oracle_fn(oracle), slots=2)
+    inl = tile.Link(1 << 12, 1232)
+    outl = tile.Link(1 << 12, tile.TPU_DCACHE_MTU, data_sz=(len(ps) + 8) * (tile.TPU_DCACHE_MTU + 64))
+    vm = tile.VerifyMuxTile(inl, outl, ver, hashmap_seed=0x42, batch_txn_max=32, inflight_max=2, log_max=1 << 12,
+                            round_robin_idx=1, round_robin_cnt=3, batch_wait_us=100, metrics=True)
+    for p in ps:
+        inl.publish(p)
+    vm.run(len(ps), timeout_s=60)
+    m = vm.metrics()
+    exp_out, _ = tile_model.verify_tile_model(ps, 0x42, oracle_fn(oracle), rr_idx=1, rr_cnt=3)
+    own = [p for k, p in enumerate(ps) if k % 3 == 1]
+    failed = [p for k, p in enumerate(ps) if k % 3 == 1 and exp_out[k] == tile.LOG_PARSE_FAIL]
+    li = m["link_in"][0]
+    assert li["published_count"] + li["filtered_count"] == len(own)
+    assert li["filtered_count"] == len(failed) > 0
+    assert li["filtered_size_bytes"] == sum(len(p) for p in failed)
+    assert li["published_size_bytes"] == sum(len(p) for p in own) - li["filtered_size_bytes"]
+    assert li["overrun_polling_count"] == li["overrun_reading_count"] == 0
+    assert sum(m["fragment_handled_size_bytes"]["counts"]) == li["published_count"]
+    assert sum(m["fragment_filtered_size_bytes"]["counts"]) == li["filtered_count"]
+    assert sum(m["loop_filter_before_fragment_duration_ticks"]["counts"]) == len(ps) - len(own)
+    assert sum(m["loop_caught_up_duration_ticks"]["counts"]) > 0 and m["housekeeping_cnt"] > 0
+    assert m["tick_per_ns"] > 0.1 and m["tile_tid"] > 0 and m["stem_in_backpressure"] == 0
+    vm.close()
