@@ -405,12 +405,15 @@ def sync_latency(arena, txns, calls=1000, threads=64):
 
 
 TILE_RUNS = (  # name, verify tiles, quic links (producers), offered txn/s (-1: prefilled links, the tiles' capacity)
-    ("mux1_capacity", 1, 1, -1.0),
+    # the paced runs first, so a latency line never runs behind a capacity run's multi-GB prefill; at most
+    # two engines (18 streams) in the child: three at 32 HW queues slowed every later run in the process
+    # (profiles/r04/tile_run_order.md)
     ("mux1_paced_12M", 1, 2, 12e6),
     ("mux1_paced_16M", 1, 2, 16e6),
-    ("mux2_capacity", 2, 2, -1.0),
     ("mux2_paced_20M", 2, 4, 20e6),
     ("mux2_paced_24M", 2, 4, 24e6),
+    ("mux1_capacity", 1, 1, -1.0),
+    ("mux2_capacity", 2, 2, -1.0),
 )
 # quic -> verify link depth: paced runs at the reference's (config->tiles.verify.receive_buffer_size,
 # default.toml:888-893: 16384, fd_frankendancer.c:59), with the stream published TILE_PACED_REPS times
@@ -418,6 +421,10 @@ TILE_RUNS = (  # name, verify tiles, quic links (producers), offered txn/s (-1: 
 # before the tiles start, so their links hold the whole stream
 TILE_DEPTH_LG_PACED, TILE_DEPTH_LG_PREFILL, TILE_PACED_REPS = 14, 21, 4
 TILE_BATCH, TILE_INFLIGHT = 16384, 8   # txns per GPU batch, batches in flight per tile
+# multi-signature frags: a batch also closes at this many signatures by the frag-size bound the tile sees
+# (~9.5 per cfg3 frag for ~6.5 real): ~2.6 K cfg3 txns, so 8 batches in flight are ~1.3 ms of GPU work
+# (49152: 1-tile p99 batch 5.8 ms, 2 tiles 59-65 M sig/s; 24576: 3.0 ms, 67-70 M; profiles/r04/tile_run_order.md)
+TILE_CFG3_SIG_MAX = 24576
 TILE_RUNS_CFG3 = (  # the same tile over cfg3 frags (1-12 signatures, payloads up to the 1232-B MTU: SURVEY 8(d) cfg5)
     ("mux1_capacity_cfg3", 1, 1, -1.0),
     ("mux2_capacity_cfg3", 2, 2, -1.0),
@@ -439,6 +446,8 @@ def tile_cmd(device, cpus, npz, out, runs=TILE_RUNS, multi=0):
            "--depth-lg-paced", str(TILE_DEPTH_LG_PACED), "--paced-reps", str(TILE_PACED_REPS),
            "--wait-us", "200", "--pin", "1", "--hw-queues", str(TILE_HW_QUEUES), "--reps", str(TILE_REPS),
            "--payload-npz", npz, "--device", str(device), "--sweep", sweep, "--out", out]
+    if multi:
+        cmd += ["--batch-sig-max", str(TILE_CFG3_SIG_MAX)]
     if cpus:
         cmd += ["--cpu-list", ",".join(str(c) for c in cpus)]
     return cmd

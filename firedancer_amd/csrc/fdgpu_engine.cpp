@@ -400,6 +400,25 @@ static uint32_t kflags(const fdgpu_engine_t *e) {
          ((e->cfg.flags & FDGPU_FLAG_PAIR) && !(e->cfg.flags & FDGPU_FLAG_KEY_CACHE) ? FDGPU_FLAG_KPAIR : 0u);
 }
 
+/* FDGPU_FLAG_PAIR_AUTO: a ring batch of at most this many signatures takes
+   the two-lane kernel while at most one other batch of the engine is still
+   running on the device (tools/pair_probe.py: 0.75x the one-lane kernel's
+   time up to 8 K signatures, 0.77x at 16 K, 0.82x at 32 K; 1.24x at 64 K,
+   where the chip fills) */
+static constexpr uint64_t FDGPU_PAIR_AUTO_MAX = 32768;
+
+/* the kernel flags of a ring batch of n_sig signatures (ring_mu held) */
+static uint32_t ring_kflags(const fdgpu_engine_t *e, uint64_t n_sig) {
+  uint32_t f = kflags(e);
+  if ((e->cfg.flags & FDGPU_FLAG_PAIR_AUTO) && !(f & FDGPU_FLAG_KCACHE) && n_sig <= FDGPU_PAIR_AUTO_MAX) {
+    uint32_t busy = 0;
+    for (const auto &c : e->slots)
+      busy += c.ticket >= 0 && !(e->flag_poll && __atomic_load_n(c.h_flag, __ATOMIC_ACQUIRE) == c.flag_seq);
+    if (busy <= 1) f |= FDGPU_FLAG_KPAIR;
+  }
+  return f;
+}
+
 extern "C" {
 
 char const *fdgpu_last_error(void) { return g_err.c_str(); }
@@ -497,8 +516,9 @@ int fdgpu_engine_info(fdgpu_engine_t *e, uint32_t *grid_blocks, uint32_t *block_
    workspace (grown on demand; callers on other streams synchronise first). */
 static int enqueue_verify(fdgpu_engine_t *e, const uint8_t *d_arena, const fdgpu_sig_desc_t *d_sigs,
                           const uint32_t *d_perm, uint64_t n_sig, const fdgpu_txn_desc_t *d_txns, uint64_t n_txn,
-                          int8_t *d_sig_codes, int8_t *d_txn_codes, hipStream_t st, uint32_t *ws = nullptr) {
-  const uint32_t flags = kflags(e);
+                          int8_t *d_sig_codes, int8_t *d_txn_codes, hipStream_t st, uint32_t *ws = nullptr,
+                          uint32_t flags = ~0u) {
+  if (flags == ~0u) flags = kflags(e);
   if (!ws && n_sig > e->ws_sig) {
     HIPCHK(hipStreamSynchronize(st), FDGPU_ERR_DEVICE);
     HIPCHK(hipStreamSynchronize(e->compute), FDGPU_ERR_DEVICE);
@@ -552,7 +572,7 @@ static int64_t submit_slot(fdgpu_engine_t *e, Slot *s, uint64_t arena_sz, fdgpu_
      overlap each other on the GPU (a 64K-signature batch fills only half of
      the resident wave slots) */
   int rc = enqueue_verify(e, s->d_arena, s->d_sigs, perm ? s->d_perm : nullptr, (uint64_t)ns, s->d_txns, txn_cnt,
-                          s->d_sig_codes, s->d_txn_codes, s->stream, s->d_ws);
+                          s->d_sig_codes, s->d_txn_codes, s->stream, s->d_ws, ring_kflags(e, (uint64_t)ns));
   if (rc) return rc;
   if (txn_cnt) HIPCHK(hipMemcpyAsync(s->h_codes, s->d_txn_codes, txn_cnt, hipMemcpyDeviceToHost, s->stream), FDGPU_ERR_DEVICE);
   ++s->flag_seq;
@@ -816,7 +836,7 @@ int64_t fdgpu_submit_frags(fdgpu_engine_t *e, uint8_t const *arena, uint64_t are
                                   s->d_sig0, s->d_blocktot, s->d_n_sig, s->d_sigs, s->d_txns, s->stream),
            FDGPU_ERR_DEVICE);
     HIPCHK(fdgpu_launch_verify_sigs(s->d_arena, s->d_sigs, (uint32_t)bound, nullptr, e->d_btab, s->d_ws, s->d_sig_codes,
-                                    kflags(e), s->stream, s->d_n_sig, e->resident_blocks, e->kc_seed),
+                                    ring_kflags(e, bound), s->stream, s->d_n_sig, e->resident_blocks, e->kc_seed),
            FDGPU_ERR_DEVICE);
     HIPCHK(fdgpu_launch_frag_finish(s->d_txns, (uint32_t)n, s->d_sig_codes, s->d_txn_sz, s->d_fx, s->d_txn_out,
                                     (int8_t *)s->d_tr, s->d_tr + tr_base, s->stream),
@@ -938,7 +958,7 @@ int64_t fdgpu_submit_frags_io(fdgpu_engine_t *e, fdgpu_frag_io_t const *fio, uin
                                           s->d_n_sig, s->stream),
            FDGPU_ERR_DEVICE);
     HIPCHK(fdgpu_launch_verify_sigs(s->d_arena, s->d_sigs, (uint32_t)bound, nullptr, e->d_btab, s->d_ws, s->d_sig_codes,
-                                    kflags(e), s->stream, s->d_n_sig, e->resident_blocks, e->kc_seed, zero_cnt),
+                                    ring_kflags(e, bound), s->stream, s->d_n_sig, e->resident_blocks, e->kc_seed, zero_cnt),
            FDGPU_ERR_DEVICE);
     HIPCHK(fdgpu_launch_frag_finish_io(s->d_txns, (uint32_t)n, s->d_sig_codes, s->d_txn_sz, d_fx, s->d_txn_out,
                                        s->d_arena, hash_seed, out_dev, (int8_t *)s->d_trh, (uint64_t *)(s->d_trh + cb),
@@ -1438,6 +1458,10 @@ bool sync_run(SyncState &st, const std::vector<SyncReq *> &batch) {
     if (st.eng) fdgpu_engine_close(st.eng);
     fdgpu_cfg_t cfg{};
     cfg.max_txn = SYNC_BATCH_MAX; cfg.max_sig = SYNC_BATCH_MAX * 16; cfg.ring_depth = 1;
+    /* a call's batch is small (one txn per concurrent caller): the two-lane
+       kernel's shorter wave is the call's latency (FDGPU_SYNC_PAIR=0: off) */
+    const char *sp = getenv("FDGPU_SYNC_PAIR");
+    cfg.flags = (sp && sp[0] == '0') ? 0u : FDGPU_FLAG_PAIR_AUTO;
     cfg.max_arena = std::min<uint64_t>(std::max<uint64_t>(SYNC_BATCH_MAX * (96 * 16 + 1232), need * 2),
                                        2 * SYNC_ARENA_MAX);
     const char *dv = getenv("FDGPU_SYNC_DEVICE");

@@ -45,5 +45,6 @@ def test_tile_cmd_cfg3():
     cmd = bench.tile_cmd(1, [], "/tmp/y.npz", "/tmp/y.jsonl", bench.TILE_RUNS_CFG3, multi=1)
     args = bench_tile.make_parser().parse_args(cmd[2:])
     assert args.multi == 1 and args.device == 1 and args.cpu_list == ""
+    assert args.batch_sig_max == bench.TILE_CFG3_SIG_MAX
     assert len(args.sweep.split(";")) == len(bench.TILE_RUNS_CFG3)
     assert all(r[3] == -1.0 for r in bench.TILE_RUNS_CFG3)       # capacity lines

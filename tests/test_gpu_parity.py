@@ -574,3 +574,23 @@ def test_pair_kernel_path(vectors, oracle, ref_mapping):
             assert (got == oracle.verify_txns(arena, txns, nthreads=8)).all()
         finally:
             eng.close()
+
+
+def test_pair_auto_ring(oracle):
+    """FDGPU_FLAG_PAIR_AUTO: each ring batch picks the two-lane or one-lane
+    kernel by its size and how many of the engine's batches are running.
+    Four batches in flight on a depth-4 ring (sizes either side of the 32 K
+    cap, so both kernels run, some while others are busy) must each match
+    the oracle."""
+    import firedancer_amd as fa
+    eng = fa.VerifyEngine(0, max_txn=40000, ring_depth=4, pair_auto=True)
+    try:
+        sets = [workload.cfg1(1500, seed=0xA2A), workload.cfg1(36000, seed=0xA2B),
+                workload.cfg3(700, seed=0xA2C), workload.make_txns(2500, 0xA2D, corrupt=0.5)]
+        tks = [eng.submit(arena, txns) for arena, txns, _ in sets]
+        for tk, (arena, txns, _) in zip(tks, sets):
+            got = eng.poll(tk, blocking=True)
+            exp = oracle.verify_txns(arena, txns, nthreads=8)
+            assert (got == exp).all(), np.nonzero(got != exp)[0][:10]
+    finally:
+        eng.close()
