@@ -75,6 +75,13 @@ struct MuxMetrics {
     fdt_histf_sample(&h, next - now);
     now = next;
   }
+  /* k loop iterations ended at once: k samples, each a k-th of the time */
+  void lap_n(fdt_histf_t &h, uint64_t k) {
+    if (!out) return;
+    const uint64_t next = __rdtsc(), d = (next - now) / k;
+    for (uint64_t j = 0; j < k; j++) fdt_histf_sample(&h, d);
+    now = next;
+  }
   void write() {
     if (!out) return;
     m.housekeeping_cnt++;
@@ -86,6 +93,215 @@ struct MuxMetrics {
 }  // namespace
 
 /* ------------------------------------------------------------------ mux */
+
+namespace {
+
+/* the vmux tile's own instance of the loop (below, after its callbacks) */
+bool is_vmux_callbacks(const fdt_mux_callbacks_t *cb);
+int vmux_loop(const fdt_mux_cfg_t *cfg, void *ctx, const volatile uint64_t *halt, fdt_mux_stats_t *stats_out);
+
+/* the loop's calls out: through the callback table (any tile) ... */
+struct CbHooks {
+  const fdt_mux_callbacks_t *cb;
+  void *ctx;
+  void metrics_write() { if (cb->metrics_write) cb->metrics_write(ctx); }
+  void during_housekeeping() { if (cb->during_housekeeping) cb->during_housekeeping(ctx); }
+  void before_credit(fdt_mux_context_t *m) { if (cb->before_credit) cb->before_credit(ctx, m); }
+  void after_credit(fdt_mux_context_t *m, int *p) { if (cb->after_credit) cb->after_credit(ctx, m, p); }
+  uint64_t skip(uint64_t, uint64_t) { return 0; }
+  void skipped(uint64_t, uint64_t, uint64_t) {}
+  bool has_before_frag() const { return cb->before_frag != nullptr; }
+  void before_frag(uint64_t i, uint64_t seq, uint64_t sig, int *f) { cb->before_frag(ctx, i, seq, sig, f); }
+  void during_frag(uint64_t i, uint64_t seq, uint64_t sig, uint64_t chunk, uint64_t sz, int *f) {
+    if (cb->during_frag) cb->during_frag(ctx, i, seq, sig, chunk, sz, f);
+  }
+  void after_frag(uint64_t i, uint64_t seq, uint64_t *sig, uint64_t *chunk, uint64_t *sz, uint64_t *tsorig, int *f,
+                  fdt_mux_context_t *m) {
+    if (cb->after_frag) cb->after_frag(ctx, i, seq, sig, chunk, sz, tsorig, f, m);
+  }
+};
+
+template <class H>
+int mux_loop(const fdt_mux_cfg_t *cfg, H &h, const volatile uint64_t *halt, fdt_mux_stats_t *stats_out) {
+  if (cfg->in_cnt > FDT_MUX_IN_MAX || cfg->out_cnt > FDT_MUX_OUT_MAX) return -1;
+  const uint64_t in_cnt = cfg->in_cnt, out_cnt = cfg->out_cnt, flags = cfg->flags;
+  const bool copy = (flags & FDT_MUX_FLAG_COPY) != 0;
+  uint64_t min_in_depth = UINT64_MAX;
+  for (uint64_t i = 0; i < in_cnt; i++) {
+    if (!cfg->in_mcache[i] || !pow2(cfg->in_depth[i])) return -1;
+    min_in_depth = std::min(min_in_depth, cfg->in_depth[i]);
+  }
+  /* out stream (fd_mux.c:209-219: no mcache -> a 128-deep dummy, no consumers) */
+  fdt_frag_meta_t *mcache = cfg->out_mcache;
+  const uint64_t depth = mcache ? cfg->out_depth : 128;
+  if (mcache && !pow2(depth)) return -1;
+  if (!mcache && out_cnt) return -1;
+  for (uint64_t j = 0; j < out_cnt; j++) if (!cfg->out_fseq[j]) return -1;
+  /* credits (fd_mux.c:326-335) */
+  const uint64_t cr_max_max = copy ? depth : std::min(min_in_depth, depth);
+  const uint64_t cr_max = cfg->cr_max ? cfg->cr_max : cr_max_max;
+  if (cr_max < 1 || cr_max > cr_max_max) return -1;
+  const uint64_t burst = cfg->burst ? cfg->burst : 1;
+  const uint64_t lazy = cfg->lazy_iters ? cfg->lazy_iters : 16;
+
+  uint64_t in_seq[FDT_MUX_IN_MAX], out_seq[FDT_MUX_OUT_MAX];
+  for (uint64_t i = 0; i < in_cnt; i++) in_seq[i] = cfg->in_seq0[i];
+  for (uint64_t j = 0; j < out_cnt; j++) out_seq[j] = ld_acq(cfg->out_fseq[j]);
+  uint64_t seq = cfg->out_seq0, cr_avail = 0, cr_filt = 0, in_rr = 0;
+  fdt_mux_stats_t st{};
+  MuxMetrics mx(cfg->metrics);
+  fdt_mux_metrics_t &M = mx.m;
+  for (uint64_t hk = 0;; hk--) {
+    st.loops++;
+    if (!hk) {
+      hk = lazy;
+      /* housekeeping (fd_mux.c:391-491): receive credits from the outs, send
+         our position to the ins, metrics, user callbacks, halt (the cnc signal) */
+      for (uint64_t j = 0; j < out_cnt; j++) out_seq[j] = ld_acq(cfg->out_fseq[j]);
+      const uint64_t exposed = copy ? 0 : cr_max - cr_avail + cr_filt;
+      for (uint64_t i = 0; i < in_cnt; i++) if (cfg->in_fseq[i]) st_rel(cfg->in_fseq[i], in_seq[i] - exposed);
+      M.stem_in_backpressure = mx.in_backp;
+      mx.write();
+      h.metrics_write();
+      if (halt && *halt) break;
+      if (cr_avail < cr_max) {
+        cr_avail = cr_max;
+        for (uint64_t j = 0; j < out_cnt; j++) {
+          const int64_t lag = std::max<int64_t>((int64_t)(seq - out_seq[j]), 0);
+          const uint64_t out_cr = (uint64_t)std::max<int64_t>((int64_t)cr_max - lag, 0);
+          cr_avail = std::min(cr_avail, out_cr);
+        }
+        if (cr_avail == cr_max) cr_filt = 0;
+      }
+      h.during_housekeeping();
+      mx.lap(M.loop_housekeeping_duration_ticks);
+    }
+
+    fdt_mux_context_t mux = {mcache, depth, &cr_avail, &seq, out_cnt ? 1ull : 0ull};
+    h.before_credit(&mux);
+    if (cr_avail < cr_filt + burst) {                                   /* fd_mux.c:548-556 */
+      st.backpressure++;
+      M.stem_backpressure_count += (uint64_t)!mx.in_backp;              /* transitions into backpressure */
+      mx.in_backp = true;
+      mx.lap(M.loop_backpressure_duration_ticks);
+      continue;
+    }
+    mx.in_backp = false;
+    int poll_in = 1;
+    h.after_credit(&mux, &poll_in);
+    if (!poll_in || !in_cnt) { mx.lap(M.loop_finish_duration_ticks); continue; }
+
+    const uint64_t i = in_rr;
+    in_rr = in_rr + 1 == in_cnt ? 0 : in_rr + 1;
+    /* a filter that is a pure function of the seq (the verify tiles' round
+       robin, fd_verify.c:46) names the seqs it would drop: the loop reads the
+       line of the first seq it keeps, and when that one is published, so are
+       the ones before it -- they are filtered as the reference filters them
+       one loop each (fd_mux.c:612-624), without their lines */
+    const uint64_t skip = h.skip(i, in_seq[i]);
+    const uint64_t s_next = in_seq[i] + skip;
+    const fdt_frag_meta_t *line = cfg->in_mcache[i] + (s_next & (cfg->in_depth[i] - 1));
+    /* the line 16 frags ahead: a tile that reads every frag's line streams
+       the whole mcache */
+    __builtin_prefetch(cfg->in_mcache[i] + ((s_next + 16) & (cfg->in_depth[i] - 1)));
+    const uint64_t seq_found = ld_acq(&line->seq);
+    const int64_t diff = (int64_t)(s_next - seq_found);
+    if (diff) {                                     /* caught up, or overrun (fd_mux.c:595-609) */
+      if (diff < 0) {
+        const uint64_t lost = seq_found - in_seq[i];
+        st.overrun_polling += lost;
+        M.link_in[i].overrun_polling_count++;
+        M.link_in[i].overrun_polling_frag_count += lost;
+        in_seq[i] = seq_found;
+        mx.lap(M.loop_overrun_polling_duration_ticks);
+      } else if (skip) {
+        /* the kept seq is not out yet: filter the skipped ones that are (the
+           last ones of a stream have no kept seq after them) */
+        const uint64_t mask = cfg->in_depth[i] - 1;
+        const uint64_t k = ld_acq(&cfg->in_mcache[i][(s_next - 1) & mask].seq) == s_next - 1 ? skip
+                         : ld_acq(&cfg->in_mcache[i][in_seq[i] & mask].seq) == in_seq[i] ? 1 : 0;
+        if (k) {
+          h.skipped(i, in_seq[i], k);
+          if (!copy) cr_filt += k * (uint64_t)(cr_avail < cr_max);
+          st.in_frags += k;
+          st.filtered_before += k;
+          in_seq[i] += k;
+          mx.lap_n(M.loop_filter_before_fragment_duration_ticks, k);
+        } else {
+          mx.lap(M.loop_caught_up_duration_ticks);
+        }
+      } else {
+        mx.lap(M.loop_caught_up_duration_ticks);
+      }
+      continue;
+    }
+    if (skip) {
+      h.skipped(i, in_seq[i], skip);
+      if (!copy) cr_filt += skip * (uint64_t)(cr_avail < cr_max);
+      st.in_frags += skip;
+      st.filtered_before += skip;
+      mx.lap_n(M.loop_filter_before_fragment_duration_ticks, skip);
+      in_seq[i] = s_next;
+    }
+    uint64_t sig = line->sig;
+    st.in_frags++;
+    if (h.has_before_frag()) {
+      int filter = 0;
+      h.before_frag(i, seq_found, sig, &filter);
+      if (filter) {
+        if (!copy) cr_filt += (uint64_t)(cr_avail < cr_max);
+        in_seq[i]++;
+        st.filtered_before++;
+        mx.lap(M.loop_filter_before_fragment_duration_ticks);
+        continue;
+      }
+    }
+    std::atomic_thread_fence(std::memory_order_acquire);
+    uint64_t chunk = line->chunk, sz = line->sz;
+    const uint64_t ctl = line->ctl, tsorig = line->tsorig;
+    std::atomic_thread_fence(std::memory_order_acquire);
+    const uint64_t seq_test = ld_acq(&line->seq);
+    int filter = 0;
+    h.during_frag(i, seq_found, sig, chunk, sz, &filter);
+    /* the reference checks the seq read before during_frag (fd_mux.c:641-655);
+       the quic -> verify link has no backpressure, so the payload copy is
+       checked too */
+    const uint64_t seq_test2 = ld_acq(&line->seq);
+    if (seq_test != seq_found || seq_test2 != seq_found) {
+      st.overrun_reading++;
+      M.link_in[i].overrun_reading_count++;
+      in_seq[i] = seq_test2;
+      mx.lap(M.loop_overrun_reading_duration_ticks);
+      continue;
+    }
+    uint64_t out_sz = sz, out_tsorig = tsorig;
+    if (!filter) h.after_frag(i, seq_found, &sig, &chunk, &out_sz, &out_tsorig, &filter, &mux);
+    if (filter) {
+      if (!copy) cr_filt += (uint64_t)(cr_avail < cr_max);
+      st.filtered_after++;
+    } else if (!(flags & FDT_MUX_FLAG_MANUAL_PUBLISH)) {
+      fdt_mux_publish(&mux, sig, chunk, out_sz, ctl, out_tsorig, (uint32_t)now_ns());
+      st.published++;
+    }
+    in_seq[i]++;
+    /* fd_mux.c:690-697: PublishedCount/Size or FilteredCount/Size of the in link */
+    fdt_link_in_metrics_t &L = M.link_in[i];
+    if (filter) { L.filtered_count++; L.filtered_size_bytes += sz; }
+    else        { L.published_count++; L.published_size_bytes += sz; }
+    if (mx.out) {
+      mx.lap(filter ? M.loop_filter_after_fragment_duration_ticks : M.loop_finish_duration_ticks);
+      fdt_histf_sample(filter ? &M.fragment_filtered_size_bytes : &M.fragment_handled_size_bytes, sz);
+    }
+  }
+  /* halting (fd_mux.c:701-714): every exposed frag counts as consumed */
+  for (uint64_t i = 0; i < in_cnt; i++) if (cfg->in_fseq[i]) st_rel(cfg->in_fseq[i], in_seq[i]);
+  mx.write();
+  if (stats_out) *stats_out = st;
+  return 0;
+}
+
+}  // namespace
+
 
 extern "C" {
 
@@ -126,149 +342,10 @@ void fdt_mux_publish(fdt_mux_context_t *ctx, uint64_t sig, uint64_t chunk, uint6
 
 int fdt_mux_run(const fdt_mux_cfg_t *cfg, const fdt_mux_callbacks_t *cb, void *ctx, const volatile uint64_t *halt,
                 fdt_mux_stats_t *stats_out) {
-  if (!cfg || !cb || cfg->in_cnt > FDT_MUX_IN_MAX || cfg->out_cnt > FDT_MUX_OUT_MAX) return -1;
-  const uint64_t in_cnt = cfg->in_cnt, out_cnt = cfg->out_cnt, flags = cfg->flags;
-  const bool copy = (flags & FDT_MUX_FLAG_COPY) != 0;
-  uint64_t min_in_depth = UINT64_MAX;
-  for (uint64_t i = 0; i < in_cnt; i++) {
-    if (!cfg->in_mcache[i] || !pow2(cfg->in_depth[i])) return -1;
-    min_in_depth = std::min(min_in_depth, cfg->in_depth[i]);
-  }
-  /* out stream (fd_mux.c:209-219: no mcache -> a 128-deep dummy, no consumers) */
-  fdt_frag_meta_t *mcache = cfg->out_mcache;
-  const uint64_t depth = mcache ? cfg->out_depth : 128;
-  if (mcache && !pow2(depth)) return -1;
-  if (!mcache && out_cnt) return -1;
-  for (uint64_t j = 0; j < out_cnt; j++) if (!cfg->out_fseq[j]) return -1;
-  /* credits (fd_mux.c:326-335) */
-  const uint64_t cr_max_max = copy ? depth : std::min(min_in_depth, depth);
-  const uint64_t cr_max = cfg->cr_max ? cfg->cr_max : cr_max_max;
-  if (cr_max < 1 || cr_max > cr_max_max) return -1;
-  const uint64_t burst = cfg->burst ? cfg->burst : 1;
-  const uint64_t lazy = cfg->lazy_iters ? cfg->lazy_iters : 16;
-
-  uint64_t in_seq[FDT_MUX_IN_MAX], out_seq[FDT_MUX_OUT_MAX];
-  for (uint64_t i = 0; i < in_cnt; i++) in_seq[i] = cfg->in_seq0[i];
-  for (uint64_t j = 0; j < out_cnt; j++) out_seq[j] = ld_acq(cfg->out_fseq[j]);
-  uint64_t seq = cfg->out_seq0, cr_avail = 0, cr_filt = 0, in_rr = 0;
-  fdt_mux_stats_t st{};
-  MuxMetrics mx(cfg->metrics);
-  fdt_mux_metrics_t &M = mx.m;
-  for (uint64_t hk = 0;; hk--) {
-    st.loops++;
-    if (!hk) {
-      hk = lazy;
-      /* housekeeping (fd_mux.c:391-491): receive credits from the outs, send
-         our position to the ins, metrics, user callbacks, halt (the cnc signal) */
-      for (uint64_t j = 0; j < out_cnt; j++) out_seq[j] = ld_acq(cfg->out_fseq[j]);
-      const uint64_t exposed = copy ? 0 : cr_max - cr_avail + cr_filt;
-      for (uint64_t i = 0; i < in_cnt; i++) if (cfg->in_fseq[i]) st_rel(cfg->in_fseq[i], in_seq[i] - exposed);
-      M.stem_in_backpressure = mx.in_backp;
-      mx.write();
-      if (cb->metrics_write) cb->metrics_write(ctx);
-      if (halt && *halt) break;
-      if (cr_avail < cr_max) {
-        cr_avail = cr_max;
-        for (uint64_t j = 0; j < out_cnt; j++) {
-          const int64_t lag = std::max<int64_t>((int64_t)(seq - out_seq[j]), 0);
-          const uint64_t out_cr = (uint64_t)std::max<int64_t>((int64_t)cr_max - lag, 0);
-          cr_avail = std::min(cr_avail, out_cr);
-        }
-        if (cr_avail == cr_max) cr_filt = 0;
-      }
-      if (cb->during_housekeeping) cb->during_housekeeping(ctx);
-      mx.lap(M.loop_housekeeping_duration_ticks);
-    }
-
-    fdt_mux_context_t mux = {mcache, depth, &cr_avail, &seq, out_cnt ? 1ull : 0ull};
-    if (cb->before_credit) cb->before_credit(ctx, &mux);
-    if (cr_avail < cr_filt + burst) {                                   /* fd_mux.c:548-556 */
-      st.backpressure++;
-      M.stem_backpressure_count += (uint64_t)!mx.in_backp;              /* transitions into backpressure */
-      mx.in_backp = true;
-      mx.lap(M.loop_backpressure_duration_ticks);
-      continue;
-    }
-    mx.in_backp = false;
-    int poll_in = 1;
-    if (cb->after_credit) cb->after_credit(ctx, &mux, &poll_in);
-    if (!poll_in || !in_cnt) { mx.lap(M.loop_finish_duration_ticks); continue; }
-
-    const uint64_t i = in_rr;
-    in_rr = in_rr + 1 == in_cnt ? 0 : in_rr + 1;
-    const fdt_frag_meta_t *line = cfg->in_mcache[i] + (in_seq[i] & (cfg->in_depth[i] - 1));
-    /* the line 16 frags ahead: a tile that reads every frag's line (round
-       robin over tiles, fd_verify.c:46) streams the whole mcache */
-    __builtin_prefetch(cfg->in_mcache[i] + ((in_seq[i] + 16) & (cfg->in_depth[i] - 1)));
-    const uint64_t seq_found = ld_acq(&line->seq);
-    const int64_t diff = (int64_t)(in_seq[i] - seq_found);
-    if (diff) {                                     /* caught up, or overrun (fd_mux.c:595-609) */
-      if (diff < 0) {
-        st.overrun_polling += (uint64_t)(-diff);
-        M.link_in[i].overrun_polling_count++;
-        M.link_in[i].overrun_polling_frag_count += (uint64_t)(-diff);
-        in_seq[i] = seq_found;
-        mx.lap(M.loop_overrun_polling_duration_ticks);
-      } else {
-        mx.lap(M.loop_caught_up_duration_ticks);
-      }
-      continue;
-    }
-    uint64_t sig = line->sig;
-    st.in_frags++;
-    if (cb->before_frag) {
-      int filter = 0;
-      cb->before_frag(ctx, i, seq_found, sig, &filter);
-      if (filter) {
-        if (!copy) cr_filt += (uint64_t)(cr_avail < cr_max);
-        in_seq[i]++;
-        st.filtered_before++;
-        mx.lap(M.loop_filter_before_fragment_duration_ticks);
-        continue;
-      }
-    }
-    std::atomic_thread_fence(std::memory_order_acquire);
-    uint64_t chunk = line->chunk, sz = line->sz;
-    const uint64_t ctl = line->ctl, tsorig = line->tsorig;
-    std::atomic_thread_fence(std::memory_order_acquire);
-    const uint64_t seq_test = ld_acq(&line->seq);
-    int filter = 0;
-    if (cb->during_frag) cb->during_frag(ctx, i, seq_found, sig, chunk, sz, &filter);
-    /* the reference checks the seq read before during_frag (fd_mux.c:641-655);
-       the quic -> verify link has no backpressure, so the payload copy is
-       checked too */
-    const uint64_t seq_test2 = ld_acq(&line->seq);
-    if (seq_test != seq_found || seq_test2 != seq_found) {
-      st.overrun_reading++;
-      M.link_in[i].overrun_reading_count++;
-      in_seq[i] = seq_test2;
-      mx.lap(M.loop_overrun_reading_duration_ticks);
-      continue;
-    }
-    uint64_t out_sz = sz, out_tsorig = tsorig;
-    if (!filter && cb->after_frag) cb->after_frag(ctx, i, seq_found, &sig, &chunk, &out_sz, &out_tsorig, &filter, &mux);
-    if (filter) {
-      if (!copy) cr_filt += (uint64_t)(cr_avail < cr_max);
-      st.filtered_after++;
-    } else if (!(flags & FDT_MUX_FLAG_MANUAL_PUBLISH)) {
-      fdt_mux_publish(&mux, sig, chunk, out_sz, ctl, out_tsorig, (uint32_t)now_ns());
-      st.published++;
-    }
-    in_seq[i]++;
-    /* fd_mux.c:690-697: PublishedCount/Size or FilteredCount/Size of the in link */
-    fdt_link_in_metrics_t &L = M.link_in[i];
-    if (filter) { L.filtered_count++; L.filtered_size_bytes += sz; }
-    else        { L.published_count++; L.published_size_bytes += sz; }
-    if (mx.out) {
-      mx.lap(filter ? M.loop_filter_after_fragment_duration_ticks : M.loop_finish_duration_ticks);
-      fdt_histf_sample(filter ? &M.fragment_filtered_size_bytes : &M.fragment_handled_size_bytes, sz);
-    }
-  }
-  /* halting (fd_mux.c:701-714): every exposed frag counts as consumed */
-  for (uint64_t i = 0; i < in_cnt; i++) if (cfg->in_fseq[i]) st_rel(cfg->in_fseq[i], in_seq[i]);
-  mx.write();
-  if (stats_out) *stats_out = st;
-  return 0;
+  if (!cfg || !cb) return -1;
+  if (is_vmux_callbacks(cb)) return vmux_loop(cfg, ctx, halt, stats_out);
+  CbHooks h{cb, ctx};
+  return mux_loop(cfg, h, halt, stats_out);
 }
 
 }  // extern "C"
@@ -825,6 +902,47 @@ void vm_after_credit(void *ctx, fdt_mux_context_t *mux, int *opt_poll_in) {
   if (due || stuck) t->submit();
   if (!*opt_poll_in || t->error || !t->can_take()) { *opt_poll_in = 0; return; }
   if (!t->room_ok && !(t->room_ok = t->room(mux))) { *opt_poll_in = 0; t->st.backpressure++; }
+}
+
+/* ... or straight into the verify tile's callbacks, inlined into its own
+   instance of the loop, with the round-robin filter applied as a skip */
+struct VmHooks {
+  fdgpu_vmux *t;
+  void metrics_write() {}
+  void during_housekeeping() {}
+  void before_credit(fdt_mux_context_t *) {}
+  void after_credit(fdt_mux_context_t *m, int *p) { vm_after_credit(t, m, p); }
+  /* seqs of link i from seq on that another tile of the round robin takes */
+  uint64_t skip(uint64_t, uint64_t seq) const {
+    const uint64_t cnt = t->cfg.round_robin_cnt;
+    if (cnt == 1) return 0;
+    const uint64_t r = t->rr_mask ? (seq & t->rr_mask) : seq % cnt, idx = t->cfg.round_robin_idx;
+    return idx >= r ? idx - r : idx + cnt - r;
+  }
+  void skipped(uint64_t, uint64_t seq, uint64_t k) {
+    t->st.in_frags += k;
+    t->st.filtered_rr += k;
+    for (uint64_t j = 0; j < k; j++) t->log(seq + j, FDGPU_VTILE_LOG_FILTERED);
+  }
+  bool has_before_frag() const { return true; }
+  void before_frag(uint64_t i, uint64_t seq, uint64_t sig, int *f) { vm_before_frag(t, i, seq, sig, f); }
+  void during_frag(uint64_t i, uint64_t seq, uint64_t sig, uint64_t chunk, uint64_t sz, int *f) {
+    vm_during_frag(t, i, seq, sig, chunk, sz, f);
+  }
+  void after_frag(uint64_t i, uint64_t seq, uint64_t *sig, uint64_t *chunk, uint64_t *sz, uint64_t *tsorig, int *f,
+                  fdt_mux_context_t *m) {
+    vm_after_frag(t, i, seq, sig, chunk, sz, tsorig, f, m);
+  }
+};
+
+bool is_vmux_callbacks(const fdt_mux_callbacks_t *cb) {
+  return cb->before_frag == vm_before_frag && cb->during_frag == vm_during_frag && cb->after_frag == vm_after_frag &&
+         cb->after_credit == vm_after_credit && !cb->before_credit && !cb->during_housekeeping && !cb->metrics_write;
+}
+
+int vmux_loop(const fdt_mux_cfg_t *cfg, void *ctx, const volatile uint64_t *halt, fdt_mux_stats_t *stats_out) {
+  VmHooks h{(fdgpu_vmux *)ctx};
+  return mux_loop(cfg, h, halt, stats_out);
 }
 
 }  // namespace

@@ -57,7 +57,7 @@ static int nv_poll_io(void *ctx, int64_t ticket, int8_t *codes, uint64_t *tags, 
   nv_t *v = (nv_t *)ctx;
   const uint64_t n = v->cnt[ticket % NV_RING];
   fdgpu_frag_io_t const *f = v->sz[ticket % NV_RING];
-  for (uint64_t i = 0; i < n; i++) { tags[i] = nv_tag++; out_szs[i] = (uint16_t)(f[i].sz + 32u); }
+  for (uint64_t i = 0; i < n; i++) { tags[i] = __atomic_fetch_add(&nv_tag, 1, __ATOMIC_RELAXED); out_szs[i] = (uint16_t)(f[i].sz + 32u); }
   return nv_poll(ctx, ticket, codes, blocking);
 }
 
