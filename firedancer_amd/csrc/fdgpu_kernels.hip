@@ -234,8 +234,11 @@ FDG_DEV void dsm_k(ge_p2 &acc2, uint32_t (&kd)[KD_WORDS], const uint32_t *wsl, u
 /* [S]B by the fixed-base comb: S (< L, or 0 for rejected lanes) in signed
    radix 2^W; one mixed addition per digit from table i; each entry (one
    128-B line, random across the 67-MB table) is loaded one digit ahead of
-   its use so the load latency hides behind the previous addition. */
-FDG_DEV void comb_sb(ge_p3 &acc, const uint32_t (&S)[8], const uint32_t *__restrict__ btab) {
+   its use so the load latency hides behind the previous addition.  [lo, hi)
+   sums only the digits of tables lo..hi-1 (the two-lane kernel splits the
+   comb over a pair: 2 + 2 x 7 additions instead of 15 per lane). */
+FDG_DEV void comb_sb(ge_p3 &acc, const uint32_t (&S)[8], const uint32_t *__restrict__ btab, uint32_t lo = 0,
+                     uint32_t hi = BC_NDIG) {
   constexpr int NW = COMB_WORDS(BC_W, BC_NDIG), SLOT = COMB_SLOT(BC_W);
   uint32_t dg[NW];
   sc_recode_comb<(int)BC_W, (int)BC_NDIG>(dg, S);
@@ -255,12 +258,14 @@ FDG_DEV void comb_sb(ge_p3 &acc, const uint32_t (&S)[8], const uint32_t *__restr
     }
   };
   uint32_t qa[32], qb[32];
+#pragma unroll 1
+  for (uint32_t i = 0; i < lo; i++) (void)next_digit();
   int d = next_digit();
-  load_entry(qa, 0, d);
+  load_entry(qa, lo, d);
   /* the first digit's entry is the starting point (no addition to O) */
   {
     const int dn = next_digit();
-    load_entry(qb, 1, dn);
+    load_entry(qb, lo + 1, dn);
     ge_niels_regs_to_p3(acc, qa, d < 0);
 #pragma unroll
     for (int w = 0; w < 32; w++) qa[w] = qb[w];
@@ -268,9 +273,9 @@ FDG_DEV void comb_sb(ge_p3 &acc, const uint32_t (&S)[8], const uint32_t *__restr
   }
   ge_p1p1 t;
 #pragma unroll 1
-  for (uint32_t i = 1; i < BC_NDIG; i++) {
+  for (uint32_t i = lo + 1; i < hi; i++) {
     const int dn = next_digit();
-    if (i + 1 < BC_NDIG) load_entry(qb, i + 1, dn);
+    if (i + 1 < hi) load_entry(qb, i + 1, dn);
     ge_add_niels_regs(t, acc, qa, d < 0);
     ge_p1p1_to_p3(acc, t);
 #pragma unroll
@@ -766,9 +771,18 @@ fdgpu_verify_pair_kernel(const uint8_t *__restrict__ arena, const fdgpu_sig_desc
     hs_wscalar(w, hs.v, hs.v_neg, S);
 #pragma unroll
     for (int j = 0; j < 8; j++) w[j] = half ? w[j] : S[j];
-    ge_p3 WB;
-    comb_sb(WB, w, btab);
-    ge_cached c; ge_p3_to_cached(c, WB);
+    /* the A lane sums the comb's low tables, the R lane its high ones; the
+       halves are exchanged and added */
+    ge_p3 WB, WBo;
+    comb_sb(WB, w, btab, rl ? BC_NDIG / 2u : 0u, rl ? BC_NDIG : BC_NDIG / 2u);
+    fe_xchg_pair(WBo.X, WB.X);
+    fe_xchg_pair(WBo.Y, WB.Y);
+    fe_xchg_pair(WBo.Z, WB.Z);
+    fe_xchg_pair(WBo.T, WB.T);
+    ge_cached c; ge_p3_to_cached(c, WBo);
+    ge_p1p1 tw; ge_add_cached(tw, WB, c, false);
+    ge_p1p1_to_p3(WB, tw);
+    ge_p3_to_cached(c, WB);
     if (!rl) atab_store(wsl, FDGPU_WS_SB, c);
   }
   if (full && !rl) {
