@@ -421,6 +421,10 @@ TILE_RUNS = (  # name, verify tiles, quic links (producers), offered txn/s (-1: 
 # before the tiles start, so their links hold the whole stream
 TILE_DEPTH_LG_PACED, TILE_DEPTH_LG_PREFILL, TILE_PACED_REPS = 14, 21, 4
 TILE_BATCH, TILE_INFLIGHT = 16384, 8   # txns per GPU batch, batches in flight per tile
+# tile engines: FDGPU_FLAG_PAIR_AUTO -- the two-lane verify while an engine's batches leave the GPU idle
+# (paced: p50 batch latency 1.13 vs 1.40 ms at 12 M txn/s, 1.47 vs 1.81 at 24 M; capacity unchanged;
+# profiles/r04/tile_pair.md)
+TILE_PAIR = 2
 # multi-signature frags: a batch also closes at this many signatures by the frag-size bound the tile sees
 # (~9.5 per cfg3 frag for ~6.5 real): ~2.6 K cfg3 txns, so 8 batches in flight are ~1.3 ms of GPU work
 # (49152: 1-tile p99 batch 5.8 ms, 2 tiles 59-65 M sig/s; 24576: 3.0 ms, 67-70 M; profiles/r04/tile_run_order.md)
@@ -445,6 +449,7 @@ def tile_cmd(device, cpus, npz, out, runs=TILE_RUNS, multi=0):
            "--multi", str(int(multi)), "--producers-same-as-tiles", "1", "--depth-lg", str(TILE_DEPTH_LG_PREFILL),
            "--depth-lg-paced", str(TILE_DEPTH_LG_PACED), "--paced-reps", str(TILE_PACED_REPS),
            "--wait-us", "200", "--pin", "1", "--hw-queues", str(TILE_HW_QUEUES), "--reps", str(TILE_REPS),
+           "--pair", str(TILE_PAIR),
            "--payload-npz", npz, "--device", str(device), "--sweep", sweep, "--out", out]
     if multi:
         cmd += ["--batch-sig-max", str(TILE_CFG3_SIG_MAX)]

@@ -80,6 +80,7 @@ struct Slot {
   uint32_t *d_ws = nullptr;   /* this slot's workspace: slots run concurrently on their own streams; */
   uint64_t ws_sig = 0;        /* sized on demand to the largest batch the slot has carried */
   int64_t ticket = -1;      /* -1: free */
+  uint64_t k_sigs = 0;      /* signatures (the launch's bound) of its verify: FDGPU_FLAG_PAIR_AUTO's load */
   bool staged = false;      /* reserved by fdgpu_stage_acquire, not yet submitted */
   bool held = false;        /* polled with fdgpu_poll_keep, awaiting fdgpu_release */
   uint64_t txn_cnt = 0;
@@ -400,21 +401,27 @@ static uint32_t kflags(const fdgpu_engine_t *e) {
          ((e->cfg.flags & FDGPU_FLAG_PAIR) && !(e->cfg.flags & FDGPU_FLAG_KEY_CACHE) ? FDGPU_FLAG_KPAIR : 0u);
 }
 
-/* FDGPU_FLAG_PAIR_AUTO: a ring batch of at most this many signatures takes
-   the two-lane kernel while at most one other batch of the engine is still
-   running on the device (tools/pair_probe.py: 0.75x the one-lane kernel's
-   time up to 8 K signatures, 0.77x at 16 K, 0.82x at 32 K; 1.24x at 64 K,
-   where the chip fills) */
-static constexpr uint64_t FDGPU_PAIR_AUTO_MAX = 32768;
+/* FDGPU_FLAG_PAIR_AUTO: a ring batch takes the two-lane kernel while the
+   signatures of the engine's running batches and its own (launch bounds:
+   a gathered batch's count is known only on the device), two lanes each,
+   leave part of the chip's resident lanes idle (256 CUs x 4 SIMDs x 2 waves
+   x 64 = 131,072): a wave's lifetime is then the batch's latency
+   (profiles/r04/pair_rocprof.txt: 0.73x the one-lane kernel's time at 4-16 K
+   signatures, 0.76x at 32 K; pair_probe.jsonl: 1.2x at 64 K, where two lanes
+   per signature fill the chip).  A loaded engine keeps the one-lane kernel,
+   which does ~1.4x less work per signature. */
+static constexpr uint64_t FDGPU_PAIR_AUTO_SIGS = 49152;
 
-/* the kernel flags of a ring batch of n_sig signatures (ring_mu held) */
-static uint32_t ring_kflags(const fdgpu_engine_t *e, uint64_t n_sig) {
+/* the kernel flags of slot s's ring batch of n_sig signatures (ring_mu held) */
+static uint32_t ring_kflags(fdgpu_engine_t *e, Slot *s, uint64_t n_sig) {
   uint32_t f = kflags(e);
-  if ((e->cfg.flags & FDGPU_FLAG_PAIR_AUTO) && !(f & FDGPU_FLAG_KCACHE) && n_sig <= FDGPU_PAIR_AUTO_MAX) {
-    uint32_t busy = 0;
+  s->k_sigs = n_sig;
+  if ((e->cfg.flags & FDGPU_FLAG_PAIR_AUTO) && !(f & FDGPU_FLAG_KCACHE) && n_sig <= FDGPU_PAIR_AUTO_SIGS) {
+    uint64_t load = n_sig;
     for (const auto &c : e->slots)
-      busy += c.ticket >= 0 && !(e->flag_poll && __atomic_load_n(c.h_flag, __ATOMIC_ACQUIRE) == c.flag_seq);
-    if (busy <= 1) f |= FDGPU_FLAG_KPAIR;
+      if (&c != s && c.ticket >= 0 && !(e->flag_poll && __atomic_load_n(c.h_flag, __ATOMIC_ACQUIRE) == c.flag_seq))
+        load += c.k_sigs;
+    if (load <= FDGPU_PAIR_AUTO_SIGS) f |= FDGPU_FLAG_KPAIR;
   }
   return f;
 }
@@ -572,7 +579,7 @@ static int64_t submit_slot(fdgpu_engine_t *e, Slot *s, uint64_t arena_sz, fdgpu_
      overlap each other on the GPU (a 64K-signature batch fills only half of
      the resident wave slots) */
   int rc = enqueue_verify(e, s->d_arena, s->d_sigs, perm ? s->d_perm : nullptr, (uint64_t)ns, s->d_txns, txn_cnt,
-                          s->d_sig_codes, s->d_txn_codes, s->stream, s->d_ws, ring_kflags(e, (uint64_t)ns));
+                          s->d_sig_codes, s->d_txn_codes, s->stream, s->d_ws, ring_kflags(e, s, (uint64_t)ns));
   if (rc) return rc;
   if (txn_cnt) HIPCHK(hipMemcpyAsync(s->h_codes, s->d_txn_codes, txn_cnt, hipMemcpyDeviceToHost, s->stream), FDGPU_ERR_DEVICE);
   ++s->flag_seq;
@@ -836,7 +843,7 @@ int64_t fdgpu_submit_frags(fdgpu_engine_t *e, uint8_t const *arena, uint64_t are
                                   s->d_sig0, s->d_blocktot, s->d_n_sig, s->d_sigs, s->d_txns, s->stream),
            FDGPU_ERR_DEVICE);
     HIPCHK(fdgpu_launch_verify_sigs(s->d_arena, s->d_sigs, (uint32_t)bound, nullptr, e->d_btab, s->d_ws, s->d_sig_codes,
-                                    ring_kflags(e, bound), s->stream, s->d_n_sig, e->resident_blocks, e->kc_seed),
+                                    ring_kflags(e, s, bound), s->stream, s->d_n_sig, e->resident_blocks, e->kc_seed),
            FDGPU_ERR_DEVICE);
     HIPCHK(fdgpu_launch_frag_finish(s->d_txns, (uint32_t)n, s->d_sig_codes, s->d_txn_sz, s->d_fx, s->d_txn_out,
                                     (int8_t *)s->d_tr, s->d_tr + tr_base, s->stream),
@@ -958,7 +965,7 @@ int64_t fdgpu_submit_frags_io(fdgpu_engine_t *e, fdgpu_frag_io_t const *fio, uin
                                           s->d_n_sig, s->stream),
            FDGPU_ERR_DEVICE);
     HIPCHK(fdgpu_launch_verify_sigs(s->d_arena, s->d_sigs, (uint32_t)bound, nullptr, e->d_btab, s->d_ws, s->d_sig_codes,
-                                    ring_kflags(e, bound), s->stream, s->d_n_sig, e->resident_blocks, e->kc_seed, zero_cnt),
+                                    ring_kflags(e, s, bound), s->stream, s->d_n_sig, e->resident_blocks, e->kc_seed, zero_cnt),
            FDGPU_ERR_DEVICE);
     HIPCHK(fdgpu_launch_frag_finish_io(s->d_txns, (uint32_t)n, s->d_sig_codes, s->d_txn_sz, d_fx, s->d_txn_out,
                                        s->d_arena, hash_seed, out_dev, (int8_t *)s->d_trh, (uint64_t *)(s->d_trh + cb),

@@ -130,9 +130,10 @@ typedef struct {
                                       that leave the GPU's wave slots idle (small / latency-bound batches),
                                       ~1.4x the work per signature, so slower on batches that fill the GPU;
                                       same codes.  Ignored with FDGPU_FLAG_KEY_CACHE */
-#define FDGPU_FLAG_PAIR_AUTO 32u  /* the FDGPU_FLAG_PAIR kernel for a ring batch of <= 32 K signatures while at
-                                      most one other batch of the engine is running (the GPU is mostly idle:
-                                      latency); the one-lane kernel otherwise.  Same codes either way */
+#define FDGPU_FLAG_PAIR_AUTO 32u  /* the FDGPU_FLAG_PAIR kernel for a ring batch while it and the engine's
+                                      running batches hold <= 48 K signatures (launch bounds): the GPU has idle
+                                      wave slots, latency is a wave's lifetime; the one-lane kernel otherwise.
+                                      Same codes either way */
 
 /* Status codes of the engine API (distinct from verify codes). */
 #define FDGPU_OK            ( 0)

@@ -79,6 +79,9 @@ def make_parser():
     ap.add_argument("--batch-sig-max", type=int, default=0,
                     help="(mux tile) signatures per batch, counted by the frag-size bound the tile sees "
                          "(0: 12 x batch): bounds the GPU work, and the latency, of multi-signature batches")
+    ap.add_argument("--pair", type=int, default=0,
+                    help="(mux tile) verify kernel: 0 one lane per signature, 1 two lanes (FDGPU_FLAG_PAIR), "
+                         "2 two lanes while the engine is otherwise idle (FDGPU_FLAG_PAIR_AUTO)")
     ap.add_argument("--tiles-per-engine", type=int, default=1,
                     help="verify tiles sharing one engine (its ring slots): a process's HIP streams are hardware "
                          "queues, and past ~20 of them the GPU's scheduler time-slices the queues")
@@ -397,7 +400,7 @@ def engine_pool(args, n, batch, inflight, device):
     opening and closing engines keeps creating HIP streams -- after a few
     dozen, new streams share hardware queues and batches of one tile
     serialise behind another's (a run after a 3-tile run took 2.5x as long
-    per batch with the same kernel durations, profiles/r04/tile_stream_reuse.md)."""
+    per batch with the same kernel durations, profiles/r04/tile_run_order.md)."""
     key = (batch, inflight, device)
     pool = _POOL.setdefault(key, [])
     frag_bytes = (tile.TPU_DCACHE_MTU + 63) // 64 * 64
@@ -405,7 +408,8 @@ def engine_pool(args, n, batch, inflight, device):
     while len(pool) < n:
         k = len(pool)
         e = fa.VerifyEngine(device if device is not None else k % args.gpus, max_txn=batch, max_sig=batch * 12,
-                            max_arena=batch * frag_bytes, ring_depth=inflight)
+                            max_arena=batch * frag_bytes, ring_depth=inflight, pair=args.pair == 1,
+                            pair_auto=args.pair == 2)
         if getattr(args, "reserve", 1):
             e.reserve()      # every slot sized for the largest batch now, not inside the run (as a tile's init does)
         pool.append(e)
