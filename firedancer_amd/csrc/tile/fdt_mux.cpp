@@ -442,7 +442,8 @@ struct fdgpu_vmux {
   uint64_t cur_fp = 0, cur_sc = 0, cur_tag = 0;   /* gpu_parse: its peeked footprint, signature count, tag */
   std::vector<VBatch> storage;
   std::vector<VBatch *> pool;
-  std::deque<VBatch *> inflight;
+  std::deque<VBatch *> inflight;          /* submitted, in ingest order, until published */
+  uint32_t busy = 0;                      /* ... of which still on the verifier (not polled done) */
   VBatch *open = nullptr;
   std::vector<uint32_t> pub_chunk;        /* chunk of each recently published out seq */
   uint64_t pub_mask = 0, published_total = 0;
@@ -497,26 +498,38 @@ struct fdgpu_vmux {
     return w + FRAG_CHUNKS <= tail;
   }
 
+  /* a non-blocking poll of one submitted batch: 1 done (its results are
+     in the batch, its verifier slot is free), 0 pending, -1 error */
+  int poll_one(VBatch *b, int *poll_in) {
+    const uint64_t p0 = now_ns();
+    const int rc = gather ? ver.poll_io(ver.ctx, b->ticket, b->codes.data(), b->tags.data(), b->out_szs.data(), 0)
+                   : gpu_parse ? ver.poll_frags(ver.ctx, b->ticket, b->codes.data(), b->trailers.data(), 0)
+                               : ver.poll(ver.ctx, b->ticket, b->codes.data(), 0);
+    const uint64_t p1 = now_ns(), dp = p1 - p0;
+    st.poll_ns += dp;
+    st.polls++;
+    if (rc == FDGPU_PENDING) return 0;
+    st.poll_done_ns += dp;
+    st.batch_gpu_ns += p1 - b->t_submit;
+    if (rc != FDGPU_OK) { error = rc; *poll_in = 0; return -1; }
+    b->done = true;
+    busy--;
+    for (uint32_t k : b->lost) b->codes[k] = (int8_t)FDGPU_CODE_LAPPED;
+    return 1;
+  }
+
   /* tag, tcache, publish -- strictly in ingest order (fd_verify.h:45-89,
-     fd_verify.c:138-147) */
+     fd_verify.c:138-147).  Batches finish on the GPU out of order (several
+     run at once on their own streams): every finished one is polled, which
+     frees its verifier slot for the next batch, while publishing waits for
+     the oldest. */
   void resolve(fdt_mux_context_t *mux, int *poll_in) {
+    if (busy > 1)
+      for (size_t j = 1; j < inflight.size(); j++)
+        if (!inflight[j]->done && poll_one(inflight[j], poll_in) < 0) return;
     while (!inflight.empty()) {
       VBatch *b = inflight.front();
-      if (!b->done) {
-        const uint64_t p0 = now_ns();
-        const int rc = gather ? ver.poll_io(ver.ctx, b->ticket, b->codes.data(), b->tags.data(), b->out_szs.data(), 0)
-                       : gpu_parse ? ver.poll_frags(ver.ctx, b->ticket, b->codes.data(), b->trailers.data(), 0)
-                                   : ver.poll(ver.ctx, b->ticket, b->codes.data(), 0);
-        const uint64_t dp = now_ns() - p0;
-        st.poll_ns += dp;
-        st.polls++;
-        if (rc == FDGPU_PENDING) return;
-        st.poll_done_ns += dp;
-        st.batch_gpu_ns += now_ns() - b->t_submit;
-        if (rc != FDGPU_OK) { error = rc; *poll_in = 0; return; }
-        b->done = true;
-        for (uint32_t k : b->lost) b->codes[k] = (int8_t)FDGPU_CODE_LAPPED;
-      }
+      if (!b->done && poll_one(b, poll_in) <= 0) return;
       const uint64_t t_pub = now_ns();
       struct Acc { uint64_t &ns; uint64_t t0; ~Acc() { ns += now_ns() - t0; } } acc{st.publish_ns, t_pub};
       const uint32_t tspub = (uint32_t)t_pub;
@@ -700,7 +713,7 @@ struct fdgpu_vmux {
     struct Acc { uint64_t &ns; uint64_t t0; ~Acc() { ns += now_ns() - t0; } } acc{st.submit_ns, s0};
     if (gather && lap_margin != ~0ull) lap_guard(*open);    /* also while the batch fills or waits for a slot */
     if (!open->closed && s0 - open->t_first < cfg.batch_wait_ns) return;
-    if (inflight.size() >= cfg.inflight_max) return;
+    if (busy >= cfg.inflight_max) return;
     int64_t t;
     if (gather) {
       const size_t n = open->cnt;
@@ -721,6 +734,7 @@ struct fdgpu_vmux {
     open->t_submit = now_ns();
     st.batch_fill_ns += open->t_submit - open->t_first;
     inflight.push_back(open);
+    busy++;
     open = nullptr;
     st.batches++;
   }
@@ -951,7 +965,7 @@ extern "C" {
 
 uint64_t fdgpu_vmux_dcache_data_sz(uint64_t cr_max, uint32_t batch_txn_max, uint32_t inflight_max) {
   if (!inflight_max) inflight_max = 2;
-  return (cr_max + (uint64_t)(inflight_max + 1) * batch_txn_max + 2) * FRAG_CHUNKS * FDT_CHUNK_SZ;
+  return (cr_max + (2 * (uint64_t)inflight_max + 1) * batch_txn_max + 2) * FRAG_CHUNKS * FDT_CHUNK_SZ;
 }
 
 fdgpu_vmux_t *fdgpu_vmux_new(const fdgpu_vmux_cfg_t *cfg, fdgpu_verifier_t ver) {
@@ -1018,7 +1032,7 @@ fdgpu_vmux_t *fdgpu_vmux_new(const fdgpu_vmux_cfg_t *cfg, fdgpu_verifier_t ver) 
   while (n < c.cr_max) n <<= 1;
   t->pub_chunk.assign(n, 0);
   t->pub_mask = n - 1;
-  t->storage.resize(c.inflight_max + 1);
+  t->storage.resize(2 * (uint64_t)c.inflight_max + 1);    /* on the GPU, done but not yet published, open */
   for (auto &b : t->storage) {
     b.codes.resize(c.batch_txn_max);
     b.txns.reserve(c.batch_txn_max);

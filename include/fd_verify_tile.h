@@ -480,18 +480,23 @@ int  fdt_mux_run( fdt_mux_cfg_t const * cfg, fdt_mux_callbacks_t const * callbac
                    (fdt_txn_peek) to reserve the trailer, and the frag goes
                    to the batch as {payload, trailer place}: the GPU parses,
                    and the trailer is copied in at publish;
-     after_credit  poll in-flight batches and resolve completed ones strictly
-                   in ingest order (tcache query -> verify code -> insert ->
-                   fdt_mux_publish of the frag where it already lies), while
-                   credits last (opt_poll_in = 0 when they run out); submit
-                   the open batch when full / after batch_wait_ns; stop
-                   polling the ins (opt_poll_in = 0) while the out dcache has
-                   no room for one more frag.
+     after_credit  poll in-flight batches (every one the verifier still
+                   holds: a finished batch frees its verifier slot at once,
+                   whatever its place in line) and resolve completed ones
+                   strictly in ingest order (tcache query -> verify code ->
+                   insert -> fdt_mux_publish of the frag where it already
+                   lies), while credits last (opt_poll_in = 0 when they run
+                   out); submit the open batch when full / after
+                   batch_wait_ns while fewer than inflight_max batches are on
+                   the verifier (up to inflight_max more may wait, finished,
+                   for their turn to publish); stop polling the ins
+                   (opt_poll_in = 0) while the out dcache has no room for one
+                   more frag.
    Out-dcache accounting: the region from the oldest frag that may still be
    read -- published within the last cr_max - cr_avail (the mux's exposed
    count) or reserved by a batch not yet resolved -- to the write cursor is
    live; a frag is copied in only if a maximal one fits before that region.
-   Size the dcache for cr_max + (inflight_max + 1) * batch_txn_max frags of
+   Size the dcache for cr_max + (2 inflight_max + 1) * batch_txn_max frags of
    FDT_TPU_DCACHE_MTU (fdgpu_vmux_dcache_data_sz) or the tile stalls early. */
 typedef struct {
   uint64_t        in_cnt;

@@ -314,18 +314,26 @@ def run_once_mux(args, ps, arena, offs, sizes, n_sig, modes, tiles_n, batch, inf
         reps = max(1, getattr(args, "paced_reps", 1))
         feeds = [(np.tile(offs[j::P], reps), np.tile(sizes[j::P], reps)) for j in range(P)]
     n_total = sum(len(f[0]) for f in feeds)
+
+    def start_tiles():
+        keep = os.sched_getaffinity(0)
+        for k, vm in enumerate(vms):
+            if args.pin:
+                os.sched_setaffinity(0, {cpus[(P + k) % len(cpus)]})
+            vm.start()
+        os.sched_setaffinity(0, keep)
+
+    # paced: the tiles are polling before the first frag is published (a producer that starts first
+    # laps a tile still starting up: ~4 x the link depth lost in one run of r04k / r04n)
+    if not prefill:
+        start_tiles()
     start = time.perf_counter()
     prods = [start_producer(args, inls[j], arena, feeds[j][0], feeds[j][1], 0.0 if prefill else rate / P, cpus, j)
              for j in range(P)]
     if prefill:
         joined = [pr.join() for pr in prods]
         start = time.perf_counter()
-    keep = os.sched_getaffinity(0)
-    for k, vm in enumerate(vms):
-        if args.pin:
-            os.sched_setaffinity(0, {cpus[(P + k) % len(cpus)]})
-        vm.start()
-    os.sched_setaffinity(0, keep)
+        start_tiles()
     # done: every frag's outcome final -- or, when frags were lost to the
     # producers (lapped: the tiles log those too; skipped by the mux while it
     # lagged: never seen), the producers finished and the tiles sit idle with
