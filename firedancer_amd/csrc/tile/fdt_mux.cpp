@@ -449,6 +449,7 @@ struct fdgpu_vmux {
   uint64_t pub_mask = 0, published_total = 0;
   int error = 0;
   uint32_t calls = 0;                     /* after_credit calls (rate-limits verifier polls) */
+  uint64_t due_tsc = 0, stall_max_tick = 0;   /* the every-32nd call's time stamp counter, the longest gap */
   fdgpu_vtile_stats_t st{};
   std::vector<uint64_t> lat;
   fdgpu_link_t links[FDT_MUX_IN_MAX] = {};   /* gather: the in mcaches, re-checked by the device after its read */
@@ -710,7 +711,10 @@ struct fdgpu_vmux {
   void submit() {
     if (!open || !open->cnt) return;
     const uint64_t s0 = now_ns();
-    struct Acc { uint64_t &ns; uint64_t t0; ~Acc() { ns += now_ns() - t0; } } acc{st.submit_ns, s0};
+    struct Acc {
+      uint64_t &ns, &mx; uint64_t t0;
+      ~Acc() { const uint64_t d = now_ns() - t0; ns += d; mx = std::max(mx, d); }
+    } acc{st.submit_ns, st.submit_max_ns, s0};
     if (gather && lap_margin != ~0ull) lap_guard(*open);    /* also while the batch fills or waits for a slot */
     if (!open->closed && s0 - open->t_first < cfg.batch_wait_ns) return;
     if (busy >= cfg.inflight_max) return;
@@ -752,7 +756,7 @@ struct fdgpu_vmux {
 
 namespace {
 
-void vm_before_frag(void *ctx, uint64_t in_idx, uint64_t seq, uint64_t sig, int *opt_filter) {
+__attribute__((always_inline)) inline void vm_before_frag(void *ctx, uint64_t in_idx, uint64_t seq, uint64_t sig, int *opt_filter) {
   (void)in_idx; (void)sig;
   auto *t = (fdgpu_vmux *)ctx;
   t->st.in_frags++;
@@ -764,7 +768,7 @@ void vm_before_frag(void *ctx, uint64_t in_idx, uint64_t seq, uint64_t sig, int 
   }
 }
 
-void vm_during_frag(void *ctx, uint64_t in_idx, uint64_t seq, uint64_t sig, uint64_t chunk, uint64_t sz,
+__attribute__((always_inline)) inline void vm_during_frag(void *ctx, uint64_t in_idx, uint64_t seq, uint64_t sig, uint64_t chunk, uint64_t sz,
                     int *opt_filter) {
   (void)sig;
   auto *t = (fdgpu_vmux *)ctx;
@@ -797,7 +801,7 @@ void vm_during_frag(void *ctx, uint64_t in_idx, uint64_t seq, uint64_t sig, uint
   t->cur_ok = true;
 }
 
-void vm_after_frag(void *ctx, uint64_t in_idx, uint64_t seq, uint64_t *opt_sig, uint64_t *opt_chunk,
+__attribute__((always_inline)) inline void vm_after_frag(void *ctx, uint64_t in_idx, uint64_t seq, uint64_t *opt_sig, uint64_t *opt_chunk,
                    uint64_t *opt_sz, uint64_t *opt_tsorig, int *opt_filter, fdt_mux_context_t *mux) {
   (void)in_idx; (void)opt_sig; (void)opt_chunk; (void)mux;
   auto *t = (fdgpu_vmux *)ctx;
@@ -907,10 +911,15 @@ void vm_after_frag(void *ctx, uint64_t in_idx, uint64_t seq, uint64_t *opt_sig, 
    the verifier is polled (an event query) and the partial-batch timer read
    only every 32nd call, or at once when the tile cannot take the next frag
    or is mid-way through publishing a completed batch. */
-void vm_after_credit(void *ctx, fdt_mux_context_t *mux, int *opt_poll_in) {
+__attribute__((always_inline)) inline void vm_after_credit(void *ctx, fdt_mux_context_t *mux, int *opt_poll_in) {
   auto *t = (fdgpu_vmux *)ctx;
   if (t->error) { *opt_poll_in = 0; return; }
   const bool due = (++t->calls & 31u) == 0;
+  if (due) {                                   /* the tile's longest stall between two of these */
+    const uint64_t now = __rdtsc();
+    if (t->due_tsc) t->stall_max_tick = std::max(t->stall_max_tick, now - t->due_tsc);
+    t->due_tsc = now;
+  }
   const bool stuck = t->open ? t->open->closed : t->pool.empty();
   if (due || stuck || (!t->inflight.empty() && t->inflight.front()->done)) t->resolve(mux, opt_poll_in);
   if (due || stuck) t->submit();
@@ -1070,6 +1079,7 @@ fdt_mux_callbacks_t fdgpu_vmux_callbacks(void) {
 
 void fdgpu_vmux_stats(const fdgpu_vmux_t *t, fdgpu_vtile_stats_t *out) {
   *out = t->st;
+  out->stall_max_ns = (uint64_t)((double)t->stall_max_tick / tick_per_ns());
   out->lat_cnt = t->lat.size();
 }
 

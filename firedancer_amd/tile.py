@@ -116,7 +116,8 @@ class VTileStats(c.Structure):
                                           "verify_failed", "dedup", "published", "batches", "sigs",
                                           "backpressure", "lat_cnt", "verify_errors", "ingest_ns", "submit_ns",
                                           "poll_ns", "no_slot_steps", "polls", "poll_done_ns",
-                                          "publish_ns", "batch_fill_ns", "batch_gpu_ns", "lapped", "rescued")]
+                                          "publish_ns", "batch_fill_ns", "batch_gpu_ns", "lapped", "rescued",
+                                          "submit_max_ns", "stall_max_ns")]
 
     def as_dict(self):
         return {n: getattr(self, n) for n, _ in self._fields_}

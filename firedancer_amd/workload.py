@@ -114,6 +114,39 @@ def idle_first(cpus, sample_s=0.2):
     return sorted(cpus, key=lambda c: (b.get(c, 0) - a.get(c, 0), cpus.index(c)))
 
 
+def _l3_of(cpu):
+    """(package, L3 id) of a logical CPU, from /sys (None when unknown)"""
+    base = f"/sys/devices/system/cpu/cpu{cpu}/"
+    try:
+        return (open(base + "topology/physical_package_id").read().strip(),
+                open(base + "cache/index3/id").read().strip())
+    except OSError:
+        return None
+
+
+def same_l3_first(cpus, need):
+    """`cpus` (least busy first, idle_first) reordered so that the first
+    `need` share one L3 (one CCD of an EPYC): the quietest L3 group that has
+    `need` of them, in their order, then the rest.  A tile reads every
+    mcache line its producers write, so a producer and a tile on different
+    CCDs (or sockets) move every line across the fabric.  Unchanged when no
+    group has `need` or the topology is unknown."""
+    groups = {}
+    for rank, c in enumerate(cpus):
+        groups.setdefault(_l3_of(c), []).append((rank, c))
+    best = None
+    for key, members in groups.items():
+        if key is None or len(members) < need:
+            continue
+        score = sum(r for r, _ in members[:need])          # lower: quieter (earlier in idle order)
+        if best is None or score < best[0]:
+            best = (score, [c for _, c in members[:need]])
+    if best is None:
+        return list(cpus)
+    head = best[1]
+    return head + [c for c in cpus if c not in head]
+
+
 def physical_cpus(limit=BOX_CPU_SHARE):
     """One logical CPU per physical core among the CPUs this process may run
     on (SMT siblings skipped; /sys topology), at most `limit`: the CPU
