@@ -277,7 +277,7 @@ def latency_and_pcie(eng, arena, txns, batch, nbatches, pin_cpu=None):
             "pcie_inclusive_registered_sigs_per_s_per_gpu": round(pcie_reg, 1)}
 
 
-def latency_frag_io(eng, arena, txns, ref_codes, batch, nbatches, pin_cpu=None, views_n=4):
+def latency_frag_io(eng, arena, txns, ref_codes, batch, nbatches, pin_cpu=None, views_n=4, keep_raw=False):
     """p50/p99 submit -> results-on-host latency of the verify tile's own
     path, gathered frag batches (fdgpu_submit_frags_io): `batch` raw payloads
     at 64-B chunk offsets of a registered "in dcache", read there by the
@@ -350,11 +350,14 @@ def latency_frag_io(eng, arena, txns, ref_codes, batch, nbatches, pin_cpu=None, 
 
     def pct(x, q):
         return round(float(np.percentile(x, q)), 3)
-    return {"p50_batch_latency_gathered_ms": pct(lat[:, 0], 50), "p99_batch_latency_gathered_ms": pct(lat[:, 0], 99),
-            "latency_split_gathered_ms": {"submit_p50_p99": [pct(lat[:, 1], 50), pct(lat[:, 1], 99)],
-                                          "rest_p50_p99": [pct(lat[:, 0] - lat[:, 1], 50),
-                                                           pct(lat[:, 0] - lat[:, 1], 99)]},
-            "gathered_codes_equal": ok}
+    out = {"p50_batch_latency_gathered_ms": pct(lat[:, 0], 50), "p99_batch_latency_gathered_ms": pct(lat[:, 0], 99),
+           "latency_split_gathered_ms": {"submit_p50_p99": [pct(lat[:, 1], 50), pct(lat[:, 1], 99)],
+                                         "rest_p50_p99": [pct(lat[:, 0] - lat[:, 1], 50),
+                                                          pct(lat[:, 0] - lat[:, 1], 99)]},
+           "gathered_codes_equal": ok}
+    if keep_raw:
+        out["lat_ms"] = [round(float(x), 4) for x in lat[:, 0]]
+    return out
 
 
 def sync_latency(arena, txns, calls=1000, threads=64):

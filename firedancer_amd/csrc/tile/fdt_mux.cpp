@@ -110,6 +110,7 @@ struct CbHooks {
   void after_credit(fdt_mux_context_t *m, int *p) { if (cb->after_credit) cb->after_credit(ctx, m, p); }
   uint64_t skip(uint64_t, uint64_t) { return 0; }
   void skipped(uint64_t, uint64_t, uint64_t) {}
+  void caught_up(uint64_t) {}
   bool has_before_frag() const { return cb->before_frag != nullptr; }
   void before_frag(uint64_t i, uint64_t seq, uint64_t sig, int *f) { cb->before_frag(ctx, i, seq, sig, f); }
   void during_frag(uint64_t i, uint64_t seq, uint64_t sig, uint64_t chunk, uint64_t sz, int *f) {
@@ -228,9 +229,11 @@ int mux_loop(const fdt_mux_cfg_t *cfg, H &h, const volatile uint64_t *halt, fdt_
           in_seq[i] += k;
           mx.lap_n(M.loop_filter_before_fragment_duration_ticks, k);
         } else {
+          h.caught_up(i);
           mx.lap(M.loop_caught_up_duration_ticks);
         }
       } else {
+        h.caught_up(i);
         mx.lap(M.loop_caught_up_duration_ticks);
       }
       continue;
@@ -389,6 +392,7 @@ struct VBatch {
   bool done = false;
   size_t next = 0;                   /* next item to resolve */
   uint64_t t_first = 0, t_submit = 0;
+  uint64_t cu_first = 0;              /* the tile's caught_up_cnt when the batch took its first frag */
 
   void reset() {
     first_chunk = end_off = sig_cnt = tr_used = 0;
@@ -444,12 +448,15 @@ struct fdgpu_vmux {
   std::vector<VBatch *> pool;
   std::deque<VBatch *> inflight;          /* submitted, in ingest order, until published */
   uint32_t busy = 0;                      /* ... of which still on the verifier (not polled done) */
+  uint32_t sweeps = 0;                    /* resolve calls (rate-limits polling the batches behind the oldest) */
   VBatch *open = nullptr;
   std::vector<uint32_t> pub_chunk;        /* chunk of each recently published out seq */
   uint64_t pub_mask = 0, published_total = 0;
   int error = 0;
   uint32_t calls = 0;                     /* after_credit calls (rate-limits verifier polls) */
   uint64_t due_tsc = 0, stall_max_tick = 0;   /* the every-32nd call's time stamp counter, the longest gap */
+  uint64_t caught_up_cnt = 0;             /* polls of an in link that found nothing new ... */
+  bool sees_caught_up = false;            /* ... counted (the loop's own instance; a callback table: the timer alone) */
   fdgpu_vtile_stats_t st{};
   std::vector<uint64_t> lat;
   fdgpu_link_t links[FDT_MUX_IN_MAX] = {};   /* gather: the in mcaches, re-checked by the device after its read */
@@ -525,7 +532,7 @@ struct fdgpu_vmux {
      frees its verifier slot for the next batch, while publishing waits for
      the oldest. */
   void resolve(fdt_mux_context_t *mux, int *poll_in) {
-    if (busy > 1)
+    if (busy > 1 && !(sweeps++ & 7u))          /* every 8th call: a poll is a runtime call, a slot freed a few us late costs little */
       for (size_t j = 1; j < inflight.size(); j++)
         if (!inflight[j]->done && poll_one(inflight[j], poll_in) < 0) return;
     while (!inflight.empty()) {
@@ -716,7 +723,12 @@ struct fdgpu_vmux {
       ~Acc() { const uint64_t d = now_ns() - t0; ns += d; mx = std::max(mx, d); }
     } acc{st.submit_ns, st.submit_max_ns, s0};
     if (gather && lap_margin != ~0ull) lap_guard(*open);    /* also while the batch fills or waits for a slot */
-    if (!open->closed && s0 - open->t_first < cfg.batch_wait_ns) return;
+    /* a partial batch goes out once its oldest frag waited batch_wait_ns and
+       the tile has since found its in links drained; while frags keep
+       coming faster than it reads them, the batch fills (capacity: full
+       batches, not a timer's worth) */
+    if (!open->closed && (s0 - open->t_first < cfg.batch_wait_ns || (sees_caught_up && caught_up_cnt == open->cu_first)))
+      return;
     if (busy >= cfg.inflight_max) return;
     int64_t t;
     if (gather) {
@@ -813,7 +825,7 @@ __attribute__((always_inline)) inline void vm_after_frag(void *ctx, uint64_t in_
     /* reserve the out frag's room from the size alone (the tile never reads
        the payload); the GPU writes [payload][pad][fd_txn_t][u16] there */
     VBatch &b = *t->open;
-    if (!b.cnt) { b.first_chunk = t->out_chunk; b.t_first = now_ns(); }
+    if (!b.cnt) { b.first_chunk = t->out_chunk; b.t_first = now_ns(); b.cu_first = t->caught_up_cnt; }
     const uint64_t off = (t->out_chunk - b.first_chunk) << FDT_CHUNK_LG_SZ;
     const uint32_t cap = t->cap_of[payload_sz];                  /* payload_sz <= FDT_TPU_MTU: during_frag */
     const uint32_t li = (uint32_t)t->cur_in;
@@ -851,7 +863,7 @@ __attribute__((always_inline)) inline void vm_after_frag(void *ctx, uint64_t in_
     (void)txn;
     const uint64_t sc = t->cur_sc, fp = t->cur_fp;
     VBatch &b = *t->open;
-    if (!b.cnt) { b.first_chunk = t->out_chunk; b.t_first = now_ns(); }
+    if (!b.cnt) { b.first_chunk = t->out_chunk; b.t_first = now_ns(); b.cu_first = t->caught_up_cnt; }
     const uint64_t off = (t->out_chunk - b.first_chunk) << FDT_CHUNK_LG_SZ;
     __builtin_prefetch(b.items.data() + b.items.size() + 6, 1);      /* reserved: stores a few frags ahead */
     __builtin_prefetch(b.frags.data() + b.frags.size() + 12, 1);
@@ -884,7 +896,7 @@ __attribute__((always_inline)) inline void vm_after_frag(void *ctx, uint64_t in_
   const uint64_t new_sz = toff + tsz + 2;
   const fdt_txn_t *tt = (const fdt_txn_t *)txn_t;
   VBatch &b = *t->open;                                 /* after_credit made sure one is open */
-  if (!b.cnt) { b.first_chunk = t->out_chunk; b.t_first = now_ns(); }
+  if (!b.cnt) { b.first_chunk = t->out_chunk; b.t_first = now_ns(); b.cu_first = t->caught_up_cnt; }
   const uint64_t off = (t->out_chunk - b.first_chunk) << FDT_CHUNK_LG_SZ;
   fdgpu_txn_t d;
   d.msg_off = (uint32_t)(off + tt->message_off);
@@ -942,6 +954,7 @@ struct VmHooks {
     const uint64_t r = t->rr_mask ? (seq & t->rr_mask) : seq % cnt, idx = t->cfg.round_robin_idx;
     return idx >= r ? idx - r : idx + cnt - r;
   }
+  void caught_up(uint64_t) { t->caught_up_cnt++; }
   void skipped(uint64_t, uint64_t seq, uint64_t k) {
     t->st.in_frags += k;
     t->st.filtered_rr += k;
@@ -965,7 +978,10 @@ bool is_vmux_callbacks(const fdt_mux_callbacks_t *cb) {
 
 int vmux_loop(const fdt_mux_cfg_t *cfg, void *ctx, const volatile uint64_t *halt, fdt_mux_stats_t *stats_out) {
   VmHooks h{(fdgpu_vmux *)ctx};
-  return mux_loop(cfg, h, halt, stats_out);
+  h.t->sees_caught_up = true;
+  const int rc = mux_loop(cfg, h, halt, stats_out);
+  h.t->sees_caught_up = false;
+  return rc;
 }
 
 }  // namespace
