@@ -519,6 +519,10 @@ def tile_lines(device, arena, txns, modes, cpus, cfg3=None):
     on this GPU, 16K-txn batches, 8 in flight, producers and tiles pinned to
     their own cores, in a child process (tile_cmd).  Every run checks that
     exactly the verified txns were published."""
+    from firedancer_amd.workload import same_l3_first
+    # producers and tiles of a run on one CCD when one has room (a tile and its producers on two
+    # sockets ran a quarter slower, profiles/r04/tile_host_cost.md)
+    cpus = same_l3_first(list(cpus), 6) if cpus else cpus
     out = _tile_child(device, cpus, arena, txns, modes, TILE_RUNS)
     out["tile_mux2_vs_mux1_capacity"] = round(out["tile_mux2_capacity_txns_per_s"] /
                                               out["tile_mux1_capacity_txns_per_s"], 3)
