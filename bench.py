@@ -500,6 +500,10 @@ def _tile_child(device, cpus, arena, txns, modes, runs, tag=""):
         out[f"tile_{name}_rescued"] = max(x["counters"]["rescued"] for x in reps)
         out[f"tile_{name}_parse_fail"] = res["counters"]["parse_fail"]
         out[f"tile_{name}_published_ok"] = all(x["published_ok"] for x in reps)
+        # the tile's longest gap between two of its polls, worst of the runs: a core taken away (another
+        # tenant's thread on it, the runtime blocking) -- a paced link laps a tile stalled for
+        # depth / per-link rate (16384 / 5 M/s = 3.3 ms)
+        out[f"tile_{name}_stall_max_ms"] = round(max(x["counters"].get("stall_max_ns", 0) for x in reps) / 1e6, 2)
     return out
 
 
