@@ -108,6 +108,23 @@ struct Slot {
   uint8_t *h_io = nullptr, *d_ioh = nullptr;  /* pinned [frag records][payload addresses]; its device view */
   fdgpu_frag_ex_t *d_fxio = nullptr;          /* the records, kept on the device by the gather */
   uint8_t *d_trh = nullptr;                   /* h_tr's device-side address (results written in place) */
+  /* FDGPU_FLAG_MERGE: the batch's gather + parse are queued and its verify
+     waits to be merged with the other batches ready (merge_kick), which then
+     queues the rest of the batch behind it */
+  hipEvent_t parsed = nullptr;
+  bool vpending = false;
+  uint32_t m_n = 0;
+  uint64_t m_seed = 0, m_cb = 0, m_bound = 0;
+  uint8_t *m_out = nullptr;
+};
+
+/* a merge stream of an FDGPU_FLAG_MERGE engine */
+struct Merge {
+  hipStream_t stream = nullptr;
+  uint32_t *h_flag = nullptr, *d_flag = nullptr;   /* seq after each merged verify: free when equal */
+  uint32_t seq = 0;
+  fdgpu_mbatch_t *h_tab = nullptr, *d_tab = nullptr;   /* tabs x ring_depth batch entries, pinned */
+  std::vector<hipEvent_t> ev;                          /* one per table: the launch that read it is done */
 };
 
 }  // namespace
@@ -138,6 +155,11 @@ struct fdgpu_engine {
   std::vector<Reg> regions;
   bool drop_flag = false;            /* test hook (FDGPU_DEBUG_DROP_FLAG=1): the stream never writes the
                                         completion word, so polls must finish through the event */
+  /* FDGPU_FLAG_MERGE */
+  std::vector<Merge> merges;
+  std::vector<Slot *> pending;       /* batches parsed (or parsing) whose verify is not launched */
+  uint32_t merge_rr = 0, merge_tabs = 0;
+  uint64_t merge_launches = 0, merge_batches = 0;
 };
 
 namespace {
@@ -147,6 +169,7 @@ void slot_free(Slot &s) {
   if (s.h2d_done) (void)hipEventDestroy(s.h2d_done);
   if (s.comp_done) (void)hipEventDestroy(s.comp_done);
   if (s.done) (void)hipEventDestroy(s.done);
+  if (s.parsed) (void)hipEventDestroy(s.parsed);
   if (s.h_arena) (void)hipHostFree(s.h_arena);
   if (s.h_sigs) (void)hipHostFree(s.h_sigs);
   if (s.h_perm) (void)hipHostFree(s.h_perm);
@@ -175,6 +198,7 @@ bool slot_alloc(Slot &s, const fdgpu_cfg_t &c) {
   HIPCHK(hipEventCreateWithFlags(&s.h2d_done, hipEventDisableTiming), false);
   HIPCHK(hipEventCreateWithFlags(&s.comp_done, hipEventDisableTiming), false);
   HIPCHK(hipEventCreateWithFlags(&s.done, hipEventDisableTiming), false);
+  HIPCHK(hipEventCreateWithFlags(&s.parsed, hipEventDisableTiming), false);
   HIPCHK(hipHostMalloc((void **)&s.h_arena, arena, hipHostMallocDefault), false);
   HIPCHK(hipHostMalloc((void **)&s.h_sigs, c.max_sig * sizeof(fdgpu_sig_desc_t) + 16, hipHostMallocDefault), false);
   HIPCHK(hipHostMalloc((void **)&s.h_perm, c.max_sig * sizeof(uint32_t) + 16, hipHostMallocDefault), false);
@@ -477,6 +501,32 @@ fdgpu_engine_t *fdgpu_engine_open(int device, fdgpu_cfg_t const *cfg_in) {
     (void)hipGetLastError();
     *s0.h_flag = 0;
   }
+  if (cfg.flags & FDGPU_FLAG_MERGE) {
+    /* two merge streams (a merged verify's tail overlaps the next one's
+       start); a table is reused only after 2 x ring_depth + 2 launches on its
+       stream, by when the launch that read it has finished (every launch in
+       flight holds a batch not yet complete, so at most ring_depth are) */
+    const char *ms = getenv("FDGPU_MERGE_STREAMS");
+    const uint32_t nms = ms && ms[0] == '1' ? 1u : 2u;
+    e->merge_tabs = 2 * cfg.ring_depth + 2;
+    e->merges.resize(nms);
+    for (auto &m : e->merges) {
+      if (hipStreamCreateWithFlags(&m.stream, hipStreamNonBlocking) != hipSuccess ||
+          hipHostMalloc((void **)&m.h_flag, 64, hipHostMallocDefault) != hipSuccess ||
+          hipHostGetDevicePointer((void **)&m.d_flag, m.h_flag, 0) != hipSuccess ||
+          hipHostMalloc((void **)&m.h_tab, (size_t)e->merge_tabs * cfg.ring_depth * sizeof(fdgpu_mbatch_t),
+                        hipHostMallocDefault) != hipSuccess ||
+          hipHostGetDevicePointer((void **)&m.d_tab, m.h_tab, 0) != hipSuccess) {
+        set_err("merge stream");
+        return fail();
+      }
+      *m.h_flag = 0;
+      m.ev.resize(e->merge_tabs);
+      for (auto &ev : m.ev)
+        if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) { set_err("merge event"); return fail(); }
+    }
+    e->pending.reserve(cfg.ring_depth);
+  }
   return e;
 }
 
@@ -488,7 +538,14 @@ void fdgpu_engine_close(fdgpu_engine_t *e) {
             g_sp_loop.load() / 1e3 / g_sp_calls.load(), g_sp_enq.load() / 1e3 / g_sp_calls.load());
   (void)hipSetDevice(e->device);
   if (e->compute) (void)hipStreamSynchronize(e->compute);
+  for (auto &m : e->merges) if (m.stream) (void)hipStreamSynchronize(m.stream);
   for (auto &s : e->slots) { if (s.stream) (void)hipStreamSynchronize(s.stream); slot_free(s); }
+  for (auto &m : e->merges) {
+    for (auto ev : m.ev) if (ev) (void)hipEventDestroy(ev);
+    if (m.h_tab) (void)hipHostFree(m.h_tab);
+    if (m.h_flag) (void)hipHostFree(m.h_flag);
+    if (m.stream) (void)hipStreamDestroy(m.stream);
+  }
   for (auto &r : e->regions) region_release(e->device, r.base);
   for (auto st : e->batch_streams) (void)hipStreamSynchronize(st);   /* btab is read there */
   if (e->d_btab) btab_release(e->device, e->d_btab);
@@ -737,6 +794,10 @@ int64_t fdgpu_stage_submit(fdgpu_engine_t *e, uint64_t arena_sz, fdgpu_txn_t con
   return submit_slot(e, s, arena_sz, txns, txn_cnt);
 }
 
+namespace {
+int merge_kick(fdgpu_engine_t *e, bool force);
+}
+
 static int poll_slot(fdgpu_engine_t *e, int64_t ticket, int8_t *txn_codes, int blocking, bool keep,
                      uint8_t *trailers = nullptr, uint64_t *tags = nullptr, uint16_t *out_szs = nullptr) {
   if (!e) return FDGPU_ERR_INVAL;
@@ -744,6 +805,12 @@ static int poll_slot(fdgpu_engine_t *e, int64_t ticket, int8_t *txn_codes, int b
   Slot *s = nullptr;
   for (auto &c : e->slots) if (c.ticket == ticket && ticket >= 0 && !c.held) { s = &c; break; }
   if (!s) { set_err("unknown ticket %lld", (long long)ticket); return FDGPU_ERR_TICKET; }
+  if (!e->pending.empty()) {                   /* FDGPU_FLAG_MERGE: verifies waiting for a merge stream */
+    HIPCHK(hipSetDevice(e->device), FDGPU_ERR_DEVICE);
+    const int rc = merge_kick(e, blocking && s->vpending);
+    if (rc) return rc;
+    if (s->vpending) return FDGPU_PENDING;     /* non-blocking: not even launched */
+  }
   if (blocking) {
     HIPCHK(hipSetDevice(e->device), FDGPU_ERR_DEVICE);
     lk.unlock();                               /* the slot is this caller's until it is polled */
@@ -877,6 +944,93 @@ uint32_t fdgpu_frag_out_cap(uint32_t sz) {
    frags into the registered out region and [codes][tags][out sizes] into the
    slot's pinned results, both in place, and the stream stores the completion
    word.  No copies are queued. */
+}  // extern "C"
+
+namespace {
+
+/* the rest of a gathered batch after its verify: finish (out frags and
+   results written over the bus), the completion word, the done event */
+int io_tail(fdgpu_engine_t *e, Slot *s) {
+  const uint64_t n = s->m_n, cb = s->m_cb;
+  HIPCHK(fdgpu_launch_frag_finish_io(s->d_txns, (uint32_t)n, s->d_sig_codes, s->d_txn_sz, s->d_fxio, s->d_txn_out,
+                                     s->d_arena, s->m_seed, s->m_out, (int8_t *)s->d_trh, (uint64_t *)(s->d_trh + cb),
+                                     (uint16_t *)(s->d_trh + cb + n * 8), s->stream),
+         FDGPU_ERR_DEVICE);
+  ++s->flag_seq;
+  if (e->flag_poll && !e->drop_flag) HIPCHK(hipStreamWriteValue32(s->stream, s->d_flag, s->flag_seq, 0), FDGPU_ERR_DEVICE);
+  HIPCHK(hipEventRecord(s->done, s->stream), FDGPU_ERR_DEVICE);
+  return FDGPU_OK;
+}
+
+bool merge_free(const fdgpu_engine_t *e, const Merge &m) {
+  if (e->flag_poll) return __atomic_load_n(m.h_flag, __ATOMIC_ACQUIRE) == m.seq;
+  return !m.seq || hipEventQuery(m.ev[(m.seq - 1) % e->merge_tabs]) == hipSuccess;
+}
+
+/* FDGPU_FLAG_MERGE (ring_mu held): the verifies of the batches waiting, as
+   one launch on a merge stream that is idle -- or, forced (a blocking poll
+   waits on one of them), on the next one anyway -- then each batch's tail on
+   its own stream behind it */
+int merge_kick(fdgpu_engine_t *e, bool force) {
+  if (e->pending.empty()) return FDGPU_OK;
+  const uint32_t nms = (uint32_t)e->merges.size();
+  int mi = -1;
+  for (uint32_t k = 0; k < nms && mi < 0; k++) {
+    const uint32_t j = (e->merge_rr + k) % nms;
+    if (merge_free(e, e->merges[j])) mi = (int)j;
+  }
+  if (mi < 0) {
+    if (!force) return FDGPU_OK;
+    mi = (int)(e->merge_rr % nms);
+  }
+  e->merge_rr = (uint32_t)mi + 1;
+  Merge &m = e->merges[(size_t)mi];
+  const uint32_t ti = m.seq % e->merge_tabs;
+  const uint32_t nb = (uint32_t)e->pending.size();
+  for (Slot *s : e->pending) HIPCHK(hipStreamWaitEvent(m.stream, s->parsed, 0), FDGPU_ERR_DEVICE);
+  if (nb == 1) {                               /* alone: the ring path's kernels (FDGPU_FLAG_PAIR_AUTO applies) */
+    Slot *s = e->pending[0];
+    HIPCHK(fdgpu_launch_verify_sigs(s->d_arena, s->d_sigs, (uint32_t)s->m_bound, nullptr, e->d_btab, s->d_ws,
+                                    s->d_sig_codes, ring_kflags(e, s, s->m_bound), m.stream, s->d_n_sig,
+                                    e->resident_blocks, e->kc_seed, 1),
+           FDGPU_ERR_DEVICE);
+  } else {
+    fdgpu_mbatch_t *tab = m.h_tab + (size_t)ti * e->cfg.ring_depth;
+    uint32_t grid_max = 0, slow_max = 0;
+    for (uint32_t j = 0; j < nb; j++) {
+      Slot *s = e->pending[j];
+      const uint32_t grid = (uint32_t)((s->m_bound + FDGPU_BLOCK - 1) / FDGPU_BLOCK);
+      const uint32_t slow = grid < e->resident_blocks ? grid : e->resident_blocks;
+      uint32_t *cnt = fdgpu_verify_cnt_word(s->d_ws, (uint32_t)s->m_bound);
+      s->k_sigs = s->m_bound;
+      tab[j] = fdgpu_mbatch_t{s->d_arena, s->d_sigs, s->d_n_sig, s->d_ws, s->d_sig_codes,
+                              cnt - (size_t)grid * FDGPU_BLOCK, cnt, (uint32_t)s->m_bound, slow};
+      grid_max = grid > grid_max ? grid : grid_max;
+      slow_max = slow > slow_max ? slow : slow_max;
+    }
+    HIPCHK(fdgpu_launch_verify_multi(m.d_tab + (size_t)ti * e->cfg.ring_depth, nb, grid_max, slow_max, e->d_btab,
+                                     kflags(e) & ~(uint32_t)FDGPU_FLAG_KPAIR, m.stream),
+           FDGPU_ERR_DEVICE);
+  }
+  HIPCHK(hipEventRecord(m.ev[ti], m.stream), FDGPU_ERR_DEVICE);
+  ++m.seq;
+  if (e->flag_poll) HIPCHK(hipStreamWriteValue32(m.stream, m.d_flag, m.seq, 0), FDGPU_ERR_DEVICE);
+  for (Slot *s : e->pending) {
+    HIPCHK(hipStreamWaitEvent(s->stream, m.ev[ti], 0), FDGPU_ERR_DEVICE);
+    const int rc = io_tail(e, s);
+    if (rc) return rc;
+    s->vpending = false;
+  }
+  e->merge_launches++;
+  e->merge_batches += nb;
+  e->pending.clear();
+  return FDGPU_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
 int64_t fdgpu_submit_frags_io(fdgpu_engine_t *e, fdgpu_frag_io_t const *fio, uint64_t n, uint8_t *out,
                               uint64_t out_sz, uint64_t hash_seed, fdgpu_link_t const *links, uint64_t link_cnt) {
   const uint64_t sp0 = g_sp_on ? sp_now() : 0;
@@ -964,6 +1118,19 @@ int64_t fdgpu_submit_frags_io(fdgpu_engine_t *e, fdgpu_frag_io_t const *fio, uin
     HIPCHK(fdgpu_launch_frag_parse_expand(s->d_arena, d_fx, (uint32_t)n, s->d_txn_out, s->d_txn_sz, s->d_sigs, s->d_txns,
                                           s->d_n_sig, s->stream),
            FDGPU_ERR_DEVICE);
+    if (!e->merges.empty() && zero_cnt && bound) {
+      /* the verify waits to be merged with the other batches ready (merge_kick) */
+      HIPCHK(hipEventRecord(s->parsed, s->stream), FDGPU_ERR_DEVICE);
+      s->vpending = true;
+      s->m_n = (uint32_t)n; s->m_seed = hash_seed; s->m_out = out_dev; s->m_cb = cb; s->m_bound = bound;
+      e->pending.push_back(s);
+      s->staged = false; s->held = false; s->polls = 0; s->frag = true; s->io = true; s->tr_sz = 0; s->tr_base = 0;
+      s->ticket = e->next_ticket++;
+      s->txn_cnt = n;
+      const int rc = merge_kick(e, false);
+      if (rc) return rc;
+      return s->ticket;
+    }
     HIPCHK(fdgpu_launch_verify_sigs(s->d_arena, s->d_sigs, (uint32_t)bound, nullptr, e->d_btab, s->d_ws, s->d_sig_codes,
                                     ring_kflags(e, s, bound), s->stream, s->d_n_sig, e->resident_blocks, e->kc_seed, zero_cnt),
            FDGPU_ERR_DEVICE);

@@ -83,6 +83,23 @@ hipError_t fdgpu_launch_verify_sigs(const uint8_t *d_arena, const fdgpu_sig_desc
 /* the verify launch's queue counter for an n_sig grid in d_ws: a caller whose
    earlier kernel on the stream zeroes it passes cnt_zeroed (no memset) */
 uint32_t  *fdgpu_verify_cnt_word(uint32_t *d_ws, uint32_t n_sig);
+/* One batch of a merged verify launch (FDGPU_FLAG_MERGE): what
+   fdgpu_launch_verify_sigs takes per batch, read by each block from a table
+   in pinned host memory (blockIdx.y picks the batch). */
+typedef struct {
+  const uint8_t *arena;
+  const fdgpu_sig_desc_t *sigs;
+  const uint32_t *n_sig;       /* the count, produced on the device (parse + expand) */
+  uint32_t *ws;                /* the batch's workspace; its fallback queue and counter follow the lanes */
+  int8_t *codes;
+  uint32_t *queue, *cnt;
+  uint32_t bound;              /* the launch bound of the count: the batch's blocks */
+  uint32_t slow;               /* fallback blocks */
+} fdgpu_mbatch_t;
+/* one verify (one lane per signature) + one fallback launch over nb batches:
+   grids {max blocks, nb} */
+hipError_t fdgpu_launch_verify_multi(const fdgpu_mbatch_t *mb, uint32_t nb, uint32_t grid_max, uint32_t slow_max,
+                                     const uint32_t *d_btab, uint32_t flags, hipStream_t stream);
 /* d_accept (NULL: not written): ceil(n_txn / 64) words, bit t = txn t verified */
 hipError_t fdgpu_launch_combine(const fdgpu_txn_desc_t *d_txns, uint32_t n_txn, const int8_t *d_sig_codes,
                                 int8_t *d_txn_codes, uint64_t *d_accept, hipStream_t stream);

@@ -486,19 +486,20 @@ FDG_DEV void hs_chain(ge_p1p1 &t, uint32_t (&ud)[5], uint32_t (&vd)[5], bool u_n
 }
 
 /* The verify kernel of the half-size path; codes of lanes it settles are
-   written here, lanes whose split failed are queued for fdgpu_full_kernel. */
+   written here, lanes whose split failed are queued for fdgpu_full_kernel.
+   The body takes its block index: the merged launch (fdgpu_verify_hs_multi_kernel)
+   runs it for the batch blockIdx.y names. */
 template <bool KC>
-__global__ void __launch_bounds__(FDGPU_BLOCK, FDGPU_VERIFY_WAVES)
-fdgpu_verify_hs_kernel(const uint8_t *__restrict__ arena, const fdgpu_sig_desc_t *__restrict__ sigs, uint32_t n_sig_arg,
-                       const uint32_t *__restrict__ n_sig_dev, const uint32_t *__restrict__ btab,
-                       uint32_t *__restrict__ ws, const uint32_t *__restrict__ perm, int8_t *__restrict__ codes,
-                       uint32_t *__restrict__ queue, uint32_t *__restrict__ queue_cnt, uint32_t flags,
-                       const uint32_t *__restrict__ key_of, const uint32_t *__restrict__ kverd) {
+FDG_DEV void verify_hs_body(const uint8_t *__restrict__ arena, const fdgpu_sig_desc_t *__restrict__ sigs, uint32_t n_sig_arg,
+                            const uint32_t *__restrict__ n_sig_dev, const uint32_t *__restrict__ btab,
+                            uint32_t *__restrict__ ws, const uint32_t *__restrict__ perm, int8_t *__restrict__ codes,
+                            uint32_t *__restrict__ queue, uint32_t *__restrict__ queue_cnt, uint32_t flags,
+                            const uint32_t *__restrict__ key_of, const uint32_t *__restrict__ kverd, uint32_t bx) {
   /* n_sig_dev: the count is produced on the device (GPU-side ingest) and the
      grid covers an upper bound; blocks past it leave at once */
   const uint32_t n_sig = n_sig_dev ? *n_sig_dev : n_sig_arg;
-  if (blockIdx.x * blockDim.x >= n_sig) return;
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (bx * blockDim.x >= n_sig) return;
+  const uint32_t i = bx * blockDim.x + threadIdx.x;
   const bool active = i < n_sig;
   const bool ref_map = (flags & FDGPU_FLAG_REF_MAP) != 0;
   const fdgpu_sig_desc_t d = sigs[active ? i : n_sig - 1];
@@ -637,6 +638,30 @@ fdgpu_verify_hs_kernel(const uint8_t *__restrict__ arena, const fdgpu_sig_desc_t
       if (full) queue[base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull))] = i;
     }
   }
+}
+
+template <bool KC>
+__global__ void __launch_bounds__(FDGPU_BLOCK, FDGPU_VERIFY_WAVES)
+fdgpu_verify_hs_kernel(const uint8_t *__restrict__ arena, const fdgpu_sig_desc_t *__restrict__ sigs, uint32_t n_sig_arg,
+                       const uint32_t *__restrict__ n_sig_dev, const uint32_t *__restrict__ btab,
+                       uint32_t *__restrict__ ws, const uint32_t *__restrict__ perm, int8_t *__restrict__ codes,
+                       uint32_t *__restrict__ queue, uint32_t *__restrict__ queue_cnt, uint32_t flags,
+                       const uint32_t *__restrict__ key_of, const uint32_t *__restrict__ kverd) {
+  verify_hs_body<KC>(arena, sigs, n_sig_arg, n_sig_dev, btab, ws, perm, codes, queue, queue_cnt, flags, key_of, kverd,
+                     blockIdx.x);
+}
+
+/* Several batches' verifies as ONE launch (FDGPU_FLAG_MERGE): block (x, y)
+   is block x of batch y.  Concurrent 16 K-signature launches from separate
+   streams share the CUs badly -- eight 8 K launches at once take 1.33 ms,
+   one 64 K launch 0.85 ms (profiles/r04/conc_probe.jsonl) -- so an engine
+   with several batches ready verifies them together. */
+__global__ void __launch_bounds__(FDGPU_BLOCK, FDGPU_VERIFY_WAVES)
+fdgpu_verify_hs_multi_kernel(const fdgpu_mbatch_t *__restrict__ mb, const uint32_t *__restrict__ btab, uint32_t flags) {
+  const fdgpu_mbatch_t b = mb[blockIdx.y];
+  if (blockIdx.x * blockDim.x >= b.bound) return;
+  verify_hs_body<false>(b.arena, b.sigs, b.bound, b.n_sig, btab, b.ws, nullptr, b.codes, b.queue, b.cnt, flags, nullptr,
+                        nullptr, blockIdx.x);
 }
 
 /* ---------------- two lanes per signature (FDGPU_FLAG_KPAIR) ----------------
@@ -951,10 +976,14 @@ fdgpu_key_table_kernel(const uint8_t *__restrict__ arena, const fdgpu_sig_desc_t
 __global__ void __launch_bounds__(FDGPU_BLOCK, FDGPU_VERIFY_WAVES)
 fdgpu_full_kernel(uint32_t *__restrict__ ws, const uint32_t *__restrict__ perm, int8_t *__restrict__ codes,
                   const uint32_t *__restrict__ queue, const uint32_t *__restrict__ queue_cnt, uint32_t slots,
-                  const uint32_t *__restrict__ key_of) {
+                  const uint32_t *__restrict__ key_of);
+
+FDG_DEV void full_body(uint32_t *__restrict__ ws, const uint32_t *__restrict__ perm, int8_t *__restrict__ codes,
+                       const uint32_t *__restrict__ queue, const uint32_t *__restrict__ queue_cnt, uint32_t slots,
+                       const uint32_t *__restrict__ key_of, uint32_t bx) {
   const uint32_t cnt = *queue_cnt;
-  if (blockIdx.x * blockDim.x >= cnt) return;
-  for (uint32_t q = blockIdx.x * blockDim.x + threadIdx.x; q < cnt; q += slots) {
+  if (bx * blockDim.x >= cnt) return;
+  for (uint32_t q = bx * blockDim.x + threadIdx.x; q < cnt; q += slots) {
     const uint32_t i = queue[q];
     uint32_t *wsl = ws + (size_t)i * FDGPU_WS_LANE_WORDS;
     const uint32_t *park = wsl + FDGPU_WS_PARK * FDGPU_ATAB_WORDS;
@@ -972,6 +1001,21 @@ fdgpu_full_kernel(uint32_t *__restrict__ ws, const uint32_t *__restrict__ perm, 
     eq = eq && fe_eq(Rc.Y, l);
     codes[out_idx(perm, i)] = (int8_t)(eq ? 0 : -3);
   }
+}
+
+__global__ void __launch_bounds__(FDGPU_BLOCK, FDGPU_VERIFY_WAVES)
+fdgpu_full_kernel(uint32_t *__restrict__ ws, const uint32_t *__restrict__ perm, int8_t *__restrict__ codes,
+                  const uint32_t *__restrict__ queue, const uint32_t *__restrict__ queue_cnt, uint32_t slots,
+                  const uint32_t *__restrict__ key_of) {
+  full_body(ws, perm, codes, queue, queue_cnt, slots, key_of, blockIdx.x);
+}
+
+/* the fallback of a merged verify: block (x, y) serves batch y's queue */
+__global__ void __launch_bounds__(FDGPU_BLOCK, FDGPU_VERIFY_WAVES)
+fdgpu_full_multi_kernel(const fdgpu_mbatch_t *__restrict__ mb) {
+  const fdgpu_mbatch_t b = mb[blockIdx.y];
+  if (blockIdx.x >= b.slow) return;
+  full_body(b.ws, nullptr, b.codes, b.queue, b.cnt, b.slow * FDGPU_BLOCK, nullptr, blockIdx.x);
 }
 
 /* Per transaction: fd_ed25519_verify_batch_single_msg's first-error order
@@ -1589,6 +1633,14 @@ hipError_t fdgpu_launch_verify_sigs(const uint8_t *d_arena, const fdgpu_sig_desc
   }
   hipLaunchKernelGGL(fdgpu_full_kernel, dim3(slow_blocks), dim3(FDGPU_BLOCK), 0, stream, d_ws, d_perm, d_sig_codes,
                      queue, cnt, slow_blocks * FDGPU_BLOCK, key_of);
+  return hipGetLastError();
+}
+
+hipError_t fdgpu_launch_verify_multi(const fdgpu_mbatch_t *mb, uint32_t nb, uint32_t grid_max, uint32_t slow_max,
+                                     const uint32_t *d_btab, uint32_t flags, hipStream_t stream) {
+  if (!nb || !grid_max) return hipSuccess;
+  hipLaunchKernelGGL(fdgpu_verify_hs_multi_kernel, dim3(grid_max, nb), dim3(FDGPU_BLOCK), 0, stream, mb, d_btab, flags);
+  hipLaunchKernelGGL(fdgpu_full_multi_kernel, dim3(slow_max ? slow_max : 1, nb), dim3(FDGPU_BLOCK), 0, stream, mb);
   return hipGetLastError();
 }
 

@@ -130,6 +130,11 @@ typedef struct {
                                       that leave the GPU's wave slots idle (small / latency-bound batches),
                                       ~1.4x the work per signature, so slower on batches that fill the GPU;
                                       same codes.  Ignored with FDGPU_FLAG_KEY_CACHE */
+#define FDGPU_FLAG_MERGE     64u  /* gathered frag batches (fdgpu_submit_frags_io): the verifies of the batches
+                                      ready at once run as ONE launch on a stream of the engine's own, each
+                                      batch's gather / parse before it and its finish after it on the batch's
+                                      slot stream (a verify is launched from submit and poll calls, so the
+                                      caller polls; a blocking poll launches what is waiting).  Same codes */
 #define FDGPU_FLAG_PAIR_AUTO 32u  /* the FDGPU_FLAG_PAIR kernel for a ring batch while it and the engine's
                                       running batches hold <= 48 K signatures (launch bounds): the GPU has idle
                                       wave slots, latency is a wave's lifetime; the one-lane kernel otherwise.

@@ -424,3 +424,65 @@ def test_frag_io_pair_kernel(oracle):
                 eng.host_unregister(out_buf)
     finally:
         eng.close()
+
+
+@pytest.mark.gpu
+def test_frag_io_merged_verify(oracle):
+    """FDGPU_FLAG_MERGE: gathered batches submitted back to back have their
+    verifies merged into shared launches (one block row per batch) on the
+    engine's merge streams, launched from submit and poll calls.  Four
+    batches (cfg1 and cfg3 payloads, different sizes) in flight at once,
+    polled non-blocking, blocking and out of order: codes, tags, out sizes
+    and every out-frag byte equal those of an engine without the flag, and
+    the codes equal the oracle's."""
+    import firedancer_amd as fa
+    from firedancer_amd import _lib
+    L = _lib.lib()
+    sets = []
+    for gen, n, seed in ((workload.cfg1, 1800, 0xC1), (workload.cfg3, 400, 0xC2), (workload.cfg1, 700, 0xC3),
+                         (workload.cfg3, 900, 0xC4)):
+        a, t, _ = gen(n, seed=seed)
+        sets.append([p for p in workload.payloads(a, t) if tile.txn_parse(p)[0]])
+    results = {}
+    for merge in (False, True):
+        eng = fa.VerifyEngine(0, max_txn=2048, ring_depth=4, merge=merge)
+        bufs = []
+        try:
+            tks = []
+            for ps in sets:
+                in_buf, out_buf = _pages(len(ps) * 1280), _pages(len(ps) * 2176)
+                eng.host_register(in_buf)
+                eng.host_register(out_buf)
+                bufs += [in_buf, out_buf]
+                fio = np.zeros(len(ps), dtype=tile.FRAG_IO_DTYPE)
+                o = 0
+                for k, p in enumerate(ps):
+                    in_buf[k * 1280:k * 1280 + len(p)] = np.frombuffer(p, dtype=np.uint8)
+                    cap = L.fdgpu_frag_out_cap(len(p))
+                    fio[k] = (in_buf.ctypes.data + k * 1280, len(p), o, cap, 0, 0)
+                    o += (cap + 63) // 64 * 64
+                tks.append((eng.submit_frags_io(fio, out_buf, o, 0x44), out_buf, o))
+            res = [None] * len(tks)
+            for j in (2, 0):                                  # blocking, out of order (2 may still wait to merge)
+                res[j] = eng.poll_frags_io(tks[j][0], blocking=True)
+            for j in (3, 1):                                  # non-blocking until done
+                r = None
+                while r is None:
+                    r = eng.poll_frags_io(tks[j][0], blocking=False)
+                res[j] = r
+            results[merge] = [(c.copy(), tg.copy(), sz.copy(), bytes(ob[:o])) for (c, tg, sz), (_, ob, o) in zip(res, tks)]
+        finally:
+            for b in bufs:
+                eng.host_unregister(b)
+            eng.close()
+    for j, ps in enumerate(sets):
+        (c0, t0, s0, o0), (c1, t1, s1, o1) = results[False][j], results[True][j]
+        assert (c0 == c1).all() and (t0 == t1).all() and (s0 == s1).all() and o0 == o1, j
+        arena = np.frombuffer(b"".join(ps) + b"\0" * 16, dtype=np.uint8)
+        offs = np.cumsum([0] + [len(p) for p in ps])
+        td = np.zeros(len(ps), dtype=workload.TXN_DTYPE)
+        for k, p in enumerate(ps):
+            d = tile.txn_decode(tile.txn_parse(p)[1])
+            td[k] = (int(offs[k]) + d["message_off"], len(p) - d["message_off"],
+                     int(offs[k]) + d["signature_off"], int(offs[k]) + d["acct_addr_off"], d["signature_cnt"])
+        assert (c1 == oracle.verify_txns(arena, td, nthreads=8)).all(), j

@@ -82,6 +82,9 @@ def make_parser():
     ap.add_argument("--pair", type=int, default=0,
                     help="(mux tile) verify kernel: 0 one lane per signature, 1 two lanes (FDGPU_FLAG_PAIR), "
                          "2 two lanes while the engine is otherwise idle (FDGPU_FLAG_PAIR_AUTO)")
+    ap.add_argument("--merge", type=int, default=0,
+                    help="(mux tile) 1: FDGPU_FLAG_MERGE engines -- the verifies of an engine's batches ready at "
+                         "once run as one launch")
     ap.add_argument("--tiles-per-engine", type=int, default=1,
                     help="verify tiles sharing one engine (its ring slots): a process's HIP streams are hardware "
                          "queues, and past ~20 of them the GPU's scheduler time-slices the queues")
@@ -417,7 +420,7 @@ def engine_pool(args, n, batch, inflight, device):
         k = len(pool)
         e = fa.VerifyEngine(device if device is not None else k % args.gpus, max_txn=batch, max_sig=batch * 12,
                             max_arena=batch * frag_bytes, ring_depth=inflight, pair=args.pair == 1,
-                            pair_auto=args.pair == 2)
+                            pair_auto=args.pair == 2, merge=bool(getattr(args, "merge", 0)))
         if getattr(args, "reserve", 1):
             e.reserve()      # every slot sized for the largest batch now, not inside the run (as a tile's init does)
         pool.append(e)
