@@ -12,9 +12,10 @@
                                             (impl fd_ed25519_user.c:312-322)
        Served by the GPU engine (device 0, opened on first use); results
        are bit-identical to the reference's AVX-512 build.
-       LATENCY: each call is one GPU round trip, ~0.7 ms (measured p50/p99
-       690/710 us on MI355X, bench.py `sync_call_latency_*`: the verify
-       kernel's one-wave lifetime plus launches and read-back), against
+       LATENCY: each call is one GPU round trip, ~0.5 ms (measured p50/p99
+       514-517/523-529 us on MI355X, bench.py `sync_call_latency_*`: the
+       two-lane verify kernel's one-wave lifetime plus launches and
+       read-back; FDGPU_SYNC_PAIR=0: the one-lane kernel, 690/710 us), against
        ~33 us for the reference's CPU verify.  Concurrent callers are
        coalesced into one batch per round trip (group commit), so throughput
        grows with the number of calling threads.  Latency-bound callers
