@@ -629,12 +629,15 @@ def split_verify_output(frag_payload):
 class PyVerifier:
     """A verifier backed by a Python callable fn(arena uint8[], txns TXN_DTYPE[]) -> int8 codes.
     For tests of the tile logic without a GPU (the callable is the test's
-    checker); `lag` makes each batch report PENDING for that many polls."""
+    checker); `lag` makes each batch report PENDING for that many polls
+    (`lag_fn(ticket)`, when given, sets it per batch: batches then complete
+    out of order, as the engine's do on their own streams; `done` records
+    the order the batches completed in)."""
 
-    def __init__(self, fn, slots=2, lag=0):
-        self.fn, self.slots, self.lag = fn, slots, lag
+    def __init__(self, fn, slots=2, lag=0, lag_fn=None):
+        self.fn, self.slots, self.lag, self.lag_fn = fn, slots, lag, lag_fn
         self.results, self.polls, self.next = {}, {}, 0
-        self.batches = []
+        self.batches, self.done, self.lags = [], [], {}
 
         def submit(ctx, arena, arena_sz, txns, n):
             if len(self.results) >= self.slots:
@@ -647,16 +650,19 @@ class PyVerifier:
             self.next += 1
             self.results[k] = np.asarray(self.fn(a, t), dtype=np.int8)
             self.polls[k] = 0
+            if self.lag_fn is not None:
+                self.lags[k] = self.lag_fn(k)
             return k
 
         def poll(ctx, ticket, codes, blocking):
             if ticket not in self.results:
                 return -13
-            if not blocking and self.polls[ticket] < self.lag:
+            if not blocking and self.polls[ticket] < self.lags.get(ticket, self.lag):
                 self.polls[ticket] += 1
                 return 1                                      # FDGPU_PENDING
             r = self.results.pop(ticket)
             self.polls.pop(ticket)
+            self.done.append(ticket)
             if len(r):
                 c.memmove(codes, r.ctypes.data, len(r))
             return 0
@@ -695,6 +701,8 @@ class PyVerifier:
             self.results[k] = codes[:n]
             self.trailers[k] = bytes(tr)
             self.polls[k] = 0
+            if self.lag_fn is not None:
+                self.lags[k] = self.lag_fn(k)
             return k
 
         def poll_frags(ctx, ticket, codes, trailers, blocking):
@@ -763,17 +771,20 @@ class PyVerifier:
             self.results[k] = None
             self.io[k] = work
             self.polls[k] = 0
+            if self.lag_fn is not None:
+                self.lags[k] = self.lag_fn(k)
             return k
 
         def poll_io(ctx, ticket, codes, tags, out_szs, blocking):
             if ticket not in self.io:
                 return -13
-            if not blocking and self.polls[ticket] < self.lag:
+            if not blocking and self.polls[ticket] < self.lags.get(ticket, self.lag):
                 self.polls[ticket] += 1
                 return 1                                      # FDGPU_PENDING
             r, t, o = self.io.pop(ticket)()
             self.results.pop(ticket)
             self.polls.pop(ticket)
+            self.done.append(ticket)
             if len(r):
                 c.memmove(codes, r.ctypes.data, len(r))
                 c.memmove(tags, t.ctypes.data, 8 * len(t))
