@@ -731,6 +731,17 @@ def main():
         import torch
         ndev = torch.cuda.device_count()
         device = dist.local_rank % ndev if ndev > 0 else dist.local_rank
+    # the cfg5 tile lines first, in their child process, before this process
+    # opens any engine: the tiles' 16+ slot streams then have the device's
+    # hardware queues to themselves (with this process's engines open beside
+    # them, one tile ran 34.5 M txn/s against 38 M alone; profiles/r04/tile_run_order.md)
+    cfg3 = workload.cfg3(args.cfg3_txns, seed=workload.CFG3_SEED + dist.rank) if args.cfg3_txns else None
+    tl = None
+    if args.tile and not args.no_extras:
+        tl = tile_lines(device, arena, txns, modes, cpus, cfg3=cfg3)
+        tl["tile_mux1_capacity_txns_per_s_node"] = round(dist.sum(tl["tile_mux1_capacity_txns_per_s"]), 1)
+        tl["tile_published_ok_all_ranks"] = dist.sum(
+            1 if all(v for k, v in tl.items() if k.endswith("_published_ok")) else 0) == dist.world
     eng = VerifyEngine(device, max_txn=args.latency_batch, max_sig=2 * args.latency_batch,
                        max_arena=args.latency_batch * 1232, ring_depth=RING_DEPTH)
     # `queues` device-resident copies of the batch, each on its own HIP stream
@@ -773,12 +784,7 @@ def main():
         extras["latency_batch_txns"] = args.latency_batch
         if dist.rank == 0:
             extras.update(sync_latency(arena, txns))
-        cfg3 = workload.cfg3(args.cfg3_txns, seed=workload.CFG3_SEED + dist.rank) if args.cfg3_txns else None
-        if args.tile:
-            tl = tile_lines(device, arena, txns, modes, cpus, cfg3=cfg3)
-            tl["tile_mux1_capacity_txns_per_s_node"] = round(dist.sum(tl["tile_mux1_capacity_txns_per_s"]), 1)
-            tl["tile_published_ok_all_ranks"] = dist.sum(
-                1 if all(v for k, v in tl.items() if k.endswith("_published_ok")) else 0) == dist.world
+        if tl is not None:
             extras.update(tl)
         if args.cfg3_txns:
             eng_nb = VerifyEngine(device, max_txn=1024, ring_depth=1, bucket=False)
