@@ -340,33 +340,10 @@ def _aligned(nbytes, align):
     return buf[off:off + nbytes]
 
 
-_HUGE = 2 << 20
-
-
-def _huge_buf(nbytes):
-    """nbytes on 2 MB-aligned transparent huge pages (madvise), as the
-    reference's workspaces sit on huge / gigantic pages (fd_wksp): a link's
-    mcache and dcache, read in place by the GPU, then cost the device one
-    translation per 2 MB instead of per 4 KB.  Falls back to 4 KB pages."""
-    import mmap
-    size = (nbytes + _HUGE - 1) // _HUGE * _HUGE
-    m = mmap.mmap(-1, size + _HUGE, flags=mmap.MAP_PRIVATE | mmap.MAP_ANONYMOUS)
-    try:
-        m.madvise(mmap.MADV_HUGEPAGE)
-    except (AttributeError, OSError, ValueError):
-        pass
-    raw = np.frombuffer(m, dtype=np.uint8)
-    off = (-raw.ctypes.data) % _HUGE
-    return raw[off:off + nbytes]             # the array keeps the mapping alive; unmapped with its last view
-
-
 def _page_buf(nbytes):
     """nbytes in whole pages of their own: a buffer the GPU engines may
     register (fdgpu_host_register pins whole pages) without sharing a page
-    with another buffer.  Large buffers (>= 8 MB: link dcaches and deep
-    mcaches) go on huge pages (FDT_HUGE=0: never)."""
-    if nbytes >= 4 * _HUGE and os.environ.get("FDT_HUGE", "1") != "0":
-        return _huge_buf(nbytes)
+    with another buffer."""
     return _aligned((nbytes + 4095) // 4096 * 4096, 4096)[:nbytes]
 
 
