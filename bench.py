@@ -428,6 +428,9 @@ TILE_BATCH, TILE_INFLIGHT = 16384, 8   # txns per GPU batch, batches in flight p
 # (paced: p50 batch latency 1.13 vs 1.40 ms at 12 M txn/s, 1.47 vs 1.81 at 24 M; capacity unchanged;
 # profiles/r04/tile_pair.md)
 TILE_PAIR = 2
+# ... and FDGPU_FLAG_SPREAD_AUTO: one verify block per CU while an engine's batches fit the chip that way
+# (concurrent small launches otherwise stack two blocks per CU; profiles/r04/spread.md)
+TILE_SPREAD = 2
 # multi-signature frags: a batch also closes at this many signatures by the frag-size bound the tile sees
 # (~9.5 per cfg3 frag for ~6.5 real): ~2.6 K cfg3 txns, so 8 batches in flight are ~1.3 ms of GPU work
 # (49152: 1-tile p99 batch 5.8 ms, 2 tiles 59-65 M sig/s; 24576: 3.0 ms, 67-70 M; profiles/r04/tile_run_order.md)
@@ -452,7 +455,7 @@ def tile_cmd(device, cpus, npz, out, runs=TILE_RUNS, multi=0):
            "--multi", str(int(multi)), "--producers-same-as-tiles", "1", "--depth-lg", str(TILE_DEPTH_LG_PREFILL),
            "--depth-lg-paced", str(TILE_DEPTH_LG_PACED), "--paced-reps", str(TILE_PACED_REPS),
            "--wait-us", "200", "--pin", "1", "--hw-queues", str(TILE_HW_QUEUES), "--reps", str(TILE_REPS),
-           "--pair", str(TILE_PAIR),
+           "--pair", str(TILE_PAIR), "--spread", str(TILE_SPREAD),
            "--payload-npz", npz, "--device", str(device), "--sweep", sweep, "--out", out]
     if multi:
         cmd += ["--batch-sig-max", str(TILE_CFG3_SIG_MAX)]

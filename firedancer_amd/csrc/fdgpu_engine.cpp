@@ -81,6 +81,7 @@ struct Slot {
   uint64_t ws_sig = 0;        /* sized on demand to the largest batch the slot has carried */
   int64_t ticket = -1;      /* -1: free */
   uint64_t k_sigs = 0;      /* signatures (the launch's bound) of its verify: FDGPU_FLAG_PAIR_AUTO's load */
+  uint64_t k_lanes = 0;     /* and its lanes (two per signature for the two-lane kernel): FDGPU_FLAG_SPREAD_AUTO's */
   bool staged = false;      /* reserved by fdgpu_stage_acquire, not yet submitted */
   bool held = false;        /* polled with fdgpu_poll_keep, awaiting fdgpu_release */
   uint64_t txn_cnt = 0;
@@ -420,6 +421,7 @@ static bool bucket(const fdgpu_engine_t *e) { return !(e->cfg.flags & FDGPU_FLAG
 /* the kernels' flags for this engine's configuration */
 static uint32_t kflags(const fdgpu_engine_t *e) {
   return ((e->cfg.flags & FDGPU_FLAG_REF_MAPPING) ? FDGPU_FLAG_REF_MAP : 0u) |
+         ((e->cfg.flags & FDGPU_FLAG_SPREAD) ? FDGPU_FLAG_KSPREAD : 0u) |
          ((e->cfg.flags & FDGPU_FLAG_FULL_PATH) ? FDGPU_FLAG_KFULL : 0u) |
          ((e->cfg.flags & FDGPU_FLAG_KEY_CACHE) ? FDGPU_FLAG_KCACHE : 0u) |
          ((e->cfg.flags & FDGPU_FLAG_PAIR) && !(e->cfg.flags & FDGPU_FLAG_KEY_CACHE) ? FDGPU_FLAG_KPAIR : 0u);
@@ -436,17 +438,33 @@ static uint32_t kflags(const fdgpu_engine_t *e) {
    which does ~1.4x less work per signature. */
 static constexpr uint64_t FDGPU_PAIR_AUTO_SIGS = 49152;
 
+/* FDGPU_FLAG_SPREAD_AUTO: a ring batch's verify blocks take one CU each
+   (FDGPU_FLAG_KSPREAD: dynamic LDS that leaves no room for a second block)
+   while its lanes and those of the engine's running batches fit the chip
+   one block per CU (256 CUs x 256 lanes).  Concurrent launches from other
+   streams otherwise stack two blocks on a CU while other CUs idle: four
+   16 K launches at once verify 82 M sigs/s spread against 55 M packed, but
+   spread caps the chip at ~89 M where packing reaches 106 M with 12+
+   launches (profiles/r04/spread.md). */
+static constexpr uint64_t FDGPU_SPREAD_AUTO_LANES = 65536;
+
 /* the kernel flags of slot s's ring batch of n_sig signatures (ring_mu held) */
 static uint32_t ring_kflags(fdgpu_engine_t *e, Slot *s, uint64_t n_sig) {
   uint32_t f = kflags(e);
+  const uint64_t auto_flags = e->cfg.flags & (FDGPU_FLAG_PAIR_AUTO | FDGPU_FLAG_SPREAD_AUTO);
   s->k_sigs = n_sig;
-  if ((e->cfg.flags & FDGPU_FLAG_PAIR_AUTO) && !(f & FDGPU_FLAG_KCACHE) && n_sig <= FDGPU_PAIR_AUTO_SIGS) {
-    uint64_t load = n_sig;
+  if (auto_flags && !(f & FDGPU_FLAG_KCACHE)) {
+    uint64_t load = n_sig, lanes = 0;
     for (const auto &c : e->slots)
-      if (&c != s && c.ticket >= 0 && !(e->flag_poll && __atomic_load_n(c.h_flag, __ATOMIC_ACQUIRE) == c.flag_seq))
+      if (&c != s && c.ticket >= 0 && !(e->flag_poll && __atomic_load_n(c.h_flag, __ATOMIC_ACQUIRE) == c.flag_seq)) {
         load += c.k_sigs;
-    if (load <= FDGPU_PAIR_AUTO_SIGS) f |= FDGPU_FLAG_KPAIR;
+        lanes += c.k_lanes;
+      }
+    if ((auto_flags & FDGPU_FLAG_PAIR_AUTO) && load <= FDGPU_PAIR_AUTO_SIGS) f |= FDGPU_FLAG_KPAIR;
+    lanes += (f & FDGPU_FLAG_KPAIR) ? 2 * n_sig : n_sig;
+    if ((auto_flags & FDGPU_FLAG_SPREAD_AUTO) && lanes <= FDGPU_SPREAD_AUTO_LANES) f |= FDGPU_FLAG_KSPREAD;
   }
+  s->k_lanes = (f & FDGPU_FLAG_KPAIR) ? 2 * n_sig : n_sig;
   return f;
 }
 
@@ -1635,7 +1653,7 @@ bool sync_run(SyncState &st, const std::vector<SyncReq *> &batch) {
     /* a call's batch is small (one txn per concurrent caller): the two-lane
        kernel's shorter wave is the call's latency (FDGPU_SYNC_PAIR=0: off) */
     const char *sp = getenv("FDGPU_SYNC_PAIR");
-    cfg.flags = (sp && sp[0] == '0') ? 0u : FDGPU_FLAG_PAIR_AUTO;
+    cfg.flags = (sp && sp[0] == '0') ? 0u : FDGPU_FLAG_PAIR_AUTO | FDGPU_FLAG_SPREAD_AUTO;
     cfg.max_arena = std::min<uint64_t>(std::max<uint64_t>(SYNC_BATCH_MAX * (96 * 16 + 1232), need * 2),
                                        2 * SYNC_ARENA_MAX);
     const char *dv = getenv("FDGPU_SYNC_DEVICE");

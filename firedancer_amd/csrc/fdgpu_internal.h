@@ -54,6 +54,11 @@ typedef struct {
 #define FDGPU_FLAG_KFULL    2u            /* half-size path: every lane takes the full-length fallback */
 #define FDGPU_FLAG_KCACHE   4u            /* half-size path: one -A decode + table per distinct key */
 #define FDGPU_FLAG_KPAIR    8u            /* half-size path, two lanes per signature (fdgpu_verify_pair_kernel) */
+#define FDGPU_FLAG_KSPREAD  16u           /* one verify block per CU: dynamic LDS that leaves no room for a second */
+/* the verify block's static LDS is 80 KB (two fill a CU's 160 KB), the
+   two-lane block's 40 KB: these make one block per CU the most that fits */
+#define FDGPU_SPREAD_LDS       1024u
+#define FDGPU_SPREAD_LDS_PAIR  (40u * 1024u + 1024u)
 /* SHA-512 block-count groups of the host-side bucketing (expand): messages of
    more blocks than this share the last group */
 #define FDGPU_NBLK_GROUPS   32u

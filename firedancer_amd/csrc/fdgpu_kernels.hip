@@ -1625,10 +1625,12 @@ hipError_t fdgpu_launch_verify_sigs(const uint8_t *d_arena, const fdgpu_sig_desc
     key_of = kof;
   } else if (flags & FDGPU_FLAG_KPAIR) {
     const uint32_t pgrid = (2u * n_sig + FDGPU_BLOCK - 1) / FDGPU_BLOCK;     /* two lanes per signature */
-    hipLaunchKernelGGL(fdgpu_verify_pair_kernel, dim3(pgrid), dim3(FDGPU_BLOCK), 0, stream, d_arena, d_sigs, n_sig,
+    hipLaunchKernelGGL(fdgpu_verify_pair_kernel, dim3(pgrid), dim3(FDGPU_BLOCK),
+                       (flags & FDGPU_FLAG_KSPREAD) ? FDGPU_SPREAD_LDS_PAIR : 0, stream, d_arena, d_sigs, n_sig,
                        d_n_sig, d_btab, d_ws, d_perm, d_sig_codes, queue, cnt, flags);
   } else {
-    hipLaunchKernelGGL(fdgpu_verify_hs_kernel<false>, dim3(grid), dim3(FDGPU_BLOCK), 0, stream, d_arena, d_sigs, n_sig,
+    hipLaunchKernelGGL(fdgpu_verify_hs_kernel<false>, dim3(grid), dim3(FDGPU_BLOCK),
+                       (flags & FDGPU_FLAG_KSPREAD) ? FDGPU_SPREAD_LDS : 0, stream, d_arena, d_sigs, n_sig,
                        d_n_sig, d_btab, d_ws, d_perm, d_sig_codes, queue, cnt, flags, nullptr, nullptr);
   }
   hipLaunchKernelGGL(fdgpu_full_kernel, dim3(slow_blocks), dim3(FDGPU_BLOCK), 0, stream, d_ws, d_perm, d_sig_codes,

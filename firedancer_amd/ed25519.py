@@ -27,6 +27,8 @@ FLAG_KEY_CACHE = 8      # one A decode + table per distinct public key of a batc
 FLAG_PAIR = 16          # two lanes per signature: a shorter verify for batches that leave the GPU idle
 FLAG_PAIR_AUTO = 32     # the two-lane kernel for small ring batches while the engine is otherwise idle
 FLAG_MERGE = 64         # gathered batches' verifies merged into shared launches
+FLAG_SPREAD = 128       # one verify block per CU
+FLAG_SPREAD_AUTO = 256  # ... while the engine's batches fit the chip that way
 
 # fdgpu_txn_t as a numpy record (msg_off, msg_sz, sig_off, pub_off, sig_cnt)
 TXN_DTYPE = np.dtype([("msg_off", "<u4"), ("msg_sz", "<u4"), ("sig_off", "<u4"),
@@ -102,13 +104,15 @@ class VerifyEngine:
     verify_txns() is submit + blocking poll."""
 
     def __init__(self, device=0, max_txn=1 << 16, max_sig=None, max_arena=None, ring_depth=2, ref_mapping=False,
-                 bucket=True, full_path=False, key_cache=False, pair=False, pair_auto=False, merge=False):
+                 bucket=True, full_path=False, key_cache=False, pair=False, pair_auto=False, merge=False,
+                 spread=False, spread_auto=False):
         L = _lib.lib()
         # max_sig default: 12 signatures per txn (FD_TXN_ACTUAL_SIG_MAX), as the engine's own default
         self.max_sig = max_sig or 12 * max_txn
         flags = ((FLAG_REF_MAPPING if ref_mapping else 0) | (0 if bucket else FLAG_NO_BUCKET) |
                  (FLAG_FULL_PATH if full_path else 0) | (FLAG_KEY_CACHE if key_cache else 0) |
-                 (FLAG_PAIR if pair else 0) | (FLAG_PAIR_AUTO if pair_auto else 0) | (FLAG_MERGE if merge else 0))
+                 (FLAG_PAIR if pair else 0) | (FLAG_PAIR_AUTO if pair_auto else 0) | (FLAG_MERGE if merge else 0) |
+                 (FLAG_SPREAD if spread else 0) | (FLAG_SPREAD_AUTO if spread_auto else 0))
         cfg = _lib.FdgpuCfg(max_txn, self.max_sig, max_arena or 1232 * max_txn, ring_depth, flags)
         self._cfg = cfg
         self.max_arena = cfg.max_arena

@@ -136,6 +136,11 @@ typedef struct {
                                       batch's gather / parse before it and its finish after it on the batch's
                                       slot stream (a verify is launched from submit and poll calls, so the
                                       caller polls; a blocking poll launches what is waiting).  Same codes */
+#define FDGPU_FLAG_SPREAD    128u /* one verify block per CU (the launch reserves LDS a second block would need):
+                                      concurrent small launches from several streams then spread over the CUs
+                                      instead of stacking two blocks on one while others idle.  Same codes */
+#define FDGPU_FLAG_SPREAD_AUTO 256u /* FDGPU_FLAG_SPREAD for a ring batch while its lanes and those of the
+                                      engine's running batches fit the chip one block per CU (65,536) */
 #define FDGPU_FLAG_PAIR_AUTO 32u  /* the FDGPU_FLAG_PAIR kernel for a ring batch while it and the engine's
                                       running batches hold <= 48 K signatures (launch bounds): the GPU has idle
                                       wave slots, latency is a wave's lifetime; the one-lane kernel otherwise.

@@ -94,7 +94,7 @@ def test_engine_flags_match_header():
     hdr = {m.group(1): int(m.group(2)) for m in re.finditer(r"#define\s+FDGPU_FLAG_(\w+)\s+(\d+)u", text)}
     py = {"REF_MAPPING": ed.FLAG_REF_MAPPING, "NO_BUCKET": ed.FLAG_NO_BUCKET, "FULL_PATH": ed.FLAG_FULL_PATH,
           "KEY_CACHE": ed.FLAG_KEY_CACHE, "PAIR": ed.FLAG_PAIR, "PAIR_AUTO": ed.FLAG_PAIR_AUTO,
-          "MERGE": ed.FLAG_MERGE}
+          "MERGE": ed.FLAG_MERGE, "SPREAD": ed.FLAG_SPREAD, "SPREAD_AUTO": ed.FLAG_SPREAD_AUTO}
     assert hdr == py, (hdr, py)
 
 

@@ -23,6 +23,7 @@ def test_tile_cmd_parses():
     assert args.hw_queues == bench.TILE_HW_QUEUES and args.reps == bench.TILE_REPS
     assert args.depth_lg == 21                                       # a prefill fits its links
     assert args.pair == bench.TILE_PAIR == 2                           # FDGPU_FLAG_PAIR_AUTO tile engines
+    assert args.spread == bench.TILE_SPREAD == 2                       # FDGPU_FLAG_SPREAD_AUTO
     # paced runs: the reference's quic -> verify depth (receive_buffer_size, default.toml:888-893), and a
     # stream long enough that the producers can lap the tiles (>= 20 x the depth per link)
     assert args.depth_lg_paced == 14 and args.lap_guard == 1

@@ -594,3 +594,33 @@ def test_pair_auto_ring(oracle):
             assert (got == exp).all(), np.nonzero(got != exp)[0][:10]
     finally:
         eng.close()
+
+
+def test_spread_launch(vectors, oracle):
+    """FDGPU_FLAG_SPREAD (one verify block per CU: the launch reserves the
+    LDS a second block would need) with the one-lane and the two-lane
+    kernel, and FDGPU_FLAG_SPREAD_AUTO with PAIR_AUTO over four ring batches
+    in flight: the golden vectors' codes and the oracle's on cfg1 / cfg3
+    sets.  Placement only -- the codes are the same launches'."""
+    import firedancer_amd as fa
+    sets = [workload.cfg1(3000, seed=0xA3A), workload.cfg3(500, seed=0xA3B)]
+    for kw in (dict(spread=True), dict(spread=True, pair=True)):
+        eng = fa.VerifyEngine(0, max_txn=8192, **kw)
+        try:
+            vs, arena, txns = _vector_batch(vectors)
+            codes = eng.verify_txns(arena, txns)
+            bad = [(v["src"], v["tc_id"], v["code"], int(c)) for v, c in zip(vs, codes) if c != v["code"]]
+            assert not bad, (kw, bad[:20])
+            for arena, txns, _ in sets:
+                assert (eng.verify_txns(arena, txns) == oracle.verify_txns(arena, txns, nthreads=8)).all(), kw
+        finally:
+            eng.close()
+    eng = fa.VerifyEngine(0, max_txn=40000, ring_depth=4, pair_auto=True, spread_auto=True)
+    try:
+        more = sets + [workload.cfg1(36000, seed=0xA3C), workload.make_txns(2500, 0xA3D, corrupt=0.5)]
+        tks = [eng.submit(arena, txns) for arena, txns, _ in more]
+        for tk, (arena, txns, _) in zip(tks, more):
+            got = eng.poll(tk, blocking=True)
+            assert (got == oracle.verify_txns(arena, txns, nthreads=8)).all()
+    finally:
+        eng.close()

@@ -82,6 +82,9 @@ def make_parser():
     ap.add_argument("--pair", type=int, default=0,
                     help="(mux tile) verify kernel: 0 one lane per signature, 1 two lanes (FDGPU_FLAG_PAIR), "
                          "2 two lanes while the engine is otherwise idle (FDGPU_FLAG_PAIR_AUTO)")
+    ap.add_argument("--spread", type=int, default=0,
+                    help="(mux tile) verify blocks: 0 as the GPU packs them, 1 one per CU (FDGPU_FLAG_SPREAD), "
+                         "2 one per CU while the engine's batches fit the chip that way (FDGPU_FLAG_SPREAD_AUTO)")
     ap.add_argument("--merge", type=int, default=0,
                     help="(mux tile) 1: FDGPU_FLAG_MERGE engines -- the verifies of an engine's batches ready at "
                          "once run as one launch")
@@ -412,7 +415,7 @@ def engine_pool(args, n, batch, inflight, device):
     dozen, new streams share hardware queues and batches of one tile
     serialise behind another's (a run after a 3-tile run took 2.5x as long
     per batch with the same kernel durations, profiles/r04/tile_run_order.md)."""
-    key = (batch, inflight, device)
+    key = (batch, inflight, device)     # (the flags are per process: a sweep's runs share them)
     pool = _POOL.setdefault(key, [])
     frag_bytes = (tile.TPU_DCACHE_MTU + 63) // 64 * 64
     new = []
@@ -420,7 +423,8 @@ def engine_pool(args, n, batch, inflight, device):
         k = len(pool)
         e = fa.VerifyEngine(device if device is not None else k % args.gpus, max_txn=batch, max_sig=batch * 12,
                             max_arena=batch * frag_bytes, ring_depth=inflight, pair=args.pair == 1,
-                            pair_auto=args.pair == 2, merge=bool(getattr(args, "merge", 0)))
+                            pair_auto=args.pair == 2, merge=bool(getattr(args, "merge", 0)),
+                            spread=getattr(args, "spread", 0) == 1, spread_auto=getattr(args, "spread", 0) == 2)
         if getattr(args, "reserve", 1):
             e.reserve()      # every slot sized for the largest batch now, not inside the run (as a tile's init does)
         pool.append(e)
