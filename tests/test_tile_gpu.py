@@ -156,6 +156,39 @@ def test_vmux_mixed_stream_vs_model_gpu(engines, oracle, gpu_parse):
     ver.close()
 
 
+def test_vmux_bench_engine_flags_gpu(oracle):
+    """The tile over engines opened as bench.py's tile lines open them
+    (FDGPU_FLAG_PAIR_AUTO | FDGPU_FLAG_SPREAD_AUTO): small batches take the
+    two-lane kernel, one block per CU; every outcome and the published
+    stream (gathered mode: out frags written by the GPU) equal the
+    sequential model's."""
+    from test_tile import _mixed_stream
+    es = [fa.VerifyEngine(0, max_txn=4096, max_sig=4096 * 12, max_arena=4096 * 1232, ring_depth=4, pair_auto=True,
+                          spread_auto=True) for _ in range(2)]
+    try:
+        ps = _mixed_stream(3000, seed=0x51)
+        seed = 0xBEEF
+        inl = tile.Link(1 << 13, 1232)
+        outl = tile.Link(1 << 13, tile.TPU_DCACHE_MTU, data_sz=tile.vmux_dcache_data_sz(1 << 13, 257, 4))
+        ver = tile.EngineVerifier(es)
+        vm = tile.VerifyMuxTile(inl, outl, ver, hashmap_seed=seed, batch_txn_max=257, inflight_max=4,
+                                log_max=1 << 14, gpu_parse=2)
+        for p in ps:
+            inl.publish(p)
+        vm.run(len(ps), timeout_s=60)
+        exp, pub = tile_model.verify_tile_model(ps, seed, lambda a, t: oracle.verify_txns(a, t))
+        seqs, codes = vm.log()
+        assert seqs.tolist() == list(range(len(ps))) and codes.tolist() == exp
+        outs = outl.drain()
+        assert [(m["sig"], tile.split_verify_output(f)) for m, f in outs] == [(t, (p, raw)) for p, raw, t in pub]
+        assert vm.stats()["verify_errors"] == 0 and vm.idle()
+        vm.close()
+        ver.close()
+    finally:
+        for e in es:
+            e.close()
+
+
 @pytest.mark.parametrize("gpu_parse", [0, 2])
 def test_vmux_two_tiles_share_engines_gpu(engines, oracle, gpu_parse):
     """Two verify mux tiles on their own threads take the round-robin shares
