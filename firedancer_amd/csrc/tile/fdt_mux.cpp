@@ -455,12 +455,6 @@ struct fdgpu_vmux {
   int error = 0;
   uint32_t calls = 0;                     /* after_credit calls (rate-limits verifier polls) */
   uint64_t due_tsc = 0, stall_max_tick = 0;   /* the every-32nd call's time stamp counter, the longest gap */
-  /* the tile's own clock for its batch timing and stats: the time stamp
-     counter scaled to ns (a clock_gettime per poll was a tenth of the
-     tile's polling time); published frags keep CLOCK_MONOTONIC stamps */
-  double ns_per_tick = 0;
-  uint64_t vclock() const { return (uint64_t)((double)__rdtsc() * ns_per_tick); }
-  uint64_t gpu_ns_avg = 0;                /* batches' submit -> done time, smoothed: polls wait for part of it */
   uint64_t caught_up_cnt = 0;             /* polls of an in link that found nothing new ... */
   bool sees_caught_up = false;            /* ... counted (the loop's own instance; a callback table: the timer alone) */
   fdgpu_vtile_stats_t st{};
@@ -515,18 +509,16 @@ struct fdgpu_vmux {
   /* a non-blocking poll of one submitted batch: 1 done (its results are
      in the batch, its verifier slot is free), 0 pending, -1 error */
   int poll_one(VBatch *b, int *poll_in) {
-    const uint64_t p0 = vclock();
+    const uint64_t p0 = now_ns();
     const int rc = gather ? ver.poll_io(ver.ctx, b->ticket, b->codes.data(), b->tags.data(), b->out_szs.data(), 0)
                    : gpu_parse ? ver.poll_frags(ver.ctx, b->ticket, b->codes.data(), b->trailers.data(), 0)
                                : ver.poll(ver.ctx, b->ticket, b->codes.data(), 0);
-    const uint64_t p1 = vclock(), dp = p1 - p0;
+    const uint64_t p1 = now_ns(), dp = p1 - p0;
     st.poll_ns += dp;
     st.polls++;
     if (rc == FDGPU_PENDING) return 0;
     st.poll_done_ns += dp;
-    const uint64_t g = p1 - b->t_submit;
-    st.batch_gpu_ns += g;
-    gpu_ns_avg = gpu_ns_avg ? (7 * gpu_ns_avg + g) / 8 : g;
+    st.batch_gpu_ns += p1 - b->t_submit;
     if (rc != FDGPU_OK) { error = rc; *poll_in = 0; return -1; }
     b->done = true;
     busy--;
@@ -540,22 +532,17 @@ struct fdgpu_vmux {
      frees its verifier slot for the next batch, while publishing waits for
      the oldest. */
   void resolve(fdt_mux_context_t *mux, int *poll_in) {
-    if (inflight.empty()) return;
-    /* a batch is not polled before it can have finished: half the smoothed
-       round trip of the batches before it, at most 0.5 ms (a poll is a
-       runtime call; the tile used to make ~1,000 of them per batch) */
-    const uint64_t now = vclock(), hold = std::min<uint64_t>(gpu_ns_avg / 2, 500000);
-    if (busy > 1 && !(sweeps++ & 7u))          /* every 8th call: a slot freed a few us late costs little */
+    if (busy > 1 && !(sweeps++ & 7u))          /* every 8th call: a poll is a runtime call, a slot freed a few us late costs little */
       for (size_t j = 1; j < inflight.size(); j++)
-        if (!inflight[j]->done && now - inflight[j]->t_submit >= hold && poll_one(inflight[j], poll_in) < 0) return;
+        if (!inflight[j]->done && poll_one(inflight[j], poll_in) < 0) return;
     while (!inflight.empty()) {
       VBatch *b = inflight.front();
-      if (!b->done && (now - b->t_submit < hold || poll_one(b, poll_in) <= 0)) return;
+      if (!b->done && poll_one(b, poll_in) <= 0) return;
       const uint64_t t_pub = now_ns();
       struct Acc { uint64_t &ns; uint64_t t0; ~Acc() { ns += now_ns() - t0; } } acc{st.publish_ns, t_pub};
       const uint32_t tspub = (uint32_t)t_pub;
       if (!(gather ? resolve_gather(*b, mux, poll_in, tspub) : resolve_items(*b, mux, poll_in, tspub))) return;
-      if (lat.size() < (1u << 22) && b->cnt) lat.push_back(vclock() - b->t_first);
+      if (lat.size() < (1u << 22) && b->cnt) lat.push_back(now_ns() - b->t_first);
       inflight.pop_front();
       b->reset();
       pool.push_back(b);
@@ -730,11 +717,11 @@ struct fdgpu_vmux {
 
   void submit() {
     if (!open || !open->cnt) return;
-    const uint64_t s0 = vclock();
+    const uint64_t s0 = now_ns();
     struct Acc {
-      const fdgpu_vmux *t; uint64_t &ns, &mx; uint64_t t0;
-      ~Acc() { const uint64_t d = t->vclock() - t0; ns += d; mx = std::max(mx, d); }
-    } acc{this, st.submit_ns, st.submit_max_ns, s0};
+      uint64_t &ns, &mx; uint64_t t0;
+      ~Acc() { const uint64_t d = now_ns() - t0; ns += d; mx = std::max(mx, d); }
+    } acc{st.submit_ns, st.submit_max_ns, s0};
     if (gather && lap_margin != ~0ull) lap_guard(*open);    /* also while the batch fills or waits for a slot */
     /* a partial batch goes out once its oldest frag waited batch_wait_ns and
        the tile has since found its in links drained; while frags keep
@@ -760,7 +747,7 @@ struct fdgpu_vmux {
     if (t == FDGPU_ERR_INVAL) { reject_open(); return; }
     if (t < 0) { error = (int)t; return; }
     open->ticket = t;
-    open->t_submit = vclock();
+    open->t_submit = now_ns();
     st.batch_fill_ns += open->t_submit - open->t_first;
     inflight.push_back(open);
     busy++;
@@ -838,7 +825,7 @@ __attribute__((always_inline)) inline void vm_after_frag(void *ctx, uint64_t in_
     /* reserve the out frag's room from the size alone (the tile never reads
        the payload); the GPU writes [payload][pad][fd_txn_t][u16] there */
     VBatch &b = *t->open;
-    if (!b.cnt) { b.first_chunk = t->out_chunk; b.t_first = t->vclock(); b.cu_first = t->caught_up_cnt; }
+    if (!b.cnt) { b.first_chunk = t->out_chunk; b.t_first = now_ns(); b.cu_first = t->caught_up_cnt; }
     const uint64_t off = (t->out_chunk - b.first_chunk) << FDT_CHUNK_LG_SZ;
     const uint32_t cap = t->cap_of[payload_sz];                  /* payload_sz <= FDT_TPU_MTU: during_frag */
     const uint32_t li = (uint32_t)t->cur_in;
@@ -876,7 +863,7 @@ __attribute__((always_inline)) inline void vm_after_frag(void *ctx, uint64_t in_
     (void)txn;
     const uint64_t sc = t->cur_sc, fp = t->cur_fp;
     VBatch &b = *t->open;
-    if (!b.cnt) { b.first_chunk = t->out_chunk; b.t_first = t->vclock(); b.cu_first = t->caught_up_cnt; }
+    if (!b.cnt) { b.first_chunk = t->out_chunk; b.t_first = now_ns(); b.cu_first = t->caught_up_cnt; }
     const uint64_t off = (t->out_chunk - b.first_chunk) << FDT_CHUNK_LG_SZ;
     __builtin_prefetch(b.items.data() + b.items.size() + 6, 1);      /* reserved: stores a few frags ahead */
     __builtin_prefetch(b.frags.data() + b.frags.size() + 12, 1);
@@ -909,7 +896,7 @@ __attribute__((always_inline)) inline void vm_after_frag(void *ctx, uint64_t in_
   const uint64_t new_sz = toff + tsz + 2;
   const fdt_txn_t *tt = (const fdt_txn_t *)txn_t;
   VBatch &b = *t->open;                                 /* after_credit made sure one is open */
-  if (!b.cnt) { b.first_chunk = t->out_chunk; b.t_first = t->vclock(); b.cu_first = t->caught_up_cnt; }
+  if (!b.cnt) { b.first_chunk = t->out_chunk; b.t_first = now_ns(); b.cu_first = t->caught_up_cnt; }
   const uint64_t off = (t->out_chunk - b.first_chunk) << FDT_CHUNK_LG_SZ;
   fdgpu_txn_t d;
   d.msg_off = (uint32_t)(off + tt->message_off);
@@ -1066,7 +1053,6 @@ fdgpu_vmux_t *fdgpu_vmux_new(const fdgpu_vmux_cfg_t *cfg, fdgpu_verifier_t ver) 
   t->ver = ver;
   t->out_chunk = c.out_chunk0;
   t->rr_mask = (c.round_robin_cnt & (c.round_robin_cnt - 1)) == 0 ? c.round_robin_cnt - 1 : 0;
-  t->ns_per_tick = 1.0 / tick_per_ns();
   uint64_t n = 1;
   while (n < c.cr_max) n <<= 1;
   t->pub_chunk.assign(n, 0);
