@@ -634,8 +634,9 @@ class PyVerifier:
     out of order, as the engine's do on their own streams; `done` records
     the order the batches completed in)."""
 
-    def __init__(self, fn, slots=2, lag=0, lag_fn=None):
+    def __init__(self, fn, slots=2, lag=0, lag_fn=None, read_at_submit=False):
         self.fn, self.slots, self.lag, self.lag_fn = fn, slots, lag, lag_fn
+        self.read_at_submit = read_at_submit          # gathered batches: payloads read at submit, not at the poll
         self.results, self.polls, self.next = {}, {}, 0
         self.batches, self.done, self.lags = [], [], {}
 
@@ -769,7 +770,11 @@ class PyVerifier:
             k = self.next
             self.next += 1
             self.results[k] = None
-            self.io[k] = work
+            if self.read_at_submit:
+                done = work()
+                self.io[k] = lambda: done
+            else:
+                self.io[k] = work
             self.polls[k] = 0
             if self.lag_fn is not None:
                 self.lags[k] = self.lag_fn(k)

@@ -380,11 +380,13 @@ def test_vmux_gather_lap_guard_rescues_waiting_frags(oracle):
 def test_vmux_gather_span_cap_closes_batches(oracle):
     """gpu_parse 2: a batch closes once it spans lap_span_max seqs of a link
     (default depth / 2), whatever its txn cap: 4 round-robin tiles' shares of
-    a 64-deep link go out as batches of at most 32 / 4 frags each."""
+    a 64-deep link go out as batches of at most 32 / 4 frags each.  (The
+    stand-in reads each batch's payloads at submit, as the device does soon
+    after; when the tile polls does not matter here.)"""
     ps = _mixed_stream(400, seed=23)
     inl = tile.Link(64, 1232)
     outl = tile.Link(1 << 10, tile.TPU_DCACHE_MTU, data_sz=(len(ps) + 8) * (tile.TPU_DCACHE_MTU + 64))
-    ver = tile.PyVerifier(oracle_fn(oracle), slots=4)
+    ver = tile.PyVerifier(oracle_fn(oracle), slots=4, read_at_submit=True)
     vm = tile.VerifyMuxTile(inl, outl, ver, hashmap_seed=0x79, batch_txn_max=1000, inflight_max=4, log_max=1 << 12,
                             batch_wait_us=1e6, round_robin_idx=1, round_robin_cnt=4, gpu_parse=2)
     vm.start()
