@@ -819,6 +819,21 @@ int merge_kick(fdgpu_engine_t *e, bool force);
 static int poll_slot(fdgpu_engine_t *e, int64_t ticket, int8_t *txn_codes, int blocking, bool keep,
                      uint8_t *trailers = nullptr, uint64_t *tags = nullptr, uint16_t *out_szs = nullptr) {
   if (!e) return FDGPU_ERR_INVAL;
+  /* a batch still on the device is answered without the ring lock: the
+     caller owns its ticket's slot until a poll returns it done, so the slot's
+     ticket and completion word are stable here; the runtime check below
+     (every 256th poll) and everything else take the lock */
+  bool counted = false;                        /* this poll already counted in the slot's polls */
+  if (!blocking && e->flag_poll && e->merges.empty() && ticket >= 0)
+    for (auto &c : e->slots)
+      if (__atomic_load_n(&c.ticket, __ATOMIC_RELAXED) == ticket) {
+        if (!__atomic_load_n(&c.held, __ATOMIC_RELAXED) &&
+            __atomic_load_n(c.h_flag, __ATOMIC_ACQUIRE) != __atomic_load_n(&c.flag_seq, __ATOMIC_RELAXED)) {
+          counted = true;
+          if ((__atomic_add_fetch(&c.polls, 1u, __ATOMIC_RELAXED) & 255u) != 0) return FDGPU_PENDING;
+        }
+        break;
+      }
   std::unique_lock<std::mutex> lk(e->ring_mu);
   Slot *s = nullptr;
   for (auto &c : e->slots) if (c.ticket == ticket && ticket >= 0 && !c.held) { s = &c; break; }
@@ -842,7 +857,7 @@ static int poll_slot(fdgpu_engine_t *e, int64_t ticket, int8_t *txn_codes, int b
        an error ends the wait (the tile stops instead of polling forever), a
        completed event means the batch is done. */
     if (__atomic_load_n(s->h_flag, __ATOMIC_ACQUIRE) != s->flag_seq) {
-      if ((++s->polls & 255u) != 0) return FDGPU_PENDING;
+      if (!counted && (++s->polls & 255u) != 0) return FDGPU_PENDING;
       const uint64_t now = sp_now();
       if (now - s->last_query < 1000000ull) return FDGPU_PENDING;
       s->last_query = now;

@@ -718,10 +718,6 @@ struct fdgpu_vmux {
   void submit() {
     if (!open || !open->cnt) return;
     const uint64_t s0 = now_ns();
-    struct Acc {
-      uint64_t &ns, &mx; uint64_t t0;
-      ~Acc() { const uint64_t d = now_ns() - t0; ns += d; mx = std::max(mx, d); }
-    } acc{st.submit_ns, st.submit_max_ns, s0};
     if (gather && lap_margin != ~0ull) lap_guard(*open);    /* also while the batch fills or waits for a slot */
     /* a partial batch goes out once its oldest frag waited batch_wait_ns and
        the tile has since found its in links drained; while frags keep
@@ -730,6 +726,12 @@ struct fdgpu_vmux {
     if (!open->closed && (s0 - open->t_first < cfg.batch_wait_ns || (sees_caught_up && caught_up_cnt == open->cu_first)))
       return;
     if (busy >= cfg.inflight_max) return;
+    /* timed from before the lap guard's pass; the calls that return above
+       (most: one every 32 frags) are not, which saves them a clock read */
+    struct Acc {
+      uint64_t &ns, &mx; uint64_t t0;
+      ~Acc() { const uint64_t d = now_ns() - t0; ns += d; mx = std::max(mx, d); }
+    } acc{st.submit_ns, st.submit_max_ns, s0};
     int64_t t;
     if (gather) {
       const size_t n = open->cnt;

@@ -279,7 +279,7 @@ typedef struct {
   uint64_t verify_errors;   /* txns of batches the verifier rejected as malformed (failed, not published) */
   /* where the tile's time goes (ingest_ns: fdgpu_vtile only) */
   uint64_t ingest_ns;       /* polling the in link, copying and parsing frags */
-  uint64_t submit_ns;       /* inside the verifier's submit / stage calls (and the submit-wait checks) */
+  uint64_t submit_ns;       /* inside the verifier's submit / stage calls (fdgpu_vmux: and the lap guard's pass before each) */
   uint64_t poll_ns;         /* inside the verifier's non-blocking polls */
   uint64_t no_slot_steps;   /* steps that could not open a batch: every batch or ring slot in flight */
   uint64_t polls;           /* non-blocking polls (fdgpu_vmux) */
