@@ -280,7 +280,7 @@ typedef struct {
   /* where the tile's time goes (ingest_ns: fdgpu_vtile only) */
   uint64_t ingest_ns;       /* polling the in link, copying and parsing frags */
   uint64_t submit_ns;       /* inside the verifier's submit / stage calls (fdgpu_vmux: and the lap guard's pass before each) */
-  uint64_t poll_ns;         /* inside the verifier's non-blocking polls */
+  uint64_t poll_ns;         /* inside the verifier's non-blocking polls (fdgpu_vmux: every 8th timed, x 8) */
   uint64_t no_slot_steps;   /* steps that could not open a batch: every batch or ring slot in flight */
   uint64_t polls;           /* non-blocking polls (fdgpu_vmux) */
   uint64_t poll_done_ns;    /* the part of poll_ns in polls that completed (the results' read-out) */
