@@ -13,6 +13,7 @@
    Untrusted descriptors are bounds-checked on the host before anything is
    handed to the GPU (offsets + sizes must lie inside the arena). */
 #include <hip/hip_runtime.h>
+#include <immintrin.h>
 
 #include <algorithm>
 #include <atomic>
@@ -1098,6 +1099,7 @@ int64_t fdgpu_submit_frags_io(fdgpu_engine_t *e, fdgpu_frag_io_t const *fio, uin
   const uint64_t src_at = (n * sizeof(fdgpu_frag_ex_t) + 63) & ~63ull;
   const uint64_t chk_at = src_at + ((n * sizeof(uint64_t) + 63) & ~63ull);
   if (!slot_io_bufs(*s, e->cfg)) return FDGPU_ERR_DEVICE;
+  static_assert(sizeof(fdgpu_frag_ex_t) == 16, "one 16-B streaming store per record");
   fdgpu_frag_ex_t *h_fx = (fdgpu_frag_ex_t *)s->h_io;
   uint64_t *h_src = (uint64_t *)(s->h_io + src_at);
   uint64_t *h_chk = (uint64_t *)(s->h_io + chk_at);
@@ -1118,19 +1120,22 @@ int64_t fdgpu_submit_frags_io(fdgpu_engine_t *e, fdgpu_frag_io_t const *fio, uin
     }
     if (!rc || f.src < rc->base || f.src + q > rc->end) rc = region_of(e, (uintptr_t)f.src, q);
     if (!rc) { set_err("frag %llu: payload not inside a registered region", (unsigned long long)t); return FDGPU_ERR_INVAL; }
-    h_src[t] = rc->dbase + (f.src - rc->base);
-    h_fx[t] = fdgpu_frag_ex_t{(uint32_t)dev_off, f.sz, f.out_off, f.out_cap};
-    if (f.link) {
-      h_chk[2 * t] = ldev[f.link - 1] + (f.seq & lmask[f.link - 1]) * 32u;    /* fd_frag_meta_t.seq: offset 0 */
-      h_chk[2 * t + 1] = f.seq;
+    /* streaming stores: the records are for the device (read over the bus),
+       not this core -- no line fills for them, nothing for the bus to snoop */
+    _mm_stream_si64((long long *)&h_src[t], (long long)(rc->dbase + (f.src - rc->base)));
+    _mm_stream_si128((__m128i *)&h_fx[t], _mm_set_epi32((int)f.out_cap, (int)f.out_off, (int)f.sz, (int)dev_off));
+    if (f.link) {                                       /* {line address, seq}; fd_frag_meta_t.seq: offset 0 */
+      _mm_stream_si128((__m128i *)&h_chk[2 * t],
+                       _mm_set_epi64x((long long)f.seq, (long long)(ldev[f.link - 1] + (f.seq & lmask[f.link - 1]) * 32u)));
       any_chk = true;
     } else {
-      h_chk[2 * t] = 0;
+      _mm_stream_si64((long long *)&h_chk[2 * t], 0);
     }
     dev_off += q;
     if (dev_off > e->cfg.max_arena) { set_err("frags exceed the engine's arena"); return FDGPU_ERR_INVAL; }
     bound += fdt_frag_sig_bound(f.sz);
   }
+  _mm_sfence();                                        /* the streamed records reach memory before the launches */
   if (bound > e->cfg.max_sig) { set_err("batch may exceed max_sig (%llu)", (unsigned long long)e->cfg.max_sig); return FDGPU_ERR_INVAL; }
   const uint64_t sp1 = g_sp_on ? sp_now() : 0;
   if (!slot_ws(*s, bound)) return FDGPU_ERR_DEVICE;
