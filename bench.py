@@ -433,8 +433,11 @@ TILE_PAIR = 2
 TILE_SPREAD = 2
 # multi-signature frags: a batch also closes at this many signatures by the frag-size bound the tile sees
 # (~9.5 per cfg3 frag for ~6.5 real): ~2.6 K cfg3 txns, so 8 batches in flight are ~1.3 ms of GPU work
-# (49152: 1-tile p99 batch 5.8 ms, 2 tiles 59-65 M sig/s; 24576: 3.0 ms, 67-70 M; profiles/r04/tile_run_order.md)
+# (49152: 1-tile p99 batch 5.8 ms, 2 tiles 59-65 M sig/s; 24576: 3.0 ms, 67-70 M; profiles/r04/tile_run_order.md).
+# Two tiles share the chip, so each takes half-size batches: 16384 gave two tiles 65.7 M sigs/s at p99 4.7 ms
+# against 24576's 69.0 M at 7.2 ms (profiles/r04/tile_cfg3_cap/)
 TILE_CFG3_SIG_MAX = 24576
+TILE_CFG3_SIG_MAX_BY_TILES = {1: 24576, 2: 16384}
 TILE_RUNS_CFG3 = (  # the same tile over cfg3 frags (1-12 signatures, payloads up to the 1232-B MTU: SURVEY 8(d) cfg5)
     ("mux1_capacity_cfg3", 1, 1, -1.0),
     ("mux2_capacity_cfg3", 2, 2, -1.0),
@@ -450,7 +453,9 @@ def tile_cmd(device, cpus, npz, out, runs=TILE_RUNS, multi=0):
     its HIP runtime gives the tile engines' slot streams hardware queues of
     their own, instead of the ones this process's headline, latency and ingest
     engines already hold (shared queues serialise the tiles' batches)."""
-    sweep = ";".join(f"{tiles_n},{TILE_BATCH},{TILE_INFLIGHT},{rate:g},{prods}" for _, tiles_n, prods, rate in runs)
+    sweep = ";".join(f"{tiles_n},{TILE_BATCH},{TILE_INFLIGHT},{rate:g},{prods}" +
+                     (f",{TILE_CFG3_SIG_MAX_BY_TILES.get(tiles_n, TILE_CFG3_SIG_MAX)}" if multi else "")
+                     for _, tiles_n, prods, rate in runs)
     cmd = [sys.executable, os.path.join(REPO, "tools", "bench_tile.py"), "--mux", "1", "--gpu-parse", "2",
            "--multi", str(int(multi)), "--producers-same-as-tiles", "1", "--depth-lg", str(TILE_DEPTH_LG_PREFILL),
            "--depth-lg-paced", str(TILE_DEPTH_LG_PACED), "--paced-reps", str(TILE_PACED_REPS),
@@ -492,6 +497,7 @@ def _tile_child(device, cpus, arena, txns, modes, runs, tag=""):
         out[f"tile_{name}_txns_per_s"] = res["txns_per_s"]
         if tag:
             out[f"tile_{name}_sigs_per_s"] = res["sigs_per_s"]
+            out[f"tile_{name}_batch_sig_max"] = res["batch_sig_max"]
         out[f"tile_{name}_batch_latency_ms_p50_p99"] = [lat["p50"], lat["p99"]]
         out[f"tile_{name}_link_depth"] = res["link_depth"]
         if rate > 0:       # what the producers achieved (the line's name is the rate asked of them)
@@ -540,7 +546,8 @@ def tile_lines(device, arena, txns, modes, cpus, cfg3=None):
                           "fd_txn_parse, verify, dedup tag and out-frag assembly on the GPU; muxT: T verify tiles "
                           "reading P quic->verify links (one producer thread each; P = T for capacity, 2T paced), one engine "
                           "per tile on this GPU, "
-                          f"cfg1 frags (_cfg3: cfg3 frags), {TILE_BATCH}-txn batches, {TILE_INFLIGHT} in flight, {TILE_HW_QUEUES} HIP hardware "
+                          f"cfg1 frags (_cfg3: cfg3 frags, batches closed at _batch_sig_max signatures by the frag-size "
+                          f"bound: half-size for two tiles), {TILE_BATCH}-txn batches, {TILE_INFLIGHT} in flight, {TILE_HW_QUEUES} HIP hardware "
                           "queues, in a child process (tools/bench_tile.py); capacity: every frag published into "
                           f"2^{TILE_DEPTH_LG_PREFILL}-deep links before the tiles start, timed from tile start to the "
                           f"last outcome; paced_R: R txn/s asked of the producers in total (achieved: _offered_txns_per_s) "

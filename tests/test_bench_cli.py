@@ -50,3 +50,8 @@ def test_tile_cmd_cfg3():
     assert args.batch_sig_max == bench.TILE_CFG3_SIG_MAX
     assert len(args.sweep.split(";")) == len(bench.TILE_RUNS_CFG3)
     assert all(r[3] == -1.0 for r in bench.TILE_RUNS_CFG3)       # capacity lines
+    # each run's signature cap (the sweep's sixth field): half-size batches when two tiles share the chip
+    runs = [tuple(float(x) for x in r.split(",")) for r in args.sweep.split(";")]
+    for (name, tiles_n, prods, rate), run in zip(bench.TILE_RUNS_CFG3, runs):
+        assert len(run) == 6 and run[5] == bench.TILE_CFG3_SIG_MAX_BY_TILES[tiles_n]
+    assert bench.TILE_CFG3_SIG_MAX_BY_TILES[2] < bench.TILE_CFG3_SIG_MAX_BY_TILES[1] == bench.TILE_CFG3_SIG_MAX

@@ -66,7 +66,8 @@ def make_parser():
                     help="GPU_MAX_HW_QUEUES for this process (applied before HIP starts; 0: the environment's)")
     ap.add_argument("--out", default="")
     ap.add_argument("--sweep", default="",
-                    help="';'-separated runs of 'tiles,batch,inflight,rate[,producers]' over the same txns")
+                    help="';'-separated runs of 'tiles,batch,inflight,rate[,producers[,batch_sig_max]]' over the "
+                         "same txns (batch_sig_max 0: --batch-sig-max)")
     ap.add_argument("--payload-npz", default="",
                     help="take the frags from this .npz (arena, offs, sizes, modes, n_sig: bench.py's tile lines) "
                          "instead of generating --txns")
@@ -121,11 +122,12 @@ def main():
     runs = [r for r in runs for _ in range(max(1, args.reps))]
     ok = True
     lines = []
-    prods0 = args.producers
+    prods0, sig_max0 = args.producers, args.batch_sig_max
     for run in runs:
         tiles_n, batch, inflight, rate = run[:4]
-        # a fifth field sets the run's quic links (producers)
+        # a fifth field sets the run's quic links (producers), a sixth its batches' signature cap
         args.producers = int(run[4]) if len(run) > 4 else int(tiles_n) if args.producers_same_as_tiles else prods0
+        args.batch_sig_max = int(run[5]) if len(run) > 5 and run[5] > 0 else sig_max0
         args.depth_lg = args.depth_lg_paced if rate > 0 and args.depth_lg_paced else depth_lg
         if args.mux:
             res = run_once_mux(args, ps, arena, offs, sizes, n_sig, modes, int(tiles_n), int(batch), int(inflight),
