@@ -454,7 +454,7 @@ struct fdgpu_vmux {
   uint64_t pub_mask = 0, published_total = 0;
   int error = 0;
   uint32_t calls = 0;                     /* after_credit calls (rate-limits verifier polls) */
-  uint64_t due_tsc = 0, stall_max_tick = 0;   /* the every-32nd call's time stamp counter, the longest gap */
+  uint64_t due_tsc = 0, stall_max_tick = 0;   /* the every-64th call's time stamp counter, the longest gap */
   uint64_t caught_up_cnt = 0;             /* polls of an in link that found nothing new ... */
   bool sees_caught_up = false;            /* ... counted (the loop's own instance; a callback table: the timer alone) */
   fdgpu_vtile_stats_t st{};
@@ -731,7 +731,7 @@ struct fdgpu_vmux {
       return;
     if (busy >= cfg.inflight_max) return;
     /* timed from before the lap guard's pass; the calls that return above
-       (most: one every 32 frags) are not, which saves them a clock read */
+       (most: one every 64 frags) are not, which saves them a clock read */
     struct Acc {
       uint64_t &ns, &mx; uint64_t t0;
       ~Acc() { const uint64_t d = now_ns() - t0; ns += d; mx = std::max(mx, d); }
@@ -927,12 +927,12 @@ __attribute__((always_inline)) inline void vm_after_frag(void *ctx, uint64_t in_
 
 /* after_credit runs once per mux loop iteration, i.e. about once per frag:
    the verifier is polled (an event query) and the partial-batch timer read
-   only every 32nd call, or at once when the tile cannot take the next frag
+   only every 64th call, or at once when the tile cannot take the next frag
    or is mid-way through publishing a completed batch. */
 __attribute__((always_inline)) inline void vm_after_credit(void *ctx, fdt_mux_context_t *mux, int *opt_poll_in) {
   auto *t = (fdgpu_vmux *)ctx;
   if (t->error) { *opt_poll_in = 0; return; }
-  const bool due = (++t->calls & 31u) == 0;
+  const bool due = (++t->calls & 63u) == 0;
   if (due) {                                   /* the tile's longest stall between two of these */
     const uint64_t now = __rdtsc();
     if (t->due_tsc) t->stall_max_tick = std::max(t->stall_max_tick, now - t->due_tsc);

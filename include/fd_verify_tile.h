@@ -291,7 +291,7 @@ typedef struct {
                                (FDGPU_CODE_LAPPED; also counted in overrun) */
   uint64_t rescued;         /* gpu_parse 2: payloads the lap guard copied on the tile's core at submit */
   uint64_t submit_max_ns;   /* the longest single batch submit (fdgpu_vmux) */
-  uint64_t stall_max_ns;    /* the longest the tile went between two of its every-32nd-call polls: a
+  uint64_t stall_max_ns;    /* the longest the tile went between two of its every-64th-call polls: a
                                stalled core (descheduled, blocked in a runtime call) (fdgpu_vmux) */
 } fdgpu_vtile_stats_t;
 
