@@ -74,6 +74,8 @@ def parse():
                     help="device batches verified round-robin, each on its own HIP stream (1: one stream)")
     ap.add_argument("--cfg3-txns", type=int, default=150_000,
                     help="multi-signature (cfg3) txns for the secondary device-resident line (0: skip)")
+    ap.add_argument("--host-fed", type=int, default=1,
+                    help="1: add the host-fed line (the cfg2 batch from host memory through the engine's ring)")
     ap.add_argument("--tile", type=int, default=1, help="1: add the cfg5 verify-tile lines (tango in -> GPU -> tango out)")
     ap.add_argument("--adv-txns", type=int, default=1_000_000,
                     help="txns of each adversarial batch (all equation failures / all corrupted R; 0: skip)")
@@ -168,6 +170,7 @@ def aggregate(dist, n_sig, steps, dt):
     return total / dt_max, dt_max
 
 
+FDGPU_ARENA_SLACK = 160   # readable bytes past a batch arena's last payload byte (fdgpu_internal.h)
 RING_DEPTH = 8        # ring slots (one stream + workspace each) of the latency/PCIe engine (8: tools/pcie_probe.py)
 
 
@@ -275,6 +278,79 @@ def latency_and_pcie(eng, arena, txns, batch, nbatches, pin_cpu=None):
             "submit_parts_ms": {"staged": parts, "registered": parts_reg},
             "pcie_inclusive_sigs_per_s_per_gpu": round(pcie, 1),
             "pcie_inclusive_registered_sigs_per_s_per_gpu": round(pcie_reg, 1)}
+
+
+HOST_FED_RING = 3       # 1M-txn slots of the host-fed engine: a batch's upload runs under the previous verify
+HOST_FED_STEPS = 12
+
+
+def host_fed(device, arena, txns, n_sig, ref_codes, value, steps=HOST_FED_STEPS, ring=HOST_FED_RING, pin_cpu=None):
+    """The north-star shim path at the headline size (VERDICT r04 item 2;
+    SURVEY 8(b)(ii), 8(d) "ingest is the only secondary bound"): the same
+    cfg2 batch of 1M txns fed from HOST memory through the engine's ring
+    (fdgpu_submit: per-signature expansion on the host, H2D upload, verify,
+    codes back to the host), `ring` slots, each slot's upload overlapping the
+    other slots' verifies; timed from the first submit to the last batch's
+    codes on the host.  Two feeds: the arena registered with the engine
+    (fdgpu_host_register: the upload is a DMA straight from it) and staged
+    (copied into the slot's pinned arena by the engine's copy threads first).
+    The H2D bytes per batch (arena + 16-B signature descriptors + 4-B
+    permutation + 8-B txn descriptors) over the run give the achieved ingest
+    rate, next to the link's own H2D rate measured in the same run."""
+    from firedancer_amd import VerifyEngine, _lib
+    L = _lib.lib()
+    arena = np.ascontiguousarray(arena, dtype=np.uint8)
+    n_txn = len(txns)
+    eng = VerifyEngine(device, max_txn=n_txn, max_sig=n_sig, max_arena=arena.nbytes, ring_depth=ring)
+    h2d_bytes = arena.nbytes + FDGPU_ARENA_SLACK + n_sig * (16 + 4) + n_txn * 8
+    out = {"host_fed_batch_txns": n_txn, "host_fed_ring_slots": ring, "host_fed_steps": steps,
+           "host_fed_h2d_bytes_per_batch": h2d_bytes}
+    keep = os.sched_getaffinity(0)
+    try:
+        def feed(tag):
+            ok = True
+            tks = [eng.submit(arena, txns) for _ in range(ring)]            # every slot warm (workspace sized)
+            for tk in tks:
+                ok &= bool((eng.poll(tk, blocking=True) == ref_codes).all())
+            if pin_cpu is not None:
+                os.sched_setaffinity(0, {pin_cpu})
+            tks, last = [], None
+            t0 = time.perf_counter()
+            for _ in range(steps):
+                if len(tks) == ring:
+                    last = eng.poll(tks.pop(0), blocking=True)
+                tks.append(eng.submit(arena, txns))
+            for tk in tks:
+                last = eng.poll(tk, blocking=True)
+            dt = time.perf_counter() - t0
+            os.sched_setaffinity(0, keep)
+            ok &= bool((last == ref_codes).all())
+            parts = submit_parts(steps)
+            out[f"host_fed_{tag}_sigs_per_s"] = round(steps * n_sig / dt, 1)
+            out[f"host_fed_{tag}_ms_per_batch"] = round(dt / steps * 1e3, 3)
+            out[f"host_fed_{tag}_h2d_gbps"] = round(steps * h2d_bytes / dt / 1e9, 2)
+            out[f"host_fed_{tag}_submit_parts_ms"] = parts
+            out[f"host_fed_{tag}_codes_equal"] = ok
+
+        eng.host_register(arena)
+        try:
+            out["host_fed_h2d_link_gbps"] = round(L.fdgpu_debug_h2d_gbps(eng._h, arena.ctypes.data,
+                                                                         min(arena.nbytes, 256 << 20), 10), 2)
+            feed("registered")
+        finally:
+            eng.host_unregister(arena)
+        feed("staged")
+    finally:
+        os.sched_setaffinity(0, keep)
+        eng.close()
+    out["host_fed_registered_vs_device_resident"] = round(out["host_fed_registered_sigs_per_s"] / value, 4)
+    out["host_fed_staged_vs_device_resident"] = round(out["host_fed_staged_sigs_per_s"] / value, 4)
+    out["host_fed_note"] = (f"{n_txn} cfg2 txns per batch from host memory through fdgpu_submit ({ring} ring slots: "
+                            "expansion on the host, H2D, verify, codes back), first submit to last codes on the "
+                            "host; registered: DMA straight from the registered arena; staged: copied into pinned "
+                            "slots first; h2d_gbps: the batches' H2D bytes over the run; h2d_link_gbps: 256 MB "
+                            "copies from the registered arena alone (HIP events)")
+    return out
 
 
 def latency_frag_io(eng, arena, txns, ref_codes, batch, nbatches, pin_cpu=None, views_n=4, keep_raw=False):
@@ -445,31 +521,51 @@ TILE_RUNS_CFG3 = (  # the same tile over cfg3 frags (1-12 signatures, payloads u
 
 
 TILE_REPS = 5   # a capacity run drains 1M frags in a few tens of ms: the median of five
+# the deployable shape: the same tile as the engine process
+# (python -m firedancer_amd.engine_proc) over shared-memory links that a producer
+# process (tools/quic_feed.py) publishes into, every page faulted in before the
+# run; each run starts both processes (engine open + warm-up ~3 s), so three runs each
+TILE_RUNS_XPROC = (
+    ("xproc_mux1_paced_16M", 1, 2, 16e6),
+    ("xproc_mux2_paced_24M", 2, 4, 24e6),
+    ("xproc_mux1_capacity", 1, 1, -1.0),
+)
+TILE_REPS_XPROC = 3
+TILE_DEPTH_LG_PREFILL_XPROC = 21      # as the in-process capacity lines: the lap guard never sees a prefilled frag at risk
 
 
-def tile_cmd(device, cpus, npz, out, runs=TILE_RUNS, multi=0):
+def tile_cmd(rank, cpus, npz, out, runs=TILE_RUNS, multi=0, xproc=False):
     """tools/bench_tile.py's command line for the cfg5 runs (tests/test_bench_cli.py
     parses it with bench_tile's own parser).  The tiles run in a child process:
     its HIP runtime gives the tile engines' slot streams hardware queues of
     their own, instead of the ones this process's headline, latency and ingest
-    engines already hold (shared queues serialise the tiles' batches)."""
+    engines already hold (shared queues serialise the tiles' batches).  The
+    child picks its GPU as rank % the devices it sees (--device-rank): this
+    process has not started a HIP runtime when the child runs, so a node of
+    N ranks has at most N GPU processes at any time (a rank's own engines
+    open only after its child has exited)."""
     sweep = ";".join(f"{tiles_n},{TILE_BATCH},{TILE_INFLIGHT},{rate:g},{prods}" +
                      (f",{TILE_CFG3_SIG_MAX_BY_TILES.get(tiles_n, TILE_CFG3_SIG_MAX)}" if multi else "")
                      for _, tiles_n, prods, rate in runs)
     cmd = [sys.executable, os.path.join(REPO, "tools", "bench_tile.py"), "--mux", "1", "--gpu-parse", "2",
            "--multi", str(int(multi)), "--producers-same-as-tiles", "1", "--depth-lg", str(TILE_DEPTH_LG_PREFILL),
            "--depth-lg-paced", str(TILE_DEPTH_LG_PACED), "--paced-reps", str(TILE_PACED_REPS),
-           "--wait-us", "200", "--pin", "1", "--hw-queues", str(TILE_HW_QUEUES), "--reps", str(TILE_REPS),
+           "--wait-us", "200", "--pin", "1", "--hw-queues", str(TILE_HW_QUEUES),
+           "--reps", str(TILE_REPS_XPROC if xproc else TILE_REPS),
            "--pair", str(TILE_PAIR), "--spread", str(TILE_SPREAD),
-           "--payload-npz", npz, "--device", str(device), "--sweep", sweep, "--out", out]
+           "--payload-npz", npz, "--device-rank", str(rank), "--sweep", sweep, "--out", out]
     if multi:
         cmd += ["--batch-sig-max", str(TILE_CFG3_SIG_MAX)]
+    if xproc:
+        cmd += ["--xproc", "1", "--pages", "4k", "--depth-lg", str(TILE_DEPTH_LG_PREFILL_XPROC)]
     if cpus:
         cmd += ["--cpu-list", ",".join(str(c) for c in cpus)]
     return cmd
 
 
-def _tile_child(device, cpus, arena, txns, modes, runs, tag=""):
+def _tile_child(rank, cpus, arena, txns, modes, runs, tag=""):
+    xp = tag == "xproc"
+    reps_n = TILE_REPS_XPROC if xp else TILE_REPS
     """tools/bench_tile.py in a child process over these txns as raw frags:
     {tile_<name>_...} per run (median of TILE_REPS)."""
     import subprocess
@@ -481,21 +577,21 @@ def _tile_child(device, cpus, arena, txns, modes, runs, tag=""):
     with tempfile.TemporaryDirectory() as td:
         npz, res_path = os.path.join(td, "frags.npz"), os.path.join(td, "tile.jsonl")
         np.savez(npz, arena=parena, offs=poffs, sizes=psizes, modes=modes, n_sig=int(txns["sig_cnt"].sum()))
-        r = subprocess.run(tile_cmd(device, cpus, npz, res_path, runs, multi=tag == "cfg3"), capture_output=True,
-                           text=True, timeout=600)
+        r = subprocess.run(tile_cmd(rank, cpus, npz, res_path, runs, multi=tag == "cfg3", xproc=xp),
+                           capture_output=True, text=True, timeout=600)
         if r.returncode not in (0, 1) or not os.path.exists(res_path):
             raise RuntimeError(f"tools/bench_tile.py failed ({r.returncode}): {r.stderr[-2000:]}")
         res_all = [json.loads(x) for x in open(res_path) if x.strip()]
-    if len(res_all) != len(runs) * TILE_REPS:
-        raise RuntimeError(f"tools/bench_tile.py gave {len(res_all)} runs, expected {len(runs) * TILE_REPS}")
+    if len(res_all) != len(runs) * reps_n:
+        raise RuntimeError(f"tools/bench_tile.py gave {len(res_all)} runs, expected {len(runs) * reps_n}")
     for i, (name, tiles_n, prods, rate) in enumerate(runs):
-        reps = res_all[i * TILE_REPS:(i + 1) * TILE_REPS]
+        reps = res_all[i * reps_n:(i + 1) * reps_n]
         assert all(x["tiles"] == tiles_n and x["producers"] == prods for x in reps)
         res = sorted(reps, key=lambda x: x["txns_per_s"])[len(reps) // 2]
         out[f"tile_{name}_txns_per_s_runs"] = [x["txns_per_s"] for x in reps]
         lat = res["batch_latency_ms"]
         out[f"tile_{name}_txns_per_s"] = res["txns_per_s"]
-        if tag:
+        if tag == "cfg3":
             out[f"tile_{name}_sigs_per_s"] = res["sigs_per_s"]
             out[f"tile_{name}_batch_sig_max"] = res["batch_sig_max"]
         out[f"tile_{name}_batch_latency_ms_p50_p99"] = [lat["p50"], lat["p99"]]
@@ -516,7 +612,7 @@ def _tile_child(device, cpus, arena, txns, modes, runs, tag=""):
     return out
 
 
-def tile_lines(device, arena, txns, modes, cpus, cfg3=None):
+def tile_lines(rank, arena, txns, modes, cpus, cfg3=None):
     """BASELINE configs[4] (cfg5) on this rank's GPU: the verify tile in the
     reference's shape -- the fd_verify.c:232-246 callbacks (fdgpu_vmux) on
     the mux loop (fdt_mux_run, FD_MUX_FLAG_COPY | MANUAL_PUBLISH), tcache and
@@ -536,12 +632,22 @@ def tile_lines(device, arena, txns, modes, cpus, cfg3=None):
     # producers and tiles of a run on one CCD when one has room (a tile and its producers on two
     # sockets ran a quarter slower, profiles/r04/tile_host_cost.md)
     cpus = same_l3_first(list(cpus), 6) if cpus else cpus
-    out = _tile_child(device, cpus, arena, txns, modes, TILE_RUNS)
+    out = _tile_child(rank, cpus, arena, txns, modes, TILE_RUNS)
     out["tile_mux2_vs_mux1_capacity"] = round(out["tile_mux2_capacity_txns_per_s"] /
                                               out["tile_mux1_capacity_txns_per_s"], 3)
     if cfg3 is not None:
-        out.update(_tile_child(device, cpus, *cfg3, TILE_RUNS_CFG3, tag="cfg3"))
+        out.update(_tile_child(rank, cpus, *cfg3, TILE_RUNS_CFG3, tag="cfg3"))
         out["tile_cfg3_txns"] = len(cfg3[1])
+    # the deployable shape: producers and tiles in separate processes
+    out.update(_tile_child(rank, cpus, arena, txns, modes, TILE_RUNS_XPROC, tag="xproc"))
+    for name, inproc in (("xproc_mux1_paced_16M", "mux1_paced_16M"), ("xproc_mux2_paced_24M", "mux2_paced_24M")):
+        out[f"tile_{name}_vs_in_process"] = round(out[f"tile_{name}_txns_per_s"] / out[f"tile_{inproc}_txns_per_s"], 3)
+    out["tile_xproc_config"] = ("the same tile in the engine process (python -m firedancer_amd.engine_proc) over "
+                                "/dev/shm links a separate producer process (tools/quic_feed.py) publishes into, "
+                                "every link page faulted in before the run (4 KB pages: this host offers no shared "
+                                "2 MB pages, tile.hugepage_support()); paced: the reference's 16384-deep links; "
+                                f"capacity: one 2^{TILE_DEPTH_LG_PREFILL_XPROC}-deep link prefilled by the producer "
+                                f"process; median of {TILE_REPS_XPROC} runs, each starting both processes")
     out["tile_config"] = ("fdgpu_vmux on fdt_mux_run (the reference's mux-callback verify tile), payload gather, "
                           "fd_txn_parse, verify, dedup tag and out-frag assembly on the GPU; muxT: T verify tiles "
                           "reading P quic->verify links (one producer thread each; P = T for capacity, 2T paced), one engine "
@@ -734,24 +840,25 @@ def main():
     t_gen = time.perf_counter()
     arena, txns, modes = workload.cfg1(args.txns, seed=rank_seed(dist.rank))
     t_gen = time.perf_counter() - t_gen
-    # one process per GPU; more ranks than visible GPUs (a rehearsal of the
-    # multi-rank path on a one-GPU box) share devices round robin
-    device = dist.local_rank
-    if dist.world > 1:
-        import torch
-        ndev = torch.cuda.device_count()
-        device = dist.local_rank % ndev if ndev > 0 else dist.local_rank
     # the cfg5 tile lines first, in their child process, before this process
-    # opens any engine: the tiles' 16+ slot streams then have the device's
-    # hardware queues to themselves (with this process's engines open beside
-    # them, one tile ran 34.5 M txn/s against 38 M alone; profiles/r04/tile_run_order.md)
+    # starts a HIP runtime or opens any engine: the tiles' 16+ slot streams
+    # then have the device's hardware queues to themselves (with this
+    # process's engines open beside them, one tile ran 34.5 M txn/s against
+    # 38 M alone; profiles/r04/tile_run_order.md), and a rank and its child
+    # are never two GPU processes at once
     cfg3 = workload.cfg3(args.cfg3_txns, seed=workload.CFG3_SEED + dist.rank) if args.cfg3_txns else None
     tl = None
     if args.tile and not args.no_extras:
-        tl = tile_lines(device, arena, txns, modes, cpus, cfg3=cfg3)
+        tl = tile_lines(dist.local_rank, arena, txns, modes, cpus, cfg3=cfg3)
         tl["tile_mux1_capacity_txns_per_s_node"] = round(dist.sum(tl["tile_mux1_capacity_txns_per_s"]), 1)
         tl["tile_published_ok_all_ranks"] = dist.sum(
             1 if all(v for k, v in tl.items() if k.endswith("_published_ok")) else 0) == dist.world
+    # one process per GPU; more ranks than visible GPUs (a rehearsal of the
+    # multi-rank path on a one-GPU box) share devices round robin
+    ndev = _lib.lib().fdgpu_device_count()
+    if ndev < 1:
+        raise SystemExit("bench.py: no HIP device visible")
+    device = dist.local_rank % ndev
     eng = VerifyEngine(device, max_txn=args.latency_batch, max_sig=2 * args.latency_batch,
                        max_arena=args.latency_batch * 1232, ring_depth=RING_DEPTH)
     # `queues` device-resident copies of the batch, each on its own HIP stream
@@ -802,6 +909,9 @@ def main():
             eng_nb.close()
         if args.keypool_txns:
             extras.update(key_cache_rate(eng, device, args.keypool_txns, workload.CFG1_SEED + 0x700 + dist.rank))
+        if args.host_fed:
+            extras.update(host_fed(device, arena, txns, n_sig, batch.codes(), value / dist.world,
+                                   pin_cpu=(cpus[1] if len(cpus) > 1 else cpus[0]) if cpus else None))
         if args.adv_txns:
             extras.update(adversarial(eng, args.adv_txns, workload.CFG1_SEED + 0x400 + dist.rank,
                                       (kv_ms + kc_ms) / n_sig, cpus))

@@ -54,6 +54,8 @@ def lib():
     L.fdgpu_engine_close.restype = None
     L.fdgpu_last_error.argtypes = []
     L.fdgpu_last_error.restype = c.c_char_p
+    L.fdgpu_device_count.argtypes = []
+    L.fdgpu_device_count.restype = c.c_int
     L.fdgpu_kernel_path.argtypes = []
     L.fdgpu_kernel_path.restype = c.c_char_p
     L.fdgpu_submit.argtypes = [vp, vp, c.c_uint64, vp, c.c_uint64]
@@ -120,6 +122,8 @@ def lib():
     L.fdgpu_poll_frags_io.restype = c.c_int
     L.fdgpu_debug_submit_times.argtypes = [vp, c.c_uint64]
     L.fdgpu_debug_submit_times.restype = c.c_uint64
+    L.fdgpu_debug_h2d_gbps.argtypes = [vp, vp, c.c_uint64, c.c_int]
+    L.fdgpu_debug_h2d_gbps.restype = c.c_double
     L.fdgpu_frag_out_cap.argtypes = [c.c_uint32]
     L.fdgpu_frag_out_cap.restype = c.c_uint32
     L.fdgpu_ed25519_verify.argtypes = [u8p, c.c_uint64, u8p, u8p]

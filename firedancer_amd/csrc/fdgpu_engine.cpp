@@ -115,10 +115,17 @@ struct Slot {
      queues the rest of the batch behind it */
   hipEvent_t parsed = nullptr;
   bool vpending = false;
+  bool failed = false;        /* its merged verify could not be queued: the next poll reports the error */
   uint32_t m_n = 0;
   uint64_t m_seed = 0, m_cb = 0, m_bound = 0;
   uint8_t *m_out = nullptr;
 };
+
+/* poll_slot answers a pending batch without the ring lock, reading a slot's
+   ticket, held, flag_seq and polls atomically; every write of those fields
+   (under ring_mu) is an atomic store too, so the two sides never race */
+template <class T> inline void st_rlx(T &f, T v) { __atomic_store_n(&f, v, __ATOMIC_RELAXED); }
+inline void slot_flag_next(Slot *s) { __atomic_store_n(&s->flag_seq, s->flag_seq + 1, __ATOMIC_RELEASE); }
 
 /* a merge stream of an FDGPU_FLAG_MERGE engine */
 struct Merge {
@@ -473,6 +480,12 @@ extern "C" {
 
 char const *fdgpu_last_error(void) { return g_err.c_str(); }
 
+int fdgpu_device_count(void) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || n < 1) { (void)hipGetLastError(); return -1; }
+  return n;
+}
+
 fdgpu_engine_t *fdgpu_engine_open(int device, fdgpu_cfg_t const *cfg_in) {
   fdgpu_cfg_t cfg{};
   if (cfg_in) cfg = *cfg_in;
@@ -658,15 +671,15 @@ static int64_t submit_slot(fdgpu_engine_t *e, Slot *s, uint64_t arena_sz, fdgpu_
                           s->d_sig_codes, s->d_txn_codes, s->stream, s->d_ws, ring_kflags(e, s, (uint64_t)ns));
   if (rc) return rc;
   if (txn_cnt) HIPCHK(hipMemcpyAsync(s->h_codes, s->d_txn_codes, txn_cnt, hipMemcpyDeviceToHost, s->stream), FDGPU_ERR_DEVICE);
-  ++s->flag_seq;
+  slot_flag_next(s);
   if (e->flag_poll && !e->drop_flag) HIPCHK(hipStreamWriteValue32(s->stream, s->d_flag, s->flag_seq, 0), FDGPU_ERR_DEVICE);
   HIPCHK(hipEventRecord(s->done, s->stream), FDGPU_ERR_DEVICE);
   s->staged = false;
-  s->held = false;
-  s->polls = 0;
+  st_rlx(s->held, false);
+  st_rlx(s->polls, 0u);
   s->frag = false;
   s->io = false;
-  s->ticket = e->next_ticket++;
+  st_rlx(s->ticket, e->next_ticket++);
   s->txn_cnt = txn_cnt;
   return s->ticket;
 }
@@ -791,6 +804,33 @@ uint64_t fdgpu_debug_submit_times(uint64_t *out, uint64_t max) {
   return m;
 }
 
+double fdgpu_debug_h2d_gbps(fdgpu_engine_t *e, void const *src, uint64_t sz, int iters) {
+  if (!e || !src || !sz || iters < 1 || sz > e->cfg.max_arena) { set_err("bad argument"); return -1.0; }
+  std::lock_guard<std::mutex> lk(e->ring_mu);
+  Slot *s = free_slot(e);
+  if (!s) { set_err("all ring slots hold unpolled batches"); return -1.0; }
+  HIPCHK(hipSetDevice(e->device), -1.0);
+  hipEvent_t a, b;
+  HIPCHK(hipEventCreate(&a), -1.0);
+  if (hipEventCreate(&b) != hipSuccess) { (void)hipEventDestroy(a); set_err("event"); return -1.0; }
+  double gbps = -1.0;
+  float ms = 0.f;
+  if (hipMemcpyAsync(s->d_arena, src, sz, hipMemcpyHostToDevice, s->stream) == hipSuccess &&   /* warm */
+      hipEventRecord(a, s->stream) == hipSuccess) {
+    bool ok = true;
+    for (int i = 0; i < iters && ok; i++)
+      ok = hipMemcpyAsync(s->d_arena, src, sz, hipMemcpyHostToDevice, s->stream) == hipSuccess;
+    if (ok && hipEventRecord(b, s->stream) == hipSuccess && hipEventSynchronize(b) == hipSuccess &&
+        hipEventElapsedTime(&ms, a, b) == hipSuccess && ms > 0.f)
+      gbps = (double)sz * iters / (ms * 1e-3) / 1e9;
+  }
+  (void)hipGetLastError();
+  (void)hipEventDestroy(a);
+  (void)hipEventDestroy(b);
+  if (gbps < 0) set_err("h2d timing failed");
+  return gbps;
+}
+
 uint8_t *fdgpu_stage_acquire(fdgpu_engine_t *e, uint64_t *cap) {
   if (!e) return nullptr;
   std::lock_guard<std::mutex> lk(e->ring_mu);
@@ -839,6 +879,12 @@ static int poll_slot(fdgpu_engine_t *e, int64_t ticket, int8_t *txn_codes, int b
   Slot *s = nullptr;
   for (auto &c : e->slots) if (c.ticket == ticket && ticket >= 0 && !c.held) { s = &c; break; }
   if (!s) { set_err("unknown ticket %lld", (long long)ticket); return FDGPU_ERR_TICKET; }
+  if (s->failed) {                             /* its merged verify was never queued (merge_kick) */
+    s->failed = false;
+    st_rlx(s->ticket, (int64_t)-1);
+    set_err("ticket %lld: its verify could not be queued", (long long)ticket);
+    return FDGPU_ERR_DEVICE;
+  }
   if (!e->pending.empty()) {                   /* FDGPU_FLAG_MERGE: verifies waiting for a merge stream */
     HIPCHK(hipSetDevice(e->device), FDGPU_ERR_DEVICE);
     const int rc = merge_kick(e, blocking && s->vpending);
@@ -858,7 +904,7 @@ static int poll_slot(fdgpu_engine_t *e, int64_t ticket, int8_t *txn_codes, int b
        an error ends the wait (the tile stops instead of polling forever), a
        completed event means the batch is done. */
     if (__atomic_load_n(s->h_flag, __ATOMIC_ACQUIRE) != s->flag_seq) {
-      if (!counted && (++s->polls & 255u) != 0) return FDGPU_PENDING;
+      if (!counted && (__atomic_add_fetch(&s->polls, 1u, __ATOMIC_RELAXED) & 255u) != 0) return FDGPU_PENDING;
       const uint64_t now = sp_now();
       if (now - s->last_query < 1000000ull) return FDGPU_PENDING;
       s->last_query = now;
@@ -882,8 +928,8 @@ static int poll_slot(fdgpu_engine_t *e, int64_t ticket, int8_t *txn_codes, int b
     if (txn_codes && s->txn_cnt) memcpy(txn_codes, s->frag ? (const int8_t *)s->h_tr : s->h_codes, s->txn_cnt);
     if (trailers && s->frag && s->tr_sz) memcpy(trailers, s->h_tr + s->tr_base, s->tr_sz);
   }
-  if (keep) s->held = true;
-  else s->ticket = -1;
+  if (keep) st_rlx(s->held, true);
+  else st_rlx(s->ticket, (int64_t)-1);
   return FDGPU_OK;
 }
 
@@ -951,17 +997,17 @@ int64_t fdgpu_submit_frags(fdgpu_engine_t *e, uint8_t const *arena, uint64_t are
            FDGPU_ERR_DEVICE);
     HIPCHK(hipMemcpyAsync(s->h_tr, s->d_tr, tr_base + trailer_sz, hipMemcpyDeviceToHost, s->stream), FDGPU_ERR_DEVICE);
   }
-  ++s->flag_seq;
+  slot_flag_next(s);
   if (e->flag_poll && !e->drop_flag) HIPCHK(hipStreamWriteValue32(s->stream, s->d_flag, s->flag_seq, 0), FDGPU_ERR_DEVICE);
   HIPCHK(hipEventRecord(s->done, s->stream), FDGPU_ERR_DEVICE);
   s->staged = false;
-  s->held = false;
-  s->polls = 0;
+  st_rlx(s->held, false);
+  st_rlx(s->polls, 0u);
   s->frag = true;
   s->io = false;
   s->tr_sz = trailer_sz;
   s->tr_base = tr_base;
-  s->ticket = e->next_ticket++;
+  st_rlx(s->ticket, e->next_ticket++);
   s->txn_cnt = n;
   return s->ticket;
 }
@@ -990,7 +1036,7 @@ int io_tail(fdgpu_engine_t *e, Slot *s) {
                                      s->d_arena, s->m_seed, s->m_out, (int8_t *)s->d_trh, (uint64_t *)(s->d_trh + cb),
                                      (uint16_t *)(s->d_trh + cb + n * 8), s->stream),
          FDGPU_ERR_DEVICE);
-  ++s->flag_seq;
+  slot_flag_next(s);
   if (e->flag_poll && !e->drop_flag) HIPCHK(hipStreamWriteValue32(s->stream, s->d_flag, s->flag_seq, 0), FDGPU_ERR_DEVICE);
   HIPCHK(hipEventRecord(s->done, s->stream), FDGPU_ERR_DEVICE);
   return FDGPU_OK;
@@ -1005,7 +1051,21 @@ bool merge_free(const fdgpu_engine_t *e, const Merge &m) {
    one launch on a merge stream that is idle -- or, forced (a blocking poll
    waits on one of them), on the next one anyway -- then each batch's tail on
    its own stream behind it */
+int merge_kick_queue(fdgpu_engine_t *e, bool force);
+
+/* a HIP error part-way leaves batches with tickets issued and nothing (or
+   only part) queued for them: each is marked failed, so its poll returns
+   the error instead of waiting for a completion word that never comes */
 int merge_kick(fdgpu_engine_t *e, bool force) {
+  const int rc = merge_kick_queue(e, force);
+  if (rc) {
+    for (Slot *s : e->pending) if (s->vpending) { s->vpending = false; s->failed = true; }
+    e->pending.clear();
+  }
+  return rc;
+}
+
+int merge_kick_queue(fdgpu_engine_t *e, bool force) {
   if (e->pending.empty()) return FDGPU_OK;
   const uint32_t nms = (uint32_t)e->merges.size();
   int mi = -1;
@@ -1037,6 +1097,7 @@ int merge_kick(fdgpu_engine_t *e, bool force) {
       const uint32_t slow = grid < e->resident_blocks ? grid : e->resident_blocks;
       uint32_t *cnt = fdgpu_verify_cnt_word(s->d_ws, (uint32_t)s->m_bound);
       s->k_sigs = s->m_bound;
+      s->k_lanes = s->m_bound;                 /* one lane each: the merged launch never takes the pair kernel */
       tab[j] = fdgpu_mbatch_t{s->d_arena, s->d_sigs, s->d_n_sig, s->d_ws, s->d_sig_codes,
                               cnt - (size_t)grid * FDGPU_BLOCK, cnt, (uint32_t)s->m_bound, slow};
       grid_max = grid > grid_max ? grid : grid_max;
@@ -1073,16 +1134,20 @@ int64_t fdgpu_submit_frags_io(fdgpu_engine_t *e, fdgpu_frag_io_t const *fio, uin
   if (link_cnt > FDGPU_LINK_MAX) { set_err("more than %lu links", (unsigned long)FDGPU_LINK_MAX); return FDGPU_ERR_INVAL; }
   std::lock_guard<std::mutex> lk(e->ring_mu);
   const fdgpu_engine::Reg *ro = out_sz ? region_of(e, (uintptr_t)out, out_sz) : nullptr;
-  if (out_sz && !ro) { set_err("out range not inside a registered region"); return FDGPU_ERR_INVAL; }
+  if (out_sz && !ro) { set_err("out range not inside a registered region"); return FDGPU_ERR_UNREG; }
   /* each named link's mcache: its device-side address (the lines are read
      in place over the bus) */
   uint64_t ldev[FDGPU_LINK_MAX], lmask[FDGPU_LINK_MAX];
   for (uint64_t l = 0; l < link_cnt; l++) {
     const uint64_t d = links[l].depth;
-    const fdgpu_engine::Reg *rm = (d && !(d & (d - 1))) ? region_of(e, (uintptr_t)links[l].mcache, d * 32u) : nullptr;
-    if (!rm || (links[l].mcache & 7u)) {
-      set_err("link %llu: mcache not inside a registered region (or a bad depth)", (unsigned long long)l);
+    if (!d || (d & (d - 1)) || (links[l].mcache & 7u)) {
+      set_err("link %llu: bad depth or a misaligned mcache", (unsigned long long)l);
       return FDGPU_ERR_INVAL;
+    }
+    const fdgpu_engine::Reg *rm = region_of(e, (uintptr_t)links[l].mcache, d * 32u);
+    if (!rm) {
+      set_err("link %llu: mcache not inside a registered region", (unsigned long long)l);
+      return FDGPU_ERR_UNREG;
     }
     ldev[l] = rm->dbase + (links[l].mcache - rm->base);
     lmask[l] = d - 1;
@@ -1119,7 +1184,7 @@ int64_t fdgpu_submit_frags_io(fdgpu_engine_t *e, fdgpu_frag_io_t const *fio, uin
       return FDGPU_ERR_INVAL;
     }
     if (!rc || f.src < rc->base || f.src + q > rc->end) rc = region_of(e, (uintptr_t)f.src, q);
-    if (!rc) { set_err("frag %llu: payload not inside a registered region", (unsigned long long)t); return FDGPU_ERR_INVAL; }
+    if (!rc) { set_err("frag %llu: payload not inside a registered region", (unsigned long long)t); return FDGPU_ERR_UNREG; }
     /* streaming stores: the records are for the device (read over the bus),
        not this core -- no line fills for them, nothing for the bus to snoop */
     _mm_stream_si64((long long *)&h_src[t], (long long)(rc->dbase + (f.src - rc->base)));
@@ -1162,8 +1227,8 @@ int64_t fdgpu_submit_frags_io(fdgpu_engine_t *e, fdgpu_frag_io_t const *fio, uin
       s->vpending = true;
       s->m_n = (uint32_t)n; s->m_seed = hash_seed; s->m_out = out_dev; s->m_cb = cb; s->m_bound = bound;
       e->pending.push_back(s);
-      s->staged = false; s->held = false; s->polls = 0; s->frag = true; s->io = true; s->tr_sz = 0; s->tr_base = 0;
-      s->ticket = e->next_ticket++;
+      s->staged = false; st_rlx(s->held, false); st_rlx(s->polls, 0u); s->frag = true; s->io = true; s->tr_sz = 0; s->tr_base = 0;
+      st_rlx(s->ticket, e->next_ticket++);
       s->txn_cnt = n;
       const int rc = merge_kick(e, false);
       if (rc) return rc;
@@ -1177,17 +1242,17 @@ int64_t fdgpu_submit_frags_io(fdgpu_engine_t *e, fdgpu_frag_io_t const *fio, uin
                                        (uint16_t *)(s->d_trh + cb + n * 8), s->stream),
            FDGPU_ERR_DEVICE);
   }
-  ++s->flag_seq;
+  slot_flag_next(s);
   if (e->flag_poll && !e->drop_flag) HIPCHK(hipStreamWriteValue32(s->stream, s->d_flag, s->flag_seq, 0), FDGPU_ERR_DEVICE);
   HIPCHK(hipEventRecord(s->done, s->stream), FDGPU_ERR_DEVICE);
   s->staged = false;
-  s->held = false;
-  s->polls = 0;
+  st_rlx(s->held, false);
+  st_rlx(s->polls, 0u);
   s->frag = true;
   s->io = true;
   s->tr_sz = 0;
   s->tr_base = 0;
-  s->ticket = e->next_ticket++;
+  st_rlx(s->ticket, e->next_ticket++);
   s->txn_cnt = n;
   if (g_sp_on) {
     const uint64_t sp2 = sp_now();
@@ -1212,7 +1277,7 @@ int fdgpu_release(fdgpu_engine_t *e, int64_t ticket) {
   if (!e) return FDGPU_ERR_INVAL;
   std::lock_guard<std::mutex> lk(e->ring_mu);
   for (auto &c : e->slots)
-    if (c.ticket == ticket && ticket >= 0 && c.held) { c.held = false; c.ticket = -1; return FDGPU_OK; }
+    if (c.ticket == ticket && ticket >= 0 && c.held) { st_rlx(c.held, false); st_rlx(c.ticket, (int64_t)-1); return FDGPU_OK; }
   set_err("ticket %lld not held", (long long)ticket);
   return FDGPU_ERR_TICKET;
 }

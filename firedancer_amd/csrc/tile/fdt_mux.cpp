@@ -13,6 +13,7 @@
 #include <algorithm>
 #include <atomic>
 #include <cmath>
+#include <cstddef>
 #include <cstring>
 #include <deque>
 #include <new>
@@ -82,11 +83,22 @@ struct MuxMetrics {
     for (uint64_t j = 0; j < k; j++) fdt_histf_sample(&h, d);
     now = next;
   }
+  /* a seqlock over the shared copy: its housekeeping_cnt is odd while a
+     write is under way and twice the writes so far once it is done; the
+     words go out as relaxed atomic stores, so an observer that reads the
+     count, copies and re-reads it gets a consistent snapshot or retries */
   void write() {
     if (!out) return;
-    m.housekeeping_cnt++;
+    const uint64_t k = ++m.housekeeping_cnt;
+    uint64_t *seq = &out->housekeeping_cnt;
+    __atomic_store_n(seq, 2 * k - 1, __ATOMIC_RELAXED);
     std::atomic_thread_fence(std::memory_order_release);
-    std::memcpy((void *)out, &m, sizeof m);
+    static_assert(sizeof m % 8 == 0 && offsetof(fdt_mux_metrics_t, housekeeping_cnt) + 8 == sizeof m,
+                  "the sequence word is the last");
+    const uint64_t *src = (const uint64_t *)&m;
+    uint64_t *dst = (uint64_t *)out;
+    for (size_t w = 0; w + 1 < sizeof m / 8; w++) __atomic_store_n(dst + w, src[w], __ATOMIC_RELAXED);
+    __atomic_store_n(seq, 2 * k, __ATOMIC_RELEASE);
   }
 };
 
@@ -341,6 +353,23 @@ void fdt_mux_publish(fdt_mux_context_t *ctx, uint64_t sig, uint64_t chunk, uint6
   fdt_mcache_publish(ctx->mcache, ctx->depth, seq, sig, chunk, sz, ctl, tsorig, tspub);
   *ctx->cr_avail -= ctx->cr_decrement_amount;
   *ctx->seq = seq + 1;
+}
+
+int fdt_mux_metrics_snapshot(const fdt_mux_metrics_t *src, fdt_mux_metrics_t *dst, uint64_t max_tries) {
+  const uint64_t *s = (const uint64_t *)src;
+  uint64_t *d = (uint64_t *)dst;
+  const size_t nw = sizeof *src / 8;
+  for (uint64_t k = 0; k < max_tries; k++) {
+    const uint64_t seq0 = __atomic_load_n(&src->housekeeping_cnt, __ATOMIC_ACQUIRE);
+    if (seq0 & 1) { _mm_pause(); continue; }
+    for (size_t w = 0; w + 1 < nw; w++) d[w] = __atomic_load_n(s + w, __ATOMIC_RELAXED);
+    std::atomic_thread_fence(std::memory_order_acquire);
+    if (__atomic_load_n(&src->housekeeping_cnt, __ATOMIC_RELAXED) == seq0) {
+      dst->housekeeping_cnt = seq0;
+      return 0;
+    }
+  }
+  return -1;
 }
 
 int fdt_mux_run(const fdt_mux_cfg_t *cfg, const fdt_mux_callbacks_t *cb, void *ctx, const volatile uint64_t *halt,

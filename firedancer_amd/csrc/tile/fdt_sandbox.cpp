@@ -53,21 +53,26 @@ uint64_t mono_ns() {
 
 extern "C" {
 
-uint64_t fdt_link_footprint(uint64_t depth, uint64_t mtu) {
+uint64_t fdt_link_footprint_sz(uint64_t depth, uint64_t mtu, uint64_t data_sz) {
   if (!depth || (depth & (depth - 1)) || !mtu) return 0;
+  if (!data_sz) data_sz = fdt_dcache_data_sz(mtu, depth);
+  data_sz = align_up(data_sz, FDT_CHUNK_SZ);
+  if (data_sz < 2 * align_up(mtu, FDT_CHUNK_SZ)) return 0;       /* the compact ring holds two frags */
   const uint64_t dc_off = align_up(LINK_HDR + depth * sizeof(fdt_frag_meta_t), 4096);
-  return align_up(dc_off + fdt_dcache_data_sz(mtu, depth), 4096);
+  return align_up(dc_off + data_sz, 4096);
 }
 
-int fdt_link_new(void *mem, uint64_t depth, uint64_t mtu, uint64_t seq0) {
-  const uint64_t fp = fdt_link_footprint(depth, mtu);
+uint64_t fdt_link_footprint(uint64_t depth, uint64_t mtu) { return fdt_link_footprint_sz(depth, mtu, 0); }
+
+int fdt_link_new_sz(void *mem, uint64_t depth, uint64_t mtu, uint64_t seq0, uint64_t data_sz) {
+  const uint64_t fp = fdt_link_footprint_sz(depth, mtu, data_sz);
   if (!mem || !fp || ((uintptr_t)mem & 4095)) return -1;
   auto *h = (link_hdr *)mem;
   h->magic = 0;                                   /* not joinable until fully formatted */
   h->depth = depth;
   h->mtu = mtu;
   h->seq0 = seq0;
-  h->data_sz = fdt_dcache_data_sz(mtu, depth);
+  h->data_sz = align_up(data_sz ? data_sz : fdt_dcache_data_sz(mtu, depth), FDT_CHUNK_SZ);
   h->mcache_off = LINK_HDR;
   h->dcache_off = align_up(LINK_HDR + depth * sizeof(fdt_frag_meta_t), 4096);
   *(volatile uint64_t *)((uint8_t *)mem + FSEQ_OFF) = seq0;
@@ -75,6 +80,8 @@ int fdt_link_new(void *mem, uint64_t depth, uint64_t mtu, uint64_t seq0) {
   __atomic_store_n(&h->magic, LINK_MAGIC, __ATOMIC_RELEASE);
   return 0;
 }
+
+int fdt_link_new(void *mem, uint64_t depth, uint64_t mtu, uint64_t seq0) { return fdt_link_new_sz(mem, depth, mtu, seq0, 0); }
 
 int fdt_link_join(void *mem, fdt_link_t *out) {
   if (!mem || !out) return -1;

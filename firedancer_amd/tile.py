@@ -289,6 +289,8 @@ def lib():
         "fdt_tpu_reasm_slot_state": (c.c_int, [vp, c.c_uint32]),
         "fdt_link_footprint": (u64, [u64, u64]),
         "fdt_link_new": (c.c_int, [vp, u64, u64, u64]),
+        "fdt_link_footprint_sz": (u64, [u64, u64, u64]),
+        "fdt_link_new_sz": (c.c_int, [vp, u64, u64, u64, u64]),
         "fdt_link_join": (c.c_int, [vp, c.POINTER(LinkT)]),
         "fdt_sandbox_enter": (c.c_int, [c.c_int]),
         "fdgpu_dtile_run_sandboxed": (None, [vp, u64, u64, c.POINTER(DTileStats), c.c_int]),
@@ -310,6 +312,7 @@ def lib():
         "fdgpu_vmux_latencies": (u64, [vp, vp, u64]),
         "fdgpu_vmux_log_enable": (None, [vp, u64]),
         "fdgpu_vmux_log": (u64, [vp, vp, vp, u64]),
+        "fdt_mux_metrics_snapshot": (c.c_int, [c.POINTER(MuxMetrics), c.POINTER(MuxMetrics), u64]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -345,6 +348,107 @@ def _page_buf(nbytes):
     register (fdgpu_host_register pins whole pages) without sharing a page
     with another buffer."""
     return _aligned((nbytes + 4095) // 4096 * 4096, 4096)[:nbytes]
+
+
+HUGE_PAGE = 2 << 20
+PAGES = ("4k", "thp", "shm-thp", "hugetlb")
+
+
+def _smaps_huge_bytes(addr, length):
+    """Bytes of [addr, addr + length) this process maps with 2 MB pages
+    (AnonHugePages + ShmemPmdMapped + FilePmdMapped of the overlapping
+    mappings in /proc/self/smaps, scaled to the overlap)."""
+    end, tot, cur = addr + length, 0, None
+    try:
+        f = open("/proc/self/smaps")
+    except OSError:
+        return 0
+    with f:
+        for line in f:
+            head = line.split(None, 1)[0]
+            if "-" in head and not head.endswith(":"):
+                lo, hi = (int(x, 16) for x in head.split("-"))
+                cur = (lo, hi) if lo < end and hi > addr else None
+            elif cur and head in ("AnonHugePages:", "ShmemPmdMapped:", "FilePmdMapped:"):
+                kb = int(line.split()[1])
+                lo, hi = cur
+                ov = min(hi, end) - max(lo, addr)
+                tot += kb * 1024 * ov // (hi - lo)
+    return tot
+
+
+def hugepage_support():
+    """What this host offers for 2 MB pages (the reference's workspaces sit on
+    pre-allocated huge/gigantic pages, src/disco/topo/fd_topo.c:262-278):
+    anonymous THP ("thp": in-process links), shmem THP ("shm-thp": links other
+    processes join) and a hugetlbfs pool ("hugetlb")."""
+    def rd(p):
+        try:
+            return open(p).read().strip()
+        except OSError:
+            return ""
+    sel = lambda v: v[v.index("[") + 1:v.index("]")] if "[" in v else v   # noqa: E731
+    thp, shm = sel(rd("/sys/kernel/mm/transparent_hugepage/enabled")), \
+        sel(rd("/sys/kernel/mm/transparent_hugepage/shmem_enabled"))
+    mi = {ln.split(":")[0]: ln.split(":")[1].split()[0] for ln in rd("/proc/meminfo").splitlines() if ":" in ln}
+    mounts = [ln.split()[1] for ln in rd("/proc/mounts").splitlines() if ln.split()[2:3] == ["hugetlbfs"]]
+    return {"thp": thp in ("always", "madvise"), "shm-thp": shm in ("always", "within_size", "advise", "force"),
+            "hugetlb": int(mi.get("HugePages_Free", 0)) > 0 and bool(mounts),
+            "thp_enabled": thp, "shmem_enabled": shm, "hugetlb_free": int(mi.get("HugePages_Free", 0)),
+            "hugetlbfs_mounts": mounts}
+
+
+class _Region:
+    """A 4096-aligned byte region for link memory, faulted in (every page
+    written) before it is used, so no first touch lands in a timed run.
+    pages: "4k" (anonymous / the file's pages), "thp" (anonymous memory
+    madvise'd MADV_HUGEPAGE: 2 MB pages when the host allows), "shm-thp" (a
+    /dev/shm file madvise'd the same: other processes can join it), "hugetlb"
+    (a file on a hugetlbfs mount)."""
+
+    def __init__(self, nbytes, path=None, pages="4k", create=True):
+        if pages not in PAGES:
+            raise ValueError(f"pages must be one of {PAGES}")
+        if pages == "thp" and path:
+            raise ValueError("anonymous THP cannot back a shared link: use shm-thp or hugetlb")
+        align = HUGE_PAGE if pages != "4k" else 4096
+        self.pages, self.path = pages, path
+        if path:
+            size = (nbytes + align - 1) // align * align
+            if create:
+                fd = os.open(path, os.O_RDWR | os.O_CREAT | os.O_TRUNC, 0o600)
+            else:
+                fd = os.open(path, os.O_RDWR)
+            try:
+                if create:
+                    os.ftruncate(fd, size)
+                else:
+                    size = os.fstat(fd).st_size
+                self._mm = mmap.mmap(fd, size, mmap.MAP_SHARED | getattr(mmap, "MAP_POPULATE", 0),
+                                     mmap.PROT_READ | mmap.PROT_WRITE)
+            finally:
+                os.close(fd)
+            if pages == "shm-thp":
+                self._mm.madvise(mmap.MADV_HUGEPAGE)
+            self.buf = np.frombuffer(self._mm, dtype=np.uint8)
+            self.size = size
+        else:
+            size = (nbytes + align - 1) // align * align
+            self._mm = mmap.mmap(-1, size + align, mmap.MAP_PRIVATE | mmap.MAP_ANONYMOUS,
+                                 mmap.PROT_READ | mmap.PROT_WRITE)
+            raw = np.frombuffer(self._mm, dtype=np.uint8)
+            off = (-raw.ctypes.data) % align
+            if pages == "thp":
+                self._mm.madvise(mmap.MADV_HUGEPAGE, off, size)
+            self.buf = raw[off:off + size]
+            self.size = size
+        if create:
+            self.buf[:] = 0                       # fault every page in now (the link's producer writes them later)
+        else:
+            _ = int(self.buf[::4096].sum())         # joiner: map every page (MAP_POPULATE did, where it exists)
+
+    def huge_bytes(self):
+        return _smaps_huge_bytes(self.buf.ctypes.data, self.size)
 
 
 # ---------------------------------------------------------------- basics
@@ -439,15 +543,25 @@ class Link:
     """One tango link: an mcache of `depth` frag metas and a compact dcache
     sized for `depth` frags of up to `mtu` bytes (chunk 0 = dcache start)."""
 
-    def __init__(self, depth, mtu, seq0=0, data_sz=None):
+    def __init__(self, depth, mtu, seq0=0, data_sz=None, pages=None):
+        """pages: None (numpy pages, faulted in on first use), or "4k" / "thp":
+        the mcache and dcache in one region faulted in before use
+        (_Region), on 2 MB pages for "thp" where the host allows."""
         L = lib()
         if depth & (depth - 1):
             raise ValueError("depth must be a power of 2")
         self.depth, self.mtu, self.seq0 = depth, mtu, seq0
-        self.mcache = _page_buf(depth * 32).view(FRAG_META_DTYPE)
         data_sz = data_sz or L.fdt_dcache_data_sz(mtu, depth)   # explicit: a dcache sized by its producer
         data_sz = (data_sz + CHUNK_SZ - 1) // CHUNK_SZ * CHUNK_SZ
-        self.dcache = _page_buf(data_sz)
+        if pages:
+            mo = (depth * 32 + 4095) // 4096 * 4096
+            self._mem = _Region(mo + data_sz, pages=pages)
+            self._region = self._mem.buf                       # one region: the engines register it whole
+            self.mcache = self._region[:depth * 32].view(FRAG_META_DTYPE)
+            self.dcache = self._region[mo:mo + data_sz]
+        else:
+            self.mcache = _page_buf(depth * 32).view(FRAG_META_DTYPE)
+            self.dcache = _page_buf(data_sz)
         self.chunk0 = 0
         self.chunk1 = data_sz // CHUNK_SZ
         self.wmark = L.fdt_dcache_wmark(self.chunk0, self.chunk1, mtu)
@@ -457,32 +571,31 @@ class Link:
         self._pub_seq, self._pub_chunk = seq0, 0
 
     @classmethod
-    def shm_create(cls, path, depth, mtu, seq0=0):
-        """A link formatted in a shared-memory file (fdt_link_new), joinable
-        by other processes with shm_join(path): the engine process and the
-        sandboxed tiles share links this way (fd_wksp's role)."""
-        fp = lib().fdt_link_footprint(depth, mtu)
+    def shm_create(cls, path, depth, mtu, seq0=0, data_sz=0, pages="4k"):
+        """A link formatted in a shared-memory file (fdt_link_new_sz),
+        joinable by other processes with shm_join(path): the engine process
+        and the sandboxed tiles share links this way (fd_wksp's role).  The
+        whole region is faulted in before it is formatted (pages "4k", or
+        "shm-thp" / "hugetlb" for 2 MB pages where the host offers them:
+        hugepage_support())."""
+        fp = lib().fdt_link_footprint_sz(depth, mtu, data_sz)
         if not fp:
             raise ValueError("bad link parameters")
-        fd = os.open(path, os.O_RDWR | os.O_CREAT | os.O_TRUNC, 0o600)
-        try:
-            os.ftruncate(fd, fp)
-            mm = mmap.mmap(fd, fp, mmap.MAP_SHARED, mmap.PROT_READ | mmap.PROT_WRITE)
-        finally:
-            os.close(fd)
-        region = np.frombuffer(mm, dtype=np.uint8)
-        if lib().fdt_link_new(region.ctypes.data, depth, mtu, seq0):
+        mem = _Region(fp, path=path, pages=pages)
+        if lib().fdt_link_new_sz(mem.buf.ctypes.data, depth, mtu, seq0, data_sz):
             raise RuntimeError("fdt_link_new failed")
-        return cls._from_region(mm, region)
+        return cls._from_region(mem, mem.buf)
 
     @classmethod
-    def shm_join(cls, path):
-        fd = os.open(path, os.O_RDWR)
-        try:
-            mm = mmap.mmap(fd, os.fstat(fd).st_size, mmap.MAP_SHARED, mmap.PROT_READ | mmap.PROT_WRITE)
-        finally:
-            os.close(fd)
-        return cls._from_region(mm, np.frombuffer(mm, dtype=np.uint8))
+    def shm_join(cls, path, pages="4k"):
+        """Joins a link another process formatted (every page mapped now)."""
+        mem = _Region(0, path=path, pages=pages if pages != "thp" else "4k", create=False)
+        return cls._from_region(mem, mem.buf)
+
+    def huge_bytes(self):
+        """Bytes of this link's memory on 2 MB pages in this process."""
+        mem = getattr(self, "_mem", None) or getattr(self, "_mm", None)
+        return mem.huge_bytes() if isinstance(mem, _Region) else 0
 
     @classmethod
     def _from_region(cls, mm, region):
@@ -1056,7 +1169,14 @@ class VerifyMuxTile:
     def metrics(self):
         """The reference's metrics (Tile, Stem, Link in) as the mux loop last
         wrote them (metrics=True), or None."""
-        return self._metrics.as_dict(len(self.in_links)) if self._metrics is not None else None
+        if self._metrics is None:
+            return None
+        snap = MuxMetrics()          # a consistent copy (the loop's writes are a seqlock)
+        if lib().fdt_mux_metrics_snapshot(c.byref(self._metrics), c.byref(snap), 1 << 20):
+            raise RuntimeError("fdt_mux_metrics_snapshot: no stable copy")
+        d = snap.as_dict(len(self.in_links))
+        d["housekeeping_cnt"] //= 2            # the sequence word counts two per write
+        return d
 
     def latencies_ns(self):
         n = self.stats()["lat_cnt"]

@@ -153,6 +153,10 @@ typedef struct {
 #define FDGPU_ERR_DEVICE    (-11)
 #define FDGPU_ERR_FULL      (-12)
 #define FDGPU_ERR_TICKET    (-13)
+/* a gathered batch names host memory no fdgpu_host_register call of the
+   engine covers (a payload, the out range, an in link's mcache): a wiring
+   error of the caller, not a malformed batch -- the verify tile stops on it */
+#define FDGPU_ERR_UNREG     (-14)
 
 /* Opens an engine on HIP device `device`.  Returns NULL on failure (no
    device, allocation failure); fdgpu_last_error() describes it. */
@@ -383,6 +387,9 @@ int fdgpu_engine_info( fdgpu_engine_t * e, uint32_t * grid_blocks, uint32_t * bl
 /* The kernels one verify launches, as a static string, e.g.
    "halfsize: fdgpu_verify_hs_kernel + fdgpu_full_kernel" (the build's path). */
 char const * fdgpu_kernel_path( void );
+/* HIP devices visible to this process (hipGetDeviceCount; starts the HIP
+   runtime), or -1 when the runtime reports none / fails. */
+int          fdgpu_device_count( void );
 
 /* --------------------------------------------------------- diagnostics */
 
@@ -391,6 +398,11 @@ char const * fdgpu_kernel_path( void );
    rest (copies and launches enqueued)} in ns -> out[3 i .. 3 i + 2].
    Returns the number of calls written. */
 uint64_t fdgpu_debug_submit_times( uint64_t * out, uint64_t max );
+/* Host -> device copy rate (GB/s) of sz bytes at src (pinned or inside a
+   registered region: a DMA; pageable: the runtime's staged copy) into a free
+   ring slot's arena, iters copies timed with HIP events on the slot's
+   stream: the PCIe ceiling beside a host-fed verify rate.  < 0 on error. */
+double   fdgpu_debug_h2d_gbps( fdgpu_engine_t * e, void const * src, uint64_t sz, int iters );
 /* Used by the parity tests to check each stage of the path on the GPU in
    isolation.  Host pointers; synchronous.  Return FDGPU_OK or < 0. */
 

@@ -407,7 +407,10 @@ typedef struct {
    groups Link (in side, per in link), Stem and Tile; accumulated as
    fd_mux.c:370-379,440-451,525-697 does), written by fdt_mux_run into
    *cfg->metrics at every housekeeping event and when it halts, for an
-   observer thread or process to read (word-wise; counters only grow).
+   observer thread or process to read: housekeeping_cnt is a seqlock
+   sequence (odd while a write is under way, twice the writes once done), so
+   an observer reads it, copies the struct, re-reads it and retries while it
+   was odd or changed (fdt_mux_metrics_snapshot does exactly that).
    Histograms are the reference's fd_histf: 16 exponential buckets between
    a min and a max, the first for samples < min, the last for >= max, and
    the sum of all samples.  Loop durations are sampled in ticks (the time
@@ -450,8 +453,13 @@ typedef struct fdt_mux_metrics {
   fdt_histf_t fragment_handled_size_bytes;
   fdt_link_in_metrics_t link_in[ FDT_MUX_IN_MAX ];
   double   tick_per_ns;                          /* the "seconds" converter: seconds = ticks / tick_per_ns / 1e9 */
-  uint64_t housekeeping_cnt;                     /* metrics writes so far */
+  uint64_t housekeeping_cnt;                     /* 2 x metrics writes so far; odd while one is under way */
 } fdt_mux_metrics_t;
+
+/* A consistent copy of *src (a metrics struct another thread or process is
+   writing) into *dst; 0 on success, -1 when no stable copy was seen within
+   max_tries attempts. */
+int fdt_mux_metrics_snapshot( fdt_mux_metrics_t const * src, fdt_mux_metrics_t * dst, uint64_t max_tries );
 
 /* The mux run loop (fd_mux.c:387-699) with the cnc replaced by a halt word:
    housekeeping every lazy_iters iterations (out credits from the out fseqs,
@@ -687,6 +695,12 @@ typedef struct {
 
 uint64_t fdt_link_footprint( uint64_t depth, uint64_t mtu );   /* 0 on bad parameters */
 int      fdt_link_new      ( void * mem, uint64_t depth, uint64_t mtu, uint64_t seq0 );
+/* The same with the dcache's data size given (0: fdt_dcache_data_sz(mtu,
+   depth)): the verify mux tile's out dcache also holds its batches in
+   flight (fdgpu_vmux_dcache_data_sz).  data_sz is rounded up to 64 B and
+   must hold two mtu-sized frags. */
+uint64_t fdt_link_footprint_sz( uint64_t depth, uint64_t mtu, uint64_t data_sz );
+int      fdt_link_new_sz      ( void * mem, uint64_t depth, uint64_t mtu, uint64_t seq0, uint64_t data_sz );
 int      fdt_link_join     ( void * mem, fdt_link_t * out );   /* 0, or -1 if not a formatted link */
 
 /* Enters the tiles' seccomp policy (src/app/fdctl/run/tiles/

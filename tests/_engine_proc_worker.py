@@ -1,6 +1,10 @@
-"""Spawned-process target for tests/test_engine_proc.py: the engine process
-(firedancer_amd.engine_proc.serve) over shared-memory links, with the CPU
-oracle as the test's verifier (CPU test) or the GPU engine (GPU test)."""
+"""The engine process's command line (firedancer_amd/engine_proc.py main) for
+the CPU tests: the same gather-mode verify mux tiles over shared-memory
+links, with the test's checker -- the CPU oracle behind a host stand-in of
+the engine's gathered-batch calls (tile.PyVerifier: each payload read late,
+at the poll that completes its batch, its in-mcache line re-checked after
+the read) -- in place of the GPU engines.  tools/xproc.py runs it as
+`python tests/_engine_proc_worker.py <engine_proc arguments>`."""
 import os
 import sys
 
@@ -8,20 +12,14 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, REPO)
 
 
-def run(in_path, out_path, frag_cnt, use_gpu, result_q, tile_kw):
-    try:
-        from firedancer_amd import engine_proc, tile
-        if use_gpu:
-            from firedancer_amd import VerifyEngine
-            eng = VerifyEngine(0, max_txn=4096, max_sig=4096 * 12, max_arena=4096 * 1232, ring_depth=3)
-            ver = tile.EngineVerifier([eng])
-        else:
-            from oracle import oracle as orc
-            ver = tile.PyVerifier(lambda arena, txns: orc.verify_txns(arena, txns), slots=3, lag=1)
-        st = engine_proc.serve(in_path, out_path, ver, frag_cnt, timeout_s=90.0, **tile_kw)
-        if use_gpu:
-            ver.close()
-            eng.close()
-        result_q.put(("ok", st))
-    except BaseException as e:          # report, never hang the parent
-        result_q.put(("err", repr(e)))
+def oracle_verifiers(T, a):
+    from firedancer_amd import tile
+    from oracle import oracle as orc
+    vers = [tile.PyVerifier(lambda arena, txns: orc.verify_txns(arena, txns), slots=a.inflight, lag=1)
+            for _ in range(T)]
+    return vers, (lambda: None), {"device": None, "verifier": "oracle (test stand-in)"}
+
+
+if __name__ == "__main__":
+    from firedancer_amd import engine_proc
+    sys.exit(engine_proc.main(sys.argv[1:], make_verifiers=oracle_verifiers))

@@ -19,7 +19,7 @@ def test_tile_cmd_parses():
     assert cmd[1].endswith("tools/bench_tile.py")
     args = bench_tile.make_parser().parse_args(cmd[2:])
     assert args.mux == 1 and args.gpu_parse == 2 and args.producers_same_as_tiles == 1
-    assert args.payload_npz == "/tmp/x.npz" and args.cpu_list == "3,4,5,6" and args.device == 0
+    assert args.payload_npz == "/tmp/x.npz" and args.cpu_list == "3,4,5,6" and args.device_rank == 0
     assert args.hw_queues == bench.TILE_HW_QUEUES and args.reps == bench.TILE_REPS
     assert args.depth_lg == 21                                       # a prefill fits its links
     assert args.pair == bench.TILE_PAIR == 2                           # FDGPU_FLAG_PAIR_AUTO tile engines
@@ -46,7 +46,7 @@ def test_tile_runs_shape():
 def test_tile_cmd_cfg3():
     cmd = bench.tile_cmd(1, [], "/tmp/y.npz", "/tmp/y.jsonl", bench.TILE_RUNS_CFG3, multi=1)
     args = bench_tile.make_parser().parse_args(cmd[2:])
-    assert args.multi == 1 and args.device == 1 and args.cpu_list == ""
+    assert args.multi == 1 and args.device_rank == 1 and args.cpu_list == ""
     assert args.batch_sig_max == bench.TILE_CFG3_SIG_MAX
     assert len(args.sweep.split(";")) == len(bench.TILE_RUNS_CFG3)
     assert all(r[3] == -1.0 for r in bench.TILE_RUNS_CFG3)       # capacity lines
@@ -55,3 +55,16 @@ def test_tile_cmd_cfg3():
     for (name, tiles_n, prods, rate), run in zip(bench.TILE_RUNS_CFG3, runs):
         assert len(run) == 6 and run[5] == bench.TILE_CFG3_SIG_MAX_BY_TILES[tiles_n]
     assert bench.TILE_CFG3_SIG_MAX_BY_TILES[2] < bench.TILE_CFG3_SIG_MAX_BY_TILES[1] == bench.TILE_CFG3_SIG_MAX
+
+
+def test_parent_rank_starts_no_hip_before_its_tile_child():
+    """bench.py must not start a HIP runtime in a rank
+    before that rank's tile child runs (8 ranks + 8 children would be 16 GPU
+    processes beside the launcher); the child derives its device from the
+    rank.  Checked on the source: no torch.cuda call anywhere, and the first
+    device count comes after the tile lines."""
+    src = open(os.path.join(REPO, "bench.py")).read()
+    main = src[src.index("def main():"):]
+    assert "torch.cuda" not in src
+    assert main.index("tile_lines(") < main.index("fdgpu_device_count()")
+    assert main.index("fdgpu_device_count()") < main.index("VerifyEngine(")

@@ -1,21 +1,33 @@
-"""Process separation of the verify stage: tango
-links in shared memory joined by independent processes, the engine process
-(firedancer_amd/engine_proc.py) running the batched verify tile, and the
-dedup tile inside the reference's seccomp policy (verify.seccomppolicy /
-dedup.seccomppolicy: write + fsync only).  Outputs are checked frag by frag
-against the sequential models of the reference loops (tests/tile_model.py).
-The CPU tests use the oracle as the engine process's verifier; the GPU test
-runs the same pipeline over the MI355X engine."""
-import multiprocessing as mp
+"""Process separation of the verify stage, in the
+shape the reference's topology runs it (fd_frankendancer.c:59-60,131-133,
+fd_topo_run.c:50-171): tango links in shared memory (every page faulted in
+before use), a producer process publishing into the quic -> verify link
+(tools/quic_feed.py), the engine process (firedancer_amd/engine_proc.py)
+running the gather-mode verify mux tile -- the tile every bench number comes
+from -- over that link, and the dedup tile in a process of its own inside
+the reference's seccomp policy (verify.seccomppolicy / dedup.seccomppolicy:
+write + fsync only).  tools/xproc.py launches the three.  Outputs are
+checked frag by frag against the sequential models of the reference loops
+(tests/tile_model.py).  The CPU tests run the engine process's loop over the
+oracle (tests/_engine_proc_worker.py); the GPU tests over the MI355X."""
 import os
 import signal
+import sys
 import uuid
 
 import pytest
 
-from firedancer_amd import tile
+import numpy as np
+
+from firedancer_amd import tile, workload
 import tile_model
 from test_tile import _mixed_stream
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "tools"))
+import xproc  # noqa: E402
+
+CPU_ENGINE = [sys.executable, os.path.join(REPO, "tests", "_engine_proc_worker.py")]
 
 
 def _shm_path(tag):
@@ -75,89 +87,112 @@ def test_shm_link_join_roundtrip():
         os.unlink(path)
 
 
-def _pipeline(ps, use_gpu, oracle, batch=64):
-    """quic (this process) -> verify (engine process) -> dedup (sandboxed
-    child) over three shared-memory links."""
+def _npz(tmp_path, ps):
+    arena, offs, sizes = workload.pack_payloads(ps)
+    p = str(tmp_path / "frags.npz")
+    np.savez(p, arena=arena, offs=offs, sizes=sizes)
+    return p
+
+
+def _xproc_vs_model(tmp_path, ps, oracle, tiles=1, dedup=True, engine_cmd=None, **kw):
+    """producer process -> engine process (T gather-mode mux tiles, round
+    robin over one quic -> verify link) -> sandboxed dedup process; every
+    frag's outcome, every tile's published stream and the dedup tile's
+    output against the sequential models."""
     seed, dseed = 0x5EEDF00D, 0xD5
-    paths = [_shm_path(n) for n in ("qv", "vd", "dd")]
-    try:
-        inl = tile.Link.shm_create(paths[0], 1 << 12, 1232)
-        vd = tile.Link.shm_create(paths[1], 1 << 12, tile.TPU_DCACHE_MTU)
-        dd = tile.Link.shm_create(paths[2], 1 << 12, tile.TPU_DCACHE_MTU)
-        exp_out, exp_pub = tile_model.verify_tile_model(ps, seed, lambda a, t: oracle.verify_txns(a, t))
-        ctx = mp.get_context("spawn")
-        q = ctx.Queue()
-        import _engine_proc_worker
-        eng = ctx.Process(target=_engine_proc_worker.run,
-                          args=(paths[0], paths[1], len(ps), use_gpu, q,
-                                dict(hashmap_seed=seed, batch_txn_max=batch, inflight_max=3)))
-        eng.start()
-        dt = tile.DedupTile([vd], dd, hashmap_seed=dseed, tcache_depth=1 << 14)
-        # the sandboxed dedup child is forked only from a process that has not
-        # initialised the GPU (GPU test: the dedup tile runs here afterwards)
-        pid, dstats = dt.fork_sandboxed(len(exp_pub), idle_s=60.0) if not use_gpu else (None, None)
-        for p in ps:
-            inl.publish(p)
-        kind, st = q.get(timeout=180)
-        eng.join(timeout=60)
-        assert kind == "ok", st
-        if pid is not None:
-            _, status = os.waitpid(pid, 0)
-            assert os.WIFEXITED(status) and os.WEXITSTATUS(status) == 0, status
-        else:
-            dt.run_until_idle()
-            dstats = dt.stats
-        # verify tile: the reference loop's outcome for every frag
-        assert st["published"] == exp_out.count(0) and st["dedup"] == exp_out.count(-2)
-        assert st["verify_failed"] == exp_out.count(-1) and st["parse_fail"] == exp_out.count(1)
-        vouts = vd.drain()
-        assert [(m["sig"], tile.split_verify_output(f)[0]) for m, f in vouts] == [(t, p) for p, _, t in exp_pub]
-        # sandboxed dedup tile: every verified txn once, sig 0
-        exp_d = tile_model.dedup_model([f for _, f in vouts], dseed, 1 << 14)
-        got = dd.drain()
-        assert [f for _, f in got] == exp_d and all(m["sig"] == 0 for m, _ in got)
-        ds = dstats()
-        assert ds["in_frags"] == len(vouts) and ds["published"] == len(exp_d) and ds["overrun"] == 0
-        return exp_out
-    finally:
-        for p in paths:
-            if os.path.exists(p):
-                os.unlink(p)
+    exp = [tile_model.verify_tile_model(ps, seed, lambda a, t: oracle.verify_txns(a, t), rr_idx=k, rr_cnt=tiles)
+           for k in range(tiles)]
+    n_pub = sum(len(pub) for _, pub in exp)
+    res = xproc.run(_npz(tmp_path, ps), len(ps), tiles=tiles, producers=1, seed=seed, dedup=dedup,
+                    dedup_frags=n_pub, log=True, engine_cmd=engine_cmd, timeout=180, **kw)
+    st = res["engine"]["stats"]
+    assert st["verify_errors"] == 0 and st["corrupt"] == 0 and st["overrun"] == 0
+    for k, (exp_out, exp_pub) in enumerate(exp):
+        seqs, codes = res["logs"][k]
+        assert seqs.tolist() == list(range(len(ps))) and codes.tolist() == exp_out
+        assert [(sig, tile.split_verify_output(f)) for sig, f in res["out_frags"][k]] == \
+            [(t, (p, raw)) for p, raw, t in exp_pub]
+    if dedup:
+        ds = res["dedup"]["stats"]
+        assert res["dedup"]["exit"] == 0 and ds["overrun"] == 0 and ds["in_frags"] == n_pub
+        if tiles == 1:                     # one in link: the dedup tile's order is the verify tile's
+            exp_d = tile_model.dedup_model([f for _, f in res["out_frags"][0]], dseed, 1 << 14)
+            assert [f for _, f in res["dedup_frags"]] == exp_d
+        assert all(sig == 0 for sig, _ in res["dedup_frags"])
+    return res, exp
 
 
-def test_engine_process_pipeline_cpu(oracle):
+def test_engine_process_pipeline_cpu(tmp_path, oracle):
     ps = _mixed_stream(600, seed=71)
-    exp_out = _pipeline(ps, False, oracle)
-    assert exp_out.count(-2) > 10 and exp_out.count(-1) > 10
+    res, exp = _xproc_vs_model(tmp_path, ps, oracle, engine_cmd=CPU_ENGINE, depth=1 << 12, batch=64, inflight=3)
+    assert exp[0][0].count(-2) > 10 and exp[0][0].count(-1) > 10
+    assert res["engine"]["verifier"].startswith("oracle")
+
+
+def test_engine_process_two_tiles_cpu(tmp_path, oracle):
+    """Two verify tiles in the engine process take the round-robin shares of
+    the link (fd_verify.c:46), each into its own out link."""
+    ps = _mixed_stream(800, seed=74)
+    _xproc_vs_model(tmp_path, ps, oracle, tiles=2, engine_cmd=CPU_ENGINE, depth=1 << 12, batch=64, inflight=3)
 
 
 @pytest.mark.gpu
-def test_engine_process_pipeline_gpu(oracle):
+def test_engine_process_pipeline_gpu(tmp_path, oracle):
+    """The deployable shape on the MI355X: the engine process's gather tile
+    reads every payload where the producer process wrote it (the link's
+    shared-memory region registered with its engine), verifies it on the GPU
+    and writes its out frag; two tiles in the second run."""
     ps = _mixed_stream(3000, seed=72)
-    exp_out = _pipeline(ps, True, oracle, batch=512)
-    assert exp_out.count(0) > 1000
+    res, exp = _xproc_vs_model(tmp_path, ps, oracle, depth=1 << 12, batch=512, inflight=3)
+    assert exp[0][0].count(0) > 1000 and res["engine"]["device"] == 0
+    _xproc_vs_model(tmp_path, ps, oracle, tiles=2, depth=1 << 12, batch=512, inflight=3, dedup=False)
 
 
 @pytest.mark.gpu
-def test_engine_process_cli_gpu(oracle):
+def test_engine_process_lapped_gpu(tmp_path, oracle):
+    """The cross-process gather tile against a producer process that laps it:
+    lap guard off, batches held 3 ms, a 1024-deep link fed at 1 M frags/s.
+    The device's re-check drops exactly the frags the producer overwrote
+    before the read; every kept frag's outcome and the published stream equal
+    the model's over exactly those frags, none published torn."""
+    seed = 0x1AB
+    ps = _mixed_stream(20000, seed=31)
+    res = xproc.run(_npz(tmp_path, ps), len(ps), tiles=1, producers=1, mode="paced", rate=1.0e6, depth=1024,
+                    batch=4096, inflight=3, wait_us=3000, lap_guard=False, seed=seed, log=True, timeout=180)
+    st, mux = res["engine"]["stats"], res["engine"]["mux"]
+    assert st["corrupt"] == 0 and st["verify_errors"] == 0
+    seqs, codes = res["logs"][0]
+    assert len(seqs) + mux["overrun_polling"] + mux["overrun_reading"] == len(ps)
+    lost = codes == tile.LOG_LOST
+    assert int(lost.sum()) == st["lapped"] > 1000
+    kept = seqs[~lost].tolist()
+    exp_out, exp_pub = tile_model.verify_tile_model([ps[s] for s in kept], seed,
+                                                    lambda a, t: oracle.verify_txns(a, t), seqs=kept)
+    assert codes[~lost].tolist() == exp_out and len(kept) > 2000
+    assert [(sig, tile.split_verify_output(f)) for sig, f in res["out_frags"][0]] == \
+        [(t, (p, raw)) for p, raw, t in exp_pub]
+
+
+@pytest.mark.gpu
+def test_engine_process_cli_gpu(oracle, tmp_path):
     """`python -m firedancer_amd.engine_proc` as an operator starts it: joins
-    the links by path, verifies on the GPU, prints the tile's stats."""
+    links another process formatted, verifies on the GPU, prints the tiles'
+    stats."""
     import json
     import subprocess
-    import sys
     ps = _mixed_stream(1500, seed=73)
     paths = [_shm_path(n) for n in ("qv", "vd")]
     try:
         inl = tile.Link.shm_create(paths[0], 1 << 12, 1232)
-        vd = tile.Link.shm_create(paths[1], 1 << 12, tile.TPU_DCACHE_MTU)
+        vd = tile.Link.shm_create(paths[1], 1 << 12, tile.TPU_DCACHE_MTU,
+                                  data_sz=tile.vmux_dcache_data_sz(1 << 12, 512, 3))
         for p in ps:
             inl.publish(p)
         r = subprocess.run([sys.executable, "-m", "firedancer_amd.engine_proc", "--in", paths[0], "--out", paths[1],
-                            "--frags", str(len(ps)), "--batch", "512", "--timeout", "60"],
-                           capture_output=True, text=True, timeout=120,
-                           cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+                            "--frags", str(len(ps)), "--batch", "512", "--inflight", "3", "--timeout", "60"],
+                           capture_output=True, text=True, timeout=120, cwd=REPO)
         assert r.returncode == 0, r.stderr[-2000:]
-        st = json.loads(r.stdout.strip().splitlines()[-1])
+        st = json.loads(r.stdout.strip().splitlines()[-1])["stats"]
         exp_out, exp_pub = tile_model.verify_tile_model(ps, 0x5EEDF00D, lambda a, t: oracle.verify_txns(a, t))
         assert st["published"] == exp_out.count(0) and st["verify_failed"] == exp_out.count(-1)
         assert [m["sig"] for m, _ in vd.drain()] == [t for _, _, t in exp_pub]

@@ -297,7 +297,7 @@ def test_ring_frag_io_batches(engine, oracle, txn_fixtures, quic_corpus):
         stray = np.zeros(4096, dtype=np.uint8)
         fio = np.zeros(1, dtype=FRAG_IO_DTYPE)
         fio[0] = ((stray.ctypes.data + 63) // 64 * 64, 100, 0, L.fdgpu_frag_out_cap(100), 0, 0)
-        with pytest.raises(RuntimeError):
+        with pytest.raises(RuntimeError, match=r"\(-14\)"):          # FDGPU_ERR_UNREG: a wiring error
             engine.submit_frags_io(fio, out_buf, 4096, seed)
     finally:
         engine.host_unregister(in_buf)

@@ -501,3 +501,44 @@ def test_vmux_reference_metrics(oracle):
     assert sum(m["loop_caught_up_duration_ticks"]["counts"]) > 0 and m["housekeeping_cnt"] > 0
     assert m["tick_per_ns"] > 0.1 and m["tile_tid"] > 0 and m["stem_in_backpressure"] == 0
     vm.close()
+
+
+def test_vmux_metrics_snapshots_are_consistent(oracle):
+    """the loop's metrics copy is a seqlock.  Snapshots taken
+    while the tile runs are each internally consistent -- the handled-size
+    histogram holds exactly the link's published count, the filtered one its
+    filtered count -- and the counters never go backwards between them."""
+    import threading
+    ps = _mixed_stream(4000, seed=43)
+    ver = tile.PyVerifier(oracle_fn(oracle), slots=2)
+    inl = tile.Link(1 << 13, 1232)
+    outl = tile.Link(1 << 13, tile.TPU_DCACHE_MTU, data_sz=(len(ps) + 8) * (tile.TPU_DCACHE_MTU + 64))
+    vm = tile.VerifyMuxTile(inl, outl, ver, hashmap_seed=0x43, batch_txn_max=64, inflight_max=2,
+                            batch_wait_us=50, metrics=True, lazy_iters=1)
+    snaps, stop = [], threading.Event()
+
+    def watch():
+        while not stop.is_set():
+            snaps.append(vm.metrics())
+
+    th = threading.Thread(target=watch)
+    for p in ps:
+        inl.publish(p)
+    th.start()
+    try:
+        vm.run(len(ps), timeout_s=60)
+    finally:
+        stop.set()
+        th.join()
+    snaps.append(vm.metrics())
+    assert len(snaps) > 5
+    last = (0, 0, 0)
+    for m in snaps:
+        li = m["link_in"][0]
+        assert sum(m["fragment_handled_size_bytes"]["counts"]) == li["published_count"]
+        assert sum(m["fragment_filtered_size_bytes"]["counts"]) == li["filtered_count"]
+        cur = (m["housekeeping_cnt"], li["published_count"], li["filtered_count"])
+        assert all(a >= b for a, b in zip(cur, last))
+        last = cur
+    assert last[1] + last[2] == len(ps)
+    vm.close()

@@ -326,6 +326,33 @@ def test_vmux_gather_lap_guard_gpu(engines, oracle):
     assert kept >= len(ps) * 0.95, (st, mst)
 
 
+def test_vmux_gather_unregistered_mcache_is_fatal_gpu(engines):
+    """a gather tile whose in-link mcache was never registered
+    with the engines (only the dcaches were) must stop with the engine's
+    FDGPU_ERR_UNREG (-14) at its first submit -- not reject every batch as
+    malformed while it looks healthy."""
+    from test_tile import _mixed_stream
+    ps = _mixed_stream(300, seed=5)
+    inl = tile.Link(1 << 10, 1232)
+    outl = tile.Link(1 << 10, tile.TPU_DCACHE_MTU, data_sz=tile.vmux_dcache_data_sz(1 << 10, 64, 2))
+    ver = tile.EngineVerifier(engines[:1])
+    vm = tile.VerifyMuxTile(inl, outl, ver, batch_txn_max=64, inflight_max=2, gpu_parse=2, register=False)
+    for b in (outl.dcache, inl.dcache):
+        engines[0].host_register(b)
+    try:
+        for p in ps:
+            inl.publish(p)
+        with pytest.raises(RuntimeError, match="-14"):
+            vm.run(len(ps), timeout_s=30)
+        st = vm.stats()
+        assert st["published"] == 0 and st["verify_errors"] == 0
+    finally:
+        vm.close()
+        ver.close()
+        for b in (outl.dcache, inl.dcache):
+            engines[0].host_unregister(b)
+
+
 def test_vmux_gather_reads_reasm_link_gpu(oracle, engines):
     """The gather-mode mux tile on the reference's actual quic -> verify link
     type, the TPU reassembly slot arena (fd_tpu.h:20-45, fd_frankendancer.c:

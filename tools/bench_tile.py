@@ -96,11 +96,29 @@ def make_parser():
                     help="1: size every engine slot for max_sig before timing (fdgpu_engine_reserve)")
     ap.add_argument("--cpu-list", default="", help="','-separated CPUs to pin producers and tiles to, in order")
     ap.add_argument("--device", type=int, default=-1, help="the GPU every tile's engine uses (-1: tile k on k %% gpus)")
+    ap.add_argument("--xproc", type=int, default=0,
+                    help="1: the deployable shape -- producers in a process of their own (tools/quic_feed.py), the "
+                         "gather-mode mux tiles in the engine process (python -m firedancer_amd.engine_proc), links "
+                         "in shared memory faulted in before the run (tools/xproc.py); this process opens no engine")
+    ap.add_argument("--pages", default="4k", help="(xproc) link memory: 4k, shm-thp or hugetlb (tile.PAGES)")
+    ap.add_argument("--link-pages", default="",
+                    help="(in-process mux) link memory faulted in before the run: 4k or thp (anonymous 2 MB "
+                         "pages); empty: numpy pages faulted in by their first use")
+    ap.add_argument("--dedup", type=int, default=0, help="(xproc) 1: a sandboxed dedup process reads the out links")
+    ap.add_argument("--device-rank", type=int, default=-1,
+                    help="(bench.py's ranks) the GPU every tile's engine uses is this rank %% the visible devices: the "
+                         "child counts them, so its parent rank starts no HIP runtime of its own before the tiles run")
     return ap
 
 
 def main():
     args = make_parser().parse_args()
+    if args.device_rank >= 0 and not args.xproc:
+        from firedancer_amd import _lib
+        ndev = _lib.lib().fdgpu_device_count()
+        if ndev < 1:
+            raise SystemExit("bench_tile: no HIP device visible")
+        args.device = args.device_rank % ndev
     t0 = time.time()
     if args.payload_npz:
         z = np.load(args.payload_npz)
@@ -113,6 +131,10 @@ def main():
         arena, offs, sizes = workload.pack_payloads(ps)
         n_sig = int(t["sig_cnt"].sum())
         del a, t
+    if args.xproc and not args.payload_npz:
+        import tempfile
+        _NPZ["path"] = os.path.join(tempfile.mkdtemp(prefix="fdgpu_bt_"), "frags.npz")
+        np.savez(_NPZ["path"], arena=arena, offs=offs, sizes=sizes)
     print(f"[bench_tile] {len(ps)} txns / {n_sig} sigs ready in {time.time() - t0:.1f}s", flush=True)
     cpus = [int(x) for x in args.cpu_list.split(",") if x] or None
     depth_lg = args.depth_lg
@@ -129,7 +151,10 @@ def main():
         args.producers = int(run[4]) if len(run) > 4 else int(tiles_n) if args.producers_same_as_tiles else prods0
         args.batch_sig_max = int(run[5]) if len(run) > 5 and run[5] > 0 else sig_max0
         args.depth_lg = args.depth_lg_paced if rate > 0 and args.depth_lg_paced else depth_lg
-        if args.mux:
+        if args.xproc:
+            res = run_once_xproc(args, n_sig, modes, len(ps), int(tiles_n), int(batch), int(inflight), rate,
+                                 cpus=cpus)
+        elif args.mux:
             res = run_once_mux(args, ps, arena, offs, sizes, n_sig, modes, int(tiles_n), int(batch), int(inflight),
                                rate, cpus=cpus, device=args.device if args.device >= 0 else None)
         else:
@@ -147,6 +172,58 @@ def main():
     return 0 if ok else 1
 
 
+def run_once_xproc(args, n_sig, modes, n_payloads, tiles_n, batch, inflight, rate, cpus=None):
+    """One run of the cross-process shape (tools/xproc.py): links in shared
+    memory, producers in their own process, the gather-mode mux tiles in the
+    engine process; the same result keys as run_once_mux."""
+    import xproc
+    npz = args.payload_npz or _NPZ["path"]
+    P = max(1, args.producers)
+    prefill = rate < 0
+    reps = 1 if prefill else max(1, getattr(args, "paced_reps", 1))
+    cpus = cpus or workload.physical_cpus()[getattr(args, "cpu_offset", 0):] or workload.physical_cpus()
+    dev_rank = args.device_rank if args.device_rank >= 0 else max(args.device, 0)
+    r = xproc.run(npz, n_payloads, tiles=tiles_n, producers=P, mode="prefill" if prefill else "paced",
+                  rate=0.0 if prefill else rate, reps=reps, depth=1 << args.depth_lg, batch=batch, inflight=inflight,
+                  wait_us=args.wait_us, batch_sig_max=getattr(args, "batch_sig_max", 0), pages=args.pages,
+                  cpus=cpus[:P + tiles_n + 1], device_rank=dev_rank, dedup=bool(args.dedup),
+                  lap_guard=bool(args.lap_guard), pair=args.pair, spread=args.spread, hw_queues=args.hw_queues,
+                  dedup_frags=int((modes == 0).sum()) * (sum(xproc.quic_feed.frag_counts(n_payloads, P,
+                                  "prefill" if prefill else "paced", reps)) // n_payloads))
+    er, feed = r["engine"], r["feed"]
+    n_total = r["txns"]
+    wall = r["wall_s"]
+    agg = er["stats"]
+    res = {
+        "metric": "verify mux tile end-to-end transactions/s, cross-process (quic process -> engine process -> "
+                  "out links)",
+        "tile": "fdgpu_vmux on fdt_mux_run in the engine process (python -m firedancer_amd.engine_proc); the GPU "
+                "reads the payloads where the producer process wrote them (shared-memory links registered with the "
+                "engines), parses, verifies and writes the out frags",
+        "xproc": True, "pages": args.pages, "dedup_process": bool(args.dedup),
+        "producers": P, "txns_per_s": round(n_total / wall, 1), "sigs_per_s": round(n_sig * n_total / n_payloads / wall, 1),
+        "wall_s": round(wall, 4), "producer_s": round(max(feed["producer_s"]), 4),
+        "producer_published": int(sum(feed["published"])), "gpus": args.gpus, "tiles": tiles_n,
+        "batch_txn_max": batch, "inflight": inflight, "engines": tiles_n, "engine_slots": inflight,
+        "batch_sig_max": getattr(args, "batch_sig_max", 0) or batch * 12, "rate_target": rate, "prefill": prefill,
+        "link_depth": 1 << args.depth_lg, "offered_txns_per_s": None if prefill else feed["offered_per_s"],
+        "stream_reps": reps, "lap_guard": int(args.lap_guard),
+        "workload": "cfg3 (1-12 sigs/txn, payload <= 1232 B, 10% corrupted)" if getattr(args, "multi", 0)
+        else "cfg1 (1 sig, msg U[180,220] B, 10% corrupted)",
+        "txns": n_total, "sigs": n_sig * n_total // n_payloads, "batch_wait_us": args.wait_us,
+        "cpus": cpus[:P + tiles_n + 1], "batch_latency_ms": er["batch_latency_ms"], "counters": agg,
+        "mux": er["mux"], "expected_published": int((modes == 0).sum()) * (n_total // n_payloads),
+        "in_huge_bytes": r["in_huge_bytes"], "engine_pid": er["pid"], "feed_pid": feed["pid"],
+    }
+    if "dedup" in r:
+        res["dedup"] = r["dedup"]
+    res["published_ok"] = agg["published"] == res["expected_published"]
+    return res
+
+
+_NPZ = {"path": ""}
+
+
 def start_producer(args, inl, arena, offs, sizes, rate, cpus, k=0):
     """The producer's C thread inherits the creating thread's CPU mask: pin
     this thread to cpus[k] around its start."""
@@ -161,59 +238,9 @@ def start_producer(args, inl, arena, offs, sizes, rate, cpus, k=0):
 
 
 def warm(engines, inflight, out_bytes=0, batch=64):
-    """A full-size batch through every ring slot of every engine before the
-    timed region: a HIP stream's first submission creates its hardware queue
-    (milliseconds), and a slot sizes its workspace (and the gather path its
-    out image) on first use to the batch it carries -- both would otherwise
-    land inside the run."""
-    a, t, _ = workload.cfg1(64, seed=7)
-    ps = workload.payloads(a, t)
-    ps = [ps[k % len(ps)] for k in range(batch)]
-    a, t, _ = workload.cfg1(batch, seed=7)
-    pa, po, psz = workload.pack_payloads(ps)
-    fx = np.zeros(len(ps), dtype=tile.FRAG_EX_DTYPE)
-    fx["off"], fx["sz"] = po, psz
-    tr = 0
-    for k, p in enumerate(ps):
-        fp, _ = tile.txn_peek(p)
-        fx[k]["tr_off"], fx[k]["tr_cap"] = tr, fp
-        tr += (fp + 3) & ~3
-    for e in engines:
-        tks = [e.submit(a, t) for _ in range(inflight)]
-        for tk in tks:
-            e.poll(tk, blocking=True)
-        tks = [e.submit_frags(pa, fx, tr) for _ in range(inflight)]     # the slots' GPU-parse buffers too
-        for tk in tks:
-            e.poll_frags(tk, blocking=True)
-    if out_bytes:
-        warm_io(engines, inflight, ps, out_bytes)
-
-
-def warm_io(engines, inflight, ps, out_bytes):
-    """The gather path's slot buffers (payload addresses, the out image sized
-    for a full batch's out bytes) through every ring slot."""
-    from firedancer_amd.ed25519 import FRAG_IO_DTYPE
-    from firedancer_amd import _lib
-    L = _lib.lib()
-    src = np.zeros(len(ps) * 1280 + 8192, dtype=np.uint8)
-    src = src[(-src.ctypes.data) % 4096:][:len(ps) * 1280 + 4096]
-    out = np.zeros(out_bytes + 8192, dtype=np.uint8)
-    out = out[(-out.ctypes.data) % 4096:][:out_bytes + 4096]
-    fio = np.zeros(len(ps), dtype=FRAG_IO_DTYPE)
-    o = 0
-    for k, p in enumerate(ps):
-        src[k * 1280:k * 1280 + len(p)] = np.frombuffer(p, dtype=np.uint8)
-        cap = L.fdgpu_frag_out_cap(len(p))
-        fio[k] = (src.ctypes.data + k * 1280, len(p), o, cap, 0, 0)
-        o += (cap + 63) // 64 * 64
-    for e in engines:
-        e.host_register(src)
-        e.host_register(out)
-        tks = [e.submit_frags_io(fio, out, out_bytes, 1) for _ in range(inflight)]
-        for tk in tks:
-            e.poll_frags_io(tk, blocking=True)
-        e.host_unregister(src)
-        e.host_unregister(out)
+    """engine_proc.warm_engines: every ring slot warmed before the timed region"""
+    from firedancer_amd.engine_proc import warm_engines
+    warm_engines(engines, inflight, out_bytes=out_bytes, batch=batch)
 
 
 def run_once(args, ps, arena, offs, sizes, n_sig, modes, tiles_n, batch, inflight, rate):
@@ -292,11 +319,13 @@ def run_once_mux(args, ps, arena, offs, sizes, n_sig, modes, tiles_n, batch, inf
     # tiles sharing an engine share its `inflight` ring slots (each tile may hold up to all of them)
     engines = engine_pool(args, (tiles_n + tpe - 1) // tpe, batch, inflight, device)
     P = max(1, args.producers)
-    inls = [tile.Link(1 << args.depth_lg, 1232) for _ in range(P)]
+    lp = getattr(args, "link_pages", "") or None
+    inls = [tile.Link(1 << args.depth_lg, 1232, pages=lp) for _ in range(P)]
     vms, vers = [], []
     for k in range(tiles_n):
         ver = tile.EngineVerifier([engines[k // tpe]])
-        outl = tile.Link(1 << 14, tile.TPU_DCACHE_MTU, data_sz=tile.vmux_dcache_data_sz(1 << 14, batch, inflight))
+        outl = tile.Link(1 << 14, tile.TPU_DCACHE_MTU, data_sz=tile.vmux_dcache_data_sz(1 << 14, batch, inflight),
+                         pages=lp)
         guard = {} if getattr(args, "lap_guard", 1) else dict(lap_span_max=tile.LAP_OFF, lap_margin=tile.LAP_OFF)
         vms.append(tile.VerifyMuxTile(inls, outl, ver, batch_txn_max=batch, inflight_max=inflight,
                                       batch_wait_us=args.wait_us, round_robin_idx=k, round_robin_cnt=tiles_n,
@@ -391,6 +420,7 @@ def run_once_mux(args, ps, arena, offs, sizes, n_sig, modes, tiles_n, batch, inf
         # what the producers actually offered: frags published / their publishing time
         "offered_txns_per_s": round(n_pub / prod_s, 1) if prod_s > 0 and not prefill else None,
         "stream_reps": reps, "lap_guard": int(getattr(args, "lap_guard", 1)),
+        "link_pages": lp or "numpy (first-touch)", "in_huge_bytes": [ln.huge_bytes() for ln in inls],
         "workload": "cfg3 (1-12 sigs/txn, payload <= 1232 B, 10% corrupted)" if getattr(args, "multi", 0) else "cfg1 (1 sig, msg U[180,220] B, 10% corrupted)",
         "txns": n_total, "sigs": n_sig * n_total // len(ps), "batch_wait_us": args.wait_us, "cpus": cpus[:P + tiles_n],
         "batch_latency_ms": {"p50": round(float(np.percentile(lat, 50)), 3) if len(lat) else None,
