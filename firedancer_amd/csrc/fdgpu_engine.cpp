@@ -108,7 +108,9 @@ struct Slot {
      demand); the read-back is [codes][tags][out sizes] in h_tr */
   bool io = false;
   uint8_t *h_io = nullptr, *d_ioh = nullptr;  /* pinned [frag records][payload addresses]; its device view */
-  fdgpu_frag_ex_t *d_fxio = nullptr;          /* the records, kept on the device by the gather */
+  fdgpu_frag_ex_t *d_fxio = nullptr;          /* the records, kept on the device by the ingest */
+  uint32_t *d_io_cnt = nullptr;               /* the ingest's signature count: zero at the start of a gathered
+                                                 batch (cleared by the finish of the slot's previous one) */
   uint8_t *d_trh = nullptr;                   /* h_tr's device-side address (results written in place) */
   /* FDGPU_FLAG_MERGE: the batch's gather + parse are queued and its verify
      waits to be merged with the other batches ready (merge_kick), which then
@@ -196,7 +198,8 @@ void slot_free(Slot &s) {
   if (s.h_tr) (void)hipHostFree(s.h_tr);
   if (s.h_io) (void)hipHostFree(s.h_io);
   for (void *p : {(void *)s.d_fx, (void *)s.d_txn_out, (void *)s.d_txn_sz, (void *)s.d_txd, (void *)s.d_cnt,
-                  (void *)s.d_sig0, (void *)s.d_blocktot, (void *)s.d_n_sig, (void *)s.d_tr, (void *)s.d_fxio})
+                  (void *)s.d_sig0, (void *)s.d_blocktot, (void *)s.d_n_sig, (void *)s.d_tr, (void *)s.d_fxio,
+                  (void *)s.d_io_cnt})
     if (p) (void)hipFree(p);
   s = Slot{};
 }
@@ -286,6 +289,8 @@ bool slot_io_bufs(Slot &s, const fdgpu_cfg_t &c) {
   HIPCHK(hipHostMalloc((void **)&s.h_io, bytes, hipHostMallocDefault), false);
   HIPCHK(hipHostGetDevicePointer((void **)&s.d_ioh, s.h_io, 0), false);
   HIPCHK(hipMalloc((void **)&s.d_fxio, m * sizeof(fdgpu_frag_ex_t)), false);
+  HIPCHK(hipMalloc((void **)&s.d_io_cnt, 64), false);
+  HIPCHK(hipMemsetAsync(s.d_io_cnt, 0, 64, s.stream), false);    /* ordered before the slot's first batch */
   return true;
 }
 
@@ -1034,7 +1039,7 @@ int io_tail(fdgpu_engine_t *e, Slot *s) {
   const uint64_t n = s->m_n, cb = s->m_cb;
   HIPCHK(fdgpu_launch_frag_finish_io(s->d_txns, (uint32_t)n, s->d_sig_codes, s->d_txn_sz, s->d_fxio, s->d_txn_out,
                                      s->d_arena, s->m_seed, s->m_out, (int8_t *)s->d_trh, (uint64_t *)(s->d_trh + cb),
-                                     (uint16_t *)(s->d_trh + cb + n * 8), s->stream),
+                                     (uint16_t *)(s->d_trh + cb + n * 8), s->d_io_cnt, s->stream),
          FDGPU_ERR_DEVICE);
   slot_flag_next(s);
   if (e->flag_poll && !e->drop_flag) HIPCHK(hipStreamWriteValue32(s->stream, s->d_flag, s->flag_seq, 0), FDGPU_ERR_DEVICE);
@@ -1085,7 +1090,7 @@ int merge_kick_queue(fdgpu_engine_t *e, bool force) {
   if (nb == 1) {                               /* alone: the ring path's kernels (FDGPU_FLAG_PAIR_AUTO applies) */
     Slot *s = e->pending[0];
     HIPCHK(fdgpu_launch_verify_sigs(s->d_arena, s->d_sigs, (uint32_t)s->m_bound, nullptr, e->d_btab, s->d_ws,
-                                    s->d_sig_codes, ring_kflags(e, s, s->m_bound), m.stream, s->d_n_sig,
+                                    s->d_sig_codes, ring_kflags(e, s, s->m_bound), m.stream, s->d_io_cnt,
                                     e->resident_blocks, e->kc_seed, 1),
            FDGPU_ERR_DEVICE);
   } else {
@@ -1094,11 +1099,12 @@ int merge_kick_queue(fdgpu_engine_t *e, bool force) {
     for (uint32_t j = 0; j < nb; j++) {
       Slot *s = e->pending[j];
       const uint32_t grid = (uint32_t)((s->m_bound + FDGPU_BLOCK - 1) / FDGPU_BLOCK);
-      const uint32_t slow = grid < e->resident_blocks ? grid : e->resident_blocks;
+      uint32_t slow = grid < e->resident_blocks ? grid : e->resident_blocks;
+      if (slow > FDGPU_FULL_BLOCKS) slow = FDGPU_FULL_BLOCKS;
       uint32_t *cnt = fdgpu_verify_cnt_word(s->d_ws, (uint32_t)s->m_bound);
       s->k_sigs = s->m_bound;
       s->k_lanes = s->m_bound;                 /* one lane each: the merged launch never takes the pair kernel */
-      tab[j] = fdgpu_mbatch_t{s->d_arena, s->d_sigs, s->d_n_sig, s->d_ws, s->d_sig_codes,
+      tab[j] = fdgpu_mbatch_t{s->d_arena, s->d_sigs, s->d_io_cnt, s->d_ws, s->d_sig_codes,
                               cnt - (size_t)grid * FDGPU_BLOCK, cnt, (uint32_t)s->m_bound, slow};
       grid_max = grid > grid_max ? grid : grid_max;
       slow_max = slow > slow_max ? slow : slow_max;
@@ -1213,13 +1219,11 @@ int64_t fdgpu_submit_frags_io(fdgpu_engine_t *e, fdgpu_frag_io_t const *fio, uin
   if (n) {
     const fdgpu_frag_ex_t *d_fx = s->d_fxio;
     const bool zero_cnt = !(kflags(e) & FDGPU_FLAG_KCACHE);
-    HIPCHK(fdgpu_launch_frag_gather((const uint64_t *)(s->d_ioh + src_at), (const fdgpu_frag_ex_t *)s->d_ioh,
-                                    any_chk ? (const uint64_t *)(s->d_ioh + chk_at) : nullptr, (uint32_t)n,
-                                    s->d_arena, s->d_fxio, zero_cnt ? fdgpu_verify_cnt_word(s->d_ws, (uint32_t)bound) : nullptr,
-                                    s->d_n_sig, s->stream),
-           FDGPU_ERR_DEVICE);
-    HIPCHK(fdgpu_launch_frag_parse_expand(s->d_arena, d_fx, (uint32_t)n, s->d_txn_out, s->d_txn_sz, s->d_sigs, s->d_txns,
-                                          s->d_n_sig, s->stream),
+    HIPCHK(fdgpu_launch_frag_ingest_io((const uint64_t *)(s->d_ioh + src_at), (const fdgpu_frag_ex_t *)s->d_ioh,
+                                       any_chk ? (const uint64_t *)(s->d_ioh + chk_at) : nullptr, (uint32_t)n,
+                                       s->d_arena, s->d_fxio, s->d_txn_out, s->d_txn_sz, s->d_sigs, s->d_txns,
+                                       s->d_io_cnt,
+                                       zero_cnt ? fdgpu_verify_cnt_word(s->d_ws, (uint32_t)bound) : nullptr, s->stream),
            FDGPU_ERR_DEVICE);
     if (!e->merges.empty() && zero_cnt && bound) {
       /* the verify waits to be merged with the other batches ready (merge_kick) */
@@ -1235,11 +1239,12 @@ int64_t fdgpu_submit_frags_io(fdgpu_engine_t *e, fdgpu_frag_io_t const *fio, uin
       return s->ticket;
     }
     HIPCHK(fdgpu_launch_verify_sigs(s->d_arena, s->d_sigs, (uint32_t)bound, nullptr, e->d_btab, s->d_ws, s->d_sig_codes,
-                                    ring_kflags(e, s, bound), s->stream, s->d_n_sig, e->resident_blocks, e->kc_seed, zero_cnt),
+                                    ring_kflags(e, s, bound), s->stream, s->d_io_cnt, e->resident_blocks, e->kc_seed,
+                                    zero_cnt),
            FDGPU_ERR_DEVICE);
     HIPCHK(fdgpu_launch_frag_finish_io(s->d_txns, (uint32_t)n, s->d_sig_codes, s->d_txn_sz, d_fx, s->d_txn_out,
                                        s->d_arena, hash_seed, out_dev, (int8_t *)s->d_trh, (uint64_t *)(s->d_trh + cb),
-                                       (uint16_t *)(s->d_trh + cb + n * 8), s->stream),
+                                       (uint16_t *)(s->d_trh + cb + n * 8), s->d_io_cnt, s->stream),
            FDGPU_ERR_DEVICE);
   }
   slot_flag_next(s);

@@ -59,6 +59,16 @@ typedef struct {
    two-lane block's 40 KB: these make one block per CU the most that fits */
 #define FDGPU_SPREAD_LDS       1024u
 #define FDGPU_SPREAD_LDS_PAIR  (40u * 1024u + 1024u)
+/* The verify blocks (two 256-VGPR waves per SIMD) fill every SIMD's register
+   file, so a kernel queued behind or beside a running verify starts its
+   workgroups only as verify blocks retire: a launch of many workgroups then
+   waits through many retirements before its last one runs (rocprofv3, host-fed
+   1M batches: an empty fallback launch of 512 blocks took 0.8 ms, the 3,907-
+   block combine 0.66 ms; profiles/r05/hostfed_trace.md).  The short kernels
+   around the verify therefore run on few, fat workgroups that stride over
+   their work: */
+#define FDGPU_FULL_BLOCKS   16u           /* the fallback chain: its queue is ~empty (split failures ~2^-30) */
+#define FDGPU_AUX_BLOCKS    64u           /* combine, the gathered batches' ingest and finish */
 /* SHA-512 block-count groups of the host-side bucketing (expand): messages of
    more blocks than this share the last group */
 #define FDGPU_NBLK_GROUPS   32u
@@ -145,28 +155,32 @@ hipError_t fdgpu_launch_frag_ring(const uint8_t *d_arena, const fdgpu_frag_ex_t 
 hipError_t fdgpu_launch_frag_finish(const fdgpu_txn_desc_t *d_tds, uint32_t n, const int8_t *d_sig_codes,
                                     const uint16_t *d_txn_sz, const fdgpu_frag_ex_t *d_fx, const uint8_t *d_txn_out,
                                     int8_t *d_codes, uint8_t *d_trailers, hipStream_t stream);
-/* fdgpu_submit_frags_io: one wave per frag copies its payload (16-B units)
-   from host memory (d_src[i], the registered region's device-side address)
-   to d_arena + d_fx[i].off; with d_chk (n pairs {mcache line address, seq},
-   line 0: none) the line is re-read after the copy and a republished one
-   marks the kept record FDGPU_FX_LAPPED; the finish kernel writes per frag
-   the code, the dedup tag and the out frag's size, and assembles the out
-   frag at d_out + d_fx[i].tr_off ([payload][pad][fd_txn_t][u16 sz]) */
+/* fdgpu_submit_frags_io's kernels, each on at most FDGPU_AUX_BLOCKS blocks
+   whose waves stride over groups of 64 frags.  Ingest: per group, the wave
+   reads the 64 records and payload addresses (one coalesced read of each over
+   the bus), copies the group's payloads (16-B units, flattened over the
+   group, four loads in flight per lane) from host memory (d_src[i], the
+   registered region's device-side address) to d_arena + d_fx[i].off; with
+   d_chk (n pairs {mcache line address, seq}, line 0: none) each line is
+   re-read once the payload loads have returned, and a republished one marks
+   the kept record FDGPU_FX_LAPPED; then lane i parses frag i (fd_txn_parse)
+   and the wave takes its descriptor slots with one atomic add on *d_n_sig,
+   which must be zero at the start (the finish kernel of the slot's previous
+   gathered batch clears it: d_zero_next).  Finish: per group, lane i writes
+   frag i's code, dedup tag and out size, then the wave assembles the group's
+   out frags at d_out + d_fx[i].tr_off ([payload][pad][fd_txn_t][u16 sz]) in
+   16-B stores. */
 #define FDGPU_FX_LAPPED 0x80000000u     /* in fdgpu_frag_ex_t.tr_cap (out_cap <= 0xFFFF) */
 uint64_t   fdgpu_frag_fp_bound(uint32_t sz);
-hipError_t fdgpu_launch_frag_gather(const uint64_t *d_src, const fdgpu_frag_ex_t *d_fx, const uint64_t *d_chk, uint32_t n,
-                                    uint8_t *d_arena, fdgpu_frag_ex_t *d_fx_dev, uint32_t *d_zero_word,
-                                    uint32_t *d_zero_word2, hipStream_t stream);
-/* gathered batches: parse + descriptor expansion in one launch, each wave
-   taking its descriptor slots with one atomic add on *d_n_sig (which must
-   start at zero: the gather kernel clears it) */
-hipError_t fdgpu_launch_frag_parse_expand(const uint8_t *d_arena, const fdgpu_frag_ex_t *d_fx, uint32_t n,
-                                          uint8_t *d_txn_out, uint16_t *d_txn_sz, fdgpu_sig_desc_t *d_sigs,
-                                          fdgpu_txn_desc_t *d_tds, uint32_t *d_n_sig, hipStream_t stream);
+hipError_t fdgpu_launch_frag_ingest_io(const uint64_t *d_src, const fdgpu_frag_ex_t *d_fx, const uint64_t *d_chk,
+                                       uint32_t n, uint8_t *d_arena, fdgpu_frag_ex_t *d_fx_dev, uint8_t *d_txn_out,
+                                       uint16_t *d_txn_sz, fdgpu_sig_desc_t *d_sigs, fdgpu_txn_desc_t *d_tds,
+                                       uint32_t *d_n_sig, uint32_t *d_zero_word, hipStream_t stream);
 hipError_t fdgpu_launch_frag_finish_io(const fdgpu_txn_desc_t *d_tds, uint32_t n, const int8_t *d_sig_codes,
                                        const uint16_t *d_txn_sz, const fdgpu_frag_ex_t *d_fx, const uint8_t *d_txn_out,
                                        const uint8_t *d_arena, uint64_t hash_seed, uint8_t *d_out, int8_t *d_codes,
-                                       uint64_t *d_tags, uint16_t *d_out_szs, hipStream_t stream);
+                                       uint64_t *d_tags, uint16_t *d_out_szs, uint32_t *d_zero_next,
+                                       hipStream_t stream);
 hipError_t fdgpu_launch_test_hs_split(const uint32_t *d_in, uint32_t *d_out, uint32_t n, hipStream_t stream);
 
 #ifdef __cplusplus

@@ -1027,24 +1027,27 @@ __global__ void __launch_bounds__(256) fdgpu_combine_kernel(const fdgpu_txn_desc
                                                             const int8_t *__restrict__ sig_codes,
                                                             int8_t *__restrict__ txn_codes,
                                                             uint64_t *__restrict__ accept) {
-  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-  int code = -1;
-  if (t < n_txn) {
-    const fdgpu_txn_desc_t d = txns[t];
-    if (d.sig_cnt >= 1 && d.sig_cnt <= 16) {             /* else ERR_SIG (fd_ed25519_user.c:238-241) */
-      int first_struct = 0, any_msg = 0;
-      for (uint32_t j = 0; j < d.sig_cnt; j++) {
-        const int c = sig_codes[d.sig0 + j];
-        if (c == -3) any_msg = 1;
-        else if (c != 0 && first_struct == 0) first_struct = c;
+  /* FDGPU_AUX_BLOCKS blocks stride over the batch, 256 txns a step */
+  for (uint32_t t0 = blockIdx.x * blockDim.x; t0 < n_txn; t0 += gridDim.x * blockDim.x) {
+    const uint32_t t = t0 + threadIdx.x;
+    int code = -1;
+    if (t < n_txn) {
+      const fdgpu_txn_desc_t d = txns[t];
+      if (d.sig_cnt >= 1 && d.sig_cnt <= 16) {             /* else ERR_SIG (fd_ed25519_user.c:238-241) */
+        int first_struct = 0, any_msg = 0;
+        for (uint32_t j = 0; j < d.sig_cnt; j++) {
+          const int c = sig_codes[d.sig0 + j];
+          if (c == -3) any_msg = 1;
+          else if (c != 0 && first_struct == 0) first_struct = c;
+        }
+        /* pass 1 reports its first failure before any pass-2 (equation) failure */
+        code = first_struct ? first_struct : (any_msg ? -3 : 0);
       }
-      /* pass 1 reports its first failure before any pass-2 (equation) failure */
-      code = first_struct ? first_struct : (any_msg ? -3 : 0);
+      txn_codes[t] = (int8_t)code;
     }
-    txn_codes[t] = (int8_t)code;
+    const uint64_t ok = __ballot(t < n_txn && code == 0);   /* every lane of the wave takes part */
+    if (accept && (threadIdx.x & 63u) == 0 && t < n_txn) accept[t >> 6] = ok;
   }
-  const uint64_t ok = __ballot(t < n_txn && code == 0);   /* every lane of the wave takes part */
-  if (accept && (threadIdx.x & 63u) == 0 && t < n_txn) accept[t >> 6] = ok;
 }
 
 /* ---------------- test / diagnostic kernels ---------------- */
@@ -1309,58 +1312,6 @@ __global__ void __launch_bounds__(1024) fdgpu_frag_scan_expand_small_kernel(
   }
 }
 
-/* Gathered batches: parse and expand in one launch, lane per txn, no scan
-   kernel.  Each wave scans its 64 signature counts and takes its run of
-   descriptor slots with one atomic add on *n_sig (zeroed by the gather
-   kernel), so the descriptors stay dense in [0, n_sig) -- grouped by wave
-   in whatever order the waves ran, which the codes do not depend on: every
-   txn records its own first slot (tds[t].sig0).  The parse itself is
-   fdgpu_frag_parse_kernel's. */
-__global__ void __launch_bounds__(64) fdgpu_frag_parse_expand_kernel(
-    const uint8_t *__restrict__ arena, const fdgpu_frag_ex_t *__restrict__ fx, uint32_t n,
-    uint8_t *__restrict__ txn_out, uint16_t *__restrict__ txn_sz, fdgpu_sig_desc_t *__restrict__ sigs,
-    fdgpu_txn_desc_t *__restrict__ tds, uint32_t *__restrict__ n_sig) {
-  const uint32_t t = blockIdx.x * 64u + threadIdx.x, lane = threadIdx.x;
-  uint32_t c = 0;
-  fdgpu_txn_t d{};
-  if (t < n) {
-    const fdgpu_frag_ex_t f = fx[t];
-    fdt_txn_t *x = (fdt_txn_t *)(txn_out + (size_t)t * FDT_TXN_MAX_SZ);
-    uint64_t why = 0;
-    /* a lapped payload (the gather's re-check) may be torn: not parsed */
-    uint64_t fp = (f.tr_cap & FDGPU_FX_LAPPED) ? 0u : fdt_parse_core(arena + f.off, f.sz, x, &why);
-    const uint32_t sc = fp ? x->signature_cnt : 0u;
-    c = (sc >= 1u && sc <= 16u) ? sc : 0u;
-    if (c > fdt_frag_sig_bound(f.sz)) { c = 0u; fp = 0u; }      /* cannot happen for a parsed txn */
-    if (fp) {
-      d.msg_off = f.off + x->message_off;
-      d.msg_sz = f.sz - x->message_off;
-      d.sig_off = f.off + x->signature_off;
-      d.pub_off = f.off + x->acct_addr_off;
-    }
-    txn_sz[t] = (uint16_t)fp;
-  }
-  const uint32_t incl = wave_incl_scan(c);
-  const uint32_t total = (uint32_t)__shfl((int)incl, 63, 64);
-  uint32_t base = 0;
-  if (lane == 63u && total) base = atomicAdd(n_sig, total);
-  base = (uint32_t)__shfl((int)base, 63, 64);
-  if (t >= n) return;
-  const uint32_t s0 = base + incl - c;
-  fdgpu_txn_desc_t td;
-  td.sig0 = s0;
-  td.sig_cnt = c;
-  tds[t] = td;
-  for (uint32_t j = 0; j < c; j++) {
-    fdgpu_sig_desc_t sd;
-    sd.msg_off = d.msg_off;
-    sd.msg_sz = d.msg_sz;
-    sd.sig_off = d.sig_off + 64u * j;
-    sd.pub_off = d.pub_off + 32u * j;
-    sigs[s0 + j] = sd;
-  }
-}
-
 /* The end of a ring-slot frag batch in one launch, per txn: the
    batch_single_msg combine of its signatures' codes, FDGPU_CODE_PARSE_FAIL
    for a payload that is not a transaction, and its parsed fd_txn_t copied
@@ -1405,125 +1356,242 @@ __global__ void __launch_bounds__(256) fdgpu_frag_finish_kernel(const fdgpu_txn_
   codes[t] = (int8_t)code;
 }
 
-/* Gathered frag batches (fdgpu_submit_frags_io).  Gather: one wave per frag
-   reads its record and payload address from the slot's pinned upload buffer
-   and copies the payload's 16-B units from host memory (the registered in
-   dcache), both read in place over the bus, to its packed, 16-B aligned
-   place in the batch arena; the units past sz lie in the payload's own 64-B
-   chunks.  With chk, a frag whose pair {line, seq} names an in-mcache line
-   is then re-checked as the reference's mux re-checks after its copy
-   (fd_mux.c:641-655): once the wave's payload loads have returned, the line's
-   seq is read again over the bus (a system-scope load: no cache in between);
-   any other value than the frag's seq means the producer republished the
-   line, so its payload may have been rewritten under the read, and the
-   record is kept with FDGPU_FX_LAPPED set (no parse, no verdict).  The
-   record is kept on the device (fx_dev) for the later kernels, and the
-   first thread clears the verify kernel's queue counter (zero_word): the
-   batch needs no upload copy and no memset. */
-__global__ void __launch_bounds__(256) fdgpu_frag_gather_kernel(const uint64_t *__restrict__ src,
-                                                                const fdgpu_frag_ex_t *__restrict__ fx,
-                                                                const uint64_t *__restrict__ chk, uint32_t n,
-                                                                uint8_t *__restrict__ arena,
-                                                                fdgpu_frag_ex_t *__restrict__ fx_dev,
-                                                                uint32_t *__restrict__ zero_word,
-                                                                uint32_t *__restrict__ zero_word2) {
-  const uint32_t f = blockIdx.x * 4u + (threadIdx.x >> 6), lane = threadIdx.x & 63u;
-  if (blockIdx.x == 0 && threadIdx.x == 0) {
-    if (zero_word) *zero_word = 0u;
-    if (zero_word2) *zero_word2 = 0u;
-  }
-  if (f >= n) return;
-  const uint4 *s = (const uint4 *)src[f];
-  fdgpu_frag_ex_t x = fx[f];
-  uint4 *d = (uint4 *)(arena + x.off);
-  const uint32_t nq = (x.sz + 15u) >> 4;
-  for (uint32_t q = lane; q < nq; q += 64u) d[q] = s[q];
-  if (chk) {
-    const uint64_t line = chk[2u * f];
-    if (line) {
-      /* every payload load of the wave has returned before the line is read */
-      __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      const uint64_t seq = __hip_atomic_load((const uint64_t *)line, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-      if (seq != chk[2u * f + 1u]) x.tr_cap |= FDGPU_FX_LAPPED;
-    }
-  }
-  if (lane == 0) fx_dev[f] = x;
+/* Gathered frag batches (fdgpu_submit_frags_io).  Both kernels run on at
+   most FDGPU_AUX_BLOCKS blocks (fdgpu_internal.h: beside running verifies a
+   launch's workgroups start only as verify blocks retire) and each wave
+   strides over groups of 64 frags, lane i of a group owning frag 64 g + i. */
+
+/* the group's lane that owns flattened unit k: the first lane whose
+   inclusive unit count exceeds k (incl is non-decreasing over the lanes) */
+FDG_DEV uint32_t unit_owner(uint32_t incl, uint32_t k) {
+  uint32_t o = 0;
+#pragma unroll
+  for (uint32_t b = 32; b; b >>= 1)
+    if ((uint32_t)__shfl((int)incl, (int)(o + b - 1u), 64) <= k) o += b;
+  return o;
 }
 
-/* Finish: one wave per frag.  Lane 0 writes the frag's code (the
-   batch_single_msg combine of its signatures; FDGPU_CODE_PARSE_FAIL;
+/* Ingest: per group, lane i reads frag i's record and payload address from
+   the slot's pinned upload buffer (one coalesced read of each over the bus),
+   then the wave copies the group's payloads from host memory (the registered
+   in dcache, read in place) to their packed, 16-B aligned places in the batch
+   arena -- the payloads' 16-B units flattened over the group, four loads in
+   flight per lane (the units past sz lie in the payload's own 64-B chunks).
+   With chk, a frag whose pair {line, seq} names an in-mcache line is then
+   re-checked as the reference's mux re-checks after its copy (fd_mux.c:
+   641-655): once the wave's payload loads have returned, the line's seq is
+   read again over the bus (a system-scope load: no cache in between); any
+   other value than the frag's seq means the producer republished the line,
+   so its payload may have been rewritten under the read, and the record is
+   kept with FDGPU_FX_LAPPED set (no parse, no verdict).  An agent-scope
+   acquire (L1 invalidate) then makes the copied bytes visible to the
+   group's own loads, and lane i parses frag i (fd_txn_parse,
+   fdgpu_frag_parse_kernel's parse) and the wave takes its run of descriptor
+   slots with one atomic add on *n_sig, so the descriptors stay dense in
+   [0, n_sig) grouped by wave (every txn records its own first slot).  The
+   records are kept on the device (fx_dev) for the finish kernel; the first
+   thread clears the verify kernel's queue counter (zero_word). */
+__global__ void __launch_bounds__(256) fdgpu_frag_ingest_io_kernel(
+    const uint64_t *__restrict__ src, const fdgpu_frag_ex_t *__restrict__ fx, const uint64_t *__restrict__ chk,
+    uint32_t n, uint8_t *__restrict__ arena, fdgpu_frag_ex_t *__restrict__ fx_dev, uint8_t *__restrict__ txn_out,
+    uint16_t *__restrict__ txn_sz, fdgpu_sig_desc_t *__restrict__ sigs, fdgpu_txn_desc_t *__restrict__ tds,
+    uint32_t *__restrict__ n_sig, uint32_t *__restrict__ zero_word) {
+  const uint32_t lane = threadIdx.x & 63u, wpb = blockDim.x >> 6;
+  if (blockIdx.x == 0 && threadIdx.x == 0 && zero_word) *zero_word = 0u;
+  for (uint32_t g = blockIdx.x * wpb + (threadIdx.x >> 6); g * 64u < n; g += gridDim.x * wpb) {
+    const uint32_t f = g * 64u + lane;
+    const bool act = f < n;
+    const uint64_t s = act ? src[f] : 0ull;
+    fdgpu_frag_ex_t x = act ? fx[f] : fdgpu_frag_ex_t{0u, 0u, 0u, 0u};
+    const uint64_t line = (act && chk) ? chk[2u * f] : 0ull;
+    const uint64_t seq = line ? chk[2u * f + 1u] : 0ull;
+    const uint32_t nq = (x.sz + 15u) >> 4;
+    const uint32_t incl = wave_incl_scan(nq), excl = incl - nq;
+    const uint32_t total = (uint32_t)__shfl((int)incl, 63, 64);
+    /* unit k of the group: its owner lane's source and arena place (all
+       lanes take part in the shuffles; a lane past the end reads the last
+       unit's arena place instead of the bus, and stores nothing) */
+    auto unit = [&](uint32_t k, const uint4 *&sp, uint4 *&dp) {
+      const uint32_t kk = k < total ? k : total - 1u;
+      const uint32_t o = unit_owner(incl, kk);
+      const uint32_t u = kk - (uint32_t)__shfl((int)excl, (int)o, 64);
+      sp = (const uint4 *)(uint64_t)__shfl((long long)s, (int)o, 64) + u;
+      dp = (uint4 *)(arena + (uint32_t)__shfl((int)x.off, (int)o, 64)) + u;
+      if (k >= total) sp = dp;
+    };
+    for (uint32_t k0 = 0; k0 < total; k0 += 256u) {
+      const uint4 *s0, *s1, *s2, *s3;
+      uint4 *d0, *d1, *d2, *d3;
+      unit(k0 + lane, s0, d0);
+      unit(k0 + 64u + lane, s1, d1);
+      unit(k0 + 128u + lane, s2, d2);
+      unit(k0 + 192u + lane, s3, d3);
+      const uint4 v0 = *s0, v1 = *s1, v2 = *s2, v3 = *s3;       /* four loads over the bus in flight */
+      if (k0 + lane < total) *d0 = v0;
+      if (k0 + 64u + lane < total) *d1 = v1;
+      if (k0 + 128u + lane < total) *d2 = v2;
+      if (k0 + 192u + lane < total) *d3 = v3;
+    }
+    /* every payload load of the wave has returned (and every copy store is
+       done: vmcnt counts both on gfx9) before a line is re-read */
+    __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (line) {
+      const uint64_t cur = __hip_atomic_load((const uint64_t *)line, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      if (cur != seq) x.tr_cap |= FDGPU_FX_LAPPED;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");      /* this CU's L1 holds none of the old arena bytes */
+    uint32_t c = 0;
+    fdgpu_txn_t dt{};
+    if (act) {
+      fx_dev[f] = x;
+      fdt_txn_t *t = (fdt_txn_t *)(txn_out + (size_t)f * FDT_TXN_MAX_SZ);
+      uint64_t why = 0;
+      /* a lapped payload may be torn: not parsed */
+      uint64_t fp = (x.tr_cap & FDGPU_FX_LAPPED) ? 0u : fdt_parse_core(arena + x.off, x.sz, t, &why);
+      const uint32_t sc = fp ? t->signature_cnt : 0u;
+      c = (sc >= 1u && sc <= 16u) ? sc : 0u;
+      if (c > fdt_frag_sig_bound(x.sz)) { c = 0u; fp = 0u; }      /* cannot happen for a parsed txn */
+      if (fp) {
+        dt.msg_off = x.off + t->message_off;
+        dt.msg_sz = x.sz - t->message_off;
+        dt.sig_off = x.off + t->signature_off;
+        dt.pub_off = x.off + t->acct_addr_off;
+      }
+      txn_sz[f] = (uint16_t)fp;
+    }
+    const uint32_t ci = wave_incl_scan(c);
+    const uint32_t ct = (uint32_t)__shfl((int)ci, 63, 64);
+    uint32_t base = 0;
+    if (lane == 63u && ct) base = atomicAdd(n_sig, ct);
+    base = (uint32_t)__shfl((int)base, 63, 64);
+    if (!act) continue;
+    const uint32_t s0 = base + ci - c;
+    fdgpu_txn_desc_t td;
+    td.sig0 = s0;
+    td.sig_cnt = c;
+    tds[f] = td;
+    for (uint32_t j = 0; j < c; j++) {
+      fdgpu_sig_desc_t sd;
+      sd.msg_off = dt.msg_off;
+      sd.msg_sz = dt.msg_sz;
+      sd.sig_off = dt.sig_off + 64u * j;
+      sd.pub_off = dt.pub_off + 32u * j;
+      sigs[s0 + j] = sd;
+    }
+  }
+}
+
+/* byte b of frag's out frag [payload sz][pad to 2][fd_txn_t fp][u16 sz] */
+FDG_DEV uint32_t out_frag_byte(uint32_t b, const uint8_t *pl, uint32_t sz, uint32_t toff, const uint8_t *tr,
+                               uint32_t fp) {
+  if (b < sz) return pl[b];
+  if (b < toff) return 0u;
+  if (b < toff + fp) return tr[b - toff];
+  const uint32_t k = b - toff - fp;
+  return k < 2u ? (sz >> (8u * k)) & 0xffu : 0u;
+}
+
+/* Finish: per group, lane i writes frag i's code (the batch_single_msg
+   combine of its signatures; FDGPU_CODE_PARSE_FAIL; FDGPU_CODE_LAPPED;
    FDGPU_CODE_TRAILER_CAP when the out frag would not fit the caller's
    reservation), its dedup tag (fd_hash of the first signature,
-   fd_verify.h:66) and its out size; the wave writes the out frag as
-   fd_verify.c:93-136 lays it out in the out dcache -- [payload][pad to 2]
-   [fd_txn_t][u16 payload_sz] -- one 16-bit word per lane (the fd_txn_t
-   starts 2-aligned).  (A completion word stored by the kernel's last block
-   was tried: the system-scope fence each block then needs writes back the
-   L2 under the concurrent verify kernels and halved the tile's rate; the
-   stream's own write after the kernel stays.) */
-FDG_DEV void frag_finish_io_one(uint32_t f, uint32_t lane, const fdgpu_txn_desc_t *__restrict__ txns,
-                                const int8_t *__restrict__ sig_codes, const uint16_t *__restrict__ txn_sz,
-                                const fdgpu_frag_ex_t *__restrict__ fx, const uint8_t *__restrict__ txn_out,
-                                const uint8_t *__restrict__ arena, uint64_t seed, uint8_t *__restrict__ out,
-                                int8_t *__restrict__ codes, uint64_t *__restrict__ tags,
-                                uint16_t *__restrict__ out_szs) {
-  const uint32_t fp = txn_sz[f];
-  const fdgpu_frag_ex_t x = fx[f];                    /* off: arena, sz, tr_off: out offset, tr_cap: its room */
-  const bool lapped = (x.tr_cap & FDGPU_FX_LAPPED) != 0u;   /* fp is 0 then */
-  const uint32_t toff = (x.sz + 1u) & ~1u, osz = toff + fp + 2u;
-  const bool fits = fp && osz <= x.tr_cap;
-  const fdt_txn_t *t = (const fdt_txn_t *)(txn_out + (size_t)f * FDT_TXN_MAX_SZ);
-  const uint8_t *pl = arena + x.off;
-  if (lane == 0) {
-    int code = lapped ? FDGPU_CODE_LAPPED : FDGPU_CODE_PARSE_FAIL;
-    uint64_t tag = 0;
-    if (fp) {
-      tag = fdt_hash_core(seed, pl + t->signature_off, 64);
-      if (!fits) {
-        code = FDGPU_CODE_TRAILER_CAP;
-      } else {
-        code = -1;
-        const fdgpu_txn_desc_t d = txns[f];
-        if (d.sig_cnt >= 1 && d.sig_cnt <= 16) {           /* else ERR_SIG (fd_ed25519_user.c:238-241) */
-          int first_struct = 0, any_msg = 0;
-          for (uint32_t j = 0; j < d.sig_cnt; j++) {
-            const int c = sig_codes[d.sig0 + j];
-            if (c == -3) any_msg = 1;
-            else if (c != 0 && first_struct == 0) first_struct = c;
-          }
-          code = first_struct ? first_struct : (any_msg ? -3 : 0);
-        }
-      }
-    }
-    codes[f] = (int8_t)code;
-    tags[f] = tag;
-    out_szs[f] = (uint16_t)(fits ? osz : 0u);
-  }
-  if (!fits) return;
-  const uint16_t *tr = (const uint16_t *)t;
-  uint16_t *o = (uint16_t *)(out + x.tr_off);
-  for (uint32_t h = lane; h < osz / 2u; h += 64u) {
-    const uint32_t b = 2u * h;
-    uint16_t v;
-    if (b < toff) {
-      v = *(const uint16_t *)(pl + b);              /* arena offsets are 16-B aligned */
-      if (b + 1u >= x.sz) v &= 0x00ffu;               /* the pad byte */
-    } else if (b < toff + fp) {
-      v = tr[(b - toff) / 2u];
-    } else {
-      v = (uint16_t)x.sz;
-    }
-    o[h] = v;
-  }
-}
-
+   fd_verify.h:66) and its out size (coalesced over the lanes); then the wave
+   writes the group's out frags as fd_verify.c:93-136 lays them out in the
+   out dcache -- [payload][pad to 2][fd_txn_t][u16 payload_sz] -- one 16-B
+   unit per lane and step, the units flattened over the group: a unit inside
+   the payload is one 16-B load from the arena, the others are assembled
+   byte by byte; a unit that would pass the frag's reservation (or an out
+   frag not 16-B aligned) is written in 2-B stores up to the frag's end.  The
+   first thread clears the slot's ingest counter for its next gathered batch
+   (zero_next; the verify that read it is complete).  (A completion word
+   stored by the kernel's last block was tried: the system-scope fence each
+   block then needs writes back the L2 under the concurrent verify kernels
+   and halved the tile's rate; the stream's own write after the kernel
+   stays.) */
 __global__ void __launch_bounds__(256) fdgpu_frag_finish_io_kernel(
     const fdgpu_txn_desc_t *__restrict__ txns, uint32_t n, const int8_t *__restrict__ sig_codes,
     const uint16_t *__restrict__ txn_sz, const fdgpu_frag_ex_t *__restrict__ fx, const uint8_t *__restrict__ txn_out,
     const uint8_t *__restrict__ arena, uint64_t seed, uint8_t *__restrict__ out, int8_t *__restrict__ codes,
-    uint64_t *__restrict__ tags, uint16_t *__restrict__ out_szs) {
-  const uint32_t f = blockIdx.x * 4u + (threadIdx.x >> 6), lane = threadIdx.x & 63u;
-  if (f < n) frag_finish_io_one(f, lane, txns, sig_codes, txn_sz, fx, txn_out, arena, seed, out, codes, tags, out_szs);
+    uint64_t *__restrict__ tags, uint16_t *__restrict__ out_szs, uint32_t *__restrict__ zero_next) {
+  const uint32_t lane = threadIdx.x & 63u, wpb = blockDim.x >> 6;
+  if (blockIdx.x == 0 && threadIdx.x == 0 && zero_next) *zero_next = 0u;
+  for (uint32_t g = blockIdx.x * wpb + (threadIdx.x >> 6); g * 64u < n; g += gridDim.x * wpb) {
+    const uint32_t f = g * 64u + lane;
+    const bool act = f < n;
+    uint32_t fp = 0, osz = 0, toff = 0;
+    fdgpu_frag_ex_t x{0u, 0u, 0u, 0u};            /* off: arena, sz, tr_off: out offset, tr_cap: its room */
+    bool fits = false;
+    if (act) {
+      fp = txn_sz[f];
+      x = fx[f];
+      const bool lapped = (x.tr_cap & FDGPU_FX_LAPPED) != 0u;   /* fp is 0 then */
+      toff = (x.sz + 1u) & ~1u;
+      osz = toff + fp + 2u;
+      fits = fp && osz <= x.tr_cap;
+      const fdt_txn_t *t = (const fdt_txn_t *)(txn_out + (size_t)f * FDT_TXN_MAX_SZ);
+      int code = lapped ? FDGPU_CODE_LAPPED : FDGPU_CODE_PARSE_FAIL;
+      uint64_t tag = 0;
+      if (fp) {
+        tag = fdt_hash_core(seed, arena + x.off + t->signature_off, 64);
+        if (!fits) {
+          code = FDGPU_CODE_TRAILER_CAP;
+        } else {
+          code = -1;
+          const fdgpu_txn_desc_t d = txns[f];
+          if (d.sig_cnt >= 1 && d.sig_cnt <= 16) {           /* else ERR_SIG (fd_ed25519_user.c:238-241) */
+            int first_struct = 0, any_msg = 0;
+            for (uint32_t j = 0; j < d.sig_cnt; j++) {
+              const int c = sig_codes[d.sig0 + j];
+              if (c == -3) any_msg = 1;
+              else if (c != 0 && first_struct == 0) first_struct = c;
+            }
+            code = first_struct ? first_struct : (any_msg ? -3 : 0);
+          }
+        }
+      }
+      codes[f] = (int8_t)code;
+      tags[f] = tag;
+      out_szs[f] = (uint16_t)(fits ? osz : 0u);
+    }
+    const uint32_t nu = fits ? (osz + 15u) >> 4 : 0u;
+    const uint32_t incl = wave_incl_scan(nu), excl = incl - nu;
+    const uint32_t total = (uint32_t)__shfl((int)incl, 63, 64);
+    for (uint32_t k0 = 0; k0 < total; k0 += 64u) {       /* wave-uniform: every lane takes part in the shuffles */
+      const uint32_t k = k0 + lane < total ? k0 + lane : total - 1u;
+      const uint32_t o = unit_owner(incl, k);
+      const uint32_t u = k - (uint32_t)__shfl((int)excl, (int)o, 64);
+      const uint32_t off = (uint32_t)__shfl((int)x.off, (int)o, 64), sz = (uint32_t)__shfl((int)x.sz, (int)o, 64);
+      const uint32_t oof = (uint32_t)__shfl((int)x.tr_off, (int)o, 64);
+      const uint32_t cap = (uint32_t)__shfl((int)x.tr_cap, (int)o, 64) & 0xFFFFu;
+      const uint32_t ofp = (uint32_t)__shfl((int)fp, (int)o, 64), oosz = (uint32_t)__shfl((int)osz, (int)o, 64);
+      const uint32_t otoff = (sz + 1u) & ~1u, b0 = 16u * u;
+      const uint8_t *pl = arena + off;
+      const uint8_t *tr = txn_out + (size_t)(g * 64u + o) * FDT_TXN_MAX_SZ;
+      uint8_t *dst = out + oof + b0;
+      if (k0 + lane >= total) continue;
+      if (b0 + 16u <= cap && !(((uintptr_t)dst) & 15u)) {
+        uint4 w;
+        if (b0 + 16u <= sz) {
+          w = *(const uint4 *)(pl + b0);                      /* arena offsets are 16-B aligned */
+        } else {
+          uint32_t q[4];
+#pragma unroll
+          for (int i = 0; i < 4; i++) {
+            uint32_t v = 0;
+#pragma unroll
+            for (int j = 0; j < 4; j++) v |= out_frag_byte(b0 + 4u * i + j, pl, sz, otoff, tr, ofp) << (8 * j);
+            q[i] = v;
+          }
+          w = make_uint4(q[0], q[1], q[2], q[3]);
+        }
+        *(uint4 *)dst = w;
+      } else {
+        for (uint32_t b = b0; b < b0 + 16u && b < oosz; b += 2u)
+          *(uint16_t *)(out + oof + b) = (uint16_t)(out_frag_byte(b, pl, sz, otoff, tr, ofp) |
+                                                    (out_frag_byte(b + 1u, pl, sz, otoff, tr, ofp) << 8));
+      }
+    }
+  }
 }
 
 /* After the combine: a payload that did not parse gets FDGPU_CODE_PARSE_FAIL */
@@ -1608,7 +1676,8 @@ hipError_t fdgpu_launch_verify_sigs(const uint8_t *d_arena, const fdgpu_sig_desc
      engine's occupancy x CUs), each exiting at once when the queue holds
      nothing for it */
   if (!resident_blocks) resident_blocks = 1;
-  const uint32_t slow_blocks = grid < resident_blocks ? grid : resident_blocks;
+  uint32_t slow_blocks = grid < resident_blocks ? grid : resident_blocks;
+  if (slow_blocks > FDGPU_FULL_BLOCKS) slow_blocks = FDGPU_FULL_BLOCKS;     /* strides over its queue */
   const uint32_t *key_of = nullptr;
   if (flags & FDGPU_FLAG_KCACHE) {
     const uint64_t hts = kc_ht_slots(lanes);
@@ -1654,8 +1723,9 @@ uint32_t *fdgpu_verify_cnt_word(uint32_t *d_ws, uint32_t n_sig) {
 hipError_t fdgpu_launch_combine(const fdgpu_txn_desc_t *d_txns, uint32_t n_txn, const int8_t *d_sig_codes,
                                 int8_t *d_txn_codes, uint64_t *d_accept, hipStream_t stream) {
   if (!n_txn) return hipSuccess;
-  hipLaunchKernelGGL(fdgpu_combine_kernel, dim3((n_txn + 255) / 256), dim3(256), 0, stream, d_txns, n_txn,
-                     d_sig_codes, d_txn_codes, d_accept);
+  const uint32_t blocks = (n_txn + 255) / 256;
+  hipLaunchKernelGGL(fdgpu_combine_kernel, dim3(blocks < FDGPU_AUX_BLOCKS ? blocks : FDGPU_AUX_BLOCKS), dim3(256), 0,
+                     stream, d_txns, n_txn, d_sig_codes, d_txn_codes, d_accept);
   return hipGetLastError();
 }
 
@@ -1741,31 +1811,29 @@ hipError_t fdgpu_launch_frag_finish(const fdgpu_txn_desc_t *d_tds, uint32_t n, c
 
 uint64_t fdgpu_frag_fp_bound(uint32_t sz) { return fdt_frag_fp_bound(sz); }
 
-hipError_t fdgpu_launch_frag_gather(const uint64_t *d_src, const fdgpu_frag_ex_t *d_fx, const uint64_t *d_chk, uint32_t n,
-                                    uint8_t *d_arena, fdgpu_frag_ex_t *d_fx_dev, uint32_t *d_zero_word,
-                                    uint32_t *d_zero_word2, hipStream_t stream) {
-  if (!n) return hipSuccess;
-  hipLaunchKernelGGL(fdgpu_frag_gather_kernel, dim3((n + 3) / 4), dim3(256), 0, stream, d_src, d_fx, d_chk, n, d_arena,
-                     d_fx_dev, d_zero_word, d_zero_word2);
-  return hipGetLastError();
+static uint32_t aux_blocks(uint32_t n) {          /* waves of 64 frags, 4 per block, at most FDGPU_AUX_BLOCKS */
+  const uint32_t b = (n + 255u) / 256u;
+  return b < FDGPU_AUX_BLOCKS ? b : FDGPU_AUX_BLOCKS;
 }
 
-hipError_t fdgpu_launch_frag_parse_expand(const uint8_t *d_arena, const fdgpu_frag_ex_t *d_fx, uint32_t n,
-                                          uint8_t *d_txn_out, uint16_t *d_txn_sz, fdgpu_sig_desc_t *d_sigs,
-                                          fdgpu_txn_desc_t *d_tds, uint32_t *d_n_sig, hipStream_t stream) {
+hipError_t fdgpu_launch_frag_ingest_io(const uint64_t *d_src, const fdgpu_frag_ex_t *d_fx, const uint64_t *d_chk,
+                                       uint32_t n, uint8_t *d_arena, fdgpu_frag_ex_t *d_fx_dev, uint8_t *d_txn_out,
+                                       uint16_t *d_txn_sz, fdgpu_sig_desc_t *d_sigs, fdgpu_txn_desc_t *d_tds,
+                                       uint32_t *d_n_sig, uint32_t *d_zero_word, hipStream_t stream) {
   if (!n) return hipSuccess;
-  hipLaunchKernelGGL(fdgpu_frag_parse_expand_kernel, dim3((n + 63) / 64), dim3(64), 0, stream, d_arena, d_fx, n,
-                     d_txn_out, d_txn_sz, d_sigs, d_tds, d_n_sig);
+  hipLaunchKernelGGL(fdgpu_frag_ingest_io_kernel, dim3(aux_blocks(n)), dim3(256), 0, stream, d_src, d_fx, d_chk, n,
+                     d_arena, d_fx_dev, d_txn_out, d_txn_sz, d_sigs, d_tds, d_n_sig, d_zero_word);
   return hipGetLastError();
 }
 
 hipError_t fdgpu_launch_frag_finish_io(const fdgpu_txn_desc_t *d_tds, uint32_t n, const int8_t *d_sig_codes,
                                        const uint16_t *d_txn_sz, const fdgpu_frag_ex_t *d_fx, const uint8_t *d_txn_out,
                                        const uint8_t *d_arena, uint64_t hash_seed, uint8_t *d_out, int8_t *d_codes,
-                                       uint64_t *d_tags, uint16_t *d_out_szs, hipStream_t stream) {
+                                       uint64_t *d_tags, uint16_t *d_out_szs, uint32_t *d_zero_next,
+                                       hipStream_t stream) {
   if (!n) return hipSuccess;
-  hipLaunchKernelGGL(fdgpu_frag_finish_io_kernel, dim3((n + 3) / 4), dim3(256), 0, stream, d_tds, n, d_sig_codes,
-                     d_txn_sz, d_fx, d_txn_out, d_arena, hash_seed, d_out, d_codes, d_tags, d_out_szs);
+  hipLaunchKernelGGL(fdgpu_frag_finish_io_kernel, dim3(aux_blocks(n)), dim3(256), 0, stream, d_tds, n, d_sig_codes,
+                     d_txn_sz, d_fx, d_txn_out, d_arena, hash_seed, d_out, d_codes, d_tags, d_out_szs, d_zero_next);
   return hipGetLastError();
 }
 
