@@ -609,6 +609,13 @@ def _tile_child(rank, cpus, arena, txns, modes, runs, tag=""):
         # tenant's thread on it, the runtime blocking) -- a paced link laps a tile stalled for
         # depth / per-link rate (16384 / 5 M/s = 3.3 ms)
         out[f"tile_{name}_stall_max_ms"] = round(max(x["counters"].get("stall_max_ns", 0) for x in reps) / 1e6, 2)
+        if rate > 0:
+            # the fewest publishes any batch's oldest frag had left before its line's reuse, seen when the
+            # batch completed (after the device read it), in ms at the link's offered rate; worst of the runs
+            lm = min(x["counters"]["lap_margin_min"] for x in reps)
+            out[f"tile_{name}_lap_margin_min_seqs"] = lm if lm < 2 ** 63 else None
+            per_link = min(x["offered_txns_per_s"] / x["producers"] for x in reps if x.get("offered_txns_per_s"))
+            out[f"tile_{name}_lap_margin_min_ms"] = round(lm / per_link * 1e3, 3) if lm < 2 ** 63 else None
     return out
 
 

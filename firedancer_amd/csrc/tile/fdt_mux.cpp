@@ -409,6 +409,7 @@ struct VBatch {
   std::vector<uint64_t> tags;         /*   and the verifier's results: dedup tags, */
   std::vector<uint16_t> out_szs;      /*   out frag sizes */
   uint64_t link_first[FDT_MUX_IN_MAX];   /* gather: the oldest seq taken from each in link, */
+  uint64_t link_last[FDT_MUX_IN_MAX];    /*   the newest, */
   uint32_t guard_cur[FDT_MUX_IN_MAX];    /*   the lap guard's cursor over the items of each, */
   uint32_t link_mask = 0;                /*   and which links the batch holds frags of */
   uint64_t tr_used = 0;
@@ -556,7 +557,32 @@ struct fdgpu_vmux {
     b->done = true;
     busy--;
     for (uint32_t k : b->lost) b->codes[k] = (int8_t)FDGPU_CODE_LAPPED;
+    if (gather) note_lap_margin(*b);
     return 1;
+  }
+
+  /* gather: the batch is done (the device read its payloads before): how
+     many more publishes each of its links' oldest frag had left before the
+     producer reuses its line.  The link's newest published seq P is found by
+     bisection between the batch's newest frag of the link (published) and
+     the oldest's line reuse: published_by(s) holds exactly for s <= P. */
+  void note_lap_margin(const VBatch &b) {
+    for (uint32_t i = 0; i < cfg.in_cnt; i++) {
+      if (!(b.link_mask >> i & 1u)) continue;
+      const uint64_t reuse = b.link_first[i] + cfg.in_depth[i];     /* publishing this seq overwrites the oldest */
+      uint64_t m;
+      if (published_by(i, reuse)) {
+        m = 0;
+      } else {
+        uint64_t lo = b.link_last[i], hi = reuse;                    /* published_by(lo), !published_by(hi) */
+        while (hi - lo > 1) {
+          const uint64_t mid = lo + (hi - lo) / 2;
+          if (published_by(i, mid)) lo = mid; else hi = mid;
+        }
+        m = reuse - 1 - lo;
+      }
+      st.lap_margin_min = std::min(st.lap_margin_min, m);
+    }
   }
 
   /* tag, tcache, publish -- strictly in ingest order (fd_verify.h:45-89,
@@ -869,6 +895,7 @@ __attribute__((always_inline)) inline void vm_after_frag(void *ctx, uint64_t in_
       b.link_first[li] = seq;
       b.guard_cur[li] = (uint32_t)b.cnt;
     }
+    b.link_last[li] = seq;
     /* the frag's record is what the verifier reads: the device re-reads the
        frag's in-mcache line after the payload (link li + 1, seq) */
     fdgpu_frag_io_t &f = b.fio[b.cnt];          /* in place: no temporary (a wide reload of narrow stores stalls) */
@@ -1086,6 +1113,7 @@ fdgpu_vmux_t *fdgpu_vmux_new(const fdgpu_vmux_cfg_t *cfg, fdgpu_verifier_t ver) 
   }
   fdt_tagring_init(&t->ring, c.tcache_depth);
   t->ver = ver;
+  t->st.lap_margin_min = UINT64_MAX;
   t->out_chunk = c.out_chunk0;
   t->rr_mask = (c.round_robin_cnt & (c.round_robin_cnt - 1)) == 0 ? c.round_robin_cnt - 1 : 0;
   uint64_t n = 1;

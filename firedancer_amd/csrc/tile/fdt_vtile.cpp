@@ -456,6 +456,7 @@ fdgpu_vtile_t *fdgpu_vtile_new(const fdgpu_vtile_cfg_t *cfg, fdgpu_verifier_t ve
   auto *t = new (std::nothrow) fdgpu_vtile;
   if (!t) return nullptr;
   t->cfg = *cfg;
+  t->st.lap_margin_min = UINT64_MAX;                    /* the gather tile's measure; none here */
   if (!t->cfg.round_robin_cnt) t->cfg.round_robin_cnt = 1;
   if (!t->cfg.inflight_max) t->cfg.inflight_max = 2;
   if (!t->cfg.tcache_depth) t->cfg.tcache_depth = FDT_VERIFY_TCACHE_DEPTH;

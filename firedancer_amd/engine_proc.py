@@ -138,13 +138,9 @@ def serve(in_paths, out_paths, verifiers, frag_cnts, timeout_s=120.0, idle_s=0.0
     vms = [tile.VerifyMuxTile(ins, outs[k], verifiers[k], round_robin_idx=k, round_robin_cnt=T, log_max=log_max,
                               **tile_kw) for k in range(T)]
     try:
-        keep = os.sched_getaffinity(0)
-        for k, vm in enumerate(vms):                       # the tile thread inherits the starter's mask
-            if cpus:
-                os.sched_setaffinity(0, {cpus[k % len(cpus)]})
-            vm.start()
-        os.sched_setaffinity(0, keep)
         t_start = time.monotonic()
+        for k, vm in enumerate(vms):
+            vm.start(cpu=cpus[k % len(cpus)] if cpus else None)
         if on_start:
             on_start()
         if ready_file:
@@ -174,6 +170,7 @@ def serve(in_paths, out_paths, verifiers, frag_cnts, timeout_s=120.0, idle_s=0.0
         lat = np.concatenate([vm.latencies_ns() for vm in vms]) / 1e6 if vms else np.zeros(0)
         agg = {k: int(sum(s[k] for s in per)) for k in per[0]}
         agg["stall_max_ns"] = max(s["stall_max_ns"] for s in per)
+        agg["lap_margin_min"] = min(s["lap_margin_min"] for s in per)
         magg = {k: int(sum(m[k] for m in mux)) for k in mux[0]}
         agg["overrun_polling"], agg["overrun_reading"] = magg["overrun_polling"], magg["overrun_reading"]
         agg["overrun"] = agg["lapped"] + agg["overrun_polling"] + agg["overrun_reading"]

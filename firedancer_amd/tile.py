@@ -117,7 +117,7 @@ class VTileStats(c.Structure):
                                           "backpressure", "lat_cnt", "verify_errors", "ingest_ns", "submit_ns",
                                           "poll_ns", "no_slot_steps", "polls", "poll_done_ns",
                                           "publish_ns", "batch_fill_ns", "batch_gpu_ns", "lapped", "rescued",
-                                          "submit_max_ns", "stall_max_ns")]
+                                          "submit_max_ns", "stall_max_ns", "lap_margin_min")]
 
     def as_dict(self):
         return {n: getattr(self, n) for n, _ in self._fields_}
@@ -1123,8 +1123,12 @@ class VerifyMuxTile:
         self._threading = threading
         self._th = None
 
-    def start(self):
+    def start(self, cpu=None):
+        """Runs the mux loop on a thread of its own (pinned to `cpu` by the
+        thread itself, so the caller's own affinity is never touched)."""
         def body():
+            if cpu is not None:
+                os.sched_setaffinity(0, {cpu})
             self._rc = lib().fdt_mux_run(c.byref(self.mcfg), c.byref(self.cb), self._t, c.byref(self._halt),
                                          c.byref(self._mstats))
         self._halt.value = 0

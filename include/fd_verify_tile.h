@@ -293,6 +293,10 @@ typedef struct {
   uint64_t submit_max_ns;   /* the longest single batch submit (fdgpu_vmux) */
   uint64_t stall_max_ns;    /* the longest the tile went between two of its every-64th-call polls: a
                                stalled core (descheduled, blocked in a runtime call) (fdgpu_vmux) */
+  uint64_t lap_margin_min;  /* gpu_parse 2: the fewest further publishes any batch's oldest frag of a link
+                               had left before the producer reuses its line, taken when the batch is seen
+                               complete (so after the device's read): (oldest seq + depth - 1) - the
+                               link's newest published seq, 0 if lapped; UINT64_MAX: none measured */
 } fdgpu_vtile_stats_t;
 
 typedef struct fdgpu_vtile fdgpu_vtile_t;

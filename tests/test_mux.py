@@ -330,7 +330,35 @@ def test_vmux_gather_drops_lapped_frags(oracle):
     exp_out, _ = tile_model.verify_tile_model(ps, 0x77, oracle_fn(oracle))
     tail_out, _ = tile_model.verify_tile_model(ps[8:], 0x77, oracle_fn(oracle))
     assert codes.tolist()[8:] == tail_out
-    assert vm.stats()["overrun"] == 8
+    assert vm.stats()["overrun"] == 8 and vm.stats()["lap_margin_min"] == 0     # the first batch was lapped
+    vm.close()
+
+
+def test_vmux_gather_lap_margin(oracle):
+    """gpu_parse 2: when a batch is seen complete the tile records how many
+    more publishes its oldest frag of each link had left before the producer
+    reuses that frag's line (the lap margin a run kept).
+    A batch of seqs 0..7 on a 64-deep link completes after the producer has
+    published seq 17: seq 0's line is reused by seq 64, so 46 publishes were
+    left."""
+    ps = _mixed_stream(64, seed=12)[:18]
+    inl = tile.Link(64, 1232)
+    outl = tile.Link(64, tile.TPU_DCACHE_MTU, data_sz=64 * (tile.TPU_DCACHE_MTU + 64))
+    ver = tile.PyVerifier(oracle_fn(oracle), slots=1, lag=1 << 60)       # pending until released below
+    vm = tile.VerifyMuxTile(inl, outl, ver, hashmap_seed=0x76, batch_txn_max=8, inflight_max=1, log_max=1 << 10,
+                            batch_wait_us=100, gpu_parse=2)
+    assert vm.stats()["lap_margin_min"] == 2 ** 64 - 1                     # none measured yet
+    for p in ps[:8]:
+        inl.publish(p)
+    vm.start()
+    _wait(lambda: len(ver.batches) == 1)
+    for p in ps[8:]:
+        inl.publish(p)
+    _wait(lambda: vm.stats()["in_frags"] == 16)            # the next batch (8..15) is closed and waits
+    ver.lag = 0
+    _wait(lambda: vm.final_cnt() == len(ps))
+    vm.stop()
+    assert vm.stats()["lap_margin_min"] == 46
     vm.close()
 
 

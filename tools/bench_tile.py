@@ -353,12 +353,8 @@ def run_once_mux(args, ps, arena, offs, sizes, n_sig, modes, tiles_n, batch, inf
     n_total = sum(len(f[0]) for f in feeds)
 
     def start_tiles():
-        keep = os.sched_getaffinity(0)
         for k, vm in enumerate(vms):
-            if args.pin:
-                os.sched_setaffinity(0, {cpus[(P + k) % len(cpus)]})
-            vm.start()
-        os.sched_setaffinity(0, keep)
+            vm.start(cpu=cpus[(P + k) % len(cpus)] if args.pin else None)
 
     # paced: the tiles are polling before the first frag is published (a producer that starts first
     # laps a tile still starting up: ~4 x the link depth lost in one run of r04k / r04n)
@@ -397,6 +393,8 @@ def run_once_mux(args, ps, arena, offs, sizes, n_sig, modes, tiles_n, batch, inf
     mstats = [vm.mux_stats() for vm in vms]
     lat = np.concatenate([vm.latencies_ns() for vm in vms]) / 1e6
     agg = {k: int(sum(s[k] for s in stats)) for k in stats[0]}
+    agg["lap_margin_min"] = int(min(s["lap_margin_min"] for s in stats))
+    agg["stall_max_ns"] = int(max(s["stall_max_ns"] for s in stats))
     # every frag lost to the producers: lapped before the device read it (the
     # tile's own count, FDGPU_CODE_LAPPED), skipped while the mux lagged, or
     # overwritten while the mux read its metadata
