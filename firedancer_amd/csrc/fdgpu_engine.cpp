@@ -58,6 +58,9 @@ namespace {
 std::atomic<uint64_t> g_sp_loop{0}, g_sp_enq{0}, g_sp_calls{0}, g_sp_frags{0};
 inline uint64_t sp_now() { timespec ts; clock_gettime(CLOCK_MONOTONIC, &ts); return ts.tv_sec * 1000000000ull + ts.tv_nsec; }
 const bool g_sp_on = getenv("FDGPU_SUBMIT_PROF") && getenv("FDGPU_SUBMIT_PROF")[0] == '1';
+/* gathered batches read their payloads by DMA (FDGPU_IO_DMA=0: by the ingest
+   kernel's loads over the bus, the round-4 path) */
+const bool g_io_dma = !(getenv("FDGPU_IO_DMA") && getenv("FDGPU_IO_DMA")[0] == '0');
 /* the last FDGPU_ST_RING fdgpu_submit calls of the process: {staging copy,
    descriptor expansion, enqueue} ns (fdgpu_debug_submit_times).  Each call
    writes the entry its fetch_add drew; the words are relaxed atomics, so
@@ -111,6 +114,9 @@ struct Slot {
   fdgpu_frag_ex_t *d_fxio = nullptr;          /* the records, kept on the device by the ingest */
   uint32_t *d_io_cnt = nullptr;               /* the ingest's signature count: zero at the start of a gathered
                                                  batch (cleared by the finish of the slot's previous one) */
+  uint8_t *d_mirror = nullptr;                /* DMA gather: the batch's source ranges, copied in by the DMA
+                                                 engines, parsed and verified in place (the batch arena) */
+  uint64_t mirror_cap = 0;
   uint8_t *d_trh = nullptr;                   /* h_tr's device-side address (results written in place) */
   /* FDGPU_FLAG_MERGE: the batch's gather + parse are queued and its verify
      waits to be merged with the other batches ready (merge_kick), which then
@@ -121,6 +127,7 @@ struct Slot {
   uint32_t m_n = 0;
   uint64_t m_seed = 0, m_cb = 0, m_bound = 0;
   uint8_t *m_out = nullptr;
+  uint8_t *m_arena = nullptr;   /* the batch arena (d_arena, or d_mirror for a DMA-gathered batch) */
 };
 
 /* poll_slot answers a pending batch without the ring lock, reading a slot's
@@ -199,7 +206,7 @@ void slot_free(Slot &s) {
   if (s.h_io) (void)hipHostFree(s.h_io);
   for (void *p : {(void *)s.d_fx, (void *)s.d_txn_out, (void *)s.d_txn_sz, (void *)s.d_txd, (void *)s.d_cnt,
                   (void *)s.d_sig0, (void *)s.d_blocktot, (void *)s.d_n_sig, (void *)s.d_tr, (void *)s.d_fxio,
-                  (void *)s.d_io_cnt})
+                  (void *)s.d_io_cnt, (void *)s.d_mirror})
     if (p) (void)hipFree(p);
   s = Slot{};
 }
@@ -283,13 +290,23 @@ bool slot_frag_bufs(Slot &s, const fdgpu_cfg_t &c, uint64_t tr) {
 /* The slot's gathered-batch buffers (fdgpu_submit_frags_io), on first use:
    pinned [frag records][payload addresses][re-check pairs] the gather reads
    in place, and the records' device copy. */
+/* DMA gather: the batch's ranges may also carry other tiles' frags lying
+   between this batch's (a round robin of two takes every other frag of a
+   link), so the mirror holds twice the engine's arena */
+inline uint64_t mirror_bytes(const fdgpu_cfg_t &c) { return 2 * c.max_arena + FDGPU_ARENA_SLACK + 4096; }
+
 bool slot_io_bufs(Slot &s, const fdgpu_cfg_t &c) {
   if (s.h_io) return true;
-  const uint64_t m = c.max_txn + 1, bytes = m * (sizeof(fdgpu_frag_ex_t) + 3 * sizeof(uint64_t)) + 192;
+  const uint64_t m = c.max_txn + 1,
+                 bytes = m * (sizeof(fdgpu_frag_ex_t) + 3 * sizeof(uint64_t)) + 192 + FDGPU_IO_RANGES_MAX * 8;
   HIPCHK(hipHostMalloc((void **)&s.h_io, bytes, hipHostMallocDefault), false);
   HIPCHK(hipHostGetDevicePointer((void **)&s.d_ioh, s.h_io, 0), false);
   HIPCHK(hipMalloc((void **)&s.d_fxio, m * sizeof(fdgpu_frag_ex_t)), false);
   HIPCHK(hipMalloc((void **)&s.d_io_cnt, 64), false);
+  if (g_io_dma) {
+    HIPCHK(hipMalloc((void **)&s.d_mirror, mirror_bytes(c)), false);
+    s.mirror_cap = mirror_bytes(c) - FDGPU_ARENA_SLACK - 4096;
+  }
   HIPCHK(hipMemsetAsync(s.d_io_cnt, 0, 64, s.stream), false);    /* ordered before the slot's first batch */
   return true;
 }
@@ -461,23 +478,52 @@ static constexpr uint64_t FDGPU_PAIR_AUTO_SIGS = 49152;
    launches (profiles/r04/spread.md). */
 static constexpr uint64_t FDGPU_SPREAD_AUTO_LANES = 65536;
 
+/* The auto flags can weigh the running batches of every engine open on the
+   device, not only the caller's: each verify tile has an engine of its own,
+   and two tiles at capacity each saw about half the chip's load -- each
+   kept spreading its verifies one block per CU (and taking the two-lane
+   kernel) while the chip was full.  Measured, that view is the worse one:
+   two tiles at capacity 58.8 vs 60.1 M txn/s and, paced at 24 M, p50 / p99
+   batch latency 1.31 / 1.78 vs 0.97 / 1.07 ms (profiles/r05/auto_scope.md),
+   so the per-engine view stays the default and FDGPU_AUTO_SCOPE=device
+   selects this one.  Other engines' slots are read without their locks:
+   the fields are atomics, and a stale view only shifts the estimate by a
+   batch. */
+namespace {
+std::mutex g_dev_mu;
+std::map<int, std::vector<fdgpu_engine_t *>> g_dev_eng;
+const bool g_auto_engine_scope = !(getenv("FDGPU_AUTO_SCOPE") && !strcmp(getenv("FDGPU_AUTO_SCOPE"), "device"));
+
+/* signatures and lanes of o's running batches (s excluded) into load, lanes */
+void running_load(const fdgpu_engine_t *o, const Slot *s, uint64_t &load, uint64_t &lanes) {
+  for (const auto &c : o->slots) {
+    if (&c == s || __atomic_load_n(&c.ticket, __ATOMIC_RELAXED) < 0) continue;
+    if (o->flag_poll && __atomic_load_n(c.h_flag, __ATOMIC_ACQUIRE) == __atomic_load_n(&c.flag_seq, __ATOMIC_RELAXED))
+      continue;                                                      /* complete, not yet polled */
+    load += __atomic_load_n(&c.k_sigs, __ATOMIC_RELAXED);
+    lanes += __atomic_load_n(&c.k_lanes, __ATOMIC_RELAXED);
+  }
+}
+}  // namespace
+
 /* the kernel flags of slot s's ring batch of n_sig signatures (ring_mu held) */
 static uint32_t ring_kflags(fdgpu_engine_t *e, Slot *s, uint64_t n_sig) {
   uint32_t f = kflags(e);
   const uint64_t auto_flags = e->cfg.flags & (FDGPU_FLAG_PAIR_AUTO | FDGPU_FLAG_SPREAD_AUTO);
-  s->k_sigs = n_sig;
+  st_rlx(s->k_sigs, n_sig);
   if (auto_flags && !(f & FDGPU_FLAG_KCACHE)) {
     uint64_t load = n_sig, lanes = 0;
-    for (const auto &c : e->slots)
-      if (&c != s && c.ticket >= 0 && !(e->flag_poll && __atomic_load_n(c.h_flag, __ATOMIC_ACQUIRE) == c.flag_seq)) {
-        load += c.k_sigs;
-        lanes += c.k_lanes;
-      }
+    if (g_auto_engine_scope) {
+      running_load(e, s, load, lanes);
+    } else {
+      std::lock_guard<std::mutex> dk(g_dev_mu);
+      for (const fdgpu_engine_t *o : g_dev_eng[e->device]) running_load(o, s, load, lanes);
+    }
     if ((auto_flags & FDGPU_FLAG_PAIR_AUTO) && load <= FDGPU_PAIR_AUTO_SIGS) f |= FDGPU_FLAG_KPAIR;
     lanes += (f & FDGPU_FLAG_KPAIR) ? 2 * n_sig : n_sig;
     if ((auto_flags & FDGPU_FLAG_SPREAD_AUTO) && lanes <= FDGPU_SPREAD_AUTO_LANES) f |= FDGPU_FLAG_KSPREAD;
   }
-  s->k_lanes = (f & FDGPU_FLAG_KPAIR) ? 2 * n_sig : n_sig;
+  st_rlx(s->k_lanes, (f & FDGPU_FLAG_KPAIR) ? 2 * n_sig : n_sig);
   return f;
 }
 
@@ -564,11 +610,20 @@ fdgpu_engine_t *fdgpu_engine_open(int device, fdgpu_cfg_t const *cfg_in) {
     }
     e->pending.reserve(cfg.ring_depth);
   }
+  {
+    std::lock_guard<std::mutex> dk(g_dev_mu);
+    g_dev_eng[device].push_back(e);
+  }
   return e;
 }
 
 void fdgpu_engine_close(fdgpu_engine_t *e) {
   if (!e) return;
+  {
+    std::lock_guard<std::mutex> dk(g_dev_mu);                /* no other engine reads its slots from here on */
+    auto &v = g_dev_eng[e->device];
+    v.erase(std::remove(v.begin(), v.end(), e), v.end());
+  }
   if (g_sp_on && g_sp_calls)
     fprintf(stderr, "[fdgpu submit_frags_io] calls %llu frags %llu: loop %.1f us/call, enqueue %.1f us/call\n",
             (unsigned long long)g_sp_calls.load(), (unsigned long long)g_sp_frags.load(),
@@ -1038,7 +1093,7 @@ namespace {
 int io_tail(fdgpu_engine_t *e, Slot *s) {
   const uint64_t n = s->m_n, cb = s->m_cb;
   HIPCHK(fdgpu_launch_frag_finish_io(s->d_txns, (uint32_t)n, s->d_sig_codes, s->d_txn_sz, s->d_fxio, s->d_txn_out,
-                                     s->d_arena, s->m_seed, s->m_out, (int8_t *)s->d_trh, (uint64_t *)(s->d_trh + cb),
+                                     s->m_arena, s->m_seed, s->m_out, (int8_t *)s->d_trh, (uint64_t *)(s->d_trh + cb),
                                      (uint16_t *)(s->d_trh + cb + n * 8), s->d_io_cnt, s->stream),
          FDGPU_ERR_DEVICE);
   slot_flag_next(s);
@@ -1089,7 +1144,7 @@ int merge_kick_queue(fdgpu_engine_t *e, bool force) {
   for (Slot *s : e->pending) HIPCHK(hipStreamWaitEvent(m.stream, s->parsed, 0), FDGPU_ERR_DEVICE);
   if (nb == 1) {                               /* alone: the ring path's kernels (FDGPU_FLAG_PAIR_AUTO applies) */
     Slot *s = e->pending[0];
-    HIPCHK(fdgpu_launch_verify_sigs(s->d_arena, s->d_sigs, (uint32_t)s->m_bound, nullptr, e->d_btab, s->d_ws,
+    HIPCHK(fdgpu_launch_verify_sigs(s->m_arena, s->d_sigs, (uint32_t)s->m_bound, nullptr, e->d_btab, s->d_ws,
                                     s->d_sig_codes, ring_kflags(e, s, s->m_bound), m.stream, s->d_io_cnt,
                                     e->resident_blocks, e->kc_seed, 1),
            FDGPU_ERR_DEVICE);
@@ -1102,9 +1157,9 @@ int merge_kick_queue(fdgpu_engine_t *e, bool force) {
       uint32_t slow = grid < e->resident_blocks ? grid : e->resident_blocks;
       if (slow > FDGPU_FULL_BLOCKS) slow = FDGPU_FULL_BLOCKS;
       uint32_t *cnt = fdgpu_verify_cnt_word(s->d_ws, (uint32_t)s->m_bound);
-      s->k_sigs = s->m_bound;
-      s->k_lanes = s->m_bound;                 /* one lane each: the merged launch never takes the pair kernel */
-      tab[j] = fdgpu_mbatch_t{s->d_arena, s->d_sigs, s->d_io_cnt, s->d_ws, s->d_sig_codes,
+      st_rlx(s->k_sigs, s->m_bound);
+      st_rlx(s->k_lanes, s->m_bound);          /* one lane each: the merged launch never takes the pair kernel */
+      tab[j] = fdgpu_mbatch_t{s->m_arena, s->d_sigs, s->d_io_cnt, s->d_ws, s->d_sig_codes,
                               cnt - (size_t)grid * FDGPU_BLOCK, cnt, (uint32_t)s->m_bound, slow};
       grid_max = grid > grid_max ? grid : grid_max;
       slow_max = slow > slow_max ? slow : slow_max;
@@ -1177,35 +1232,87 @@ int64_t fdgpu_submit_frags_io(fdgpu_engine_t *e, fdgpu_frag_io_t const *fio, uin
   /* bounds: every payload inside a registered region (16-B aligned: the
      gather reads 16-B units up to round16(sz), inside the payload's own
      64-B chunks), every out frag inside out, the packed arena within
-     max_arena, the signature bound within max_sig, every named link given */
+     max_arena, the signature bound within max_sig, every named link given.
+
+     DMA gather (the default, g_io_dma): the frags' payloads are grouped into
+     ranges of source bytes -- per registered region, a run of this batch's
+     frags with gaps of at most FDGPU_IO_GAP (a round robin's other tiles'
+     frags lie between this tile's) -- and each range is copied into the
+     slot's mirror by the DMA engines; the records then name a range and an
+     offset in it, and the payloads are parsed and verified where the copy
+     put them.  More than FDGPU_IO_RANGES_MAX ranges, or more bytes than the
+     mirror holds: this batch takes the kernel-load path. */
+  const uint64_t rtab_at = chk_at + ((n * 2 * sizeof(uint64_t) + 63) & ~63ull);
+  uint64_t *h_rtab = (uint64_t *)(s->h_io + rtab_at);
+  struct Range { uintptr_t lo, hi; };
+  static thread_local Range rg[FDGPU_IO_RANGES_MAX];
+  uint32_t nr = 0;
   uint64_t dev_off = 0, bound = 0;
   bool any_chk = false;
-  const fdgpu_engine::Reg *rc = nullptr;
-  for (uint64_t t = 0; t < n; t++) {
-    const fdgpu_frag_io_t &f = fio[t];
-    const uint64_t q = ((uint64_t)f.sz + 15u) & ~15ull;
-    if (f.sz > FDT_TXN_MTU_BYTES || (f.src & 15u) || (f.out_off & 1u) || (uint64_t)f.out_off + f.out_cap > out_sz ||
-        f.out_cap > 0xFFFFu || f.link > link_cnt) {
-      set_err("frag %llu: size, alignment, out bounds or link", (unsigned long long)t);
-      return FDGPU_ERR_INVAL;
+  bool dma = g_io_dma && s->d_mirror;
+  constexpr uintptr_t FDGPU_IO_GAP = 4096;
+  auto fill = [&](bool use_dma) -> int {           /* 0, 1: redo without DMA, < 0: error */
+    const fdgpu_engine::Reg *rc = nullptr;
+    const fdgpu_engine::Reg *open_reg[16];
+    uint32_t open_rng[16], n_open = 0;
+    nr = 0; dev_off = 0; bound = 0; any_chk = false;
+    for (uint64_t t = 0; t < n; t++) {
+      const fdgpu_frag_io_t &f = fio[t];
+      const uint64_t q = ((uint64_t)f.sz + 15u) & ~15ull;
+      if (f.sz > FDT_TXN_MTU_BYTES || (f.src & 15u) || (f.out_off & 1u) || (uint64_t)f.out_off + f.out_cap > out_sz ||
+          f.out_cap > 0xFFFFu || f.link > link_cnt) {
+        set_err("frag %llu: size, alignment, out bounds or link", (unsigned long long)t);
+        return FDGPU_ERR_INVAL;
+      }
+      if (!rc || f.src < rc->base || f.src + q > rc->end) rc = region_of(e, (uintptr_t)f.src, q);
+      if (!rc) { set_err("frag %llu: payload not inside a registered region", (unsigned long long)t); return FDGPU_ERR_UNREG; }
+      uint32_t off, sz = f.sz;
+      if (use_dma) {
+        uint32_t k = 0;
+        while (k < n_open && open_reg[k] != rc) k++;
+        uint32_t ri = k < n_open ? open_rng[k] : UINT32_MAX;
+        if (ri != UINT32_MAX && f.src >= rg[ri].lo && f.src <= rg[ri].hi + FDGPU_IO_GAP) {
+          rg[ri].hi = std::max<uintptr_t>(rg[ri].hi, f.src + q);
+        } else {
+          if (nr == FDGPU_IO_RANGES_MAX || (k == n_open && n_open == 16)) return 1;
+          ri = nr++;
+          rg[ri] = Range{(uintptr_t)f.src, (uintptr_t)(f.src + q)};
+          if (k == n_open) { open_reg[n_open] = rc; n_open++; }
+          open_rng[k] = ri;
+        }
+        off = (uint32_t)(f.src - rg[ri].lo);
+        sz |= ri << 16;
+      } else {
+        /* streaming stores: the records are for the device (read over the
+           bus), not this core -- no line fills for them, nothing to snoop */
+        _mm_stream_si64((long long *)&h_src[t], (long long)(rc->dbase + (f.src - rc->base)));
+        off = (uint32_t)dev_off;
+        dev_off += q;
+        if (dev_off > e->cfg.max_arena) { set_err("frags exceed the engine's arena"); return FDGPU_ERR_INVAL; }
+      }
+      _mm_stream_si128((__m128i *)&h_fx[t], _mm_set_epi32((int)f.out_cap, (int)f.out_off, (int)sz, (int)off));
+      if (f.link) {                                       /* {line address, seq}; fd_frag_meta_t.seq: offset 0 */
+        _mm_stream_si128((__m128i *)&h_chk[2 * t],
+                         _mm_set_epi64x((long long)f.seq, (long long)(ldev[f.link - 1] + (f.seq & lmask[f.link - 1]) * 32u)));
+        any_chk = true;
+      } else {
+        _mm_stream_si64((long long *)&h_chk[2 * t], 0);
+      }
+      bound += fdt_frag_sig_bound(f.sz);
     }
-    if (!rc || f.src < rc->base || f.src + q > rc->end) rc = region_of(e, (uintptr_t)f.src, q);
-    if (!rc) { set_err("frag %llu: payload not inside a registered region", (unsigned long long)t); return FDGPU_ERR_UNREG; }
-    /* streaming stores: the records are for the device (read over the bus),
-       not this core -- no line fills for them, nothing for the bus to snoop */
-    _mm_stream_si64((long long *)&h_src[t], (long long)(rc->dbase + (f.src - rc->base)));
-    _mm_stream_si128((__m128i *)&h_fx[t], _mm_set_epi32((int)f.out_cap, (int)f.out_off, (int)f.sz, (int)dev_off));
-    if (f.link) {                                       /* {line address, seq}; fd_frag_meta_t.seq: offset 0 */
-      _mm_stream_si128((__m128i *)&h_chk[2 * t],
-                       _mm_set_epi64x((long long)f.seq, (long long)(ldev[f.link - 1] + (f.seq & lmask[f.link - 1]) * 32u)));
-      any_chk = true;
-    } else {
-      _mm_stream_si64((long long *)&h_chk[2 * t], 0);
+    if (use_dma) {                                     /* each range's place in the mirror */
+      uint64_t m = 0;
+      for (uint32_t r = 0; r < nr; r++) {
+        h_rtab[r] = m;
+        m = (m + (rg[r].hi - rg[r].lo) + 63u) & ~63ull;
+      }
+      if (m > s->mirror_cap) return 1;
     }
-    dev_off += q;
-    if (dev_off > e->cfg.max_arena) { set_err("frags exceed the engine's arena"); return FDGPU_ERR_INVAL; }
-    bound += fdt_frag_sig_bound(f.sz);
-  }
+    return 0;
+  };
+  int frc = fill(dma);
+  if (frc == 1) { dma = false; frc = fill(false); }
+  if (frc < 0) return frc;
   _mm_sfence();                                        /* the streamed records reach memory before the launches */
   if (bound > e->cfg.max_sig) { set_err("batch may exceed max_sig (%llu)", (unsigned long long)e->cfg.max_sig); return FDGPU_ERR_INVAL; }
   const uint64_t sp1 = g_sp_on ? sp_now() : 0;
@@ -1216,12 +1323,18 @@ int64_t fdgpu_submit_frags_io(fdgpu_engine_t *e, fdgpu_frag_io_t const *fio, uin
      the out frags and the results written in place over the bus -- then the
      completion word */
   uint8_t *out_dev = out_sz ? (uint8_t *)(ro->dbase + ((uintptr_t)out - ro->base)) : nullptr;
+  uint8_t *arena = dma ? s->d_mirror : s->d_arena;
   if (n) {
     const fdgpu_frag_ex_t *d_fx = s->d_fxio;
     const bool zero_cnt = !(kflags(e) & FDGPU_FLAG_KCACHE);
+    for (uint32_t r = 0; dma && r < nr; r++)
+      HIPCHK(hipMemcpyAsync(s->d_mirror + h_rtab[r], (const void *)rg[r].lo, rg[r].hi - rg[r].lo, hipMemcpyHostToDevice,
+                            s->stream),
+             FDGPU_ERR_DEVICE);
     HIPCHK(fdgpu_launch_frag_ingest_io((const uint64_t *)(s->d_ioh + src_at), (const fdgpu_frag_ex_t *)s->d_ioh,
-                                       any_chk ? (const uint64_t *)(s->d_ioh + chk_at) : nullptr, (uint32_t)n,
-                                       s->d_arena, s->d_fxio, s->d_txn_out, s->d_txn_sz, s->d_sigs, s->d_txns,
+                                       any_chk ? (const uint64_t *)(s->d_ioh + chk_at) : nullptr,
+                                       dma ? (const uint64_t *)(s->d_ioh + rtab_at) : nullptr, (uint32_t)n,
+                                       arena, s->d_fxio, s->d_txn_out, s->d_txn_sz, s->d_sigs, s->d_txns,
                                        s->d_io_cnt,
                                        zero_cnt ? fdgpu_verify_cnt_word(s->d_ws, (uint32_t)bound) : nullptr, s->stream),
            FDGPU_ERR_DEVICE);
@@ -1230,6 +1343,7 @@ int64_t fdgpu_submit_frags_io(fdgpu_engine_t *e, fdgpu_frag_io_t const *fio, uin
       HIPCHK(hipEventRecord(s->parsed, s->stream), FDGPU_ERR_DEVICE);
       s->vpending = true;
       s->m_n = (uint32_t)n; s->m_seed = hash_seed; s->m_out = out_dev; s->m_cb = cb; s->m_bound = bound;
+      s->m_arena = arena;
       e->pending.push_back(s);
       s->staged = false; st_rlx(s->held, false); st_rlx(s->polls, 0u); s->frag = true; s->io = true; s->tr_sz = 0; s->tr_base = 0;
       st_rlx(s->ticket, e->next_ticket++);
@@ -1238,12 +1352,12 @@ int64_t fdgpu_submit_frags_io(fdgpu_engine_t *e, fdgpu_frag_io_t const *fio, uin
       if (rc) return rc;
       return s->ticket;
     }
-    HIPCHK(fdgpu_launch_verify_sigs(s->d_arena, s->d_sigs, (uint32_t)bound, nullptr, e->d_btab, s->d_ws, s->d_sig_codes,
+    HIPCHK(fdgpu_launch_verify_sigs(arena, s->d_sigs, (uint32_t)bound, nullptr, e->d_btab, s->d_ws, s->d_sig_codes,
                                     ring_kflags(e, s, bound), s->stream, s->d_io_cnt, e->resident_blocks, e->kc_seed,
                                     zero_cnt),
            FDGPU_ERR_DEVICE);
     HIPCHK(fdgpu_launch_frag_finish_io(s->d_txns, (uint32_t)n, s->d_sig_codes, s->d_txn_sz, d_fx, s->d_txn_out,
-                                       s->d_arena, hash_seed, out_dev, (int8_t *)s->d_trh, (uint64_t *)(s->d_trh + cb),
+                                       arena, hash_seed, out_dev, (int8_t *)s->d_trh, (uint64_t *)(s->d_trh + cb),
                                        (uint16_t *)(s->d_trh + cb + n * 8), s->d_io_cnt, s->stream),
            FDGPU_ERR_DEVICE);
   }

@@ -171,11 +171,17 @@ hipError_t fdgpu_launch_frag_finish(const fdgpu_txn_desc_t *d_tds, uint32_t n, c
    out frags at d_out + d_fx[i].tr_off ([payload][pad][fd_txn_t][u16 sz]) in
    16-B stores. */
 #define FDGPU_FX_LAPPED 0x80000000u     /* in fdgpu_frag_ex_t.tr_cap (out_cap <= 0xFFFF) */
+/* DMA gather (d_rtab != NULL): the payloads already lie in the batch arena
+   (the DMA engines copied the batch's source ranges there); a record's sz
+   carries its range (bits 16..23) and off its offset in that range, and the
+   ingest kernel only resolves off = d_rtab[range] + off */
+#define FDGPU_IO_RANGES_MAX 255u
 uint64_t   fdgpu_frag_fp_bound(uint32_t sz);
 hipError_t fdgpu_launch_frag_ingest_io(const uint64_t *d_src, const fdgpu_frag_ex_t *d_fx, const uint64_t *d_chk,
-                                       uint32_t n, uint8_t *d_arena, fdgpu_frag_ex_t *d_fx_dev, uint8_t *d_txn_out,
-                                       uint16_t *d_txn_sz, fdgpu_sig_desc_t *d_sigs, fdgpu_txn_desc_t *d_tds,
-                                       uint32_t *d_n_sig, uint32_t *d_zero_word, hipStream_t stream);
+                                       const uint64_t *d_rtab, uint32_t n, uint8_t *d_arena,
+                                       fdgpu_frag_ex_t *d_fx_dev, uint8_t *d_txn_out, uint16_t *d_txn_sz,
+                                       fdgpu_sig_desc_t *d_sigs, fdgpu_txn_desc_t *d_tds, uint32_t *d_n_sig,
+                                       uint32_t *d_zero_word, hipStream_t stream);
 hipError_t fdgpu_launch_frag_finish_io(const fdgpu_txn_desc_t *d_tds, uint32_t n, const int8_t *d_sig_codes,
                                        const uint16_t *d_txn_sz, const fdgpu_frag_ex_t *d_fx, const uint8_t *d_txn_out,
                                        const uint8_t *d_arena, uint64_t hash_seed, uint8_t *d_out, int8_t *d_codes,

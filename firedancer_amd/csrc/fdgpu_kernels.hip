@@ -1393,19 +1393,23 @@ FDG_DEV uint32_t unit_owner(uint32_t incl, uint32_t k) {
    thread clears the verify kernel's queue counter (zero_word). */
 __global__ void __launch_bounds__(256) fdgpu_frag_ingest_io_kernel(
     const uint64_t *__restrict__ src, const fdgpu_frag_ex_t *__restrict__ fx, const uint64_t *__restrict__ chk,
-    uint32_t n, uint8_t *__restrict__ arena, fdgpu_frag_ex_t *__restrict__ fx_dev, uint8_t *__restrict__ txn_out,
-    uint16_t *__restrict__ txn_sz, fdgpu_sig_desc_t *__restrict__ sigs, fdgpu_txn_desc_t *__restrict__ tds,
-    uint32_t *__restrict__ n_sig, uint32_t *__restrict__ zero_word) {
+    const uint64_t *__restrict__ rtab, uint32_t n, uint8_t *__restrict__ arena, fdgpu_frag_ex_t *__restrict__ fx_dev,
+    uint8_t *__restrict__ txn_out, uint16_t *__restrict__ txn_sz, fdgpu_sig_desc_t *__restrict__ sigs,
+    fdgpu_txn_desc_t *__restrict__ tds, uint32_t *__restrict__ n_sig, uint32_t *__restrict__ zero_word) {
   const uint32_t lane = threadIdx.x & 63u, wpb = blockDim.x >> 6;
   if (blockIdx.x == 0 && threadIdx.x == 0 && zero_word) *zero_word = 0u;
   for (uint32_t g = blockIdx.x * wpb + (threadIdx.x >> 6); g * 64u < n; g += gridDim.x * wpb) {
     const uint32_t f = g * 64u + lane;
     const bool act = f < n;
-    const uint64_t s = act ? src[f] : 0ull;
     fdgpu_frag_ex_t x = act ? fx[f] : fdgpu_frag_ex_t{0u, 0u, 0u, 0u};
     const uint64_t line = (act && chk) ? chk[2u * f] : 0ull;
     const uint64_t seq = line ? chk[2u * f + 1u] : 0ull;
-    const uint32_t nq = (x.sz + 15u) >> 4;
+    if (rtab && act) {                                  /* DMA gather: the payload is in the arena already */
+      x.off = (uint32_t)(rtab[x.sz >> 16] + x.off);
+      x.sz &= 0xFFFFu;
+    }
+    const uint64_t s = (act && !rtab) ? src[f] : 0ull;
+    const uint32_t nq = rtab ? 0u : (x.sz + 15u) >> 4;
     const uint32_t incl = wave_incl_scan(nq), excl = incl - nq;
     const uint32_t total = (uint32_t)__shfl((int)incl, 63, 64);
     /* unit k of the group: its owner lane's source and arena place (all
@@ -1677,7 +1681,9 @@ hipError_t fdgpu_launch_verify_sigs(const uint8_t *d_arena, const fdgpu_sig_desc
      nothing for it */
   if (!resident_blocks) resident_blocks = 1;
   uint32_t slow_blocks = grid < resident_blocks ? grid : resident_blocks;
-  if (slow_blocks > FDGPU_FULL_BLOCKS) slow_blocks = FDGPU_FULL_BLOCKS;     /* strides over its queue */
+  /* strides over its queue; a tile-sized batch (<= 64 blocks) gets a quarter */
+  const uint32_t slow_cap = grid > 64u ? FDGPU_FULL_BLOCKS : FDGPU_FULL_BLOCKS / 4u;
+  if (slow_blocks > slow_cap) slow_blocks = slow_cap;
   const uint32_t *key_of = nullptr;
   if (flags & FDGPU_FLAG_KCACHE) {
     const uint64_t hts = kc_ht_slots(lanes);
@@ -1817,12 +1823,13 @@ static uint32_t aux_blocks(uint32_t n) {          /* waves of 64 frags, 4 per bl
 }
 
 hipError_t fdgpu_launch_frag_ingest_io(const uint64_t *d_src, const fdgpu_frag_ex_t *d_fx, const uint64_t *d_chk,
-                                       uint32_t n, uint8_t *d_arena, fdgpu_frag_ex_t *d_fx_dev, uint8_t *d_txn_out,
-                                       uint16_t *d_txn_sz, fdgpu_sig_desc_t *d_sigs, fdgpu_txn_desc_t *d_tds,
-                                       uint32_t *d_n_sig, uint32_t *d_zero_word, hipStream_t stream) {
+                                       const uint64_t *d_rtab, uint32_t n, uint8_t *d_arena,
+                                       fdgpu_frag_ex_t *d_fx_dev, uint8_t *d_txn_out, uint16_t *d_txn_sz,
+                                       fdgpu_sig_desc_t *d_sigs, fdgpu_txn_desc_t *d_tds, uint32_t *d_n_sig,
+                                       uint32_t *d_zero_word, hipStream_t stream) {
   if (!n) return hipSuccess;
-  hipLaunchKernelGGL(fdgpu_frag_ingest_io_kernel, dim3(aux_blocks(n)), dim3(256), 0, stream, d_src, d_fx, d_chk, n,
-                     d_arena, d_fx_dev, d_txn_out, d_txn_sz, d_sigs, d_tds, d_n_sig, d_zero_word);
+  hipLaunchKernelGGL(fdgpu_frag_ingest_io_kernel, dim3(aux_blocks(n)), dim3(256), 0, stream, d_src, d_fx, d_chk,
+                     d_rtab, n, d_arena, d_fx_dev, d_txn_out, d_txn_sz, d_sigs, d_tds, d_n_sig, d_zero_word);
   return hipGetLastError();
 }
 
