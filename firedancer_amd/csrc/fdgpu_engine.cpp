@@ -58,9 +58,14 @@ namespace {
 std::atomic<uint64_t> g_sp_loop{0}, g_sp_enq{0}, g_sp_calls{0}, g_sp_frags{0};
 inline uint64_t sp_now() { timespec ts; clock_gettime(CLOCK_MONOTONIC, &ts); return ts.tv_sec * 1000000000ull + ts.tv_nsec; }
 const bool g_sp_on = getenv("FDGPU_SUBMIT_PROF") && getenv("FDGPU_SUBMIT_PROF")[0] == '1';
-/* gathered batches read their payloads by DMA (FDGPU_IO_DMA=0: by the ingest
-   kernel's loads over the bus, the round-4 path) */
-const bool g_io_dma = !(getenv("FDGPU_IO_DMA") && getenv("FDGPU_IO_DMA")[0] == '0');
+/* FDGPU_IO_DMA=1: gathered batches read their payloads by DMA, the source
+   ranges copied into a device mirror and parsed there (engine alone, two
+   engines: 86-89 vs 80-81 M txn/s); default off, the ingest kernel's loads over
+   the bus: in the mux tiles the ranges of two tiles sharing a link interleave
+   (each copy carries the other tile's payloads too) and the range building
+   sits on the tile's thread -- two tiles 42-59 M with DMA vs 71-72 M
+   without (profiles/r05/aux_blocks.md) */
+const bool g_io_dma = getenv("FDGPU_IO_DMA") && getenv("FDGPU_IO_DMA")[0] == '1';
 /* the last FDGPU_ST_RING fdgpu_submit calls of the process: {staging copy,
    descriptor expansion, enqueue} ns (fdgpu_debug_submit_times).  Each call
    writes the entry its fetch_add drew; the words are relaxed atomics, so

@@ -68,7 +68,17 @@ typedef struct {
    around the verify therefore run on few, fat workgroups that stride over
    their work: */
 #define FDGPU_FULL_BLOCKS   16u           /* the fallback chain: its queue is ~empty (split failures ~2^-30) */
-#define FDGPU_AUX_BLOCKS    64u           /* combine, the gathered batches' ingest and finish */
+#define FDGPU_AUX_BLOCKS    64u           /* combine */
+/* The gathered batches' ingest and finish: a workgroup resident beside the
+   verify holds a verify block's slot on its CU for its whole life (its waves
+   take VGPRs the second verify wave needs), and these kernels wait on the bus,
+   so their slot time -- not their own duration -- is what the verify loses.
+   16 blocks that each keep more bus accesses in flight cost a quarter of the
+   slot time of 64 and still fill PCIe (profiles/r05/ubench_pcie.jsonl: 16 x
+   256 threads read 57 GB/s): engine-only gathered capacity, two engines,
+   69 -> 81 M txn/s, and two cfg1 tiles 58.8 -> 71.5 M
+   (profiles/r05/aux_blocks.md).  FDGPU_AUX_BLOCKS_IN / _FIN override. */
+#define FDGPU_IO_BLOCKS     16u
 /* SHA-512 block-count groups of the host-side bucketing (expand): messages of
    more blocks than this share the last group */
 #define FDGPU_NBLK_GROUPS   32u
@@ -155,7 +165,7 @@ hipError_t fdgpu_launch_frag_ring(const uint8_t *d_arena, const fdgpu_frag_ex_t 
 hipError_t fdgpu_launch_frag_finish(const fdgpu_txn_desc_t *d_tds, uint32_t n, const int8_t *d_sig_codes,
                                     const uint16_t *d_txn_sz, const fdgpu_frag_ex_t *d_fx, const uint8_t *d_txn_out,
                                     int8_t *d_codes, uint8_t *d_trailers, hipStream_t stream);
-/* fdgpu_submit_frags_io's kernels, each on at most FDGPU_AUX_BLOCKS blocks
+/* fdgpu_submit_frags_io's kernels, each on at most FDGPU_IO_BLOCKS blocks
    whose waves stride over groups of 64 frags.  Ingest: per group, the wave
    reads the 64 records and payload addresses (one coalesced read of each over
    the bus), copies the group's payloads (16-B units, flattened over the

@@ -1357,8 +1357,8 @@ __global__ void __launch_bounds__(256) fdgpu_frag_finish_kernel(const fdgpu_txn_
 }
 
 /* Gathered frag batches (fdgpu_submit_frags_io).  Both kernels run on at
-   most FDGPU_AUX_BLOCKS blocks (fdgpu_internal.h: beside running verifies a
-   launch's workgroups start only as verify blocks retire) and each wave
+   most FDGPU_IO_BLOCKS blocks (fdgpu_internal.h: a workgroup beside the
+   verify holds a verify block's slot while it waits on the bus) and each wave
    strides over groups of 64 frags, lane i of a group owning frag 64 g + i. */
 
 /* the group's lane that owns flattened unit k: the first lane whose
@@ -1485,14 +1485,18 @@ __global__ void __launch_bounds__(256) fdgpu_frag_ingest_io_kernel(
   }
 }
 
-/* byte b of frag's out frag [payload sz][pad to 2][fd_txn_t fp][u16 sz] */
-FDG_DEV uint32_t out_frag_byte(uint32_t b, const uint8_t *pl, uint32_t sz, uint32_t toff, const uint8_t *tr,
+/* bytes b, b+1 (b even) of a frag's out frag [payload sz][pad to 2]
+   [fd_txn_t fp][u16 sz] as one 16-bit word: the payload (16-B aligned in
+   the arena), the fd_txn_t (4-B aligned record, toff even) and the size
+   word all split on even offsets, so every half is one aligned 2-B load */
+FDG_DEV uint32_t out_frag_half(uint32_t b, const uint8_t *pl, uint32_t sz, uint32_t toff, const uint8_t *tr,
                                uint32_t fp) {
-  if (b < sz) return pl[b];
-  if (b < toff) return 0u;
-  if (b < toff + fp) return tr[b - toff];
-  const uint32_t k = b - toff - fp;
-  return k < 2u ? (sz >> (8u * k)) & 0xffu : 0u;
+  if (b < toff) {
+    const uint32_t v = *(const uint16_t *)(pl + b);
+    return b + 1u < sz ? v : v & 0xffu;                 /* the pad byte of an odd payload */
+  }
+  if (b < toff + fp) return *(const uint16_t *)(tr + (b - toff));
+  return b == toff + fp ? sz & 0xffffu : 0u;
 }
 
 /* Finish: per group, lane i writes frag i's code (the batch_single_msg
@@ -1580,19 +1584,15 @@ __global__ void __launch_bounds__(256) fdgpu_frag_finish_io_kernel(
         } else {
           uint32_t q[4];
 #pragma unroll
-          for (int i = 0; i < 4; i++) {
-            uint32_t v = 0;
-#pragma unroll
-            for (int j = 0; j < 4; j++) v |= out_frag_byte(b0 + 4u * i + j, pl, sz, otoff, tr, ofp) << (8 * j);
-            q[i] = v;
-          }
+          for (int i = 0; i < 4; i++)
+            q[i] = out_frag_half(b0 + 4u * i, pl, sz, otoff, tr, ofp) |
+                   (out_frag_half(b0 + 4u * i + 2u, pl, sz, otoff, tr, ofp) << 16);
           w = make_uint4(q[0], q[1], q[2], q[3]);
         }
         *(uint4 *)dst = w;
       } else {
         for (uint32_t b = b0; b < b0 + 16u && b < oosz; b += 2u)
-          *(uint16_t *)(out + oof + b) = (uint16_t)(out_frag_byte(b, pl, sz, otoff, tr, ofp) |
-                                                    (out_frag_byte(b + 1u, pl, sz, otoff, tr, ofp) << 8));
+          *(uint16_t *)(out + oof + b) = (uint16_t)out_frag_half(b, pl, sz, otoff, tr, ofp);
       }
     }
   }
@@ -1817,9 +1817,15 @@ hipError_t fdgpu_launch_frag_finish(const fdgpu_txn_desc_t *d_tds, uint32_t n, c
 
 uint64_t fdgpu_frag_fp_bound(uint32_t sz) { return fdt_frag_fp_bound(sz); }
 
-static uint32_t aux_blocks(uint32_t n) {          /* waves of 64 frags, 4 per block, at most FDGPU_AUX_BLOCKS */
+static uint32_t env_u32(const char *k, uint32_t d) {
+  const char *v = getenv(k);
+  return v && atoi(v) > 0 ? (uint32_t)atoi(v) : d;
+}
+static const uint32_t g_aux_in = env_u32("FDGPU_AUX_BLOCKS_IN", FDGPU_IO_BLOCKS);
+static const uint32_t g_aux_fin = env_u32("FDGPU_AUX_BLOCKS_FIN", FDGPU_IO_BLOCKS);
+static uint32_t aux_blocks(uint32_t n, uint32_t cap = FDGPU_AUX_BLOCKS) {   /* waves of 64 frags, 4 per block */
   const uint32_t b = (n + 255u) / 256u;
-  return b < FDGPU_AUX_BLOCKS ? b : FDGPU_AUX_BLOCKS;
+  return b < cap ? b : cap;
 }
 
 hipError_t fdgpu_launch_frag_ingest_io(const uint64_t *d_src, const fdgpu_frag_ex_t *d_fx, const uint64_t *d_chk,
@@ -1828,7 +1834,7 @@ hipError_t fdgpu_launch_frag_ingest_io(const uint64_t *d_src, const fdgpu_frag_e
                                        fdgpu_sig_desc_t *d_sigs, fdgpu_txn_desc_t *d_tds, uint32_t *d_n_sig,
                                        uint32_t *d_zero_word, hipStream_t stream) {
   if (!n) return hipSuccess;
-  hipLaunchKernelGGL(fdgpu_frag_ingest_io_kernel, dim3(aux_blocks(n)), dim3(256), 0, stream, d_src, d_fx, d_chk,
+  hipLaunchKernelGGL(fdgpu_frag_ingest_io_kernel, dim3(aux_blocks(n, g_aux_in)), dim3(256), 0, stream, d_src, d_fx, d_chk,
                      d_rtab, n, d_arena, d_fx_dev, d_txn_out, d_txn_sz, d_sigs, d_tds, d_n_sig, d_zero_word);
   return hipGetLastError();
 }
@@ -1839,7 +1845,7 @@ hipError_t fdgpu_launch_frag_finish_io(const fdgpu_txn_desc_t *d_tds, uint32_t n
                                        uint64_t *d_tags, uint16_t *d_out_szs, uint32_t *d_zero_next,
                                        hipStream_t stream) {
   if (!n) return hipSuccess;
-  hipLaunchKernelGGL(fdgpu_frag_finish_io_kernel, dim3(aux_blocks(n)), dim3(256), 0, stream, d_tds, n, d_sig_codes,
+  hipLaunchKernelGGL(fdgpu_frag_finish_io_kernel, dim3(aux_blocks(n, g_aux_fin)), dim3(256), 0, stream, d_tds, n, d_sig_codes,
                      d_txn_sz, d_fx, d_txn_out, d_arena, hash_seed, d_out, d_codes, d_tags, d_out_szs, d_zero_next);
   return hipGetLastError();
 }

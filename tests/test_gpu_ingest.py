@@ -486,3 +486,25 @@ def test_frag_io_merged_verify(oracle):
             td[k] = (int(offs[k]) + d["message_off"], len(p) - d["message_off"],
                      int(offs[k]) + d["signature_off"], int(offs[k]) + d["acct_addr_off"], d["signature_cnt"])
         assert (c1 == oracle.verify_txns(arena, td, nthreads=8)).all(), j
+
+
+def test_frag_io_dma_gather_and_small_grids():
+    """The gathered path's two other shapes, in a child process (both are read
+    once at library load): FDGPU_IO_DMA=1 -- the payload ranges copied by the
+    DMA engines into the slot's mirror and parsed, re-checked and verified
+    there -- and the ingest / finish kernels on one block each (every wave
+    strides over many 64-frag groups).  Each runs the gathered-batch tests
+    above: codes, tags and out frags against the oracle, and the lap re-check."""
+    import os
+    import subprocess
+    import sys
+    if os.environ.get("FDGPU_IO_SUBRUN"):
+        pytest.skip("inside the child run")
+    here = os.path.dirname(os.path.abspath(__file__))
+    for extra in ({"FDGPU_IO_DMA": "1"}, {"FDGPU_AUX_BLOCKS_IN": "1", "FDGPU_AUX_BLOCKS_FIN": "1"}):
+        env = dict(os.environ, FDGPU_IO_SUBRUN="1", **extra)
+        r = subprocess.run([sys.executable, "-m", "pytest", "-x", "-q", "-p", "no:cacheprovider", "-m", "gpu",
+                            os.path.join(here, "test_gpu_ingest.py"), "-k", "frag_io"],
+                           env=env, capture_output=True, text=True, timeout=600)
+        assert r.returncode == 0, (extra, r.stdout[-3000:], r.stderr[-2000:])
+        assert " passed" in r.stdout, r.stdout[-2000:]

@@ -415,7 +415,7 @@ def test_vmux_gather_reads_reasm_link_gpu(oracle, engines):
             if guard:
                 assert st["lapped"] == 0 and exp_out.count(0) > 100
             else:
-                assert st["lapped"] > 0 and len(kept) > 100
+                assert st["lapped"] > 0 and len(kept) > 20     # (how many survive is timing: DMA vs load gather)
         finally:
             vm.close()
             ver.close()

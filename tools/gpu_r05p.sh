@@ -1,0 +1,10 @@
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+O=gpurun_out/r05p; mkdir -p $O
+export TMPDIR=/tmp FDGPU_IO_DMA=0 GPU_MAX_HW_QUEUES=32
+timeout -k 10 200 python tools/make_tile_npz.py --out /tmp/cfg1.npz > $O/npz.log 2>&1 || { echo NPZ_FAILED; tail $O/npz.log; exit 1; }
+P="python -u tools/io_probe.py --npz /tmp/cfg1.npz --out $O/io.jsonl --batches 300"
+for a in "--engines 1" "--engines 2" "--engines 1 --inflight 16" "--engines 2 --inflight 12" "--engines 3" "--engines 4 --inflight 6" "--engines 2 --inflight 16" "--engines 2 --pair 0 --spread 0" "--engines 2 --batch 32768"; do
+  timeout -k 10 120 $P $a >> $O/io.log 2>&1 || { echo PROBE_FAILED $a; tail -20 $O/io.log; exit 1; }
+done
+cat $O/io.jsonl
