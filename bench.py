@@ -508,12 +508,11 @@ TILE_PAIR = 2
 # (concurrent small launches otherwise stack two blocks per CU; profiles/r04/spread.md)
 TILE_SPREAD = 2
 # multi-signature frags: a batch also closes at this many signatures by the frag-size bound the tile sees
-# (~9.5 per cfg3 frag for ~6.5 real): ~2.6 K cfg3 txns, so 8 batches in flight are ~1.3 ms of GPU work
-# (49152: 1-tile p99 batch 5.8 ms, 2 tiles 59-65 M sig/s; 24576: 3.0 ms, 67-70 M; profiles/r04/tile_run_order.md).
-# Two tiles share the chip, so each takes half-size batches: 16384 gave two tiles 65.7 M sigs/s at p99 4.7 ms
-# against 24576's 69.0 M at 7.2 ms (profiles/r04/tile_cfg3_cap/)
-TILE_CFG3_SIG_MAX = 24576
-TILE_CFG3_SIG_MAX_BY_TILES = {1: 24576, 2: 16384}
+# (~9.5 per cfg3 frag for ~6.5 real).  With the gathered kernels on 16 workgroups (round 5) one tile
+# reaches 86 M sig/s at 32768 (p99 3.0 ms) against 70.5 M at 24576, and two tiles 91 M at 24576 each
+# (p99 5.1 ms; 32768: 90 M at p99 8.6-12 ms, 49152: 90 M at 10 ms; profiles/r05/tile_cfg3_cap.md)
+TILE_CFG3_SIG_MAX = 32768
+TILE_CFG3_SIG_MAX_BY_TILES = {1: 32768, 2: 24576}
 TILE_RUNS_CFG3 = (  # the same tile over cfg3 frags (1-12 signatures, payloads up to the 1232-B MTU: SURVEY 8(d) cfg5)
     ("mux1_capacity_cfg3", 1, 1, -1.0),
     ("mux2_capacity_cfg3", 2, 2, -1.0),
@@ -914,6 +913,16 @@ def main():
             eng_nb = VerifyEngine(device, max_txn=1024, ring_depth=1, bucket=False)
             extras.update(cfg3_rate(eng, eng_nb, cfg3))
             eng_nb.close()
+        if tl is not None:
+            # the tiles against this GPU's device-resident rate of the same txns (cfg1: one signature each)
+            extras["tile_mux2_capacity_vs_device_resident"] = round(
+                extras["tile_mux2_capacity_txns_per_s"] / (value / dist.world), 3)
+            if "tile_mux2_capacity_cfg3_sigs_per_s" in extras:
+                extras["tile_mux2_vs_mux1_capacity_cfg3"] = round(
+                    extras["tile_mux2_capacity_cfg3_sigs_per_s"] / extras["tile_mux1_capacity_cfg3_sigs_per_s"], 3)
+                if "cfg3_sigs_per_s" in extras:
+                    extras["tile_mux2_capacity_cfg3_vs_device_resident"] = round(
+                        extras["tile_mux2_capacity_cfg3_sigs_per_s"] / extras["cfg3_sigs_per_s"], 3)
         if args.keypool_txns:
             extras.update(key_cache_rate(eng, device, args.keypool_txns, workload.CFG1_SEED + 0x700 + dist.rank))
         if args.host_fed:
