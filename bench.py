@@ -74,6 +74,10 @@ def parse():
                     help="device batches verified round-robin, each on its own HIP stream (1: one stream)")
     ap.add_argument("--cfg3-txns", type=int, default=150_000,
                     help="multi-signature (cfg3) txns for the secondary device-resident line (0: skip)")
+    ap.add_argument("--tile-cfg3-txns", type=int, default=250_000,
+                    help="cfg3 txns for the tile lines' _cfg3 runs (0: skip them): ~1.6 M signatures, ~70 one-tile "
+                         "batches, so the pipeline's fill and drain stay a small part of a run (150 K gave one tile "
+                         "69 M sig/s against 86 M over 1 M txns; profiles/r05/tile_cfg3_cap.md)")
     ap.add_argument("--host-fed", type=int, default=1,
                     help="1: add the host-fed line (the cfg2 batch from host memory through the engine's ring)")
     ap.add_argument("--tile", type=int, default=1, help="1: add the cfg5 verify-tile lines (tango in -> GPU -> tango out)")
@@ -855,7 +859,10 @@ def main():
     cfg3 = workload.cfg3(args.cfg3_txns, seed=workload.CFG3_SEED + dist.rank) if args.cfg3_txns else None
     tl = None
     if args.tile and not args.no_extras:
-        tl = tile_lines(dist.local_rank, arena, txns, modes, cpus, cfg3=cfg3)
+        cfg3_tile = (workload.cfg3(args.tile_cfg3_txns, seed=workload.CFG3_SEED + 0x100 + dist.rank)
+                     if args.tile_cfg3_txns else None)
+        tl = tile_lines(dist.local_rank, arena, txns, modes, cpus, cfg3=cfg3_tile)
+        del cfg3_tile
         tl["tile_mux1_capacity_txns_per_s_node"] = round(dist.sum(tl["tile_mux1_capacity_txns_per_s"]), 1)
         tl["tile_published_ok_all_ranks"] = dist.sum(
             1 if all(v for k, v in tl.items() if k.endswith("_published_ok")) else 0) == dist.world

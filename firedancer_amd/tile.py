@@ -1126,14 +1126,21 @@ class VerifyMuxTile:
     def start(self, cpu=None):
         """Runs the mux loop on a thread of its own (pinned to `cpu` by the
         thread itself, so the caller's own affinity is never touched)."""
+        up = self._threading.Event()
+
         def body():
             if cpu is not None:
                 os.sched_setaffinity(0, {cpu})
+            up.set()
             self._rc = lib().fdt_mux_run(c.byref(self.mcfg), c.byref(self.cb), self._t, c.byref(self._halt),
                                          c.byref(self._mstats))
         self._halt.value = 0
         self._th = self._threading.Thread(target=body, daemon=True)
         self._th.start()
+        # returns once the thread is entering the loop (as the reference's tiles
+        # signal RUN on their cnc before their producers start): a producer
+        # started next cannot lap a shallow link before the tile polls it
+        up.wait(10.0)
 
     def stop(self):
         if self._th is not None:
