@@ -617,6 +617,9 @@ def _tile_child(rank, cpus, arena, txns, modes, runs, tag=""):
             # batch completed (after the device read it), in ms at the link's offered rate; worst of the runs
             lm = min(x["counters"]["lap_margin_min"] for x in reps)
             out[f"tile_{name}_lap_margin_min_seqs"] = lm if lm < 2 ** 63 else None
+            out[f"tile_{name}_lap_margin_min_seqs_runs"] = [x["counters"]["lap_margin_min"] if
+                                                            x["counters"]["lap_margin_min"] < 2 ** 63 else None
+                                                            for x in reps]
             per_link = min(x["offered_txns_per_s"] / x["producers"] for x in reps if x.get("offered_txns_per_s"))
             out[f"tile_{name}_lap_margin_min_ms"] = round(lm / per_link * 1e3, 3) if lm < 2 ** 63 else None
     return out
