@@ -66,6 +66,8 @@ const bool g_sp_on = getenv("FDGPU_SUBMIT_PROF") && getenv("FDGPU_SUBMIT_PROF")[
    sits on the tile's thread -- two tiles 42-59 M with DMA vs 71-72 M
    without (profiles/r05/aux_blocks.md) */
 const bool g_io_dma = getenv("FDGPU_IO_DMA") && getenv("FDGPU_IO_DMA")[0] == '1';
+/* FDGPU_BIG_STREAMS=0: big ring batches verify on their own slot streams (A/B) */
+const bool g_big_off = getenv("FDGPU_BIG_STREAMS") && getenv("FDGPU_BIG_STREAMS")[0] == '0';
 /* the last FDGPU_ST_RING fdgpu_submit calls of the process: {staging copy,
    descriptor expansion, enqueue} ns (fdgpu_debug_submit_times).  Each call
    writes the entry its fetch_add drew; the words are relaxed atomics, so
@@ -167,6 +169,10 @@ struct fdgpu_engine {
   int8_t *d_scratch_codes = nullptr;   /* for fdgpu_verify_device with d_sig_codes == NULL */
   uint64_t scratch_cap = 0;
   std::vector<hipStream_t> batch_streams;   /* streams of device batches with their own queue */
+  /* ring batches that fill the chip on their own (FDGPU_BIG_SIGS) verify on
+     these two streams in turn, not on their slot's: see submit_slot */
+  hipStream_t big[2] = {nullptr, nullptr};
+  uint32_t big_rr = 0;
   /* the ring API (submit / stage / poll / release) may be called from several
      host threads (verify tiles sharing the node's engines) */
   std::mutex ring_mu;
@@ -637,6 +643,7 @@ void fdgpu_engine_close(fdgpu_engine_t *e) {
   if (e->compute) (void)hipStreamSynchronize(e->compute);
   for (auto &m : e->merges) if (m.stream) (void)hipStreamSynchronize(m.stream);
   for (auto &s : e->slots) { if (s.stream) (void)hipStreamSynchronize(s.stream); slot_free(s); }
+  for (auto b : e->big) if (b) { (void)hipStreamSynchronize(b); (void)hipStreamDestroy(b); }
   for (auto &m : e->merges) {
     for (auto ev : m.ev) if (ev) (void)hipEventDestroy(ev);
     if (m.h_tab) (void)hipHostFree(m.h_tab);
@@ -693,6 +700,19 @@ static int enqueue_verify(fdgpu_engine_t *e, const uint8_t *d_arena, const fdgpu
   return FDGPU_OK;
 }
 
+/* A ring batch of at least this many signatures fills every resident lane
+   of the chip (256 CUs x 4 SIMDs x 2 waves x 64 = 131,072) on its own.  Its
+   verify runs on one of the engine's two big-batch streams, in turn, after
+   its uploads (an event wait), and its read-back waits for it: at most two
+   such verifies overlap (the next one's waves fill the tail the previous
+   one leaves, as the device-resident line's two queues do), and the next
+   slots' uploads run under them.  On their own slot streams three 1 M
+   batches ran in lockstep -- three uploads at once with the GPU idle, then
+   three verifies at once -- 11.6-12.0 ms a batch from a registered arena
+   against 10.3 staged (rocprofv3 with --memory-copy-trace,
+   profiles/r05/host_fed_lockstep.md). */
+static constexpr uint64_t FDGPU_BIG_SIGS = 262144;
+
 /* Enqueue the batch already in slot s's pinned arena (arena_sz bytes). */
 /* `uploaded` = bytes of the arena whose host->device copy is already queued on
    the slot's stream (fdgpu_submit overlaps its staging memcpy with the copy) */
@@ -732,9 +752,21 @@ static int64_t submit_slot(fdgpu_engine_t *e, Slot *s, uint64_t arena_sz, fdgpu_
      slot's own stream with the slot's own workspace, so the ring's batches
      overlap each other on the GPU (a 64K-signature batch fills only half of
      the resident wave slots) */
+  hipStream_t vs = s->stream;
+  if ((uint64_t)ns >= FDGPU_BIG_SIGS && !g_big_off) {
+    for (auto &b : e->big)
+      if (!b) HIPCHK(hipStreamCreateWithFlags(&b, hipStreamNonBlocking), FDGPU_ERR_DEVICE);
+    vs = e->big[e->big_rr++ & 1u];
+    HIPCHK(hipEventRecord(s->h2d_done, s->stream), FDGPU_ERR_DEVICE);
+    HIPCHK(hipStreamWaitEvent(vs, s->h2d_done, 0), FDGPU_ERR_DEVICE);
+  }
   int rc = enqueue_verify(e, s->d_arena, s->d_sigs, perm ? s->d_perm : nullptr, (uint64_t)ns, s->d_txns, txn_cnt,
-                          s->d_sig_codes, s->d_txn_codes, s->stream, s->d_ws, ring_kflags(e, s, (uint64_t)ns));
+                          s->d_sig_codes, s->d_txn_codes, vs, s->d_ws, ring_kflags(e, s, (uint64_t)ns));
   if (rc) return rc;
+  if (vs != s->stream) {
+    HIPCHK(hipEventRecord(s->comp_done, vs), FDGPU_ERR_DEVICE);
+    HIPCHK(hipStreamWaitEvent(s->stream, s->comp_done, 0), FDGPU_ERR_DEVICE);
+  }
   if (txn_cnt) HIPCHK(hipMemcpyAsync(s->h_codes, s->d_txn_codes, txn_cnt, hipMemcpyDeviceToHost, s->stream), FDGPU_ERR_DEVICE);
   slot_flag_next(s);
   if (e->flag_poll && !e->drop_flag) HIPCHK(hipStreamWriteValue32(s->stream, s->d_flag, s->flag_seq, 0), FDGPU_ERR_DEVICE);

@@ -177,3 +177,28 @@ def test_stamps_variant_codes(tmp_path):
     env = dict(os.environ, FDGPU_LIB=so)
     r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, env=env, timeout=300)
     assert r.returncode == 0 and "ok" in r.stdout, r.stdout[-2000:] + r.stderr[-2000:]
+
+
+def test_big_ring_batches_on_shared_verify_streams(oracle):
+    """Ring batches of >= FDGPU_BIG_SIGS (262,144) signatures verify on the
+    engine's two big-batch streams in turn (each after its own uploads; its
+    read-back waits for it) while small batches keep their slot streams:
+    three 300 K batches in flight at once -- staged, from a registered arena,
+    and staged again -- with a small batch between them, every code equal
+    to the oracle's on a sample and to the workload's labels throughout."""
+    a, t, modes = workload.cfg1(300_000, seed=0xB16)
+    a_s, t_s, m_s = workload.cfg1(3000, seed=0xB17)
+    eng = fa.VerifyEngine(0, max_txn=300_000, max_arena=a.nbytes + 4096, ring_depth=4)
+    reg = np.ascontiguousarray(a).copy()
+    eng.host_register(reg)
+    try:
+        ref = oracle.verify_txns(a, t[:20000], nthreads=8)
+        tks = [eng.submit(a, t), eng.submit(reg, t), eng.submit(a_s, t_s), eng.submit(a, t)]
+        outs = [eng.poll(tk, blocking=True) for tk in tks]
+        for k in (0, 1, 3):
+            assert (outs[k][:20000] == ref).all(), k
+            assert ((outs[k] == 0) == (modes == 0)).all(), k
+        assert ((outs[2] == 0) == (m_s == 0)).all()
+    finally:
+        eng.host_unregister(reg)
+        eng.close()
