@@ -713,6 +713,11 @@ static int enqueue_verify(fdgpu_engine_t *e, const uint8_t *d_arena, const fdgpu
    profiles/r05/host_fed_lockstep.md). */
 static constexpr uint64_t FDGPU_BIG_SIGS = 262144;
 
+namespace {
+int64_t expand_par(uint64_t arena_sz, const fdgpu_txn_t *txns, uint64_t txn_cnt, uint64_t max_sig,
+                   fdgpu_sig_desc_t *sigs, fdgpu_txn_desc_t *tds, uint32_t *perm);
+}
+
 /* Enqueue the batch already in slot s's pinned arena (arena_sz bytes). */
 /* `uploaded` = bytes of the arena whose host->device copy is already queued on
    the slot's stream (fdgpu_submit overlaps its staging memcpy with the copy) */
@@ -723,7 +728,7 @@ static int64_t submit_slot(fdgpu_engine_t *e, Slot *s, uint64_t arena_sz, fdgpu_
                            uint64_t uploaded = 0, const uint8_t *src = nullptr, uint64_t t_stage = 0) {
   uint32_t *perm = bucket(e) ? s->h_perm : nullptr;
   const uint64_t t0 = sp_now();
-  const int64_t ns = expand(arena_sz, txns, txn_cnt, e->cfg.max_sig, s->h_sigs, s->h_txns, perm);
+  const int64_t ns = expand_par(arena_sz, txns, txn_cnt, e->cfg.max_sig, s->h_sigs, s->h_txns, perm);
   if (ns < 0) return FDGPU_ERR_INVAL;
   const uint64_t t1 = sp_now();
   struct Rec {                                  /* the call's times into the ring, on every return */
@@ -844,6 +849,114 @@ CopyPool &copy_pool() {
   return *p;
 }
 std::mutex g_stage_mu;                       /* one staging at a time uses the pool */
+
+/* expand() over FDGPU_COPY_THREADS parts of the transactions at once, for
+   the large batches whose single-threaded expansion (~3 ns a txn, 3 ms for
+   1 M) sat on the submitting thread beside the staging copy: pass 1 counts
+   and validates each part (signatures, block-count groups, the first bad
+   txn), pass 2 writes each part's descriptors at its prefix offsets, so the
+   output -- sig0s, descriptors, the stable block-count grouping and its
+   permutation -- is byte-identical to expand()'s, and so is the error
+   (the first failing txn in order, of either kind). */
+static constexpr uint64_t FDGPU_EXPAND_SPLIT_MIN = 65536;
+
+int64_t expand_par(uint64_t arena_sz, const fdgpu_txn_t *txns, uint64_t txn_cnt, uint64_t max_sig,
+                   fdgpu_sig_desc_t *sigs, fdgpu_txn_desc_t *tds, uint32_t *perm) {
+  if (txn_cnt < FDGPU_EXPAND_SPLIT_MIN) return expand(arena_sz, txns, txn_cnt, max_sig, sigs, tds, perm);
+  constexpr unsigned T = FDGPU_COPY_THREADS;
+  struct Part {
+    uint64_t lo = 0, hi = 0, ns = 0, bad = UINT64_MAX;
+    uint64_t grp[FDGPU_NBLK_GROUPS] = {};
+  } part[T];
+  const uint64_t per = (txn_cnt + T - 1) / T;
+  for (unsigned k = 0; k < T; k++) {
+    part[k].lo = std::min<uint64_t>(txn_cnt, k * per);
+    part[k].hi = std::min<uint64_t>(txn_cnt, part[k].lo + per);
+  }
+  std::vector<std::function<void()>> fns;
+  for (unsigned k = 0; k < T; k++)
+    fns.push_back([&, k]() {
+      Part &q = part[k];
+      for (uint64_t t = q.lo; t < q.hi; t++) {
+        const fdgpu_txn_t &x = txns[t];
+        const uint32_t cnt = x.sig_cnt;
+        tds[t].sig0 = (uint32_t)q.ns;                        /* part-relative until pass 2 */
+        tds[t].sig_cnt = cnt;
+        if (cnt == 0 || cnt > 16) { tds[t].sig_cnt = 0; continue; }
+        if ((uint64_t)x.msg_off + x.msg_sz > arena_sz || (uint64_t)x.sig_off + 64ull * cnt > arena_sz ||
+            (uint64_t)x.pub_off + 32ull * cnt > arena_sz) { q.bad = t; return; }
+        if (perm) q.grp[std::min(hram_blocks(x.msg_sz), FDGPU_NBLK_GROUPS) - 1] += cnt;
+        q.ns += cnt;
+      }
+    });
+  {
+    std::lock_guard<std::mutex> lk(g_stage_mu);
+    copy_pool().run(fns);
+  }
+  /* the first failure in transaction order: a part's bad descriptor, or the
+     txn at which the running count passes max_sig (expand()'s two checks) */
+  uint64_t base = 0;
+  for (unsigned k = 0; k < T; k++) {
+    const Part &q = part[k];
+    const uint64_t end = q.bad == UINT64_MAX ? q.hi : q.bad;
+    if (base + q.ns > max_sig || q.bad != UINT64_MAX) {
+      uint64_t ns = base;
+      for (uint64_t t = q.lo; t < end; t++) {
+        const uint32_t c = tds[t].sig_cnt;
+        if (ns + c > max_sig) { set_err("batch exceeds max_sig (%llu)", (unsigned long long)max_sig); return -1; }
+        ns += c;
+      }
+      if (q.bad != UINT64_MAX) {
+        set_err("txn %llu: descriptor out of arena bounds", (unsigned long long)q.bad);
+        return -1;
+      }
+    }
+    base += q.ns;
+  }
+  uint64_t next[T][FDGPU_NBLK_GROUPS], sig_base[T];
+  {
+    uint64_t o = 0, gbase[FDGPU_NBLK_GROUPS], acc = 0;
+    for (uint32_t g = 0; g < FDGPU_NBLK_GROUPS; g++) {
+      gbase[g] = o;
+      for (unsigned k = 0; k < T; k++) o += part[k].grp[g];
+    }
+    for (unsigned k = 0; k < T; k++) {
+      sig_base[k] = acc;
+      acc += part[k].ns;
+      for (uint32_t g = 0; g < FDGPU_NBLK_GROUPS; g++) {
+        next[k][g] = gbase[g];
+        gbase[g] += part[k].grp[g];
+      }
+    }
+  }
+  fns.clear();
+  for (unsigned k = 0; k < T; k++)
+    fns.push_back([&, k]() {
+      const Part &q = part[k];
+      uint64_t *nx = next[k];
+      for (uint64_t t = q.lo; t < q.hi; t++) {
+        const fdgpu_txn_t &x = txns[t];
+        const uint32_t s0 = tds[t].sig0 + (uint32_t)sig_base[k];
+        tds[t].sig0 = s0;
+        const uint32_t cnt = tds[t].sig_cnt;
+        if (!cnt) continue;
+        uint64_t *slot = perm ? &nx[std::min(hram_blocks(x.msg_sz), FDGPU_NBLK_GROUPS) - 1] : nullptr;
+        for (uint32_t j = 0; j < cnt; j++) {
+          const uint64_t i = slot ? (*slot)++ : (uint64_t)s0 + j;
+          sigs[i].msg_off = x.msg_off;
+          sigs[i].msg_sz = x.msg_sz;
+          sigs[i].sig_off = x.sig_off + 64u * j;
+          sigs[i].pub_off = x.pub_off + 32u * j;
+          if (perm) perm[i] = s0 + j;
+        }
+      }
+    });
+  {
+    std::lock_guard<std::mutex> lk(g_stage_mu);
+    copy_pool().run(fns);
+  }
+  return (int64_t)base;
+}
 }  // namespace
 
 extern "C" {

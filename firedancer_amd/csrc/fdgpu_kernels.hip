@@ -1577,6 +1577,11 @@ __global__ void __launch_bounds__(256) fdgpu_frag_finish_io_kernel(
       const uint8_t *tr = txn_out + (size_t)(g * 64u + o) * FDT_TXN_MAX_SZ;
       uint8_t *dst = out + oof + b0;
       if (k0 + lane >= total) continue;
+#if FDGPU_DIAG_NO_PAYLOAD_OUT
+      /* diagnostic build only (wrong output): the payload's own units are not
+         written back, to price their PCIe writes (tools/gpu_r05pay.sh) */
+      if (b0 + 16u <= sz) continue;
+#endif
       if (b0 + 16u <= cap && !(((uintptr_t)dst) & 15u)) {
         uint4 w;
         if (b0 + 16u <= sz) {
