@@ -801,6 +801,12 @@ static Slot *free_slot(fdgpu_engine_t *e) {
    which are ordered after it on the same stream. */
 static constexpr unsigned FDGPU_COPY_THREADS = 4;
 static constexpr uint64_t FDGPU_COPY_SPLIT_MIN = 4ull << 20;
+/* FDGPU_COPY_CHUNK_MB overrides the upload piece (A/B; 0: one piece per thread) */
+const uint64_t FDGPU_COPY_CHUNK = [] {
+  const char *v = getenv("FDGPU_COPY_CHUNK_MB");
+  const long long m = v ? atoll(v) : 16;
+  return m > 0 ? (uint64_t)m << 20 : UINT64_MAX;
+}();
 
 }  // extern "C"
 
@@ -974,10 +980,16 @@ static uint64_t stage_arena(fdgpu_engine_t *e, Slot *s, uint8_t const *arena, ui
       const uint64_t off = (uint64_t)i * part;
       if (off >= sz) return;
       const uint64_t n = sz - off < part ? sz - off : part;
-      memcpy(s->h_arena + off, arena + off, n);
-      if (hipSetDevice(e->device) != hipSuccess ||
-          hipMemcpyAsync(s->d_arena + off, s->h_arena + off, n, hipMemcpyHostToDevice, s->stream) != hipSuccess)
-        err[i] = 1;
+      if (hipSetDevice(e->device) != hipSuccess) { err[i] = 1; return; }
+      /* in FDGPU_COPY_CHUNK pieces, each queued for upload as soon as it is
+         copied: the DMA starts ~1 ms into the staging instead of after it
+         (a 1 M batch's 364 MB: its uploads then end ~3 ms sooner) */
+      for (uint64_t c = 0; c < n; c += FDGPU_COPY_CHUNK) {
+        const uint64_t m = n - c < FDGPU_COPY_CHUNK ? n - c : FDGPU_COPY_CHUNK;
+        memcpy(s->h_arena + off + c, arena + off + c, m);
+        if (hipMemcpyAsync(s->d_arena + off + c, s->h_arena + off + c, m, hipMemcpyHostToDevice, s->stream) !=
+            hipSuccess) { err[i] = 1; return; }
+      }
     });
   {
     std::lock_guard<std::mutex> lk(g_stage_mu);
