@@ -1396,7 +1396,7 @@ int64_t fdgpu_submit_frags_io(fdgpu_engine_t *e, fdgpu_frag_io_t const *fio, uin
      64-B chunks), every out frag inside out, the packed arena within
      max_arena, the signature bound within max_sig, every named link given.
 
-     DMA gather (the default, g_io_dma): the frags' payloads are grouped into
+     DMA gather (FDGPU_IO_DMA=1, g_io_dma): the frags' payloads are grouped into
      ranges of source bytes -- per registered region, a run of this batch's
      frags with gaps of at most FDGPU_IO_GAP (a round robin's other tiles'
      frags lie between this tile's) -- and each range is copied into the
@@ -1479,11 +1479,10 @@ int64_t fdgpu_submit_frags_io(fdgpu_engine_t *e, fdgpu_frag_io_t const *fio, uin
   if (bound > e->cfg.max_sig) { set_err("batch may exceed max_sig (%llu)", (unsigned long long)e->cfg.max_sig); return FDGPU_ERR_INVAL; }
   const uint64_t sp1 = g_sp_on ? sp_now() : 0;
   if (!slot_ws(*s, bound)) return FDGPU_ERR_DEVICE;
-  /* five kernels: gather (which also re-checks the in mcache lines, keeps
-     the records on the device and zeroes the verify queue counter and the
-     signature count), parse + expand, verify and its fallback, finish --
-     the out frags and the results written in place over the bus -- then the
-     completion word */
+  /* four kernels: ingest (gather, re-check of the in mcache lines, parse
+     and expand; it keeps the records on the device and zeroes the verify
+     queue counter), verify and its fallback, finish -- the out frags and
+     the results written in place over the bus -- then the completion word */
   uint8_t *out_dev = out_sz ? (uint8_t *)(ro->dbase + ((uintptr_t)out - ro->base)) : nullptr;
   uint8_t *arena = dma ? s->d_mirror : s->d_arena;
   if (n) {
