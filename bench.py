@@ -517,6 +517,11 @@ TILE_SPREAD = 2
 # (p99 5.1 ms; 32768: 90 M at p99 8.6-12 ms, 49152: 90 M at 10 ms; profiles/r05/tile_cfg3_cap.md)
 TILE_CFG3_SIG_MAX = 32768
 TILE_CFG3_SIG_MAX_BY_TILES = {1: 32768, 2: 24576}
+# the cfg3 capacity runs publish their 250 K-txn stream this many times over into each link (every
+# copy verified and published again: they are a stream apart, outside the tiles' 16-deep tcache),
+# ~100+ batches a run, so the pipeline's fill and drain do not weigh (150-250 K txns once: one tile
+# 69-74 M sig/s against 86 M over 1 M distinct txns; profiles/r05/tile_cfg3_cap.md)
+TILE_CFG3_PREFILL_REPS = 4
 TILE_RUNS_CFG3 = (  # the same tile over cfg3 frags (1-12 signatures, payloads up to the 1232-B MTU: SURVEY 8(d) cfg5)
     ("mux1_capacity_cfg3", 1, 1, -1.0),
     ("mux2_capacity_cfg3", 2, 2, -1.0),
@@ -558,7 +563,7 @@ def tile_cmd(rank, cpus, npz, out, runs=TILE_RUNS, multi=0, xproc=False):
            "--pair", str(TILE_PAIR), "--spread", str(TILE_SPREAD),
            "--payload-npz", npz, "--device-rank", str(rank), "--sweep", sweep, "--out", out]
     if multi:
-        cmd += ["--batch-sig-max", str(TILE_CFG3_SIG_MAX)]
+        cmd += ["--batch-sig-max", str(TILE_CFG3_SIG_MAX), "--prefill-reps", str(TILE_CFG3_PREFILL_REPS)]
     if xproc:
         cmd += ["--xproc", "1", "--pages", "4k", "--depth-lg", str(TILE_DEPTH_LG_PREFILL_XPROC)]
     if cpus:

@@ -73,6 +73,8 @@ def make_parser():
                          "instead of generating --txns")
     ap.add_argument("--depth-lg-paced", type=int, default=0,
                     help="log2 of the link depth for paced runs (rate > 0); 0: --depth-lg")
+    ap.add_argument("--prefill-reps", type=int, default=1,
+                    help="capacity runs (rate < 0): each link carries the frag stream this many times over")
     ap.add_argument("--paced-reps", type=int, default=1,
                     help="paced runs publish the frag stream this many times over (a long stream on a shallow "
                          "link: the producers can lap the tiles)")
@@ -343,8 +345,13 @@ def run_once_mux(args, ps, arena, offs, sizes, n_sig, modes, tiles_n, batch, inf
     # drain do not dominate the drain time of several tiles
     reps = 1
     if prefill:
+        # --prefill-reps R: each link's stream R times over (a small multi-signature set still gives a
+        # run of ~100 batches; a txn's copies are a whole stream apart, far outside the tcache window,
+        # so every copy is verified and published again)
         n = len(offs)
-        feeds = [(np.roll(offs, -(j * n // P)), np.roll(sizes, -(j * n // P))) for j in range(P)]
+        reps = max(1, getattr(args, "prefill_reps", 1))
+        feeds = [(np.tile(np.roll(offs, -(j * n // P)), reps), np.tile(np.roll(sizes, -(j * n // P)), reps))
+                 for j in range(P)]
     else:
         # paced: link j carries every P-th frag, the stream published paced_reps times over (a txn's
         # copies are len(ps) frags apart: far outside the tiles' 16-deep tcache window)
