@@ -558,7 +558,7 @@ def tile_cmd(rank, cpus, npz, out, runs=TILE_RUNS, multi=0, xproc=False):
     cmd = [sys.executable, os.path.join(REPO, "tools", "bench_tile.py"), "--mux", "1", "--gpu-parse", "2",
            "--multi", str(int(multi)), "--producers-same-as-tiles", "1", "--depth-lg", str(TILE_DEPTH_LG_PREFILL),
            "--depth-lg-paced", str(TILE_DEPTH_LG_PACED), "--paced-reps", str(TILE_PACED_REPS),
-           "--wait-us", "200", "--pin", "1", "--hw-queues", str(TILE_HW_QUEUES),
+           "--wait-us", "200", "--pin", "1", "--hw-queues", str(TILE_HW_QUEUES), "--warm-runs", "0" if xproc else "1",
            "--reps", str(TILE_REPS_XPROC if xproc else TILE_REPS),
            "--pair", str(TILE_PAIR), "--spread", str(TILE_SPREAD),
            "--payload-npz", npz, "--device-rank", str(rank), "--sweep", sweep, "--out", out]

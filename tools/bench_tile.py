@@ -73,6 +73,8 @@ def make_parser():
                          "instead of generating --txns")
     ap.add_argument("--depth-lg-paced", type=int, default=0,
                     help="log2 of the link depth for paced runs (rate > 0); 0: --depth-lg")
+    ap.add_argument("--warm-runs", type=int, default=0,
+                    help="untimed runs of the first sweep setting before the measured ones (in-process shapes)")
     ap.add_argument("--prefill-reps", type=int, default=1,
                     help="capacity runs (rate < 0): each link carries the frag stream this many times over")
     ap.add_argument("--paced-reps", type=int, default=1,
@@ -147,6 +149,21 @@ def main():
     ok = True
     lines = []
     prods0, sig_max0 = args.producers, args.batch_sig_max
+    # untimed warm-up runs of the first setting: the first run of a fresh process ran slow (two tiles
+    # at capacity 46 M against 69-70 M next, with the tiles' own counters equal: the time went outside
+    # them; one tile paced at 24 M lost 32 K frags there, none after)
+    for _ in range(max(0, args.warm_runs)):
+        run = runs[0]
+        args.producers = int(run[4]) if len(run) > 4 else int(run[0]) if args.producers_same_as_tiles else prods0
+        args.batch_sig_max = int(run[5]) if len(run) > 5 and run[5] > 0 else sig_max0
+        args.depth_lg = args.depth_lg_paced if run[3] > 0 and args.depth_lg_paced else depth_lg
+        if args.xproc:
+            break
+        if args.mux:
+            run_once_mux(args, ps, arena, offs, sizes, n_sig, modes, int(run[0]), int(run[1]), int(run[2]), run[3],
+                         cpus=cpus, device=args.device if args.device >= 0 else None)
+        else:
+            run_once(args, ps, arena, offs, sizes, n_sig, modes, int(run[0]), int(run[1]), int(run[2]), run[3])
     for run in runs:
         tiles_n, batch, inflight, rate = run[:4]
         # a fifth field sets the run's quic links (producers), a sixth its batches' signature cap
