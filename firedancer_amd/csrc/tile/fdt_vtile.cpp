@@ -584,6 +584,7 @@ struct fdgpu_dtile {
   std::vector<uint64_t> tcache_mem;
   void *tcache = nullptr;
   uint64_t rx_seq[16] = {};
+  uint64_t fseq_pub[16] = {};          /* what the tile last stored into each in link's fseq */
   uint64_t out_seq = 0, out_chunk = 0;
   uint32_t next_in = 0;
   fdgpu_dtile_stats_t st{};
@@ -601,7 +602,7 @@ fdgpu_dtile_t *fdgpu_dtile_new(const fdgpu_dtile_cfg_t *cfg) {
   if (!fp) { delete t; return nullptr; }
   t->tcache_mem.assign(fp / 8, 0);
   t->tcache = fdt_tcache_new(t->tcache_mem.data(), cfg->tcache_depth, cfg->tcache_map_cnt);
-  for (uint32_t i = 0; i < cfg->in_cnt; i++) t->rx_seq[i] = cfg->in_seq0[i];
+  for (uint32_t i = 0; i < cfg->in_cnt; i++) t->rx_seq[i] = t->fseq_pub[i] = cfg->in_seq0[i];
   t->out_seq = cfg->out_seq0;
   t->out_chunk = cfg->out_chunk0;
   return t;
@@ -614,6 +615,7 @@ void fdgpu_dtile_delete(fdgpu_dtile_t *t) { delete t; }
 int64_t fdgpu_dtile_step(fdgpu_dtile_t *t) {
   const fdgpu_dtile_cfg_t &c = t->cfg;
   int64_t n = 0;
+  uint32_t tspub = 0;
   for (uint32_t k = 0; k < c.in_cnt; k++) {
     const uint32_t i = (t->next_in + k) % c.in_cnt;
     fdt_frag_meta_t m;
@@ -650,12 +652,19 @@ int64_t fdgpu_dtile_step(fdgpu_dtile_t *t) {
     if ((uint64_t)txn->signature_off + 64 > sz) { t->st.corrupt++; continue; }
     const uint64_t tag = fdt_hash(c.hashmap_seed, dst + txn->signature_off, 64);
     if (fdt_tcache_insert(t->tcache, tag)) { t->st.dup++; continue; }
-    fdt_mcache_publish(c.out_mcache, c.out_depth, t->out_seq, 0, t->out_chunk, sz, m.ctl, m.tsorig,
-                       (uint32_t)now_ns());
+    if (!tspub) tspub = (uint32_t)now_ns() | 1u;            /* one clock read per pass, not per frag */
+    fdt_mcache_publish(c.out_mcache, c.out_depth, t->out_seq, 0, t->out_chunk, sz, m.ctl, m.tsorig, tspub);
     t->out_seq++;
     t->out_chunk = fdt_dcache_compact_next(t->out_chunk, sz, c.out_chunk0, c.out_wmark);
     t->st.published++;
   }
+  /* reliable links: every frag this pass took is copied out, so its line
+     and chunk may be reused -- publish the progress (fd_fseq_update) */
+  for (uint32_t i = 0; i < c.in_cnt; i++)
+    if (c.in_fseq[i] && t->fseq_pub[i] != t->rx_seq[i]) {   /* (an unchanged value is not re-stored: the line is shared) */
+      __atomic_store_n(c.in_fseq[i], t->rx_seq[i], __ATOMIC_RELEASE);
+      t->fseq_pub[i] = t->rx_seq[i];
+    }
   t->next_in = (t->next_in + 1) % c.in_cnt;
   return n;
 }

@@ -27,12 +27,14 @@ def main(argv=None):
     ap.add_argument("--ready-file", default="", help="created once the sandboxed child runs")
     ap.add_argument("--cpu", type=int, default=-1, help="pin the tile to this CPU")
     ap.add_argument("--result", default="")
+    ap.add_argument("--reliable", type=int, default=0,
+                    help="1: write the tile's progress into each in link's fseq (its producers wait for it)")
     a = ap.parse_args(argv)
     if a.cpu >= 0:
         os.sched_setaffinity(0, {a.cpu})                 # the forked child keeps it
     ins = [tile.Link.shm_join(p) for p in a.in_paths]
     out = tile.Link.shm_join(a.out)
-    dt = tile.DedupTile(ins, out, hashmap_seed=a.seed, tcache_depth=a.tcache_depth)
+    dt = tile.DedupTile(ins, out, hashmap_seed=a.seed, tcache_depth=a.tcache_depth, reliable=bool(a.reliable))
     pid, stats = dt.fork_sandboxed(a.frags, idle_s=a.idle_s)
     if a.ready_file:
         open(a.ready_file, "w").close()

@@ -236,6 +236,9 @@ def main(argv=None, make_verifiers=gpu_verifiers):
     ap.add_argument("--log", default="", help="write every frag's outcome (seq, code per tile) to this .npz")
     ap.add_argument("--timeout", type=float, default=120.0)
     ap.add_argument("--idle-ms", type=float, default=20.0)
+    ap.add_argument("--out-flow-control", type=int, default=0,
+                    help="1: each tile takes its out link's credits from the link's fseq -- a reliable consumer "
+                         "(the dedup process, dedup_proc --reliable 1) holds the tile back instead of being lapped")
     a = ap.parse_args(argv)
     cnts = [int(x) for x in a.frags.split(",")]
     if len(cnts) == 1 and len(a.in_paths) > 1:
@@ -250,7 +253,7 @@ def main(argv=None, make_verifiers=gpu_verifiers):
                     cpus=[int(x) for x in a.cpus.split(",") if x] or None, ready_file=a.ready_file or None,
                     log_max=(sum(cnts) + 16) if a.log else 0, hashmap_seed=a.seed, batch_txn_max=a.batch,
                     inflight_max=a.inflight, batch_wait_us=a.wait_us, batch_sig_max=a.batch_sig_max,
-                    gpu_parse=a.gpu_parse, **guard)
+                    gpu_parse=a.gpu_parse, flow_control=bool(a.out_flow_control), **guard)
     finally:
         close()
     res.update(info)

@@ -129,7 +129,7 @@ class DTileCfg(c.Structure):
                 ("in_wmark", c.c_uint64 * 16), ("unparsed_in_cnt", c.c_uint32),
                 ("out_mcache", vp), ("out_depth", c.c_uint64), ("out_seq0", c.c_uint64), ("out_base", vp),
                 ("out_chunk0", c.c_uint64), ("out_wmark", c.c_uint64), ("hashmap_seed", c.c_uint64),
-                ("tcache_depth", c.c_uint64), ("tcache_map_cnt", c.c_uint64)]
+                ("tcache_depth", c.c_uint64), ("tcache_map_cnt", c.c_uint64), ("in_fseq", vp * 16)]
 
 
 class DTileStats(c.Structure):
@@ -1233,13 +1233,18 @@ class DedupTile:
     """The dedup tile (fd_dedup.c) over one or more verify outputs."""
 
     def __init__(self, in_links, out_link, hashmap_seed=0xDED0, tcache_depth=4194302, tcache_map_cnt=0,
-                 unparsed_in_cnt=0):
+                 unparsed_in_cnt=0, reliable=False):
+        """reliable: the tile writes its progress into each in link's fseq (the
+        producer -- a verify tile with flow_control -- waits for it) instead of
+        being lapped when it falls behind."""
         L = lib()
         cfg = DTileCfg()
         cfg.in_cnt = len(in_links)
         for i, lk in enumerate(in_links):
             cfg.in_mcache[i], cfg.in_depth[i], cfg.in_seq0[i] = lk.mcache_ptr, lk.depth, lk.seq0
             cfg.in_base[i], cfg.in_chunk0[i], cfg.in_wmark[i] = lk.base_ptr, lk.chunk0, lk.wmark
+            if reliable:
+                cfg.in_fseq[i] = lk.fseq.ctypes.data
         cfg.unparsed_in_cnt = unparsed_in_cnt
         cfg.out_mcache, cfg.out_depth, cfg.out_seq0 = out_link.mcache_ptr, out_link.depth, out_link.seq0
         cfg.out_base, cfg.out_chunk0, cfg.out_wmark = out_link.base_ptr, out_link.chunk0, out_link.wmark

@@ -613,6 +613,12 @@ typedef struct {
   uint64_t                hashmap_seed;
   uint64_t                tcache_depth;     /* reference default 4194302 (default.toml:910) */
   uint64_t                tcache_map_cnt;   /* 0: default */
+  /* in link i's consumer fseq (NULL: none): the tile stores its next seq of
+     link i there as it consumes (fd_fseq_update, the reliable verify -> dedup
+     link of fd_topo: the verify tile's mux takes its credits from it,
+     fd_mux.c:548), so a dedup tile that falls behind holds its producers
+     back instead of being lapped */
+  uint64_t *              in_fseq[ 16 ];
 } fdgpu_dtile_cfg_t;
 
 typedef struct {

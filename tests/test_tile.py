@@ -560,6 +560,30 @@ def test_dedup_tile_two_verify_tiles(oracle):
     assert st["dup"] > 0
 
 
+def test_dedup_tile_reliable_links_publish_progress(oracle):
+    """reliable=True (the verify -> dedup links of fd_topo): the dedup tile
+    stores its next seq of each in link into that link's fseq as it consumes
+    -- what a flow-controlled verify tile takes its credits from -- and a
+    tile without it leaves the fseqs alone."""
+    ps = _mixed_stream(300, seed=22)
+    inl = tile.Link(1 << 10, 1232)
+    outs = [tile.Link(1 << 10, tile.TPU_DCACHE_MTU) for _ in range(2)]
+    vts = [tile.VerifyTile(inl, outs[k], tile.PyVerifier(oracle_fn(oracle)), hashmap_seed=100 + k,
+                           batch_txn_max=50, round_robin_idx=k, round_robin_cnt=2) for k in range(2)]
+    for p in ps:
+        inl.publish(p)
+    for vt in vts:
+        vt.run(len(ps), timeout_s=30)
+    pub = [int(vt.stats()["published"]) for vt in vts]
+    f0 = [int(o.fseq[0]) for o in outs]
+    unrel = tile.DedupTile(outs, tile.Link(1 << 10, tile.TPU_DCACHE_MTU), tcache_depth=1 << 12)
+    unrel.run_until_idle()
+    assert [int(o.fseq[0]) for o in outs] == f0
+    rel = tile.DedupTile(outs, tile.Link(1 << 10, tile.TPU_DCACHE_MTU), tcache_depth=1 << 12, reliable=True)
+    assert rel.run_until_idle() == sum(pub)
+    assert [int(o.fseq[0]) for o in outs] == [o.seq0 + n for o, n in zip(outs, pub)]
+
+
 def test_dedup_tile_unparsed_link(oracle, fixtures):
     """A gossip-style link of raw txns is parsed by the dedup tile itself
     (fd_dedup.c:147-192) and produces the verify tile's trailer format."""

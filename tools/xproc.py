@@ -97,6 +97,8 @@ def run(npz, n_payloads, tiles=1, producers=1, mode="paced", rate=0.0, reps=1, d
                    "--hw-queues", str(hw_queues), "--ready-file", ready, "--timeout", str(timeout)]
         if tcpu:
             eng_cmd += ["--cpus", ",".join(map(str, tcpu))]
+        if dedup:                            # verify -> dedup links are reliable (fd_topo): credits from the dedup's fseq
+            eng_cmd += ["--out-flow-control", "1"]
         if log:
             eng_cmd += ["--log", os.path.join(d, "log.npz")]
         feed_cmd = [sys.executable, os.path.join(REPO, "tools", "quic_feed.py"), *sum([["--link", p] for p in qv], []),
@@ -113,7 +115,7 @@ def run(npz, n_payloads, tiles=1, producers=1, mode="paced", rate=0.0, reps=1, d
         dd = None
         if dedup:
             dd_cmd = [sys.executable, "-m", "firedancer_amd.dedup_proc", *sum([["--in", p] for p in vd], []),
-                      "--out", dp, "--frags", str(dedup_frags or (1 << 62)), "--idle-s", "3"]
+                      "--out", dp, "--frags", str(dedup_frags or (1 << 62)), "--idle-s", "3", "--reliable", "1"]
             if len(cpus) > P + T:
                 dd_cmd += ["--cpu", str(cpus[P + T])]
             dd = subprocess.Popen(dd_cmd, **popen)
