@@ -624,6 +624,19 @@ int64_t fdgpu_dtile_step(fdgpu_dtile_t *t) {
     if (rc == 0) continue;
     if (rc < 0) { t->st.overrun += found - t->rx_seq[i]; t->rx_seq[i] = found; continue; }
     const uint64_t seq = t->rx_seq[i]++;
+    {
+      /* the frag 4 seqs on, if out already: its payload into the cache now
+         (the copy below is latency-bound on payloads the GPU wrote to host
+         memory), and the line 8 on */
+      const uint64_t mask = c.in_depth[i] - 1;
+      const fdt_frag_meta_t *nl = c.in_mcache[i] + ((seq + 4) & mask);
+      if (__atomic_load_n(&nl->seq, __ATOMIC_RELAXED) == seq + 4 && nl->chunk <= c.in_wmark[i]) {
+        const uint8_t *np = c.in_base[i] + ((uint64_t)nl->chunk << FDT_CHUNK_LG_SZ);
+        const uint32_t nsz = nl->sz < FDT_TPU_DCACHE_MTU ? nl->sz : FDT_TPU_DCACHE_MTU;
+        for (uint32_t o = 0; o < nsz; o += 64) __builtin_prefetch(np + o);
+      }
+      __builtin_prefetch(c.in_mcache[i] + ((seq + 8) & mask));
+    }
     t->st.in_frags++;
     n++;
     if (m.chunk < c.in_chunk0[i] || m.chunk > c.in_wmark[i] || m.sz > FDT_TPU_DCACHE_MTU) { t->st.corrupt++; continue; }
