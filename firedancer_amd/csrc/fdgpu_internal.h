@@ -29,7 +29,9 @@ typedef struct {
 #define FDGPU_ARENA_SLACK   160u          /* readable bytes past the arena (SHA block loads) */
 /* k in signed radix 16: 64 windows over the per-lane table {O, -A, .., -8A} */
 #define FDGPU_ATAB_ENTRIES  9u            /* 0 (identity), 1A .. 8A (A negated) */
-#define FDGPU_ATAB_WORDS    40u           /* u32 per cached entry */
+#ifndef FDGPU_ATAB_WORDS
+#define FDGPU_ATAB_WORDS    40u           /* u32 per cached entry (a diagnostic build may pad it) */
+#endif
 /* Fixed-base comb for [S]B: S in signed radix 2^W, digit i looked up in
    table i = {0, 1, .., 2^(W-1)} x 2^(W i) B (affine niels, one 128-B line per
    entry), so [S]B costs NDIG mixed additions and no doublings.  Tables live

@@ -414,9 +414,27 @@ FDG_DEV void hs_wscalar(uint32_t (&w)[8], const uint32_t (&v)[5], bool v_neg, co
 typedef __attribute__((address_space(3))) void lds_void_t;
 
 FDG_DEV void stage_entry(uint32_t *lds_wave, const uint32_t *tab, int e) {
+#if FDGPU_DIAG_TAB_HOT
+  /* diagnostic only (wrong codes): every lane stages entry 1 of its wave's
+     first lane's table, so the chain's table reads are L2 hits -- the same
+     VALU and LDS work with the HBM read traffic gone (DESIGN §4 traffic) */
+  (void)e;
+  const uint64_t p = (uint64_t)(tab + FDGPU_ATAB_WORDS);
+  const uint32_t *src = (const uint32_t *)(((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(p >> 32)) << 32) |
+                                           (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)p));
+#else
   const uint32_t *src = tab + (uint32_t)(e < 0 ? -e : e) * FDGPU_ATAB_WORDS;
+#endif
+#if FDGPU_DIAG_LINE8
+  /* diagnostic only (wrong codes; with FDGPU_ATAB_WORDS=64): the chain
+     stages 128 B of each 256-B-aligned entry, one cache line instead of the
+     two a 160-B entry spans -- the traffic of a packed 128-B entry */
+  constexpr int NCH = 8;
+#else
+  constexpr int NCH = 10;
+#endif
 #pragma unroll
-  for (int c = 0; c < 10; c++)
+  for (int c = 0; c < NCH; c++)
     __builtin_amdgcn_global_load_lds((const void *)(src + 4 * c), (lds_void_t *)(lds_wave + 256 * c), 16, 0, 0);
 }
 
