@@ -727,6 +727,10 @@ int64_t expand_par(uint64_t arena_sz, const fdgpu_txn_t *txns, uint64_t txn_cnt,
 static int64_t submit_slot(fdgpu_engine_t *e, Slot *s, uint64_t arena_sz, fdgpu_txn_t const *txns, uint64_t txn_cnt,
                            uint64_t uploaded = 0, const uint8_t *src = nullptr, uint64_t t_stage = 0) {
   uint32_t *perm = bucket(e) ? s->h_perm : nullptr;
+  /* a registered arena's DMA is queued first, so it runs under the
+     descriptor expansion (an arena expand() rejects leaves the slot free; the
+     next batch's copies, later on the same stream, overwrite it) */
+  if (src && arena_sz) HIPCHK(hipMemcpyAsync(s->d_arena, src, arena_sz, hipMemcpyHostToDevice, s->stream), FDGPU_ERR_DEVICE);
   const uint64_t t0 = sp_now();
   const int64_t ns = expand_par(arena_sz, txns, txn_cnt, e->cfg.max_sig, s->h_sigs, s->h_txns, perm);
   if (ns < 0) return FDGPU_ERR_INVAL;
@@ -742,8 +746,13 @@ static int64_t submit_slot(fdgpu_engine_t *e, Slot *s, uint64_t arena_sz, fdgpu_
   } rec{t_stage, t0, t1};
   if (!slot_ws(*s, (uint64_t)ns)) return FDGPU_ERR_DEVICE;
   if (src) {
-    if (arena_sz) HIPCHK(hipMemcpyAsync(s->d_arena, src, arena_sz, hipMemcpyHostToDevice, s->stream), FDGPU_ERR_DEVICE);
-    HIPCHK(hipMemsetAsync(s->d_arena + arena_sz, 0, FDGPU_ARENA_SLACK, s->stream), FDGPU_ERR_DEVICE);
+    /* the slack past a registered arena is left as it is: the SHA block
+       loads mask every byte past the message (msg_block), so only its
+       presence matters.  Zeroing it on the device cost a kernel (a fill, or
+       the blit of a small copy) queued behind the upload, which waits for a
+       CU slot the running verify holds -- the batch's descriptor copies and
+       verify waited behind it, ~7 ms a 1 M batch
+       (profiles/r05/host_fed/registered_slack.md) */
   } else {
     memset(s->h_arena + arena_sz, 0, FDGPU_ARENA_SLACK);
     const size_t asz = arena_sz + FDGPU_ARENA_SLACK - uploaded;
