@@ -179,6 +179,28 @@ def test_stamps_variant_codes(tmp_path):
     assert r.returncode == 0 and "ok" in r.stdout, r.stdout[-2000:] + r.stderr[-2000:]
 
 
+def test_registered_arena_slack_left_unwritten(oracle):
+    """A registered arena is DMA'd as it is and the slack past it on the
+    device is not zeroed (fdgpu_engine.cpp submit_slot): the SHA block loads
+    mask every byte past the message.  The slot's device arena first holds a
+    longer batch of 0xA5 bytes, then a registered arena that ends exactly at
+    its last message's last byte: every code equals the oracle's."""
+    a, t, _ = workload.cfg1(3000, seed=0x51AC)
+    end = int(max((t["msg_off"] + t["msg_sz"]).max(), (t["sig_off"] + 64).max(), (t["pub_off"] + 32).max()))
+    eng = fa.VerifyEngine(0, max_txn=4096, max_arena=a.nbytes + 8192, ring_depth=1)
+    junk = np.full(a.nbytes + 4096, 0xA5, dtype=np.uint8)
+    reg = np.full(end + 4096, 0x5A, dtype=np.uint8)
+    reg[:end] = a[:end]
+    eng.host_register(reg)
+    try:
+        eng.poll(eng.submit(junk, t), blocking=True)                       # garbage past `end` on the device
+        got = eng.poll(eng.submit(reg[:end], t), blocking=True)
+        assert (got == oracle.verify_txns(a, t, nthreads=8)).all()
+    finally:
+        eng.host_unregister(reg)
+        eng.close()
+
+
 def test_big_ring_batches_on_shared_verify_streams(oracle):
     """Ring batches of >= FDGPU_BIG_SIGS (262,144) signatures verify on the
     engine's two big-batch streams in turn (each after its own uploads; its

@@ -1,0 +1,14 @@
+# Cache-policy A/B of the chain tables: nt stores (ntst), nt table loads (ldslc), both; + the slack test
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+O=gpurun_out/r05nt; mkdir -p $O
+export TMPDIR=/tmp
+timeout -k 10 300 python -u -m pytest -x -q --timeout 240 --timeout-method thread -m gpu tests/test_gpu_engine.py -k "slack or big_ring" > $O/tests.log 2>&1 || { echo TESTS_FAILED; tail -20 $O/tests.log; exit 1; }
+tail -1 $O/tests.log
+for i in 1 2; do for v in "base::firedancer_amd/libfd_ed25519_gpu.so" "ntst::build/ntst/libfd_ed25519_gpu.so" "ldslc::build/ldslc/libfd_ed25519_gpu.so" "both::build/both/libfd_ed25519_gpu.so"; do
+  tag=${v%%::*}; lib=${v#*::}
+  FDGPU_LIB=$lib timeout -k 10 120 python3 bench.py --no-extras --steps 30 --warmup 5 > $O/time_${tag}_$i.json 2>$O/time_${tag}_$i.err || { echo TIME_FAILED $tag; tail $O/time_${tag}_$i.err; exit 1; }
+  python3 -c "
+import json
+b=json.loads(open('$O/time_${tag}_$i.json').read().strip().splitlines()[-1]); print('$tag', $i, b['value'], b['ms_per_step'], b.get('parity_mismatches'))"
+done; done
