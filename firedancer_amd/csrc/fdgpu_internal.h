@@ -45,11 +45,14 @@ typedef struct {
 /* The verify equation with half-size scalars (fdgpu_lattice.h).  Per-lane
    workspace entries (cached form, 40 words each): */
 #define HS_MAX_WIN          40u           /* radix-16 windows of |u|, |v| (< 2^159) */
-                                          /* entries 0..8: the -A table */
-#define FDGPU_WS_RTAB       FDGPU_ATAB_ENTRIES          /* entries 9..17: the -R table */
-#define FDGPU_WS_PARK       (2u * FDGPU_ATAB_ENTRIES)   /* entry: k digits, decoded R, code (full path) */
+/* A table's identity entry (digit 0) is one shared constant (g_tab_ident),
+   so a lane stores entries 1..8 of each table */
+#define FDGPU_TAB_STORED    (FDGPU_ATAB_ENTRIES - 1u)
+                                          /* entries 0..7: 1..8 of the -A table */
+#define FDGPU_WS_RTAB       FDGPU_TAB_STORED            /* entries 8..15: 1..8 of the -R table */
+#define FDGPU_WS_PARK       (2u * FDGPU_TAB_STORED)     /* entry: k digits, decoded R, code (full path) */
 #define FDGPU_WS_SB         (FDGPU_WS_PARK + 1u)        /* entry: [w]B (or [S]B) in cached form */
-#define FDGPU_WS_ENTRIES    (FDGPU_WS_SB + 1u)          /* 20 entries: 3200 B per signature */
+#define FDGPU_WS_ENTRIES    (FDGPU_WS_SB + 1u)          /* 18 entries: 2880 B per signature */
 #define FDGPU_WS_LANE_WORDS (FDGPU_WS_ENTRIES * FDGPU_ATAB_WORDS)
 #define FDGPU_BLOCK         256u
 #define FDGPU_FLAG_REF_MAP  1u            /* portable-backend error mapping */

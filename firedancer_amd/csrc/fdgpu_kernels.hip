@@ -153,9 +153,29 @@ __global__ void __launch_bounds__(64) fdgpu_bcomb_fill_kernel(const uint32_t *ba
    per-lane 8-B offset of two ds_read_b64 (unstage_entry_signed) instead of
    20 per-word selects.  atab_store / atab_load convert, so every other
    reader sees the canonical order (Y+X, Y-X, 2Z, 2dT). */
-FDG_DEV constexpr int atab_pos(int w) {
+__host__ __device__ constexpr int atab_pos(int w) {
   return w >= 20 ? w : w < 10 ? 4 * (w / 2) + (w % 2) : 4 * ((w - 10) / 2) + 2 + (w % 2);
 }
+
+/* A table's entry 0 -- the identity in cached form (Y+X = Y-X = 1, 2Z = 2,
+   2dT = 0) in the stored word order -- is this one constant for every lane
+   and table: digit-0 lookups read it (an L2 hit), and a lane's workspace
+   holds only entries 1..8 of its tables (2880 B per signature instead of
+   3200, a smaller footprint in the caches the table reads hit). */
+struct alignas(16) tab_ident_t { uint32_t w[FDGPU_ATAB_WORDS]; };
+__device__ const tab_ident_t g_tab_ident = {{1u, 0u, 1u, 0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u, 2u}};
+static_assert(atab_pos(0) == 0 && atab_pos(10) == 2 && atab_pos(20) == 20, "identity entry's stored order");
+
+/* Entry |e| of a table whose (virtual) base is `tab` (entry k at tab + 40 k
+   for k >= 1; see tab_a / tab_r): the shared identity for e == 0. */
+FDG_DEV const uint32_t *tab_entry(const uint32_t *tab, int e) {
+  return e ? tab + (uint32_t)(e < 0 ? -e : e) * FDGPU_ATAB_WORDS : g_tab_ident.w;
+}
+/* virtual bases of a lane's -A and -R tables: stored entry 1 sits at the
+   table's first workspace entry */
+FDG_DEV uint32_t *tab_a(uint32_t *wsl) { return wsl - FDGPU_ATAB_WORDS; }
+FDG_DEV const uint32_t *tab_a(const uint32_t *wsl) { return wsl - FDGPU_ATAB_WORDS; }
+FDG_DEV uint32_t *tab_r(uint32_t *wsl) { return wsl + (FDGPU_WS_RTAB - 1u) * FDGPU_ATAB_WORDS; }
 
 FDG_DEV void atab_store(uint32_t *wsl, uint32_t entry, const ge_cached &c) {
   uint4 *p = (uint4 *)(wsl + entry * FDGPU_ATAB_WORDS);
@@ -180,7 +200,7 @@ FDG_DEV int sext4(uint32_t x) { return ((int)(x << 28)) >> 28; }
 #define KD_WORDS 8        /* 64 signed radix-16 digits of k, one per nibble */
 
 FDG_DEV void atab_load(uint32_t (&q)[40], const uint32_t *wsl, int e) {
-  const uint4 *ent = (const uint4 *)(wsl + (uint32_t)(e < 0 ? -e : e) * FDGPU_ATAB_WORDS);
+  const uint4 *ent = (const uint4 *)tab_entry(wsl, e);
   uint32_t o[40];
 #pragma unroll
   for (int i = 0; i < 10; i++) {
@@ -204,7 +224,7 @@ FDG_DEV void shl4(uint32_t (&w)[8]) {
    window's sum is converted to p3 and the parked [S]B added. */
 FDG_DEV void dsm_k(ge_p2 &acc2, uint32_t (&kd)[KD_WORDS], const uint32_t *wsl, uint32_t sb_entry = FDGPU_WS_SB,
                    const uint32_t *ta = nullptr) {
-  if (!ta) ta = wsl;                      /* the -A table: own workspace, or the key cache's */
+  if (!ta) ta = tab_a(wsl);               /* the -A table: own workspace, or the key cache's */
   ge_p3 acc3;
   ge_p1p1 t;
   uint32_t q[40];
@@ -292,13 +312,12 @@ FDG_DEV void comb_sb(ge_p3 &acc, const uint32_t (&S)[8], const uint32_t *__restr
   }
 }
 
-/* Build this lane's table {O, -A, -2A, ..., -8A} (cached form) in the
-   workspace.  Even multiples by doubling the stored half (4S + 4M) instead
+/* Build this lane's table {-A, -2A, ..., -8A} (cached form; O is the
+   shared g_tab_ident) in the workspace.  Even multiples by doubling the stored half (4S + 4M) instead
    of adding -A (8M): 3 = 2 + 1, 4 = 2*2, 5 = 4 + 1, 6 = 2*3, 7 = 6 + 1,
    8 = 2*4. */
-FDG_DEV void atab_build(uint32_t *wsl, const ge_p3 &An) {
+FDG_DEV void atab_build(uint32_t *wsl, const ge_p3 &An) {   /* wsl: the table's virtual base (tab_a / tab_r) */
   ge_cached c;
-  ge_cached_0(c); atab_store(wsl, 0, c);
   ge_p3_to_cached(c, An); atab_store(wsl, 1, c);
   ge_p1p1 t; ge_p2 a2; ge_p3 P;
   ge_p3_to_p2(a2, An); ge_dbl(t, a2); ge_p1p1_to_p3(P, t);          /* 2(-A) */
@@ -427,11 +446,11 @@ FDG_DEV void stage_entry(uint32_t *lds_wave, const uint32_t *tab, int e) {
      first lane's table, so the chain's table reads are L2 hits -- the same
      VALU and LDS work with the HBM read traffic gone (DESIGN §4 traffic) */
   (void)e;
-  const uint64_t p = (uint64_t)(tab + FDGPU_ATAB_WORDS);
+  const uint64_t p = (uint64_t)tab_entry(tab, 1);
   const uint32_t *src = (const uint32_t *)(((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(p >> 32)) << 32) |
                                            (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)p));
 #else
-  const uint32_t *src = tab + (uint32_t)(e < 0 ? -e : e) * FDGPU_ATAB_WORDS;
+  const uint32_t *src = tab_entry(tab, e);
 #endif
 #if FDGPU_DIAG_LINE8
   /* diagnostic only (wrong codes; with FDGPU_ATAB_WORDS=64): the chain
@@ -474,7 +493,7 @@ FDG_DEV void unstage_entry_signed(uint32_t (&q)[40], const uint32_t *lds_wave, b
    hold -A, -R).  Leaves the completed sum of the last addition in t. */
 FDG_DEV void hs_chain(ge_p1p1 &t, uint32_t (&ud)[5], uint32_t (&vd)[5], bool u_neg, bool v_neg, uint32_t nwin,
                       const uint32_t *wsl, const uint32_t *ta) {
-  const uint32_t *tr = wsl + FDGPU_WS_RTAB * FDGPU_ATAB_WORDS;
+  const uint32_t *tr = tab_r(const_cast<uint32_t *>(wsl));
   __shared__ uint32_t s_stage[FDGPU_BLOCK / 64][2][10 * 256];
   uint32_t *st_r = &s_stage[threadIdx.x >> 6][0][0];
   uint32_t *st_a = &s_stage[threadIdx.x >> 6][1][0];
@@ -538,7 +557,7 @@ FDG_DEV void verify_hs_body(const uint8_t *__restrict__ arena, const fdgpu_sig_d
   for (int off = 32; off > 0; off >>= 1) nb = max(nb, (uint32_t)__shfl_xor((int)nb, off));
   uint32_t *wsl = lane_ws(ws, i);
   uint32_t *park = wsl + FDGPU_WS_PARK * FDGPU_ATAB_WORDS;
-  const uint32_t *ta = wsl;                    /* this lane's -A table */
+  const uint32_t *ta = tab_a(wsl);             /* this lane's -A table */
   FDGPU_STAMP(0);
   uint32_t Renc[8], Aenc[8];
   load32(Renc, arena + d.sig_off);
@@ -573,12 +592,12 @@ FDG_DEV void verify_hs_body(const uint8_t *__restrict__ arena, const fdgpu_sig_d
       const uint32_t di = active ? i : n_sig - 1u, r = key_of[di], vd = kverd[r];
       a_ok = (vd & 1u) != 0;
       a_small = (vd & 2u) != 0;
-      ta = lane_ws(ws, r);
+      ta = tab_a(lane_ws(ws, r));
     } else {
       a_ok = ge_decode(P, Aenc, ref_map);
       a_small = ge_is_small_order_affine(P);
       ge_p3_neg(Pn, P);
-      atab_build(wsl, Pn);
+      atab_build(tab_a(wsl), Pn);
     }
     FDGPU_STAMP(3);
     const bool r_ok = ge_decode(P, Renc, ref_map);
@@ -586,7 +605,7 @@ FDG_DEV void verify_hs_body(const uint8_t *__restrict__ arena, const fdgpu_sig_d
 #pragma unroll
     for (int j = 0; j < 10; j++) { park[HPARK_XR + j] = P.X.v[j]; park[HPARK_YR + j] = P.Y.v[j]; }
     ge_p3_neg(Pn, P);
-    atab_build(wsl + FDGPU_WS_RTAB * FDGPU_ATAB_WORDS, Pn);
+    atab_build(tab_r(wsl), Pn);
     if (code == 0 && !a_ok) code = ref_map ? -2 : -1;
     if (code == 0 && !r_ok) code = -1;
     if (code == 0 && a_small) code = -2;                 /* fd_ed25519_user.c:194-199 */
@@ -797,7 +816,7 @@ fdgpu_verify_pair_kernel(const uint8_t *__restrict__ arena, const fdgpu_sig_desc
       for (int j = 0; j < 10; j++) { park[HPARK_XR + j] = P.X.v[j]; park[HPARK_YR + j] = P.Y.v[j]; }
     }
     ge_p3_neg(Pn, P);
-    atab_build(wsl + (rl ? FDGPU_WS_RTAB * FDGPU_ATAB_WORDS : 0u), Pn);
+    atab_build(rl ? tab_r(wsl) : tab_a(wsl), Pn);
     /* both verdicts in both lanes, in decode2's order (A first) */
     const uint32_t mine = (ok ? 1u : 0u) | (small ? 2u : 0u);
     const uint32_t other = (uint32_t)__shfl_xor((int)mine, 1);
@@ -858,7 +877,7 @@ fdgpu_verify_pair_kernel(const uint8_t *__restrict__ arena, const fdgpu_sig_desc
 #pragma unroll 1
     for (uint32_t s2 = nwin; s2 < 40; s2++) shl4_5(dd);
     ge_p1p1 t;
-    hs_chain1(t, dd, rl ? hs.v_neg : hs.u_neg, nwin, wsl + (rl ? FDGPU_WS_RTAB * FDGPU_ATAB_WORDS : 0u));
+    hs_chain1(t, dd, rl ? hs.v_neg : hs.u_neg, nwin, rl ? tab_r(wsl) : tab_a(wsl));
     /* exchange the halves and add: both lanes hold [u](-A) + [v](-R) */
     ge_p3 mine, other;
     ge_p1p1_to_p3(mine, t);
@@ -997,7 +1016,7 @@ fdgpu_key_table_kernel(const uint8_t *__restrict__ arena, const fdgpu_sig_desc_t
   const bool a_ok = ge_decode(P, Aenc, (flags & FDGPU_FLAG_REF_MAP) != 0);
   const bool a_small = ge_is_small_order_affine(P);
   ge_p3_neg(Pn, P);
-  atab_build(lane_ws(ws, i), Pn);
+  atab_build(tab_a(lane_ws(ws, i)), Pn);
   kverd[i] = (a_ok ? 1u : 0u) | (a_small ? 2u : 0u);
 }
 
@@ -1021,7 +1040,7 @@ FDG_DEV void full_body(uint32_t *__restrict__ ws, const uint32_t *__restrict__ p
 #pragma unroll
     for (int j = 0; j < KD_WORDS; j++) kd[j] = park[HPARK_KD + j];
     ge_p2 Rc;
-    dsm_k(Rc, kd, wsl, FDGPU_WS_SB, key_of ? lane_ws(ws, key_of[i]) : wsl);
+    dsm_k(Rc, kd, wsl, FDGPU_WS_SB, tab_a(key_of ? lane_ws(ws, key_of[i]) : wsl));
     fe x, y, l;
 #pragma unroll
     for (int j = 0; j < 10; j++) { x.v[j] = park[HPARK_XR + j]; y.v[j] = park[HPARK_YR + j]; }
