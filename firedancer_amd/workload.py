@@ -100,18 +100,35 @@ def _cpu_busy_ticks():
     return out
 
 
+def _smt_siblings(cpu):
+    """The logical CPUs sharing `cpu`'s physical core (itself included)."""
+    try:
+        txt = open(f"/sys/devices/system/cpu/cpu{cpu}/topology/thread_siblings_list").read().strip()
+    except OSError:
+        return [cpu]
+    out = []
+    for part in txt.split(","):
+        lo, _, hi = part.partition("-")
+        out.extend(range(int(lo), int(hi or lo) + 1))
+    return out or [cpu]
+
+
 def idle_first(cpus, sample_s=0.2):
     """`cpus` reordered least busy first over a short sample of /proc/stat
     (ties keep their order).  On a box whose cores other tenants share, a
     pinned tile or producer thread on a busy core runs at a fraction of its
-    speed; the benches pin to the quietest cores they may use."""
+    speed; the benches pin to the quietest cores they may use.  A core's
+    busy time counts all of its SMT siblings: another tenant on the sibling
+    hyperthread shares the core (one tile at ~0.7 of its rate in alternating
+    runs on such a box, profiles/r05/tab_traffic/tcap3_*)."""
     import time
     a = _cpu_busy_ticks()
     time.sleep(sample_s)
     b = _cpu_busy_ticks()
     if not a or not b:
         return list(cpus)
-    return sorted(cpus, key=lambda c: (b.get(c, 0) - a.get(c, 0), cpus.index(c)))
+    core = {c: sum(b.get(s, 0) - a.get(s, 0) for s in _smt_siblings(c)) for c in cpus}
+    return sorted(cpus, key=lambda c: (core[c], cpus.index(c)))
 
 
 def _l3_of(cpu):

@@ -68,3 +68,22 @@ def test_parent_rank_starts_no_hip_before_its_tile_child():
     assert "torch.cuda" not in src
     assert main.index("tile_lines(") < main.index("fdgpu_device_count()")
     assert main.index("fdgpu_device_count()") < main.index("VerifyEngine(")
+
+
+def test_idle_first_counts_smt_siblings(monkeypatch):
+    """bench.py pins tile and producer threads to the quietest cores
+    (workload.idle_first); a core whose sibling hyperthread is busy counts
+    as busy, so a core shared with another tenant goes last."""
+    from firedancer_amd import workload
+    ticks = iter([{0: 0, 1: 0, 2: 0, 3: 0, 128: 0, 129: 0, 130: 0, 131: 0},
+                  {0: 5, 1: 0, 2: 0, 3: 1, 128: 0, 129: 90, 130: 0, 131: 0}])
+    monkeypatch.setattr(workload, "_cpu_busy_ticks", lambda: next(ticks))
+    monkeypatch.setattr(workload, "_smt_siblings", lambda c: [c, c + 128])
+    monkeypatch.setattr("time.sleep", lambda s: None)
+    assert workload.idle_first([0, 1, 2, 3]) == [2, 3, 0, 1]
+
+
+def test_smt_siblings_of_this_host():
+    from firedancer_amd import workload
+    s = workload._smt_siblings(0)
+    assert 0 in s and all(isinstance(c, int) for c in s)
