@@ -366,10 +366,10 @@ FDG_DEV uint32_t out_idx(const uint32_t *__restrict__ perm, uint32_t i) { return
 
 /* park words (entry FDGPU_WS_PARK) */
 #define HPARK_KD 0        /* 8 words: radix-16 digits of k (full-path lanes) */
-#define HPARK_XR 10       /* decoded R, affine x (10 words) */
-#define HPARK_YR 20       /* and y */
 #define HPARK_CODE 30     /* pass-1 code */
-static_assert(HPARK_KD + KD_WORDS <= HPARK_XR && HPARK_CODE < (int)FDGPU_ATAB_WORDS, "park layout");
+/* (decoded R is not parked: fdgpu_full_kernel compares with the -R table's
+   entry 1, projectively, so a half-size lane never writes this entry) */
+static_assert(HPARK_KD + KD_WORDS <= HPARK_CODE && HPARK_CODE < (int)FDGPU_ATAB_WORDS, "park layout");
 
 /* Signed radix-16 digits of a magnitude m < 2^160 (5 limbs): 40 nibbles in
    [-8, 7] (two's complement, digit i at bits 4(i%8) of word i/8); nd = the
@@ -602,8 +602,6 @@ FDG_DEV void verify_hs_body(const uint8_t *__restrict__ arena, const fdgpu_sig_d
     FDGPU_STAMP(3);
     const bool r_ok = ge_decode(P, Renc, ref_map);
     const bool r_small = ge_is_small_order_affine(P);
-#pragma unroll
-    for (int j = 0; j < 10; j++) { park[HPARK_XR + j] = P.X.v[j]; park[HPARK_YR + j] = P.Y.v[j]; }
     ge_p3_neg(Pn, P);
     atab_build(tab_r(wsl), Pn);
     if (code == 0 && !a_ok) code = ref_map ? -2 : -1;
@@ -811,10 +809,6 @@ fdgpu_verify_pair_kernel(const uint8_t *__restrict__ arena, const fdgpu_sig_desc
     ge_p3 P, Pn;
     const bool ok = ge_decode(P, enc, ref_map);
     const bool small = ge_is_small_order_affine(P);
-    if (rl) {
-#pragma unroll
-      for (int j = 0; j < 10; j++) { park[HPARK_XR + j] = P.X.v[j]; park[HPARK_YR + j] = P.Y.v[j]; }
-    }
     ge_p3_neg(Pn, P);
     atab_build(rl ? tab_r(wsl) : tab_a(wsl), Pn);
     /* both verdicts in both lanes, in decode2's order (A first) */
@@ -1021,7 +1015,7 @@ fdgpu_key_table_kernel(const uint8_t *__restrict__ arena, const fdgpu_sig_desc_t
 }
 
 /* The queued lanes of fdgpu_verify_hs_kernel: [S]B + [k](-A) with k's 64
-   windows (dsm_k), compared with the decoded R (affine, parked). */
+   windows (dsm_k), compared with the decoded R (from the lane's -R table). */
 __global__ void __launch_bounds__(FDGPU_BLOCK, FDGPU_VERIFY_WAVES)
 fdgpu_full_kernel(uint32_t *__restrict__ ws, const uint32_t *__restrict__ perm, int8_t *__restrict__ codes,
                   const uint32_t *__restrict__ queue, const uint32_t *__restrict__ queue_cnt, uint32_t slots,
@@ -1041,13 +1035,20 @@ FDG_DEV void full_body(uint32_t *__restrict__ ws, const uint32_t *__restrict__ p
     for (int j = 0; j < KD_WORDS; j++) kd[j] = park[HPARK_KD + j];
     ge_p2 Rc;
     dsm_k(Rc, kd, wsl, FDGPU_WS_SB, tab_a(key_of ? lane_ws(ws, key_of[i]) : wsl));
-    fe x, y, l;
+    /* == R: the -R table's entry 1 is (Y-X, Y+X, 2Z, -2dT) of R = (X:Y:Z),
+       so 2X = YmX - YpX and 2Y = YpX + YmX; compare X / Z, Y / Z crosswise */
+    uint32_t er[40];
+    atab_load(er, tab_r(wsl), 1);
+    fe ypx, ymx, z2, x2, y2, l, r;
 #pragma unroll
-    for (int j = 0; j < 10; j++) { x.v[j] = park[HPARK_XR + j]; y.v[j] = park[HPARK_YR + j]; }
-    fe_mul(l, x, Rc.Z);
-    bool eq = fe_eq(Rc.X, l);
-    fe_mul(l, y, Rc.Z);
-    eq = eq && fe_eq(Rc.Y, l);
+    for (int j = 0; j < 10; j++) { ypx.v[j] = er[j]; ymx.v[j] = er[10 + j]; z2.v[j] = er[20 + j]; }
+    fe_carry(ypx); fe_carry(ymx); fe_carry(z2);
+    fe_sub(x2, ymx, ypx);
+    fe_add(y2, ypx, ymx);
+    fe_mul(l, Rc.X, z2); fe_mul(r, x2, Rc.Z);
+    bool eq = fe_eq(l, r);
+    fe_mul(l, Rc.Y, z2); fe_mul(r, y2, Rc.Z);
+    eq = eq && fe_eq(l, r);
     codes[out_idx(perm, i)] = (int8_t)(eq ? 0 : -3);
   }
 }
