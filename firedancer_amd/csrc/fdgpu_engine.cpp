@@ -808,7 +808,10 @@ static Slot *free_slot(fdgpu_engine_t *e) {
    UINT64_MAX on a HIP error.  An arena that expand() later rejects leaves the
    slot free; its stale upload is overwritten by the next batch's copies,
    which are ordered after it on the same stream. */
-static constexpr unsigned FDGPU_COPY_THREADS = 4;
+#ifndef FDGPU_COPY_THREADS_N
+#define FDGPU_COPY_THREADS_N 4                 /* A/B builds may change it */
+#endif
+static constexpr unsigned FDGPU_COPY_THREADS = FDGPU_COPY_THREADS_N;
 static constexpr uint64_t FDGPU_COPY_SPLIT_MIN = 4ull << 20;
 /* FDGPU_COPY_CHUNK_MB overrides the upload piece (A/B; 0: one piece per thread) */
 const uint64_t FDGPU_COPY_CHUNK = [] {
