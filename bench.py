@@ -86,6 +86,9 @@ def parse():
     ap.add_argument("--keypool-txns", type=int, default=1_000_000,
                     help="txns of the signer-reuse batch (key pool of 4096) timed with and without the key "
                          "cache (0: skip)")
+    ap.add_argument("--ab-build", action="store_true",
+                    help="let a library with A/B or fault-injection switches run (fdgpu_build_info; recorded in the "
+                         "line as `build`); without it such a library is refused")
     return ap.parse_args()
 
 
@@ -854,6 +857,7 @@ def main():
     dist = Dist()
     cpus = dist.cpus()
     from firedancer_amd import VerifyEngine, _lib, workload
+    build_info = _lib.require_product_build(allow_ab=args.ab_build)    # no HIP call
 
     t_gen = time.perf_counter()
     arena, txns, modes = workload.cfg1(args.txns, seed=rank_seed(dist.rank))
@@ -1000,6 +1004,7 @@ def main():
                                  f"{kc_ms:.4f} ms; traffic source {traffic_src}"},
             "cpu_baseline": cpu,
             "self_check_codes": self_ok,
+            "build": build_info,
             "gen_s": round(t_gen, 2),
         }
         line.update(parity)

@@ -58,6 +58,8 @@ def lib():
     L.fdgpu_device_count.restype = c.c_int
     L.fdgpu_kernel_path.argtypes = []
     L.fdgpu_kernel_path.restype = c.c_char_p
+    L.fdgpu_build_info.argtypes = []
+    L.fdgpu_build_info.restype = c.c_char_p
     L.fdgpu_submit.argtypes = [vp, vp, c.c_uint64, vp, c.c_uint64]
     L.fdgpu_submit.restype = c.c_int64
     L.fdgpu_poll.argtypes = [vp, c.c_int64, vp, c.c_int]
@@ -148,6 +150,24 @@ def header_functions():
     text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
     names = re.findall(r"^[A-Za-z_][\w \t\*]*?\b(fd\w+)\s*\(", text, flags=re.M)
     return sorted(set(n for n in names if not n.startswith("FD_")))
+
+
+def build_info():
+    """The loaded library's build switches (fdgpu_build_info) as a dict;
+    "product" is 1 iff every one is at the shipped default."""
+    import json
+    return json.loads(lib().fdgpu_build_info().decode())
+
+
+def require_product_build(allow_ab=False):
+    """Raise unless the loaded library is the product build (every A/B and
+    diagnostic switch off).  allow_ab: an A/B run says so and is let through;
+    the returned dict goes into its record either way."""
+    info = build_info()
+    if not info.get("product") and not allow_ab:
+        raise RuntimeError(f"firedancer_amd: {LIB_PATH} is not the product build: {info} "
+                           "(rebuild with `make -C firedancer_amd/csrc`, or pass the A/B flag)")
+    return info
 
 
 def last_error():

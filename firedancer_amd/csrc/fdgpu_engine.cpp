@@ -121,6 +121,8 @@ struct Slot {
   fdgpu_frag_ex_t *d_fxio = nullptr;          /* the records, kept on the device by the ingest */
   uint32_t *d_io_cnt = nullptr;               /* the ingest's signature count: zero at the start of a gathered
                                                  batch (cleared by the finish of the slot's previous one) */
+  bool io_cnt_dirty = false;                  /* an ingest was queued but not its finish (an error between
+                                                 them): the next gathered batch clears the count first */
   uint8_t *d_mirror = nullptr;                /* DMA gather: the batch's source ranges, copied in by the DMA
                                                  engines, parsed and verified in place (the batch arena) */
   uint64_t mirror_cap = 0;
@@ -820,6 +822,18 @@ const uint64_t FDGPU_COPY_CHUNK = [] {
   return m > 0 ? (uint64_t)m << 20 : UINT64_MAX;
 }();
 
+char const *fdgpu_build_info(void) {
+  static thread_local char buf[512];
+  char kb[256];
+  const int kprod = fdgpu_kernel_build_info(kb, sizeof kb);
+  const char *df = getenv("FDGPU_DEBUG_DROP_FLAG");      /* fault injection: completion flags dropped */
+  const int drop = df && df[0] == '1';
+  const int prod = kprod && FDGPU_COPY_THREADS_N == 4 && !drop;
+  snprintf(buf, sizeof buf, "{%s,\"copy_threads\":%d,\"debug_drop_flag\":%d,\"product\":%d}", kb,
+           (int)FDGPU_COPY_THREADS_N, drop, prod);
+  return buf;
+}
+
 }  // extern "C"
 
 /* The staging helpers: FDGPU_COPY_THREADS - 1 process-wide threads started
@@ -1270,6 +1284,7 @@ int io_tail(fdgpu_engine_t *e, Slot *s) {
                                      s->m_arena, s->m_seed, s->m_out, (int8_t *)s->d_trh, (uint64_t *)(s->d_trh + cb),
                                      (uint16_t *)(s->d_trh + cb + n * 8), s->d_io_cnt, s->stream),
          FDGPU_ERR_DEVICE);
+  s->io_cnt_dirty = false;
   slot_flag_next(s);
   if (e->flag_poll && !e->drop_flag) HIPCHK(hipStreamWriteValue32(s->stream, s->d_flag, s->flag_seq, 0), FDGPU_ERR_DEVICE);
   HIPCHK(hipEventRecord(s->done, s->stream), FDGPU_ERR_DEVICE);
@@ -1504,6 +1519,8 @@ int64_t fdgpu_submit_frags_io(fdgpu_engine_t *e, fdgpu_frag_io_t const *fio, uin
       HIPCHK(hipMemcpyAsync(s->d_mirror + h_rtab[r], (const void *)rg[r].lo, rg[r].hi - rg[r].lo, hipMemcpyHostToDevice,
                             s->stream),
              FDGPU_ERR_DEVICE);
+    if (s->io_cnt_dirty) HIPCHK(hipMemsetAsync(s->d_io_cnt, 0, 64, s->stream), FDGPU_ERR_DEVICE);
+    s->io_cnt_dirty = false;
     HIPCHK(fdgpu_launch_frag_ingest_io((const uint64_t *)(s->d_ioh + src_at), (const fdgpu_frag_ex_t *)s->d_ioh,
                                        any_chk ? (const uint64_t *)(s->d_ioh + chk_at) : nullptr,
                                        dma ? (const uint64_t *)(s->d_ioh + rtab_at) : nullptr, (uint32_t)n,
@@ -1511,6 +1528,7 @@ int64_t fdgpu_submit_frags_io(fdgpu_engine_t *e, fdgpu_frag_io_t const *fio, uin
                                        s->d_io_cnt,
                                        zero_cnt ? fdgpu_verify_cnt_word(s->d_ws, (uint32_t)bound) : nullptr, s->stream),
            FDGPU_ERR_DEVICE);
+    s->io_cnt_dirty = true;                            /* until this batch's finish is queued */
     if (!e->merges.empty() && zero_cnt && bound) {
       /* the verify waits to be merged with the other batches ready (merge_kick) */
       HIPCHK(hipEventRecord(s->parsed, s->stream), FDGPU_ERR_DEVICE);
@@ -1521,8 +1539,10 @@ int64_t fdgpu_submit_frags_io(fdgpu_engine_t *e, fdgpu_frag_io_t const *fio, uin
       s->staged = false; st_rlx(s->held, false); st_rlx(s->polls, 0u); s->frag = true; s->io = true; s->tr_sz = 0; s->tr_base = 0;
       st_rlx(s->ticket, e->next_ticket++);
       s->txn_cnt = n;
-      const int rc = merge_kick(e, false);
-      if (rc) return rc;
+      /* a failed merge marks this batch failed: its poll reports the error
+         (returning the error here would leave the slot's ticket unknown to the
+         caller, and the slot occupied for good) */
+      (void)merge_kick(e, false);
       return s->ticket;
     }
     HIPCHK(fdgpu_launch_verify_sigs(arena, s->d_sigs, (uint32_t)bound, nullptr, e->d_btab, s->d_ws, s->d_sig_codes,
@@ -1533,6 +1553,7 @@ int64_t fdgpu_submit_frags_io(fdgpu_engine_t *e, fdgpu_frag_io_t const *fio, uin
                                        arena, hash_seed, out_dev, (int8_t *)s->d_trh, (uint64_t *)(s->d_trh + cb),
                                        (uint16_t *)(s->d_trh + cb + n * 8), s->d_io_cnt, s->stream),
            FDGPU_ERR_DEVICE);
+    s->io_cnt_dirty = false;
   }
   slot_flag_next(s);
   if (e->flag_poll && !e->drop_flag) HIPCHK(hipStreamWriteValue32(s->stream, s->d_flag, s->flag_seq, 0), FDGPU_ERR_DEVICE);

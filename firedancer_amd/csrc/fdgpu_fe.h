@@ -260,13 +260,6 @@ FDG_DEV void fe_ff_close(fe &h, uint32_t (&r)[10], uint64_t carry) {
    product wrapping past 2^255 picks up 19, and an odd-odd limb pair an
    extra 2 (weights 2^ceil(25.5 i)).  f is pre-doubled, g pre-multiplied by
    19, so each term is one v_mad_u64_u32 into a 64-bit column sum. */
-#if FDGPU_FE_WHOLE_ASM
-}  // namespace fdgpu
-namespace fdgpu {
-#include "fdgpu_fe_asm.h"
-FDG_DEV void fe_sq(fe &h, const fe &f) { fe_sq_sh0(h, f); }
-FDG_DEV void fe_sq2(fe &h, const fe &f) { fe_sq_sh1(h, f); }
-#else
 FDG_DEV void fe_mul(fe &h, const fe &f, const fe &g) {
   uint32_t g19[10], f2[10];
 #pragma unroll
@@ -341,7 +334,6 @@ FDG_DEV void fe_sq_sh(fe &h, const fe &f) {
 FDG_DEV void fe_sq(fe &h, const fe &f) { fe_sq_sh<0>(h, f); }
 /* h = 2 f^2 (f <= R) */
 FDG_DEV void fe_sq2(fe &h, const fe &f) { fe_sq_sh<1>(h, f); }
-#endif
 
 FDG_DEV void fe_sqn(fe &h, const fe &f, int n) {
   fe_sq(h, f);

@@ -134,6 +134,9 @@ hipError_t fdgpu_launch_verify_multi(const fdgpu_mbatch_t *mb, uint32_t nb, uint
 hipError_t fdgpu_launch_combine(const fdgpu_txn_desc_t *d_txns, uint32_t n_txn, const int8_t *d_sig_codes,
                                 int8_t *d_txn_codes, uint64_t *d_accept, hipStream_t stream);
 hipError_t fdgpu_verify_occupancy(int *blocks_per_cu);
+/* the kernels' compile-time switches as JSON members into buf; 1 iff all are
+   at the shipped defaults */
+int        fdgpu_kernel_build_info(char *buf, size_t n);
 size_t     fdgpu_ws_bytes(uint64_t n_sig);
 
 /* test/diagnostic kernels */

@@ -38,6 +38,23 @@ using namespace fdgpu;
 #ifndef FDGPU_VERIFY_WAVES
 #define FDGPU_VERIFY_WAVES 2  /* waves per SIMD of the verify kernel: decode/pow chains want ~190 VGPRs */
 #endif
+/* A/B build switches.  The shipped library is built with every one at the
+   default below; fdgpu_build_info() reports them and smoke() / bench.py
+   refuse a library built otherwise (unless told it is an A/B build).
+     FDGPU_TAB_STORE_NT   non-temporal stores of the chain tables
+     FDGPU_TAB_LOAD_CPOL  cache-policy bits of the chain's LDS-DMA table loads
+     FDGPU_WS_SLOT        chain tables in a per-device pool indexed by resident
+                          block slot instead of by signature */
+#ifndef FDGPU_TAB_STORE_NT
+#define FDGPU_TAB_STORE_NT 0
+#endif
+#ifndef FDGPU_TAB_LOAD_CPOL
+#define FDGPU_TAB_LOAD_CPOL 0
+#endif
+#ifndef FDGPU_WS_SLOT
+#define FDGPU_WS_SLOT 0
+#endif
+#define FDGPU_WS_SLOTS 4096u        /* wave slots of the pool (>= the 2,048 verify waves a device keeps resident) */
 
 namespace {
 
@@ -343,6 +360,37 @@ FDG_DEV uint32_t *lane_ws(uint32_t *ws, uint32_t i) {
   return ws + (size_t)i * FDGPU_WS_LANE_WORDS;
 }
 
+/* FDGPU_WS_SLOT: the slot pool follows the comb tables in the per-device
+   allocation (fdgpu_btab_bytes): a bitmap of FDGPU_WS_SLOTS bits (512 B),
+   then one 64-lane workspace per slot.  A wave claims a free slot at its
+   start and frees it at its end, so at most the device's resident verify
+   waves' tables are live, and a new wave rewrites lines an earlier wave used
+   instead of allocating fresh ones.  No wait: a wave that finds no free slot
+   (never, with more slots than resident waves) keeps its per-signature
+   workspace.  Per wave, not per block: a block-wide slot index in LDS would
+   push the block past 80 KB, and two no longer fit a CU. */
+#define WS_SLOT_NONE 0xFFFFFFFFu
+#define BTAB_WORDS ((size_t)BC_NDIG * BC_ENT * FDGPU_BCOMB_STRIDE)
+FDG_DEV uint32_t *ws_slot_bitmap(const uint32_t *btab) { return const_cast<uint32_t *>(btab) + BTAB_WORDS; }
+FDG_DEV uint32_t *ws_slot_lanes(const uint32_t *btab, uint32_t slot) {
+  return ws_slot_bitmap(btab) + FDGPU_WS_SLOTS / 32u + (size_t)slot * 64u * FDGPU_WS_LANE_WORDS;
+}
+FDG_DEV uint32_t ws_slot_claim(uint32_t *bm, uint32_t seed) {
+  constexpr uint32_t NW = FDGPU_WS_SLOTS / 32u;
+  for (uint32_t t = 0; t < 2u * NW; t++) {
+    const uint32_t w = (seed + t) % NW;
+    uint32_t v = __hip_atomic_load(bm + w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    while (v != 0xFFFFFFFFu) {
+      const uint32_t b = (uint32_t)__builtin_ctz(~v);
+      const uint32_t old = atomicOr(bm + w, 1u << b);
+      if (!(old & (1u << b))) return w * 32u + b;
+      v = old | (1u << b);
+    }
+  }
+  return WS_SLOT_NONE;
+}
+FDG_DEV void ws_slot_release(uint32_t *bm, uint32_t slot) { atomicAnd(bm + slot / 32u, ~(1u << (slot % 32u))); }
+
 /* Output slot of lane i: signatures may be verified in an order grouped by
    SHA-512 block count (perm[i] = the signature's index in the caller's
    order); codes are always written in the caller's order. */
@@ -441,28 +489,8 @@ FDG_DEV void hs_wscalar(uint32_t (&w)[8], const uint32_t (&v)[5], bool v_neg, co
 typedef __attribute__((address_space(3))) void lds_void_t;
 
 FDG_DEV void stage_entry(uint32_t *lds_wave, const uint32_t *tab, int e) {
-#if FDGPU_DIAG_TAB_HOT
-  /* diagnostic only (wrong codes): every lane stages entry 1 of its wave's
-     first lane's table, so the chain's table reads are L2 hits -- the same
-     VALU and LDS work with the HBM read traffic gone (DESIGN §4 traffic) */
-  (void)e;
-  const uint64_t p = (uint64_t)tab_entry(tab, 1);
-  const uint32_t *src = (const uint32_t *)(((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(p >> 32)) << 32) |
-                                           (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)p));
-#else
   const uint32_t *src = tab_entry(tab, e);
-#endif
-#if FDGPU_DIAG_LINE8
-  /* diagnostic only (wrong codes; with FDGPU_ATAB_WORDS=64): the chain
-     stages 128 B of each 256-B-aligned entry, one cache line instead of the
-     two a 160-B entry spans -- the traffic of a packed 128-B entry */
-  constexpr int NCH = 8;
-#else
   constexpr int NCH = 10;
-#endif
-#ifndef FDGPU_TAB_LOAD_CPOL
-#define FDGPU_TAB_LOAD_CPOL 0                   /* cache-policy bits of the table loads (A/B builds) */
-#endif
 #pragma unroll
   for (int c = 0; c < NCH; c++)
     __builtin_amdgcn_global_load_lds((const void *)(src + 4 * c), (lds_void_t *)(lds_wave + 256 * c), 16, 0,
@@ -556,6 +584,14 @@ FDG_DEV void verify_hs_body(const uint8_t *__restrict__ arena, const fdgpu_sig_d
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) nb = max(nb, (uint32_t)__shfl_xor((int)nb, off));
   uint32_t *wsl = lane_ws(ws, i);
+#if FDGPU_WS_SLOT
+  uint32_t w_slot = WS_SLOT_NONE;
+  if (!KC) {
+    if ((threadIdx.x & 63u) == 0) w_slot = ws_slot_claim(ws_slot_bitmap(btab), (bx * 4u + (threadIdx.x >> 6)) * 7u);
+    w_slot = __builtin_amdgcn_readfirstlane(w_slot);
+    if (w_slot != WS_SLOT_NONE) wsl = ws_slot_lanes(btab, w_slot) + (size_t)(threadIdx.x & 63u) * FDGPU_WS_LANE_WORDS;
+  }
+#endif
   uint32_t *park = wsl + FDGPU_WS_PARK * FDGPU_ATAB_WORDS;
   const uint32_t *ta = tab_a(wsl);             /* this lane's -A table */
   FDGPU_STAMP(0);
@@ -643,6 +679,13 @@ FDG_DEV void verify_hs_body(const uint8_t *__restrict__ arena, const fdgpu_sig_d
 #pragma unroll
     for (int j = 0; j < KD_WORDS; j++) park[HPARK_KD + j] = kd[j];
     park[HPARK_CODE] = 0u;
+#if FDGPU_WS_SLOT
+    /* fdgpu_full_kernel reads the lane's workspace by signature: a slot
+       lane parks a copy of its tables, [S]B and k there */
+    uint32_t *own = lane_ws(ws, i);
+    if (own != wsl)
+      for (uint32_t q = 0; q < FDGPU_WS_LANE_WORDS / 4u; q++) ((uint4 *)own)[q] = ((const uint4 *)wsl)[q];
+#endif
   }
   FDGPU_STAMP(6);
   bool eq = false;
@@ -685,6 +728,12 @@ FDG_DEV void verify_hs_body(const uint8_t *__restrict__ arena, const fdgpu_sig_d
       if (full) queue[base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull))] = i;
     }
   }
+#if FDGPU_WS_SLOT
+  if (!KC && w_slot != WS_SLOT_NONE) {          /* every access of the wave to its slot has completed: free it */
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if ((threadIdx.x & 63u) == 0) ws_slot_release(ws_slot_bitmap(btab), w_slot);
+  }
+#endif
 }
 
 template <bool KC>
@@ -1627,11 +1676,6 @@ __global__ void __launch_bounds__(256) fdgpu_frag_finish_io_kernel(
       const uint8_t *tr = txn_out + (size_t)(g * 64u + o) * FDT_TXN_MAX_SZ;
       uint8_t *dst = out + oof + b0;
       if (k0 + lane >= total) continue;
-#if FDGPU_DIAG_NO_PAYLOAD_OUT
-      /* diagnostic build only (wrong output): the payload's own units are not
-         written back, to price their PCIe writes (tools/gpu_r05pay.sh) */
-      if (b0 + 16u <= sz) continue;
-#endif
       if (b0 + 16u <= cap && !(((uintptr_t)dst) & 15u)) {
         uint4 w;
         if (b0 + 16u <= sz) {
@@ -1681,12 +1725,29 @@ extern "C" {
 
 char const *fdgpu_kernel_path(void) { return "halfsize: fdgpu_verify_hs_kernel + fdgpu_full_kernel"; }
 
-size_t fdgpu_btab_bytes(void) { return (size_t)BC_NDIG * BC_ENT * FDGPU_BCOMB_STRIDE * sizeof(uint32_t); }
+#ifndef FDGPU_PHASE_STAMPS
+#define FDGPU_PHASE_STAMPS 0
+#endif
+/* every compile-time switch of the kernels, as JSON members; the return
+   value is 1 iff each is at the shipped default (fdgpu_build_info) */
+int fdgpu_kernel_build_info(char *buf, size_t n) {
+  snprintf(buf, n, "\"verify_waves\":%d,\"atab_words\":%u,\"tab_store_nt\":%d,\"tab_load_cpol\":%d,\"ws_slot\":%d,"
+           "\"phase_stamps\":%d", (int)FDGPU_VERIFY_WAVES, (unsigned)FDGPU_ATAB_WORDS, (int)FDGPU_TAB_STORE_NT,
+           (int)FDGPU_TAB_LOAD_CPOL, (int)FDGPU_WS_SLOT, (int)FDGPU_PHASE_STAMPS);
+  return FDGPU_VERIFY_WAVES == 2 && FDGPU_ATAB_WORDS == 40u && FDGPU_TAB_STORE_NT == 0 && FDGPU_TAB_LOAD_CPOL == 0 &&
+         FDGPU_WS_SLOT == 0 && FDGPU_PHASE_STAMPS == 0;
+}
+
+size_t fdgpu_btab_bytes(void) {
+  return (BTAB_WORDS + (FDGPU_WS_SLOT ? FDGPU_WS_SLOTS / 32u + (size_t)FDGPU_WS_SLOTS * 64u * FDGPU_WS_LANE_WORDS : 0)) *
+         sizeof(uint32_t);
+}
 
 hipError_t fdgpu_btab_build(uint32_t *d_btab, hipStream_t stream) {
   uint32_t *bases = nullptr, *scratch = nullptr;
   const uint32_t lanes = BC_NDIG * BC_CHUNKS;
-  hipError_t e = hipMalloc((void **)&bases, BC_NDIG * 40 * sizeof(uint32_t));
+  hipError_t e = FDGPU_WS_SLOT ? hipMemsetAsync(d_btab + BTAB_WORDS, 0, FDGPU_WS_SLOTS / 8u, stream) : hipSuccess;
+  if (e == hipSuccess) e = hipMalloc((void **)&bases, BC_NDIG * 40 * sizeof(uint32_t));
   if (e == hipSuccess) e = hipMalloc((void **)&scratch, (size_t)lanes * FDGPU_BCOMB_CHUNK * 10 * sizeof(uint32_t));
   if (e == hipSuccess) {
     hipLaunchKernelGGL(fdgpu_bcomb_base_kernel, dim3(1), dim3(64), 0, stream, bases);

@@ -150,7 +150,7 @@ void fdgpu_dtile_run_sandboxed(fdgpu_dtile_t *t, uint64_t frag_target, uint64_t 
   int rc = 0;
   /* the clock is read only on idle passes, every 256th: a pass that took a
      frag costs no clock read and no stats copy beyond the step itself */
-  for (uint32_t idle = 0;;) {
+  for (uint64_t idle = 0;;) {                          /* 64-bit: never wraps back to the first check */
     if (fdgpu_dtile_step(t) > 0) {
       idle = 0;
       fdgpu_dtile_stats(t, &st);

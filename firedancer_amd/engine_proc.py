@@ -169,8 +169,11 @@ def serve(in_paths, out_paths, verifiers, frag_cnts, timeout_s=120.0, idle_s=0.0
         mux = [vm.mux_stats() for vm in vms]
         lat = np.concatenate([vm.latencies_ns() for vm in vms]) / 1e6 if vms else np.zeros(0)
         agg = {k: int(sum(s[k] for s in per)) for k in per[0]}
-        agg["stall_max_ns"] = max(s["stall_max_ns"] for s in per)
-        agg["lap_margin_min"] = min(s["lap_margin_min"] for s in per)
+        for k in agg:                       # extremes combine as extremes, not sums
+            if k.endswith("_max") or k.endswith("_max_ns"):
+                agg[k] = max(s[k] for s in per)
+            elif k.endswith("_min") or k.endswith("_min_ns"):
+                agg[k] = min(s[k] for s in per)
         magg = {k: int(sum(m[k] for m in mux)) for k in mux[0]}
         agg["overrun_polling"], agg["overrun_reading"] = magg["overrun_polling"], magg["overrun_reading"]
         agg["overrun"] = agg["lapped"] + agg["overrun_polling"] + agg["overrun_reading"]

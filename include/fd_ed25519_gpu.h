@@ -387,6 +387,12 @@ int fdgpu_engine_info( fdgpu_engine_t * e, uint32_t * grid_blocks, uint32_t * bl
 /* The kernels one verify launches, as a static string, e.g.
    "halfsize: fdgpu_verify_hs_kernel + fdgpu_full_kernel" (the build's path). */
 char const * fdgpu_kernel_path( void );
+/* The library's build, as a JSON object: every compile-time switch of the
+   kernels and the engine (A/B builds change them), the fault-injection
+   environment variables the engine honours, and "product": 1 iff all of them
+   are at the shipped defaults.  No HIP call.  __graft_entry__.smoke() and
+   bench.py refuse a library that reports "product": 0. */
+char const * fdgpu_build_info( void );
 /* HIP devices visible to this process (hipGetDeviceCount; starts the HIP
    runtime), or -1 when the runtime reports none / fails. */
 int          fdgpu_device_count( void );

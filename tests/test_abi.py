@@ -21,7 +21,7 @@ def test_exports_every_header_function():
     names = _lib.header_functions()
     for fn in REF_API:
         assert fn in names
-    assert len(names) == 50, names          # + fdgpu_device_count, fdgpu_debug_h2d_gbps (round 5)
+    assert len(names) == 51, names          # + fdgpu_build_info (round 6)
     L = _lib.lib()
     for n in names:
         assert hasattr(L, n), n
@@ -96,6 +96,35 @@ def test_engine_flags_match_header():
           "KEY_CACHE": ed.FLAG_KEY_CACHE, "PAIR": ed.FLAG_PAIR, "PAIR_AUTO": ed.FLAG_PAIR_AUTO,
           "MERGE": ed.FLAG_MERGE, "SPREAD": ed.FLAG_SPREAD, "SPREAD_AUTO": ed.FLAG_SPREAD_AUTO}
     assert hdr == py, (hdr, py)
+
+
+def test_shipped_library_is_product_build():
+    """fdgpu_build_info() of the library smoke() and bench.py load: every A/B
+    switch at its shipped default, no fault injection; the stamps variant is
+    reported as not a product build (so the guard is not vacuous)."""
+    info = _lib.build_info()
+    assert info["product"] == 1, info
+    assert (info["verify_waves"], info["atab_words"], info["tab_store_nt"], info["tab_load_cpol"], info["ws_slot"],
+            info["phase_stamps"], info["debug_drop_flag"]) == (2, 40, 0, 0, 0, 0, 0), info
+    assert _lib.require_product_build() == info
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    probe = ("import json, sys; sys.path.insert(0, {r!r}); from firedancer_amd import _lib; "
+             "print(json.dumps(_lib.build_info()))").format(r=repo)
+    stamps = os.path.join(repo, "build", "stamps", "libfd_ed25519_gpu.so")
+    if os.path.exists(stamps):
+        r = subprocess.run(["python", "-c", probe], capture_output=True, text=True, env={**os.environ, "FDGPU_LIB": stamps})
+        assert r.returncode == 0, r.stderr
+        import json
+        st = json.loads(r.stdout)
+        assert st["phase_stamps"] == 1 and st["product"] == 0, st
+    r = subprocess.run(["python", "-c", probe], capture_output=True, text=True,
+                       env={**os.environ, "FDGPU_DEBUG_DROP_FLAG": "1"})
+    assert '"product": 0' in r.stdout and '"debug_drop_flag": 1' in r.stdout, r.stdout + r.stderr
+    # no wrong-code diagnostic switch is left in the product sources
+    csrc = os.path.join(repo, "firedancer_amd", "csrc")
+    for f in os.listdir(csrc):
+        if f.endswith((".hip", ".h", ".cpp")):
+            assert "FDGPU_DIAG_" not in open(os.path.join(csrc, f)).read(), f
 
 
 def test_stamps_variant_builds():
