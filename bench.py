@@ -536,10 +536,19 @@ TILE_REPS = 5   # a capacity run drains 1M frags in a few tens of ms: the median
 # (python -m firedancer_amd.engine_proc) over shared-memory links that a producer
 # process (tools/quic_feed.py) publishes into, every page faulted in before the
 # run; each run starts both processes (engine open + warm-up ~3 s), so three runs each
+# Fields after the rate: engine processes sharing the links (tiles / E each, global round-robin shares --
+# the multi-GPU form of the stage, here on this rank's one GPU) and 1 when the sandboxed dedup process reads
+# every verify -> dedup link reliably at the reference's tcache depth (4,194,302, default.toml:910): the
+# e2e lines are timed to the dedup's last frag (fd_frankendancer.c:136, the node's verify -> dedup path)
 TILE_RUNS_XPROC = (
     ("xproc_mux1_paced_16M", 1, 2, 16e6),
     ("xproc_mux2_paced_24M", 2, 4, 24e6),
     ("xproc_mux1_capacity", 1, 1, -1.0),
+    ("xproc_mux2_capacity", 2, 2, -1.0),
+    ("xproc_2proc_capacity", 2, 2, -1.0, 2, 0),
+    ("xproc_2proc_paced_24M", 2, 4, 24e6, 2, 0),
+    ("xproc_e2e_dedup_capacity", 2, 2, -1.0, 1, 1),
+    ("xproc_e2e_dedup_paced_2M", 2, 4, 2e6, 1, 1),
 )
 TILE_REPS_XPROC = 3
 TILE_DEPTH_LG_PREFILL_XPROC = 21      # as the in-process capacity lines: the lap guard never sees a prefilled frag at risk
@@ -556,8 +565,9 @@ def tile_cmd(rank, cpus, npz, out, runs=TILE_RUNS, multi=0, xproc=False):
     N ranks has at most N GPU processes at any time (a rank's own engines
     open only after its child has exited)."""
     sweep = ";".join(f"{tiles_n},{TILE_BATCH},{TILE_INFLIGHT},{rate:g},{prods}" +
-                     (f",{TILE_CFG3_SIG_MAX_BY_TILES.get(tiles_n, TILE_CFG3_SIG_MAX)}" if multi else "")
-                     for _, tiles_n, prods, rate in runs)
+                     (f",{TILE_CFG3_SIG_MAX_BY_TILES.get(tiles_n, TILE_CFG3_SIG_MAX)}" if multi else
+                      f",0,{rest[0]},{rest[1]}" if rest else "")
+                     for _, tiles_n, prods, rate, *rest in runs)
     cmd = [sys.executable, os.path.join(REPO, "tools", "bench_tile.py"), "--mux", "1", "--gpu-parse", "2",
            "--multi", str(int(multi)), "--producers-same-as-tiles", "1", "--depth-lg", str(TILE_DEPTH_LG_PREFILL),
            "--depth-lg-paced", str(TILE_DEPTH_LG_PACED), "--paced-reps", str(TILE_PACED_REPS),
@@ -595,9 +605,12 @@ def _tile_child(rank, cpus, arena, txns, modes, runs, tag=""):
         res_all = [json.loads(x) for x in open(res_path) if x.strip()]
     if len(res_all) != len(runs) * reps_n:
         raise RuntimeError(f"tools/bench_tile.py gave {len(res_all)} runs, expected {len(runs) * reps_n}")
-    for i, (name, tiles_n, prods, rate) in enumerate(runs):
+    for i, (name, tiles_n, prods, rate, *rest) in enumerate(runs):
         reps = res_all[i * reps_n:(i + 1) * reps_n]
         assert all(x["tiles"] == tiles_n and x["producers"] == prods for x in reps)
+        if rest:
+            assert all(x["engine_procs"] == rest[0] and ("dedup" in x) == bool(rest[1]) for x in reps)
+            out[f"tile_{name}_engine_procs"] = rest[0]
         res = sorted(reps, key=lambda x: x["txns_per_s"])[len(reps) // 2]
         out[f"tile_{name}_txns_per_s_runs"] = [x["txns_per_s"] for x in reps]
         lat = res["batch_latency_ms"]
@@ -616,6 +629,11 @@ def _tile_child(rank, cpus, arena, txns, modes, runs, tag=""):
         out[f"tile_{name}_rescued"] = max(x["counters"]["rescued"] for x in reps)
         out[f"tile_{name}_parse_fail"] = res["counters"]["parse_fail"]
         out[f"tile_{name}_published_ok"] = all(x["published_ok"] for x in reps)
+        if rest and rest[1]:           # the dedup tile in the loop, reliable links, the reference's depth
+            out[f"tile_{name}_dedup_ok"] = all(x["dedup_ok"] for x in reps)
+            out[f"tile_{name}_dedup_tcache_depth"] = res["dedup_tcache_depth"]
+            ds = res["dedup"]["stats"]
+            out[f"tile_{name}_dedup_in_published_dup"] = [ds["in_frags"], ds["published"], ds["dup"]]
         # the tile's longest gap between two of its polls, worst of the runs: a core taken away (another
         # tenant's thread on it, the runtime blocking) -- a paced link laps a tile stalled for
         # depth / per-link rate (16384 / 5 M/s = 3.3 ms)
@@ -877,7 +895,7 @@ def main():
         del cfg3_tile
         tl["tile_mux1_capacity_txns_per_s_node"] = round(dist.sum(tl["tile_mux1_capacity_txns_per_s"]), 1)
         tl["tile_published_ok_all_ranks"] = dist.sum(
-            1 if all(v for k, v in tl.items() if k.endswith("_published_ok")) else 0) == dist.world
+            1 if all(v for k, v in tl.items() if k.endswith(("_published_ok", "_dedup_ok"))) else 0) == dist.world
     # one process per GPU; more ranks than visible GPUs (a rehearsal of the
     # multi-rank path on a one-GPU box) share devices round robin
     ndev = _lib.lib().fdgpu_device_count()

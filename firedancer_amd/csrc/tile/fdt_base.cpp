@@ -206,6 +206,25 @@ int fdt_tcache_insert(void *tc, uint64_t tag) {
   return 0;
 }
 
+void fdt_tcache_prefetch(const void *tc, uint64_t tag) {
+  tcache_view v{(uint64_t *)const_cast<void *>(tc)};
+  __builtin_prefetch(v.map() + (tag & (v.map_cnt() - 1)));
+}
+
+void fdt_tcache_prefetch_evict(const void *tc, uint64_t ahead) {
+  tcache_view v{(uint64_t *)const_cast<void *>(tc)};
+  uint64_t k = v.oldest() + ahead;
+  while (k >= v.depth()) k -= v.depth();
+  const uint64_t victim = v.ring()[k];
+  if (victim != FDT_TCACHE_TAG_NULL) __builtin_prefetch(v.map() + (victim & (v.map_cnt() - 1)));
+}
+
+uint64_t fdt_tcache_insert_many(void *tc, const uint64_t *tags, uint64_t n) {
+  uint64_t dup = 0;
+  for (uint64_t i = 0; i < n; i++) dup += (uint64_t)fdt_tcache_insert(tc, tags[i]);
+  return dup;
+}
+
 void fdt_tagring_init(fdt_tagring_t *r, uint64_t depth) {
   std::memset(r, 0, sizeof *r);
   r->depth = depth < 1 ? 1 : depth > FDT_TAGRING_MAX ? FDT_TAGRING_MAX : depth;

@@ -144,9 +144,9 @@ int fdt_sandbox_enter(int logfile_fd) {
    timeout, 3 sandbox could not be entered.  Never returns. */
 void fdgpu_dtile_run_sandboxed(fdgpu_dtile_t *t, uint64_t frag_target, uint64_t idle_ns_max,
                                fdgpu_dtile_stats_t *stats_out, int logfile_fd) {
-  if (fdt_sandbox_enter(logfile_fd)) syscall(__NR_exit_group, 3);
+  if (fdgpu_dtile_rehome(t) || fdt_sandbox_enter(logfile_fd)) syscall(__NR_exit_group, 3);
   fdgpu_dtile_stats_t st;
-  uint64_t last = mono_ns();
+  uint64_t last = mono_ns(), last_frag = 0;
   int rc = 0;
   /* the clock is read only on idle passes, every 256th: a pass that took a
      frag costs no clock read and no stats copy beyond the step itself */
@@ -154,17 +154,18 @@ void fdgpu_dtile_run_sandboxed(fdgpu_dtile_t *t, uint64_t frag_target, uint64_t 
     if (fdgpu_dtile_step(t) > 0) {
       idle = 0;
       fdgpu_dtile_stats(t, &st);
-      if (st.in_frags + st.overrun >= frag_target) break;
+      if (st.in_frags + st.overrun >= frag_target) { last_frag = mono_ns(); break; }
       continue;
     }
     if ((++idle & 255u) == 0) {
       const uint64_t now = mono_ns();
-      if (idle == 256u) last = now;                     /* the first idle check since the last frag */
+      if (idle == 256u) last = last_frag = now;         /* the first idle check since the last frag */
       fdgpu_dtile_stats(t, &st);
       if (st.in_frags + st.overrun >= frag_target) break;
       if (now - last > idle_ns_max) { rc = 1; break; }
     }
   }
+  st.done_ns = st.in_frags ? last_frag : 0;
   memcpy(stats_out, &st, sizeof(st));
   __atomic_thread_fence(__ATOMIC_SEQ_CST);
   syscall(__NR_exit_group, rc);

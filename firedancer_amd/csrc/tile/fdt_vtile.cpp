@@ -28,9 +28,11 @@
    Out-link flow control: with out_fseq set, publishing stops while the
    consumer is a full mcache depth behind (the mux credit check,
    fd_mux.c:548). */
+#include <sys/mman.h>
 #include <time.h>
 
 #include <algorithm>
+#include <cstddef>
 #include <atomic>
 #include <cstdlib>
 #include <cstring>
@@ -579,9 +581,38 @@ uint64_t fdgpu_vtile_log(const fdgpu_vtile_t *t, uint64_t *seqs, int8_t *codes, 
 
 /* --------------------------------------------------------- dedup tile */
 
+/* The dedup tile's tcache at the reference's depth is a 64 MB map + a 32 MB
+   ring that every frag touches at random: on 4 KB pages each probe also
+   misses the TLB, so the region asks for transparent huge pages (anonymous
+   THP is madvise-only on the hosts measured).  A forked child re-homes it
+   into memory of its own before entering the sandbox (fdgpu_dtile_rehome): a
+   copy-on-write huge page would be split on the child's first write. */
+namespace {
+struct huge_region {
+  void *map = nullptr;
+  size_t len = 0;
+  void *base = nullptr;
+};
+constexpr size_t HUGE_SZ = 2ull << 20;
+huge_region huge_alloc(size_t bytes) {
+  huge_region r;
+  r.len = (bytes + 2 * HUGE_SZ - 1) & ~(HUGE_SZ - 1);
+  r.map = mmap(nullptr, r.len, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
+  if (r.map == MAP_FAILED) return huge_region{};
+  r.base = (void *)(((uintptr_t)r.map + HUGE_SZ - 1) & ~(uintptr_t)(HUGE_SZ - 1));
+  (void)madvise(r.base, bytes, MADV_HUGEPAGE);     /* a hint: 4 KB pages if the host offers none */
+  return r;
+}
+void huge_free(huge_region &r) {
+  if (r.map) munmap(r.map, r.len);
+  r = huge_region{};
+}
+}  // namespace
+
 struct fdgpu_dtile {
   fdgpu_dtile_cfg_t cfg{};
-  std::vector<uint64_t> tcache_mem;
+  huge_region tc_mem;
+  uint64_t tc_bytes = 0;
   void *tcache = nullptr;
   uint64_t rx_seq[16] = {};
   uint64_t fseq_pub[16] = {};          /* what the tile last stored into each in link's fseq */
@@ -600,15 +631,30 @@ fdgpu_dtile_t *fdgpu_dtile_new(const fdgpu_dtile_cfg_t *cfg) {
   t->cfg = *cfg;
   const uint64_t fp = fdt_tcache_footprint(cfg->tcache_depth, cfg->tcache_map_cnt);
   if (!fp) { delete t; return nullptr; }
-  t->tcache_mem.assign(fp / 8, 0);
-  t->tcache = fdt_tcache_new(t->tcache_mem.data(), cfg->tcache_depth, cfg->tcache_map_cnt);
+  t->tc_mem = huge_alloc(fp);
+  if (!t->tc_mem.base) { delete t; return nullptr; }
+  t->tc_bytes = fp;
+  t->tcache = fdt_tcache_new(t->tc_mem.base, cfg->tcache_depth, cfg->tcache_map_cnt);
   for (uint32_t i = 0; i < cfg->in_cnt; i++) t->rx_seq[i] = t->fseq_pub[i] = cfg->in_seq0[i];
   t->out_seq = cfg->out_seq0;
   t->out_chunk = cfg->out_chunk0;
   return t;
 }
 
-void fdgpu_dtile_delete(fdgpu_dtile_t *t) { delete t; }
+void fdgpu_dtile_delete(fdgpu_dtile_t *t) {
+  if (!t) return;
+  huge_free(t->tc_mem);
+  delete t;
+}
+
+int fdgpu_dtile_rehome(fdgpu_dtile_t *t) {
+  huge_region r = huge_alloc(t->tc_bytes);
+  if (!r.base) return -1;
+  std::memcpy(r.base, t->tc_mem.base, t->tc_bytes);
+  t->tc_mem = r;                      /* the old mapping stays (shared with the parent until it exits) */
+  t->tcache = r.base;
+  return 0;
+}
 
 /* One pass over the in links, at most one frag from each (the mux's
    round-robin service order), fd_dedup.c:89-205. */
@@ -636,6 +682,26 @@ int64_t fdgpu_dtile_step(fdgpu_dtile_t *t) {
         for (uint32_t o = 0; o < nsz; o += 64) __builtin_prefetch(np + o);
       }
       __builtin_prefetch(c.in_mcache[i] + ((seq + 8) & mask));
+      /* the tcache lines of the insert two frags on (its tag, from the payload
+         prefetched two steps ago: a hint only, every value re-read below) and
+         of the tag the insert after it evicts: each a random line of a map
+         that outgrows every cache at the reference's depth */
+      if (i >= c.unparsed_in_cnt) {
+        const fdt_frag_meta_t *ml = c.in_mcache[i] + ((seq + 2) & mask);
+        const uint64_t msq = __atomic_load_n(&ml->seq, __ATOMIC_RELAXED);
+        const uint64_t mch = ml->chunk, msz = ml->sz;
+        if (msq == seq + 2 && mch >= c.in_chunk0[i] && mch <= c.in_wmark[i] && msz >= 2 && msz <= FDT_TPU_DCACHE_MTU) {
+          const uint8_t *mp = c.in_base[i] + (mch << FDT_CHUNK_LG_SZ);
+          uint16_t psz;
+          std::memcpy(&psz, mp + msz - 2, 2);
+          if (align2(psz) + sizeof(fdt_txn_t) + 2 <= msz) {
+            uint16_t so;
+            std::memcpy(&so, mp + align2(psz) + offsetof(fdt_txn_t, signature_off), 2);
+            if ((uint64_t)so + 64 <= msz) fdt_tcache_prefetch(t->tcache, fdt_hash(c.hashmap_seed, mp + so, 64));
+          }
+        }
+        fdt_tcache_prefetch_evict(t->tcache, 3);
+      }
     }
     t->st.in_frags++;
     n++;
@@ -683,6 +749,8 @@ int64_t fdgpu_dtile_step(fdgpu_dtile_t *t) {
 }
 
 void fdgpu_dtile_stats(const fdgpu_dtile_t *t, fdgpu_dtile_stats_t *out) { *out = t->st; }
+
+void *fdgpu_dtile_tcache(fdgpu_dtile_t *t) { return t ? t->tcache : nullptr; }
 
 }  // extern "C"
 

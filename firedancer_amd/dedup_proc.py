@@ -22,7 +22,8 @@ def main(argv=None):
     ap.add_argument("--out", required=True)
     ap.add_argument("--frags", type=int, required=True, help="stop once this many frags were consumed or lost")
     ap.add_argument("--seed", type=lambda x: int(x, 0), default=0xD5)
-    ap.add_argument("--tcache-depth", type=int, default=1 << 14)
+    ap.add_argument("--tcache-depth", type=int, default=4194302,
+                    help="the reference's signature_cache_size (default.toml:910, fd_frankendancer.c:263)")
     ap.add_argument("--idle-s", type=float, default=10.0, help="stop after this long with no frag")
     ap.add_argument("--ready-file", default="", help="created once the sandboxed child runs")
     ap.add_argument("--cpu", type=int, default=-1, help="pin the tile to this CPU")

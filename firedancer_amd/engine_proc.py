@@ -19,11 +19,21 @@ The tile this process runs is the measured one: T verify mux tiles
 gather mode (gpu_parse 2): the device reads each payload where the producer
 process wrote it (the in links' regions are registered with the engines),
 parses, verifies, tags it and writes the out frag into the out link's
-dcache; tile k takes the round-robin share k of every in link
-(fd_verify.c:46) and publishes into out link k.
+dcache; tile k publishes into out link k.
+
+A node's verify stage spans its GPUs the way the reference spans cores:
+verify_tile_cnt tiles each read every quic -> verify link and take the
+round-robin share `seq % verify_tile_cnt == tile index` of it
+(src/app/fdctl/run/topos/fd_frankendancer.c:99,131-133,
+src/app/fdctl/run/tiles/fd_verify.c:36-47).  Here tile k of this process is
+global tile rr_idx + k of rr_cnt (--rr-idx / --rr-cnt), and its engine sits
+on devices[k % len(devices)] (--devices): one process per GPU (N processes,
+--rr-idx p*T --rr-cnt N*T, --devices p) or one process over several GPUs
+(--devices 0,1,...) share the same links, with no collective between them.
 
     python -m firedancer_amd.engine_proc --in /dev/shm/quic_verify_0 \\
-        [--in ...] --out /dev/shm/verify_dedup_0 [--out ...] --frags N[,N...]
+        [--in ...] --out /dev/shm/verify_dedup_0 [--out ...] --frags N[,N...] \\
+        [--devices 0,1] [--rr-idx 0 --rr-cnt 2]
 
 runs until every frag the producers will publish (--frags, per in link) has
 its outcome -- or, once the producers are done, until the tiles sit idle --
@@ -96,13 +106,15 @@ def warm_engines(engines, inflight, out_bytes=0, batch=64):
 
 
 def open_engines(n, device, batch, inflight, pair=2, spread=2, gather=True):
-    """n tile engines on `device` as the tile lines open them (one per tile;
-    the comb table is shared per device), every slot reserved and warmed."""
+    """n tile engines as the tile lines open them (one per tile; the comb
+    table is shared per device), every slot reserved and warmed.  device: one
+    HIP device for all, or a list (engine k on device[k % len])."""
     from . import VerifyEngine
     frag_bytes = (tile.TPU_DCACHE_MTU + 63) // 64 * 64
+    devs = list(device) if isinstance(device, (list, tuple)) else [device]
     es = []
-    for _ in range(n):
-        e = VerifyEngine(device, max_txn=batch, max_sig=batch * 12, max_arena=batch * frag_bytes,
+    for k in range(n):
+        e = VerifyEngine(devs[k % len(devs)], max_txn=batch, max_sig=batch * 12, max_arena=batch * frag_bytes,
                          ring_depth=inflight, pair=pair == 1, pair_auto=pair == 2, spread=spread == 1,
                          spread_auto=spread == 2)
         e.reserve()
@@ -120,10 +132,21 @@ def _producers_done(ins, frag_cnts):
     return True
 
 
+def round_robin_shares(rr_idx, rr_cnt, T):
+    """The global round-robin index of each of this process's T tiles
+    (fd_verify.c:46: tile i of verify_tile_cnt takes seq % cnt == i):
+    rr_idx .. rr_idx+T-1 of rr_cnt (0: T)."""
+    rr_cnt = rr_cnt or T
+    if T < 1 or rr_idx < 0 or rr_idx + T > rr_cnt:
+        raise ValueError(f"round robin: {T} tiles from index {rr_idx} of {rr_cnt}")
+    return list(range(rr_idx, rr_idx + T))
+
+
 def serve(in_paths, out_paths, verifiers, frag_cnts, timeout_s=120.0, idle_s=0.02, cpus=None, ready_file=None,
-          log_max=0, on_start=None, **tile_kw):
+          log_max=0, on_start=None, rr_idx=0, rr_cnt=0, **tile_kw):
     """Join the links, run one gather-mode verify mux tile per out link
-    (tile k: round-robin share k of every in link, verifiers[k], out link k)
+    (tile k: round-robin share rr_idx + k of rr_cnt (0: of this process's
+    tiles) of every in link, verifiers[k], out link k)
     until the outcome of every frag is final -- or, when frags were lost to
     the producers, until they are done and the tiles sit idle for idle_s --
     then return {stats, mux, per-tile stats, latencies, times}.  cpus: tile
@@ -132,11 +155,12 @@ def serve(in_paths, out_paths, verifiers, frag_cnts, timeout_s=120.0, idle_s=0.0
     ins = [tile.Link.shm_join(p) for p in in_paths]
     outs = [tile.Link.shm_join(p) for p in out_paths]
     T = len(outs)
+    rr = round_robin_shares(rr_idx, rr_cnt, T)
     frag_cnts = list(frag_cnts)
     n_total = sum(frag_cnts)
     tile_kw.setdefault("gpu_parse", 2)
-    vms = [tile.VerifyMuxTile(ins, outs[k], verifiers[k], round_robin_idx=k, round_robin_cnt=T, log_max=log_max,
-                              **tile_kw) for k in range(T)]
+    vms = [tile.VerifyMuxTile(ins, outs[k], verifiers[k], round_robin_idx=rr[k], round_robin_cnt=rr_cnt or T,
+                              log_max=log_max, **tile_kw) for k in range(T)]
     try:
         t_start = time.monotonic()
         for k, vm in enumerate(vms):
@@ -177,7 +201,7 @@ def serve(in_paths, out_paths, verifiers, frag_cnts, timeout_s=120.0, idle_s=0.0
         magg = {k: int(sum(m[k] for m in mux)) for k in mux[0]}
         agg["overrun_polling"], agg["overrun_reading"] = magg["overrun_polling"], magg["overrun_reading"]
         agg["overrun"] = agg["lapped"] + agg["overrun_polling"] + agg["overrun_reading"]
-        res = {"pid": os.getpid(), "tiles": T, "in_links": len(ins), "frags": n_total,
+        res = {"pid": os.getpid(), "tiles": T, "rr_idx": rr_idx, "rr_cnt": rr_cnt or T, "in_links": len(ins), "frags": n_total,
                "t_start": t_start, "t_done": t_done, "stats": agg, "mux": magg, "per_tile": per,
                "final": [int(vm.final_cnt()) for vm in vms],
                "batch_latency_ms": {"p50": round(float(np.percentile(lat, 50)), 3) if len(lat) else None,
@@ -192,17 +216,29 @@ def serve(in_paths, out_paths, verifiers, frag_cnts, timeout_s=120.0, idle_s=0.0
             vm.close()
 
 
-def gpu_verifiers(T, a):
-    """The product's verifiers: one GPU engine per tile (its own ring slots,
-    the device's shared comb table), opened, reserved and warmed."""
-    from . import _lib
-    device = a.device
-    if a.device_rank >= 0:
-        ndev = _lib.lib().fdgpu_device_count()
+def tile_devices(T, a, ndev=None):
+    """The HIP device of each of this process's T tiles: --devices (tile k on
+    the (k % n)-th), else --device-rank % the visible devices, else --device."""
+    if a.devices:
+        devs = [int(x) for x in a.devices.split(",") if x.strip()]
+    elif a.device_rank >= 0:
+        if ndev is None:
+            from . import _lib
+            ndev = _lib.lib().fdgpu_device_count()
         if ndev < 1:
             raise SystemExit("engine_proc: no HIP device visible")
-        device = a.device_rank % ndev
-    engines = open_engines(T, device, a.batch, a.inflight, pair=a.pair, spread=a.spread, gather=a.gpu_parse == 2)
+        devs = [a.device_rank % ndev]
+    else:
+        devs = [a.device]
+    return [devs[k % len(devs)] for k in range(T)]
+
+
+def gpu_verifiers(T, a):
+    """The product's verifiers: one GPU engine per tile (its own ring slots,
+    the device's shared comb table) on the tile's device, opened, reserved
+    and warmed."""
+    devs = tile_devices(T, a)
+    engines = open_engines(T, devs, a.batch, a.inflight, pair=a.pair, spread=a.spread, gather=a.gpu_parse == 2)
     vers = [tile.EngineVerifier([engines[k]]) for k in range(T)]
 
     def close():
@@ -210,7 +246,7 @@ def gpu_verifiers(T, a):
             v.close()
         for e in engines:
             e.close()
-    return vers, close, {"device": device}
+    return vers, close, {"device": devs[0], "devices": devs}
 
 
 def main(argv=None, make_verifiers=gpu_verifiers):
@@ -223,6 +259,12 @@ def main(argv=None, make_verifiers=gpu_verifiers):
     ap.add_argument("--frags", required=True, help="frags the producer publishes on each in link (N or N1,N2,...)")
     ap.add_argument("--device", type=int, default=0)
     ap.add_argument("--device-rank", type=int, default=-1, help="device = this rank %% the visible devices")
+    ap.add_argument("--devices", default="", help="','-separated HIP devices: tile k's engine on the (k %% n)-th "
+                                                  "(overrides --device / --device-rank)")
+    ap.add_argument("--rr-idx", type=int, default=0,
+                    help="global round-robin index of this process's first tile (tile k takes share rr_idx + k)")
+    ap.add_argument("--rr-cnt", type=int, default=0,
+                    help="verify tiles over every engine process reading these in links (0: this process's)")
     ap.add_argument("--batch", type=int, default=16384)
     ap.add_argument("--inflight", type=int, default=8)
     ap.add_argument("--batch-sig-max", type=int, default=0)
@@ -256,7 +298,8 @@ def main(argv=None, make_verifiers=gpu_verifiers):
                     cpus=[int(x) for x in a.cpus.split(",") if x] or None, ready_file=a.ready_file or None,
                     log_max=(sum(cnts) + 16) if a.log else 0, hashmap_seed=a.seed, batch_txn_max=a.batch,
                     inflight_max=a.inflight, batch_wait_us=a.wait_us, batch_sig_max=a.batch_sig_max,
-                    gpu_parse=a.gpu_parse, flow_control=bool(a.out_flow_control), **guard)
+                    gpu_parse=a.gpu_parse, flow_control=bool(a.out_flow_control), rr_idx=a.rr_idx, rr_cnt=a.rr_cnt,
+                    **guard)
     finally:
         close()
     res.update(info)

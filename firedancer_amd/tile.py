@@ -133,7 +133,8 @@ class DTileCfg(c.Structure):
 
 
 class DTileStats(c.Structure):
-    _fields_ = [(n, c.c_uint64) for n in ("in_frags", "dup", "published", "overrun", "corrupt", "parse_fail")]
+    _fields_ = [(n, c.c_uint64) for n in ("in_frags", "dup", "published", "overrun", "corrupt", "parse_fail",
+                                          "done_ns")]
 
     def as_dict(self):
         return {n: getattr(self, n) for n, _ in self._fields_}
@@ -250,6 +251,7 @@ def lib():
         "fdt_tcache_reset": (None, [vp]),
         "fdt_tcache_query": (c.c_int, [vp, u64]),
         "fdt_tcache_insert": (c.c_int, [vp, u64]),
+        "fdt_tcache_insert_many": (u64, [vp, vp, u64]),
         "fdt_hash": (u64, [u64, vp, u64]),
         "fdt_txn_footprint": (u64, [u64, u64]),
         "fdt_txn_parse": (u64, [vp, u64, vp, c.POINTER(ParseCounters)]),
@@ -274,6 +276,7 @@ def lib():
         "fdgpu_dtile_delete": (None, [vp]),
         "fdgpu_dtile_step": (i64, [vp]),
         "fdgpu_dtile_stats": (None, [vp, c.POINTER(DTileStats)]),
+        "fdgpu_dtile_tcache": (vp, [vp]),
         "fdgpu_producer_start": (vp, [vp, u64, u64, vp, u64, u64, vp, vp, vp, u64, c.c_double]),
         "fdgpu_replay_verify": (c.c_int, [Verifier, vp, vp, vp, u64, u64, u64, vp]),
         "fdgpu_fec_roots_verify": (c.c_int, [Verifier, vp, vp, vp, c.c_int, u64, u64, vp]),
@@ -1269,6 +1272,13 @@ class DedupTile:
         s = DTileStats()
         lib().fdgpu_dtile_stats(self._t, c.byref(s))
         return s.as_dict()
+
+    def tcache_fill(self, n, seed=1):
+        """Insert n pseudo-random tags into the tile's tcache (a long-running
+        tile's steady state: the ring full, every insert evicting); returns
+        the dups among them."""
+        tags = np.random.default_rng(seed).integers(1, 2 ** 63, size=n, dtype=np.uint64)
+        return int(lib().fdt_tcache_insert_many(lib().fdgpu_dtile_tcache(self._t), tags.ctypes.data, n))
 
     def fork_sandboxed(self, frag_target, idle_s=10.0, logfile_fd=2):
         """Runs this tile in a forked child process inside the tiles' seccomp

@@ -115,6 +115,16 @@ void     fdt_tcache_reset    ( void * tcache );
 int      fdt_tcache_query    ( void const * tcache, uint64_t tag );
 /* returns dup (1: already present, unchanged; 0: inserted, oldest evicted) */
 int      fdt_tcache_insert   ( void * tcache, uint64_t tag );
+/* fdt_tcache_insert of tags[0..n) in order; returns how many were dups
+   (e.g. to bring a tcache to its steady state -- full ring, every insert
+   evicting -- before a measurement) */
+uint64_t fdt_tcache_insert_many( void * tcache, uint64_t const * tags, uint64_t n );
+/* Cache hints for a coming insert (no effect on the contents): the map line
+   a query / insert of tag starts its probe at, and the map line of the tag
+   the ahead-th next insert will evict.  A deep tcache's map (4,194,302 deep:
+   64 MB) misses every cache on both. */
+void     fdt_tcache_prefetch      ( void const * tcache, uint64_t tag );
+void     fdt_tcache_prefetch_evict( void const * tcache, uint64_t ahead );
 
 /* A small tcache as a ring scan: the verify tile's 16-deep tcache
    (fd_verify.h:6-7) answers exactly as fdt_tcache_query / fdt_tcache_insert
@@ -623,6 +633,7 @@ typedef struct {
 
 typedef struct {
   uint64_t in_frags, dup, published, overrun, corrupt, parse_fail;
+  uint64_t done_ns;   /* fdgpu_dtile_run_sandboxed: CLOCK_MONOTONIC when the run's last frag was consumed (0: none) */
 } fdgpu_dtile_stats_t;
 
 typedef struct fdgpu_dtile fdgpu_dtile_t;
@@ -630,6 +641,13 @@ fdgpu_dtile_t * fdgpu_dtile_new   ( fdgpu_dtile_cfg_t const * cfg );
 void            fdgpu_dtile_delete( fdgpu_dtile_t * t );
 int64_t         fdgpu_dtile_step  ( fdgpu_dtile_t * t );   /* frags consumed this step */
 void            fdgpu_dtile_stats ( fdgpu_dtile_t const * t, fdgpu_dtile_stats_t * out );
+/* The dedup tile's tcache (depth cfg.tcache_depth), e.g. to fill it before a
+   measurement (fdt_tcache_insert_many). */
+void *          fdgpu_dtile_tcache( fdgpu_dtile_t * t );
+/* Moves the tcache into memory of this process's own (huge pages where the
+   host offers them), contents kept: a forked child calls it before entering
+   the sandbox (fdgpu_dtile_run_sandboxed does).  0, or -1 (no memory). */
+int             fdgpu_dtile_rehome( fdgpu_dtile_t * t );
 
 /* ------------------------------------ TPU reassembly (§8(f) row 2) */
 

@@ -87,3 +87,26 @@ def test_smt_siblings_of_this_host():
     from firedancer_amd import workload
     s = workload._smt_siblings(0)
     assert 0 in s and all(isinstance(c, int) for c in s)
+
+
+def test_tile_cmd_xproc_runs():
+    """The cross-process lines: every run of bench.TILE_RUNS_XPROC reaches
+    bench_tile with its engine-process count and dedup switch (the sweep's
+    seventh and eighth fields), among them two engine processes sharing the
+    links and the e2e runs through the sandboxed dedup."""
+    cmd = bench.tile_cmd(0, [3, 4, 5, 6, 7], "/tmp/z.npz", "/tmp/z.jsonl", bench.TILE_RUNS_XPROC, xproc=True)
+    args = bench_tile.make_parser().parse_args(cmd[2:])
+    assert args.xproc == 1 and args.reps == bench.TILE_REPS_XPROC
+    assert args.dedup_depth == 4194302                  # the reference's signature_cache_size (default.toml:910)
+    runs = [tuple(float(x) for x in r.split(",")) for r in args.sweep.split(";")]
+    assert len(runs) == len(bench.TILE_RUNS_XPROC)
+    seen = set()
+    for (name, tiles_n, prods, rate, *rest), run in zip(bench.TILE_RUNS_XPROC, runs):
+        assert run[:5] == (tiles_n, bench.TILE_BATCH, bench.TILE_INFLIGHT, rate, prods)
+        if rest:
+            procs, dedup = rest
+            assert len(run) == 8 and run[6] == procs and run[7] == dedup and tiles_n % procs == 0
+            seen.add((procs > 1, bool(dedup)))
+        else:
+            assert len(run) == 5
+    assert (True, False) in seen and (False, True) in seen

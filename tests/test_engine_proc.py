@@ -94,17 +94,48 @@ def _npz(tmp_path, ps):
     return p
 
 
-def _xproc_vs_model(tmp_path, ps, oracle, tiles=1, dedup=True, engine_cmd=None, **kw):
-    """producer process -> engine process (T gather-mode mux tiles, round
-    robin over one quic -> verify link) -> sandboxed dedup process; every
-    frag's outcome, every tile's published stream and the dedup tile's
-    output against the sequential models."""
+def _sig0(f):
+    payload, raw = tile.split_verify_output(f)
+    so = tile.txn_decode(raw)["signature_off"]
+    return payload[so:so + 64]
+
+
+def _check_dedup_multi_link(tile_outs, dedup_out):
+    """The dedup tile over several verify -> dedup links: which link it
+    services first is a matter of timing (the mux's round robin over ready
+    links), so the check is by content: with the reference's tcache depth
+    (4,194,302, far above these streams) every distinct first signature the
+    verify tiles published comes out exactly once, as one of the frags that
+    carried it, and the frags of each link keep that link's order."""
+    by_sig = {}
+    for k, frags in enumerate(tile_outs):
+        for j, f in enumerate(frags):
+            by_sig.setdefault(_sig0(f), []).append((k, j, f))
+    got = [_sig0(f) for f in dedup_out]
+    assert len(got) == len(set(got)) == len(by_sig)
+    pos = {k: -1 for k in range(len(tile_outs))}
+    for f, s in zip(dedup_out, got):
+        src = [(k, j) for k, j, g in by_sig[s] if g == f]
+        assert src, "dedup published a frag no verify tile published"
+        if len(by_sig[s]) == 1:                       # carried by one link only: that link's order holds
+            k, j = src[0]
+            assert j > pos[k]
+            pos[k] = j
+
+
+def _xproc_vs_model(tmp_path, ps, oracle, tiles=1, dedup=True, engine_cmd=None, engine_procs=1, **kw):
+    """producer process -> engine process(es) (T gather-mode mux tiles, round
+    robin over one quic -> verify link; with engine_procs=E, E processes of
+    T/E tiles each take global shares rr_idx..rr_idx+T/E-1 of T) ->
+    sandboxed dedup process; every frag's outcome, every tile's published
+    stream and the dedup tile's output against the sequential models."""
     seed, dseed = 0x5EEDF00D, 0xD5
     exp = [tile_model.verify_tile_model(ps, seed, lambda a, t: oracle.verify_txns(a, t), rr_idx=k, rr_cnt=tiles)
            for k in range(tiles)]
     n_pub = sum(len(pub) for _, pub in exp)
     res = xproc.run(_npz(tmp_path, ps), len(ps), tiles=tiles, producers=1, seed=seed, dedup=dedup,
-                    dedup_frags=n_pub, log=True, engine_cmd=engine_cmd, timeout=180, **kw)
+                    dedup_frags=n_pub, log=True, engine_cmd=engine_cmd, timeout=180, engine_procs=engine_procs, **kw)
+    assert res["engine_procs"] == engine_procs and len(res["engines"]) == engine_procs
     st = res["engine"]["stats"]
     assert st["verify_errors"] == 0 and st["corrupt"] == 0 and st["overrun"] == 0
     for k, (exp_out, exp_pub) in enumerate(exp):
@@ -116,9 +147,12 @@ def _xproc_vs_model(tmp_path, ps, oracle, tiles=1, dedup=True, engine_cmd=None, 
         ds = res["dedup"]["stats"]
         assert res["dedup"]["exit"] == 0 and ds["overrun"] == 0 and ds["in_frags"] == n_pub
         if tiles == 1:                     # one in link: the dedup tile's order is the verify tile's
-            exp_d = tile_model.dedup_model([f for _, f in res["out_frags"][0]], dseed, 1 << 14)
+            exp_d = tile_model.dedup_model([f for _, f in res["out_frags"][0]], dseed, xproc.DEDUP_TCACHE_DEPTH)
             assert [f for _, f in res["dedup_frags"]] == exp_d
+        else:
+            _check_dedup_multi_link([[f for _, f in o] for o in res["out_frags"]], [f for _, f in res["dedup_frags"]])
         assert all(sig == 0 for sig, _ in res["dedup_frags"])
+        assert res["dedup"]["stats"]["done_ns"] > 0
     return res, exp
 
 
@@ -136,6 +170,36 @@ def test_engine_process_two_tiles_cpu(tmp_path, oracle):
     _xproc_vs_model(tmp_path, ps, oracle, tiles=2, engine_cmd=CPU_ENGINE, depth=1 << 12, batch=64, inflight=3)
 
 
+def test_two_engine_processes_share_link_cpu(tmp_path, oracle):
+    """Two engine processes on one shared quic -> verify link, one tile each,
+    as global tiles 0 and 1 of 2 (--rr-idx 0/1 --rr-cnt 2, fd_verify.c:46):
+    each equals tile_model(rr_idx, 2) frag by frag, and the sandboxed dedup
+    over both out links publishes every distinct verified txn once."""
+    ps = _mixed_stream(900, seed=75)
+    res, exp = _xproc_vs_model(tmp_path, ps, oracle, tiles=2, engine_procs=2, engine_cmd=CPU_ENGINE, depth=1 << 12,
+                               batch=64, inflight=3)
+    assert [e["rr_idx"] for e in res["engines"]] == [0, 1] and all(e["rr_cnt"] == 2 for e in res["engines"])
+    assert len({e["pid"] for e in res["engines"]}) == 2
+    assert all(len(pub) > 100 for _, pub in exp)
+
+
+def test_engine_proc_devices_and_round_robin_args():
+    """--devices maps tile k to the (k % n)-th device; --rr-idx/--rr-cnt
+    outside the tiles' range is refused."""
+    from firedancer_amd import engine_proc
+    import argparse
+    a = argparse.Namespace(devices="3,5", device_rank=-1, device=0)
+    assert engine_proc.tile_devices(3, a) == [3, 5, 3]
+    a = argparse.Namespace(devices="", device_rank=9, device=0)
+    assert engine_proc.tile_devices(2, a, ndev=8) == [1, 1]
+    a = argparse.Namespace(devices="", device_rank=-1, device=2)
+    assert engine_proc.tile_devices(1, a) == [2]
+    assert engine_proc.round_robin_shares(2, 8, 2) == [2, 3] and engine_proc.round_robin_shares(0, 0, 3) == [0, 1, 2]
+    for bad in ((1, 1, 1), (7, 8, 2), (-1, 4, 1), (0, 4, 0)):
+        with pytest.raises(ValueError):
+            engine_proc.round_robin_shares(*bad)
+
+
 @pytest.mark.gpu
 def test_engine_process_pipeline_gpu(tmp_path, oracle):
     """The deployable shape on the MI355X: the engine process's gather tile
@@ -146,6 +210,21 @@ def test_engine_process_pipeline_gpu(tmp_path, oracle):
     res, exp = _xproc_vs_model(tmp_path, ps, oracle, depth=1 << 12, batch=512, inflight=3)
     assert exp[0][0].count(0) > 1000 and res["engine"]["device"] == 0
     _xproc_vs_model(tmp_path, ps, oracle, tiles=2, depth=1 << 12, batch=512, inflight=3, dedup=False)
+
+
+@pytest.mark.gpu
+def test_engine_processes_multi_device_gpu(tmp_path, oracle):
+    """The multi-GPU form of the verify stage on the box's one GPU: two
+    engine processes sharing the quic -> verify link (global tiles 0 and 1
+    of 2), the sandboxed dedup over both out links at the reference's tcache
+    depth; then one process whose two tiles are placed by --devices 0,0 (on
+    an 8-GPU node: --devices 0,1,...)."""
+    ps = _mixed_stream(4000, seed=76)
+    res, _ = _xproc_vs_model(tmp_path, ps, oracle, tiles=2, engine_procs=2, depth=1 << 12, batch=512, inflight=3)
+    assert [e["devices"] for e in res["engines"]] == [[0], [0]]
+    res, _ = _xproc_vs_model(tmp_path, ps, oracle, tiles=2, engine_procs=1, proc_devices=["0,0"], depth=1 << 12,
+                             batch=512, inflight=3)
+    assert res["engine"]["devices"] == [0, 0]
 
 
 @pytest.mark.gpu

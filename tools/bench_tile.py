@@ -66,8 +66,9 @@ def make_parser():
                     help="GPU_MAX_HW_QUEUES for this process (applied before HIP starts; 0: the environment's)")
     ap.add_argument("--out", default="")
     ap.add_argument("--sweep", default="",
-                    help="';'-separated runs of 'tiles,batch,inflight,rate[,producers[,batch_sig_max]]' over the "
-                         "same txns (batch_sig_max 0: --batch-sig-max)")
+                    help="';'-separated runs of 'tiles,batch,inflight,rate[,producers[,batch_sig_max[,engine_procs"
+                         "[,dedup]]]]' over the same txns (batch_sig_max 0: --batch-sig-max; engine_procs and dedup: "
+                         "xproc runs, 0 = the flags')")
     ap.add_argument("--payload-npz", default="",
                     help="take the frags from this .npz (arena, offs, sizes, modes, n_sig: bench.py's tile lines) "
                          "instead of generating --txns")
@@ -109,6 +110,11 @@ def make_parser():
                     help="(in-process mux) link memory faulted in before the run: 4k or thp (anonymous 2 MB "
                          "pages); empty: numpy pages faulted in by their first use")
     ap.add_argument("--dedup", type=int, default=0, help="(xproc) 1: a sandboxed dedup process reads the out links")
+    ap.add_argument("--dedup-depth", type=int, default=4194302,
+                    help="(xproc) the dedup tile's tcache depth (the reference's signature_cache_size)")
+    ap.add_argument("--engine-procs", type=int, default=1,
+                    help="(xproc) engine processes sharing the quic -> verify links, tiles / E tiles each (global "
+                         "round-robin shares, engine_proc --rr-idx / --rr-cnt)")
     ap.add_argument("--device-rank", type=int, default=-1,
                     help="(bench.py's ranks) the GPU every tile's engine uses is this rank %% the visible devices: the "
                          "child counts them, so its parent rank starts no HIP runtime of its own before the tiles run")
@@ -164,11 +170,15 @@ def main():
                          cpus=cpus, device=args.device if args.device >= 0 else None)
         else:
             run_once(args, ps, arena, offs, sizes, n_sig, modes, int(run[0]), int(run[1]), int(run[2]), run[3])
+    procs0, dedup0 = args.engine_procs, args.dedup
     for run in runs:
         tiles_n, batch, inflight, rate = run[:4]
-        # a fifth field sets the run's quic links (producers), a sixth its batches' signature cap
+        # a fifth field sets the run's quic links (producers), a sixth its batches' signature cap, a seventh
+        # and eighth (xproc) its engine processes and whether the sandboxed dedup reads the out links
         args.producers = int(run[4]) if len(run) > 4 else int(tiles_n) if args.producers_same_as_tiles else prods0
         args.batch_sig_max = int(run[5]) if len(run) > 5 and run[5] > 0 else sig_max0
+        args.engine_procs = int(run[6]) if len(run) > 6 and run[6] > 0 else procs0
+        args.dedup = int(run[7]) if len(run) > 7 else dedup0
         args.depth_lg = args.depth_lg_paced if rate > 0 and args.depth_lg_paced else depth_lg
         if args.xproc:
             res = run_once_xproc(args, n_sig, modes, len(ps), int(tiles_n), int(batch), int(inflight), rate,
@@ -181,7 +191,7 @@ def main():
         line = json.dumps(res)
         print(line, flush=True)
         lines.append(line)
-        ok &= res["published_ok"] and res["counters"]["overrun"] == 0
+        ok &= res["published_ok"] and res["counters"]["overrun"] == 0 and res.get("dedup_ok", True)
     if args.out:
         with open(args.out, "w") as f:
             f.write("\n".join(lines) + "\n")
@@ -202,13 +212,15 @@ def run_once_xproc(args, n_sig, modes, n_payloads, tiles_n, batch, inflight, rat
     reps = 1 if prefill else max(1, getattr(args, "paced_reps", 1))
     cpus = cpus or workload.physical_cpus()[getattr(args, "cpu_offset", 0):] or workload.physical_cpus()
     dev_rank = args.device_rank if args.device_rank >= 0 else max(args.device, 0)
+    E = max(1, getattr(args, "engine_procs", 1))
     r = xproc.run(npz, n_payloads, tiles=tiles_n, producers=P, mode="prefill" if prefill else "paced",
                   rate=0.0 if prefill else rate, reps=reps, depth=1 << args.depth_lg, batch=batch, inflight=inflight,
                   wait_us=args.wait_us, batch_sig_max=getattr(args, "batch_sig_max", 0), pages=args.pages,
                   cpus=cpus[:P + tiles_n + 1], device_rank=dev_rank, dedup=bool(args.dedup),
                   lap_guard=bool(args.lap_guard), pair=args.pair, spread=args.spread, hw_queues=args.hw_queues,
                   dedup_frags=int((modes == 0).sum()) * (sum(xproc.quic_feed.frag_counts(n_payloads, P,
-                                  "prefill" if prefill else "paced", reps)) // n_payloads))
+                                  "prefill" if prefill else "paced", reps)) // n_payloads),
+                  engine_procs=E, dedup_depth=getattr(args, "dedup_depth", xproc.DEDUP_TCACHE_DEPTH))
     er, feed = r["engine"], r["feed"]
     n_total = r["txns"]
     wall = r["wall_s"]
@@ -224,6 +236,7 @@ def run_once_xproc(args, n_sig, modes, n_payloads, tiles_n, batch, inflight, rat
         "wall_s": round(wall, 4), "producer_s": round(max(feed["producer_s"]), 4),
         "producer_published": int(sum(feed["published"])), "gpus": args.gpus, "tiles": tiles_n,
         "batch_txn_max": batch, "inflight": inflight, "engines": tiles_n, "engine_slots": inflight,
+        "engine_procs": E, "engine_pids": er["pid"],
         "batch_sig_max": getattr(args, "batch_sig_max", 0) or batch * 12, "rate_target": rate, "prefill": prefill,
         "link_depth": 1 << args.depth_lg, "offered_txns_per_s": None if prefill else feed["offered_per_s"],
         "stream_reps": reps, "lap_guard": int(args.lap_guard),
@@ -235,7 +248,13 @@ def run_once_xproc(args, n_sig, modes, n_payloads, tiles_n, batch, inflight, rat
         "in_huge_bytes": r["in_huge_bytes"], "engine_pid": er["pid"], "feed_pid": feed["pid"],
     }
     if "dedup" in r:
+        # with the dedup in the loop the run is timed to its last frag (xproc: wall_s), and the verify -> dedup
+        # links are reliable: every frag the verify tiles published must have reached it, nothing overrun
         res["dedup"] = r["dedup"]
+        res["dedup_tcache_depth"] = getattr(args, "dedup_depth", xproc.DEDUP_TCACHE_DEPTH)
+        ds = r["dedup"]["stats"]
+        res["dedup_ok"] = (r["dedup"]["exit"] == 0 and ds["overrun"] == 0 and ds["corrupt"] == 0
+                           and ds["in_frags"] == agg["published"] and ds["published"] + ds["dup"] == ds["in_frags"])
     res["published_ok"] = agg["published"] == res["expected_published"]
     return res
 

@@ -52,7 +52,8 @@ def main(argv=None):
     ap.add_argument("--rate", type=float, default=0.0, help="paced: frags/s over all links (0: unpaced)")
     ap.add_argument("--reps", type=int, default=1)
     ap.add_argument("--cpus", default="", help="producer j pinned to the j-th CPU")
-    ap.add_argument("--wait-file", default="", help="start publishing once this file exists")
+    ap.add_argument("--wait-file", action="append", default=[],
+                    help="start publishing once this file exists (repeat: once all of them exist)")
     ap.add_argument("--timeout", type=float, default=120.0)
     ap.add_argument("--result", default="")
     a = ap.parse_args(argv)
@@ -62,11 +63,11 @@ def main(argv=None):
     P = len(links)
     fd = feeds(offs, sizes, P, a.mode, a.reps)
     cpus = [int(x) for x in a.cpus.split(",") if x]
-    if a.wait_file:
-        t0 = time.monotonic()
-        while not os.path.exists(a.wait_file):
+    t0 = time.monotonic()
+    for wf in a.wait_file:
+        while not os.path.exists(wf):
             if time.monotonic() - t0 > a.timeout:
-                raise SystemExit("quic_feed: timed out waiting for " + a.wait_file)
+                raise SystemExit("quic_feed: timed out waiting for " + wf)
             time.sleep(0.0005)
     keep = os.sched_getaffinity(0)
     prods = []

@@ -7,9 +7,11 @@ starts
 
   * the QUIC side: tools/quic_feed.py, one producer thread per quic -> verify
     link (a process that never touches the GPU);
-  * the engine process: python -m firedancer_amd.engine_proc, T gather-mode
+  * the engine processes: python -m firedancer_amd.engine_proc, T gather-mode
     verify mux tiles over every in link, tile k publishing into its own
-    verify -> dedup link;
+    verify -> dedup link -- in one process, or spread over E processes that
+    share the in links, process p running global tiles p*T/E .. (p+1)*T/E-1
+    of T (--rr-idx / --rr-cnt: fd_verify.c:46's seq % verify_tile_cnt);
   * optionally the dedup tile: python -m firedancer_amd.dedup_proc, a
     sandboxed child reading every verify -> dedup link;
 
@@ -35,6 +37,9 @@ from firedancer_amd import tile  # noqa: E402
 import quic_feed  # noqa: E402
 
 OUT_DEPTH = 1 << 14
+# the dedup tile's tcache depth: the reference's signature_cache_size
+# (src/app/fdctl/config/default.toml:910, wired at fd_frankendancer.c:263)
+DEDUP_TCACHE_DEPTH = 4194302
 
 
 def _wait_file(path, procs, timeout):
@@ -65,19 +70,28 @@ def _finish(p, timeout, what):
 def run(npz, n_payloads, tiles=1, producers=1, mode="paced", rate=0.0, reps=1, depth=1 << 14, batch=16384,
         inflight=8, wait_us=200.0, batch_sig_max=0, pages="4k", cpus=None, device_rank=0, dedup=False,
         dedup_frags=0, log=False, lap_guard=True, pair=2, spread=2, seed=0x5EEDF00D, timeout=300.0,
-        hw_queues=32, engine_cmd=None):
+        hw_queues=32, engine_cmd=None, engine_procs=1, proc_devices=None, dedup_depth=DEDUP_TCACHE_DEPTH):
     """One cross-process run over the payloads in `npz` (arena, offs, sizes;
     n_payloads of them).  engine_cmd: the engine process's command before
     its arguments (default: python -m firedancer_amd.engine_proc; the CPU
-    tests run the same loop over their checker instead).  Returns {engine, feed, dedup, wall_s, txns_per_s,
-    ...}; with log=True also the tiles' per-frag outcomes (engine["logs"]:
-    [(seqs, codes)] per tile) and the out links' frags (out_frags: per tile
-    [(sig, payload)]) and the dedup tile's out frags (dedup_frags)."""
+    tests run the same loop over their checker instead).  engine_procs: E
+    engine processes over the same in links, tiles // E tiles each;
+    proc_devices: per process the --devices string (default: every process
+    --device-rank device_rank).  Returns {engine, engines, feed, dedup,
+    wall_s, txns_per_s, ...} (engine: the processes' stats combined,
+    engines: each process's own); with log=True also the tiles' per-frag
+    outcomes (logs: [(seqs, codes)] per global tile) and the out links'
+    frags (out_frags: per tile [(sig, payload)]) and the dedup tile's out
+    frags (dedup_frags)."""
     cpus = list(cpus or [])
+    E = max(1, engine_procs)
+    if tiles % E:
+        raise ValueError(f"{tiles} tiles over {E} engine processes")
     d = tempfile.mkdtemp(prefix="fdgpu_xp_", dir="/dev/shm")
     procs = []
     try:
         P, T = producers, tiles
+        TE = T // E
         qv = [os.path.join(d, f"qv{j}") for j in range(P)]
         vd = [os.path.join(d, f"vd{k}") for k in range(T)]
         ins = [tile.Link.shm_create(p, depth, tile.TPU_MTU, pages=pages) for p in qv]
@@ -87,20 +101,25 @@ def run(npz, n_payloads, tiles=1, producers=1, mode="paced", rate=0.0, reps=1, d
         if dedup:
             tile.Link.shm_create(dp, 1 << 16, tile.TPU_DCACHE_MTU)
         cnts = quic_feed.frag_counts(n_payloads, P, mode, reps)
-        ready = os.path.join(d, "engine.ready")
+        readies = [os.path.join(d, f"engine{e}.ready") for e in range(E)]
         pcpu, tcpu = cpus[:P], cpus[P:P + T]
-        eng_cmd = [*(engine_cmd or [sys.executable, "-m", "firedancer_amd.engine_proc"]), *sum([["--in", p] for p in qv], []),
-                   *sum([["--out", p] for p in vd], []), "--frags", ",".join(map(str, cnts)),
-                   "--device-rank", str(device_rank), "--batch", str(batch), "--inflight", str(inflight),
-                   "--batch-sig-max", str(batch_sig_max), "--wait-us", str(wait_us), "--seed", hex(seed),
-                   "--pair", str(pair), "--spread", str(spread), "--lap-guard", str(int(lap_guard)),
-                   "--hw-queues", str(hw_queues), "--ready-file", ready, "--timeout", str(timeout)]
-        if tcpu:
-            eng_cmd += ["--cpus", ",".join(map(str, tcpu))]
-        if dedup:                            # verify -> dedup links are reliable (fd_topo): credits from the dedup's fseq
-            eng_cmd += ["--out-flow-control", "1"]
-        if log:
-            eng_cmd += ["--log", os.path.join(d, "log.npz")]
+        eng_cmds = []
+        for e in range(E):
+            c = [*(engine_cmd or [sys.executable, "-m", "firedancer_amd.engine_proc"]),
+                 *sum([["--in", p] for p in qv], []), *sum([["--out", p] for p in vd[e * TE:(e + 1) * TE]], []),
+                 "--frags", ",".join(map(str, cnts)), "--rr-idx", str(e * TE), "--rr-cnt", str(T),
+                 "--batch", str(batch), "--inflight", str(inflight),
+                 "--batch-sig-max", str(batch_sig_max), "--wait-us", str(wait_us), "--seed", hex(seed),
+                 "--pair", str(pair), "--spread", str(spread), "--lap-guard", str(int(lap_guard)),
+                 "--hw-queues", str(hw_queues), "--ready-file", readies[e], "--timeout", str(timeout)]
+            c += ["--devices", proc_devices[e]] if proc_devices else ["--device-rank", str(device_rank)]
+            if tcpu:
+                c += ["--cpus", ",".join(map(str, tcpu[e * TE:(e + 1) * TE]))]
+            if dedup:                        # verify -> dedup links are reliable (fd_topo): credits from the dedup's fseq
+                c += ["--out-flow-control", "1"]
+            if log:
+                c += ["--log", os.path.join(d, f"log{e}.npz")]
+            eng_cmds.append(c)
         feed_cmd = [sys.executable, os.path.join(REPO, "tools", "quic_feed.py"), *sum([["--link", p] for p in qv], []),
                     "--npz", npz, "--mode", mode, "--rate", str(rate), "--reps", str(reps)]
         if pcpu:
@@ -109,34 +128,41 @@ def run(npz, n_payloads, tiles=1, producers=1, mode="paced", rate=0.0, reps=1, d
         feed = None
         if mode == "prefill":                    # every frag published before the tiles start
             feed = _finish(subprocess.Popen(feed_cmd, **popen), timeout, "quic_feed")
-        eng = subprocess.Popen(eng_cmd, **popen)
-        procs.append(eng)
-        _wait_file(ready, [eng], timeout)
+        engs = [subprocess.Popen(c, **popen) for c in eng_cmds]
+        procs += engs
+        for r in readies:
+            _wait_file(r, engs, timeout)
         dd = None
         if dedup:
             dd_cmd = [sys.executable, "-m", "firedancer_amd.dedup_proc", *sum([["--in", p] for p in vd], []),
-                      "--out", dp, "--frags", str(dedup_frags or (1 << 62)), "--idle-s", "3", "--reliable", "1"]
+                      "--out", dp, "--frags", str(dedup_frags or (1 << 62)), "--idle-s", "3", "--reliable", "1",
+                      "--tcache-depth", str(dedup_depth)]
             if len(cpus) > P + T:
                 dd_cmd += ["--cpu", str(cpus[P + T])]
             dd = subprocess.Popen(dd_cmd, **popen)
             procs.append(dd)
         if mode != "prefill":
-            fp = subprocess.Popen(feed_cmd + ["--wait-file", ready], **popen)
+            fp = subprocess.Popen(feed_cmd + sum([["--wait-file", r] for r in readies], []), **popen)
             procs.append(fp)
             feed = _finish(fp, timeout, "quic_feed")
-        er = _finish(eng, timeout, "engine_proc")
-        res = {"engine": er, "feed": feed}
+        ers = [_finish(p, timeout, "engine_proc") for p in engs]
+        er = combine_engine_results(ers)
+        res = {"engine": er, "engines": ers, "feed": feed}
         if dd is not None:
             res["dedup"] = _finish(dd, 60, "dedup_proc")
         t0 = er["t_start"] if mode == "prefill" else max(er["t_start"], feed["t_start"])
-        wall = er["t_done"] - t0
+        # with the dedup in the loop the run ends when its last frag has gone through it
+        t_end = max(er["t_done"], res["dedup"]["stats"]["done_ns"] * 1e-9) if dd is not None else er["t_done"]
+        wall = t_end - t0
         n_total = sum(cnts)
         res.update({"wall_s": round(wall, 6), "txns": n_total, "txns_per_s": round(n_total / wall, 1),
-                    "frag_counts": cnts, "pages": pages, "link_depth": depth,
+                    "frag_counts": cnts, "pages": pages, "link_depth": depth, "engine_procs": E,
                     "in_huge_bytes": er.get("in_huge_bytes"), "feed_huge_bytes": feed.get("huge_bytes")})
         if log:
-            z = np.load(os.path.join(d, "log.npz"))
-            res["logs"] = [(z[f"seq{k}"], z[f"code{k}"]) for k in range(T)]
+            res["logs"] = []
+            for e in range(E):
+                z = np.load(os.path.join(d, f"log{e}.npz"))
+                res["logs"] += [(z[f"seq{k}"], z[f"code{k}"]) for k in range(TE)]
             res["out_frags"] = [[(m["sig"], bytes(f)) for m, f in ln.drain()] for ln in outs]
             if dedup:
                 res["dedup_frags"] = [(m["sig"], bytes(f)) for m, f in tile.Link.shm_join(dp).drain()]
@@ -148,6 +174,28 @@ def run(npz, n_payloads, tiles=1, producers=1, mode="paced", rate=0.0, reps=1, d
                 p.kill()
                 p.wait()
         shutil.rmtree(d, ignore_errors=True)
+
+
+def combine_engine_results(ers):
+    """The engine processes' results as one: counters summed (extremes as
+    extremes), started at the first process's start, done at the last's."""
+    if len(ers) == 1:
+        return ers[0]
+    out = dict(ers[0])
+    st = {}
+    for k in ers[0]["stats"]:
+        xs = [r["stats"][k] for r in ers]
+        st[k] = max(xs) if k.endswith(("_max", "_max_ns")) else min(xs) if k.endswith(("_min", "_min_ns")) else sum(xs)
+    out.update({"stats": st, "mux": {k: sum(r["mux"][k] for r in ers) for k in ers[0]["mux"]},
+                "tiles": sum(r["tiles"] for r in ers), "t_start": min(r["t_start"] for r in ers),
+                "t_done": max(r["t_done"] for r in ers), "pid": [r["pid"] for r in ers],
+                "per_tile": sum((r["per_tile"] for r in ers), []), "final": sum((r["final"] for r in ers), []),
+                "devices": sum((r.get("devices") or [r.get("device")] for r in ers), [])})
+    lat = [r["batch_latency_ms"] for r in ers]
+    out["batch_latency_ms"] = {"p50": max((x["p50"] for x in lat if x["p50"] is not None), default=None),
+                               "p99": max((x["p99"] for x in lat if x["p99"] is not None), default=None),
+                               "n": sum(x["n"] for x in lat), "note": "worst process's percentile"}
+    return out
 
 
 def save_payloads(ps, path):
