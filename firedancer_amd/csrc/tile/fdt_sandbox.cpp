@@ -19,6 +19,9 @@
      [4096, ...)      mcache: depth x fdt_frag_meta_t (fd_mcache.h:265-322)
      [dcache_off, ..) compact dcache for depth frags of <= mtu (fd_dcache.h) */
 #include <errno.h>
+#include <sched.h>
+#include <signal.h>
+#include <ucontext.h>
 #include <linux/audit.h>
 #include <linux/filter.h>
 #include <linux/seccomp.h>
@@ -28,6 +31,8 @@
 #include <sys/syscall.h>
 #include <time.h>
 #include <unistd.h>
+
+#include <vector>
 
 #include "../../../include/fd_verify_tile.h"
 
@@ -135,6 +140,107 @@ int fdt_sandbox_enter(int logfile_fd) {
   if (prctl(PR_SET_NO_NEW_PRIVS, 1, 0, 0, 0)) return -errno;
   if (syscall(__NR_seccomp, SECCOMP_SET_MODE_FILTER, 0, &prog)) return -errno;
   return 0;
+}
+
+/* ------------------------------------------------- engine process policy
+
+   The GPU engine process cannot run under the tiles' write/fsync policy: every
+   submission and completion of the HIP runtime is an ioctl on the device's
+   file descriptors, its worker threads wait on futexes and the runtime maps
+   and unmaps memory as it runs.  What it never needs once its engines are
+   open, warmed and registered is a NEW resource from outside the process:
+   no open, socket, exec, fork, ptrace, mount, kill of another process.  So
+   the engine process enters (after privileged init, as fd_topo_run.c:96-103
+   enters the tiles' policies) a policy that allows the resource-neutral
+   syscalls below, ioctl only on the device fds it already holds, clone only
+   for threads -- and kills the process on anything else, for every thread
+   (SECCOMP_FILTER_FLAG_TSYNC: the runtime's threads included).
+
+   Report mode (bring-up and tests): a syscall outside the list is refused
+   all the same -- it fails with EPERM instead of killing the process, and
+   is recorded (fdt_sandbox_report), so one run lists everything the
+   policy refused.  Nothing outside the list is ever carried out. */
+
+namespace {
+
+uint64_t g_refused_bits[8];        /* syscalls < 512 refused (report mode) */
+uint64_t g_refused_cnt;
+
+void report_sigsys(int, siginfo_t *si, void *uc_) {
+  const long nr = si->si_syscall;
+  if (nr >= 0 && nr < 512) __atomic_fetch_or(&g_refused_bits[nr >> 6], 1ull << (nr & 63), __ATOMIC_RELAXED);
+  __atomic_fetch_add(&g_refused_cnt, 1, __ATOMIC_RELAXED);
+  ((ucontext_t *)uc_)->uc_mcontext.gregs[REG_RAX] = -EPERM;     /* the call fails; it was not made */
+}
+
+/* the syscalls of a running engine process (the HIP runtime's submissions,
+   waits and memory management, the tiles' clocks and yields, the Python
+   loop around them), none of which reaches outside the process */
+const uint32_t ENGINE_ALLOW[] = {
+  __NR_read, __NR_write, __NR_pread64, __NR_pwrite64, __NR_readv, __NR_writev, __NR_lseek, __NR_fstat,
+  __NR_newfstatat, __NR_close, __NR_fsync, __NR_fdatasync, __NR_dup, __NR_fcntl,
+  __NR_mmap, __NR_munmap, __NR_mprotect, __NR_mremap, __NR_madvise, __NR_brk, __NR_mlock, __NR_munlock,
+  __NR_futex, __NR_sched_yield, __NR_nanosleep, __NR_clock_nanosleep, __NR_clock_gettime, __NR_clock_getres,
+  __NR_gettimeofday, __NR_select, __NR_pselect6, __NR_poll, __NR_ppoll, __NR_epoll_wait, __NR_epoll_pwait,
+  __NR_getpid, __NR_gettid, __NR_getppid, __NR_getuid, __NR_geteuid, __NR_getgid, __NR_getegid,
+  __NR_rt_sigprocmask, __NR_rt_sigaction, __NR_rt_sigreturn, __NR_sigaltstack, __NR_tgkill,
+  __NR_sched_getaffinity, __NR_sched_setaffinity, __NR_sched_getparam, __NR_sched_getscheduler,
+  __NR_set_robust_list, __NR_rseq, __NR_getrandom, __NR_membarrier, __NR_prctl, __NR_getrusage,
+  __NR_exit, __NR_exit_group,
+};
+
+}  // namespace
+
+int fdt_sandbox_engine_enter(const int *dev_fds, int dev_fd_cnt, int report) {
+  if (dev_fd_cnt < 0 || dev_fd_cnt > 64 || (dev_fd_cnt && !dev_fds)) return -EINVAL;
+  const uint32_t KILL = SECCOMP_RET_KILL_PROCESS, ALLOW = SECCOMP_RET_ALLOW;
+  const uint32_t DENY = report ? SECCOMP_RET_TRAP : KILL;
+  std::vector<sock_filter> f;
+  auto stmt = [&](uint16_t code, uint32_t k) { f.push_back(BPF_STMT(code, k)); };
+  auto jeq = [&](uint32_t k, uint8_t jt, uint8_t jf) { f.push_back(BPF_JUMP(BPF_JMP | BPF_JEQ | BPF_K, k, jt, jf)); };
+  stmt(BPF_LD | BPF_W | BPF_ABS, offsetof(struct seccomp_data, arch));
+  jeq(AUDIT_ARCH_X86_64, 1, 0);
+  stmt(BPF_RET | BPF_K, KILL);
+  stmt(BPF_LD | BPF_W | BPF_ABS, offsetof(struct seccomp_data, nr));
+  for (uint32_t nr : ENGINE_ALLOW) {
+    jeq(nr, 0, 1);
+    stmt(BPF_RET | BPF_K, ALLOW);
+  }
+  /* clone: threads only (CLONE_THREAD in the flags, arg 0); clone3: ENOSYS,
+     so the C library falls back to clone, whose flags the filter can read */
+  jeq(__NR_clone3, 0, 1);
+  stmt(BPF_RET | BPF_K, SECCOMP_RET_ERRNO | ENOSYS);
+  jeq(__NR_clone, 0, 4);
+  stmt(BPF_LD | BPF_W | BPF_ABS, offsetof(struct seccomp_data, args[0]));
+  f.push_back(BPF_JUMP(BPF_JMP | BPF_JSET | BPF_K, CLONE_THREAD, 0, 1));
+  stmt(BPF_RET | BPF_K, ALLOW);
+  stmt(BPF_RET | BPF_K, DENY);
+  /* ioctl: only on the device fds held at entry (/dev/kfd, the render nodes) */
+  jeq(__NR_ioctl, 0, (uint8_t)(2 + 2 * dev_fd_cnt));
+  stmt(BPF_LD | BPF_W | BPF_ABS, offsetof(struct seccomp_data, args[0]));
+  for (int i = 0; i < dev_fd_cnt; i++) {
+    jeq((uint32_t)dev_fds[i], 0, 1);
+    stmt(BPF_RET | BPF_K, ALLOW);
+  }
+  stmt(BPF_RET | BPF_K, DENY);
+  stmt(BPF_RET | BPF_K, DENY);
+  if (f.size() > 4096) return -E2BIG;
+  if (report) {
+    struct sigaction sa;
+    memset(&sa, 0, sizeof sa);
+    sa.sa_sigaction = report_sigsys;
+    sa.sa_flags = SA_SIGINFO | SA_NODEFER;
+    if (sigaction(SIGSYS, &sa, nullptr)) return -errno;
+  }
+  struct sock_fprog prog = {(unsigned short)f.size(), f.data()};
+  if (prctl(PR_SET_NO_NEW_PRIVS, 1, 0, 0, 0)) return -errno;
+  if (syscall(__NR_seccomp, SECCOMP_SET_MODE_FILTER, SECCOMP_FILTER_FLAG_TSYNC, &prog)) return -errno;
+  return 0;
+}
+
+uint64_t fdt_sandbox_report(uint64_t *bits8) {
+  for (int i = 0; i < 8; i++) bits8[i] = __atomic_load_n(&g_refused_bits[i], __ATOMIC_RELAXED);
+  return __atomic_load_n(&g_refused_cnt, __ATOMIC_RELAXED);
 }
 
 /* Dedup tile main loop inside the sandbox (a child process of whoever set

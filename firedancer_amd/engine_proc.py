@@ -53,6 +53,8 @@ from . import tile
 # tile engine owns `inflight` slot streams; two busy streams sharing a queue
 # serialise
 DEFAULT_HW_QUEUES = 32
+# the engine seccomp policy (fdt_sandbox_engine_enter) once the tiles run
+DEFAULT_SANDBOX = 0
 
 
 def warm_engines(engines, inflight, out_bytes=0, batch=64):
@@ -143,7 +145,7 @@ def round_robin_shares(rr_idx, rr_cnt, T):
 
 
 def serve(in_paths, out_paths, verifiers, frag_cnts, timeout_s=120.0, idle_s=0.02, cpus=None, ready_file=None,
-          log_max=0, on_start=None, rr_idx=0, rr_cnt=0, **tile_kw):
+          log_max=0, on_start=None, rr_idx=0, rr_cnt=0, sandbox=0, **tile_kw):
     """Join the links, run one gather-mode verify mux tile per out link
     (tile k: round-robin share rr_idx + k of rr_cnt (0: of this process's
     tiles) of every in link, verifiers[k], out link k)
@@ -151,7 +153,11 @@ def serve(in_paths, out_paths, verifiers, frag_cnts, timeout_s=120.0, idle_s=0.0
     the producers, until they are done and the tiles sit idle for idle_s --
     then return {stats, mux, per-tile stats, latencies, times}.  cpus: tile
     k's thread is pinned to cpus[k].  ready_file: created once the tiles are
-    polling (a producer process waits for it)."""
+    polling (a producer process waits for it).  sandbox: 1 -- from then on
+    the process runs inside the engine policy (tile.engine_sandbox_enter:
+    no open, socket, exec or fork; ioctl only on the GPU driver's fds held
+    now), 2 -- the same policy in report mode (a refused call fails and is
+    listed in the result instead of killing the process), 0 -- none."""
     ins = [tile.Link.shm_join(p) for p in in_paths]
     outs = [tile.Link.shm_join(p) for p in out_paths]
     T = len(outs)
@@ -171,6 +177,9 @@ def serve(in_paths, out_paths, verifiers, frag_cnts, timeout_s=120.0, idle_s=0.0
             with open(ready_file + ".tmp", "w") as f:
                 f.write(str(os.getpid()))
             os.rename(ready_file + ".tmp", ready_file)
+        in_huge = [ln.huge_bytes() for ln in ins]          # (reads /proc/self/smaps: before the sandbox)
+        if sandbox:                    # engines open, warmed, registered; tiles running (fd_topo_run.c:96-103)
+            tile.engine_sandbox_enter(report=sandbox == 2)
         idle_since, last = None, -1
         while any(vm.final_cnt() < n_total for vm in vms):
             now = time.monotonic()
@@ -207,13 +216,18 @@ def serve(in_paths, out_paths, verifiers, frag_cnts, timeout_s=120.0, idle_s=0.0
                "batch_latency_ms": {"p50": round(float(np.percentile(lat, 50)), 3) if len(lat) else None,
                                     "p99": round(float(np.percentile(lat, 99)), 3) if len(lat) else None,
                                     "n": int(len(lat))},
-               "in_huge_bytes": [ln.huge_bytes() for ln in ins]}
+               "in_huge_bytes": in_huge}
         if log_max:
             res["logs"] = [vm.log() for vm in vms]
+        res["sandbox"] = sandbox
+        if sandbox == 2:
+            res["sandbox_refused_calls"], res["sandbox_refused"] = tile.engine_sandbox_report()
         return res
     finally:
         for vm in vms:
             vm.close()
+        if sandbox == 2:                 # bring-up: what the policy refused, whatever the outcome
+            sys.stderr.write(f"engine_proc: sandbox refused {tile.engine_sandbox_report()}\n")
 
 
 def tile_devices(T, a, ndev=None):
@@ -281,6 +295,9 @@ def main(argv=None, make_verifiers=gpu_verifiers):
     ap.add_argument("--log", default="", help="write every frag's outcome (seq, code per tile) to this .npz")
     ap.add_argument("--timeout", type=float, default=120.0)
     ap.add_argument("--idle-ms", type=float, default=20.0)
+    ap.add_argument("--sandbox", type=int, default=DEFAULT_SANDBOX,
+                    help="1: enter the engine seccomp policy once the tiles run (no open/socket/exec/fork; ioctl "
+                         "only on the GPU driver's fds); 2: the same, refused calls reported instead of fatal; 0: none")
     ap.add_argument("--out-flow-control", type=int, default=0,
                     help="1: each tile takes its out link's credits from the link's fseq -- a reliable consumer "
                          "(the dedup process, dedup_proc --reliable 1) holds the tile back instead of being lapped")
@@ -293,25 +310,31 @@ def main(argv=None, make_verifiers=gpu_verifiers):
     T = len(a.out_paths)
     vers, close, info = make_verifiers(T, a)
     guard = {} if a.lap_guard else dict(lap_span_max=tile.LAP_OFF, lap_margin=tile.LAP_OFF)
+    # inside the sandbox nothing can be opened: the output files are opened
+    # now, and what writing them imports is imported now
+    res_f = open(a.result, "w") if a.result else None
+    log_f = open(a.log, "wb") if a.log else None
+    if log_f:
+        import zipfile  # noqa: F401  (np.savez imports it on first use)
     try:
         res = serve(a.in_paths, a.out_paths, vers, cnts, timeout_s=a.timeout, idle_s=a.idle_ms / 1e3,
                     cpus=[int(x) for x in a.cpus.split(",") if x] or None, ready_file=a.ready_file or None,
                     log_max=(sum(cnts) + 16) if a.log else 0, hashmap_seed=a.seed, batch_txn_max=a.batch,
                     inflight_max=a.inflight, batch_wait_us=a.wait_us, batch_sig_max=a.batch_sig_max,
                     gpu_parse=a.gpu_parse, flow_control=bool(a.out_flow_control), rr_idx=a.rr_idx, rr_cnt=a.rr_cnt,
-                    **guard)
+                    sandbox=a.sandbox, **guard)
     finally:
         close()
     res.update(info)
-    if a.log:
+    if log_f:
         logs = res.pop("logs")
-        np.savez(a.log, **{f"seq{k}": s for k, (s, _) in enumerate(logs)},
+        np.savez(log_f, **{f"seq{k}": s for k, (s, _) in enumerate(logs)},
                  **{f"code{k}": cd for k, (_, cd) in enumerate(logs)})
+        log_f.close()
     line = json.dumps(res)
-    if a.result:
-        with open(a.result + ".tmp", "w") as f:
-            f.write(line + "\n")
-        os.rename(a.result + ".tmp", a.result)
+    if res_f:
+        res_f.write(line + "\n")
+        res_f.close()
     print(line, flush=True)
     return 0
 

@@ -296,6 +296,8 @@ def lib():
         "fdt_link_new_sz": (c.c_int, [vp, u64, u64, u64, u64]),
         "fdt_link_join": (c.c_int, [vp, c.POINTER(LinkT)]),
         "fdt_sandbox_enter": (c.c_int, [c.c_int]),
+        "fdt_sandbox_engine_enter": (c.c_int, [vp, c.c_int, c.c_int]),
+        "fdt_sandbox_report": (u64, [vp]),
         "fdgpu_dtile_run_sandboxed": (None, [vp, u64, u64, c.POINTER(DTileStats), c.c_int]),
         "fdgpu_producer_join": (u64, [vp, c.POINTER(c.c_double)]),
         "fdgpu_producer_done": (c.c_int, [vp]),
@@ -338,6 +340,59 @@ def sandbox_enter(logfile_fd=2):
     r = lib().fdt_sandbox_enter(logfile_fd)
     if r:
         raise OSError(-r, "fdt_sandbox_enter failed")
+
+
+def device_fds():
+    """This process's open device fds of the GPU driver (/dev/kfd and the DRM
+    render nodes), the only fds the engine policy lets ioctl reach."""
+    out = []
+    for name in os.listdir("/proc/self/fd"):
+        try:
+            target = os.readlink(f"/proc/self/fd/{name}")
+        except OSError:
+            continue
+        if target == "/dev/kfd" or target.startswith("/dev/dri/"):
+            out.append(int(name))
+    return sorted(out)
+
+
+_SYSCALL_NAMES = {}
+
+
+def _syscall_names():
+    """x86-64 syscall numbers -> names (read before a sandbox is entered)."""
+    if not _SYSCALL_NAMES:
+        import re
+        for hdr in ("/usr/include/x86_64-linux-gnu/asm/unistd_64.h", "/usr/include/asm/unistd_64.h"):
+            if os.path.exists(hdr):
+                for m in re.finditer(r"#define __NR_(\w+)\s+(\d+)", open(hdr).read()):
+                    _SYSCALL_NAMES[int(m.group(2))] = m.group(1)
+                break
+    return _SYSCALL_NAMES
+
+
+def engine_sandbox_enter(report=False):
+    """Enters the engine process's seccomp policy for every thread of this
+    process (fdt_sandbox_engine_enter; irreversible): resource-neutral
+    syscalls, ioctl on the GPU driver's fds held now, threads only; anything
+    else kills the process -- or, with report=True, fails with EPERM and is
+    recorded for engine_sandbox_report().  Returns the device fds allowed."""
+    fds = device_fds()
+    _syscall_names()
+    arr = (c.c_int * max(1, len(fds)))(*fds)
+    r = lib().fdt_sandbox_engine_enter(arr, len(fds), int(bool(report)))
+    if r:
+        raise OSError(-r, "fdt_sandbox_engine_enter failed")
+    return fds
+
+
+def engine_sandbox_report():
+    """(refused call count, sorted names of the refused syscalls) in report mode"""
+    bits = (c.c_uint64 * 8)()
+    n = lib().fdt_sandbox_report(bits)
+    names = _syscall_names()
+    return int(n), sorted(names.get(k * 64 + j, str(k * 64 + j)) for k in range(8) for j in range(64)
+                          if bits[k] >> j & 1)
 
 
 def _aligned(nbytes, align):

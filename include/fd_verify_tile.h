@@ -736,6 +736,18 @@ int      fdt_link_join     ( void * mem, fdt_link_t * out );   /* 0, or -1 if no
    2 / logfile_fd, fsync(logfile_fd), clock_gettime and exit are allowed;
    any other syscall kills the process.  Returns 0 or -errno. */
 int      fdt_sandbox_enter ( int logfile_fd );
+/* The engine process's policy (fdt_sandbox.cpp): after its engines are
+   open, warmed and registered, every thread of the process may only use the
+   resource-neutral syscalls a running HIP runtime and the tiles need, ioctl
+   only on dev_fds (the device fds it holds: /dev/kfd, /dev/dri/renderD*),
+   clone only for threads; anything else (open, socket, exec, fork, ...)
+   kills the process.  report != 0 (bring-up, tests): such a syscall fails
+   with EPERM instead of killing, and is recorded (fdt_sandbox_report); it is
+   never carried out either way.  Returns 0 or -errno. */
+int      fdt_sandbox_engine_enter( int const * dev_fds, int dev_fd_cnt, int report );
+/* Report mode: bits8[k] bit j set = syscall 64 k + j was refused; returns
+   how many calls were refused. */
+uint64_t fdt_sandbox_report( uint64_t * bits8 );
 /* Runs a dedup tile inside the sandbox until frag_target frags were
    consumed (or lost to overrun) or none arrived for idle_ns_max; writes the
    final stats to stats_out (shared memory) and exits the calling process

@@ -15,6 +15,7 @@ sys.path.insert(0, REPO)
 def oracle_verifiers(T, a):
     from firedancer_amd import tile
     from oracle import oracle as orc
+    orc.lib()                       # loaded before the process enters its sandbox (--sandbox)
     vers = [tile.PyVerifier(lambda arena, txns: orc.verify_txns(arena, txns), slots=a.inflight, lag=1)
             for _ in range(T)]
     return vers, (lambda: None), {"device": None, "verifier": "oracle (test stand-in)"}

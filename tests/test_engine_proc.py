@@ -66,6 +66,55 @@ def test_sandbox_kills_other_syscalls():
     assert os.WIFSIGNALED(status) and os.WTERMSIG(status) == signal.SIGSYS, status
 
 
+def test_engine_sandbox_kills_open():
+    """The engine process's policy (fdt_sandbox_engine_enter, every thread):
+    the calls a running engine makes pass -- memory, futexes, clocks, a
+    thread, writes -- and opening a file kills the process with SIGSYS."""
+    def child():
+        import threading
+        tile.engine_sandbox_enter()
+        buf = np.zeros(1 << 22, dtype=np.uint8)            # mmap / munmap
+        th = threading.Thread(target=lambda: buf.sum())   # clone (a thread), futex
+        th.start()
+        th.join()
+        os.write(2, b"")
+        os.open("/dev/null", os.O_RDONLY)
+        os._exit(0)
+    status = _fork_and_wait(child)
+    assert os.WIFSIGNALED(status) and os.WTERMSIG(status) == signal.SIGSYS, status
+
+
+def test_engine_sandbox_report_mode():
+    """Report mode refuses the same calls without killing: open fails with
+    EPERM and is listed; a process (fork) is refused too; ioctl is refused on
+    an fd that is not the GPU driver's."""
+    r, w = os.pipe()
+    pid = os.fork()
+    if pid == 0:
+        try:
+            import fcntl
+            import termios
+            tile.engine_sandbox_enter(report=True)
+            errs = []
+            for what in (lambda: os.open("/dev/null", os.O_RDONLY), os.fork,
+                         lambda: fcntl.ioctl(0, termios.FIONREAD, b"    ")):
+                try:
+                    what()
+                    errs.append("allowed")
+                except OSError as e:
+                    errs.append(e.errno)
+            n, names = tile.engine_sandbox_report()
+            os.write(w, repr((errs, n, names)).encode())
+        finally:
+            os._exit(0)
+    os.close(w)
+    _, status = os.waitpid(pid, 0)
+    errs, n, names = eval(os.read(r, 4096).decode())
+    assert os.WIFEXITED(status) and os.WEXITSTATUS(status) == 0, status
+    assert errs == [1, 1, 1] and n >= 3, (errs, n)
+    assert "openat" in names and "ioctl" in names and ("clone" in names or "fork" in names), names
+
+
 def test_shm_link_join_roundtrip():
     """A link formatted in a /dev/shm file is the same link when joined by
     path: publish on one mapping, poll on the other; the consumer fseq is
@@ -161,6 +210,19 @@ def test_engine_process_pipeline_cpu(tmp_path, oracle):
     res, exp = _xproc_vs_model(tmp_path, ps, oracle, engine_cmd=CPU_ENGINE, depth=1 << 12, batch=64, inflight=3)
     assert exp[0][0].count(-2) > 10 and exp[0][0].count(-1) > 10
     assert res["engine"]["verifier"].startswith("oracle")
+
+
+def test_engine_process_sandboxed_cpu(tmp_path, oracle):
+    """The engine process inside its seccomp policy (--sandbox 1) once the
+    tiles run: the same frag-by-frag outcomes, its result reports the
+    policy; in report mode (--sandbox 2) nothing was refused."""
+    ps = _mixed_stream(500, seed=77)
+    res, _ = _xproc_vs_model(tmp_path, ps, oracle, engine_cmd=CPU_ENGINE, depth=1 << 12, batch=64, inflight=3,
+                             sandbox=1)
+    assert res["engine"]["sandbox"] == 1
+    res, _ = _xproc_vs_model(tmp_path, ps, oracle, engine_cmd=CPU_ENGINE, depth=1 << 12, batch=64, inflight=3,
+                             sandbox=2, dedup=False)
+    assert res["engine"]["sandbox"] == 2 and res["engine"]["sandbox_refused"] == [], res["engine"]["sandbox_refused"]
 
 
 def test_engine_process_two_tiles_cpu(tmp_path, oracle):

@@ -70,14 +70,16 @@ def _finish(p, timeout, what):
 def run(npz, n_payloads, tiles=1, producers=1, mode="paced", rate=0.0, reps=1, depth=1 << 14, batch=16384,
         inflight=8, wait_us=200.0, batch_sig_max=0, pages="4k", cpus=None, device_rank=0, dedup=False,
         dedup_frags=0, log=False, lap_guard=True, pair=2, spread=2, seed=0x5EEDF00D, timeout=300.0,
-        hw_queues=32, engine_cmd=None, engine_procs=1, proc_devices=None, dedup_depth=DEDUP_TCACHE_DEPTH):
+        hw_queues=32, engine_cmd=None, engine_procs=1, proc_devices=None, dedup_depth=DEDUP_TCACHE_DEPTH,
+        sandbox=None):
     """One cross-process run over the payloads in `npz` (arena, offs, sizes;
     n_payloads of them).  engine_cmd: the engine process's command before
     its arguments (default: python -m firedancer_amd.engine_proc; the CPU
     tests run the same loop over their checker instead).  engine_procs: E
     engine processes over the same in links, tiles // E tiles each;
     proc_devices: per process the --devices string (default: every process
-    --device-rank device_rank).  Returns {engine, engines, feed, dedup,
+    --device-rank device_rank); sandbox: the engine processes' --sandbox
+    (None: their default).  Returns {engine, engines, feed, dedup,
     wall_s, txns_per_s, ...} (engine: the processes' stats combined,
     engines: each process's own); with log=True also the tiles' per-frag
     outcomes (logs: [(seqs, codes)] per global tile) and the out links'
@@ -117,6 +119,8 @@ def run(npz, n_payloads, tiles=1, producers=1, mode="paced", rate=0.0, reps=1, d
                 c += ["--cpus", ",".join(map(str, tcpu[e * TE:(e + 1) * TE]))]
             if dedup:                        # verify -> dedup links are reliable (fd_topo): credits from the dedup's fseq
                 c += ["--out-flow-control", "1"]
+            if sandbox is not None:
+                c += ["--sandbox", str(sandbox)]
             if log:
                 c += ["--log", os.path.join(d, f"log{e}.npz")]
             eng_cmds.append(c)
