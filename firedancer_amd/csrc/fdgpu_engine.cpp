@@ -1979,10 +1979,17 @@ int fdgpu_sync(fdgpu_engine_t *e) {
    callers instead of serialising on a lock.  The caller's current HIP device
    is saved and restored.
 
+   A call whose message does not fit one batch arena (32-bit offsets: about
+   2 GB) is verified alone: its k = SHA-512(R || A || M) is hashed on the
+   device in arena-sized pieces of M (fdgpu_sha512_stream_kernel), then the
+   verify runs from those digests -- the reference hashes any msg_sz
+   (fd_ed25519_user.c:205-207), so size is never an error here.
+   FDGPU_SYNC_ARENA_MAX=<bytes> lowers that limit (tests reach the path with
+   small messages).
+
    The reference API has no error channel besides the verify codes, and it
    never answers a good signature with an error.  So an engine failure (no
-   device, a HIP error, a call beyond the engine's 32-bit arena) aborts the
-   process by default, with the reason on stderr: a transient GPU fault must
+   device, a HIP error) aborts the process by default, with the reason on stderr: a transient GPU fault must
    not turn valid transactions or blocks into rejected ones (replay's
    fd_executor_txn_verify, the shred FEC-root checks).  A caller that prefers
    to reject instead sets FDGPU_SYNC_FAIL_CLOSED=1: every call of the failed
@@ -2025,7 +2032,12 @@ constexpr uint64_t SYNC_BATCH_MAX = 4096;    /* calls per coalesced batch */
    the batch's need (room to grow) and must stay within 32-bit offsets
    (fdgpu_engine_open), so a batch holds at most half of that; a single call
    needing more cannot run on the engine at all */
-constexpr uint64_t SYNC_ARENA_MAX = (0xFFFFFFF0ull - FDGPU_ARENA_SLACK) / 2;
+constexpr uint64_t SYNC_ARENA_LIMIT = (0xFFFFFFF0ull - FDGPU_ARENA_SLACK) / 2;
+const uint64_t SYNC_ARENA_MAX = [] {
+  const char *v = getenv("FDGPU_SYNC_ARENA_MAX");       /* tests: reach the piecewise path with small messages */
+  const unsigned long long m = v ? strtoull(v, nullptr, 0) : 0;
+  return m >= 1024 && m < SYNC_ARENA_LIMIT ? (uint64_t)m : SYNC_ARENA_LIMIT;
+}();
 inline uint64_t sync_need(uint64_t msg_sz, uint32_t n) { return 96ull * n + msg_sz; }
 
 void sync_failed(SyncState &st, const char *what) {
@@ -2038,12 +2050,108 @@ void sync_failed(SyncState &st, const char *what) {
   }
 }
 
+bool sync_open(SyncState &st, uint64_t need);
+bool sync_run_prehashed(SyncState &st, SyncReq &r);
+bool sync_fill_run(SyncState &st, const std::vector<SyncReq *> &batch, uint64_t need);
+
 /* the leader's batch: returns false on an engine failure */
 bool sync_run(SyncState &st, const std::vector<SyncReq *> &batch) {
   uint64_t need = 0;
   for (const SyncReq *r : batch) need += sync_need(r->msg_sz, r->n);
-  if (need > SYNC_ARENA_MAX) { set_err("a call needs %llu arena bytes (at most %llu)", (unsigned long long)need,
-                                       (unsigned long long)SYNC_ARENA_MAX); return false; }
+  if (need > SYNC_ARENA_MAX) {
+    if (batch.size() == 1) return sync_run_prehashed(st, *batch[0]);    /* a call alone: its message in pieces */
+    set_err("a batch needs %llu arena bytes (at most %llu)", (unsigned long long)need,
+            (unsigned long long)SYNC_ARENA_MAX);
+    return false;
+  }
+  if (!sync_open(st, need)) return false;
+  return sync_fill_run(st, batch, need);
+}
+
+/* One call whose message exceeds a batch arena: k_i = SHA-512(R_i || A_i ||
+   M) for its n signatures on the device, a piece of M (at most
+   SYNC_ARENA_MAX bytes) per launch of fdgpu_sha512_stream_kernel, then the
+   verify from those digests and the batch_single_msg combine -- the same
+   code a batch would give it.  Buffers are the call's own (a rare path). */
+bool sync_run_prehashed(SyncState &st, SyncReq &r) {
+  if (!sync_open(st, 0)) return false;
+  fdgpu_engine_t *e = st.eng;
+  HIPCHK(hipSetDevice(e->device), false);
+  const uint32_t n = r.n;
+  const uint64_t sig_at = 0, pub_at = 64ull * n, st_at = (pub_at + 32ull * n + 63) & ~63ull;
+  const uint64_t arena_sz = st_at + 64ull * n;
+  const uint64_t piece = std::max<uint64_t>(256, SYNC_ARENA_MAX & ~127ull);
+  const uint64_t per_launch = piece / 128 - 1;            /* blocks whose message bytes fit one piece */
+  uint8_t *d_arena = nullptr, *d_m = nullptr, *d_ra = nullptr, *d_codes = nullptr;
+  fdgpu_sig_desc_t *d_sigs = nullptr;
+  fdgpu_txn_desc_t *d_txn = nullptr;
+  uint32_t *d_ws = nullptr;
+  bool ok = false;
+  do {
+    if (hipMalloc((void **)&d_arena, arena_sz + FDGPU_ARENA_SLACK) != hipSuccess ||
+        hipMalloc((void **)&d_m, piece) != hipSuccess || hipMalloc((void **)&d_ra, 64ull * n) != hipSuccess ||
+        hipMalloc((void **)&d_codes, 2ull * n + 32) != hipSuccess ||
+        hipMalloc((void **)&d_sigs, n * sizeof(fdgpu_sig_desc_t)) != hipSuccess ||
+        hipMalloc((void **)&d_txn, sizeof(fdgpu_txn_desc_t)) != hipSuccess ||
+        hipMalloc((void **)&d_ws, fdgpu_ws_bytes(n)) != hipSuccess) {
+      set_err("prehashed call: device allocation");
+      break;
+    }
+    std::vector<uint8_t> h_arena(arena_sz, 0), h_ra(64ull * n);
+    std::vector<fdgpu_sig_desc_t> h_sigs(n);
+    for (uint32_t i = 0; i < n; i++) {
+      memcpy(h_arena.data() + sig_at + 64ull * i, r.sigs + 64ull * i, 64);
+      memcpy(h_arena.data() + pub_at + 32ull * i, r.pubs + 32ull * i, 32);
+      memcpy(h_ra.data() + 64ull * i, r.sigs + 64ull * i, 32);        /* R */
+      memcpy(h_ra.data() + 64ull * i + 32, r.pubs + 32ull * i, 32);   /* A */
+      h_sigs[i] = fdgpu_sig_desc_t{(uint32_t)(st_at + 64ull * i), 0u, (uint32_t)(sig_at + 64ull * i),
+                                   (uint32_t)(pub_at + 32ull * i)};
+    }
+    const fdgpu_txn_desc_t h_txn{0u, n};
+    hipStream_t s = e->compute;
+    if (hipMemcpyAsync(d_arena, h_arena.data(), arena_sz, hipMemcpyHostToDevice, s) != hipSuccess ||
+        hipMemcpyAsync(d_ra, h_ra.data(), 64ull * n, hipMemcpyHostToDevice, s) != hipSuccess ||
+        hipMemcpyAsync(d_sigs, h_sigs.data(), n * sizeof(fdgpu_sig_desc_t), hipMemcpyHostToDevice, s) != hipSuccess ||
+        hipMemcpyAsync(d_txn, &h_txn, sizeof h_txn, hipMemcpyHostToDevice, s) != hipSuccess) {
+      set_err("prehashed call: upload");
+      break;
+    }
+    const uint64_t total = fdgpu_sha512_stream_blocks(r.msg_sz);
+    bool hashed = true;
+    for (uint64_t b0 = 0; b0 < total && hashed; b0 += per_launch) {
+      const uint64_t b1 = std::min(total, b0 + per_launch);
+      /* the message bytes of blocks [b0, b1): M[128 b0 - 64, 128 b1 + 64) within M */
+      const uint64_t m0 = b0 ? 128 * b0 - 64 : 0, m1 = std::min<uint64_t>(r.msg_sz, 128 * b1 + 64);
+      const uint64_t mlen = m1 > m0 ? m1 - m0 : 0;
+      hashed = (!mlen || hipMemcpyAsync(d_m, r.msg + m0, mlen, hipMemcpyHostToDevice, s) == hipSuccess) &&
+               fdgpu_launch_sha512_stream(d_m, m0, mlen, r.msg_sz, b0, (uint32_t)(b1 - b0), d_ra,
+                                          (uint64_t *)(d_arena + st_at), n, s) == hipSuccess &&
+               hipStreamSynchronize(s) == hipSuccess;              /* the piece buffer is reused next */
+    }
+    if (!hashed) { set_err("prehashed call: hashing"); break; }
+    int8_t code = 0;
+    if (fdgpu_launch_verify_prehashed(d_arena, d_sigs, n, e->d_btab, d_ws, (int8_t *)d_codes, e->cfg.flags, s) !=
+            hipSuccess ||
+        fdgpu_launch_combine(d_txn, 1, (const int8_t *)d_codes, (int8_t *)d_codes + n + 16, nullptr, s) !=
+            hipSuccess ||
+        hipMemcpyAsync(&code, d_codes + n + 16, 1, hipMemcpyDeviceToHost, s) != hipSuccess ||
+        hipStreamSynchronize(s) != hipSuccess) {
+      set_err("prehashed call: verify");
+      break;
+    }
+    r.code = code;
+    ok = true;
+  } while (0);
+  (void)hipStreamSynchronize(e->compute);
+  for (void *p : {(void *)d_arena, (void *)d_m, (void *)d_ra, (void *)d_codes, (void *)d_sigs, (void *)d_txn,
+                  (void *)d_ws})
+    if (p) (void)hipFree(p);
+  return ok;
+}
+
+/* the coalesced batch's engine, (re)opened for a batch needing `need` arena
+   bytes (0: as it is) */
+bool sync_open(SyncState &st, uint64_t need) {
   if (!st.eng || need > st.eng->cfg.max_arena) {
     if (st.eng) fdgpu_engine_close(st.eng);
     fdgpu_cfg_t cfg{};
@@ -2053,11 +2161,16 @@ bool sync_run(SyncState &st, const std::vector<SyncReq *> &batch) {
     const char *sp = getenv("FDGPU_SYNC_PAIR");
     cfg.flags = (sp && sp[0] == '0') ? 0u : FDGPU_FLAG_PAIR_AUTO | FDGPU_FLAG_SPREAD_AUTO;
     cfg.max_arena = std::min<uint64_t>(std::max<uint64_t>(SYNC_BATCH_MAX * (96 * 16 + 1232), need * 2),
-                                       2 * SYNC_ARENA_MAX);
+                                       2 * SYNC_ARENA_LIMIT);
     const char *dv = getenv("FDGPU_SYNC_DEVICE");
     st.eng = fdgpu_engine_open(dv ? atoi(dv) : 0, &cfg);
     if (!st.eng) return false;
   }
+  return true;
+}
+
+/* the batch's calls into the arena, one txn each, verified on the engine */
+bool sync_fill_run(SyncState &st, const std::vector<SyncReq *> &batch, uint64_t need) {
   st.arena.resize(need);
   st.txns.resize(batch.size());
   st.codes.resize(batch.size());
@@ -2080,12 +2193,6 @@ bool sync_run(SyncState &st, const std::vector<SyncReq *> &batch) {
 int sync_verify(const uint8_t *msg, uint64_t msg_sz, const uint8_t *sigs, const uint8_t *pubs, uint32_t n) {
   if (n == 0 || n > 16) return FD_ED25519_ERR_SIG;            /* fd_ed25519_user.c:238-241 */
   SyncState &st = sync_state();
-  if (sync_need(msg_sz, n) > SYNC_ARENA_MAX) {                /* fits no batch: fails alone, never queued */
-    st.calls.fetch_add(1, std::memory_order_relaxed);
-    set_err("a %llu-byte message exceeds the engine's 32-bit arena", (unsigned long long)msg_sz);
-    sync_failed(st, "call too large for the GPU engine");
-    return FD_ED25519_ERR_SIG;
-  }
   st.calls.fetch_add(1, std::memory_order_relaxed);
   SyncReq req{msg, sigs, pubs, msg_sz, n};
   std::unique_lock<std::mutex> lk(st.mu);
@@ -2094,7 +2201,8 @@ int sync_verify(const uint8_t *msg, uint64_t msg_sz, const uint8_t *sigs, const 
     if (st.leader) { st.cv.wait(lk); continue; }
     st.leader = true;                          /* this thread verifies everything queued so far */
     std::vector<SyncReq *> batch;
-    /* as many queued calls as fit one batch's arena (each call fits alone) */
+    /* as many queued calls as fit one batch's arena; a call that fits no
+       arena is taken alone (its message is then hashed in pieces) */
     size_t take = 0;
     uint64_t need = 0;
     while (take < st.pending.size() && take < SYNC_BATCH_MAX) {

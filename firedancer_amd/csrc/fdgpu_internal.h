@@ -110,6 +110,19 @@ hipError_t fdgpu_launch_verify_sigs(const uint8_t *d_arena, const fdgpu_sig_desc
                                     int8_t *d_sig_codes, uint32_t flags, hipStream_t stream,
                                     const uint32_t *d_n_sig, uint32_t resident_blocks, uint64_t kc_seed,
                                     int cnt_zeroed = 0);
+/* The synchronous API's messages too large for one arena: SHA-512(R_i ||
+   A_i || M) of n <= 64 signatures over one message, a piece of M per launch
+   (blocks [blk0, blk0 + nblk) of fdgpu_sha512_stream_blocks(msg_sz); d_mbuf
+   = M[m0, m0 + mlen) covering those blocks' message bytes; d_ra = n x (R ||
+   A); d_state = n x 8 words), then the verify from those states
+   (descriptor i: msg_off = the offset of state i in d_arena, 8-B aligned). */
+uint64_t   fdgpu_sha512_stream_blocks(uint64_t msg_sz);
+hipError_t fdgpu_launch_sha512_stream(const uint8_t *d_mbuf, uint64_t m0, uint64_t mlen, uint64_t msg_sz,
+                                      uint64_t blk0, uint32_t nblk, const uint8_t *d_ra, uint64_t *d_state,
+                                      uint32_t n, hipStream_t stream);
+hipError_t fdgpu_launch_verify_prehashed(const uint8_t *d_arena, const fdgpu_sig_desc_t *d_sigs, uint32_t n_sig,
+                                         const uint32_t *d_btab, uint32_t *d_ws, int8_t *d_sig_codes, uint32_t flags,
+                                         hipStream_t stream);
 /* the verify launch's queue counter for an n_sig grid in d_ws: a caller whose
    earlier kernel on the stream zeroes it passes cnt_zeroed (no memset) */
 uint32_t  *fdgpu_verify_cnt_word(uint32_t *d_ws, uint32_t n_sig);

@@ -565,8 +565,11 @@ FDG_DEV void hs_chain(ge_p1p1 &t, uint32_t (&ud)[5], uint32_t (&vd)[5], bool u_n
 /* The verify kernel of the half-size path; codes of lanes it settles are
    written here, lanes whose split failed are queued for fdgpu_full_kernel.
    The body takes its block index: the merged launch (fdgpu_verify_hs_multi_kernel)
-   runs it for the batch blockIdx.y names. */
-template <bool KC>
+   runs it for the batch blockIdx.y names.  PH (prehashed, the synchronous
+   API's messages too large for one arena): the descriptor's msg_off holds
+   the lane's SHA-512(R || A || M) state words, hashed beforehand in pieces
+   by fdgpu_sha512_stream_kernel; the product instantiations have PH false. */
+template <bool KC, bool PH = false>
 FDG_DEV void verify_hs_body(const uint8_t *__restrict__ arena, const fdgpu_sig_desc_t *__restrict__ sigs, uint32_t n_sig_arg,
                             const uint32_t *__restrict__ n_sig_dev, const uint32_t *__restrict__ btab,
                             uint32_t *__restrict__ ws, const uint32_t *__restrict__ perm, int8_t *__restrict__ codes,
@@ -602,7 +605,12 @@ FDG_DEV void verify_hs_body(const uint8_t *__restrict__ arena, const fdgpu_sig_d
   uint32_t k[8];
   {
     uint64_t h[8];
-    sha512_hram(h, Renc, Aenc, arena + d.msg_off, d.msg_sz, nb);
+    if (PH) {
+#pragma unroll
+      for (int j = 0; j < 8; j++) h[j] = ((const uint64_t *)(arena + d.msg_off))[j];
+    } else {
+      sha512_hram(h, Renc, Aenc, arena + d.msg_off, d.msg_sz, nb);
+    }
     FDGPU_STAMP(1);
     uint32_t kx[16];
 #pragma unroll
@@ -736,15 +744,59 @@ FDG_DEV void verify_hs_body(const uint8_t *__restrict__ arena, const fdgpu_sig_d
 #endif
 }
 
-template <bool KC>
+template <bool KC, bool PH = false>
 __global__ void __launch_bounds__(FDGPU_BLOCK, FDGPU_VERIFY_WAVES)
 fdgpu_verify_hs_kernel(const uint8_t *__restrict__ arena, const fdgpu_sig_desc_t *__restrict__ sigs, uint32_t n_sig_arg,
                        const uint32_t *__restrict__ n_sig_dev, const uint32_t *__restrict__ btab,
                        uint32_t *__restrict__ ws, const uint32_t *__restrict__ perm, int8_t *__restrict__ codes,
                        uint32_t *__restrict__ queue, uint32_t *__restrict__ queue_cnt, uint32_t flags,
                        const uint32_t *__restrict__ key_of, const uint32_t *__restrict__ kverd) {
-  verify_hs_body<KC>(arena, sigs, n_sig_arg, n_sig_dev, btab, ws, perm, codes, queue, queue_cnt, flags, key_of, kverd,
-                     blockIdx.x);
+  verify_hs_body<KC, PH>(arena, sigs, n_sig_arg, n_sig_dev, btab, ws, perm, codes, queue, queue_cnt, flags, key_of,
+                         kverd, blockIdx.x);
+}
+
+/* SHA-512(R_i || A_i || M) of one message shared by n <= 64 signatures (lane
+   i: signature i), over blocks [blk0, blk0 + nblk) of the n streams, in a
+   launch per piece of M: the synchronous API's messages too large for one
+   arena.  state: n x 8 words (initialised by the launch with blk0 == 0),
+   left as sha512_hram leaves its h.  mbuf holds M[m0, m0 + mlen): every
+   message byte of the launch's blocks (the host's piece).  Block b of a
+   stream is R || A || M[0, 64) for b = 0 and M[128 b - 64, 128 b + 64)
+   after, padded past msg_sz and length-terminated as sha512_hram does;
+   bytes are gathered one by one (a rare path, one wave). */
+__global__ void __launch_bounds__(64) fdgpu_sha512_stream_kernel(const uint8_t *__restrict__ mbuf, uint64_t m0,
+                                                                 uint64_t mlen, uint64_t msg_sz, uint64_t blk0,
+                                                                 uint32_t nblk, const uint8_t *__restrict__ ra,
+                                                                 uint64_t *__restrict__ state, uint32_t n) {
+  const uint32_t i = threadIdx.x;
+  if (i >= n) return;
+  const uint64_t H0[8] = {0x6a09e667f3bcc908ULL, 0xbb67ae8584caa73bULL, 0x3c6ef372fe94f82bULL,
+                          0xa54ff53a5f1d36f1ULL, 0x510e527fade682d1ULL, 0x9b05688c2b3e6c1fULL,
+                          0x1f83d9abfb41bd6bULL, 0x5be0cd19137e2179ULL};
+  uint64_t h[8];
+  for (int j = 0; j < 8; j++) h[j] = blk0 ? state[8 * i + j] : H0[j];
+  const uint64_t total = (64u + msg_sz + 16u) / 128u + 1u, bitlen = (64u + msg_sz) * 8u;
+  for (uint64_t b = blk0; b < blk0 + nblk; b++) {
+    uint64_t w[16];
+    for (int t = 0; t < 16; t++) {
+      uint64_t v = 0;
+      for (int j = 0; j < 8; j++) {
+        const uint64_t s = 128u * b + 8u * (uint64_t)t + (uint64_t)j;     /* position in R || A || M */
+        uint32_t byte;
+        if (s < 64u) {
+          byte = ra[64u * i + s];
+        } else {
+          const uint64_t g = s - 64u;                                     /* position in M */
+          byte = g < msg_sz ? (g >= m0 && g < m0 + mlen ? mbuf[g - m0] : 0u) : g == msg_sz ? 0x80u : 0u;
+        }
+        v = (v << 8) | byte;
+      }
+      w[t] = v;
+    }
+    if (b + 1 == total) { w[14] = 0; w[15] = bitlen; }
+    sha512_compress(h, w);
+  }
+  for (int j = 0; j < 8; j++) state[8 * i + j] = h[j];
 }
 
 /* Several batches' verifies as ONE launch (FDGPU_FLAG_MERGE): block (x, y)
@@ -1826,6 +1878,34 @@ hipError_t fdgpu_launch_verify_sigs(const uint8_t *d_arena, const fdgpu_sig_desc
   }
   hipLaunchKernelGGL(fdgpu_full_kernel, dim3(slow_blocks), dim3(FDGPU_BLOCK), 0, stream, d_ws, d_perm, d_sig_codes,
                      queue, cnt, slow_blocks * FDGPU_BLOCK, key_of);
+  return hipGetLastError();
+}
+
+uint64_t fdgpu_sha512_stream_blocks(uint64_t msg_sz) { return (64u + msg_sz + 16u) / 128u + 1u; }
+
+hipError_t fdgpu_launch_sha512_stream(const uint8_t *d_mbuf, uint64_t m0, uint64_t mlen, uint64_t msg_sz,
+                                      uint64_t blk0, uint32_t nblk, const uint8_t *d_ra, uint64_t *d_state,
+                                      uint32_t n, hipStream_t stream) {
+  if (!n || n > 64 || !nblk) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(fdgpu_sha512_stream_kernel, dim3(1), dim3(64), 0, stream, d_mbuf, m0, mlen, msg_sz, blk0, nblk,
+                     d_ra, d_state, n);
+  return hipGetLastError();
+}
+
+hipError_t fdgpu_launch_verify_prehashed(const uint8_t *d_arena, const fdgpu_sig_desc_t *d_sigs, uint32_t n_sig,
+                                         const uint32_t *d_btab, uint32_t *d_ws, int8_t *d_sig_codes, uint32_t flags,
+                                         hipStream_t stream) {
+  if (!n_sig) return hipSuccess;
+  const uint32_t grid = (n_sig + FDGPU_BLOCK - 1) / FDGPU_BLOCK;
+  const size_t lanes = (size_t)grid * FDGPU_BLOCK;
+  uint32_t *queue = d_ws + lanes * FDGPU_WS_LANE_WORDS, *cnt = queue + lanes;
+  hipError_t e = hipMemsetAsync(cnt, 0, sizeof(uint32_t), stream);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL((fdgpu_verify_hs_kernel<false, true>), dim3(grid), dim3(FDGPU_BLOCK), 0, stream, d_arena, d_sigs,
+                     n_sig, nullptr, d_btab, d_ws, nullptr, d_sig_codes, queue, cnt, flags & FDGPU_FLAG_REF_MAP,
+                     nullptr, nullptr);
+  hipLaunchKernelGGL(fdgpu_full_kernel, dim3(1), dim3(FDGPU_BLOCK), 0, stream, d_ws, nullptr, d_sig_codes, queue, cnt,
+                     FDGPU_BLOCK, nullptr);
   return hipGetLastError();
 }
 

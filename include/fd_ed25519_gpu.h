@@ -22,10 +22,13 @@
        (TLS handshakes, gossip, repair, the precompile) should keep the
        reference's CPU fd_ed25519_verify; INTEGRATION.md 1 shows how both
        link into one process (the fdgpu_ed25519_* names below).
-       The caller thread's current HIP device is preserved.  The reference
+       The caller thread's current HIP device is preserved.  Any msg_sz is
+       verified, as the reference's (fd_ed25519_user.c:205-207): a message
+       beyond one batch arena (32-bit offsets, ~2 GB) is hashed on the GPU in
+       arena-sized pieces, then verified from its digests.  The reference
        API returns verify codes only and never rejects a good signature, so
-       an engine failure (no GPU, a HIP error, a message beyond the engine's
-       32-bit arena, ~2 GB) aborts the process with the reason on stderr.
+       an engine failure (no GPU, a HIP error) aborts the process with the
+       reason on stderr.
        FDGPU_SYNC_FAIL_CLOSED=1 in the environment makes every call of the
        failed batch return FD_ED25519_ERR_SIG instead (fdgpu_sync_errors()
        counts the failures).  FDGPU_SYNC_DEVICE=<n> selects the device

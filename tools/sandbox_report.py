@@ -37,14 +37,16 @@ def main():
     for mode in (int(x) for x in a.modes.split(",")):
         for procs in (1, 2):
             r = xproc.run(npz, len(ps), tiles=2, producers=2, mode="prefill", depth=1 << 16, batch=4096, inflight=4,
-                          dedup=True, dedup_frags=exp, engine_procs=procs, sandbox=mode, timeout=120)
+                          dedup=True, dedup_frags=2 * exp, engine_procs=procs, sandbox=mode, timeout=120)
             ers = r["engines"]
             print(json.dumps({"sandbox": mode, "engine_procs": procs,
                               "refused": [e.get("sandbox_refused") for e in ers],
                               "refused_calls": [e.get("sandbox_refused_calls") for e in ers],
-                              "published": r["engine"]["stats"]["published"], "expected": exp,
+                              "published": r["engine"]["stats"]["published"], "expected": 2 * exp,
                               "dedup_published": r["dedup"]["stats"]["published"],
-                              "txns_per_s": r["txns_per_s"]}), flush=True)
+                              "txns_per_s": r["txns_per_s"],
+                              "stderr_refused": [ln for e in ers for ln in e.get("stderr_tail", "").splitlines()
+                                                 if "refused" in ln]}), flush=True)
 
 
 if __name__ == "__main__":

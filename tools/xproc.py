@@ -64,7 +64,10 @@ def _finish(p, timeout, what):
         raise RuntimeError(f"{what} timed out: {err[-3000:]}")
     if p.returncode != 0:
         raise RuntimeError(f"{what} failed ({p.returncode}): {err[-3000:]}")
-    return json.loads(out.strip().splitlines()[-1])
+    res = json.loads(out.strip().splitlines()[-1])
+    if isinstance(res, dict) and err:
+        res["stderr_tail"] = err[-2000:]
+    return res
 
 
 def run(npz, n_payloads, tiles=1, producers=1, mode="paced", rate=0.0, reps=1, depth=1 << 14, batch=16384,
