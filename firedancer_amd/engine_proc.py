@@ -54,7 +54,7 @@ from . import tile
 # serialise
 DEFAULT_HW_QUEUES = 32
 # the engine seccomp policy (fdt_sandbox_engine_enter) once the tiles run
-DEFAULT_SANDBOX = 0
+DEFAULT_SANDBOX = 1
 
 
 def warm_engines(engines, inflight, out_bytes=0, batch=64):

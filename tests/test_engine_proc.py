@@ -93,16 +93,20 @@ def test_engine_sandbox_report_mode():
     if pid == 0:
         try:
             import fcntl
+            import resource
             import termios
             tile.engine_sandbox_enter(report=True)
             errs = []
+            resource.getrlimit(resource.RLIMIT_NOFILE)            # prlimit64 of itself, reading: allowed
             for what in (lambda: os.open("/dev/null", os.O_RDONLY), os.fork,
-                         lambda: fcntl.ioctl(0, termios.FIONREAD, b"    ")):
+                         lambda: fcntl.ioctl(0, termios.FIONREAD, b"    "),
+                         lambda: resource.setrlimit(resource.RLIMIT_NOFILE, resource.getrlimit(resource.RLIMIT_NOFILE)),
+                         lambda: resource.prlimit(os.getppid(), resource.RLIMIT_NOFILE)):
                 try:
                     what()
                     errs.append("allowed")
-                except OSError as e:
-                    errs.append(e.errno)
+                except (OSError, ValueError) as e:          # (setrlimit reports EPERM as ValueError)
+                    errs.append(getattr(e, "errno", None) or 1)
             n, names = tile.engine_sandbox_report()
             os.write(w, repr((errs, n, names)).encode())
         finally:
@@ -111,8 +115,9 @@ def test_engine_sandbox_report_mode():
     _, status = os.waitpid(pid, 0)
     errs, n, names = eval(os.read(r, 4096).decode())
     assert os.WIFEXITED(status) and os.WEXITSTATUS(status) == 0, status
-    assert errs == [1, 1, 1] and n >= 3, (errs, n)
+    assert errs == [1, 1, 1, 1, 1] and n >= 5, (errs, n)
     assert "openat" in names and "ioctl" in names and ("clone" in names or "fork" in names), names
+    assert "prlimit64" in names, names
 
 
 def test_shm_link_join_roundtrip():
@@ -271,6 +276,7 @@ def test_engine_process_pipeline_gpu(tmp_path, oracle):
     ps = _mixed_stream(3000, seed=72)
     res, exp = _xproc_vs_model(tmp_path, ps, oracle, depth=1 << 12, batch=512, inflight=3)
     assert exp[0][0].count(0) > 1000 and res["engine"]["device"] == 0
+    assert res["engine"]["sandbox"] == 1                 # the engine policy is on by default (fdt_sandbox_engine_enter)
     _xproc_vs_model(tmp_path, ps, oracle, tiles=2, depth=1 << 12, batch=512, inflight=3, dedup=False)
 
 
