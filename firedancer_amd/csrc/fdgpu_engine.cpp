@@ -186,6 +186,9 @@ struct fdgpu_engine {
   std::vector<Reg> regions;
   bool drop_flag = false;            /* test hook (FDGPU_DEBUG_DROP_FLAG=1): the stream never writes the
                                         completion word, so polls must finish through the event */
+  uint32_t fail_merge_at = 0;        /* test hook (FDGPU_DEBUG_FAIL_MERGE=k): the k-th merge launch fails
+                                        before queueing anything, as a HIP error part-way would */
+  uint32_t merge_calls = 0;
   /* FDGPU_FLAG_MERGE */
   std::vector<Merge> merges;
   std::vector<Slot *> pending;       /* batches parsed (or parsing) whose verify is not launched */
@@ -590,6 +593,8 @@ fdgpu_engine_t *fdgpu_engine_open(int device, fdgpu_cfg_t const *cfg_in) {
   {
     const char *pe = getenv("FDGPU_POLL_EVENT"), *df = getenv("FDGPU_DEBUG_DROP_FLAG");
     e->drop_flag = df && df[0] == '1';
+    const char *fm = getenv("FDGPU_DEBUG_FAIL_MERGE");
+    e->fail_merge_at = fm ? (uint32_t)atoi(fm) : 0u;
     Slot &s0 = e->slots[0];
     if (!(pe && pe[0] == '1') && hipStreamWriteValue32(s0.stream, s0.d_flag, 0x5a5a5a5au, 0) == hipSuccess &&
         hipStreamSynchronize(s0.stream) == hipSuccess)
@@ -827,10 +832,11 @@ char const *fdgpu_build_info(void) {
   char kb[256];
   const int kprod = fdgpu_kernel_build_info(kb, sizeof kb);
   const char *df = getenv("FDGPU_DEBUG_DROP_FLAG");      /* fault injection: completion flags dropped */
-  const int drop = df && df[0] == '1';
-  const int prod = kprod && FDGPU_COPY_THREADS_N == 4 && !drop;
-  snprintf(buf, sizeof buf, "{%s,\"copy_threads\":%d,\"debug_drop_flag\":%d,\"product\":%d}", kb,
-           (int)FDGPU_COPY_THREADS_N, drop, prod);
+  const char *fm = getenv("FDGPU_DEBUG_FAIL_MERGE");     /* fault injection: a merge launch fails */
+  const int drop = df && df[0] == '1', fail_merge = fm ? atoi(fm) : 0;
+  const int prod = kprod && FDGPU_COPY_THREADS_N == 4 && !drop && !fail_merge;
+  snprintf(buf, sizeof buf, "{%s,\"copy_threads\":%d,\"debug_drop_flag\":%d,\"debug_fail_merge\":%d,\"product\":%d}",
+           kb, (int)FDGPU_COPY_THREADS_N, drop, fail_merge, prod);
   return buf;
 }
 
@@ -1316,6 +1322,10 @@ int merge_kick(fdgpu_engine_t *e, bool force) {
 
 int merge_kick_queue(fdgpu_engine_t *e, bool force) {
   if (e->pending.empty()) return FDGPU_OK;
+  if (e->fail_merge_at && ++e->merge_calls == e->fail_merge_at) {
+    set_err("injected merge failure (FDGPU_DEBUG_FAIL_MERGE)");
+    return FDGPU_ERR_DEVICE;
+  }
   const uint32_t nms = (uint32_t)e->merges.size();
   int mi = -1;
   for (uint32_t k = 0; k < nms && mi < 0; k++) {

@@ -508,3 +508,55 @@ def test_frag_io_dma_gather_and_small_grids():
                            env=env, capture_output=True, text=True, timeout=600)
         assert r.returncode == 0, (extra, r.stdout[-3000:], r.stderr[-2000:])
         assert " passed" in r.stdout, r.stdout[-2000:]
+
+
+@pytest.mark.gpu
+def test_frag_io_failed_merge_then_good_batch(oracle, monkeypatch):
+    """a gathered batch whose merged verify fails after its
+    ingest was queued (injected: FDGPU_DEBUG_FAIL_MERGE=1) leaves the slot's
+    device-side signature count behind; the poll reports the failure (the
+    submit returns the ticket), and the next batch on the same slot -- one
+    ring slot, so it is the same one -- clears the count first: its codes equal
+    the oracle's."""
+    import firedancer_amd as fa
+    from firedancer_amd import _lib
+    L = _lib.lib()
+    monkeypatch.setenv("FDGPU_DEBUG_FAIL_MERGE", "1")
+    eng = fa.VerifyEngine(0, max_txn=2048, ring_depth=1, merge=True)
+    monkeypatch.delenv("FDGPU_DEBUG_FAIL_MERGE")
+    bufs = []
+    try:
+        outs = []
+        for seed in (0xD1, 0xD2):
+            a, t, _ = workload.cfg1(1500, seed=seed)
+            ps = [p for p in workload.payloads(a, t) if tile.txn_parse(p)[0]]
+            in_buf, out_buf = _pages(len(ps) * 1280), _pages(len(ps) * 2176)
+            eng.host_register(in_buf)
+            eng.host_register(out_buf)
+            bufs += [in_buf, out_buf]
+            fio = np.zeros(len(ps), dtype=tile.FRAG_IO_DTYPE)
+            o = 0
+            for k, p in enumerate(ps):
+                in_buf[k * 1280:k * 1280 + len(p)] = np.frombuffer(p, dtype=np.uint8)
+                cap = L.fdgpu_frag_out_cap(len(p))
+                fio[k] = (in_buf.ctypes.data + k * 1280, len(p), o, cap, 0, 0)
+                o += (cap + 63) // 64 * 64
+            outs.append((ps, fio, out_buf, o))
+        ps, fio, out_buf, o = outs[0]
+        tk = eng.submit_frags_io(fio, out_buf, o, 0x55)          # its merge fails: a ticket all the same
+        with pytest.raises(RuntimeError):
+            eng.poll_frags_io(tk, blocking=True)
+        ps, fio, out_buf, o = outs[1]
+        codes, _, _ = eng.poll_frags_io(eng.submit_frags_io(fio, out_buf, o, 0x55), blocking=True)
+        arena = np.frombuffer(b"".join(ps) + b"\0" * 16, dtype=np.uint8)
+        offs = np.cumsum([0] + [len(p) for p in ps])
+        td = np.zeros(len(ps), dtype=workload.TXN_DTYPE)
+        for k, p in enumerate(ps):
+            d = tile.txn_decode(tile.txn_parse(p)[1])
+            td[k] = (int(offs[k]) + d["message_off"], len(p) - d["message_off"],
+                     int(offs[k]) + d["signature_off"], int(offs[k]) + d["acct_addr_off"], d["signature_cnt"])
+        assert (codes == oracle.verify_txns(arena, td, nthreads=8)).all()
+    finally:
+        for b in bufs:
+            eng.host_unregister(b)
+        eng.close()
