@@ -160,6 +160,9 @@ def serve(in_paths, out_paths, verifiers, frag_cnts, timeout_s=120.0, idle_s=0.0
     listed in the result instead of killing the process), 0 -- none."""
     ins = [tile.Link.shm_join(p) for p in in_paths]
     outs = [tile.Link.shm_join(p) for p in out_paths]
+    # huge-page accounting reads /proc/self/smaps: before the sandbox, and
+    # before the timed region (tens of ms on a 2 GB link of 4 KB pages)
+    in_huge = [ln.huge_bytes() for ln in ins]
     T = len(outs)
     rr = round_robin_shares(rr_idx, rr_cnt, T)
     frag_cnts = list(frag_cnts)
@@ -177,7 +180,6 @@ def serve(in_paths, out_paths, verifiers, frag_cnts, timeout_s=120.0, idle_s=0.0
             with open(ready_file + ".tmp", "w") as f:
                 f.write(str(os.getpid()))
             os.rename(ready_file + ".tmp", ready_file)
-        in_huge = [ln.huge_bytes() for ln in ins]          # (reads /proc/self/smaps: before the sandbox)
         if sandbox:                    # engines open, warmed, registered; tiles running (fd_topo_run.c:96-103)
             tile.engine_sandbox_enter(report=sandbox == 2)
         idle_since, last = None, -1
