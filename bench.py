@@ -498,6 +498,9 @@ TILE_RUNS = (  # name, verify tiles, quic links (producers), offered txn/s (-1: 
     ("mux1_paced_16M", 1, 2, 16e6),
     ("mux2_paced_20M", 2, 4, 20e6),
     ("mux2_paced_24M", 2, 4, 24e6),
+    # the reference's link depth near the producers' limit (~9-12 M frags/s a thread): what two tiles sustain
+    # with nothing lost at 16384 deep
+    ("mux2_paced_36M", 2, 4, 36e6),
     ("mux1_capacity", 1, 1, -1.0),
     ("mux2_capacity", 2, 2, -1.0),
 )
