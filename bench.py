@@ -589,6 +589,7 @@ def tile_cmd(rank, cpus, npz, out, runs=TILE_RUNS, multi=0, xproc=False):
 
 def _tile_child(rank, cpus, arena, txns, modes, runs, tag=""):
     xp = tag == "xproc"
+    runs = tuple(runs)
     reps_n = TILE_REPS_XPROC if xp else TILE_REPS
     """tools/bench_tile.py in a child process over these txns as raw frags:
     {tile_<name>_...} per run (median of TILE_REPS)."""
@@ -654,7 +655,15 @@ def _tile_child(rank, cpus, arena, txns, modes, runs, tag=""):
     return out
 
 
-def tile_lines(rank, arena, txns, modes, cpus, cfg3=None):
+def xproc_runs(world):
+    """The cross-process lines a rank runs: with several ranks on a node, not
+    the ones that start two engine processes (8 ranks x 2 would be 16 GPU
+    processes at once; a rank's own engines open only after its tile lines,
+    so one engine process per rank keeps the node at one per GPU)."""
+    return TILE_RUNS_XPROC if world == 1 else tuple(r for r in TILE_RUNS_XPROC if not (len(r) > 4 and r[4] > 1))
+
+
+def tile_lines(rank, arena, txns, modes, cpus, cfg3=None, world=1):
     """BASELINE configs[4] (cfg5) on this rank's GPU: the verify tile in the
     reference's shape -- the fd_verify.c:232-246 callbacks (fdgpu_vmux) on
     the mux loop (fdt_mux_run, FD_MUX_FLAG_COPY | MANUAL_PUBLISH), tcache and
@@ -681,15 +690,21 @@ def tile_lines(rank, arena, txns, modes, cpus, cfg3=None):
         out.update(_tile_child(rank, cpus, *cfg3, TILE_RUNS_CFG3, tag="cfg3"))
         out["tile_cfg3_txns"] = len(cfg3[1])
     # the deployable shape: producers and tiles in separate processes
-    out.update(_tile_child(rank, cpus, arena, txns, modes, TILE_RUNS_XPROC, tag="xproc"))
+    out.update(_tile_child(rank, cpus, arena, txns, modes, xproc_runs(world), tag="xproc"))
     for name, inproc in (("xproc_mux1_paced_16M", "mux1_paced_16M"), ("xproc_mux2_paced_24M", "mux2_paced_24M")):
         out[f"tile_{name}_vs_in_process"] = round(out[f"tile_{name}_txns_per_s"] / out[f"tile_{inproc}_txns_per_s"], 3)
     out["tile_xproc_config"] = ("the same tile in the engine process (python -m firedancer_amd.engine_proc) over "
                                 "/dev/shm links a separate producer process (tools/quic_feed.py) publishes into, "
                                 "every link page faulted in before the run (4 KB pages: this host offers no shared "
                                 "2 MB pages, tile.hugepage_support()); paced: the reference's 16384-deep links; "
-                                f"capacity: one 2^{TILE_DEPTH_LG_PREFILL_XPROC}-deep link prefilled by the producer "
-                                f"process; median of {TILE_REPS_XPROC} runs, each starting both processes")
+                                f"capacity: one 2^{TILE_DEPTH_LG_PREFILL_XPROC}-deep link per tile prefilled by the "
+                                "producer process; the engine process inside its seccomp policy once its tiles run "
+                                "(engine_proc --sandbox 1); _2proc_: two engine processes, one tile each, as global "
+                                "tiles 0 and 1 of 2 over the same links (--rr-idx/--rr-cnt: the multi-GPU form, here "
+                                "on this rank's GPU; single-rank runs only); _e2e_dedup_: the sandboxed dedup process "
+                                "reads both out links reliably at the reference's tcache depth (4194302) and the run "
+                                "is timed to its last frag (_dedup_in_published_dup: frags in, published, dropped as "
+                                f"duplicates); median of {TILE_REPS_XPROC} runs, each starting every process")
     out["tile_config"] = ("fdgpu_vmux on fdt_mux_run (the reference's mux-callback verify tile), payload gather, "
                           "fd_txn_parse, verify, dedup tag and out-frag assembly on the GPU; muxT: T verify tiles "
                           "reading P quic->verify links (one producer thread each; P = T for capacity, 2T paced), one engine "
@@ -894,7 +909,7 @@ def main():
     if args.tile and not args.no_extras:
         cfg3_tile = (workload.cfg3(args.tile_cfg3_txns, seed=workload.CFG3_SEED + 0x100 + dist.rank)
                      if args.tile_cfg3_txns else None)
-        tl = tile_lines(dist.local_rank, arena, txns, modes, cpus, cfg3=cfg3_tile)
+        tl = tile_lines(dist.local_rank, arena, txns, modes, cpus, cfg3=cfg3_tile, world=dist.world)
         del cfg3_tile
         tl["tile_mux1_capacity_txns_per_s_node"] = round(dist.sum(tl["tile_mux1_capacity_txns_per_s"]), 1)
         tl["tile_published_ok_all_ranks"] = dist.sum(

@@ -110,3 +110,13 @@ def test_tile_cmd_xproc_runs():
         else:
             assert len(run) == 5
     assert (True, False) in seen and (False, True) in seen
+
+
+def test_xproc_runs_per_world():
+    """One rank of one: every cross-process line, two engine processes
+    included; several ranks on a node: no line that starts two engine
+    processes per rank (the node stays at one GPU process per GPU)."""
+    assert bench.xproc_runs(1) == bench.TILE_RUNS_XPROC
+    multi = bench.xproc_runs(8)
+    assert multi and all(not (len(r) > 4 and r[4] > 1) for r in multi)
+    assert any(len(r) > 5 and r[5] for r in multi)                 # the e2e dedup lines stay
