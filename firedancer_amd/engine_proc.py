@@ -134,6 +134,17 @@ def _producers_done(ins, frag_cnts):
     return True
 
 
+def _cache_source_lines():
+    """Read every loaded module's source into linecache now: inside the
+    engine policy a traceback could not open them (open is refused, and in
+    enforce mode fatal), so an error after entry would die without one."""
+    import linecache
+    for m in list(sys.modules.values()):
+        f = getattr(m, "__file__", None)
+        if f and f.endswith(".py"):
+            linecache.getlines(f)
+
+
 def round_robin_shares(rr_idx, rr_cnt, T):
     """The global round-robin index of each of this process's T tiles
     (fd_verify.c:46: tile i of verify_tile_cnt takes seq % cnt == i):
@@ -181,6 +192,7 @@ def serve(in_paths, out_paths, verifiers, frag_cnts, timeout_s=120.0, idle_s=0.0
                 f.write(str(os.getpid()))
             os.rename(ready_file + ".tmp", ready_file)
         if sandbox:                    # engines open, warmed, registered; tiles running (fd_topo_run.c:96-103)
+            _cache_source_lines()
             tile.engine_sandbox_enter(report=sandbox == 2)
         idle_since, last = None, -1
         while any(vm.final_cnt() < n_total for vm in vms):

@@ -347,3 +347,28 @@ def test_engine_process_cli_gpu(oracle, tmp_path):
         for p in paths:
             if os.path.exists(p):
                 os.unlink(p)
+
+
+def test_traceback_inside_engine_policy():
+    """An error after the engine process entered its policy still prints a
+    traceback with source lines (engine_proc caches them before entry;
+    reading a source file then would be a refused open)."""
+    r, w = os.pipe()
+    pid = os.fork()
+    if pid == 0:
+        try:
+            import traceback
+            from firedancer_amd import engine_proc
+            engine_proc._cache_source_lines()
+            tile.engine_sandbox_enter()
+            try:
+                engine_proc.round_robin_shares(5, 2, 1)
+            except ValueError:
+                os.write(w, traceback.format_exc().encode())
+        finally:
+            os._exit(0)
+    os.close(w)
+    _, status = os.waitpid(pid, 0)
+    tb = os.read(r, 65536).decode()
+    assert os.WIFEXITED(status) and os.WEXITSTATUS(status) == 0, status
+    assert "raise ValueError" in tb and "round_robin_shares" in tb, tb
