@@ -19,6 +19,7 @@
      [4096, ...)      mcache: depth x fdt_frag_meta_t (fd_mcache.h:265-322)
      [dcache_off, ..) compact dcache for depth frags of <= mtu (fd_dcache.h) */
 #include <errno.h>
+#include <fcntl.h>
 #include <sched.h>
 #include <signal.h>
 #include <ucontext.h>
@@ -188,14 +189,14 @@ void report_sigsys(int, siginfo_t *si, void *uc_) {
    loop around them), none of which reaches outside the process */
 const uint32_t ENGINE_ALLOW[] = {
   __NR_read, __NR_write, __NR_pread64, __NR_pwrite64, __NR_readv, __NR_writev, __NR_lseek, __NR_fstat,
-  __NR_newfstatat, __NR_close, __NR_fsync, __NR_fdatasync, __NR_dup, __NR_fcntl,
+  __NR_close, __NR_fsync, __NR_fdatasync, __NR_dup, __NR_fcntl,
   __NR_mmap, __NR_munmap, __NR_mprotect, __NR_mremap, __NR_madvise, __NR_brk, __NR_mlock, __NR_munlock,
   __NR_futex, __NR_sched_yield, __NR_nanosleep, __NR_clock_nanosleep, __NR_clock_gettime, __NR_clock_getres,
   __NR_gettimeofday, __NR_select, __NR_pselect6, __NR_poll, __NR_ppoll, __NR_epoll_wait, __NR_epoll_pwait,
   __NR_getpid, __NR_gettid, __NR_getppid, __NR_getuid, __NR_geteuid, __NR_getgid, __NR_getegid,
   __NR_rt_sigprocmask, __NR_rt_sigaction, __NR_rt_sigreturn, __NR_sigaltstack, __NR_tgkill,
   __NR_sched_getaffinity, __NR_sched_setaffinity, __NR_sched_getparam, __NR_sched_getscheduler,
-  __NR_set_robust_list, __NR_rseq, __NR_getrandom, __NR_membarrier, __NR_prctl, __NR_getrusage,
+  __NR_set_robust_list, __NR_rseq, __NR_getrandom, __NR_membarrier, __NR_getrusage,
   __NR_mbind, __NR_get_mempolicy,                     /* the HIP runtime's NUMA placement of host memory */
   __NR_exit, __NR_exit_group,
 };
@@ -224,6 +225,21 @@ int fdt_sandbox_engine_enter(const int *dev_fds, int dev_fd_cnt, int report) {
   jeq(__NR_clone, 0, 4);
   stmt(BPF_LD | BPF_W | BPF_ABS, offsetof(struct seccomp_data, args[0]));
   f.push_back(BPF_JUMP(BPF_JMP | BPF_JSET | BPF_K, CLONE_THREAD, 0, 1));
+  stmt(BPF_RET | BPF_K, ALLOW);
+  stmt(BPF_RET | BPF_K, DENY);
+  /* newfstatat: the fstat form only (AT_EMPTY_PATH on an fd held: the C
+     library's fstat), no lookup of a path */
+  jeq(__NR_newfstatat, 0, 4);
+  stmt(BPF_LD | BPF_W | BPF_ABS, offsetof(struct seccomp_data, args[3]));
+  f.push_back(BPF_JUMP(BPF_JMP | BPF_JSET | BPF_K, AT_EMPTY_PATH, 0, 1));
+  stmt(BPF_RET | BPF_K, ALLOW);
+  stmt(BPF_RET | BPF_K, DENY);
+  /* prctl: thread names only (PR_SET_NAME / PR_GET_NAME), not the options
+     that would open the process to others (PR_SET_PTRACER, _DUMPABLE) */
+  jeq(__NR_prctl, 0, 5);
+  stmt(BPF_LD | BPF_W | BPF_ABS, offsetof(struct seccomp_data, args[0]));
+  jeq(PR_SET_NAME, 1, 0);
+  jeq(PR_GET_NAME, 0, 1);
   stmt(BPF_RET | BPF_K, ALLOW);
   stmt(BPF_RET | BPF_K, DENY);
   /* prlimit64: reading this process's own limits only (pid 0, no new

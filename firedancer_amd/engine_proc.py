@@ -137,12 +137,16 @@ def _producers_done(ins, frag_cnts):
 def _cache_source_lines():
     """Read every loaded module's source into linecache now: inside the
     engine policy a traceback could not open them (open is refused, and in
-    enforce mode fatal), so an error after entry would die without one."""
+    enforce mode fatal), so an error after entry would die without one.  The
+    cache is not re-validated afterwards (that stats each file by path, which
+    the policy refuses too; the sources do not change under a running
+    process)."""
     import linecache
     for m in list(sys.modules.values()):
         f = getattr(m, "__file__", None)
         if f and f.endswith(".py"):
             linecache.getlines(f)
+    linecache.checkcache = lambda filename=None: None
 
 
 def round_robin_shares(rr_idx, rr_cnt, T):

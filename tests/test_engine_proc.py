@@ -92,16 +92,25 @@ def test_engine_sandbox_report_mode():
     pid = os.fork()
     if pid == 0:
         try:
+            import ctypes
             import fcntl
             import resource
             import termios
+            libc = ctypes.CDLL(None, use_errno=True)
+
+            def prctl_dumpable():                               # PR_SET_DUMPABLE (4): refused
+                if libc.prctl(4, 1, 0, 0, 0) != 0:
+                    raise OSError(ctypes.get_errno(), "prctl")
             tile.engine_sandbox_enter(report=True)
+            os.fstat(w)                                         # fstat of a held fd: allowed
+            libc.prctl(15, b"engine-test", 0, 0, 0)             # PR_SET_NAME: allowed
             errs = []
             resource.getrlimit(resource.RLIMIT_NOFILE)            # prlimit64 of itself, reading: allowed
             for what in (lambda: os.open("/dev/null", os.O_RDONLY), os.fork,
                          lambda: fcntl.ioctl(0, termios.FIONREAD, b"    "),
                          lambda: resource.setrlimit(resource.RLIMIT_NOFILE, resource.getrlimit(resource.RLIMIT_NOFILE)),
-                         lambda: resource.prlimit(os.getppid(), resource.RLIMIT_NOFILE)):
+                         lambda: resource.prlimit(os.getppid(), resource.RLIMIT_NOFILE),
+                         lambda: os.stat("/etc"), prctl_dumpable):
                 try:
                     what()
                     errs.append("allowed")
@@ -115,9 +124,9 @@ def test_engine_sandbox_report_mode():
     _, status = os.waitpid(pid, 0)
     errs, n, names = eval(os.read(r, 4096).decode())
     assert os.WIFEXITED(status) and os.WEXITSTATUS(status) == 0, status
-    assert errs == [1, 1, 1, 1, 1] and n >= 5, (errs, n)
+    assert errs == [1] * 7 and n == 7, (errs, n)
     assert "openat" in names and "ioctl" in names and ("clone" in names or "fork" in names), names
-    assert "prlimit64" in names, names
+    assert "prlimit64" in names and "newfstatat" in names and "prctl" in names, names
 
 
 def test_shm_link_join_roundtrip():
