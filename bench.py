@@ -549,7 +549,7 @@ TILE_RUNS_XPROC = (
     ("xproc_mux1_capacity", 1, 1, -1.0),
     ("xproc_mux2_capacity", 2, 2, -1.0),
     ("xproc_2proc_capacity", 2, 2, -1.0, 2, 0),
-    ("xproc_2proc_paced_24M", 2, 4, 24e6, 2, 0),
+    ("xproc_2proc_paced_12M", 2, 4, 12e6, 2, 0),
     ("xproc_e2e_dedup_capacity", 2, 2, -1.0, 1, 1),
     ("xproc_e2e_dedup_paced_2M", 2, 4, 2e6, 1, 1),
 )
