@@ -4,6 +4,7 @@ against the reference's own test expectations (test_txn_parse.c,
 test_tcache.c, test_verify.c) and against sequential models of the reference
 loops.  The verify tiles here run over a PyVerifier whose verdicts come from
 the CPU oracle (the GPU engine is exercised by test_tile_gpu.py)."""
+import ctypes
 import hashlib
 import os
 import random
@@ -582,6 +583,92 @@ def test_dedup_tile_reliable_links_publish_progress(oracle):
     rel = tile.DedupTile(outs, tile.Link(1 << 10, tile.TPU_DCACHE_MTU), tcache_depth=1 << 12, reliable=True)
     assert rel.run_until_idle() == sum(pub)
     assert [int(o.fseq[0]) for o in outs] == [o.seq0 + n for o, n in zip(outs, pub)]
+
+
+def _verify_outputs(ps):
+    """verify-tile out frags ([payload][pad][fd_txn_t][u16 payload sz]) of the parseable payloads"""
+    outs = []
+    for p in ps:
+        sz, raw = tile.txn_parse(p)
+        if sz:
+            outs.append(p + (b"\0" if len(p) & 1 else b"") + raw + len(p).to_bytes(2, "little"))
+    return outs
+
+
+def test_dedup_tile_steady_state_tcache_vs_model():
+    """The dedup tile with its tcache in the steady state (filled with
+    `depth` other tags first: every insert evicts) against the model fed the
+    same tags: same published stream, same dups -- the eviction order, the
+    prefetched map lines and the huge-page region change nothing -- over a
+    link that also carries frags whose trailers lie (sizes and offsets out of
+    range: counted corrupt, never read past the frag)."""
+    rng = np.random.default_rng(0xDEDE)
+    base = _verify_outputs(_mixed_stream(700, seed=23))
+    stream = []
+    for k in range(3000):
+        r = rng.random()
+        if r < 0.08:                                  # a frag whose trailer lies
+            f = bytearray(rng.integers(0, 256, size=int(rng.integers(2, 300)), dtype=np.uint8).tobytes())
+            f[-2:] = int(rng.integers(0, 65536)).to_bytes(2, "little")
+            stream.append(bytes(f))
+        else:                                         # a verified txn, often seen before (near or far back)
+            stream.append(base[int(rng.integers(0, len(base)))])
+    depth = 1024
+    inl = tile.Link(1 << 12, tile.TPU_DCACHE_MTU)
+    for f in stream:
+        inl.publish(f)
+    dout = tile.Link(1 << 12, tile.TPU_DCACHE_MTU)
+    dt = tile.DedupTile([inl], dout, hashmap_seed=0xD5, tcache_depth=depth)
+    assert dt.tcache_fill(depth + 77, seed=5) == 0
+    dt.run_until_idle()
+    model = tile_model.TCacheModel(depth)
+    for t in np.random.default_rng(5).integers(1, 2 ** 63, size=depth + 77, dtype=np.uint64):
+        model.insert(int(t))
+    exp, corrupt = [], 0
+    for f in stream:
+        psz = int.from_bytes(f[-2:], "little")
+        toff = (psz + 1) & ~1
+        if toff + ctypes.sizeof(tile.TxnHdr) + 2 > len(f):
+            corrupt += 1
+            continue
+        so = tile.TxnHdr.from_buffer_copy(f[toff:toff + ctypes.sizeof(tile.TxnHdr)]).signature_off
+        if so + 64 > len(f):
+            corrupt += 1
+            continue
+        if not model.insert(tile.fd_hash(0xD5, f[so:so + 64])):
+            exp.append(f)
+    st = dt.stats()
+    assert [f for _, f in dout.drain()] == exp
+    assert st["published"] == len(exp) and st["corrupt"] == corrupt and corrupt > 100
+    assert st["in_frags"] == len(stream) and st["dup"] == len(stream) - len(exp) - corrupt
+
+
+def test_dedup_tile_reference_depth():
+    """At the reference's signature_cache_size (4,194,302, default.toml:910),
+    the tile's default: a txn seen again after 18 K other frags is dropped,
+    where a 16,384-deep tcache has forgotten it and publishes it again."""
+    def sig0(f):
+        so = tile.TxnHdr.from_buffer_copy(tile.split_verify_output(f)[1]).signature_off
+        return so, f[so:so + 64]
+    outs = list({sig0(f)[1]: f for f in _verify_outputs(_mixed_stream(500, seed=24))}.values())
+
+    def variant(f, c):                              # the same frag with another first signature
+        so = sig0(f)[0]
+        b = bytearray(f)
+        b[so:so + 3] = bytes((0xA5, c >> 8, c & 0xFF))
+        return bytes(b)
+    filler = [variant(f, c) for c in range((1 << 14) // len(outs) + 2) for f in outs]
+    stream = outs + filler + outs                   # the second copies ~18 K frags after the first
+    assert len({sig0(f)[1] for f in stream}) == len(outs) + len(filler) > (1 << 14) + len(outs)
+    for depth, exp in ((4194302, len(outs) + len(filler)), (1 << 14, len(stream))):
+        inl = tile.Link(1 << 16, tile.TPU_DCACHE_MTU)
+        for f in stream:
+            inl.publish(f)
+        dout = tile.Link(1 << 10, tile.TPU_DCACHE_MTU)
+        dt = tile.DedupTile([inl], dout, tcache_depth=depth)
+        assert dt.run_until_idle() == len(stream)
+        st = dt.stats()
+        assert st["published"] == exp and st["dup"] == len(stream) - exp, (depth, st)
 
 
 def test_dedup_tile_unparsed_link(oracle, fixtures):
