@@ -2140,7 +2140,7 @@ bool sync_run_prehashed(SyncState &st, SyncReq &r) {
     }
     if (!hashed) { set_err("prehashed call: hashing"); break; }
     int8_t code = 0;
-    if (fdgpu_launch_verify_prehashed(d_arena, d_sigs, n, e->d_btab, d_ws, (int8_t *)d_codes, e->cfg.flags, s) !=
+    if (fdgpu_launch_verify_prehashed(d_arena, d_sigs, n, e->d_btab, d_ws, (int8_t *)d_codes, kflags(e), s) !=
             hipSuccess ||
         fdgpu_launch_combine(d_txn, 1, (const int8_t *)d_codes, (int8_t *)d_codes + n + 16, nullptr, s) !=
             hipSuccess ||
