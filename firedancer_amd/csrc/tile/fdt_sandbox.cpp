@@ -18,8 +18,11 @@
                       dcache_off; the consumer fseq on its own 128-B line
      [4096, ...)      mcache: depth x fdt_frag_meta_t (fd_mcache.h:265-322)
      [dcache_off, ..) compact dcache for depth frags of <= mtu (fd_dcache.h) */
+#include <dirent.h>
 #include <errno.h>
 #include <fcntl.h>
+#include <stdio.h>
+#include <stdlib.h>
 #include <sched.h>
 #include <signal.h>
 #include <ucontext.h>
@@ -33,6 +36,7 @@
 #include <time.h>
 #include <unistd.h>
 
+#include <algorithm>
 #include <vector>
 
 #include "../../../include/fd_verify_tile.h"
@@ -202,6 +206,30 @@ const uint32_t ENGINE_ALLOW[] = {
 };
 
 }  // namespace
+
+int fdt_sandbox_driver_fds(int *out, int max) {
+  DIR *d = opendir("/proc/self/fd");
+  if (!d) return -errno;
+  const int self = dirfd(d);
+  int n = 0;
+  for (struct dirent *e; (e = readdir(d));) {
+    char *end = nullptr;
+    const long fd = strtol(e->d_name, &end, 10);
+    if (!e->d_name[0] || *end || fd == self) continue;
+    char link[64], target[256];
+    snprintf(link, sizeof link, "/proc/self/fd/%ld", fd);
+    const ssize_t k = readlink(link, target, sizeof target - 1);
+    if (k <= 0) continue;
+    target[k] = 0;
+    if (strcmp(target, "/dev/kfd") && strncmp(target, "/dev/dri/", 9)) continue;
+    if (n < max) out[n] = (int)fd;
+    n++;
+  }
+  closedir(d);
+  if (n > max) return -ENOSPC;
+  std::sort(out, out + n);
+  return n;
+}
 
 int fdt_sandbox_engine_enter(const int *dev_fds, int dev_fd_cnt, int report) {
   if (dev_fd_cnt < 0 || dev_fd_cnt > 64 || (dev_fd_cnt && !dev_fds)) return -EINVAL;

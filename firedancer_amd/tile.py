@@ -298,6 +298,7 @@ def lib():
         "fdt_sandbox_enter": (c.c_int, [c.c_int]),
         "fdt_sandbox_engine_enter": (c.c_int, [vp, c.c_int, c.c_int]),
         "fdt_sandbox_report": (u64, [vp]),
+        "fdt_sandbox_driver_fds": (c.c_int, [vp, c.c_int]),
         "fdgpu_dtile_run_sandboxed": (None, [vp, u64, u64, c.POINTER(DTileStats), c.c_int]),
         "fdgpu_producer_join": (u64, [vp, c.POINTER(c.c_double)]),
         "fdgpu_producer_done": (c.c_int, [vp]),
@@ -344,16 +345,13 @@ def sandbox_enter(logfile_fd=2):
 
 def device_fds():
     """This process's open device fds of the GPU driver (/dev/kfd and the DRM
-    render nodes), the only fds the engine policy lets ioctl reach."""
-    out = []
-    for name in os.listdir("/proc/self/fd"):
-        try:
-            target = os.readlink(f"/proc/self/fd/{name}")
-        except OSError:
-            continue
-        if target == "/dev/kfd" or target.startswith("/dev/dri/"):
-            out.append(int(name))
-    return sorted(out)
+    render nodes; fdt_sandbox_driver_fds), the only fds the engine policy lets
+    ioctl reach."""
+    buf = (c.c_int * 64)()
+    n = lib().fdt_sandbox_driver_fds(buf, 64)
+    if n < 0:
+        raise OSError(-n, "fdt_sandbox_driver_fds failed")
+    return list(buf[:n])
 
 
 _SYSCALL_NAMES = {}

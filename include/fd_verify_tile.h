@@ -745,6 +745,11 @@ int      fdt_sandbox_enter ( int logfile_fd );
    with EPERM instead of killing, and is recorded (fdt_sandbox_report); it is
    never carried out either way.  Returns 0 or -errno. */
 int      fdt_sandbox_engine_enter( int const * dev_fds, int dev_fd_cnt, int report );
+/* The GPU driver's fds this process holds (/proc/self/fd entries naming
+   /dev/kfd or /dev/dri/...), ascending, into out[0..max): the dev_fds of
+   fdt_sandbox_engine_enter.  Returns the count, or -errno (-ENOSPC: more
+   than max). */
+int      fdt_sandbox_driver_fds( int * out, int max );
 /* Report mode: bits8[k] bit j set = syscall 64 k + j was refused; returns
    how many calls were refused. */
 uint64_t fdt_sandbox_report( uint64_t * bits8 );

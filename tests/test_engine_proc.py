@@ -381,3 +381,20 @@ def test_traceback_inside_engine_policy():
     tb = os.read(r, 65536).decode()
     assert os.WIFEXITED(status) and os.WEXITSTATUS(status) == 0, status
     assert "raise ValueError" in tb and "round_robin_shares" in tb, tb
+
+
+def test_driver_fds_found_by_path(tmp_path):
+    """fdt_sandbox_driver_fds lists exactly the fds naming the GPU driver's
+    devices: none here without them, and an fd of another file is never
+    listed."""
+    f = open(tmp_path / "x", "w")
+    try:
+        fds = tile.device_fds()
+        assert f.fileno() not in fds
+        for fd in fds:
+            assert os.readlink(f"/proc/self/fd/{fd}") == "/dev/kfd" or \
+                os.readlink(f"/proc/self/fd/{fd}").startswith("/dev/dri/")
+        if not os.path.exists("/dev/kfd"):
+            assert fds == []
+    finally:
+        f.close()
