@@ -259,6 +259,16 @@ def test_two_engine_processes_share_link_cpu(tmp_path, oracle):
     assert all(len(pub) > 100 for _, pub in exp)
 
 
+def test_eight_engine_processes_cpu(tmp_path, oracle):
+    """verify_tile_cnt = 8 as eight engine processes over one link (global
+    tiles 0..7 of 8), the dedup over their eight out links: frag by frag
+    against tile_model(k, 8) (the CPU stand-in verifier)."""
+    ps = _mixed_stream(1600, seed=79)
+    res, exp = _xproc_vs_model(tmp_path, ps, oracle, tiles=8, engine_procs=8, engine_cmd=CPU_ENGINE, depth=1 << 12,
+                               batch=64, inflight=2)
+    assert sorted(e["rr_idx"] for e in res["engines"]) == list(range(8))
+
+
 def test_engine_proc_devices_and_round_robin_args():
     """--devices maps tile k to the (k % n)-th device; --rr-idx/--rr-cnt
     outside the tiles' range is refused."""
@@ -302,6 +312,22 @@ def test_engine_processes_multi_device_gpu(tmp_path, oracle):
     res, _ = _xproc_vs_model(tmp_path, ps, oracle, tiles=2, engine_procs=1, proc_devices=["0,0"], depth=1 << 12,
                              batch=512, inflight=3)
     assert res["engine"]["devices"] == [0, 0]
+
+
+@pytest.mark.gpu
+def test_eight_engine_processes_gpu(tmp_path, oracle):
+    """The node shape of BASELINE cfg5 -- verify_tile_cnt = 8, one GPU per
+    tile (fd_frankendancer.c:99,131-133) -- rehearsed on the box's one GPU:
+    eight engine processes, each one tile as global tile k of 8 over the same
+    quic -> verify link (--rr-idx k --rr-cnt 8), each inside its seccomp
+    policy, the sandboxed dedup over the eight out links at the reference's
+    depth.  Every tile equals tile_model(k, 8) frag by frag; the dedup's
+    output is every distinct verified txn once."""
+    ps = _mixed_stream(4000, seed=78)
+    res, exp = _xproc_vs_model(tmp_path, ps, oracle, tiles=8, engine_procs=8, depth=1 << 12, batch=256, inflight=2)
+    assert sorted(e["rr_idx"] for e in res["engines"]) == list(range(8))
+    assert all(e["rr_cnt"] == 8 and e["sandbox"] == 1 for e in res["engines"])
+    assert all(len(pub) > 200 for _, pub in exp)
 
 
 @pytest.mark.gpu
