@@ -663,6 +663,80 @@ def xproc_runs(world):
     return TILE_RUNS_XPROC if world == 1 else tuple(r for r in TILE_RUNS_XPROC if not (len(r) > 4 and r[4] > 1))
 
 
+NODE_RUNS = (  # name, quic links (producers), offered txn/s (-1: prefilled), runs -- one tile per GPU of the node
+    ("node_e2e_dedup_capacity", 2, -1.0, 2),
+    ("node_e2e_dedup_paced_2M", 4, 2e6, 2),
+)
+
+
+def node_lines(dist, arena, txns, modes, cpus, engine_cmd=None, depth_lg=None, batch=TILE_BATCH,
+               inflight=TILE_INFLIGHT):
+    """BASELINE cfg5 at the node's scale (world > 1; rank 0 runs it while the
+    other ranks wait at a barrier, before any rank starts a HIP runtime of its
+    own): verify_tile_cnt = world -- one engine process per GPU, one tile each
+    as global tile r of world over the same quic -> verify links
+    (fd_frankendancer.c:99,131-133, fd_verify.c:46), each inside its seccomp
+    policy -- and the one sandboxed dedup tile over every verify -> dedup link,
+    reliably, at the reference's tcache depth; timed from the first frag to the
+    dedup's last.  Every frag's outcome reaches the dedup or the run is not ok.
+    engine_cmd / depth_lg (prefill, paced) / batch / inflight: the CPU test's
+    stand-in engine and small links (tests/_multirank_worker.py)."""
+    depth_lg = depth_lg or (TILE_DEPTH_LG_PREFILL, TILE_DEPTH_LG_PACED)
+    import tempfile
+    sys.path.insert(0, os.path.join(REPO, "tools"))
+    import xproc
+    from firedancer_amd import workload
+    every = [None] * dist.world
+    dist.dist.all_gather_object(every, list(cpus or []))
+    node_cpus = sorted(set(c for cs in every for c in cs))
+    out = {}
+    if dist.rank == 0:
+        ps = workload.payloads(arena, txns)
+        pa, po, psz = workload.pack_payloads(ps)
+        with tempfile.TemporaryDirectory() as td:
+            npz = os.path.join(td, "frags.npz")
+            np.savez(npz, arena=pa, offs=po, sizes=psz)
+            exp_once = int((modes == 0).sum())
+            for name, P, rate, reps_n in NODE_RUNS:
+                prefill = rate < 0
+                reps = 1 if prefill else TILE_PACED_REPS
+                depth = 1 << (depth_lg[0] if prefill else depth_lg[1])
+                mult = sum(xproc.quic_feed.frag_counts(len(ps), P, "prefill" if prefill else "paced", reps)) // len(ps)
+                runs = []
+                for _ in range(reps_n):
+                    r = xproc.run(npz, len(ps), tiles=dist.world, producers=P, mode="prefill" if prefill else "paced",
+                                  rate=0.0 if prefill else rate, reps=reps, depth=depth, batch=batch,
+                                  inflight=inflight, pair=TILE_PAIR, spread=TILE_SPREAD, dedup=True,
+                                  engine_cmd=engine_cmd,
+                                  dedup_frags=exp_once * mult, engine_procs=dist.world,
+                                  proc_device_ranks=list(range(dist.world)),
+                                  cpus=node_cpus[:P + dist.world + 1] if len(node_cpus) > P + dist.world else None,
+                                  timeout=300)
+                    st, ds = r["engine"]["stats"], r["dedup"]["stats"]
+                    runs.append({"txns_per_s": r["txns_per_s"], "published": st["published"],
+                                 "published_ok": st["published"] == exp_once * mult,
+                                 "dedup_ok": (r["dedup"]["exit"] == 0 and ds["overrun"] == 0 and
+                                              ds["in_frags"] == st["published"] and
+                                              ds["published"] + ds["dup"] == ds["in_frags"]),
+                                 "overrun": st["overrun"], "dedup": [ds["in_frags"], ds["published"], ds["dup"]],
+                                 "lat": r["engine"]["batch_latency_ms"]})
+                med = sorted(runs, key=lambda x: x["txns_per_s"])[len(runs) // 2]
+                out[f"tile_{name}_txns_per_s"] = med["txns_per_s"]
+                out[f"tile_{name}_txns_per_s_runs"] = [x["txns_per_s"] for x in runs]
+                out[f"tile_{name}_published_ok"] = all(x["published_ok"] for x in runs)
+                out[f"tile_{name}_dedup_ok"] = all(x["dedup_ok"] for x in runs)
+                out[f"tile_{name}_overruns"] = max(x["overrun"] for x in runs)
+                out[f"tile_{name}_dedup_in_published_dup"] = med["dedup"]
+                out[f"tile_{name}_batch_latency_ms_p50_p99_worst_gpu"] = [med["lat"]["p50"], med["lat"]["p99"]]
+        out["tile_node_config"] = (f"{dist.world} engine processes, one per GPU (--device-rank r), one verify tile each "
+                                   f"as global tile r of {dist.world} over the same quic -> verify links (P per line), "
+                                   "each in its seccomp policy; the sandboxed dedup over every verify -> dedup link at "
+                                   "tcache depth 4194302; capacity: links prefilled 2^21 deep; paced: 16384-deep links, "
+                                   f"the stream {TILE_PACED_REPS}x over; cfg1 frags of rank 0; median of the runs")
+    dist.barrier()
+    return out
+
+
 def tile_lines(rank, arena, txns, modes, cpus, cfg3=None, world=1):
     """BASELINE configs[4] (cfg5) on this rank's GPU: the verify tile in the
     reference's shape -- the fd_verify.c:232-246 callbacks (fdgpu_vmux) on
@@ -914,6 +988,9 @@ def main():
         tl["tile_mux1_capacity_txns_per_s_node"] = round(dist.sum(tl["tile_mux1_capacity_txns_per_s"]), 1)
         tl["tile_published_ok_all_ranks"] = dist.sum(
             1 if all(v for k, v in tl.items() if k.endswith(("_published_ok", "_dedup_ok"))) else 0) == dist.world
+        if dist.world > 1:             # the node's GPUs as one verify stage (before any rank starts HIP)
+            dist.barrier()
+            tl.update(node_lines(dist, arena, txns, modes, cpus))
     # one process per GPU; more ranks than visible GPUs (a rehearsal of the
     # multi-rank path on a one-GPU box) share devices round robin
     ndev = _lib.lib().fdgpu_device_count()

@@ -32,8 +32,15 @@ def main():
     ok = int(((codes == 0) == (modes == 0)).all())
     first = int.from_bytes(arena[1:9].tobytes(), "little")
     firsts = dist.sum(first % 1000003)
+    # the node-level cfg5 lines (bench.node_lines): rank 0 runs one engine
+    # process per rank over shared links, the other rank waits at the barrier;
+    # the CPU stand-in engine, small links
+    a2, t2, m2 = workload.cfg1(400, seed=0x40DE, nthreads=1)
+    node = bench.node_lines(dist, a2, t2, m2, cpus,
+                            engine_cmd=[sys.executable, os.path.join(REPO, "tests", "_engine_proc_worker.py")],
+                            depth_lg=(12, 12), batch=64, inflight=2)
     out = {"rank": dist.rank, "value": value, "dt_max": dt_max, "ok": ok, "firsts_sum": firsts,
-           "first": first % 1000003, "cpus": cpus}
+           "first": first % 1000003, "cpus": cpus, "node": node}
     path = os.environ["MULTIRANK_OUT"] + f".{dist.rank}"
     json.dump(out, open(path, "w"))
     dist.close()

@@ -26,3 +26,16 @@ def test_two_rank_gloo(tmp_path):
     # ranks sharing one host affinity get disjoint physical cores (tile threads, oracle)
     assert res[0]["cpus"] and res[1]["cpus"]
     assert not set(res[0]["cpus"]) & set(res[1]["cpus"])
+    # the node-level cfg5 lines: on rank 0 only, every frag through two engine processes and the dedup
+    node = res[0]["node"]
+    assert res[1]["node"] == {}
+    for name, *_ in bench_runs():
+        assert node[f"tile_{name}_published_ok"] and node[f"tile_{name}_dedup_ok"], (name, node)
+        assert node[f"tile_{name}_overruns"] == 0 and node[f"tile_{name}_txns_per_s"] > 0
+    assert "2 engine processes" in node["tile_node_config"]
+
+
+def bench_runs():
+    sys.path.insert(0, REPO)
+    import bench
+    return bench.NODE_RUNS

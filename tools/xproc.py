@@ -74,14 +74,16 @@ def run(npz, n_payloads, tiles=1, producers=1, mode="paced", rate=0.0, reps=1, d
         inflight=8, wait_us=200.0, batch_sig_max=0, pages="4k", cpus=None, device_rank=0, dedup=False,
         dedup_frags=0, log=False, lap_guard=True, pair=2, spread=2, seed=0x5EEDF00D, timeout=300.0,
         hw_queues=32, engine_cmd=None, engine_procs=1, proc_devices=None, dedup_depth=DEDUP_TCACHE_DEPTH,
-        sandbox=None):
+        sandbox=None, proc_device_ranks=None):
     """One cross-process run over the payloads in `npz` (arena, offs, sizes;
     n_payloads of them).  engine_cmd: the engine process's command before
     its arguments (default: python -m firedancer_amd.engine_proc; the CPU
     tests run the same loop over their checker instead).  engine_procs: E
     engine processes over the same in links, tiles // E tiles each;
     proc_devices: per process the --devices string (default: every process
-    --device-rank device_rank); sandbox: the engine processes' --sandbox
+    --device-rank device_rank; proc_device_ranks: per process its
+    --device-rank, the device being that % the visible devices -- a launcher
+    that must not start a HIP runtime itself); sandbox: the engine processes' --sandbox
     (None: their default).  Returns {engine, engines, feed, dedup,
     wall_s, txns_per_s, ...} (engine: the processes' stats combined,
     engines: each process's own); with log=True also the tiles' per-frag
@@ -117,7 +119,8 @@ def run(npz, n_payloads, tiles=1, producers=1, mode="paced", rate=0.0, reps=1, d
                  "--batch-sig-max", str(batch_sig_max), "--wait-us", str(wait_us), "--seed", hex(seed),
                  "--pair", str(pair), "--spread", str(spread), "--lap-guard", str(int(lap_guard)),
                  "--hw-queues", str(hw_queues), "--ready-file", readies[e], "--timeout", str(timeout)]
-            c += ["--devices", proc_devices[e]] if proc_devices else ["--device-rank", str(device_rank)]
+            c += (["--devices", proc_devices[e]] if proc_devices else
+                  ["--device-rank", str(proc_device_ranks[e] if proc_device_ranks else device_rank)])
             if tcpu:
                 c += ["--cpus", ",".join(map(str, tcpu[e * TE:(e + 1) * TE]))]
             if dedup:                        # verify -> dedup links are reliable (fd_topo): credits from the dedup's fseq
