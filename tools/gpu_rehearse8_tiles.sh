@@ -43,4 +43,5 @@ tail -1 $o/gpu_procs.txt
 python3 -c "
 import json; d=json.loads(open('$o/bench8.json').read().strip().splitlines()[-1])
 print({k: d[k] for k in ('value','n_gpus','ms_per_step','parity_checked_txns','parity_mismatches','tile_published_ok_all_ranks','tile_mux1_capacity_txns_per_s_node') if k in d})
+print({k: v for k, v in d.items() if k.startswith('tile_node')})
 "
