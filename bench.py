@@ -967,7 +967,6 @@ def main():
     dist = Dist()
     cpus = dist.cpus()
     from firedancer_amd import VerifyEngine, _lib, workload
-    build_info = _lib.require_product_build(allow_ab=args.ab_build)    # no HIP call
 
     t_gen = time.perf_counter()
     arena, txns, modes = workload.cfg1(args.txns, seed=rank_seed(dist.rank))
@@ -991,6 +990,10 @@ def main():
         if dist.world > 1:             # the node's GPUs as one verify stage (before any rank starts HIP)
             dist.barrier()
             tl.update(node_lines(dist, arena, txns, modes, cpus))
+    # the engine library is loaded only now (loading the HIP runtime library
+    # opens the driver: a rank holding it through its tile lines would be one
+    # more GPU process beside its tile engines); a non-product build is refused
+    build_info = _lib.require_product_build(allow_ab=args.ab_build)
     # one process per GPU; more ranks than visible GPUs (a rehearsal of the
     # multi-rank path on a one-GPU box) share devices round robin
     ndev = _lib.lib().fdgpu_device_count()

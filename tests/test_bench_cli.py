@@ -66,7 +66,10 @@ def test_parent_rank_starts_no_hip_before_its_tile_child():
     src = open(os.path.join(REPO, "bench.py")).read()
     main = src[src.index("def main():"):]
     assert "torch.cuda" not in src
-    assert main.index("tile_lines(") < main.index("fdgpu_device_count()")
+    # the engine library itself (libamdhip64 with it) is loaded only after the tile and node lines
+    assert main.index("tile_lines(") < main.index("require_product_build(") < main.index("fdgpu_device_count()")
+    assert main.index("node_lines(") < main.index("require_product_build(")
+    assert "_lib.lib()" not in main[:main.index("require_product_build(")]
     assert main.index("fdgpu_device_count()") < main.index("VerifyEngine(")
 
 

@@ -17,15 +17,21 @@ while time.time() - t0 < 1000:
             continue
         try:
             with open(f"/proc/{p}/maps") as f:
-                if "/dev/kfd" in f.read():
-                    n += 1
+                held = "/dev/kfd" in f.read()
+            if not held:                   # an open driver fd counts too (the box's process guard counts those)
+                for fd in os.listdir(f"/proc/{p}/fd"):
+                    t = os.readlink(f"/proc/{p}/fd/{fd}")
+                    if t == "/dev/kfd" or t.startswith("/dev/dri/"):
+                        held = True
+                        break
+            n += held
         except OSError:
             pass
     peak = max(peak, n)
     if time.time() - last > 5:
         print(f"t={time.time() - t0:.0f}s gpu_procs={n} peak={peak}", flush=True)
         last = time.time()
-    time.sleep(0.5)
+    time.sleep(0.2)
 PY
 sampler=$!
 echo "[$(date +%T)] 8 ranks on one GPU, tile lines on"
