@@ -86,6 +86,12 @@ def parse():
     ap.add_argument("--keypool-txns", type=int, default=1_000_000,
                     help="txns of the signer-reuse batch (key pool of 4096) timed with and without the key "
                          "cache (0: skip)")
+    ap.add_argument("--node-lines", type=int, default=0,
+                    help="multi-rank runs: 1 adds the node-level cfg5 lines (bench.node_lines: one engine process "
+                         "per GPU over shared links, the dedup over all of them); off by default, so a node's GPU "
+                         "process count stays at the ranks' own")
+    ap.add_argument("--node-procs", type=int, default=0,
+                    help="engine processes of the node lines (0: one per rank; a one-GPU rehearsal keeps it small)")
     ap.add_argument("--ab-build", action="store_true",
                     help="let a library with A/B or fault-injection switches run (fdgpu_build_info; recorded in the "
                          "line as `build`); without it such a library is refused")
@@ -670,7 +676,7 @@ NODE_RUNS = (  # name, quic links (producers), offered txn/s (-1: prefilled), ru
 
 
 def node_lines(dist, arena, txns, modes, cpus, engine_cmd=None, depth_lg=None, batch=TILE_BATCH,
-               inflight=TILE_INFLIGHT):
+               inflight=TILE_INFLIGHT, procs=None):
     """BASELINE cfg5 at the node's scale (world > 1; rank 0 runs it while the
     other ranks wait at a barrier, before any rank starts a HIP runtime of its
     own): verify_tile_cnt = world -- one engine process per GPU, one tile each
@@ -680,8 +686,11 @@ def node_lines(dist, arena, txns, modes, cpus, engine_cmd=None, depth_lg=None, b
     reliably, at the reference's tcache depth; timed from the first frag to the
     dedup's last.  Every frag's outcome reaches the dedup or the run is not ok.
     engine_cmd / depth_lg (prefill, paced) / batch / inflight: the CPU test's
-    stand-in engine and small links (tests/_multirank_worker.py)."""
+    stand-in engine and small links (tests/_multirank_worker.py).  procs:
+    engine processes (default one per rank; engine process k on device
+    rank k)."""
     depth_lg = depth_lg or (TILE_DEPTH_LG_PREFILL, TILE_DEPTH_LG_PACED)
+    procs = procs or dist.world
     import tempfile
     sys.path.insert(0, os.path.join(REPO, "tools"))
     import xproc
@@ -704,13 +713,13 @@ def node_lines(dist, arena, txns, modes, cpus, engine_cmd=None, depth_lg=None, b
                 mult = sum(xproc.quic_feed.frag_counts(len(ps), P, "prefill" if prefill else "paced", reps)) // len(ps)
                 runs = []
                 for _ in range(reps_n):
-                    r = xproc.run(npz, len(ps), tiles=dist.world, producers=P, mode="prefill" if prefill else "paced",
+                    r = xproc.run(npz, len(ps), tiles=procs, producers=P, mode="prefill" if prefill else "paced",
                                   rate=0.0 if prefill else rate, reps=reps, depth=depth, batch=batch,
                                   inflight=inflight, pair=TILE_PAIR, spread=TILE_SPREAD, dedup=True,
                                   engine_cmd=engine_cmd,
-                                  dedup_frags=exp_once * mult, engine_procs=dist.world,
-                                  proc_device_ranks=list(range(dist.world)),
-                                  cpus=node_cpus[:P + dist.world + 1] if len(node_cpus) > P + dist.world else None,
+                                  dedup_frags=exp_once * mult, engine_procs=procs,
+                                  proc_device_ranks=list(range(procs)),
+                                  cpus=node_cpus[:P + procs + 1] if len(node_cpus) > P + procs else None,
                                   timeout=300)
                     st, ds = r["engine"]["stats"], r["dedup"]["stats"]
                     runs.append({"txns_per_s": r["txns_per_s"], "published": st["published"],
@@ -728,8 +737,8 @@ def node_lines(dist, arena, txns, modes, cpus, engine_cmd=None, depth_lg=None, b
                 out[f"tile_{name}_overruns"] = max(x["overrun"] for x in runs)
                 out[f"tile_{name}_dedup_in_published_dup"] = med["dedup"]
                 out[f"tile_{name}_batch_latency_ms_p50_p99_worst_gpu"] = [med["lat"]["p50"], med["lat"]["p99"]]
-        out["tile_node_config"] = (f"{dist.world} engine processes, one per GPU (--device-rank r), one verify tile each "
-                                   f"as global tile r of {dist.world} over the same quic -> verify links (P per line), "
+        out["tile_node_config"] = (f"{procs} engine processes, one per GPU (--device-rank r), one verify tile each "
+                                   f"as global tile r of {procs} over the same quic -> verify links (P per line), "
                                    "each in its seccomp policy; the sandboxed dedup over every verify -> dedup link at "
                                    "tcache depth 4194302; capacity: links prefilled 2^21 deep; paced: 16384-deep links, "
                                    f"the stream {TILE_PACED_REPS}x over; cfg1 frags of rank 0; median of the runs")
@@ -987,9 +996,9 @@ def main():
         tl["tile_mux1_capacity_txns_per_s_node"] = round(dist.sum(tl["tile_mux1_capacity_txns_per_s"]), 1)
         tl["tile_published_ok_all_ranks"] = dist.sum(
             1 if all(v for k, v in tl.items() if k.endswith(("_published_ok", "_dedup_ok"))) else 0) == dist.world
-        if dist.world > 1:             # the node's GPUs as one verify stage (before any rank starts HIP)
+        if dist.world > 1 and args.node_lines:   # the node's GPUs as one verify stage (before any rank starts HIP)
             dist.barrier()
-            tl.update(node_lines(dist, arena, txns, modes, cpus))
+            tl.update(node_lines(dist, arena, txns, modes, cpus, procs=args.node_procs or dist.world))
     # the engine library is loaded only now (loading the HIP runtime library
     # opens the driver: a rank holding it through its tile lines would be one
     # more GPU process beside its tile engines); a non-product build is refused

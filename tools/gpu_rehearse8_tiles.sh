@@ -39,6 +39,7 @@ t0=$(date +%s)
 timeout -k 10 1000 python -m torch.distributed.run --nnodes=1 --nproc-per-node 8 --master-addr 127.0.0.1 \
   --master-port 29533 bench.py --gpus 8 --steps 5 --warmup 1 --txns 200000 --adv-txns 100000 \
   --keypool-txns 100000 --cfg3-txns 30000 --tile-cfg3-txns 30000 --latency-batches 200 --cpu-sample 100000 \
+  --node-lines 1 --node-procs 4 \
   > $o/bench8.json 2> $o/bench8.err
 rc=$?
 t1=$(date +%s)
