@@ -158,7 +158,7 @@ int fdt_sandbox_enter(int logfile_fd) {
    the engine process enters (after privileged init, as fd_topo_run.c:96-103
    enters the tiles' policies) a policy that allows the resource-neutral
    syscalls below, ioctl only on the device fds it already holds, clone only
-   for threads -- and kills the process on anything else, for every thread
+   for threads, tgkill only to its own threads -- and kills the process on anything else, for every thread
    (SECCOMP_FILTER_FLAG_TSYNC: the runtime's threads included).
 
    Report mode (bring-up and tests): a syscall outside the list is refused
@@ -198,7 +198,7 @@ const uint32_t ENGINE_ALLOW[] = {
   __NR_futex, __NR_sched_yield, __NR_nanosleep, __NR_clock_nanosleep, __NR_clock_gettime, __NR_clock_getres,
   __NR_gettimeofday, __NR_select, __NR_pselect6, __NR_poll, __NR_ppoll, __NR_epoll_wait, __NR_epoll_pwait,
   __NR_getpid, __NR_gettid, __NR_getppid, __NR_getuid, __NR_geteuid, __NR_getgid, __NR_getegid,
-  __NR_rt_sigprocmask, __NR_rt_sigaction, __NR_rt_sigreturn, __NR_sigaltstack, __NR_tgkill,
+  __NR_rt_sigprocmask, __NR_rt_sigaction, __NR_rt_sigreturn, __NR_sigaltstack,
   __NR_sched_getaffinity, __NR_sched_setaffinity, __NR_sched_getparam, __NR_sched_getscheduler,
   __NR_set_robust_list, __NR_rseq, __NR_getrandom, __NR_membarrier, __NR_getrusage,
   __NR_mbind, __NR_get_mempolicy,                     /* the HIP runtime's NUMA placement of host memory */
@@ -255,8 +255,17 @@ int fdt_sandbox_engine_enter(const int *dev_fds, int dev_fd_cnt, int report) {
   f.push_back(BPF_JUMP(BPF_JMP | BPF_JSET | BPF_K, CLONE_THREAD, 0, 1));
   stmt(BPF_RET | BPF_K, ALLOW);
   stmt(BPF_RET | BPF_K, DENY);
-  /* newfstatat: the fstat form only (AT_EMPTY_PATH on an fd held: the C
-     library's fstat), no lookup of a path */
+  /* tgkill: signals to this process's own threads only (thread group = our
+     pid: raise, abort, pthread_kill); a signal to any other process is refused */
+  jeq(__NR_tgkill, 0, 4);
+  stmt(BPF_LD | BPF_W | BPF_ABS, offsetof(struct seccomp_data, args[0]));
+  jeq((uint32_t)getpid(), 0, 1);
+  stmt(BPF_RET | BPF_K, ALLOW);
+  stmt(BPF_RET | BPF_K, DENY);
+  /* newfstatat: the fstat form only (AT_EMPTY_PATH, as the C library's
+     fstat issues it).  The flag does not stop a non-empty path from being
+     looked up, and the filter cannot read the string: such a call can read a
+     path's metadata, but it opens nothing and yields no fd */
   jeq(__NR_newfstatat, 0, 4);
   stmt(BPF_LD | BPF_W | BPF_ABS, offsetof(struct seccomp_data, args[3]));
   f.push_back(BPF_JUMP(BPF_JMP | BPF_JSET | BPF_K, AT_EMPTY_PATH, 0, 1));
