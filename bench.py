@@ -170,6 +170,14 @@ class Dist:
         return part[:BOX_CPU_SHARE]
 
 
+_T0 = time.monotonic()
+
+
+def progress(msg, rank=0):
+    """one progress line on stderr (stdout carries only the JSON line)"""
+    print(f"[bench r{rank} {time.monotonic() - _T0:6.1f}s] {msg}", file=sys.stderr, flush=True)
+
+
 def rank_seed(rank):
     """Each rank verifies its own independent cfg1 shard (weak scaling)."""
     from firedancer_amd import workload
@@ -608,10 +616,26 @@ def _tile_child(rank, cpus, arena, txns, modes, runs, tag=""):
     with tempfile.TemporaryDirectory() as td:
         npz, res_path = os.path.join(td, "frags.npz"), os.path.join(td, "tile.jsonl")
         np.savez(npz, arena=parena, offs=poffs, sizes=psizes, modes=modes, n_sig=int(txns["sig_cnt"].sum()))
-        r = subprocess.run(tile_cmd(rank, cpus, npz, res_path, runs, multi=tag == "cfg3", xproc=xp),
-                           capture_output=True, text=True, timeout=600)
-        if r.returncode not in (0, 1) or not os.path.exists(res_path):
-            raise RuntimeError(f"tools/bench_tile.py failed ({r.returncode}): {r.stderr[-2000:]}")
+        # the child's per-run lines are echoed to stderr as they come (a long bench stays visibly alive)
+        err_path = os.path.join(td, "tile.err")
+        with open(err_path, "w") as err:
+            p = subprocess.Popen(tile_cmd(rank, cpus, npz, res_path, runs, multi=tag == "cfg3", xproc=xp),
+                                 stdout=subprocess.PIPE, stderr=err, text=True)
+            import threading
+            killer = threading.Timer(600, p.kill)          # the child's time limit
+            killer.start()
+            for ln in p.stdout:
+                if ln.startswith("{"):
+                    try:
+                        x = json.loads(ln)
+                        ln = f"tiles {x.get('tiles')} producers {x.get('producers')}: {x.get('txns_per_s')} txn/s"
+                    except ValueError:
+                        pass
+                progress(f"tile{('_' + tag) if tag else ''} {ln.strip()[:160]}", rank)
+            rc = p.wait()
+            killer.cancel()
+        if rc not in (0, 1) or not os.path.exists(res_path):
+            raise RuntimeError(f"tools/bench_tile.py failed ({rc}): {open(err_path).read()[-2000:]}")
         res_all = [json.loads(x) for x in open(res_path) if x.strip()]
     if len(res_all) != len(runs) * reps_n:
         raise RuntimeError(f"tools/bench_tile.py gave {len(res_all)} runs, expected {len(runs) * reps_n}")
@@ -977,6 +1001,7 @@ def main():
     cpus = dist.cpus()
     from firedancer_amd import VerifyEngine, _lib, workload
 
+    progress("generating the cfg1 batch", dist.rank)
     t_gen = time.perf_counter()
     arena, txns, modes = workload.cfg1(args.txns, seed=rank_seed(dist.rank))
     t_gen = time.perf_counter() - t_gen
@@ -1002,6 +1027,7 @@ def main():
     # the engine library is loaded only now (loading the HIP runtime library
     # opens the driver: a rank holding it through its tile lines would be one
     # more GPU process beside its tile engines); a non-product build is refused
+    progress("device-resident timed loop", dist.rank)
     build_info = _lib.require_product_build(allow_ab=args.ab_build)
     # one process per GPU; more ranks than visible GPUs (a rehearsal of the
     # multi-rank path on a one-GPU box) share devices round robin
@@ -1044,16 +1070,19 @@ def main():
 
     extras = {}
     if not args.no_extras:
+        progress("latency and PCIe-inclusive legs", dist.rank)
         extras = latency_and_pcie(eng, arena, txns, args.latency_batch, args.latency_batches,
                                   pin_cpu=(cpus[1] if len(cpus) > 1 else cpus[0]) if cpus else None)
         extras.update(latency_frag_io(eng, arena, txns, batch.codes(), args.latency_batch, args.latency_batches,
                                       pin_cpu=(cpus[1] if len(cpus) > 1 else cpus[0]) if cpus else None))
         extras["latency_batch_txns"] = args.latency_batch
         if dist.rank == 0:
+            progress("synchronous API", dist.rank)
             extras.update(sync_latency(arena, txns))
         if tl is not None:
             extras.update(tl)
         if args.cfg3_txns:
+            progress("cfg3", dist.rank)
             eng_nb = VerifyEngine(device, max_txn=1024, ring_depth=1, bucket=False)
             extras.update(cfg3_rate(eng, eng_nb, cfg3))
             eng_nb.close()
@@ -1068,11 +1097,14 @@ def main():
                     extras["tile_mux2_capacity_cfg3_vs_device_resident"] = round(
                         extras["tile_mux2_capacity_cfg3_sigs_per_s"] / extras["cfg3_sigs_per_s"], 3)
         if args.keypool_txns:
+            progress("key pool", dist.rank)
             extras.update(key_cache_rate(eng, device, args.keypool_txns, workload.CFG1_SEED + 0x700 + dist.rank))
         if args.host_fed:
+            progress("host-fed 1M batches", dist.rank)
             extras.update(host_fed(device, arena, txns, n_sig, batch.codes(), value / dist.world,
                                    pin_cpu=(cpus[1] if len(cpus) > 1 else cpus[0]) if cpus else None))
         if args.adv_txns:
+            progress("adversarial batches", dist.rank)
             extras.update(adversarial(eng, args.adv_txns, workload.CFG1_SEED + 0x400 + dist.rank,
                                       (kv_ms + kc_ms) / n_sig, cpus))
     cpu = None
@@ -1080,6 +1112,7 @@ def main():
     if not args.no_extras:
         # full-size cfg2 parity: every GPU code of this rank's batch against the
         # oracle (rank 0 also times that oracle run as the CPU baseline)
+        progress("parity against the oracle / CPU baseline", dist.rank)
         gpu_codes = batch.codes()
         n_chk = min(args.cpu_sample, len(txns))
         if dist.rank == 0 and dist.world == 1:
@@ -1091,6 +1124,7 @@ def main():
         parity = {"parity_checked_txns": int(dist.sum(n_chk)), "parity_mismatches": int(dist.sum(mism)),
                   "parity_codes": {int(c): int(k) for c, k in zip(*np.unique(cpu_codes, return_counts=True))}}
     if not args.no_extras:
+        progress("GPU ingest", dist.rank)
         extras.update(gpu_ingest(eng, arena, txns, batch.codes()))
     for b in batches:
         b.free()
