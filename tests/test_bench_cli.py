@@ -123,3 +123,34 @@ def test_xproc_runs_per_world():
     multi = bench.xproc_runs(8)
     assert multi and all(not (len(r) > 4 and r[4] > 1) for r in multi)
     assert any(len(r) > 5 and r[5] for r in multi)                 # the e2e dedup lines stay
+
+
+def test_tile_child_streams_progress_and_parses(monkeypatch, capsys):
+    """_tile_child echoes each of the child's lines to stderr as it comes (a
+    long bench stays visibly alive; stdout keeps only the JSON line) and
+    reads the runs back from the child's result file."""
+    import json
+    from firedancer_amd import workload
+    arena, txns, modes = workload.cfg1(64, seed=1)
+    runs = (("mux1_fake", 1, 1, 1e6),)
+    n = len(runs) * bench.TILE_REPS
+
+    def fake_cmd(rank, cpus, npz, out, runs, multi=0, xproc=False):
+        row = dict(tiles=1, producers=1, txns_per_s=0.0, batch_latency_ms=dict(p50=1.0, p99=2.0), link_depth=16,
+                   offered_txns_per_s=1e6, published_ok=True,
+                   counters=dict(overrun=0, lapped=0, rescued=0, parse_fail=0, stall_max_ns=0, lap_margin_min=5))
+        code = (f"import json\nrows = []\nprint('[bench_tile] ready', flush=True)\n"
+                f"for i in range({n}):\n    r = dict({row!r}, txns_per_s=1.0 + i)\n"
+                f"    print(json.dumps(r), flush=True)\n    rows.append(json.dumps(r))\n"
+                f"open({out!r}, 'w').write(chr(10).join(rows) + chr(10))\n")
+        return [sys.executable, "-c", code]
+
+    monkeypatch.setattr(bench, "tile_cmd", fake_cmd)
+    out = bench._tile_child(0, None, arena, txns, modes, runs)
+    cap = capsys.readouterr()
+    assert cap.out == ""
+    assert cap.err.count("tile tiles 1 producers 1:") == n and "[bench_tile] ready" in cap.err
+    assert out["tile_mux1_fake_txns_per_s_runs"] == [1.0 + i for i in range(n)]
+    assert out["tile_mux1_fake_txns_per_s"] == sorted(out["tile_mux1_fake_txns_per_s_runs"])[n // 2]
+    assert out["tile_mux1_fake_published_ok"] is True
+    json.dumps(out)
